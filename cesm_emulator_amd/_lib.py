@@ -1,0 +1,67 @@
+"""Loader for libcesm_hip.so.
+
+The ctypes signatures are parsed from include/cesm_hip.h so the header stays the single
+source of truth for the C ABI.  There is no fallback: if the library is missing or a symbol
+is absent, importing the product path raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import re
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+HEADER = PKG.parent / "include" / "cesm_hip.h"
+LIBPATH = PKG / "libcesm_hip.so"
+
+_CTYPE = {"int": ctypes.c_int, "int64_t": ctypes.c_int64, "float": ctypes.c_float, "double": ctypes.c_double}
+
+
+def parse_header(path: Path = HEADER):
+    """Return {name: (restype, [argtypes])} for every `int cesm_*(...)` declaration."""
+    text = path.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    decls = {}
+    for m in re.finditer(r"\bint\s+(cesm_\w+)\s*\(([^)]*)\)\s*;", text, flags=re.S):
+        name, args = m.group(1), m.group(2)
+        types = []
+        for a in args.split(","):
+            a = " ".join(a.replace("const", " ").split())
+            if not a:
+                continue
+            if "*" in a or a.startswith("hipStream_t"):
+                types.append(ctypes.c_void_p)
+            else:
+                base = a.rsplit(" ", 1)[0]
+                types.append(_CTYPE[base])
+        decls[name] = (ctypes.c_int, types)
+    return decls
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIBPATH.exists():
+            raise RuntimeError(f"{LIBPATH} not built: run `python -m cesm_emulator_amd.build` "
+                               "(the HIP path has no CPU/PyTorch fallback)")
+        handle = ctypes.CDLL(str(LIBPATH))
+        for name, (res, args) in parse_header().items():
+            fn = getattr(handle, name)  # AttributeError -> missing export, fail loudly
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+class KernelError(RuntimeError):
+    pass
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise KernelError(f"{name} failed with code {rc}")
+    return rc

@@ -1,0 +1,51 @@
+"""Build libcesm_hip.so (gfx950) in-tree: one hipcc compile per csrc/*.hip, linked with hipcc.
+
+Usage: python -m cesm_emulator_amd.build [--force]
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+CSRC = PKG / "csrc"
+ROOT = PKG.parent
+OBJ = ROOT / "build" / "obj"
+LIB = PKG / "libcesm_hip.so"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-I", str(ROOT / "include")]
+
+
+def _compile(src: Path) -> Path:
+    out = OBJ / (src.stem + ".o")
+    deps = [src, CSRC / "common.h"]
+    if out.exists() and all(out.stat().st_mtime >= d.stat().st_mtime for d in deps):
+        return out
+    cmd = [HIPCC, *FLAGS, "-c", str(src), "-o", str(out)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr}")
+    return out
+
+
+def build(force: bool = False) -> Path:
+    OBJ.mkdir(parents=True, exist_ok=True)
+    srcs = sorted(CSRC.glob("*.hip"))
+    if force:
+        for o in OBJ.glob("*.o"):
+            o.unlink()
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        objs = list(ex.map(_compile, srcs))
+    if force or not LIB.exists() or any(o.stat().st_mtime > LIB.stat().st_mtime for o in objs):
+        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", *map(str, objs), "-o", str(LIB)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr}")
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv))

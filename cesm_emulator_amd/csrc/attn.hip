@@ -1,0 +1,626 @@
+// Attention cores of video_net:
+//  * temporal softmax attention (video_net.py:368-454): per pixel, per head, over the frame
+//    axis F: q*scale -> RoPE (rotary_embedding.py:29-48, 146-163) on q and k -> q.k + rel-pos
+//    bias (video_net.py:268-310) -> softmax -> attn.v.  The QKV / output projections run on the
+//    MFMA conv kernel as 1x1 convs; this file is the per-pixel core (tiny F x F x 32 problems,
+//    VALU, one lane per (pixel, head, query frame)).
+//  * spatial linear attention core (video_net.py:313-347): k-softmax over all H*W positions of
+//    a frame (split-n with rescaled partial contexts, deterministic combine), q-softmax over the
+//    32 head dims, out = context^T q.
+//
+// Layouts (channels-last, voxel v = (b*F + f)*HW + p):
+//   qkv [V][768] = q | k | v, head-major inside each (channel = h*32 + d)
+//   out [V][256]
+#include "common.h"
+
+namespace {
+
+constexpr int DH = 32;      // head dim
+constexpr int NH = 8;       // heads
+constexpr int INNER = 256;  // NH*DH
+constexpr int QKV = 768;
+
+// rot[f][i] = (cos, sin) of f * freqs[i], i < 16
+__global__ void rope_table_kernel(const float* __restrict__ freqs, float* __restrict__ rot, int F) {
+  const int t = threadIdx.x + blockIdx.x * blockDim.x;
+  if (t >= F * 16) return;
+  const int f = t / 16, i = t % 16;
+  const float a = (float)f * freqs[i];
+  rot[t * 2] = cosf(a);
+  rot[t * 2 + 1] = sinf(a);
+}
+
+template <typename T>
+__device__ __forceinline__ void load32(const T* p, float* v) {
+#pragma unroll
+  for (int i = 0; i < 32; i += 8) load8(p + i, v + i);
+}
+template <typename T>
+__device__ __forceinline__ void store32(T* p, const float* v) {
+#pragma unroll
+  for (int i = 0; i < 32; i += 8) store8(p + i, v + i);
+}
+// x'[2i] = x[2i] c - x[2i+1] s ; x'[2i+1] = x[2i+1] c + x[2i] s   (sign = +1)
+// inverse (transpose) with sign = -1
+__device__ __forceinline__ void rope(float* v, const float* rot, float sign) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const float c = rot[i * 2], s = sign * rot[i * 2 + 1];
+    const float a = v[2 * i], b = v[2 * i + 1];
+    v[2 * i] = a * c - b * s;
+    v[2 * i + 1] = b * c + a * s;
+  }
+}
+
+// grid: x = pixel-block (grid-stride), y = b*NH + h. Block = G groups of F lanes (G = 256/F).
+template <typename T>
+__global__ __launch_bounds__(256) void tattn_fwd_kernel(const T* __restrict__ qkv, const float* __restrict__ bias,
+                                                        const float* __restrict__ rotg, T* __restrict__ out,
+                                                        float* __restrict__ lse, int F, int HW, float scale) {
+  __shared__ float rot[128 * 32];
+  __shared__ float sb[32 * 32];
+  const int b = blockIdx.y / NH, h = blockIdx.y % NH;
+  for (int e = threadIdx.x; e < F * 32; e += blockDim.x) rot[e] = rotg[e];
+  for (int e = threadIdx.x; e < F * F; e += blockDim.x) sb[e] = bias[h * F * F + e];
+  __syncthreads();
+  const int G = 256 / F;
+  const int g = threadIdx.x / F, i = threadIdx.x % F;
+  if (g >= G) return;
+  const int npb = (HW + G - 1) / G;
+  for (int pb = blockIdx.x; pb < npb; pb += gridDim.x) {
+    const int p = pb * G + g;
+    if (p >= HW) continue;
+    const int64_t vi = ((int64_t)b * F + i) * HW + p;
+    float q[32], acc[32];
+    load32(qkv + vi * QKV + h * DH, q);
+#pragma unroll
+    for (int d = 0; d < 32; ++d) { q[d] *= scale; acc[d] = 0.f; }
+    rope(q, rot + i * 32, 1.f);
+    float m = -INFINITY, l = 0.f;
+    for (int j = 0; j < F; ++j) {
+      const int64_t vj = ((int64_t)b * F + j) * HW + p;
+      float k[32];
+      load32(qkv + vj * QKV + INNER + h * DH, k);
+      rope(k, rot + j * 32, 1.f);
+      float s = 0.f;
+#pragma unroll
+      for (int d = 0; d < 32; ++d) s = fmaf(q[d], k[d], s);
+      s += sb[i * F + j];
+      float v[32];
+      load32(qkv + vj * QKV + 2 * INNER + h * DH, v);
+      const float mn = fmaxf(m, s);
+      const float corr = expf(m - mn);
+      const float pj = expf(s - mn);
+      l = l * corr + pj;
+#pragma unroll
+      for (int d = 0; d < 32; ++d) acc[d] = fmaf(pj, v[d], acc[d] * corr);
+      m = mn;
+    }
+    const float inv = 1.f / l;
+#pragma unroll
+    for (int d = 0; d < 32; ++d) acc[d] *= inv;
+    store32(out + vi * INNER + h * DH, acc);
+    if (lse) lse[(((int64_t)b * NH + h) * HW + p) * F + i] = m + logf(l);
+  }
+}
+
+// backward.  Phase 1 (lane = query i): D_i, dq_i, dbias row accumulation.
+//            Phase 2 (lane = key j):   dk_j, dv_j.
+// dbias partials: part[blockIdx.y][blockIdx.x][i][j] (the block's sum over its pixels)
+template <typename T>
+__global__ __launch_bounds__(256) void tattn_bwd_kernel(const T* __restrict__ qkv, const T* __restrict__ o,
+                                                        const T* __restrict__ dout, const float* __restrict__ lse,
+                                                        const float* __restrict__ bias,
+                                                        const float* __restrict__ rotg, T* __restrict__ dqkv,
+                                                        float* __restrict__ dbias_part, int F, int HW, float scale) {
+  __shared__ float rot[128 * 32];
+  __shared__ float sb[32 * 32];
+  __shared__ float sD[256], sL[256];
+  __shared__ float red[256];
+  const int b = blockIdx.y / NH, h = blockIdx.y % NH;
+  for (int e = threadIdx.x; e < F * 32; e += blockDim.x) rot[e] = rotg[e];
+  for (int e = threadIdx.x; e < F * F; e += blockDim.x) sb[e] = bias[h * F * F + e];
+  __syncthreads();
+  const int G = 256 / F;
+  const int g = threadIdx.x / F, i = threadIdx.x % F;
+  const bool lane_ok = g < G;
+  float dbacc[32];
+  for (int j = 0; j < 32; ++j) dbacc[j] = 0.f;
+  const int npb = (HW + G - 1) / G;
+  for (int pb = blockIdx.x; pb < npb; pb += gridDim.x) {
+    const int p = pb * G + g;
+    const bool ok = lane_ok && p < HW;
+    // ---- phase 1: lane = query row i
+    float D = 0.f, L = 0.f;
+    if (ok) {
+      const int64_t vi = ((int64_t)b * F + i) * HW + p;
+      float q[32], dq[32], dO[32];
+      load32(dout + vi * INNER + h * DH, dO);
+      {
+        float ov[32];
+        load32(o + vi * INNER + h * DH, ov);
+#pragma unroll
+        for (int d = 0; d < 32; ++d) D = fmaf(dO[d], ov[d], D);
+      }
+      L = lse[(((int64_t)b * NH + h) * HW + p) * F + i];
+      load32(qkv + vi * QKV + h * DH, q);
+#pragma unroll
+      for (int d = 0; d < 32; ++d) { q[d] *= scale; dq[d] = 0.f; }
+      rope(q, rot + i * 32, 1.f);
+      for (int j = 0; j < F; ++j) {
+        const int64_t vj = ((int64_t)b * F + j) * HW + p;
+        float k[32], v[32];
+        load32(qkv + vj * QKV + INNER + h * DH, k);
+        load32(qkv + vj * QKV + 2 * INNER + h * DH, v);
+        rope(k, rot + j * 32, 1.f);
+        float s = 0.f, dp = 0.f;
+#pragma unroll
+        for (int d = 0; d < 32; ++d) { s = fmaf(q[d], k[d], s); dp = fmaf(dO[d], v[d], dp); }
+        s += sb[i * F + j];
+        const float P = expf(s - L);
+        const float dS = P * (dp - D);
+        if (j < 32) dbacc[j] += dS;
+#pragma unroll
+        for (int d = 0; d < 32; ++d) dq[d] = fmaf(dS, k[d], dq[d]);
+      }
+      rope(dq, rot + i * 32, -1.f);
+#pragma unroll
+      for (int d = 0; d < 32; ++d) dq[d] *= scale;
+      store32(dqkv + vi * QKV + h * DH, dq);
+    }
+    sD[threadIdx.x] = D;
+    sL[threadIdx.x] = L;
+    __syncthreads();
+    // ---- phase 2: lane = key row j (= i index of this lane)
+    if (ok) {
+      const int j = i;
+      const int64_t vj = ((int64_t)b * F + j) * HW + p;
+      float k[32], dk[32], dv[32];
+      load32(qkv + vj * QKV + INNER + h * DH, k);
+      rope(k, rot + j * 32, 1.f);
+      float v[32];
+      load32(qkv + vj * QKV + 2 * INNER + h * DH, v);
+#pragma unroll
+      for (int d = 0; d < 32; ++d) { dk[d] = 0.f; dv[d] = 0.f; }
+      for (int ii = 0; ii < F; ++ii) {
+        const int64_t vi = ((int64_t)b * F + ii) * HW + p;
+        float q[32], dO[32];
+        load32(qkv + vi * QKV + h * DH, q);
+#pragma unroll
+        for (int d = 0; d < 32; ++d) q[d] *= scale;
+        rope(q, rot + ii * 32, 1.f);
+        load32(dout + vi * INNER + h * DH, dO);
+        float s = 0.f, dp = 0.f;
+#pragma unroll
+        for (int d = 0; d < 32; ++d) { s = fmaf(q[d], k[d], s); dp = fmaf(dO[d], v[d], dp); }
+        s += sb[ii * F + j];
+        const int t2 = g * F + ii;
+        const float P = expf(s - sL[t2]);
+        const float dS = P * (dp - sD[t2]);
+#pragma unroll
+        for (int d = 0; d < 32; ++d) { dk[d] = fmaf(dS, q[d], dk[d]); dv[d] = fmaf(P, dO[d], dv[d]); }
+      }
+      rope(dk, rot + j * 32, -1.f);
+      store32(dqkv + vj * QKV + INNER + h * DH, dk);
+      store32(dqkv + vj * QKV + 2 * INNER + h * DH, dv);
+    }
+    __syncthreads();
+  }
+  // deterministic block reduction of dbias rows: for each j, sum lanes with the same i
+  float* outp = dbias_part + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * F * F;
+  for (int j = 0; j < F; ++j) {
+    red[threadIdx.x] = (lane_ok && j < 32) ? dbacc[j] : 0.f;
+    __syncthreads();
+    if ((int)threadIdx.x < F) {
+      float s = 0.f;
+      for (int gg = 0; gg < G; ++gg) s += red[gg * F + threadIdx.x];
+      outp[threadIdx.x * F + j] = s;
+    }
+    __syncthreads();
+  }
+}
+
+// rel-pos bias (video_net.py:268-310): bias[h][i][j] = table[bucket(j - i)][h]
+__device__ int relpos_bucket(int rel, int num_buckets, int max_distance) {
+  int n = -rel;
+  const int nb = num_buckets / 2;
+  int ret = n < 0 ? nb : 0;
+  n = n < 0 ? -n : n;
+  const int max_exact = nb / 2;
+  if (n < max_exact) return ret + n;
+  // float32 log as in torch: (log(n/max_exact) / log(max_distance/max_exact) * (nb-max_exact)).long()
+  const float lg = logf((float)n / (float)max_exact) / logf((float)max_distance / (float)max_exact) *
+                   (float)(nb - max_exact);
+  int large = max_exact + (int)lg;
+  if (large > nb - 1) large = nb - 1;
+  return ret + large;
+}
+
+__global__ void relpos_fwd_kernel(const float* __restrict__ table, float* __restrict__ bias, int F, int heads,
+                                  int num_buckets, int max_distance) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= heads * F * F) return;
+  const int h = t / (F * F), r = t % (F * F);
+  const int i = r / F, j = r % F;
+  bias[t] = table[relpos_bucket(j - i, num_buckets, max_distance) * heads + h];
+}
+
+// dtable[bucket][h] (+)= sum over (i,j) with that bucket of sum over parts of dbias_part
+__global__ void relpos_bwd_kernel(const float* __restrict__ part, int nparts_per_h, int B, float* __restrict__ dtable,
+                                  int F, int heads, int num_buckets, int max_distance, int accumulate) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= num_buckets * heads) return;
+  const int bk = t / heads, h = t % heads;
+  float s = 0.f;
+  for (int i = 0; i < F; ++i)
+    for (int j = 0; j < F; ++j) {
+      if (relpos_bucket(j - i, num_buckets, max_distance) != bk) continue;
+      for (int b = 0; b < B; ++b)
+        for (int k = 0; k < nparts_per_h; ++k)
+          s += part[((int64_t)(b * heads + h) * nparts_per_h + k) * F * F + i * F + j];
+    }
+  dtable[t] = accumulate ? dtable[t] + s : s;
+}
+
+// ---------------------------------------------------------------- spatial linear attention
+constexpr int SLA_TILE = 64;
+
+// grid: x = chunk, y = frame*NH + h.  pm/pl: [frame*NH+h][chunk][32], pctx: [..][chunk][32][32]
+template <typename T>
+__global__ __launch_bounds__(256) void sla_ctx_partial_kernel(const T* __restrict__ qkv, float* __restrict__ pm,
+                                                              float* __restrict__ pl, float* __restrict__ pctx,
+                                                              int HW, int chunk) {
+  __shared__ float sk[DH][SLA_TILE + 1];
+  __shared__ float sv[SLA_TILE][DH + 1];
+  __shared__ float smax[DH];
+  const int fh = blockIdx.y;
+  const int f = fh / NH, h = fh % NH;
+  const int n0 = blockIdx.x * chunk, n1 = min(HW, n0 + chunk);
+  const int tid = threadIdx.x;
+  const int d = tid >> 3, e0 = (tid & 7) * 4;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+  const T* base = qkv + (int64_t)f * HW * QKV;
+  for (int t0 = n0; t0 < n1; t0 += SLA_TILE) {
+    // stage k[d][n], v[n][e] for the tile: 64 voxels x (32 k + 32 v); thread -> (voxel, 8-chunk)
+    {
+      const int vx = tid >> 2, part = tid & 3;  // 64 voxels x 4 parts of 8
+      const int n = t0 + vx;
+      float kk[8], vv[8];
+      if (n < n1) {
+        load8(base + (int64_t)n * QKV + INNER + h * DH + part * 8, kk);
+        load8(base + (int64_t)n * QKV + 2 * INNER + h * DH + part * 8, vv);
+      } else {
+        for (int x = 0; x < 8; ++x) { kk[x] = -INFINITY; vv[x] = 0.f; }
+      }
+#pragma unroll
+      for (int x = 0; x < 8; ++x) { sk[part * 8 + x][vx] = kk[x]; sv[vx][part * 8 + x] = vv[x]; }
+    }
+    __syncthreads();
+    if (tid < DH) {
+      float mx = -INFINITY;
+      for (int x = 0; x < SLA_TILE; ++x) mx = fmaxf(mx, sk[tid][x]);
+      smax[tid] = mx;
+    }
+    __syncthreads();
+    const float mn = fmaxf(m, smax[d]);
+    const float corr = (m == -INFINITY) ? 0.f : expf(m - mn);
+    l *= corr;
+#pragma unroll
+    for (int x = 0; x < 4; ++x) acc[x] *= corr;
+    __syncthreads();
+    for (int x = 0; x < SLA_TILE; ++x) {
+      const float pexp = expf(sk[d][x] - mn);
+      l += pexp;
+#pragma unroll
+      for (int y = 0; y < 4; ++y) acc[y] = fmaf(pexp, sv[x][e0 + y], acc[y]);
+    }
+    m = mn;
+    __syncthreads();
+  }
+  const int64_t pi = (int64_t)fh * gridDim.x + blockIdx.x;
+  if ((tid & 7) == 0) { pm[pi * DH + d] = m; pl[pi * DH + d] = l; }
+#pragma unroll
+  for (int y = 0; y < 4; ++y) pctx[(pi * DH + d) * DH + e0 + y] = acc[y];
+}
+
+// combine: ctx[fh][d][e] = sum_c pctx_c e^{m_c - m} / l ; ml[fh][d] = (m, l)
+__global__ void sla_ctx_combine_kernel(const float* __restrict__ pm, const float* __restrict__ pl,
+                                       const float* __restrict__ pctx, float* __restrict__ ctx,
+                                       float* __restrict__ ml, int nchunk) {
+  const int fh = blockIdx.x;
+  const int d = threadIdx.x >> 5, e = threadIdx.x & 31;  // 1024 threads
+  float m = -INFINITY;
+  for (int c = 0; c < nchunk; ++c) m = fmaxf(m, pm[((int64_t)fh * nchunk + c) * DH + d]);
+  float l = 0.f, s = 0.f;
+  for (int c = 0; c < nchunk; ++c) {
+    const int64_t pi = (int64_t)fh * nchunk + c;
+    const float w = expf(pm[pi * DH + d] - m);
+    l = fmaf(pl[pi * DH + d], w, l);
+    s = fmaf(pctx[(pi * DH + d) * DH + e], w, s);
+  }
+  ctx[((int64_t)fh * DH + d) * DH + e] = s / l;
+  if (e == 0) { ml[((int64_t)fh * DH + d) * 2] = m; ml[((int64_t)fh * DH + d) * 2 + 1] = l; }
+}
+
+// out[v][h*32+e] = sum_d ctx[f,h][d][e] * qs[d], qs = softmax_d(q) * scale
+// grid: x = voxel block (32 voxels x 8 heads = 256 threads), y = frame
+template <typename T>
+__global__ __launch_bounds__(256) void sla_out_kernel(const T* __restrict__ qkv, const float* __restrict__ ctx,
+                                                      T* __restrict__ out, int HW, float scale) {
+  __shared__ float sc[NH * DH * DH];
+  const int f = blockIdx.y;
+  for (int e = threadIdx.x; e < NH * DH * DH; e += 256) sc[e] = ctx[(int64_t)f * NH * DH * DH + e];
+  __syncthreads();
+  const int h = threadIdx.x & 7, vl = threadIdx.x >> 3;
+  const int p = blockIdx.x * 32 + vl;
+  if (p >= HW) return;
+  const int64_t v = (int64_t)f * HW + p;
+  float q[32];
+  load32(qkv + v * QKV + h * DH, q);
+  float mx = -INFINITY;
+#pragma unroll
+  for (int d = 0; d < 32; ++d) mx = fmaxf(mx, q[d]);
+  float s = 0.f;
+#pragma unroll
+  for (int d = 0; d < 32; ++d) { q[d] = expf(q[d] - mx); s += q[d]; }
+  const float inv = scale / s;
+  float o[32];
+#pragma unroll
+  for (int e = 0; e < 32; ++e) o[e] = 0.f;
+  const float* C = sc + h * DH * DH;
+#pragma unroll 4
+  for (int d = 0; d < 32; ++d) {
+    const float qd = q[d] * inv;
+#pragma unroll
+    for (int e = 0; e < 32; e += 4) {
+      const f32x4 c4 = *reinterpret_cast<const f32x4*>(C + d * DH + e);
+      o[e] = fmaf(c4[0], qd, o[e]);
+      o[e + 1] = fmaf(c4[1], qd, o[e + 1]);
+      o[e + 2] = fmaf(c4[2], qd, o[e + 2]);
+      o[e + 3] = fmaf(c4[3], qd, o[e + 3]);
+    }
+  }
+  store32(out + v * INNER + h * DH, o);
+}
+
+// dctx partial: pd[fh][chunk][d][e] = sum_n qs[d][n] dout[e][n]
+template <typename T>
+__global__ __launch_bounds__(256) void sla_dctx_partial_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
+                                                               float* __restrict__ pd, int HW, int chunk,
+                                                               float scale) {
+  __shared__ float sq[SLA_TILE][DH + 1];
+  __shared__ float sg[SLA_TILE][DH + 1];
+  const int fh = blockIdx.y;
+  const int f = fh / NH, h = fh % NH;
+  const int n0 = blockIdx.x * chunk, n1 = min(HW, n0 + chunk);
+  const int tid = threadIdx.x;
+  const int d = tid >> 3, e0 = (tid & 7) * 4;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  const T* qb = qkv + (int64_t)f * HW * QKV;
+  const T* gb = dout + (int64_t)f * HW * INNER;
+  for (int t0 = n0; t0 < n1; t0 += SLA_TILE) {
+    if (tid < SLA_TILE) {
+      const int n = t0 + tid;
+      float q[32], gg[32];
+      if (n < n1) {
+        load32(qb + (int64_t)n * QKV + h * DH, q);
+        load32(gb + (int64_t)n * INNER + h * DH, gg);
+        float mx = -INFINITY;
+        for (int x = 0; x < 32; ++x) mx = fmaxf(mx, q[x]);
+        float s = 0.f;
+        for (int x = 0; x < 32; ++x) { q[x] = expf(q[x] - mx); s += q[x]; }
+        const float inv = scale / s;
+        for (int x = 0; x < 32; ++x) q[x] *= inv;
+      } else {
+        for (int x = 0; x < 32; ++x) { q[x] = 0.f; gg[x] = 0.f; }
+      }
+      for (int x = 0; x < 32; ++x) { sq[tid][x] = q[x]; sg[tid][x] = gg[x]; }
+    }
+    __syncthreads();
+    for (int x = 0; x < SLA_TILE; ++x) {
+      const float qd = sq[x][d];
+#pragma unroll
+      for (int y = 0; y < 4; ++y) acc[y] = fmaf(qd, sg[x][e0 + y], acc[y]);
+    }
+    __syncthreads();
+  }
+  const int64_t pi = (int64_t)fh * gridDim.x + blockIdx.x;
+#pragma unroll
+  for (int y = 0; y < 4; ++y) pd[(pi * DH + d) * DH + e0 + y] = acc[y];
+}
+
+// dctx[fh] = sum over chunks ; cvec[fh][d] = sum_e dctx[d][e]*ctx[d][e]
+__global__ void sla_dctx_combine_kernel(const float* __restrict__ pd, const float* __restrict__ ctx,
+                                        float* __restrict__ dctx, float* __restrict__ cvec, int nchunk) {
+  const int fh = blockIdx.x;
+  const int d = threadIdx.x >> 5, e = threadIdx.x & 31;
+  float s = 0.f;
+  for (int c = 0; c < nchunk; ++c) s += pd[(((int64_t)fh * nchunk + c) * DH + d) * DH + e];
+  dctx[((int64_t)fh * DH + d) * DH + e] = s;
+  float prod = s * ctx[((int64_t)fh * DH + d) * DH + e];
+  // reduce over e (32 lanes of the same d share a half-wave)
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) prod += __shfl_xor(prod, o, 64);
+  if (e == 0) cvec[(int64_t)fh * DH + d] = prod;
+}
+
+// per voxel, per head: dq, dk, dv
+template <typename T>
+__global__ __launch_bounds__(256) void sla_bwd_voxel_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
+                                                            const float* __restrict__ ctx,
+                                                            const float* __restrict__ dctx,
+                                                            const float* __restrict__ ml,
+                                                            const float* __restrict__ cvec, T* __restrict__ dqkv,
+                                                            int HW, float scale) {
+  __shared__ float sc[NH * DH * DH];
+  __shared__ float sdc[NH * DH * DH];
+  const int f = blockIdx.y;
+  for (int e = threadIdx.x; e < NH * DH * DH; e += 256) {
+    sc[e] = ctx[(int64_t)f * NH * DH * DH + e];
+    sdc[e] = dctx[(int64_t)f * NH * DH * DH + e];
+  }
+  __syncthreads();
+  const int h = threadIdx.x & 7, vl = threadIdx.x >> 3;
+  const int p = blockIdx.x * 32 + vl;
+  if (p >= HW) return;
+  const int64_t v = (int64_t)f * HW + p;
+  const float* C = sc + h * DH * DH;
+  const float* DC = sdc + h * DH * DH;
+  const int64_t fh = (int64_t)f * NH + h;
+  // ---- dq
+  {
+    float q[32], g[32];
+    load32(qkv + v * QKV + h * DH, q);
+    load32(dout + v * INNER + h * DH, g);
+    float mx = -INFINITY;
+#pragma unroll
+    for (int d = 0; d < 32; ++d) mx = fmaxf(mx, q[d]);
+    float s = 0.f;
+#pragma unroll
+    for (int d = 0; d < 32; ++d) { q[d] = expf(q[d] - mx); s += q[d]; }
+    const float inv = 1.f / s;
+    float dsm[32], dot = 0.f;
+#pragma unroll
+    for (int d = 0; d < 32; ++d) {
+      q[d] *= inv;  // sm
+      float t = 0.f;
+#pragma unroll
+      for (int e = 0; e < 32; ++e) t = fmaf(C[d * DH + e], g[e], t);
+      dsm[d] = scale * t;
+      dot = fmaf(q[d], dsm[d], dot);
+    }
+#pragma unroll
+    for (int d = 0; d < 32; ++d) dsm[d] = q[d] * (dsm[d] - dot);
+    store32(dqkv + v * QKV + h * DH, dsm);
+  }
+  // ---- dk, dv
+  {
+    float k[32], vv[32];
+    load32(qkv + v * QKV + INNER + h * DH, k);
+    load32(qkv + v * QKV + 2 * INNER + h * DH, vv);
+    float dk[32], dv[32];
+#pragma unroll
+    for (int e = 0; e < 32; ++e) dv[e] = 0.f;
+#pragma unroll 4
+    for (int d = 0; d < 32; ++d) {
+      const float m = ml[(fh * DH + d) * 2], l = ml[(fh * DH + d) * 2 + 1];
+      const float ks = expf(k[d] - m) / l;
+      float t = 0.f;
+#pragma unroll
+      for (int e = 0; e < 32; ++e) {
+        t = fmaf(DC[d * DH + e], vv[e], t);
+        dv[e] = fmaf(DC[d * DH + e], ks, dv[e]);
+      }
+      dk[d] = ks * (t - cvec[fh * DH + d]);
+    }
+    store32(dqkv + v * QKV + INNER + h * DH, dk);
+    store32(dqkv + v * QKV + 2 * INNER + h * DH, dv);
+  }
+}
+
+template <typename F>
+static int dispatch_dt(int dtype, F&& f) {
+  if (dtype == CESM_DT_BF16) { f((bf16*)nullptr); return CESM_OK; }
+  if (dtype == CESM_DT_F32) { f((float*)nullptr); return CESM_OK; }
+  return CESM_EINVAL;
+}
+
+static int sla_chunk(int HW) {
+  // ~2048 positions per chunk, multiple of the tile
+  int c = 2048;
+  if (HW < c) c = ((HW + SLA_TILE - 1) / SLA_TILE) * SLA_TILE;
+  return c;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cesm_rope_table(const float* freqs, float* rot, int F, hipStream_t stream) {
+  if (F > 128) return CESM_EINVAL;
+  rope_table_kernel<<<(unsigned)cdiv(F * 16, 256), 256, 0, stream>>>(freqs, rot, F);
+  return cesm_launch_status();
+}
+
+int cesm_relpos_fwd(const float* table, float* bias, int F, int heads, int num_buckets, int max_distance,
+                    hipStream_t stream) {
+  relpos_fwd_kernel<<<(unsigned)cdiv(heads * F * F, 256), 256, 0, stream>>>(table, bias, F, heads, num_buckets,
+                                                                             max_distance);
+  return cesm_launch_status();
+}
+
+int cesm_relpos_bwd(const float* part, int nparts_per_h, int B, float* dtable, int F, int heads, int num_buckets,
+                    int max_distance, int accumulate, hipStream_t stream) {
+  relpos_bwd_kernel<<<(unsigned)cdiv(num_buckets * heads, 64), 64, 0, stream>>>(
+      part, nparts_per_h, B, dtable, F, heads, num_buckets, max_distance, accumulate);
+  return cesm_launch_status();
+}
+
+// number of pixel blocks (grid.x) used by the temporal-attention kernels for HW pixels
+int cesm_tattn_nblk(int F, int HW) {
+  const int G = 256 / F;
+  int64_t npb = cdiv(HW, G);
+  return (int)std::min<int64_t>(npb, 128);
+}
+
+int cesm_tattn_fwd(int dtype, const void* qkv, const float* bias, const float* rot, void* out, float* lse, int B,
+                   int F, int HW, float scale, hipStream_t stream) {
+  if (F < 1 || F > 32) return CESM_EUNSUPPORTED;
+  dim3 grid(cesm_tattn_nblk(F, HW), B * NH);
+  return dispatch_dt(dtype, [&](auto* tp) {
+    using T = std::remove_pointer_t<decltype(tp)>;
+    tattn_fwd_kernel<T><<<grid, 256, 0, stream>>>((const T*)qkv, bias, rot, (T*)out, lse, F, HW, scale);
+  }) ?: cesm_launch_status();
+}
+
+// dbias_part: B*NH*nblk*F*F floats, nblk = cesm_tattn_nblk(F, HW)
+int cesm_tattn_bwd(int dtype, const void* qkv, const void* o, const void* dout, const float* lse, const float* bias,
+                   const float* rot, void* dqkv, float* dbias_part, int B, int F, int HW, float scale,
+                   hipStream_t stream) {
+  if (F < 1 || F > 32) return CESM_EUNSUPPORTED;
+  dim3 grid(cesm_tattn_nblk(F, HW), B * NH);
+  return dispatch_dt(dtype, [&](auto* tp) {
+    using T = std::remove_pointer_t<decltype(tp)>;
+    tattn_bwd_kernel<T><<<grid, 256, 0, stream>>>((const T*)qkv, (const T*)o, (const T*)dout, lse, bias, rot,
+                                                  (T*)dqkv, dbias_part, F, HW, scale);
+  }) ?: cesm_launch_status();
+}
+
+int cesm_sla_nchunk(int HW) { return (int)cdiv(HW, sla_chunk(HW)); }
+
+// Nf = number of frames (B*F); ws: floats >= Nf*NH*nchunk*(32+32+1024); ctx [Nf][NH][32][32], ml [Nf][NH][32][2]
+int cesm_sla_fwd(int dtype, const void* qkv, void* out, float* ctx, float* ml, float* ws, int Nf, int HW, float scale,
+                 hipStream_t stream) {
+  const int chunk = sla_chunk(HW);
+  const int nchunk = (int)cdiv(HW, chunk);
+  float* pm = ws;
+  float* pl = pm + (int64_t)Nf * NH * nchunk * DH;
+  float* pctx = pl + (int64_t)Nf * NH * nchunk * DH;
+  return dispatch_dt(dtype, [&](auto* tp) {
+    using T = std::remove_pointer_t<decltype(tp)>;
+    sla_ctx_partial_kernel<T><<<dim3(nchunk, Nf * NH), 256, 0, stream>>>((const T*)qkv, pm, pl, pctx, HW, chunk);
+    sla_ctx_combine_kernel<<<Nf * NH, 1024, 0, stream>>>(pm, pl, pctx, ctx, ml, nchunk);
+    sla_out_kernel<T><<<dim3((unsigned)cdiv(HW, 32), Nf), 256, 0, stream>>>((const T*)qkv, ctx, (T*)out, HW, scale);
+  }) ?: cesm_launch_status();
+}
+
+// ws: floats >= Nf*NH*nchunk*1024 + Nf*NH*(1024+32)
+int cesm_sla_bwd(int dtype, const void* qkv, const void* dout, const float* ctx, const float* ml, void* dqkv,
+                 float* ws, int Nf, int HW, float scale, hipStream_t stream) {
+  const int chunk = sla_chunk(HW);
+  const int nchunk = (int)cdiv(HW, chunk);
+  float* pd = ws;
+  float* dctx = pd + (int64_t)Nf * NH * nchunk * DH * DH;
+  float* cvec = dctx + (int64_t)Nf * NH * DH * DH;
+  return dispatch_dt(dtype, [&](auto* tp) {
+    using T = std::remove_pointer_t<decltype(tp)>;
+    sla_dctx_partial_kernel<T><<<dim3(nchunk, Nf * NH), 256, 0, stream>>>((const T*)qkv, (const T*)dout, pd, HW,
+                                                                           chunk, scale);
+    sla_dctx_combine_kernel<<<Nf * NH, 1024, 0, stream>>>(pd, ctx, dctx, cvec, nchunk);
+    sla_bwd_voxel_kernel<T><<<dim3((unsigned)cdiv(HW, 32), Nf), 256, 0, stream>>>(
+        (const T*)qkv, (const T*)dout, ctx, dctx, ml, cvec, (T*)dqkv, HW, scale);
+  }) ?: cesm_launch_status();
+}
+
+}  // extern "C"

@@ -1,0 +1,106 @@
+// Shared device helpers for the CESM-emulator gfx950 kernels.
+// Storage types: float (fp32 parity mode) and __bf16 (perf mode); all arithmetic and
+// all reductions are fp32 (fp64 where a cross-workgroup statistic needs it).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define CESM_OK 0
+#define CESM_EINVAL -1
+#define CESM_EUNSUPPORTED -2
+#define CESM_ELAUNCH -3
+
+#define CESM_DT_F32 0
+#define CESM_DT_BF16 1
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+#define LDS_PTR(T) __attribute__((address_space(3))) T*
+
+static inline int cesm_launch_status() {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? CESM_OK : CESM_ELAUNCH;
+}
+
+__device__ __forceinline__ float to_f(float x) { return x; }
+__device__ __forceinline__ float to_f(bf16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f(float x);
+template <> __device__ __forceinline__ float from_f<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f<bf16>(float x) { return (bf16)x; }
+
+// 8 consecutive elements <-> 8 floats (16 B for bf16, 32 B for fp32)
+__device__ __forceinline__ void load8(const float* p, float* v) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(p);
+  const f32x4 b = *reinterpret_cast<const f32x4*>(p + 4);
+  v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+  v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+}
+__device__ __forceinline__ void load8(const bf16* p, float* v) {
+  const bf16x8 a = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (float)a[i];
+}
+__device__ __forceinline__ void store8(float* p, const float* v) {
+  f32x4 a = {v[0], v[1], v[2], v[3]};
+  f32x4 b = {v[4], v[5], v[6], v[7]};
+  *reinterpret_cast<f32x4*>(p) = a;
+  *reinterpret_cast<f32x4*>(p + 4) = b;
+}
+__device__ __forceinline__ void store8(bf16* p, const float* v) {
+  bf16x8 a;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = (bf16)v[i];
+  *reinterpret_cast<bf16x8*>(p) = a;
+}
+__device__ __forceinline__ void load4(const float* p, float* v) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(p);
+  v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+}
+__device__ __forceinline__ void load4(const bf16* p, float* v) {
+  const bf16x4 a = *reinterpret_cast<const bf16x4*>(p);
+  v[0] = (float)a[0]; v[1] = (float)a[1]; v[2] = (float)a[2]; v[3] = (float)a[3];
+}
+__device__ __forceinline__ void store4(float* p, const float* v) {
+  f32x4 a = {v[0], v[1], v[2], v[3]};
+  *reinterpret_cast<f32x4*>(p) = a;
+}
+__device__ __forceinline__ void store4(bf16* p, const float* v) {
+  bf16x4 a = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+  *reinterpret_cast<bf16x4*>(p) = a;
+}
+
+__device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x)); }
+// exact-ish silu for parity: expf (not the fast intrinsic)
+__device__ __forceinline__ float silu_p(float x) { return x / (1.f + expf(-x)); }
+__device__ __forceinline__ float dsilu_p(float x) {
+  const float s = 1.f / (1.f + expf(-x));
+  return s * (1.f + x * (1.f - s));
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// sum over aligned groups of `width` lanes (width power of two <= 64)
+__device__ __forceinline__ float group_sum(float v, int width) {
+  for (int o = width >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }

@@ -1,0 +1,836 @@
+// Implicit-GEMM convolutions on MFMA for the video_net U-Net (all convs are per-frame
+// (1,k,k), so the frame axis folds into the batch: Nb = B*F "images").
+//
+// Activations are channels-last [Nb][H][W][C].  One generic forward kernel covers every
+// conv in the net and every data-gradient (replaces ATen conv3d / conv_transpose3d at
+// video_net.py:215 (Block.proj), :246 (res_conv), :61-62 (Downsample), :65-66 (Upsample),
+// :380/:381 + :322/:323 (attention projections, as 1x1 convs), and their dgrads):
+//
+//   out[m=(n,oy,ox)][co] = bias[co] + res[m][co]
+//                        + sum_{ky,kx,ci} W[co][ky*KW+kx][ci] * X[n][iy][ix][ci]
+//   iy = (oy*S - P + ky) / U   (only when (oy*S - P + ky) % U == 0), likewise ix.
+//
+// U = 1 is an ordinary strided conv; U = 2 with flipped taps is a stride-2 transposed conv.
+// The GEMM is computed transposed (D = W * X^T) so each lane's accumulator holds 4
+// consecutive output channels of one pixel -> vectorised channels-last stores.
+//
+// Weight gradients use a second MFMA kernel (pixel axis = MFMA K) that writes fp32 split-K
+// slabs, reduced deterministically by conv_wgrad_reduce into the PyTorch weight layout.
+#include "common.h"
+
+namespace {
+
+struct ConvGeom {
+  int Nb, Hi, Wi, Ho, Wo;
+  int C1, C2;       // input channels from source 1 / source 2 (concat on channel axis)
+  int Cout, Co1;    // output channels; [0,Co1) -> y1, [Co1,Cout) -> y2
+  int KH, KW, S, P, U;
+};
+
+__device__ __forceinline__ bool tap_src(const ConvGeom& g, int oy, int ox, int ky, int kx, int& iy, int& ix) {
+  int ny = oy * g.S - g.P + ky;
+  int nx = ox * g.S - g.P + kx;
+  if (g.U != 1) {
+    if ((ny % g.U) != 0 || (nx % g.U) != 0) return false;  // negative remainders are non-zero too
+    ny /= g.U;
+    nx /= g.U;
+  }
+  iy = ny;
+  ix = nx;
+  return (unsigned)ny < (unsigned)g.Hi && (unsigned)nx < (unsigned)g.Wi;
+}
+
+// ----------------------------------------------------------------------------------------
+// forward / dgrad kernel
+// ----------------------------------------------------------------------------------------
+constexpr int BK = 32;       // K per staging step (channels of one tap)
+constexpr int BMP = 128;     // pixels per block
+
+template <typename T> struct KCfg;
+template <> struct KCfg<bf16> { static constexpr int VEC = 8; static constexpr int LDW = 40; };   // 80-B rows
+template <> struct KCfg<float> { static constexpr int VEC = 4; static constexpr int LDW = 36; };  // 144-B rows
+
+template <typename T, int BN>
+__global__ __launch_bounds__(256) void conv_fwd_kernel(const T* __restrict__ x1, const T* __restrict__ x2,
+                                                       const T* __restrict__ w, const float* __restrict__ bias,
+                                                       const T* __restrict__ res, const T* __restrict__ res2,
+                                                       T* __restrict__ y1, T* __restrict__ y2, ConvGeom g,
+                                                       int64_t M) {
+  constexpr int VEC = KCfg<T>::VEC;
+  constexpr int LDW = KCfg<T>::LDW;
+  constexpr int VPR = BK / VEC;          // vectors per row
+  constexpr int RPP = 256 / VPR;         // rows per pass
+  constexpr int PX_PASS = BMP / RPP;     // pixel-tile passes per thread
+  constexpr int W_PASS = BN / RPP;       // weight-tile passes per thread
+  constexpr int TM = BN / 32;            // 16-row co tiles per wave (wave covers BN/2 co)
+  constexpr int TN = 4;                  // 16-col pixel tiles per wave (wave covers 64 px)
+
+  __shared__ __attribute__((aligned(16))) T lds[2][(BMP + BN) * LDW];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int64_t m0 = (int64_t)blockIdx.x * BMP;
+  const int n0 = blockIdx.y * BN;
+  const int Cin = g.C1 + g.C2;
+  const int csteps = Cin / BK;
+  const int ksteps = g.KH * g.KW * csteps;
+
+  // per-thread staging rows
+  const int vrow = tid / VPR, vk = (tid % VPR) * VEC;
+  int pn[PX_PASS], poy[PX_PASS], pox[PX_PASS];
+  bool pval[PX_PASS];
+#pragma unroll
+  for (int p = 0; p < PX_PASS; ++p) {
+    const int64_t m = m0 + vrow + p * RPP;
+    pval[p] = m < M;
+    const int64_t mm = pval[p] ? m : 0;
+    pox[p] = (int)(mm % g.Wo);
+    const int64_t t = mm / g.Wo;
+    poy[p] = (int)(t % g.Ho);
+    pn[p] = (int)(t / g.Ho);
+  }
+
+  float xr[PX_PASS][VEC];
+  float wreg[W_PASS][VEC];
+
+  auto gload = [&](int ks) {
+    const int tap = ks / csteps;
+    const int c0 = (ks - tap * csteps) * BK;
+    const int ky = tap / g.KW, kx = tap - ky * g.KW;
+    const T* src;
+    int cs, cc;
+    if (c0 < g.C1) { src = x1; cs = g.C1; cc = c0; } else { src = x2; cs = g.C2; cc = c0 - g.C1; }
+#pragma unroll
+    for (int p = 0; p < PX_PASS; ++p) {
+      int iy, ix;
+      if (pval[p] && tap_src(g, poy[p], pox[p], ky, kx, iy, ix)) {
+        const T* ptr = src + ((((int64_t)pn[p] * g.Hi + iy) * g.Wi + ix) * cs + cc + vk);
+        if constexpr (VEC == 8) load8(ptr, xr[p]); else load4(ptr, xr[p]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) xr[p][i] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < W_PASS; ++p) {
+      const int co = n0 + vrow + p * RPP;
+      const T* ptr = w + ((int64_t)co * (g.KH * g.KW) + tap) * Cin + c0 + vk;
+      if constexpr (VEC == 8) load8(ptr, wreg[p]); else load4(ptr, wreg[p]);
+    }
+  };
+  auto sstore = [&](int buf) {
+    T* A = lds[buf];              // weights  [BN][LDW]
+    T* B = lds[buf] + BN * LDW;   // pixels   [BMP][LDW]
+#pragma unroll
+    for (int p = 0; p < W_PASS; ++p) {
+      T* d = A + (vrow + p * RPP) * LDW + vk;
+      if constexpr (VEC == 8) store8(d, wreg[p]); else store4(d, wreg[p]);
+    }
+#pragma unroll
+    for (int p = 0; p < PX_PASS; ++p) {
+      T* d = B + (vrow + p * RPP) * LDW + vk;
+      if constexpr (VEC == 8) store8(d, xr[p]); else store4(d, xr[p]);
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  gload(0);
+  sstore(0);
+  __syncthreads();
+
+  const int lr = lane & 15, lg = lane >> 4;
+  for (int ks = 0; ks < ksteps; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < ksteps) gload(ks + 1);
+    const T* A = lds[buf];
+    const T* B = lds[buf] + BN * LDW;
+    if constexpr (sizeof(T) == 2) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(A + (wr * (BN / 2) + i * 16 + lr) * LDW + lg * 8);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(B + (wc * 64 + j * 16 + lr) * LDW + lg * 8);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    } else {
+      // fp32: lane holds k = 16h + 4*lg + s; the same permutation on both operands
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f32x4 af[TM], bfr[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          af[i] = *reinterpret_cast<const f32x4*>(A + (wr * (BN / 2) + i * 16 + lr) * LDW + h * 16 + lg * 4);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          bfr[j] = *reinterpret_cast<const f32x4*>(B + (wc * 64 + j * 16 + lr) * LDW + h * 16 + lg * 4);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s], bfr[j][s], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (ks + 1 < ksteps) sstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: lane holds co = base + 4*lg + r (r=0..3) of pixel m
+  const int Co2 = g.Cout - g.Co1;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int64_t m = m0 + wc * 64 + j * 16 + lr;
+    if (m >= M) continue;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int co = n0 + wr * (BN / 2) + i * 16 + lg * 4;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (bias) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += bias[co + r];
+      }
+      if (co < g.Co1) {
+        if (res) {
+          float rv[4];
+          load4(res + m * g.Co1 + co, rv);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += rv[r];
+        }
+        store4(y1 + m * g.Co1 + co, v);
+      } else {
+        if (res2) {
+          float rv[4];
+          load4(res2 + m * Co2 + (co - g.Co1), rv);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += rv[r];
+        }
+        store4(y2 + m * Co2 + (co - g.Co1), v);
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// weight-gradient kernel: slab[split][co][tap*Cin + ci] = sum over the split's pixels of
+//   dY[m][co] * X(m, tap, ci)
+// Pixel axis is the MFMA K.  Output tile 64 co x 64 K-columns (one tap, 64 channels).
+// ----------------------------------------------------------------------------------------
+constexpr int WG_BP = 32;   // pixels per step
+
+template <typename T>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(const T* __restrict__ x1, const T* __restrict__ x2,
+                                                         const T* __restrict__ dy1, const T* __restrict__ dy2,
+                                                         float* __restrict__ slab, ConvGeom g, int64_t M,
+                                                         int64_t px_per_split) {
+  // LDS tiles are [pixel][64] row-major; bf16 rows are XOR-swizzled in 8-byte chunks so the
+  // transposed reads (ds_read_b64_tr_b16) are conflict free.
+  constexpr int VEC = sizeof(T) == 2 ? 8 : 4;
+  constexpr int ROW = 64;                    // elements per row
+  constexpr int LDR = sizeof(T) == 2 ? 64 : 65;
+  __shared__ __attribute__((aligned(16))) T tY[2][WG_BP * LDR];
+  __shared__ __attribute__((aligned(16))) T tX[2][WG_BP * LDR];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;       // wave owns co [wr*32,+32) x kcol [wc*32,+32)
+  const int Cin = g.C1 + g.C2;
+  const int co0 = blockIdx.x * 64;
+  const int kcol0 = blockIdx.y * 64;           // global K column (tap*Cin + ci)
+  const int tap = kcol0 / Cin;
+  const int ci0 = kcol0 - tap * Cin;
+  const int ky = tap / g.KW, kx = tap - ky * g.KW;
+  const int64_t pbeg = (int64_t)blockIdx.z * px_per_split;
+  const int64_t pend = min(M, pbeg + px_per_split);
+
+  const T* xs; int xcs, xcc;
+  if (ci0 < g.C1) { xs = x1; xcs = g.C1; xcc = ci0; } else { xs = x2; xcs = g.C2; xcc = ci0 - g.C1; }
+  const T* ys; int ycs, ycc;
+  const int Co2 = g.Cout - g.Co1;
+  if (co0 < g.Co1) { ys = dy1; ycs = g.Co1; ycc = co0; } else { ys = dy2; ycs = Co2; ycc = co0 - g.Co1; }
+
+  constexpr int VPR = ROW / VEC;             // 8 (bf16) / 16 (f32) vectors per row
+  constexpr int RPP = 256 / VPR;             // rows per pass: 32 / 16
+  constexpr int NP = WG_BP / RPP;            // passes: 1 / 2
+  const int vrow = tid / VPR, vcol = (tid % VPR) * VEC;
+
+  float xr[NP][VEC], yr[NP][VEC];
+  auto gload = [&](int64_t p0) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int64_t m = p0 + vrow + p * RPP;
+      bool ok = m < pend;
+      if (ok) {
+        if constexpr (VEC == 8) load8(ys + m * ycs + ycc + vcol, yr[p]); else load4(ys + m * ycs + ycc + vcol, yr[p]);
+        const int ox = (int)(m % g.Wo);
+        const int64_t t = m / g.Wo;
+        const int oy = (int)(t % g.Ho);
+        const int n = (int)(t / g.Ho);
+        int iy, ix;
+        if (tap_src(g, oy, ox, ky, kx, iy, ix)) {
+          const T* ptr = xs + ((((int64_t)n * g.Hi + iy) * g.Wi + ix) * xcs + xcc + vcol);
+          if constexpr (VEC == 8) load8(ptr, xr[p]); else load4(ptr, xr[p]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < VEC; ++i) xr[p][i] = 0.f;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) { xr[p][i] = 0.f; yr[p][i] = 0.f; }
+      }
+    }
+  };
+  auto swz = [](int r) { return (((r >> 1) & 1) << 2) | (((r >> 3) & 1) << 3); };  // in 4-element chunks
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int r = vrow + p * RPP;
+      if constexpr (sizeof(T) == 2) {
+        const int ch = (vcol >> 2) ^ swz(r);
+        store8(tY[buf] + r * LDR + ch * 4, yr[p]);
+        store8(tX[buf] + r * LDR + ch * 4, xr[p]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+          tY[buf][r * LDR + vcol + i] = yr[p][i];
+          tX[buf][r * LDR + vcol + i] = xr[p][i];
+        }
+      }
+    }
+  };
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nsteps = (int)((pend - pbeg + WG_BP - 1) / WG_BP);
+  if (nsteps > 0) {
+    gload(pbeg);
+    sstore(0);
+  }
+  __syncthreads();
+  const int lr = lane & 15, lg = lane >> 4;
+  for (int s = 0; s < nsteps; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nsteps) gload(pbeg + (int64_t)(s + 1) * WG_BP);
+    if constexpr (sizeof(T) == 2) {
+      // fragment (rows 0..15 of a 16-wide column block c0): lane group lg needs pixel rows
+      // 8lg..8lg+7; tr read: lane 4q+p addresses row (8lg + q [+4]), columns c0 + 4p.
+      const int q = lr >> 2, pp = lr & 3;
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int c0 = wr * 32 + i * 16;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const int r = lg * 8 + half * 4 + q;
+          const int ch = ((c0 >> 2) + pp) ^ swz(r);
+          s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tY[buf] + r * LDR + ch * 4));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) af[i][half * 4 + e] = __builtin_bit_cast(bf16, (short)v[e]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c0 = wc * 32 + j * 16;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const int r = lg * 8 + half * 4 + q;
+          const int ch = ((c0 >> 2) + pp) ^ swz(r);
+          s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tX[buf] + r * LDR + ch * 4));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bfr[j][half * 4 + e] = __builtin_bit_cast(bf16, (short)v[e]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    } else {
+      // fp32 16x16x4: lane holds A[row lr][k = lg] and B[k = lg][col lr]; 8 k-steps of 4 pixels
+#pragma unroll
+      for (int kk = 0; kk < WG_BP / 4; ++kk) {
+        const int r = kk * 4 + lg;
+        float a0 = tY[buf][r * LDR + wr * 32 + lr];
+        float a1 = tY[buf][r * LDR + wr * 32 + 16 + lr];
+        float b0 = tX[buf][r * LDR + wc * 32 + lr];
+        float b1 = tX[buf][r * LDR + wc * 32 + 16 + lr];
+        acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
+      }
+    }
+    if (s + 1 < nsteps) sstore(buf ^ 1);
+    __syncthreads();
+  }
+  // D[row = co][col = kcol]: lane holds col lr, rows 4lg + r
+  const int K = g.KH * g.KW * Cin;
+  float* out = slab + (int64_t)blockIdx.z * g.Cout * K;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int kc = kcol0 + wc * 32 + j * 16 + lr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wr * 32 + i * 16 + lg * 4 + r;
+        out[(int64_t)co * K + kc] = acc[i][j][r];
+      }
+    }
+}
+
+// sum slabs over splits (fixed order) and scatter into the PyTorch weight layout
+// dst[((d0*D1 + d1)*KH + kyt)*KW + kxt], with (d0,d1) = swap ? (ci,co) : (co,ci) and
+// (kyt,kxt) = flip ? (KH-1-ky, KW-1-kx) : (ky,kx).
+__global__ void conv_wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ dst, int nsplit,
+                                         int Cout, int Cin, int KH, int KW, int swap, int flip, int accumulate) {
+  const int64_t K = (int64_t)KH * KW * Cin;
+  const int64_t total = (int64_t)Cout * K;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < nsplit; ++k) s += slab[(int64_t)k * total + e];
+    const int co = (int)(e / K);
+    const int kc = (int)(e - (int64_t)co * K);
+    const int tap = kc / Cin, ci = kc - tap * Cin;
+    int ky = tap / KW, kx = tap - ky * KW;
+    if (flip) { ky = KH - 1 - ky; kx = KW - 1 - kx; }
+    const int d0 = swap ? ci : co, d1 = swap ? co : ci, D1 = swap ? Cout : Cin;
+    const int64_t di = (((int64_t)d0 * D1 + d1) * KH + ky) * KW + kx;
+    dst[di] = accumulate ? dst[di] + s : s;
+  }
+}
+
+// pack a PyTorch conv weight into the GEMM layout Wp[co][tap][ci] (cast to T)
+template <typename T>
+__global__ void conv_pack_kernel(const float* __restrict__ src, T* __restrict__ dst, int Cout, int Cin, int KH,
+                                 int KW, int swap, int flip) {
+  const int64_t K = (int64_t)KH * KW * Cin;
+  const int64_t total = (int64_t)Cout * K;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int co = (int)(e / K);
+    const int kc = (int)(e - (int64_t)co * K);
+    const int tap = kc / Cin, ci = kc - tap * Cin;
+    int ky = tap / KW, kx = tap - ky * KW;
+    if (flip) { ky = KH - 1 - ky; kx = KW - 1 - kx; }
+    const int d0 = swap ? ci : co, d1 = swap ? co : ci, D1 = swap ? Cout : Cin;
+    dst[e] = from_f<T>(src[(((int64_t)d0 * D1 + d1) * KH + ky) * KW + kx]);
+  }
+}
+
+// per-channel column sum over rows of a channels-last matrix: partial[split][c]
+template <typename T>
+__global__ void colsum_partial_kernel(const T* __restrict__ x, float* __restrict__ part, int64_t rows, int C,
+                                      int64_t rows_per_split) {
+  // block: 256 threads = (256/ (C/4)) row-lanes x (C/4) channel-quads  (C <= 1024, C % 4 == 0)
+  const int cq = C / 4;
+  const int rl = 256 / cq;
+  const int tid = threadIdx.x;
+  const int q = tid % cq, rr = tid / cq;
+  __shared__ float red[256 * 4];
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  const int64_t r0 = blockIdx.x * rows_per_split;
+  const int64_t r1 = min(rows, r0 + rows_per_split);
+  if (rr < rl) {
+    for (int64_t r = r0 + rr; r < r1; r += rl) {
+      float v[4];
+      load4(x + r * C + q * 4, v);
+      s[0] += v[0]; s[1] += v[1]; s[2] += v[2]; s[3] += v[3];
+    }
+  }
+  for (int i = 0; i < 4; ++i) red[tid * 4 + i] = s[i];
+  __syncthreads();
+  if (tid < cq) {
+    float t[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < rl; ++k)
+      for (int i = 0; i < 4; ++i) t[i] += red[(k * cq + tid) * 4 + i];
+    for (int i = 0; i < 4; ++i) part[(int64_t)blockIdx.x * C + tid * 4 + i] = t[i];
+  }
+}
+
+__global__ void colsum_final_kernel(const float* __restrict__ part, float* __restrict__ dst, int nsplit, int C,
+                                    int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int k = 0; k < nsplit; ++k) s += part[(int64_t)k * C + c];
+  dst[c] = accumulate ? dst[c] + s : s;
+}
+
+// ----------------------------------------------------------------------------------------
+// stem: Conv3d(2 -> Co, (1,7,7), pad 3) on cat([x_t broadcast over F, cond]) (video_net.py:595-600,
+// :808-815).  Inputs are the boundary NCDHW fp32 tensors: xt [B][Fx][H][W] (Fx = 1 or F),
+// cond [B][Fc][H][W].  Direct VALU conv (0.3 % of the MACs): block = 16x16 output pixels of
+// one frame, 64 output channels (Co == 64 at the default base_ch; Co % 64 == 0 handled by grid.y).
+// ----------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void stem_fwd_kernel(const float* __restrict__ xt, const float* __restrict__ cond,
+                                                       const float* __restrict__ w, const float* __restrict__ bias,
+                                                       T* __restrict__ y, int B, int F, int Fx, int Fc, int H, int W,
+                                                       int Co, int KS) {
+  const int PAD = KS / 2;
+  const int TS = 16;
+  const int TW = TS + KS - 1;
+  __shared__ float tin[2][22 * 22];
+  __shared__ float tw[64 * 2 * 49];
+  const int n = blockIdx.z;  // b*F + f
+  const int b = n / F, f = n - b * F;
+  const int ty0 = (blockIdx.x / ((W + TS - 1) / TS)) * TS;
+  const int tx0 = (blockIdx.x % ((W + TS - 1) / TS)) * TS;
+  const int cog = blockIdx.y * 64;
+  const float* s0 = xt + ((int64_t)b * Fx + (Fx == 1 ? 0 : f)) * H * W;
+  const float* s1 = cond + ((int64_t)b * Fc + (Fc == 1 ? 0 : f)) * H * W;
+  for (int e = threadIdx.x; e < TW * TW; e += 256) {
+    const int yy = ty0 - PAD + e / TW, xx = tx0 - PAD + e % TW;
+    const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+    tin[0][e] = ok ? s0[(int64_t)yy * W + xx] : 0.f;
+    tin[1][e] = ok ? s1[(int64_t)yy * W + xx] : 0.f;
+  }
+  for (int e = threadIdx.x; e < 64 * 2 * KS * KS; e += 256) tw[e] = w[(int64_t)cog * 2 * KS * KS + e];
+  __syncthreads();
+  const int py = threadIdx.x / TS, px = threadIdx.x % TS;
+  const int oy = ty0 + py, ox = tx0 + px;
+  float acc[64];
+#pragma unroll
+  for (int c = 0; c < 64; ++c) acc[c] = bias[cog + c];
+  for (int ci = 0; ci < 2; ++ci)
+    for (int ky = 0; ky < KS; ++ky)
+      for (int kx = 0; kx < KS; ++kx) {
+        const float v = tin[ci][(py + ky) * TW + px + kx];
+        const int wo = (ci * KS + ky) * KS + kx;
+#pragma unroll
+        for (int c = 0; c < 64; ++c) acc[c] = fmaf(tw[c * 2 * KS * KS + wo], v, acc[c]);
+      }
+  if (oy < H && ox < W) {
+    T* dst = y + (((int64_t)n * H + oy) * W + ox) * Co + cog;
+#pragma unroll
+    for (int c = 0; c < 64; c += 4) store4(dst + c, acc + c);
+  }
+}
+
+// stem weight gradient partials: part[blk][co][ci*KS*KS + ky*KS + kx]
+template <typename T>
+__global__ __launch_bounds__(256) void stem_wgrad_kernel(const float* __restrict__ xt, const float* __restrict__ cond,
+                                                         const T* __restrict__ dy, float* __restrict__ part, int B,
+                                                         int F, int Fx, int Fc, int H, int W, int Co, int KS,
+                                                         int ntiles) {
+  const int PAD = KS / 2;
+  const int TH = 8, TWD = 32;
+  const int IH = TH + KS - 1, IW = TWD + KS - 1;  // 14 x 38
+  __shared__ float tin[2][14 * 38];
+  __shared__ float tdy[TH * TWD * 65];
+  const int KK = 2 * KS * KS;  // 98
+  // thread -> (co, tap-group): 64 co x 4 groups
+  const int co = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int tpg = (KK + 3) / 4;
+  float acc[25];
+  for (int i = 0; i < 25; ++i) acc[i] = 0.f;
+  const int tx_tiles = (W + TWD - 1) / TWD, ty_tiles = (H + TH - 1) / TH;
+  const int per_img = tx_tiles * ty_tiles;
+  const int cog = blockIdx.y * 64;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int n = tile / per_img;
+    const int rem = tile - n * per_img;
+    const int ty0 = (rem / tx_tiles) * TH, tx0 = (rem % tx_tiles) * TWD;
+    const int b = n / F, f = n - b * F;
+    const float* s0 = xt + ((int64_t)b * Fx + (Fx == 1 ? 0 : f)) * H * W;
+    const float* s1 = cond + ((int64_t)b * Fc + (Fc == 1 ? 0 : f)) * H * W;
+    __syncthreads();
+    for (int e = threadIdx.x; e < IH * IW; e += 256) {
+      const int yy = ty0 - PAD + e / IW, xx = tx0 - PAD + e % IW;
+      const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+      tin[0][e] = ok ? s0[(int64_t)yy * W + xx] : 0.f;
+      tin[1][e] = ok ? s1[(int64_t)yy * W + xx] : 0.f;
+    }
+    for (int e = threadIdx.x; e < TH * TWD * 64; e += 256) {
+      const int p = e >> 6, c = e & 63;
+      const int yy = ty0 + p / TWD, xx = tx0 + p % TWD;
+      tdy[p * 65 + c] = (yy < H && xx < W) ? to_f(dy[(((int64_t)n * H + yy) * W + xx) * Co + cog + c]) : 0.f;
+    }
+    __syncthreads();
+    for (int p = 0; p < TH * TWD; ++p) {
+      const float g = tdy[p * 65 + co];
+      const int py = p / TWD, px = p % TWD;
+#pragma unroll
+      for (int i = 0; i < 25; ++i) {
+        const int kk = grp * tpg + i;
+        if (i < tpg && kk < KK) {
+          const int ci = kk / (KS * KS), r = kk - ci * KS * KS;
+          const int ky = r / KS, kx = r - ky * KS;
+          acc[i] = fmaf(g, tin[ci][(py + ky) * IW + px + kx], acc[i]);
+        }
+      }
+    }
+  }
+  for (int i = 0; i < tpg; ++i) {
+    const int kk = grp * tpg + i;
+    if (kk < KK) part[((int64_t)blockIdx.x * Co + cog + co) * KK + kk] = acc[i];
+  }
+}
+
+__global__ void sum_partials_kernel(const float* __restrict__ part, float* __restrict__ dst, int nsplit, int64_t n,
+                                    int accumulate) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < nsplit; ++k) s += part[(int64_t)k * n + e];
+    dst[e] = accumulate ? dst[e] + s : s;
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// head: Conv3d(C -> 1, 1) evaluated only on frame F//2 (the frame model.py:124-130 keeps).
+// out[b][y][x] (fp32 [B,1,H,W]) = bias + sum_c w[c] * x[(b*F+mid)][y][x][c]
+// ----------------------------------------------------------------------------------------
+template <typename T>
+__global__ void head_fwd_kernel(const T* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+                                float* __restrict__ out, int B, int F, int HW, int C) {
+  // one 64-lane wave per 8 pixels: 8 lanes per pixel, each lane 8 channels (C <= 64*... looped)
+  const int64_t gw = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 3;
+  const int sub = threadIdx.x & 7;
+  const int64_t total = (int64_t)B * HW;
+  if (gw >= total) return;
+  const int b = (int)(gw / HW);
+  const int64_t p = gw - (int64_t)b * HW;
+  const T* src = x + (((int64_t)b * F + F / 2) * HW + p) * C;
+  float s = 0.f;
+  for (int c = sub * 8; c < C; c += 64) {
+    float v[8];
+    load8(src + c, v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s = fmaf(v[i], w[c + i], s);
+  }
+  s = group_sum(s, 8);
+  if (sub == 0) out[gw] = s + bias[0];
+}
+
+// dX = 0 everywhere except frame mid where dX[c] = dout * w[c]
+template <typename T>
+__global__ void head_dgrad_kernel(const float* __restrict__ dout, const float* __restrict__ w, T* __restrict__ dx,
+                                  int B, int F, int HW, int C) {
+  const int64_t total = (int64_t)B * F * HW * (C / 8);
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int cq = (int)(e % (C / 8));
+    const int64_t vox = e / (C / 8);
+    const int64_t p = vox % HW;
+    const int64_t nf = vox / HW;
+    const int f = (int)(nf % F), b = (int)(nf / F);
+    float v[8];
+    const float g = (f == F / 2) ? dout[(int64_t)b * HW + p] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = g * w[cq * 8 + i];
+    store8(dx + vox * C + cq * 8, v);
+  }
+}
+
+// head weight/bias grads: part[blk][c] (c < C) and part[blk][C] = bias
+template <typename T>
+__global__ void head_wgrad_kernel(const float* __restrict__ dout, const T* __restrict__ x, float* __restrict__ part,
+                                  int B, int F, int HW, int C, int64_t px_per_blk) {
+  __shared__ float red[256];
+  const int64_t total = (int64_t)B * HW;
+  const int64_t p0 = blockIdx.x * px_per_blk, p1 = min(total, p0 + px_per_blk);
+  for (int c = 0; c <= C; ++c) {
+    float s = 0.f;
+    for (int64_t q = p0 + threadIdx.x; q < p1; q += blockDim.x) {
+      const int b = (int)(q / HW);
+      const int64_t p = q - (int64_t)b * HW;
+      const float g = dout[q];
+      s += (c == C) ? g : g * to_f(x[(((int64_t)b * F + F / 2) * HW + p) * C + c]);
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) part[(int64_t)blockIdx.x * (C + 1) + c] = red[0];
+    __syncthreads();
+  }
+}
+
+__global__ void head_reduce_kernel(const float* __restrict__ part, float* __restrict__ dw, float* __restrict__ db,
+                                   int nblk, int C, int accumulate) {
+  for (int c = threadIdx.x; c <= C; c += blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < nblk; ++k) s += part[(int64_t)k * (C + 1) + c];
+    float* d = (c == C) ? db : dw + c;
+    *d = accumulate ? *d + s : s;
+  }
+}
+
+}  // namespace
+
+// ========================================================================================
+// C ABI
+// ========================================================================================
+extern "C" {
+
+// Generic implicit-GEMM conv / dgrad.  Shapes: x1 [Nb][Hi][Wi][C1], x2 [Nb][Hi][Wi][C2] (may be
+// null if C2 == 0), wp [Cout][KH*KW][C1+C2] packed, y1 [Nb][Ho][Wo][Co1], y2 [..][Cout-Co1].
+int cesm_conv_fwd(int dtype, const void* x1, const void* x2, const void* wp, const float* bias, const void* res,
+                  const void* res2, void* y1, void* y2, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout, int Co1,
+                  int KH, int KW, int S, int P, int U, hipStream_t stream) {
+  if (Nb <= 0 || Ho <= 0 || Wo <= 0) return CESM_OK;
+  if ((C1 % BK) || (C2 % BK) || (Cout % 64) || (Co1 % 16) || Co1 > Cout || C1 <= 0) return CESM_EINVAL;
+  ConvGeom g{Nb, Hi, Wi, Ho, Wo, C1, C2, Cout, Co1, KH, KW, S, P, U};
+  const int64_t M = (int64_t)Nb * Ho * Wo;
+  const int BN = (Cout % 128 == 0) ? 128 : 64;
+  dim3 grid((unsigned)cdiv(M, BMP), Cout / BN);
+  if (dtype == CESM_DT_BF16) {
+    if (BN == 128)
+      conv_fwd_kernel<bf16, 128><<<grid, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
+                                                           (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, M);
+    else
+      conv_fwd_kernel<bf16, 64><<<grid, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
+                                                          (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, M);
+  } else if (dtype == CESM_DT_F32) {
+    if (BN == 128)
+      conv_fwd_kernel<float, 128><<<grid, 256, 0, stream>>>((const float*)x1, (const float*)x2, (const float*)wp,
+                                                            bias, (const float*)res, (const float*)res2, (float*)y1, (float*)y2, g, M);
+    else
+      conv_fwd_kernel<float, 64><<<grid, 256, 0, stream>>>((const float*)x1, (const float*)x2, (const float*)wp,
+                                                           bias, (const float*)res, (const float*)res2, (float*)y1, (float*)y2, g, M);
+  } else {
+    return CESM_EINVAL;
+  }
+  return cesm_launch_status();
+}
+
+// Weight gradient of the conv whose forward launch had geometry (…, KH, KW, S, P, U).
+// x = forward input (two sources), dy = forward output grad (two destinations, Co1 split).
+// Result accumulated/written into the PyTorch weight tensor `dw` ([D0][D1][1][KH][KW] with the
+// (swap, flip) mapping of the pack).  `slab` is an fp32 workspace of nsplit*Cout*K floats.
+int cesm_conv_wgrad(int dtype, const void* x1, const void* x2, const void* dy1, const void* dy2, float* dw,
+                    float* slab, int nsplit, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout,
+                    int Co1, int KH, int KW, int S, int P, int U, int swap, int flip, int accumulate,
+                    hipStream_t stream) {
+  const int Cin = C1 + C2;
+  if ((Cin % 64) || (C1 % 64) || (Cout % 64) || (Co1 % 64) || nsplit <= 0) return CESM_EINVAL;
+  ConvGeom g{Nb, Hi, Wi, Ho, Wo, C1, C2, Cout, Co1, KH, KW, S, P, U};
+  const int64_t M = (int64_t)Nb * Ho * Wo;
+  const int64_t pps = cdiv(cdiv(M, nsplit), WG_BP) * WG_BP;
+  const int K = KH * KW * Cin;
+  dim3 grid(Cout / 64, K / 64, nsplit);
+  if (dtype == CESM_DT_BF16)
+    conv_wgrad_kernel<bf16><<<grid, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
+                                                      (const bf16*)dy2, slab, g, M, pps);
+  else if (dtype == CESM_DT_F32)
+    conv_wgrad_kernel<float><<<grid, 256, 0, stream>>>((const float*)x1, (const float*)x2, (const float*)dy1,
+                                                       (const float*)dy2, slab, g, M, pps);
+  else
+    return CESM_EINVAL;
+  const int64_t total = (int64_t)Cout * K;
+  conv_wgrad_reduce_kernel<<<(unsigned)std::min<int64_t>(cdiv(total, 256), 2048), 256, 0, stream>>>(
+      slab, dw, nsplit, Cout, Cin, KH, KW, swap, flip, accumulate);
+  return cesm_launch_status();
+}
+
+int cesm_conv_pack(int dtype, const float* w, void* wp, int Cout, int Cin, int KH, int KW, int swap, int flip,
+                   hipStream_t stream) {
+  const int64_t total = (int64_t)Cout * KH * KW * Cin;
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(total, 256), 4096);
+  if (dtype == CESM_DT_BF16)
+    conv_pack_kernel<bf16><<<grid, 256, 0, stream>>>(w, (bf16*)wp, Cout, Cin, KH, KW, swap, flip);
+  else if (dtype == CESM_DT_F32)
+    conv_pack_kernel<float><<<grid, 256, 0, stream>>>(w, (float*)wp, Cout, Cin, KH, KW, swap, flip);
+  else
+    return CESM_EINVAL;
+  return cesm_launch_status();
+}
+
+// dst[c] (+)= sum_r x[r][c] ; part = workspace nsplit*C floats
+int cesm_colsum(int dtype, const void* x, float* dst, float* part, int nsplit, int64_t rows, int C, int accumulate,
+                hipStream_t stream) {
+  if (C % 4 || C > 1024 || nsplit <= 0) return CESM_EINVAL;
+  const int64_t rps = cdiv(rows, nsplit);
+  if (dtype == CESM_DT_BF16)
+    colsum_partial_kernel<bf16><<<nsplit, 256, 0, stream>>>((const bf16*)x, part, rows, C, rps);
+  else if (dtype == CESM_DT_F32)
+    colsum_partial_kernel<float><<<nsplit, 256, 0, stream>>>((const float*)x, part, rows, C, rps);
+  else
+    return CESM_EINVAL;
+  colsum_final_kernel<<<(unsigned)cdiv(C, 256), 256, 0, stream>>>(part, dst, nsplit, C, accumulate);
+  return cesm_launch_status();
+}
+
+int cesm_stem_fwd(int dtype, const float* xt, const float* cond, const float* w, const float* bias, void* y, int B,
+                  int F, int Fx, int Fc, int H, int W, int Co, int KS, hipStream_t stream) {
+  if (KS > 7 || Co % 64) return CESM_EINVAL;
+  dim3 grid((unsigned)(cdiv(H, 16) * cdiv(W, 16)), Co / 64, B * F);
+  if (dtype == CESM_DT_BF16)
+    stem_fwd_kernel<bf16><<<grid, 256, 0, stream>>>(xt, cond, w, bias, (bf16*)y, B, F, Fx, Fc, H, W, Co, KS);
+  else if (dtype == CESM_DT_F32)
+    stem_fwd_kernel<float><<<grid, 256, 0, stream>>>(xt, cond, w, bias, (float*)y, B, F, Fx, Fc, H, W, Co, KS);
+  else
+    return CESM_EINVAL;
+  return cesm_launch_status();
+}
+
+// stem dW (+ bias via cesm_colsum on dy); part: nblk*Co*2*KS*KS floats
+int cesm_stem_wgrad(int dtype, const float* xt, const float* cond, const void* dy, float* dw, float* part, int nblk,
+                    int B, int F, int Fx, int Fc, int H, int W, int Co, int KS, int accumulate, hipStream_t stream) {
+  if (KS > 7 || Co % 64 || nblk <= 0) return CESM_EINVAL;
+  const int ntiles = B * F * (int)cdiv(H, 8) * (int)cdiv(W, 32);
+  dim3 grid(nblk, Co / 64);
+  if (dtype == CESM_DT_BF16)
+    stem_wgrad_kernel<bf16><<<grid, 256, 0, stream>>>(xt, cond, (const bf16*)dy, part, B, F, Fx, Fc, H, W, Co, KS,
+                                                      ntiles);
+  else if (dtype == CESM_DT_F32)
+    stem_wgrad_kernel<float><<<grid, 256, 0, stream>>>(xt, cond, (const float*)dy, part, B, F, Fx, Fc, H, W, Co, KS,
+                                                       ntiles);
+  else
+    return CESM_EINVAL;
+  const int64_t n = (int64_t)Co * 2 * KS * KS;
+  sum_partials_kernel<<<(unsigned)cdiv(n, 256), 256, 0, stream>>>(part, dw, nblk, n, accumulate);
+  return cesm_launch_status();
+}
+
+int cesm_head_fwd(int dtype, const void* x, const float* w, const float* bias, float* out, int B, int F, int HW, int C,
+                  hipStream_t stream) {
+  if (C % 8) return CESM_EINVAL;
+  const int64_t threads = (int64_t)B * HW * 8;
+  const unsigned grid = (unsigned)cdiv(threads, 256);
+  if (dtype == CESM_DT_BF16)
+    head_fwd_kernel<bf16><<<grid, 256, 0, stream>>>((const bf16*)x, w, bias, out, B, F, HW, C);
+  else if (dtype == CESM_DT_F32)
+    head_fwd_kernel<float><<<grid, 256, 0, stream>>>((const float*)x, w, bias, out, B, F, HW, C);
+  else
+    return CESM_EINVAL;
+  return cesm_launch_status();
+}
+
+// head backward: dx (full [B*F][HW][C]), dw[C], db[1] (via part: nblk*(C+1) floats)
+int cesm_head_bwd(int dtype, const float* dout, const void* x, const float* w, void* dx, float* dw, float* db,
+                  float* part, int nblk, int B, int F, int HW, int C, int accumulate, hipStream_t stream) {
+  if (C % 8 || nblk <= 0) return CESM_EINVAL;
+  const int64_t total = (int64_t)B * F * HW * (C / 8);
+  const unsigned g1 = (unsigned)std::min<int64_t>(cdiv(total, 256), 8192);
+  const int64_t ppb = cdiv((int64_t)B * HW, nblk);
+  if (dtype == CESM_DT_BF16) {
+    if (dx) head_dgrad_kernel<bf16><<<g1, 256, 0, stream>>>(dout, w, (bf16*)dx, B, F, HW, C);
+    if (dw) head_wgrad_kernel<bf16><<<nblk, 256, 0, stream>>>(dout, (const bf16*)x, part, B, F, HW, C, ppb);
+  } else if (dtype == CESM_DT_F32) {
+    if (dx) head_dgrad_kernel<float><<<g1, 256, 0, stream>>>(dout, w, (float*)dx, B, F, HW, C);
+    if (dw) head_wgrad_kernel<float><<<nblk, 256, 0, stream>>>(dout, (const float*)x, part, B, F, HW, C, ppb);
+  } else {
+    return CESM_EINVAL;
+  }
+  if (dw) head_reduce_kernel<<<1, 256, 0, stream>>>(part, dw, db, nblk, C, accumulate);
+  return cesm_launch_status();
+}
+
+}  // extern "C"

@@ -1,0 +1,325 @@
+// Small ops of the training step:
+//  * time embedding + small linears (video_net.py:101-113 SinusoidalPosEmb, :651-656 time_mlp,
+//    :238-242 ResnetBlock.mlp = SiLU -> Linear) — M = batch rows, fp32
+//  * diffusion q_sample + MSE loss and its gradient (model.py:196-208)
+//  * global grad-norm clip (torch/nn/utils/clip_grad.py:165-180) + fused AdamW
+//    (torch/optim/adam.py:417-547, decoupled weight decay) over one flat fp32 parameter buffer
+//  * dtype casts and the training-window gather (dataset_single_member.py:168-196)
+#include "common.h"
+
+namespace {
+
+__global__ void sinusoidal_kernel(const int64_t* __restrict__ t, float* __restrict__ emb, int B, int dim) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int half = dim / 2;
+  if (i >= B * half) return;
+  const int b = i / half, k = i % half;
+  const float step = logf(10000.f) / (float)(half - 1);
+  const float fr = expf((float)k * -step);
+  const float a = (float)t[b] * fr;
+  emb[b * dim + k] = sinf(a);
+  emb[b * dim + half + k] = cosf(a);
+}
+
+// y[r][o] = bias[o] + sum_i act(x[r][i]) * W[o][i]; act = silu if silu_in
+__global__ void linear_small_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                        const float* __restrict__ bias, float* __restrict__ y, int R, int I, int O,
+                                        int silu_in) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= R * O) return;
+  const int r = t / O, o = t % O;
+  float s = bias ? bias[o] : 0.f;
+  const float* xr = x + (int64_t)r * I;
+  const float* wr = w + (int64_t)o * I;
+  for (int i = 0; i < I; ++i) {
+    const float xv = silu_in ? silu_p(xr[i]) : xr[i];
+    s = fmaf(xv, wr[i], s);
+  }
+  y[t] = s;
+}
+
+// dx[r][i] (+)= act'(x) * sum_o dy[r][o] W[o][i]
+__global__ void linear_small_dx_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                       const float* __restrict__ dy, float* __restrict__ dx, int R, int I, int O,
+                                       int silu_in, int accumulate) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= R * I) return;
+  const int r = t / I, i = t % I;
+  float s = 0.f;
+  for (int o = 0; o < O; ++o) s = fmaf(dy[(int64_t)r * O + o], w[(int64_t)o * I + i], s);
+  if (silu_in) s *= dsilu_p(x[t]);
+  dx[t] = accumulate ? dx[t] + s : s;
+}
+
+// dW[o][i] (+)= sum_r dy[r][o] act(x[r][i]); db[o] (+)= sum_r dy[r][o]
+__global__ void linear_small_dw_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                                       float* __restrict__ dw, float* __restrict__ db, int R, int I, int O,
+                                       int silu_in, int accumulate) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < O * I) {
+    const int o = t / I, i = t % I;
+    float s = 0.f;
+    for (int r = 0; r < R; ++r) {
+      const float xv = silu_in ? silu_p(x[(int64_t)r * I + i]) : x[(int64_t)r * I + i];
+      s = fmaf(dy[(int64_t)r * O + o], xv, s);
+    }
+    dw[t] = accumulate ? dw[t] + s : s;
+  }
+  if (db && t < O) {
+    float s = 0.f;
+    for (int r = 0; r < R; ++r) s += dy[(int64_t)r * O + t];
+    db[t] = accumulate ? db[t] + s : s;
+  }
+}
+
+// x_t = a[t_b] x0 + s[t_b] noise   (x0, noise, x_t: [B][HW] fp32)
+__global__ void q_sample_kernel(const float* __restrict__ x0, const float* __restrict__ noise,
+                                const int64_t* __restrict__ t, const float* __restrict__ sa,
+                                const float* __restrict__ s1a, float* __restrict__ xt, int B, int64_t HW) {
+  const int64_t n = (int64_t)B * HW;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int b = (int)(e / HW);
+    const int64_t ti = t[b];
+    xt[e] = sa[ti] * x0[e] + s1a[ti] * noise[e];
+  }
+}
+
+// loss partials: part[blk] = sum (pred - noise)^2
+__global__ void mse_partial_kernel(const float* __restrict__ pred, const float* __restrict__ tgt,
+                                   float* __restrict__ part, int64_t n) {
+  __shared__ float red[256];
+  float s = 0.f;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const float d = pred[e] - tgt[e];
+    s = fmaf(d, d, s);
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ void mse_final_kernel(const float* __restrict__ part, float* __restrict__ loss, int nblk, int64_t n) {
+  if (threadIdx.x != 0) return;
+  double s = 0.0;
+  for (int k = 0; k < nblk; ++k) s += part[k];
+  loss[0] = (float)(s / (double)n);
+}
+
+// dpred = gscale[0] * 2 (pred - noise) / n
+__global__ void mse_bwd_kernel(const float* __restrict__ pred, const float* __restrict__ tgt,
+                               const float* __restrict__ gscale, float* __restrict__ dpred, int64_t n) {
+  const float c = 2.f * gscale[0] / (float)n;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x)
+    dpred[e] = c * (pred[e] - tgt[e]);
+}
+
+// ---- grad norm + clip + AdamW over flat fp32 buffers
+__global__ void sumsq_partial_kernel(const float* __restrict__ g, double* __restrict__ part, int64_t n) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const float v = g[e];
+    s += (double)v * v;
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+// info[0] = total norm, info[1] = clip coef (clamped to 1), info[2] = 1 if finite (norm & loss)
+__global__ void clip_coef_kernel(const double* __restrict__ part, int nblk, float max_norm,
+                                 const float* __restrict__ loss, float* __restrict__ info) {
+  if (threadIdx.x != 0) return;
+  double s = 0.0;
+  for (int k = 0; k < nblk; ++k) s += part[k];
+  const float norm = (float)sqrt(s);
+  info[0] = norm;
+  float coef = max_norm > 0.f ? max_norm / (norm + 1e-6f) : 1.f;
+  info[1] = coef < 1.f ? coef : 1.f;
+  const bool fin = isfinite(norm) && (loss == nullptr || isfinite(loss[0]));
+  info[2] = fin ? 1.f : 0.f;
+}
+
+__global__ void adamw_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
+                             float* __restrict__ v, const float* __restrict__ info, int64_t n, float lr, float b1,
+                             float b2, float eps, float wd, float bc1, float bc2_sqrt, int use_clip) {
+  if (info && info[2] == 0.f) return;  // non-finite loss/grad: no update (train step raises)
+  const float coef = (use_clip && info) ? info[1] : 1.f;
+  const float step_size = lr / bc1;
+  const float decay = 1.f - lr * wd;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const float gr = g[e] * coef;
+    if (use_clip) g[e] = gr;
+    const float pv = p[e] * decay;
+    const float mv = m[e] + (1.f - b1) * (gr - m[e]);
+    const float vv = v[e] * b2 + (1.f - b2) * gr * gr;
+    m[e] = mv;
+    v[e] = vv;
+    const float denom = sqrtf(vv) / bc2_sqrt + eps;
+    p[e] = pv - step_size * (mv / denom);
+  }
+}
+
+template <typename T>
+__global__ void add_kernel(const T* __restrict__ a, const T* __restrict__ b, T* __restrict__ out, int64_t n8) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n8; e += (int64_t)gridDim.x * blockDim.x) {
+    float x[8], y[8];
+    load8(a + e * 8, x);
+    load8(b + e * 8, y);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] += y[i];
+    store8(out + e * 8, x);
+  }
+}
+
+template <typename TI, typename TO>
+__global__ void cast_kernel(const TI* __restrict__ x, TO* __restrict__ y, int64_t n) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x)
+    y[e] = from_f<TO>(to_f(x[e]));
+}
+
+// Training-window gather (dataset_single_member.py:168-196) from arrays resident in device or
+// pinned host memory: cond/tgt [T][M][H][W] fp32.  Per item i: (t0, m, anchor, rev, ci, cj):
+// cond_win[i][0][k][y][x] = cond[times[k]][m][ci+y][cj+x], x0[i][0][y][x] = tgt[anchor][m][..]
+// times[k] = t0 + k, with the "reverse both halves around the centre" augmentation when rev.
+__global__ void window_gather_kernel(const float* __restrict__ cond, const float* __restrict__ tgt,
+                                     const int64_t* __restrict__ items, float* __restrict__ cwin,
+                                     float* __restrict__ x0, int nitems, int K, int M, int H, int W, int h, int w,
+                                     int center) {
+  const int64_t per = (int64_t)(K + 1) * h * w;
+  const int64_t total = per * nitems;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int it = (int)(e / per);
+    int64_t r = e - (int64_t)it * per;
+    const int k = (int)(r / ((int64_t)h * w));
+    r -= (int64_t)k * h * w;
+    const int y = (int)(r / w), x = (int)(r % w);
+    const int64_t* d = items + it * 6;
+    const int64_t t0 = d[0], m = d[1], anchor = d[2], rev = d[3], ci = d[4], cj = d[5];
+    if (k < K) {
+      int kk = k;
+      if (rev) {
+        if (center) {
+          const int mid = K / 2;
+          if (k < mid) kk = mid - 1 - k;
+          else if (k > mid) kk = K - 1 - (k - mid - 1);
+        } else {
+          kk = K - 1 - k;
+        }
+      }
+      const int64_t tt = t0 + kk;
+      cwin[(((int64_t)it * K + k) * h + y) * w + x] = cond[(((tt * M + m) * H) + ci + y) * W + cj + x];
+    } else {
+      x0[((int64_t)it * h + y) * w + x] = tgt[(((anchor * M + m) * H) + ci + y) * W + cj + x];
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int cesm_sinusoidal(const int64_t* t, float* emb, int B, int dim, hipStream_t stream) {
+  sinusoidal_kernel<<<(unsigned)cdiv(B * (dim / 2), 256), 256, 0, stream>>>(t, emb, B, dim);
+  return cesm_launch_status();
+}
+
+int cesm_linear_small_fwd(const float* x, const float* w, const float* bias, float* y, int R, int I, int O,
+                          int silu_in, hipStream_t stream) {
+  linear_small_fwd_kernel<<<(unsigned)cdiv(R * O, 256), 256, 0, stream>>>(x, w, bias, y, R, I, O, silu_in);
+  return cesm_launch_status();
+}
+
+int cesm_linear_small_bwd(const float* x, const float* w, const float* dy, float* dx, float* dw, float* db, int R,
+                          int I, int O, int silu_in, int accumulate_dx, int accumulate_w, hipStream_t stream) {
+  if (dx)
+    linear_small_dx_kernel<<<(unsigned)cdiv(R * I, 256), 256, 0, stream>>>(x, w, dy, dx, R, I, O, silu_in,
+                                                                           accumulate_dx);
+  if (dw)
+    linear_small_dw_kernel<<<(unsigned)cdiv((int64_t)O * I, 256), 256, 0, stream>>>(x, dy, dw, db, R, I, O, silu_in,
+                                                                                    accumulate_w);
+  return cesm_launch_status();
+}
+
+int cesm_q_sample(const float* x0, const float* noise, const int64_t* t, const float* sa, const float* s1a,
+                  float* xt, int B, int64_t HW, hipStream_t stream) {
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv((int64_t)B * HW, 256), 4096);
+  q_sample_kernel<<<grid, 256, 0, stream>>>(x0, noise, t, sa, s1a, xt, B, HW);
+  return cesm_launch_status();
+}
+
+// loss[0] = mean((pred-tgt)^2); part: 512 floats
+int cesm_mse(const float* pred, const float* tgt, float* loss, float* part, int64_t n, hipStream_t stream) {
+  const int nblk = 512;
+  mse_partial_kernel<<<nblk, 256, 0, stream>>>(pred, tgt, part, n);
+  mse_final_kernel<<<1, 64, 0, stream>>>(part, loss, nblk, n);
+  return cesm_launch_status();
+}
+
+int cesm_mse_bwd(const float* pred, const float* tgt, const float* gscale, float* dpred, int64_t n,
+                 hipStream_t stream) {
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(n, 256), 4096);
+  mse_bwd_kernel<<<grid, 256, 0, stream>>>(pred, tgt, gscale, dpred, n);
+  return cesm_launch_status();
+}
+
+// info[3] (device): norm, clip coef, finite flag.  part: 1024 doubles.
+int cesm_grad_norm(const float* g, int64_t n, float max_norm, const float* loss, double* part, float* info,
+                   hipStream_t stream) {
+  const int nblk = 1024;
+  sumsq_partial_kernel<<<nblk, 256, 0, stream>>>(g, part, n);
+  clip_coef_kernel<<<1, 64, 0, stream>>>(part, nblk, max_norm, loss, info);
+  return cesm_launch_status();
+}
+
+int cesm_adamw(float* p, float* g, float* m, float* v, const float* info, int64_t n, float lr, float b1, float b2,
+               float eps, float wd, int step, int use_clip, hipStream_t stream) {
+  const float bc1 = 1.f - powf(b1, (float)step);
+  const float bc2 = 1.f - powf(b2, (float)step);
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(n, 256), 8192);
+  adamw_kernel<<<grid, 256, 0, stream>>>(p, g, m, v, info, n, lr, b1, b2, eps, wd, bc1, sqrtf(bc2), use_clip);
+  return cesm_launch_status();
+}
+
+int cesm_add(int dtype, const void* a, const void* b, void* out, int64_t n, hipStream_t stream) {
+  if (n % 8) return CESM_EINVAL;
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(n / 8, 256), 8192);
+  if (dtype == CESM_DT_BF16)
+    add_kernel<bf16><<<grid, 256, 0, stream>>>((const bf16*)a, (const bf16*)b, (bf16*)out, n / 8);
+  else if (dtype == CESM_DT_F32)
+    add_kernel<float><<<grid, 256, 0, stream>>>((const float*)a, (const float*)b, (float*)out, n / 8);
+  else
+    return CESM_EINVAL;
+  return cesm_launch_status();
+}
+
+int cesm_cast(int dtype_in, int dtype_out, const void* x, void* y, int64_t n, hipStream_t stream) {
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(n, 256), 8192);
+  if (dtype_in == CESM_DT_F32 && dtype_out == CESM_DT_BF16)
+    cast_kernel<float, bf16><<<grid, 256, 0, stream>>>((const float*)x, (bf16*)y, n);
+  else if (dtype_in == CESM_DT_BF16 && dtype_out == CESM_DT_F32)
+    cast_kernel<bf16, float><<<grid, 256, 0, stream>>>((const bf16*)x, (float*)y, n);
+  else if (dtype_in == CESM_DT_F32 && dtype_out == CESM_DT_F32)
+    cast_kernel<float, float><<<grid, 256, 0, stream>>>((const float*)x, (float*)y, n);
+  else
+    return CESM_EINVAL;
+  return cesm_launch_status();
+}
+
+int cesm_window_gather(const float* cond, const float* tgt, const int64_t* items, float* cwin, float* x0,
+                       int nitems, int K, int M, int H, int W, int h, int w, int center, hipStream_t stream) {
+  const int64_t total = (int64_t)(K + 1) * h * w * nitems;
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(total, 256), 8192);
+  window_gather_kernel<<<grid, 256, 0, stream>>>(cond, tgt, items, cwin, x0, nitems, K, M, H, W, h, w, center);
+  return cesm_launch_status();
+}
+
+}  // extern "C"

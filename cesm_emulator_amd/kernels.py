@@ -1,0 +1,324 @@
+"""Thin tensor-level wrappers over libcesm_hip.so (one C call each, no torch compute).
+
+Every wrapper takes torch tensors living on the current HIP device, allocates its outputs and
+workspaces through the PyTorch caching allocator (plumbing) and enqueues the kernel on
+torch's current stream.  Shapes are asserted on the host before launch so a bad call raises
+instead of faulting on the GPU.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._lib import call, lib
+
+F32, BF16 = 0, 1
+_DT = {torch.float32: F32, torch.bfloat16: BF16}
+
+
+def dtcode(t: torch.Tensor) -> int:
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise TypeError(f"unsupported dtype {t.dtype}") from None
+
+
+def S():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def P(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def _chk(t, shape=None, dtype=None):
+    if t is None:
+        return
+    if not t.is_cuda:
+        raise RuntimeError("cesm_emulator_amd kernels need device tensors (no CPU fallback)")
+    if not t.is_contiguous():
+        raise RuntimeError("expected a contiguous tensor")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise RuntimeError(f"shape mismatch: got {tuple(t.shape)}, expected {tuple(shape)}")
+    if dtype is not None and t.dtype != dtype:
+        raise RuntimeError(f"dtype mismatch: got {t.dtype}, expected {dtype}")
+
+
+def empty(shape, dtype, device):
+    return torch.empty(shape, dtype=dtype, device=device)
+
+
+# ------------------------------------------------------------------------------------ conv
+def conv_pack(w: torch.Tensor, dtype, cout, cin, kh, kw, swap, flip):
+    _chk(w, dtype=torch.float32)
+    out = empty((cout, kh * kw * cin), dtype, w.device)
+    call("cesm_conv_pack", _DT[dtype], P(w), P(out), cout, cin, kh, kw, int(swap), int(flip), S())
+    return out
+
+
+def conv_fwd(x1, x2, wp, bias, geom, res=None, res2=None, out_split=None):
+    """geom = (Ho, Wo, Cout, KH, KW, S, P, U).  Returns y (or (y1, y2) when out_split=Co1)."""
+    Ho, Wo, Cout, KH, KW, St, Pd, U = geom
+    Nb, Hi, Wi, C1 = x1.shape
+    C2 = 0 if x2 is None else x2.shape[3]
+    _chk(x1)
+    if x2 is not None:
+        _chk(x2, (Nb, Hi, Wi, C2), x1.dtype)
+    _chk(wp, (Cout, KH * KW * (C1 + C2)), x1.dtype)
+    if bias is not None:
+        _chk(bias, (Cout,), torch.float32)
+    Co1 = Cout if out_split is None else out_split
+    y1 = empty((Nb, Ho, Wo, Co1), x1.dtype, x1.device)
+    y2 = empty((Nb, Ho, Wo, Cout - Co1), x1.dtype, x1.device) if Co1 != Cout else None
+    _chk(res, (Nb, Ho, Wo, Co1), x1.dtype)
+    _chk(res2, (Nb, Ho, Wo, Cout - Co1), x1.dtype)
+    call("cesm_conv_fwd", dtcode(x1), P(x1), P(x2), P(wp), P(bias), P(res), P(res2), P(y1), P(y2), Nb, Hi, Wi, C1,
+         C2, Ho, Wo, Cout, Co1, KH, KW, St, Pd, U, S())
+    return y1 if y2 is None else (y1, y2)
+
+
+def _wgrad_nsplit(M, cout, K):
+    tiles = (cout // 64) * (K // 64)
+    n = max(1, 2048 // max(1, tiles))
+    n = min(n, max(1, M // 256))
+    return n
+
+
+def conv_wgrad(x1, x2, dy1, dy2, dw, geom, swap, flip, accumulate=True):
+    Ho, Wo, Cout, KH, KW, St, Pd, U = geom
+    Nb, Hi, Wi, C1 = x1.shape
+    C2 = 0 if x2 is None else x2.shape[3]
+    Co1 = dy1.shape[3]
+    _chk(dy1, (Nb, Ho, Wo, Co1), x1.dtype)
+    _chk(dy2, None if dy2 is None else (Nb, Ho, Wo, Cout - Co1), x1.dtype)
+    _chk(dw, dtype=torch.float32)
+    K = KH * KW * (C1 + C2)
+    M = Nb * Ho * Wo
+    nsplit = _wgrad_nsplit(M, Cout, K)
+    slab = empty((nsplit, Cout, K), torch.float32, x1.device)
+    call("cesm_conv_wgrad", dtcode(x1), P(x1), P(x2), P(dy1), P(dy2), P(dw), P(slab), nsplit, Nb, Hi, Wi, C1, C2,
+         Ho, Wo, Cout, Co1, KH, KW, St, Pd, U, int(swap), int(flip), int(accumulate), S())
+
+
+def colsum(x, dst, accumulate=True):
+    C = x.shape[-1]
+    rows = x.numel() // C
+    nsplit = int(max(1, min(1024, rows // 512)))
+    part = empty((nsplit, C), torch.float32, x.device)
+    call("cesm_colsum", dtcode(x), P(x), P(dst), P(part), nsplit, rows, C, int(accumulate), S())
+
+
+def stem_fwd(xt, cond, w, b, F, dtype):
+    B, Fx, H, W = xt.shape
+    Fc = cond.shape[1]
+    Co, _, _, KS, _ = w.shape
+    _chk(xt, dtype=torch.float32)
+    _chk(cond, (B, Fc, H, W), torch.float32)
+    y = empty((B * F, H, W, Co), dtype, xt.device)
+    call("cesm_stem_fwd", _DT[dtype], P(xt), P(cond), P(w), P(b), P(y), B, F, Fx, Fc, H, W, Co, KS, S())
+    return y
+
+
+def stem_wgrad(xt, cond, dy, dw, F, accumulate=True):
+    B, Fx, H, W = xt.shape
+    Fc = cond.shape[1]
+    Co = dy.shape[3]
+    KS = dw.shape[-1]
+    nblk = 512
+    part = empty((nblk, Co * 2 * KS * KS), torch.float32, xt.device)
+    call("cesm_stem_wgrad", dtcode(dy), P(xt), P(cond), P(dy), P(dw), P(part), nblk, B, F, Fx, Fc, H, W, Co, KS,
+         int(accumulate), S())
+
+
+def head_fwd(x, w, b, B, F):
+    Nb, H, W, C = x.shape
+    out = empty((B, 1, H, W), torch.float32, x.device)
+    call("cesm_head_fwd", dtcode(x), P(x), P(w), P(b), P(out), B, F, H * W, C, S())
+    return out
+
+
+def head_bwd(dout, x, w, dw, db, B, F, need_dx=True, accumulate=True):
+    Nb, H, W, C = x.shape
+    dx = empty(x.shape, x.dtype, x.device) if need_dx else None
+    nblk = 256
+    part = empty((nblk, C + 1), torch.float32, x.device)
+    call("cesm_head_bwd", dtcode(x), P(dout), P(x), P(w), P(dx), P(dw), P(db), P(part), nblk, B, F, H * W, C,
+         int(accumulate), S())
+    return dx
+
+
+# ------------------------------------------------------------------------------------ norms
+def gn_stats(y, B, G, eps=1e-5):
+    C = y.shape[-1]
+    rows_b = y.numel() // (C * B)
+    stats = empty((B, G, 2), torch.float32, y.device)
+    ws = empty((B * 256 * G * 2,), torch.float64, y.device)
+    call("cesm_gn_stats", dtcode(y), P(y), P(stats), P(ws), B, rows_b, C, G, float(eps), S())
+    return stats
+
+
+def gn_apply(y, stats, gamma, beta, ss, res, B, G):
+    C = y.shape[-1]
+    rows_b = y.numel() // (C * B)
+    out = empty(y.shape, y.dtype, y.device)
+    _chk(res, y.shape, y.dtype)
+    call("cesm_gn_apply", dtcode(y), P(y), P(stats), P(gamma), P(beta), P(ss), P(res), P(out), B, rows_b, C, G, S())
+    return out
+
+
+def gn_bwd(dout, y, stats, gamma, beta, ss, dgamma, dbeta, B, G, want_dss):
+    C = y.shape[-1]
+    rows_b = y.numel() // (C * B)
+    dy = empty(y.shape, y.dtype, y.device)
+    dss = empty((B, 2 * C), torch.float32, y.device) if want_dss else None
+    ws = empty((B * 256 * C * 2 + B * C * 2 + B * G * 2,), torch.float32, y.device)
+    call("cesm_gn_bwd", dtcode(y), P(dout), P(y), P(stats), P(gamma), P(beta), P(ss), P(dy), P(dss), P(dgamma),
+         P(dbeta), P(ws), B, rows_b, C, G, 1, S())
+    return dy, dss
+
+
+def ln_fwd(x, gamma, save=True, eps=1e-5):
+    C = x.shape[-1]
+    V = x.numel() // C
+    out = empty(x.shape, x.dtype, x.device)
+    mr = empty((V, 2), torch.float32, x.device) if save else None
+    call("cesm_ln_fwd", dtcode(x), P(x), P(gamma), P(out), P(mr), V, C, float(eps), S())
+    return out, mr
+
+
+def ln_bwd(dy, x, mr, gamma, dgamma, dres=None):
+    C = x.shape[-1]
+    V = x.numel() // C
+    dx = empty(x.shape, x.dtype, x.device)
+    nblk = 1024
+    part = empty((nblk, C), torch.float32, x.device)
+    _chk(dres, x.shape, x.dtype)
+    call("cesm_ln_bwd", dtcode(x), P(dy), P(x), P(mr), P(gamma), P(dres), P(dx), P(dgamma), P(part), nblk, V, C, 1,
+         S())
+    return dx
+
+
+def add(a, b):
+    out = empty(a.shape, a.dtype, a.device)
+    _chk(b, a.shape, a.dtype)
+    call("cesm_add", dtcode(a), P(a), P(b), P(out), a.numel(), S())
+    return out
+
+
+# ------------------------------------------------------------------------------------ attention
+def rope_table(freqs, F):
+    rot = empty((F, 16, 2), torch.float32, freqs.device)
+    call("cesm_rope_table", P(freqs), P(rot), F, S())
+    return rot
+
+
+def relpos_fwd(table, F, num_buckets=32, max_distance=32):
+    nb, heads = table.shape
+    bias = empty((heads, F, F), torch.float32, table.device)
+    call("cesm_relpos_fwd", P(table), P(bias), F, heads, num_buckets, max_distance, S())
+    return bias
+
+
+def tattn_fwd(qkv, bias, rot, B, F, HW, scale, save=True):
+    V = qkv.shape[0]
+    out = empty((V, 256), qkv.dtype, qkv.device)
+    lse = empty((B, 8, HW, F), torch.float32, qkv.device) if save else None
+    call("cesm_tattn_fwd", dtcode(qkv), P(qkv), P(bias), P(rot), P(out), P(lse), B, F, HW, float(scale), S())
+    return out, lse
+
+
+def tattn_bwd(qkv, o, dout, lse, bias, rot, dtable, B, F, HW, scale, num_buckets=32, max_distance=32):
+    dqkv = empty(qkv.shape, qkv.dtype, qkv.device)
+    nblk = lib().cesm_tattn_nblk(F, HW)
+    part = empty((B * 8 * nblk, F, F), torch.float32, qkv.device)
+    call("cesm_tattn_bwd", dtcode(qkv), P(qkv), P(o), P(dout), P(lse), P(bias), P(rot), P(dqkv), P(part), B, F, HW,
+         float(scale), S())
+    if dtable is not None:
+        call("cesm_relpos_bwd", P(part), nblk, B, P(dtable), F, 8, num_buckets, max_distance, 1, S())
+    return dqkv
+
+
+def sla_fwd(qkv, Nf, HW, scale):
+    nchunk = lib().cesm_sla_nchunk(HW)
+    out = empty((qkv.shape[0], 256), qkv.dtype, qkv.device)
+    ctx = empty((Nf, 8, 32, 32), torch.float32, qkv.device)
+    ml = empty((Nf, 8, 32, 2), torch.float32, qkv.device)
+    ws = empty((Nf * 8 * nchunk * (32 + 32 + 1024),), torch.float32, qkv.device)
+    call("cesm_sla_fwd", dtcode(qkv), P(qkv), P(out), P(ctx), P(ml), P(ws), Nf, HW, float(scale), S())
+    return out, ctx, ml
+
+
+def sla_bwd(qkv, dout, ctx, ml, Nf, HW, scale):
+    nchunk = lib().cesm_sla_nchunk(HW)
+    dqkv = empty(qkv.shape, qkv.dtype, qkv.device)
+    ws = empty((Nf * 8 * nchunk * 1024 + Nf * 8 * (1024 + 32),), torch.float32, qkv.device)
+    call("cesm_sla_bwd", dtcode(qkv), P(qkv), P(dout), P(ctx), P(ml), P(dqkv), P(ws), Nf, HW, float(scale), S())
+    return dqkv
+
+
+# ------------------------------------------------------------------------------------ misc
+def sinusoidal(t, dim):
+    emb = empty((t.shape[0], dim), torch.float32, t.device)
+    call("cesm_sinusoidal", P(t), P(emb), t.shape[0], dim, S())
+    return emb
+
+
+def linear_small(x, w, b, silu_in):
+    R, I = x.shape
+    O = w.shape[0]
+    y = empty((R, O), torch.float32, x.device)
+    call("cesm_linear_small_fwd", P(x), P(w), P(b), P(y), R, I, O, int(silu_in), S())
+    return y
+
+
+def linear_small_bwd(x, w, dy, dx, dw, db, silu_in, accumulate_dx):
+    R, I = x.shape
+    O = w.shape[0]
+    call("cesm_linear_small_bwd", P(x), P(w), P(dy), P(dx), P(dw), P(db), R, I, O, int(silu_in), int(accumulate_dx),
+         1, S())
+
+
+def q_sample(x0, noise, t, sa, s1a):
+    B = x0.shape[0]
+    xt = empty(x0.shape, torch.float32, x0.device)
+    call("cesm_q_sample", P(x0), P(noise), P(t), P(sa), P(s1a), P(xt), B, x0.numel() // B, S())
+    return xt
+
+
+def mse(pred, tgt):
+    loss = empty((), torch.float32, pred.device)
+    part = empty((512,), torch.float32, pred.device)
+    call("cesm_mse", P(pred), P(tgt), P(loss), P(part), pred.numel(), S())
+    return loss
+
+
+def mse_bwd(pred, tgt, gscale):
+    d = empty(pred.shape, torch.float32, pred.device)
+    call("cesm_mse_bwd", P(pred), P(tgt), P(gscale), P(d), pred.numel(), S())
+    return d
+
+
+def grad_norm(flat_grad, max_norm, loss=None):
+    info = empty((4,), torch.float32, flat_grad.device)
+    part = empty((1024,), torch.float64, flat_grad.device)
+    call("cesm_grad_norm", P(flat_grad), flat_grad.numel(), float(max_norm), P(loss), P(part), P(info), S())
+    return info
+
+
+def adamw(p, g, m, v, info, lr, b1, b2, eps, wd, step, use_clip):
+    call("cesm_adamw", P(p), P(g), P(m), P(v), P(info), p.numel(), float(lr), float(b1), float(b2), float(eps),
+         float(wd), int(step), int(use_clip), S())
+
+
+def cast(x, dtype):
+    y = empty(x.shape, dtype, x.device)
+    call("cesm_cast", dtcode(x), _DT[dtype], P(x), P(y), x.numel(), S())
+    return y
+
+
+def window_gather(cond, tgt, items, K, h, w, center):
+    T, M, H, W = cond.shape
+    n = items.shape[0]
+    cwin = empty((n, 1, K, h, w), torch.float32, items.device)
+    x0 = empty((n, 1, h, w), torch.float32, items.device)
+    call("cesm_window_gather", P(cond), P(tgt), P(items), P(cwin), P(x0), n, K, M, H, W, h, w, int(center), S())
+    return cwin, x0

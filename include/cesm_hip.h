@@ -1,0 +1,136 @@
+/*
+ * cesm_hip.h — C ABI of libcesm_hip.so, the gfx950 (MI355X) kernels behind the
+ * cesm_emulator_amd drop-in for the reference's video_net training/inference hot path.
+ *
+ * The reference (kallenordling/cesm_emulator @ 2025-09-05) is pure Python: every entry point
+ * below replaces one or more PyTorch-dispatched ATen/NCCL ops at the cited reference lines
+ * (SURVEY.md §2.2).  Conventions:
+ *   - all pointers are device pointers (hipMalloc / PyTorch caching allocator); kernels never
+ *     allocate or free — workspaces are passed in by the caller;
+ *   - activations are channels-last [N][H][W][C] with N = batch*frames, dtype = CESM_DT_F32
+ *     (parity mode) or CESM_DT_BF16 (perf mode); parameters, statistics and grads are fp32;
+ *   - every call is stream-ordered on `stream` and enqueue-only (no host sync, graph-capturable);
+ *   - return 0 on success, negative CESM_E* on bad arguments or launch failure; the Python
+ *     layer raises RuntimeError (mirroring model.py:99-132 / train.py:842-843 errors);
+ *   - `accumulate` = 1 adds into the destination gradient (grad accumulation), 0 overwrites.
+ */
+#ifndef CESM_HIP_H
+#define CESM_HIP_H
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CESM_DT_F32 0
+#define CESM_DT_BF16 1
+
+/* ---- convolutions (csrc/conv.hip) -------------------------------------------------------
+ * Generic implicit-GEMM conv on MFMA. Replaces nn.Conv3d (1,k,k) at video_net.py:215 (Block.proj),
+ * :246 (res_conv), :61-62 (Downsample), nn.ConvTranspose3d at :65-66 (Upsample), the attention
+ * projections nn.Linear :380-381 and 1x1 nn.Conv2d :322-323, and all their data gradients.
+ *   out[n,oy,ox,co] = bias[co] + res[..] + sum W[co][ky*KW+kx][ci] * X[n,(oy*S-P+ky)/U,(ox*S-P+kx)/U,ci]
+ * Input may be the channel-concat of x1 (C1 ch) and x2 (C2 ch) (video_net.py:857, :868 torch.cat);
+ * output channels [0,Co1) go to y1 and [Co1,Cout) to y2. */
+int cesm_conv_fwd(int dtype, const void* x1, const void* x2, const void* wp, const float* bias, const void* res,
+                  const void* res2, void* y1, void* y2, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout, int Co1,
+                  int KH, int KW, int S, int P, int U, hipStream_t stream);
+/* weight gradient of a cesm_conv_fwd launch; written in PyTorch layout [D0][D1][1][KH][KW] with the
+ * (swap, flip) mapping of cesm_conv_pack.  slab: nsplit*Cout*KH*KW*(C1+C2) floats. */
+int cesm_conv_wgrad(int dtype, const void* x1, const void* x2, const void* dy1, const void* dy2, float* dw,
+                    float* slab, int nsplit, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout,
+                    int Co1, int KH, int KW, int S, int P, int U, int swap, int flip, int accumulate,
+                    hipStream_t stream);
+/* PyTorch conv weight (fp32) -> GEMM layout Wp[co][tap][ci] in dtype.  swap: GEMM co is dim 1 of
+ * the torch tensor (transposed conv forward / conv dgrad); flip: taps reversed. */
+int cesm_conv_pack(int dtype, const float* w, void* wp, int Cout, int Cin, int KH, int KW, int swap, int flip,
+                   hipStream_t stream);
+/* dst[c] (+)= sum over rows of x[r][c]  (conv bias gradients) ; part: nsplit*C floats */
+int cesm_colsum(int dtype, const void* x, float* dst, float* part, int nsplit, int64_t rows, int C, int accumulate,
+                hipStream_t stream);
+/* stem Conv3d(2->Co,(1,KS,KS),pad KS/2) on cat([x_t, cond]) read straight from the NCDHW fp32 boundary
+ * tensors (video_net.py:595-600, :808-815; model.py:111-121 frame broadcast). */
+int cesm_stem_fwd(int dtype, const float* xt, const float* cond, const float* w, const float* bias, void* y, int B,
+                  int F, int Fx, int Fc, int H, int W, int Co, int KS, hipStream_t stream);
+int cesm_stem_wgrad(int dtype, const float* xt, const float* cond, const void* dy, float* dw, float* part, int nblk,
+                    int B, int F, int Fx, int Fc, int H, int W, int Co, int KS, int accumulate, hipStream_t stream);
+/* head Conv3d(C->1,1) (video_net.py:763) evaluated on frame F//2 only (model.py:124-130). */
+int cesm_head_fwd(int dtype, const void* x, const float* w, const float* bias, float* out, int B, int F, int HW, int C,
+                  hipStream_t stream);
+int cesm_head_bwd(int dtype, const float* dout, const void* x, const float* w, void* dx, float* dw, float* db,
+                  float* part, int nblk, int B, int F, int HW, int C, int accumulate, hipStream_t stream);
+
+/* ---- normalisation (csrc/norm.hip) -------------------------------------------------------
+ * GroupNorm(G,C) eps, affine, then x*(scale+1)+shift, SiLU, + residual: video_net.py:216-227, :265. */
+int cesm_gn_stats(int dtype, const void* y, float* stats, double* ws, int B, int64_t rows_b, int C, int G, float eps,
+                  hipStream_t stream);
+int cesm_gn_apply(int dtype, const void* y, const float* stats, const float* gamma, const float* beta,
+                  const float* ss, const void* res, void* out, int B, int64_t rows_b, int C, int G,
+                  hipStream_t stream);
+int cesm_gn_bwd(int dtype, const void* dout, const void* y, const float* stats, const float* gamma,
+                const float* beta, const float* ss, void* dy, float* dss, float* dgamma, float* dbeta, float* ws,
+                int B, int64_t rows_b, int C, int G, int accumulate, hipStream_t stream);
+/* channel LayerNorm (biased var, gamma only): video_net.py:78-87 */
+int cesm_ln_fwd(int dtype, const void* x, const float* gamma, void* out, float* mr, int64_t V, int C, float eps,
+                hipStream_t stream);
+/* dx = LN backward + dres (the Residual wrapper's pass-through gradient, video_net.py:75) */
+int cesm_ln_bwd(int dtype, const void* dy, const void* x, const float* mr, const float* gamma, const void* dres,
+                void* dx, float* dgamma, float* part, int nblk, int64_t V, int C, int accumulate, hipStream_t stream);
+
+/* ---- attention (csrc/attn.hip) -----------------------------------------------------------
+ * RoPE angle table (rotary_embedding.py:143-144, :275-278): rot[f][i] = (cos, sin)(f*freqs[i]). */
+int cesm_rope_table(const float* freqs, float* rot, int F, hipStream_t stream);
+/* RelativePositionBias (video_net.py:268-310): bias[h][i][j] = table[bucket(j-i)][h] and backward. */
+int cesm_relpos_fwd(const float* table, float* bias, int F, int heads, int num_buckets, int max_distance,
+                    hipStream_t stream);
+int cesm_relpos_bwd(const float* part, int nparts_per_h, int B, float* dtable, int F, int heads, int num_buckets,
+                    int max_distance, int accumulate, hipStream_t stream);
+/* temporal attention core (video_net.py:401-453 between to_qkv and to_out), qkv [V][768] -> out [V][256] */
+int cesm_tattn_nblk(int F, int HW);
+int cesm_tattn_fwd(int dtype, const void* qkv, const float* bias, const float* rot, void* out, float* lse, int B,
+                   int F, int HW, float scale, hipStream_t stream);
+int cesm_tattn_bwd(int dtype, const void* qkv, const void* o, const void* dout, const float* lse, const float* bias,
+                   const float* rot, void* dqkv, float* dbias_part, int B, int F, int HW, float scale,
+                   hipStream_t stream);
+/* spatial linear attention core (video_net.py:335-345 between to_qkv and to_out) */
+int cesm_sla_nchunk(int HW);
+int cesm_sla_fwd(int dtype, const void* qkv, void* out, float* ctx, float* ml, float* ws, int Nf, int HW, float scale,
+                 hipStream_t stream);
+int cesm_sla_bwd(int dtype, const void* qkv, const void* dout, const float* ctx, const float* ml, void* dqkv,
+                 float* ws, int Nf, int HW, float scale, hipStream_t stream);
+
+/* ---- small ops, loss, optimizer, data (csrc/misc.hip) ------------------------------------- */
+/* SinusoidalPosEmb (video_net.py:101-113) */
+int cesm_sinusoidal(const int64_t* t, float* emb, int B, int dim, hipStream_t stream);
+/* y = bias + act(x) W^T, act = SiLU when silu_in (time_mlp video_net.py:651-656, ResnetBlock.mlp :238-242) */
+int cesm_linear_small_fwd(const float* x, const float* w, const float* bias, float* y, int R, int I, int O,
+                          int silu_in, hipStream_t stream);
+int cesm_linear_small_bwd(const float* x, const float* w, const float* dy, float* dx, float* dw, float* db, int R,
+                          int I, int O, int silu_in, int accumulate_dx, int accumulate_w, hipStream_t stream);
+/* Diffusion.q_sample (model.py:196-201) and F.mse_loss (model.py:208) */
+int cesm_q_sample(const float* x0, const float* noise, const int64_t* t, const float* sa, const float* s1a,
+                  float* xt, int B, int64_t HW, hipStream_t stream);
+int cesm_mse(const float* pred, const float* tgt, float* loss, float* part, int64_t n, hipStream_t stream);
+int cesm_mse_bwd(const float* pred, const float* tgt, const float* gscale, float* dpred, int64_t n,
+                 hipStream_t stream);
+/* clip_grad_norm_ (train.py:865; torch/nn/utils/clip_grad.py:165-180) over a flat grad buffer;
+ * info = {norm, clamped clip coef, finite(loss & norm)} stays on device (no host sync). */
+int cesm_grad_norm(const float* g, int64_t n, float max_norm, const float* loss, double* part, float* info,
+                   hipStream_t stream);
+/* AdamW step (train.py:1077-1083, torch/optim/adam.py:417-547) over flat buffers; skipped on device
+ * when info[2] == 0 (non-finite), applies the clip coefficient info[1] when use_clip. */
+int cesm_adamw(float* p, float* g, float* m, float* v, const float* info, int64_t n, float lr, float b1, float b2,
+               float eps, float wd, int step, int use_clip, hipStream_t stream);
+/* out = a + b (gradient sums at residual / skip fan-outs) */
+int cesm_add(int dtype, const void* a, const void* b, void* out, int64_t n, hipStream_t stream);
+int cesm_cast(int dtype_in, int dtype_out, const void* x, void* y, int64_t n, hipStream_t stream);
+/* WindowedAllMembersDataset_random.__getitem__ gather (dataset_single_member.py:168-196);
+ * items: nitems x {t0, m, anchor, reverse, crop_i, crop_j} int64 */
+int cesm_window_gather(const float* cond, const float* tgt, const int64_t* items, float* cwin, float* x0,
+                       int nitems, int K, int M, int H, int W, int h, int w, int center, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CESM_HIP_H */

@@ -1,0 +1,407 @@
+"""Per-kernel parity on the GPU: each HIP kernel vs a float64 CPU PyTorch evaluation of the same op.
+
+fp32 kernels: relative L2 error < 1e-5 (parity mode); bf16 kernels: inputs are rounded to bf16
+before the reference is evaluated, relative L2 < 1e-2 (bf16 output rounding + fp32 accumulation).
+"""
+import math
+
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from cesm_emulator_amd import kernels as K
+from cesm_emulator_amd import video_net as VN
+
+pytestmark = pytest.mark.gpu
+
+TOL = {torch.float32: 1e-5, torch.bfloat16: 1e-2}
+
+
+def rel(a, b):
+    a = a.double().cpu()
+    b = b.double().cpu()
+    return (torch.linalg.vector_norm(a - b) / torch.linalg.vector_norm(b).clamp_min(1e-30)).item()
+
+
+def to_cl(x):  # [B,C,F,H,W] -> [B*F,H,W,C]
+    B, C, Fr, H, W = x.shape
+    return x.permute(0, 2, 3, 4, 1).reshape(B * Fr, H, W, C).contiguous()
+
+
+def from_cl(x, B):  # [B*F,H,W,C] -> [B,C,F,H,W]
+    N, H, W, C = x.shape
+    return x.reshape(B, N // B, H, W, C).permute(0, 4, 1, 2, 3).contiguous()
+
+
+class PackHost:
+    def _packed(self, w, cdt, cout, cin, kh, kw, swap, flip):
+        return K.conv_pack(w.detach().contiguous(), cdt, cout, cin, kh, kw, swap, flip)
+
+
+def make_rc(B, F, cdt):
+    return VN.RunCtx(PackHost(), B, F, cdt, True)
+
+
+def q(x, cdt):
+    """round to the kernel storage dtype, return fp64 CPU copy"""
+    return x.to(cdt).double().cpu()
+
+
+CONV_CASES = [
+    # kind, cin, cout, k, stride, pad
+    ("conv", 64, 64, 3, 1, 1),
+    ("conv", 128, 64, 3, 1, 1),
+    ("conv", 64, 128, 3, 1, 1),
+    ("conv", 64, 192, 1, 1, 0),
+    ("conv", 64, 64, 4, 2, 1),
+    ("convT", 64, 64, 4, 2, 1),
+    ("convT", 128, 128, 4, 2, 1),
+]
+
+
+@pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_bwd(dev, cdt, case):
+    kind, cin, cout, k, s, p = case
+    torch.manual_seed(0)
+    B, Fr, H, W = 2, 3, 10, 14
+    if kind == "conv":
+        mod = nn.Conv3d(cin, cout, (1, k, k), (1, s, s), (0, p, p))
+    else:
+        mod = nn.ConvTranspose3d(cin, cout, (1, k, k), (1, s, s), (0, p, p))
+    x = torch.randn(B, cin, Fr, H, W)
+    mod_ref = mod.double()
+    mod_dev = type(mod)(*([cin, cout, (1, k, k), (1, s, s), (0, p, p)])).to(dev)
+    mod_dev.load_state_dict({kk: v.float() for kk, v in mod.state_dict().items()})
+    rc = make_rc(B, Fr, cdt)
+    spec = VN.ConvSpec(mod_dev)
+    xd = to_cl(x).to(dev, cdt)
+    y, st = VN.conv_forward(rc, spec, xd)
+    xr = q(x, cdt).requires_grad_(True)
+    wr = mod_ref.weight.detach().to(cdt).double().requires_grad_(True)
+    br = mod_ref.bias.detach().double().requires_grad_(True)
+    if kind == "conv":
+        yr = F.conv3d(xr, wr, br, (1, s, s), (0, p, p))
+    else:
+        yr = F.conv_transpose3d(xr, wr, br, (1, s, s), (0, p, p))
+    assert rel(from_cl(y, B), yr) < TOL[cdt]
+    # backward
+    g = torch.randn_like(yr)
+    yr.backward(g.double())
+    gd = to_cl(g.float()).to(dev, cdt)
+    dx = VN.conv_backward(rc, spec, st, gd, True)
+    torch.cuda.synchronize()
+    gq = q(g, cdt)
+    xr2 = q(x, cdt).requires_grad_(True)
+    wr2 = wr.detach().clone().requires_grad_(True)
+    br2 = br.detach().clone().requires_grad_(True)
+    yr2 = (F.conv3d(xr2, wr2, br2, (1, s, s), (0, p, p)) if kind == "conv"
+           else F.conv_transpose3d(xr2, wr2, br2, (1, s, s), (0, p, p)))
+    yr2.backward(gq)
+    assert rel(from_cl(dx, B), xr2.grad) < TOL[cdt]
+    assert rel(mod_dev.weight.grad, wr2.grad) < TOL[cdt]
+    assert rel(mod_dev.bias.grad, br2.grad) < TOL[cdt]
+
+
+@pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
+def test_conv_concat_split_and_residual(dev, cdt):
+    """two-source input (torch.cat fused into the loader), split dgrad + fused residual grads"""
+    torch.manual_seed(1)
+    B, Fr, H, W = 1, 2, 9, 11
+    c1, c2, cout = 64, 128, 64
+    mod = nn.Conv3d(c1 + c2, cout, (1, 3, 3), padding=(0, 1, 1))
+    md = nn.Conv3d(c1 + c2, cout, (1, 3, 3), padding=(0, 1, 1)).to(dev)
+    md.load_state_dict(mod.state_dict())
+    a = torch.randn(B, c1, Fr, H, W)
+    b = torch.randn(B, c2, Fr, H, W)
+    res = torch.randn(B, cout, Fr, H, W)
+    rc = make_rc(B, Fr, cdt)
+    spec = VN.ConvSpec(md)
+    y, st = VN.conv_forward(rc, spec, to_cl(a).to(dev, cdt), to_cl(b).to(dev, cdt), res=to_cl(res).to(dev, cdt))
+    ar, br_ = q(a, cdt).requires_grad_(True), q(b, cdt).requires_grad_(True)
+    wr = mod.weight.detach().to(cdt).double().requires_grad_(True)
+    yr = F.conv3d(torch.cat([ar, br_], 1), wr, mod.bias.double(), padding=(0, 1, 1)) + q(res, cdt)
+    assert rel(from_cl(y, B), yr) < TOL[cdt]
+    g = torch.randn_like(yr)
+    gq = q(g, cdt)
+    yr.backward(gq)
+    r1 = torch.randn(B, c1, Fr, H, W)
+    r2 = torch.randn(B, c2, Fr, H, W)
+    dx1, dx2 = VN.conv_backward(rc, spec, st, to_cl(g.float()).to(dev, cdt), True,
+                                to_cl(r1).to(dev, cdt), to_cl(r2).to(dev, cdt))
+    assert rel(from_cl(dx1, B), ar.grad + q(r1, cdt)) < TOL[cdt]
+    assert rel(from_cl(dx2, B), br_.grad + q(r2, cdt)) < TOL[cdt]
+    assert rel(md.weight.grad, wr.grad) < TOL[cdt]
+
+
+@pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("with_ss", [True, False])
+def test_block_groupnorm(dev, cdt, with_ss):
+    """Block: conv -> GroupNorm(8) -> x*(scale+1)+shift -> SiLU (+residual), fwd and bwd"""
+    torch.manual_seed(2)
+    B, Fr, H, W, cin, cout = 2, 3, 8, 12, 64, 128
+    blk = VN.Block(cin, cout).to(dev)
+    with torch.no_grad():
+        blk.norm.weight.uniform_(0.5, 1.5)
+        blk.norm.bias.uniform_(-0.5, 0.5)
+    x = torch.randn(B, cin, Fr, H, W)
+    ss = torch.randn(B, 2 * cout) * 0.3 if with_ss else None
+    res = torch.randn(B, cout, Fr, H, W)
+    rc = make_rc(B, Fr, cdt)
+    out, st = VN.block_fwd(rc, blk, to_cl(x).to(dev, cdt), None, None if ss is None else ss.to(dev),
+                           to_cl(res).to(dev, cdt))
+    # reference
+    xr = q(x, cdt).requires_grad_(True)
+    wr = blk.proj.weight.detach().cpu().to(cdt).double().requires_grad_(True)
+    bconv = blk.proj.bias.detach().cpu().double().requires_grad_(True)
+    gam = blk.norm.weight.detach().cpu().double().requires_grad_(True)
+    bet = blk.norm.bias.detach().cpu().double().requires_grad_(True)
+    ssr = ss.double().requires_grad_(True) if ss is not None else None
+    y = F.conv3d(xr, wr, bconv, padding=(0, 1, 1))
+    y = q(y.detach(), cdt).requires_grad_(True) if cdt == torch.bfloat16 else y  # kernel stores y in cdt
+    h = F.group_norm(y, 8, gam, bet, 1e-5)
+    if ssr is not None:
+        sc, sh = ssr[:, :cout, None, None, None], ssr[:, cout:, None, None, None]
+        h = h * (sc + 1) + sh
+    o = F.silu(h) + q(res, cdt)
+    assert rel(from_cl(out, B), o) < TOL[cdt] * (3 if cdt == torch.bfloat16 else 1)
+    g = torch.randn_like(o)
+    o.backward(q(g, cdt))
+    dx, dss = VN.block_bwd(rc, blk, st, to_cl(g.float()).to(dev, cdt), ssr is not None)
+    tol = TOL[cdt] * (5 if cdt == torch.bfloat16 else 10)
+    assert rel(blk.norm.weight.grad, gam.grad) < tol
+    assert rel(blk.norm.bias.grad, bet.grad) < tol
+    if ssr is not None:
+        assert rel(dss, ssr.grad) < tol
+    if cdt == torch.float32:
+        assert rel(from_cl(dx, B), xr.grad) < tol
+        assert rel(blk.proj.weight.grad, wr.grad) < tol
+
+
+@pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("C", [64, 256, 512])
+def test_layernorm(dev, cdt, C):
+    torch.manual_seed(3)
+    V = 1000
+    x = torch.randn(V, C) * 2 + 0.5
+    gamma = torch.rand(C) + 0.5
+    out, mr = K.ln_fwd(x.to(dev, cdt).contiguous(), gamma.to(dev))
+    xr = q(x, cdt).requires_grad_(True)
+    gr = gamma.double().requires_grad_(True)
+    mu = xr.mean(-1, keepdim=True)
+    var = ((xr - mu) ** 2).mean(-1, keepdim=True)
+    o = (xr - mu) / torch.sqrt(var + 1e-5) * gr
+    assert rel(out, o) < TOL[cdt]
+    g = torch.randn(V, C)
+    dres = torch.randn(V, C)
+    o.backward(q(g, cdt))
+    dgam = torch.zeros(C, device=dev)
+    dx = K.ln_bwd(g.to(dev, cdt).contiguous(), x.to(dev, cdt).contiguous(), mr, gamma.to(dev), dgam,
+                  dres=dres.to(dev, cdt).contiguous())
+    assert rel(dx, xr.grad + q(dres, cdt)) < TOL[cdt] * 2
+    assert rel(dgam, gr.grad) < TOL[cdt] * 2
+
+
+def _tattn_ref(qkv, bias, freqs, B, Fr, HW, scale):
+    """oracle-style temporal attention core on qkv [B*F*HW, 768] (float64)"""
+    x = qkv.view(B, Fr, HW, 3, 8, 32).permute(3, 0, 2, 4, 1, 5)  # 3, B, HW, h, F, d
+    qq, kk, vv = x[0] * scale, x[1], x[2]
+    pos = torch.arange(Fr, dtype=torch.float64)
+    ang = (pos[:, None] * freqs.double()[None, :]).repeat_interleave(2, -1)
+
+    def rot(t):
+        t2 = t.unflatten(-1, (-1, 2))
+        rh = torch.stack((-t2[..., 1], t2[..., 0]), -1).flatten(-2)
+        return t * ang.cos() + rh * ang.sin()
+
+    qq, kk = rot(qq), rot(kk)
+    sim = torch.einsum("bphid,bphjd->bphij", qq, kk) + bias.double()
+    sim = sim - sim.amax(-1, keepdim=True)
+    o = torch.einsum("bphij,bphjd->bphid", sim.softmax(-1), vv)  # B, HW, h, F, d
+    return o.permute(0, 3, 1, 2, 4).reshape(B * Fr * HW, 256)
+
+
+@pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("Fr", [1, 3, 12])
+def test_temporal_attention_core(dev, cdt, Fr):
+    torch.manual_seed(4)
+    B, HW = 2, 77
+    qkv = torch.randn(B * Fr * HW, 768)
+    table = torch.randn(32, 8)
+    freqs = 1.0 / (10000 ** (torch.arange(0, 32, 2).float() / 32))
+    scale = 32 ** -0.5
+    bias = K.relpos_fwd(table.to(dev), Fr)
+    from oracle.ref_cpu import RelativePositionBias
+    rp = RelativePositionBias(8, 32, 32)
+    rp.relative_attention_bias.weight.data.copy_(table)
+    bias_ref = rp(Fr)
+    assert torch.equal(bias.cpu(), bias_ref)
+    rot = K.rope_table(freqs.to(dev), Fr)
+    qd = qkv.to(dev, cdt).contiguous()
+    out, lse = K.tattn_fwd(qd, bias, rot, B, Fr, HW, scale)
+    qr = q(qkv, cdt).requires_grad_(True)
+    br = bias_ref.double().requires_grad_(True)
+    o = _tattn_ref(qr, br, freqs, B, Fr, HW, scale)
+    assert rel(out, o) < TOL[cdt] * 2
+    g = torch.randn_like(o)
+    o.backward(q(g, cdt))
+    dtable = torch.zeros(32, 8, device=dev)
+    dqkv = K.tattn_bwd(qd, out, g.to(dev, cdt).contiguous(), lse, bias, rot, dtable, B, Fr, HW, scale)
+    tol = TOL[cdt] * (3 if cdt == torch.bfloat16 else 10)
+    assert rel(dqkv, qr.grad) < tol
+    # table grad: scatter of bias grad through the bucket map
+    tbl = table.double().requires_grad_(True)
+    rp2 = RelativePositionBias(8, 32, 32).double()
+    rp2.relative_attention_bias.weight.data.copy_(tbl.detach())
+    bref = rp2(Fr)
+    (bref * br.grad).sum().backward()
+    assert rel(dtable, rp2.relative_attention_bias.weight.grad) < tol
+
+
+def _sla_ref(qkv, Nf, HW, scale):
+    x = qkv.view(Nf, HW, 3, 8, 32).permute(2, 0, 3, 4, 1)  # 3, Nf, h, d, n
+    qq = x[0].softmax(dim=-2) * scale
+    kk = x[1].softmax(dim=-1)
+    ctx = torch.einsum("bhdn,bhen->bhde", kk, x[2])
+    out = torch.einsum("bhde,bhdn->bhen", ctx, qq)  # Nf, h, e, n
+    return out.permute(0, 3, 1, 2).reshape(Nf * HW, 256)
+
+
+@pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("HW", [77, 3000])
+def test_spatial_linear_attention_core(dev, cdt, HW):
+    torch.manual_seed(5)
+    Nf = 3
+    qkv = torch.randn(Nf * HW, 768) * 2
+    scale = 32 ** -0.5
+    qd = qkv.to(dev, cdt).contiguous()
+    out, ctx, ml = K.sla_fwd(qd, Nf, HW, scale)
+    qr = q(qkv, cdt).requires_grad_(True)
+    o = _sla_ref(qr, Nf, HW, scale)
+    assert rel(out, o) < TOL[cdt] * 2
+    g = torch.randn_like(o)
+    o.backward(q(g, cdt))
+    dqkv = K.sla_bwd(qd, g.to(dev, cdt).contiguous(), ctx, ml, Nf, HW, scale)
+    assert rel(dqkv, qr.grad) < TOL[cdt] * (3 if cdt == torch.bfloat16 else 10)
+
+
+@pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("Fx", [1, 3])
+def test_stem_and_head(dev, cdt, Fx):
+    torch.manual_seed(6)
+    B, Fr, H, W = 2, 3, 20, 35
+    conv = nn.Conv3d(2, 64, (1, 7, 7), padding=(0, 3, 3))
+    cd = nn.Conv3d(2, 64, (1, 7, 7), padding=(0, 3, 3)).to(dev)
+    cd.load_state_dict(conv.state_dict())
+    xt = torch.randn(B, Fx, H, W)
+    cond = torch.randn(B, Fr, H, W)
+    y = K.stem_fwd(xt.to(dev), cond.to(dev), cd.weight, cd.bias, Fr, cdt)
+    xin = torch.cat([xt[:, None].expand(B, 1, Fr, H, W), cond[:, None]], 1).double()
+    wr = conv.weight.detach().double().requires_grad_(True)
+    yr = F.conv3d(xin, wr, conv.bias.double(), padding=(0, 3, 3))
+    assert rel(from_cl(y, B), yr) < TOL[cdt]
+    g = torch.randn_like(yr)
+    yr.backward(q(g, cdt))
+    dw = torch.zeros_like(cd.weight)
+    K.stem_wgrad(xt.to(dev), cond.to(dev), to_cl(g.float()).to(dev, cdt), dw, Fr)
+    assert rel(dw, wr.grad) < TOL[cdt]
+    # head: Conv3d(64->1, 1) on frame F//2
+    hw = torch.randn(64)
+    hb = torch.randn(1)
+    x = torch.randn(B, 64, Fr, H, W)
+    out = K.head_fwd(to_cl(x).to(dev, cdt), hw.to(dev), hb.to(dev), B, Fr)
+    xr = q(x, cdt).requires_grad_(True)
+    hwr = hw.double().requires_grad_(True)
+    ref = (xr[:, :, Fr // 2] * hwr[None, :, None, None]).sum(1, keepdim=True) + hb.double()
+    assert rel(out, ref) < TOL[cdt]
+    go = torch.randn_like(ref)
+    ref.backward(go)
+    dwh = torch.zeros(64, device=dev)
+    dbh = torch.zeros(1, device=dev)
+    dx = K.head_bwd(go.float().to(dev).contiguous(), to_cl(x).to(dev, cdt), hw.to(dev), dwh, dbh, B, Fr)
+    assert rel(from_cl(dx, B), xr.grad) < TOL[cdt]
+    assert rel(dwh, hwr.grad) < TOL[cdt]
+    assert abs(dbh.item() - go.sum().item()) < 1e-3
+
+
+def test_small_linear_and_time_emb(dev):
+    torch.manual_seed(7)
+    R, I, O = 5, 64, 96
+    x = torch.randn(R, I)
+    w = torch.randn(O, I) * 0.1
+    b = torch.randn(O)
+    for silu in (False, True):
+        y = K.linear_small(x.to(dev), w.to(dev), b.to(dev), silu)
+        xr = x.double().requires_grad_(True)
+        wr = w.double().requires_grad_(True)
+        br = b.double().requires_grad_(True)
+        yr = F.linear(F.silu(xr) if silu else xr, wr, br)
+        assert rel(y, yr) < 1e-6
+        g = torch.randn(R, O)
+        yr.backward(g.double())
+        dx = torch.zeros(R, I, device=dev)
+        dw = torch.zeros(O, I, device=dev)
+        db = torch.zeros(O, device=dev)
+        K.linear_small_bwd(x.to(dev), w.to(dev), g.to(dev), dx, dw, db, silu, True)
+        assert rel(dx, xr.grad) < 1e-6 and rel(dw, wr.grad) < 1e-6 and rel(db, br.grad) < 1e-6
+    t = torch.tensor([0, 1, 17, 999])
+    emb = K.sinusoidal(t.to(dev), 64)
+    from oracle.ref_cpu import SinusoidalPosEmb
+    assert rel(emb, SinusoidalPosEmb(64)(t)) < 1e-5
+
+
+def test_adamw_clip_matches_torch(dev):
+    from cesm_emulator_amd.optim import FusedAdamW
+    torch.manual_seed(8)
+    ps = [torch.randn(37, 5), torch.randn(1000), torch.randn(3, 3, 3)]
+    gs = [[torch.randn_like(p) * 3 for p in ps] for _ in range(3)]
+    ref = [p.clone().double().requires_grad_(True) for p in ps]
+    opt_r = torch.optim.AdamW(ref, lr=2e-4, betas=(0.9, 0.999), weight_decay=1e-4)
+    dp = [nn.Parameter(p.clone().to(dev)) for p in ps]
+    opt = FusedAdamW(dp, lr=2e-4, betas=(0.9, 0.999), weight_decay=1e-4, max_grad_norm=1.0)
+    for step in range(3):
+        for r, g in zip(ref, gs[step]):
+            r.grad = g.double().clone()
+        torch.nn.utils.clip_grad_norm_(ref, 1.0)
+        opt_r.step()
+        opt.zero_grad()
+        for p, g in zip(dp, gs[step]):
+            p.grad.copy_(g.to(dev))
+        opt.step()
+    for p, r in zip(dp, ref):
+        assert rel(p.detach(), r.detach()) < 1e-6
+
+
+def test_q_sample_mse(dev):
+    from cesm_emulator_amd.model import Diffusion
+    from oracle.ref_cpu import Diffusion as RD
+    torch.manual_seed(9)
+    d = Diffusion(nn.Identity()).to(dev)
+    rd = RD(nn.Identity())
+    for name, buf in rd.named_buffers():
+        assert torch.equal(buf, getattr(d, name).cpu()), name
+    x0 = torch.randn(3, 1, 16, 24)
+    noise = torch.randn_like(x0)
+    t = torch.tensor([0, 500, 999])
+    xt, _ = d.q_sample(x0.to(dev), t.to(dev), noise.to(dev))
+    xr, _ = rd.q_sample(x0, t, noise)
+    assert rel(xt, xr) < 1e-6
+    pred = torch.randn_like(x0)
+    loss = K.mse(pred.to(dev), noise.to(dev))
+    assert abs(loss.item() - F.mse_loss(pred, noise).item()) < 1e-6
+
+
+def test_window_gather(dev):
+    """device gather == WindowedAllMembersDataset_random.__getitem__ semantics (host restatement)"""
+    from oracle.ref_data import window_item as host_window_item
+    torch.manual_seed(10)
+    T, M, H, W, Kw = 9, 3, 10, 12, 5
+    cond = torch.randn(T, M, H, W)
+    tgt = torch.randn(T, M, H, W)
+    items = torch.tensor([[0, 1, 2, 0, 1, 2], [3, 2, 5, 1, 0, 0], [4, 0, 6, 1, 2, 3]], dtype=torch.int64)
+    cw, x0 = K.window_gather(cond.to(dev), tgt.to(dev), items.to(dev), Kw, 7, 8, True)
+    for i in range(items.shape[0]):
+        c_ref, x_ref = host_window_item(cond.numpy(), tgt.numpy(), items[i].tolist(), Kw, 7, 8, True)
+        assert torch.equal(cw[i].cpu(), torch.from_numpy(c_ref))
+        assert torch.equal(x0[i].cpu(), torch.from_numpy(x_ref))
