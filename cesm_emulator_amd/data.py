@@ -97,6 +97,21 @@ class WindowSampler:
         return np.asarray([self.item(int(k)) for k in indices], dtype=np.int64).reshape(-1, 6)
 
 
+def host_gather(cond, tgt, items, K, h, w, center, out_c, out_x):
+    """Host-side batch assembly for the pinned path: out_c [n,1,K,h,w], out_x [n,1,h,w] (numpy
+    views of pinned buffers) from (T,M,H,W) fields and item rows (t0, m, anchor, rev, i, j)."""
+    for n, (t0, m, anchor, rev, i, j) in enumerate(items):
+        cw = cond[t0:t0 + K, m, i:i + h, j:j + w]
+        if rev:
+            if center:
+                mid = K // 2
+                cw = np.concatenate([cw[:mid][::-1], cw[mid:mid + 1], cw[mid + 1:][::-1]], axis=0)
+            else:
+                cw = cw[::-1]
+        out_c[n, 0] = cw
+        out_x[n, 0] = tgt[anchor, m, i:i + h, j:j + w]
+
+
 def shard_indices(n, batch_size, rank=0, world=1, shuffle=True, seed=0, epoch=0, drop_last=False):
     """DistributedSampler semantics (train.py:1002): seeded permutation per epoch, padded to a
     multiple of world, rank-strided; then cut into batches."""
@@ -183,19 +198,8 @@ class PinnedWindowLoader:
 
     def _fill_host(self, slot, items):
         hc, hx = self.host[slot]
-        Kw = self.sampler.K
         h, w = self.sampler.hw
-        for n, (t0, m, anchor, rev, i, j) in enumerate(items):
-            times = np.arange(t0, t0 + Kw)
-            cw = self.cond[times, m, i:i + h, j:j + w]
-            if rev:
-                if self.sampler.center:
-                    mid = Kw // 2
-                    cw = np.concatenate([cw[:mid][::-1], cw[mid:mid + 1], cw[mid + 1:][::-1]], axis=0)
-                else:
-                    cw = cw[::-1]
-            hc[n, 0].numpy()[...] = cw
-            hx[n, 0].numpy()[...] = self.tgt[anchor, m, i:i + h, j:j + w]
+        host_gather(self.cond, self.tgt, items, self.sampler.K, h, w, self.sampler.center, hc.numpy(), hx.numpy())
 
     def __iter__(self):
         batches = shard_indices(len(self.sampler), self.bs, self.rank, self.world, self.shuffle, self.seed,
