@@ -147,9 +147,16 @@ def main():
     probe = KernelProbe(K, lambda x1, x2, geom: geom[3] == 3 and x1.shape[1] == H and x1.shape[3] == 64
                         and x2 is None and geom[2] == 64)
 
+    def log(msg):
+        if rank == 0:
+            print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+    t_w = time.perf_counter()
     for _ in range(a.warmup):
         train_step(diff, opt, x0, cond, 1.0, dp)
     torch.cuda.synchronize()
+    log(f"warmup {a.warmup} steps: {time.perf_counter() - t_w:.1f}s, "
+        f"peak mem {torch.cuda.max_memory_allocated(dev) / 2**30:.1f} GiB")
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -200,7 +207,9 @@ def main():
         "loss": lval,
         "roofline": roof,
     }
+    log(f"timed {a.steps} steps: {elapsed:.2f}s -> {value:.2f} samples/s")
     if not a.no_cpu_baseline and world == 1:
+        log("cpu baseline (oracle fp32 train step on host cores) ...")
         out["cpu_baseline"] = cpu_baseline(cfg["unet"], F, H, W, a.cpu_crop)
     print(json.dumps(out), flush=True)
     if world > 1:
