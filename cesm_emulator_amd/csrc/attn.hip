@@ -3,10 +3,11 @@
 //    axis F: q*scale -> RoPE (rotary_embedding.py:29-48, 146-163) on q and k -> q.k + rel-pos
 //    bias (video_net.py:268-310) -> softmax -> attn.v.  The QKV / output projections run on the
 //    MFMA conv kernel as 1x1 convs; this file is the per-pixel core (tiny F x F x 32 problems,
-//    VALU, one lane per (pixel, head, query frame)).
+//    VALU, one lane per (pixel, head, frame); each lane rotates only its own q/k row and shares
+//    it with the other F lanes of its pixel through LDS).
 //  * spatial linear attention core (video_net.py:313-347): k-softmax over all H*W positions of
 //    a frame (split-n with rescaled partial contexts, deterministic combine), q-softmax over the
-//    32 head dims, out = context^T q.
+//    32 head dims, out = context^T q (one head per wave: the context is an LDS broadcast).
 //
 // Layouts (channels-last, voxel v = (b*F + f)*HW + p):
 //   qkv [V][768] = q | k | v, head-major inside each (channel = h*32 + d)
@@ -19,6 +20,8 @@ constexpr int DH = 32;      // head dim
 constexpr int NH = 8;       // heads
 constexpr int INNER = 256;  // NH*DH
 constexpr int QKV = 768;
+constexpr int TA_T = 128;   // threads per temporal-attention block
+constexpr int TA_LD = 36;   // padded LDS row (floats) for a staged 32-vector
 
 // rot[f][i] = (cos, sin) of f * freqs[i], i < 16
 __global__ void rope_table_kernel(const float* __restrict__ freqs, float* __restrict__ rot, int F) {
@@ -40,6 +43,17 @@ __device__ __forceinline__ void store32(T* p, const float* v) {
 #pragma unroll
   for (int i = 0; i < 32; i += 8) store8(p + i, v + i);
 }
+__device__ __forceinline__ void lds_store32(float* p, const float* v) {
+#pragma unroll
+  for (int i = 0; i < 32; i += 4) *reinterpret_cast<f32x4*>(p + i) = f32x4{v[i], v[i + 1], v[i + 2], v[i + 3]};
+}
+__device__ __forceinline__ void lds_load32(const float* p, float* v) {
+#pragma unroll
+  for (int i = 0; i < 32; i += 4) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(p + i);
+    v[i] = a[0]; v[i + 1] = a[1]; v[i + 2] = a[2]; v[i + 3] = a[3];
+  }
+}
 // x'[2i] = x[2i] c - x[2i+1] s ; x'[2i+1] = x[2i+1] c + x[2i] s   (sign = +1)
 // inverse (transpose) with sign = -1
 __device__ __forceinline__ void rope(float* v, const float* rot, float sign) {
@@ -52,88 +66,109 @@ __device__ __forceinline__ void rope(float* v, const float* rot, float sign) {
   }
 }
 
-// grid: x = pixel-block (grid-stride), y = b*NH + h. Block = G groups of F lanes (G = 256/F).
+// grid: x = pixel-block (grid-stride), y = b*NH + h.  Block = G = TA_T/F groups of F lanes.
 template <typename T>
-__global__ __launch_bounds__(256) void tattn_fwd_kernel(const T* __restrict__ qkv, const float* __restrict__ bias,
-                                                        const float* __restrict__ rotg, T* __restrict__ out,
-                                                        float* __restrict__ lse, int F, int HW, float scale) {
-  __shared__ float rot[128 * 32];
+__global__ __launch_bounds__(TA_T) void tattn_fwd_kernel(const T* __restrict__ qkv, const float* __restrict__ bias,
+                                                         const float* __restrict__ rotg, T* __restrict__ out,
+                                                         float* __restrict__ lse, int F, int HW, float scale) {
+  __shared__ float rot[32 * 32];
   __shared__ float sb[32 * 32];
+  __shared__ __attribute__((aligned(16))) float sk[TA_T * TA_LD];
   const int b = blockIdx.y / NH, h = blockIdx.y % NH;
   for (int e = threadIdx.x; e < F * 32; e += blockDim.x) rot[e] = rotg[e];
   for (int e = threadIdx.x; e < F * F; e += blockDim.x) sb[e] = bias[h * F * F + e];
   __syncthreads();
-  const int G = 256 / F;
-  const int g = threadIdx.x / F, i = threadIdx.x % F;
-  if (g >= G) return;
-  const int npb = (HW + G - 1) / G;
-  for (int pb = blockIdx.x; pb < npb; pb += gridDim.x) {
-    const int p = pb * G + g;
-    if (p >= HW) continue;
-    const int64_t vi = ((int64_t)b * F + i) * HW + p;
-    float q[32], acc[32];
-    load32(qkv + vi * QKV + h * DH, q);
-#pragma unroll
-    for (int d = 0; d < 32; ++d) { q[d] *= scale; acc[d] = 0.f; }
-    rope(q, rot + i * 32, 1.f);
-    float m = -INFINITY, l = 0.f;
-    for (int j = 0; j < F; ++j) {
-      const int64_t vj = ((int64_t)b * F + j) * HW + p;
-      float k[32];
-      load32(qkv + vj * QKV + INNER + h * DH, k);
-      rope(k, rot + j * 32, 1.f);
-      float s = 0.f;
-#pragma unroll
-      for (int d = 0; d < 32; ++d) s = fmaf(q[d], k[d], s);
-      s += sb[i * F + j];
-      float v[32];
-      load32(qkv + vj * QKV + 2 * INNER + h * DH, v);
-      const float mn = fmaxf(m, s);
-      const float corr = expf(m - mn);
-      const float pj = expf(s - mn);
-      l = l * corr + pj;
-#pragma unroll
-      for (int d = 0; d < 32; ++d) acc[d] = fmaf(pj, v[d], acc[d] * corr);
-      m = mn;
-    }
-    const float inv = 1.f / l;
-#pragma unroll
-    for (int d = 0; d < 32; ++d) acc[d] *= inv;
-    store32(out + vi * INNER + h * DH, acc);
-    if (lse) lse[(((int64_t)b * NH + h) * HW + p) * F + i] = m + logf(l);
-  }
-}
-
-// backward.  Phase 1 (lane = query i): D_i, dq_i, dbias row accumulation.
-//            Phase 2 (lane = key j):   dk_j, dv_j.
-// dbias partials: part[blockIdx.y][blockIdx.x][i][j] (the block's sum over its pixels)
-template <typename T>
-__global__ __launch_bounds__(256) void tattn_bwd_kernel(const T* __restrict__ qkv, const T* __restrict__ o,
-                                                        const T* __restrict__ dout, const float* __restrict__ lse,
-                                                        const float* __restrict__ bias,
-                                                        const float* __restrict__ rotg, T* __restrict__ dqkv,
-                                                        float* __restrict__ dbias_part, int F, int HW, float scale) {
-  __shared__ float rot[128 * 32];
-  __shared__ float sb[32 * 32];
-  __shared__ float sD[256], sL[256];
-  __shared__ float red[256];
-  const int b = blockIdx.y / NH, h = blockIdx.y % NH;
-  for (int e = threadIdx.x; e < F * 32; e += blockDim.x) rot[e] = rotg[e];
-  for (int e = threadIdx.x; e < F * F; e += blockDim.x) sb[e] = bias[h * F * F + e];
-  __syncthreads();
-  const int G = 256 / F;
+  const int G = TA_T / F;
   const int g = threadIdx.x / F, i = threadIdx.x % F;
   const bool lane_ok = g < G;
-  float dbacc[32];
-  for (int j = 0; j < 32; ++j) dbacc[j] = 0.f;
   const int npb = (HW + G - 1) / G;
   for (int pb = blockIdx.x; pb < npb; pb += gridDim.x) {
     const int p = pb * G + g;
     const bool ok = lane_ok && p < HW;
-    // ---- phase 1: lane = query row i
+    const int64_t vi = ((int64_t)b * F + i) * HW + p;
+    float q[32];
+    if (ok) {
+      float k[32];
+      load32(qkv + vi * QKV + INNER + h * DH, k);
+      rope(k, rot + i * 32, 1.f);
+      lds_store32(sk + threadIdx.x * TA_LD, k);
+      load32(qkv + vi * QKV + h * DH, q);
+#pragma unroll
+      for (int d = 0; d < 32; ++d) q[d] *= scale;
+      rope(q, rot + i * 32, 1.f);
+    }
+    __syncthreads();
+    if (ok) {
+      float acc[32];
+#pragma unroll
+      for (int d = 0; d < 32; ++d) acc[d] = 0.f;
+      float m = -INFINITY, l = 0.f;
+      for (int j = 0; j < F; ++j) {
+        float k[32], v[32];
+        lds_load32(sk + (g * F + j) * TA_LD, k);
+        float s = 0.f;
+#pragma unroll
+        for (int d = 0; d < 32; ++d) s = fmaf(q[d], k[d], s);
+        s += sb[i * F + j];
+        const int64_t vj = ((int64_t)b * F + j) * HW + p;
+        load32(qkv + vj * QKV + 2 * INNER + h * DH, v);
+        const float mn = fmaxf(m, s);
+        const float corr = expf(m - mn);
+        const float pj = expf(s - mn);
+        l = l * corr + pj;
+#pragma unroll
+        for (int d = 0; d < 32; ++d) acc[d] = fmaf(pj, v[d], acc[d] * corr);
+        m = mn;
+      }
+      const float inv = 1.f / l;
+#pragma unroll
+      for (int d = 0; d < 32; ++d) acc[d] *= inv;
+      store32(out + vi * INNER + h * DH, acc);
+      if (lse) lse[(((int64_t)b * NH + h) * HW + p) * F + i] = m + logf(l);
+    }
+    __syncthreads();
+  }
+}
+
+// backward.  Phase 1 (lane = query i): D_i, dq_i, dbias row accumulation (k' rows in LDS).
+//            Phase 2 (lane = key j):   dk_j, dv_j (q' rows in LDS).
+// dbias partials: part[blockIdx.y][blockIdx.x][i][j] (the block's sum over its pixels)
+template <typename T>
+__global__ __launch_bounds__(TA_T) void tattn_bwd_kernel(const T* __restrict__ qkv, const T* __restrict__ o,
+                                                         const T* __restrict__ dout, const float* __restrict__ lse,
+                                                         const float* __restrict__ bias,
+                                                         const float* __restrict__ rotg, T* __restrict__ dqkv,
+                                                         float* __restrict__ dbias_part, int F, int HW,
+                                                         float scale) {
+  __shared__ float rot[32 * 32];
+  __shared__ float sb[32 * 32];
+  __shared__ __attribute__((aligned(16))) float sv[TA_T * TA_LD];  // k' (phase 1) / q' (phase 2)
+  __shared__ float sD[TA_T], sL[TA_T];
+  __shared__ float sacc[TA_T * 33];
+  const int b = blockIdx.y / NH, h = blockIdx.y % NH;
+  for (int e = threadIdx.x; e < F * 32; e += blockDim.x) rot[e] = rotg[e];
+  for (int e = threadIdx.x; e < F * F; e += blockDim.x) sb[e] = bias[h * F * F + e];
+  for (int e = threadIdx.x; e < TA_T * 33; e += blockDim.x) sacc[e] = 0.f;
+  __syncthreads();
+  const int G = TA_T / F;
+  const int g = threadIdx.x / F, i = threadIdx.x % F;
+  const bool lane_ok = g < G;
+  float* myacc = sacc + threadIdx.x * 33;
+  const int npb = (HW + G - 1) / G;
+  for (int pb = blockIdx.x; pb < npb; pb += gridDim.x) {
+    const int p = pb * G + g;
+    const bool ok = lane_ok && p < HW;
+    const int64_t vi = ((int64_t)b * F + i) * HW + p;
+    // ---- phase 1: stage k'_i
     float D = 0.f, L = 0.f;
     if (ok) {
-      const int64_t vi = ((int64_t)b * F + i) * HW + p;
+      float k[32];
+      load32(qkv + vi * QKV + INNER + h * DH, k);
+      rope(k, rot + i * 32, 1.f);
+      lds_store32(sv + threadIdx.x * TA_LD, k);
+    }
+    __syncthreads();
+    if (ok) {
       float q[32], dq[32], dO[32];
       load32(dout + vi * INNER + h * DH, dO);
       {
@@ -148,18 +183,17 @@ __global__ __launch_bounds__(256) void tattn_bwd_kernel(const T* __restrict__ qk
       for (int d = 0; d < 32; ++d) { q[d] *= scale; dq[d] = 0.f; }
       rope(q, rot + i * 32, 1.f);
       for (int j = 0; j < F; ++j) {
-        const int64_t vj = ((int64_t)b * F + j) * HW + p;
         float k[32], v[32];
-        load32(qkv + vj * QKV + INNER + h * DH, k);
+        lds_load32(sv + (g * F + j) * TA_LD, k);
+        const int64_t vj = ((int64_t)b * F + j) * HW + p;
         load32(qkv + vj * QKV + 2 * INNER + h * DH, v);
-        rope(k, rot + j * 32, 1.f);
         float s = 0.f, dp = 0.f;
 #pragma unroll
         for (int d = 0; d < 32; ++d) { s = fmaf(q[d], k[d], s); dp = fmaf(dO[d], v[d], dp); }
         s += sb[i * F + j];
         const float P = expf(s - L);
         const float dS = P * (dp - D);
-        if (j < 32) dbacc[j] += dS;
+        myacc[j] += dS;
 #pragma unroll
         for (int d = 0; d < 32; ++d) dq[d] = fmaf(dS, k[d], dq[d]);
       }
@@ -171,25 +205,29 @@ __global__ __launch_bounds__(256) void tattn_bwd_kernel(const T* __restrict__ qk
     sD[threadIdx.x] = D;
     sL[threadIdx.x] = L;
     __syncthreads();
-    // ---- phase 2: lane = key row j (= i index of this lane)
+    // ---- phase 2: stage q'_i, lane acts as key row j = i
+    if (ok) {
+      float q[32];
+      load32(qkv + vi * QKV + h * DH, q);
+#pragma unroll
+      for (int d = 0; d < 32; ++d) q[d] *= scale;
+      rope(q, rot + i * 32, 1.f);
+      lds_store32(sv + threadIdx.x * TA_LD, q);
+    }
+    __syncthreads();
     if (ok) {
       const int j = i;
-      const int64_t vj = ((int64_t)b * F + j) * HW + p;
-      float k[32], dk[32], dv[32];
-      load32(qkv + vj * QKV + INNER + h * DH, k);
+      float k[32], v[32], dk[32], dv[32];
+      load32(qkv + vi * QKV + INNER + h * DH, k);
       rope(k, rot + j * 32, 1.f);
-      float v[32];
-      load32(qkv + vj * QKV + 2 * INNER + h * DH, v);
+      load32(qkv + vi * QKV + 2 * INNER + h * DH, v);
 #pragma unroll
       for (int d = 0; d < 32; ++d) { dk[d] = 0.f; dv[d] = 0.f; }
       for (int ii = 0; ii < F; ++ii) {
-        const int64_t vi = ((int64_t)b * F + ii) * HW + p;
         float q[32], dO[32];
-        load32(qkv + vi * QKV + h * DH, q);
-#pragma unroll
-        for (int d = 0; d < 32; ++d) q[d] *= scale;
-        rope(q, rot + ii * 32, 1.f);
-        load32(dout + vi * INNER + h * DH, dO);
+        lds_load32(sv + (g * F + ii) * TA_LD, q);
+        const int64_t vq = ((int64_t)b * F + ii) * HW + p;
+        load32(dout + vq * INNER + h * DH, dO);
         float s = 0.f, dp = 0.f;
 #pragma unroll
         for (int d = 0; d < 32; ++d) { s = fmaf(q[d], k[d], s); dp = fmaf(dO[d], v[d], dp); }
@@ -201,22 +239,18 @@ __global__ __launch_bounds__(256) void tattn_bwd_kernel(const T* __restrict__ qk
         for (int d = 0; d < 32; ++d) { dk[d] = fmaf(dS, q[d], dk[d]); dv[d] = fmaf(P, dO[d], dv[d]); }
       }
       rope(dk, rot + j * 32, -1.f);
-      store32(dqkv + vj * QKV + INNER + h * DH, dk);
-      store32(dqkv + vj * QKV + 2 * INNER + h * DH, dv);
+      store32(dqkv + vi * QKV + INNER + h * DH, dk);
+      store32(dqkv + vi * QKV + 2 * INNER + h * DH, dv);
     }
     __syncthreads();
   }
-  // deterministic block reduction of dbias rows: for each j, sum lanes with the same i
+  // deterministic block reduction of the dbias rows over the groups
   float* outp = dbias_part + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * F * F;
-  for (int j = 0; j < F; ++j) {
-    red[threadIdx.x] = (lane_ok && j < 32) ? dbacc[j] : 0.f;
-    __syncthreads();
-    if ((int)threadIdx.x < F) {
-      float s = 0.f;
-      for (int gg = 0; gg < G; ++gg) s += red[gg * F + threadIdx.x];
-      outp[threadIdx.x * F + j] = s;
-    }
-    __syncthreads();
+  for (int t = threadIdx.x; t < F * F; t += blockDim.x) {
+    const int ii = t / F, j = t % F;
+    float s = 0.f;
+    for (int gg = 0; gg < G; ++gg) s += sacc[(gg * F + ii) * 33 + j];
+    outp[t] = s;
   }
 }
 
@@ -245,20 +279,31 @@ __global__ void relpos_fwd_kernel(const float* __restrict__ table, float* __rest
   bias[t] = table[relpos_bucket(j - i, num_buckets, max_distance) * heads + h];
 }
 
-// dtable[bucket][h] (+)= sum over (i,j) with that bucket of sum over parts of dbias_part
-__global__ void relpos_bwd_kernel(const float* __restrict__ part, int nparts_per_h, int B, float* __restrict__ dtable,
-                                  int F, int heads, int num_buckets, int max_distance, int accumulate) {
+// stage 1: dbias[h][i][j] = sum over b and the pixel-block parts (one wave per element, fixed order)
+__global__ void dbias_sum_kernel(const float* __restrict__ part, float* __restrict__ dbias, int nparts_per_h, int B,
+                                 int F, int heads) {
+  const int t = blockIdx.x;  // element (h, i, j)
+  const int h = t / (F * F), r = t % (F * F);
+  float s = 0.f;
+  const int n = B * nparts_per_h;
+  for (int k = threadIdx.x; k < n; k += 64) {
+    const int b = k / nparts_per_h, kk = k - b * nparts_per_h;
+    s += part[((int64_t)(b * heads + h) * nparts_per_h + kk) * F * F + r];
+  }
+  s = wave_sum(s);
+  if (threadIdx.x == 0) dbias[t] = s;
+}
+
+// stage 2: dtable[bucket][h] (+)= sum over (i,j) with that bucket of dbias[h][i][j]
+__global__ void relpos_bwd_kernel(const float* __restrict__ dbias, float* __restrict__ dtable, int F, int heads,
+                                  int num_buckets, int max_distance, int accumulate) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= num_buckets * heads) return;
   const int bk = t / heads, h = t % heads;
   float s = 0.f;
   for (int i = 0; i < F; ++i)
-    for (int j = 0; j < F; ++j) {
-      if (relpos_bucket(j - i, num_buckets, max_distance) != bk) continue;
-      for (int b = 0; b < B; ++b)
-        for (int k = 0; k < nparts_per_h; ++k)
-          s += part[((int64_t)(b * heads + h) * nparts_per_h + k) * F * F + i * F + j];
-    }
+    for (int j = 0; j < F; ++j)
+      if (relpos_bucket(j - i, num_buckets, max_distance) == bk) s += dbias[(h * F + i) * F + j];
   dtable[t] = accumulate ? dtable[t] + s : s;
 }
 
@@ -308,7 +353,6 @@ __global__ __launch_bounds__(256) void sla_ctx_partial_kernel(const T* __restric
     l *= corr;
 #pragma unroll
     for (int x = 0; x < 4; ++x) acc[x] *= corr;
-    __syncthreads();
     for (int x = 0; x < SLA_TILE; ++x) {
       const float pexp = expf(sk[d][x] - mn);
       l += pexp;
@@ -344,16 +388,18 @@ __global__ void sla_ctx_combine_kernel(const float* __restrict__ pm, const float
 }
 
 // out[v][h*32+e] = sum_d ctx[f,h][d][e] * qs[d], qs = softmax_d(q) * scale
-// grid: x = voxel block (32 voxels x 8 heads = 256 threads), y = frame
+// grid: x = 64-voxel block, y = frame, z = head group of 4.  Wave w <-> head, lane <-> voxel, so
+// every context read is a wave-uniform LDS broadcast.
 template <typename T>
 __global__ __launch_bounds__(256) void sla_out_kernel(const T* __restrict__ qkv, const float* __restrict__ ctx,
                                                       T* __restrict__ out, int HW, float scale) {
-  __shared__ float sc[NH * DH * DH];
-  const int f = blockIdx.y;
-  for (int e = threadIdx.x; e < NH * DH * DH; e += 256) sc[e] = ctx[(int64_t)f * NH * DH * DH + e];
+  __shared__ __attribute__((aligned(16))) float sc[4 * DH * DH];
+  const int f = blockIdx.y, h0 = blockIdx.z * 4;
+  const float* src = ctx + ((int64_t)f * NH + h0) * DH * DH;
+  for (int e = threadIdx.x; e < 4 * DH * DH; e += 256) sc[e] = src[e];
   __syncthreads();
-  const int h = threadIdx.x & 7, vl = threadIdx.x >> 3;
-  const int p = blockIdx.x * 32 + vl;
+  const int w = threadIdx.x >> 6, h = h0 + w;
+  const int p = blockIdx.x * 64 + (threadIdx.x & 63);
   if (p >= HW) return;
   const int64_t v = (int64_t)f * HW + p;
   float q[32];
@@ -368,7 +414,7 @@ __global__ __launch_bounds__(256) void sla_out_kernel(const T* __restrict__ qkv,
   float o[32];
 #pragma unroll
   for (int e = 0; e < 32; ++e) o[e] = 0.f;
-  const float* C = sc + h * DH * DH;
+  const float* C = sc + w * DH * DH;
 #pragma unroll 4
   for (int d = 0; d < 32; ++d) {
     const float qd = q[d] * inv;
@@ -445,7 +491,7 @@ __global__ void sla_dctx_combine_kernel(const float* __restrict__ pd, const floa
   if (e == 0) cvec[(int64_t)fh * DH + d] = prod;
 }
 
-// per voxel, per head: dq, dk, dv
+// per voxel, per head: dq, dk, dv.  Same wave<->head / lane<->voxel mapping as sla_out.
 template <typename T>
 __global__ __launch_bounds__(256) void sla_bwd_voxel_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
                                                             const float* __restrict__ ctx,
@@ -453,21 +499,28 @@ __global__ __launch_bounds__(256) void sla_bwd_voxel_kernel(const T* __restrict_
                                                             const float* __restrict__ ml,
                                                             const float* __restrict__ cvec, T* __restrict__ dqkv,
                                                             int HW, float scale) {
-  __shared__ float sc[NH * DH * DH];
-  __shared__ float sdc[NH * DH * DH];
-  const int f = blockIdx.y;
-  for (int e = threadIdx.x; e < NH * DH * DH; e += 256) {
-    sc[e] = ctx[(int64_t)f * NH * DH * DH + e];
-    sdc[e] = dctx[(int64_t)f * NH * DH * DH + e];
+  __shared__ __attribute__((aligned(16))) float sc[4 * DH * DH];
+  __shared__ __attribute__((aligned(16))) float sdc[4 * DH * DH];
+  __shared__ float sm[4 * DH], sl[4 * DH], scv[4 * DH];
+  const int f = blockIdx.y, h0 = blockIdx.z * 4;
+  const int64_t base = ((int64_t)f * NH + h0) * DH * DH;
+  for (int e = threadIdx.x; e < 4 * DH * DH; e += 256) {
+    sc[e] = ctx[base + e];
+    sdc[e] = dctx[base + e];
+  }
+  if (threadIdx.x < 4 * DH) {
+    const int64_t fhd = ((int64_t)f * NH + h0) * DH + threadIdx.x;
+    sm[threadIdx.x] = ml[fhd * 2];
+    sl[threadIdx.x] = ml[fhd * 2 + 1];
+    scv[threadIdx.x] = cvec[fhd];
   }
   __syncthreads();
-  const int h = threadIdx.x & 7, vl = threadIdx.x >> 3;
-  const int p = blockIdx.x * 32 + vl;
+  const int w = threadIdx.x >> 6, h = h0 + w;
+  const int p = blockIdx.x * 64 + (threadIdx.x & 63);
   if (p >= HW) return;
   const int64_t v = (int64_t)f * HW + p;
-  const float* C = sc + h * DH * DH;
-  const float* DC = sdc + h * DH * DH;
-  const int64_t fh = (int64_t)f * NH + h;
+  const float* C = sc + w * DH * DH;
+  const float* DC = sdc + w * DH * DH;
   // ---- dq
   {
     float q[32], g[32];
@@ -481,12 +534,18 @@ __global__ __launch_bounds__(256) void sla_bwd_voxel_kernel(const T* __restrict_
     for (int d = 0; d < 32; ++d) { q[d] = expf(q[d] - mx); s += q[d]; }
     const float inv = 1.f / s;
     float dsm[32], dot = 0.f;
-#pragma unroll
+#pragma unroll 4
     for (int d = 0; d < 32; ++d) {
       q[d] *= inv;  // sm
       float t = 0.f;
 #pragma unroll
-      for (int e = 0; e < 32; ++e) t = fmaf(C[d * DH + e], g[e], t);
+      for (int e = 0; e < 32; e += 4) {
+        const f32x4 c4 = *reinterpret_cast<const f32x4*>(C + d * DH + e);
+        t = fmaf(c4[0], g[e], t);
+        t = fmaf(c4[1], g[e + 1], t);
+        t = fmaf(c4[2], g[e + 2], t);
+        t = fmaf(c4[3], g[e + 3], t);
+      }
       dsm[d] = scale * t;
       dot = fmaf(q[d], dsm[d], dot);
     }
@@ -504,15 +563,21 @@ __global__ __launch_bounds__(256) void sla_bwd_voxel_kernel(const T* __restrict_
     for (int e = 0; e < 32; ++e) dv[e] = 0.f;
 #pragma unroll 4
     for (int d = 0; d < 32; ++d) {
-      const float m = ml[(fh * DH + d) * 2], l = ml[(fh * DH + d) * 2 + 1];
-      const float ks = expf(k[d] - m) / l;
+      const float ks = expf(k[d] - sm[w * DH + d]) / sl[w * DH + d];
       float t = 0.f;
 #pragma unroll
-      for (int e = 0; e < 32; ++e) {
-        t = fmaf(DC[d * DH + e], vv[e], t);
-        dv[e] = fmaf(DC[d * DH + e], ks, dv[e]);
+      for (int e = 0; e < 32; e += 4) {
+        const f32x4 c4 = *reinterpret_cast<const f32x4*>(DC + d * DH + e);
+        t = fmaf(c4[0], vv[e], t);
+        t = fmaf(c4[1], vv[e + 1], t);
+        t = fmaf(c4[2], vv[e + 2], t);
+        t = fmaf(c4[3], vv[e + 3], t);
+        dv[e] = fmaf(c4[0], ks, dv[e]);
+        dv[e + 1] = fmaf(c4[1], ks, dv[e + 1]);
+        dv[e + 2] = fmaf(c4[2], ks, dv[e + 2]);
+        dv[e + 3] = fmaf(c4[3], ks, dv[e + 3]);
       }
-      dk[d] = ks * (t - cvec[fh * DH + d]);
+      dk[d] = ks * (t - scv[w * DH + d]);
     }
     store32(dqkv + v * QKV + INNER + h * DH, dk);
     store32(dqkv + v * QKV + 2 * INNER + h * DH, dv);
@@ -538,7 +603,7 @@ static int sla_chunk(int HW) {
 extern "C" {
 
 int cesm_rope_table(const float* freqs, float* rot, int F, hipStream_t stream) {
-  if (F > 128) return CESM_EINVAL;
+  if (F > 32) return CESM_EINVAL;
   rope_table_kernel<<<(unsigned)cdiv(F * 16, 256), 256, 0, stream>>>(freqs, rot, F);
   return cesm_launch_status();
 }
@@ -550,18 +615,19 @@ int cesm_relpos_fwd(const float* table, float* bias, int F, int heads, int num_b
   return cesm_launch_status();
 }
 
-int cesm_relpos_bwd(const float* part, int nparts_per_h, int B, float* dtable, int F, int heads, int num_buckets,
-                    int max_distance, int accumulate, hipStream_t stream) {
-  relpos_bwd_kernel<<<(unsigned)cdiv(num_buckets * heads, 64), 64, 0, stream>>>(
-      part, nparts_per_h, B, dtable, F, heads, num_buckets, max_distance, accumulate);
+int cesm_relpos_bwd(const float* part, int nparts_per_h, int B, float* dtable, float* ws, int F, int heads,
+                    int num_buckets, int max_distance, int accumulate, hipStream_t stream) {
+  dbias_sum_kernel<<<heads * F * F, 64, 0, stream>>>(part, ws, nparts_per_h, B, F, heads);
+  relpos_bwd_kernel<<<(unsigned)cdiv(num_buckets * heads, 64), 64, 0, stream>>>(ws, dtable, F, heads, num_buckets,
+                                                                                max_distance, accumulate);
   return cesm_launch_status();
 }
 
 // number of pixel blocks (grid.x) used by the temporal-attention kernels for HW pixels
 int cesm_tattn_nblk(int F, int HW) {
-  const int G = 256 / F;
+  const int G = TA_T / F;
   int64_t npb = cdiv(HW, G);
-  return (int)std::min<int64_t>(npb, 128);
+  return (int)std::min<int64_t>(npb, 256);
 }
 
 int cesm_tattn_fwd(int dtype, const void* qkv, const float* bias, const float* rot, void* out, float* lse, int B,
@@ -570,7 +636,7 @@ int cesm_tattn_fwd(int dtype, const void* qkv, const float* bias, const float* r
   dim3 grid(cesm_tattn_nblk(F, HW), B * NH);
   return dispatch_dt(dtype, [&](auto* tp) {
     using T = std::remove_pointer_t<decltype(tp)>;
-    tattn_fwd_kernel<T><<<grid, 256, 0, stream>>>((const T*)qkv, bias, rot, (T*)out, lse, F, HW, scale);
+    tattn_fwd_kernel<T><<<grid, TA_T, 0, stream>>>((const T*)qkv, bias, rot, (T*)out, lse, F, HW, scale);
   }) ?: cesm_launch_status();
 }
 
@@ -582,8 +648,8 @@ int cesm_tattn_bwd(int dtype, const void* qkv, const void* o, const void* dout, 
   dim3 grid(cesm_tattn_nblk(F, HW), B * NH);
   return dispatch_dt(dtype, [&](auto* tp) {
     using T = std::remove_pointer_t<decltype(tp)>;
-    tattn_bwd_kernel<T><<<grid, 256, 0, stream>>>((const T*)qkv, (const T*)o, (const T*)dout, lse, bias, rot,
-                                                  (T*)dqkv, dbias_part, F, HW, scale);
+    tattn_bwd_kernel<T><<<grid, TA_T, 0, stream>>>((const T*)qkv, (const T*)o, (const T*)dout, lse, bias, rot,
+                                                   (T*)dqkv, dbias_part, F, HW, scale);
   }) ?: cesm_launch_status();
 }
 
@@ -601,7 +667,8 @@ int cesm_sla_fwd(int dtype, const void* qkv, void* out, float* ctx, float* ml, f
     using T = std::remove_pointer_t<decltype(tp)>;
     sla_ctx_partial_kernel<T><<<dim3(nchunk, Nf * NH), 256, 0, stream>>>((const T*)qkv, pm, pl, pctx, HW, chunk);
     sla_ctx_combine_kernel<<<Nf * NH, 1024, 0, stream>>>(pm, pl, pctx, ctx, ml, nchunk);
-    sla_out_kernel<T><<<dim3((unsigned)cdiv(HW, 32), Nf), 256, 0, stream>>>((const T*)qkv, ctx, (T*)out, HW, scale);
+    sla_out_kernel<T><<<dim3((unsigned)cdiv(HW, 64), Nf, 2), 256, 0, stream>>>((const T*)qkv, ctx, (T*)out, HW,
+                                                                                scale);
   }) ?: cesm_launch_status();
 }
 
@@ -618,7 +685,7 @@ int cesm_sla_bwd(int dtype, const void* qkv, const void* dout, const float* ctx,
     sla_dctx_partial_kernel<T><<<dim3(nchunk, Nf * NH), 256, 0, stream>>>((const T*)qkv, (const T*)dout, pd, HW,
                                                                            chunk, scale);
     sla_dctx_combine_kernel<<<Nf * NH, 1024, 0, stream>>>(pd, ctx, dctx, cvec, nchunk);
-    sla_bwd_voxel_kernel<T><<<dim3((unsigned)cdiv(HW, 32), Nf), 256, 0, stream>>>(
+    sla_bwd_voxel_kernel<T><<<dim3((unsigned)cdiv(HW, 64), Nf, 2), 256, 0, stream>>>(
         (const T*)qkv, (const T*)dout, ctx, dctx, ml, cvec, (T*)dqkv, HW, scale);
   }) ?: cesm_launch_status();
 }

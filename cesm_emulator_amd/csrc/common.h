@@ -104,3 +104,18 @@ __device__ __forceinline__ float group_sum(float v, int width) {
 }
 
 static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// host-side switch for A/B runs of kernel variants (read once per process)
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+static inline bool getenv_flag(const char* name) {
+  static std::map<std::string, bool> cache;
+  auto it = cache.find(name);
+  if (it != cache.end()) return it->second;
+  const char* v = std::getenv(name);
+  const bool on = v && v[0] && std::strcmp(v, "0") != 0;
+  cache[name] = on;
+  return on;
+}

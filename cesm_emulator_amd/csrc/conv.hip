@@ -71,8 +71,10 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const T* __restrict__ x1,
   const int lane = tid & 63;
   const int wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
-  const int64_t m0 = (int64_t)blockIdx.x * BMP;
-  const int n0 = blockIdx.y * BN;
+  // grid.x = output-channel tile (fast): the Cout/BN blocks sharing one pixel tile run adjacently,
+  // so the im2col tile is re-read from L2 instead of HBM
+  const int64_t m0 = (int64_t)blockIdx.y * BMP;
+  const int n0 = blockIdx.x * BN;
   const int Cin = g.C1 + g.C2;
   const int csteps = Cin / BK;
   const int ksteps = g.KH * g.KW * csteps;
@@ -197,6 +199,143 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const T* __restrict__ x1,
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int co = n0 + wr * (BN / 2) + i * 16 + lg * 4;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (bias) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += bias[co + r];
+      }
+      if (co < g.Co1) {
+        if (res) {
+          float rv[4];
+          load4(res + m * g.Co1 + co, rv);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += rv[r];
+        }
+        store4(y1 + m * g.Co1 + co, v);
+      } else {
+        if (res2) {
+          float rv[4];
+          load4(res2 + m * Co2 + (co - g.Co1), rv);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += rv[r];
+        }
+        store4(y2 + m * Co2 + (co - g.Co1), v);
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// 3x3 / stride 1 / pad 1 conv (bf16): halo-tiled implicit GEMM.  Block = 8 x 32 output pixels of
+// one image x 64 output channels.  Per 32-channel input chunk the (8+2) x (32+2) input halo and
+// the 9 taps x 64 co weights are staged in LDS once and all 9 taps read shifted windows of the
+// halo (9x fewer input loads than im2col).  The next chunk is prefetched into registers while the
+// current one is consumed.  4 waves = 2 (co halves) x 2 (pixel halves of 4 rows).
+// ----------------------------------------------------------------------------------------
+constexpr int H3_TH = 8, H3_TW = 32;
+constexpr int H3_HH = H3_TH + 2, H3_HW = H3_TW + 2;
+constexpr int H3_NPIX = H3_HH * H3_HW;   // 340 halo pixels
+constexpr int H3_LD = 40;                // bf16 per LDS row (32 ch + 8 pad = 80 B)
+constexpr int H3_BN = 64;
+constexpr int H3_HVEC = H3_NPIX * 4;     // 16-B vectors in the halo tile
+constexpr int H3_WVEC = 9 * H3_BN * 4;   // 16-B vectors in the weight tile
+constexpr int H3_HPT = (H3_HVEC + 255) / 256;
+constexpr int H3_WPT = H3_WVEC / 256;
+
+__global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
+                                                              const bf16* __restrict__ w, const float* __restrict__ bias,
+                                                              const bf16* __restrict__ res, const bf16* __restrict__ res2,
+                                                              bf16* __restrict__ y1, bf16* __restrict__ y2, ConvGeom g,
+                                                              int tiles_x) {
+  __shared__ __attribute__((aligned(16))) bf16 sh[H3_NPIX * H3_LD];
+  __shared__ __attribute__((aligned(16))) bf16 sw[9 * H3_BN * H3_LD];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int n = blockIdx.y;
+  const int ty = blockIdx.x / tiles_x, tx = blockIdx.x - ty * tiles_x;
+  const int y0 = ty * H3_TH, x0 = tx * H3_TW;
+  const int n0 = blockIdx.z * H3_BN;
+  const int Cin = g.C1 + g.C2;
+  const int nchunk = Cin / 32;
+
+  // stage one 32-channel chunk: global -> registers -> LDS (transient registers; the second
+  // co-resident block computes while this one loads)
+  auto stage = [&](int ch) {
+    const int c0 = ch * 32;
+    const bf16* src;
+    int cs, cc;
+    if (c0 < g.C1) { src = x1; cs = g.C1; cc = c0; } else { src = x2; cs = g.C2; cc = c0 - g.C1; }
+    bf16x8 hreg[H3_HPT], wreg[H3_WPT];
+#pragma unroll
+    for (int k = 0; k < H3_HPT; ++k) {
+      const int e = tid + k * 256;
+      bf16x8 v = {};
+      if (e < H3_HVEC) {
+        const int hp = e >> 2, part = e & 3;
+        const int r = hp / H3_HW, c = hp - r * H3_HW;
+        const int iy = y0 - 1 + r, ix = x0 - 1 + c;
+        if ((unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi)
+          v = *reinterpret_cast<const bf16x8*>(src + (((int64_t)n * g.Hi + iy) * g.Wi + ix) * cs + cc + part * 8);
+      }
+      hreg[k] = v;
+    }
+#pragma unroll
+    for (int k = 0; k < H3_WPT; ++k) {
+      const int e = tid + k * 256;
+      const int row = e >> 2, part = e & 3;      // row = tap*BN + co
+      const int tap = row / H3_BN, co = row - tap * H3_BN;
+      wreg[k] = *reinterpret_cast<const bf16x8*>(w + ((int64_t)(n0 + co) * 9 + tap) * Cin + c0 + part * 8);
+    }
+#pragma unroll
+    for (int k = 0; k < H3_HPT; ++k) {
+      const int e = tid + k * 256;
+      if (e < H3_HVEC) *reinterpret_cast<bf16x8*>(sh + (e >> 2) * H3_LD + (e & 3) * 8) = hreg[k];
+    }
+#pragma unroll
+    for (int k = 0; k < H3_WPT; ++k) {
+      const int e = tid + k * 256;
+      *reinterpret_cast<bf16x8*>(sw + (e >> 2) * H3_LD + (e & 3) * 8) = wreg[k];
+    }
+  };
+
+  f32x4 acc[2][8];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int lr = lane & 15, lg = lane >> 4;
+  for (int ch = 0; ch < nchunk; ++ch) {
+    if (ch) __syncthreads();  // previous chunk fully consumed
+    stage(ch);
+    __syncthreads();
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int ky = tap / 3, kx = tap - ky * 3;
+      bf16x8 af[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(sw + (tap * H3_BN + wr * 32 + i * 16 + lr) * H3_LD + lg * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int py = wc * 4 + (j >> 1), px = (j & 1) * 16 + lr;
+        const bf16x8 bfr =
+            *reinterpret_cast<const bf16x8*>(sh + ((py + ky) * H3_HW + px + kx) * H3_LD + lg * 8);
+        acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bfr, acc[0][j], 0, 0, 0);
+        acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bfr, acc[1][j], 0, 0, 0);
+      }
+    }
+  }
+  // epilogue: lane holds co = n0 + wr*32 + i*16 + 4*lg + r of pixel (py, px)
+  const int Co2 = g.Cout - g.Co1;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int oy = y0 + wc * 4 + (j >> 1), ox = x0 + (j & 1) * 16 + lr;
+    if (oy >= g.Ho || ox >= g.Wo) continue;
+    const int64_t m = ((int64_t)n * g.Ho + oy) * g.Wo + ox;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int co = n0 + wr * 32 + i * 16 + lg * 4;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       if (bias) {
 #pragma unroll
@@ -394,6 +533,140 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const T* __restrict__ x
     }
 }
 
+// ----------------------------------------------------------------------------------------
+// 3x3 / stride 1 / pad 1 weight gradient (bf16), halo-tiled.  Block = (64 co) x (32 ci chunk) x
+// all 9 taps, looping over 8x32-pixel tiles (its share of the split-K over pixels).  Per tile the
+// dY tile [256 px][64 co] and the input halo [10x34 px][32 ci] are staged in LDS; pixels are the
+// MFMA K axis, so both operands are read transposed with ds_read_b64_tr_b16 from XOR-swizzled
+// rows (conflict-free).  Wave w: co tiles {2*(w>>1), 2*(w>>1)+1} x ci tile (w&1) x 9 taps.
+// ----------------------------------------------------------------------------------------
+constexpr int W3_TH = 8, W3_TW = 32;
+constexpr int W3_HW = W3_TW + 2, W3_NPIX = (W3_TH + 2) * (W3_TW + 2);
+
+__device__ __forceinline__ int w3_swz_dy(int r) { return (((r >> 1) & 1) << 2) | (((r >> 3) & 1) << 3); }
+__device__ __forceinline__ int w3_swz_x(int r) { return ((r >> 3) & 1) << 2; }
+
+__global__ __launch_bounds__(256, 2) void wgrad3x3_bf16_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
+                                                               const bf16* __restrict__ dy1, const bf16* __restrict__ dy2,
+                                                               float* __restrict__ slab, ConvGeom g, int tiles_x,
+                                                               int ntiles) {
+  __shared__ __attribute__((aligned(16))) bf16 sdy[W3_TH * W3_TW * 64];   // 32 KB, 128-B rows
+  __shared__ __attribute__((aligned(16))) bf16 shx[W3_NPIX * 32];         // 21.3 KB, 64-B rows
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int cot0 = (wid >> 1) * 2, cit = wid & 1;
+  const int co0 = blockIdx.x * 64, ci0 = blockIdx.y * 32;
+  const int Cin = g.C1 + g.C2;
+  const bf16* xs; int xcs, xcc;
+  if (ci0 < g.C1) { xs = x1; xcs = g.C1; xcc = ci0; } else { xs = x2; xcs = g.C2; xcc = ci0 - g.C1; }
+  const bf16* ys; int ycs, ycc;
+  const int Co2 = g.Cout - g.Co1;
+  if (co0 < g.Co1) { ys = dy1; ycs = g.Co1; ycc = co0; } else { ys = dy2; ycs = Co2; ycc = co0 - g.Co1; }
+  const int tiles_per_img = tiles_x * ((g.Ho + W3_TH - 1) / W3_TH);
+
+  f32x4 acc[2][9];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int lr = lane & 15, lg = lane >> 4, q = lr >> 2, pp = lr & 3;
+  for (int tile = blockIdx.z; tile < ntiles; tile += gridDim.z) {
+    const int n = tile / tiles_per_img;
+    const int rem = tile - n * tiles_per_img;
+    const int ty = rem / tiles_x, tx = rem - ty * tiles_x;
+    const int y0 = ty * W3_TH, x0 = tx * W3_TW;
+    __syncthreads();
+    {
+      bf16x8 yv[8], hv[6];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {       // dY: 256 px x 8 vectors
+        const int e = tid + k * 256;
+        const int p = e >> 3, part = e & 7;
+        const int oy = y0 + (p >> 5), ox = x0 + (p & 31);
+        bf16x8 v = {};
+        if (oy < g.Ho && ox < g.Wo)
+          v = *reinterpret_cast<const bf16x8*>(ys + (((int64_t)n * g.Ho + oy) * g.Wo + ox) * ycs + ycc + part * 8);
+        yv[k] = v;
+      }
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {       // halo: 340 px x 4 vectors
+        const int e = tid + k * 256;
+        bf16x8 v = {};
+        if (e < W3_NPIX * 4) {
+          const int hp = e >> 2, part = e & 3;
+          const int r = hp / W3_HW, c = hp - r * W3_HW;
+          const int iy = y0 - 1 + r, ix = x0 - 1 + c;
+          if ((unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi)
+            v = *reinterpret_cast<const bf16x8*>(xs + (((int64_t)n * g.Hi + iy) * g.Wi + ix) * xcs + xcc + part * 8);
+        }
+        hv[k] = v;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int e = tid + k * 256;
+        const int p = e >> 3, part = e & 7;  // chunk pair (2part, 2part+1) of 8-B chunks
+        const int ch = (part * 2) ^ w3_swz_dy(p);
+        *reinterpret_cast<bf16x8*>(sdy + p * 64 + ch * 4) = yv[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const int e = tid + k * 256;
+        if (e < W3_NPIX * 4) {
+          const int hp = e >> 2, part = e & 3;
+          const int ch = (part * 2) ^ w3_swz_x(hp);
+          *reinterpret_cast<bf16x8*>(shx + hp * 32 + ch * 4) = hv[k];
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int py = 0; py < W3_TH; ++py) {
+      // A = dY^T (rows co, K = 32 pixels of row py): tr reads, rows = pixel py*32 + k
+      bf16x8 af[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const int r = py * 32 + lg * 8 + half * 4 + q;
+          const int ch = ((cot0 + i) * 4 + pp) ^ w3_swz_dy(r);
+          const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(sdy + r * 64 + ch * 4));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) af[i][half * 4 + e] = __builtin_bit_cast(bf16, (short)v[e]);
+        }
+      }
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int ky = tap / 3, kx = tap - ky * 3;
+        bf16x8 bfr;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const int r = (py + ky) * W3_HW + lg * 8 + half * 4 + q + kx;
+          const int ch = (cit * 4 + pp) ^ w3_swz_x(r);
+          const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(shx + r * 32 + ch * 4));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bfr[half * 4 + e] = __builtin_bit_cast(bf16, (short)v[e]);
+        }
+        acc[0][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bfr, acc[0][tap], 0, 0, 0);
+        acc[1][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bfr, acc[1][tap], 0, 0, 0);
+      }
+    }
+  }
+  // D[co][ci] per tap: lane col lr -> ci, rows 4lg+r -> co
+  const int K = 9 * Cin;
+  float* out = slab + (int64_t)blockIdx.z * g.Cout * K;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int ci = ci0 + cit * 16 + lr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + (cot0 + i) * 16 + lg * 4 + r;
+        out[(int64_t)co * K + tap * Cin + ci] = acc[i][tap][r];
+      }
+    }
+}
+
 // sum slabs over splits (fixed order) and scatter into the PyTorch weight layout
 // dst[((d0*D1 + d1)*KH + kyt)*KW + kxt], with (d0,d1) = swap ? (ci,co) : (co,ci) and
 // (kyt,kxt) = flip ? (KH-1-ky, KW-1-kx) : (ky,kx).
@@ -462,13 +735,14 @@ __global__ void colsum_partial_kernel(const T* __restrict__ x, float* __restrict
   }
 }
 
+// one 64-lane wave per channel: lanes stride over the splits, then a fixed-order wave sum
 __global__ void colsum_final_kernel(const float* __restrict__ part, float* __restrict__ dst, int nsplit, int C,
                                     int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+  const int c = blockIdx.x;
   float s = 0.f;
-  for (int k = 0; k < nsplit; ++k) s += part[(int64_t)k * C + c];
-  dst[c] = accumulate ? dst[c] + s : s;
+  for (int k = threadIdx.x; k < nsplit; k += 64) s += part[(int64_t)k * C + c];
+  s = wave_sum(s);
+  if (threadIdx.x == 0) dst[c] = accumulate ? dst[c] + s : s;
 }
 
 // ----------------------------------------------------------------------------------------
@@ -538,7 +812,20 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(const float* __restrict
   const int co = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int tpg = (KK + 3) / 4;
   float acc[25];
-  for (int i = 0; i < 25; ++i) acc[i] = 0.f;
+  int toff[25];  // LDS offset of each of this thread's taps (-1: none), hoisted out of the pixel loop
+#pragma unroll
+  for (int i = 0; i < 25; ++i) {
+    acc[i] = 0.f;
+    const int kk = grp * tpg + i;
+    if (i < tpg && kk < KK) {
+      const int ci = kk / (KS * KS), r = kk - ci * KS * KS;
+      const int ky = r / KS, kx = r - ky * KS;
+      toff[i] = ci * (14 * 38) + ky * IW + kx;
+    } else {
+      toff[i] = -1;
+    }
+  }
+  const float* tinf = &tin[0][0];
   const int tx_tiles = (W + TWD - 1) / TWD, ty_tiles = (H + TH - 1) / TH;
   const int per_img = tx_tiles * ty_tiles;
   const int cog = blockIdx.y * 64;
@@ -562,19 +849,14 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(const float* __restrict
       tdy[p * 65 + c] = (yy < H && xx < W) ? to_f(dy[(((int64_t)n * H + yy) * W + xx) * Co + cog + c]) : 0.f;
     }
     __syncthreads();
-    for (int p = 0; p < TH * TWD; ++p) {
-      const float g = tdy[p * 65 + co];
-      const int py = p / TWD, px = p % TWD;
+    for (int py = 0; py < TH; ++py)
+      for (int px = 0; px < TWD; ++px) {
+        const float g = tdy[(py * TWD + px) * 65 + co];
+        const int base = py * IW + px;
 #pragma unroll
-      for (int i = 0; i < 25; ++i) {
-        const int kk = grp * tpg + i;
-        if (i < tpg && kk < KK) {
-          const int ci = kk / (KS * KS), r = kk - ci * KS * KS;
-          const int ky = r / KS, kx = r - ky * KS;
-          acc[i] = fmaf(g, tin[ci][(py + ky) * IW + px + kx], acc[i]);
-        }
+        for (int i = 0; i < 25; ++i)
+          if (toff[i] >= 0) acc[i] = fmaf(g, tinf[toff[i] + base], acc[i]);
       }
-    }
   }
   for (int i = 0; i < tpg; ++i) {
     const int kk = grp * tpg + i;
@@ -689,8 +971,15 @@ int cesm_conv_fwd(int dtype, const void* x1, const void* x2, const void* wp, con
   ConvGeom g{Nb, Hi, Wi, Ho, Wo, C1, C2, Cout, Co1, KH, KW, S, P, U};
   const int64_t M = (int64_t)Nb * Ho * Wo;
   const int BN = (Cout % 128 == 0) ? 128 : 64;
-  dim3 grid((unsigned)cdiv(M, BMP), Cout / BN);
-  if (dtype == CESM_DT_BF16) {
+  dim3 grid(Cout / BN, (unsigned)cdiv(M, BMP));
+  const bool halo3 = dtype == CESM_DT_BF16 && KH == 3 && KW == 3 && S == 1 && P == 1 && U == 1 && Ho == Hi &&
+                     Wo == Wi && (Co1 % H3_BN) == 0 && !getenv_flag("CESM_NO_HALO");
+  if (halo3) {
+    const int tx = (int)cdiv(Wo, H3_TW), ty = (int)cdiv(Ho, H3_TH);
+    dim3 g3(tx * ty, Nb, Cout / H3_BN);
+    conv3x3_bf16_kernel<<<g3, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
+                                                (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, tx);
+  } else if (dtype == CESM_DT_BF16) {
     if (BN == 128)
       conv_fwd_kernel<bf16, 128><<<grid, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
                                                            (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, M);
@@ -725,7 +1014,16 @@ int cesm_conv_wgrad(int dtype, const void* x1, const void* x2, const void* dy1, 
   const int64_t pps = cdiv(cdiv(M, nsplit), WG_BP) * WG_BP;
   const int K = KH * KW * Cin;
   dim3 grid(Cout / 64, K / 64, nsplit);
-  if (dtype == CESM_DT_BF16)
+  const bool halo3 = dtype == CESM_DT_BF16 && KH == 3 && KW == 3 && S == 1 && P == 1 && U == 1 && Ho == Hi &&
+                     Wo == Wi && !getenv_flag("CESM_NO_HALO");
+  if (halo3) {
+    const int tx = (int)cdiv(Wo, W3_TW);
+    const int ntiles = Nb * tx * (int)cdiv(Ho, W3_TH);
+    dim3 g3(Cout / 64, Cin / 32, std::min(nsplit, ntiles));
+    wgrad3x3_bf16_kernel<<<g3, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
+                                                 (const bf16*)dy2, slab, g, tx, ntiles);
+    nsplit = (int)g3.z;
+  } else if (dtype == CESM_DT_BF16)
     conv_wgrad_kernel<bf16><<<grid, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
                                                       (const bf16*)dy2, slab, g, M, pps);
   else if (dtype == CESM_DT_F32)
@@ -763,7 +1061,7 @@ int cesm_colsum(int dtype, const void* x, float* dst, float* part, int nsplit, i
     colsum_partial_kernel<float><<<nsplit, 256, 0, stream>>>((const float*)x, part, rows, C, rps);
   else
     return CESM_EINVAL;
-  colsum_final_kernel<<<(unsigned)cdiv(C, 256), 256, 0, stream>>>(part, dst, nsplit, C, accumulate);
+  colsum_final_kernel<<<C, 64, 0, stream>>>(part, dst, nsplit, C, accumulate);
   return cesm_launch_status();
 }
 

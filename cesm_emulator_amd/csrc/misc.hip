@@ -39,16 +39,25 @@ __global__ void linear_small_fwd_kernel(const float* __restrict__ x, const float
 }
 
 // dx[r][i] (+)= act'(x) * sum_o dy[r][o] W[o][i]
+// block = 4 waves x 64 lanes: lane <-> i (64 consecutive), wave <-> quarter of the o range
 __global__ void linear_small_dx_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                        const float* __restrict__ dy, float* __restrict__ dx, int R, int I, int O,
                                        int silu_in, int accumulate) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= R * I) return;
-  const int r = t / I, i = t % I;
+  __shared__ float red[4][64];
+  const int r = blockIdx.y;
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int wv = threadIdx.x >> 6;
   float s = 0.f;
-  for (int o = 0; o < O; ++o) s = fmaf(dy[(int64_t)r * O + o], w[(int64_t)o * I + i], s);
-  if (silu_in) s *= dsilu_p(x[t]);
-  dx[t] = accumulate ? dx[t] + s : s;
+  if (i < I)
+    for (int o = wv; o < O; o += 4) s = fmaf(dy[(int64_t)r * O + o], w[(int64_t)o * I + i], s);
+  red[wv][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (wv == 0 && i < I) {
+    s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    const int64_t t = (int64_t)r * I + i;
+    if (silu_in) s *= dsilu_p(x[t]);
+    dx[t] = accumulate ? dx[t] + s : s;
+  }
 }
 
 // dW[o][i] (+)= sum_r dy[r][o] act(x[r][i]); db[o] (+)= sum_r dy[r][o]
@@ -241,8 +250,8 @@ int cesm_linear_small_fwd(const float* x, const float* w, const float* bias, flo
 int cesm_linear_small_bwd(const float* x, const float* w, const float* dy, float* dx, float* dw, float* db, int R,
                           int I, int O, int silu_in, int accumulate_dx, int accumulate_w, hipStream_t stream) {
   if (dx)
-    linear_small_dx_kernel<<<(unsigned)cdiv(R * I, 256), 256, 0, stream>>>(x, w, dy, dx, R, I, O, silu_in,
-                                                                           accumulate_dx);
+    linear_small_dx_kernel<<<dim3((unsigned)cdiv(I, 64), R), 256, 0, stream>>>(x, w, dy, dx, R, I, O, silu_in,
+                                                                               accumulate_dx);
   if (dw)
     linear_small_dw_kernel<<<(unsigned)cdiv((int64_t)O * I, 256), 256, 0, stream>>>(x, dy, dw, db, R, I, O, silu_in,
                                                                                     accumulate_w);

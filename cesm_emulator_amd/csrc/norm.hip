@@ -333,13 +333,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
   }
 }
 
+// one 64-lane wave per channel, fixed-order reduction
 __global__ void sum_rows_kernel(const float* __restrict__ part, float* __restrict__ dst, int nrows, int C,
                                 int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+  const int c = blockIdx.x;
   float s = 0.f;
-  for (int k = 0; k < nrows; ++k) s += part[(int64_t)k * C + c];
-  dst[c] = accumulate ? dst[c] + s : s;
+  for (int k = threadIdx.x; k < nrows; k += 64) s += part[(int64_t)k * C + c];
+  s = wave_sum(s);
+  if (threadIdx.x == 0) dst[c] = accumulate ? dst[c] + s : s;
 }
 
 template <typename F>
@@ -442,7 +443,7 @@ int cesm_ln_bwd(int dtype, const void* dy, const void* x, const float* mr, const
     ln_bwd_kernel<T><<<nblk, 256, 0, stream>>>((const T*)dy, (const T*)x, mr, gamma, (const T*)dres, (T*)dx, part, V, C);
   });
   if (rc) return rc;
-  if (dgamma) sum_rows_kernel<<<(unsigned)cdiv(C, 256), 256, 0, stream>>>(part, dgamma, nblk, C, accumulate);
+  if (dgamma) sum_rows_kernel<<<C, 64, 0, stream>>>(part, dgamma, nblk, C, accumulate);
   return cesm_launch_status();
 }
 

@@ -233,7 +233,8 @@ def tattn_bwd(qkv, o, dout, lse, bias, rot, dtable, B, F, HW, scale, num_buckets
     call("cesm_tattn_bwd", dtcode(qkv), P(qkv), P(o), P(dout), P(lse), P(bias), P(rot), P(dqkv), P(part), B, F, HW,
          float(scale), S())
     if dtable is not None:
-        call("cesm_relpos_bwd", P(part), nblk, B, P(dtable), F, 8, num_buckets, max_distance, 1, S())
+        ws = empty((8, F, F), torch.float32, qkv.device)
+        call("cesm_relpos_bwd", P(part), nblk, B, P(dtable), P(ws), F, 8, num_buckets, max_distance, 1, S())
     return dqkv
 
 

@@ -84,8 +84,8 @@ int cesm_rope_table(const float* freqs, float* rot, int F, hipStream_t stream);
 /* RelativePositionBias (video_net.py:268-310): bias[h][i][j] = table[bucket(j-i)][h] and backward. */
 int cesm_relpos_fwd(const float* table, float* bias, int F, int heads, int num_buckets, int max_distance,
                     hipStream_t stream);
-int cesm_relpos_bwd(const float* part, int nparts_per_h, int B, float* dtable, int F, int heads, int num_buckets,
-                    int max_distance, int accumulate, hipStream_t stream);
+int cesm_relpos_bwd(const float* part, int nparts_per_h, int B, float* dtable, float* ws, int F, int heads,
+                    int num_buckets, int max_distance, int accumulate, hipStream_t stream);
 /* temporal attention core (video_net.py:401-453 between to_qkv and to_out), qkv [V][768] -> out [V][256] */
 int cesm_tattn_nblk(int F, int HW);
 int cesm_tattn_fwd(int dtype, const void* qkv, const float* bias, const float* rot, void* out, float* lse, int B,
