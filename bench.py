@@ -191,7 +191,7 @@ def main():
         ach = avg_flops / (avg_ms * 1e-3) / 1e12
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(ach / peak, 4), "traffic": None,
-                "kernel": "conv_fwd_kernel<bf16,64> (level-0 3x3 conv 64->64)" if a.dtype == "bf16" else
+                "kernel": "conv3x3_bf16_kernel (level-0 3x3 conv 64->64, fwd+dgrad)" if a.dtype == "bf16" else
                           "conv_fwd_kernel<float,64>", "launches": n, "avg_us": round(avg_ms * 1e3, 2),
                 "flop_per_launch": avg_flops}
     out = {
