@@ -161,7 +161,9 @@ def gn_apply(y, stats, gamma, beta, ss, res, B, G):
     rows_b = y.numel() // (C * B)
     out = empty(y.shape, y.dtype, y.device)
     _chk(res, y.shape, y.dtype)
-    call("cesm_gn_apply", dtcode(y), P(y), P(stats), P(gamma), P(beta), P(ss), P(res), P(out), B, rows_b, C, G, S())
+    ws = empty((2 * B * C,), torch.float32, y.device)
+    call("cesm_gn_apply", dtcode(y), P(y), P(stats), P(gamma), P(beta), P(ss), P(res), P(out), P(ws), B, rows_b, C,
+         G, S())
     return out
 
 
@@ -170,7 +172,7 @@ def gn_bwd(dout, y, stats, gamma, beta, ss, dgamma, dbeta, B, G, want_dss):
     rows_b = y.numel() // (C * B)
     dy = empty(y.shape, y.dtype, y.device)
     dss = empty((B, 2 * C), torch.float32, y.device) if want_dss else None
-    ws = empty((B * 256 * C * 2 + B * C * 2 + B * G * 2,), torch.float32, y.device)
+    ws = empty((B * 256 * C * 2 + B * C * 2 + B * C * 5,), torch.float32, y.device)
     call("cesm_gn_bwd", dtcode(y), P(dout), P(y), P(stats), P(gamma), P(beta), P(ss), P(dy), P(dss), P(dgamma),
          P(dbeta), P(ws), B, rows_b, C, G, 1, S())
     return dy, dss
@@ -236,6 +238,23 @@ def tattn_bwd(qkv, o, dout, lse, bias, rot, dtable, B, F, HW, scale, num_buckets
         ws = empty((8, F, F), torch.float32, qkv.device)
         call("cesm_relpos_bwd", P(part), nblk, B, P(dtable), P(ws), F, 8, num_buckets, max_distance, 1, S())
     return dqkv
+
+
+TBLOCK_C = (64, 128, 256, 512)
+
+
+def tblock_fwd(x, gamma, wqkv, wout, bias, rot, B, F, scale, save=True, eps=1e-5):
+    """fused temporal-attention block forward (bf16); x [B*F, H, W, C]"""
+    Nb, H, W, C = x.shape
+    _chk(x, dtype=torch.bfloat16)
+    _chk(wqkv, (768, C), torch.bfloat16)
+    _chk(wout, (C, 256), torch.bfloat16)
+    y = empty(x.shape, x.dtype, x.device)
+    mr = empty((Nb * H * W, 2), torch.float32, x.device) if save else None
+    lse = empty((B, 8, H * W, F), torch.float32, x.device) if save else None
+    call("cesm_tblock_fwd", P(x), P(gamma), P(wqkv), P(wout), P(bias), P(rot), P(y), P(mr), P(lse), B, F, H * W, C,
+         float(scale), float(eps), S())
+    return y, mr, lse
 
 
 def sla_fwd(qkv, Nf, HW, scale):

@@ -66,7 +66,7 @@ int cesm_head_bwd(int dtype, const float* dout, const void* x, const float* w, v
 int cesm_gn_stats(int dtype, const void* y, float* stats, double* ws, int B, int64_t rows_b, int C, int G, float eps,
                   hipStream_t stream);
 int cesm_gn_apply(int dtype, const void* y, const float* stats, const float* gamma, const float* beta,
-                  const float* ss, const void* res, void* out, int B, int64_t rows_b, int C, int G,
+                  const float* ss, const void* res, void* out, float* ws, int B, int64_t rows_b, int C, int G,
                   hipStream_t stream);
 int cesm_gn_bwd(int dtype, const void* dout, const void* y, const float* stats, const float* gamma,
                 const float* beta, const float* ss, void* dy, float* dss, float* dgamma, float* dbeta, float* ws,
@@ -93,6 +93,13 @@ int cesm_tattn_fwd(int dtype, const void* qkv, const float* bias, const float* r
 int cesm_tattn_bwd(int dtype, const void* qkv, const void* o, const void* dout, const float* lse, const float* bias,
                    const float* rot, void* dqkv, float* dbias_part, int B, int F, int HW, float scale,
                    hipStream_t stream);
+/* Fused temporal-attention block forward, bf16 (csrc/tblock.hip): y = x + Residual(PreNorm(Attention))
+ * (video_net.py:69-98, :350-454) with LN, QKV GEMM, RoPE, MFMA core, out-proj in one kernel; x,y
+ * [B*F*HW][C], wqkv [768][C], wout [C][256] packed bf16; saves mr [B*F*HW][2] and lse [B][8][HW][F].
+ * F <= 16, C in {64,128,256,512}. */
+int cesm_tblock_fwd(const void* x, const float* gamma, const void* wqkv, const void* wout, const float* bias,
+                    const float* rot, void* y, float* mr, float* lse, int B, int F, int HW, int C, float scale,
+                    float eps, hipStream_t stream);
 /* spatial linear attention core (video_net.py:335-345 between to_qkv and to_out) */
 int cesm_sla_nchunk(int HW);
 int cesm_sla_fwd(int dtype, const void* qkv, void* out, float* ctx, float* ml, float* ws, int Nf, int HW, float scale,
