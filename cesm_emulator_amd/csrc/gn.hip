@@ -34,6 +34,7 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const T* __restrict__ y, 
   const T* base = y + (int64_t)b * rows_b * C;
   float s = 0.f, ss = 0.f;
   if (rr < rl) {
+#pragma unroll 4
     for (int64_t r = r0 + rr; r < r1; r += rl) {
       float v[8];
       load8(base + r * C + c8 * 8, v);
@@ -47,9 +48,9 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const T* __restrict__ y, 
   __syncthreads();
   if (tid < G) {
     double a = 0.0, q = 0.0;
-    for (int t = 0; t < rl * cv; ++t) {
-      if (((t % cv) * 8) / gsz == tid) { a += red[t][0]; q += red[t][1]; }
-    }
+    const int g8 = gsz / 8;  // 8-channel groups per GroupNorm group (gsz % 8 == 0 checked on host)
+    for (int k = 0; k < rl; ++k)
+      for (int c = tid * g8; c < (tid + 1) * g8; ++c) { a += red[k * cv + c][0]; q += red[k * cv + c][1]; }
     double* o = part + (((int64_t)b * nchunk + chunk) * G + tid) * 2;
     o[0] = a;
     o[1] = q;
@@ -113,6 +114,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ y, 
   const int64_t rpc = (rows_b + nchunk - 1) / nchunk;
   const int64_t r0 = chunk * rpc, r1 = min(rows_b, r0 + rpc);
   const int64_t off = (int64_t)b * rows_b * C + c8 * 8;
+#pragma unroll 4
   for (int64_t r = r0 + rr; r < r1; r += rl) {
     float v[8], rv[8];
     load8(y + off + r * C, v);
@@ -143,6 +145,7 @@ __global__ __launch_bounds__(256) void gn_bwd_reduce_kernel(const T* __restrict_
   const int64_t off = (int64_t)b * rows_b * C + c8 * 8;
   float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (rr < rl) {
+#pragma unroll 4
     for (int64_t r = r0 + rr; r < r1; r += rl) {
       float v[8], d[8];
       load8(y + off + r * C, v);
@@ -251,6 +254,7 @@ __global__ __launch_bounds__(256) void gn_bwd_apply_kernel(const T* __restrict__
   const int64_t rpc = (rows_b + nchunk - 1) / nchunk;
   const int64_t r0 = chunk * rpc, r1 = min(rows_b, r0 + rpc);
   const int64_t off = (int64_t)b * rows_b * C + c8 * 8;
+#pragma unroll 4
   for (int64_t r = r0 + rr; r < r1; r += rl) {
     float v[8], d[8];
     load8(y + off + r * C, v);

@@ -219,6 +219,1043 @@ __global__ __launch_bounds__(256) void tblock_fwd_kernel(const bf16* __restrict_
   }
 }
 
+// ============================================================================================
+// Backward (dx path).  Per block: P_b pixels x F frames; loops over pixel groups (grid-stride) so
+// the rel-pos-bias and LN-gamma gradient partials stay per block.  Per head h:
+//   recompute [q'|k'|v]_h (as forward) and dO_h = dy . W_out[:, h]   (MFMA)
+//   per pixel (MFMA, frames padded to 16):
+//     S^T, P^T = exp(S^T + bias - lse), dP^T = V dO^T, D_i = sum_j P dP, dS^T = P^T (dP^T - D)
+//     dQ'^T = K'^T dS^T ; O^T = V^T P^T ;  S, P, dP, dS (row-major orientation)
+//     dK'^T = Q'^T dS ; dV^T = dO^T P       (k-slot trick: slot (g, e<4) <-> frame 4g+e)
+//   dq = scale R^T dQ', dk = R^T dK' ; dxn += [dq|dk|dv] . W_qkv[h rows]   (MFMA, registers)
+// then LN backward (+ residual dy) -> dx.  dqkv, O and xn are also written (bf16) for the two
+// weight-gradient GEMMs.
+// ============================================================================================
+template <int C>
+struct TBB {
+  static constexpr int P = C >= 256 ? 1 : 256 / C;
+  static constexpr int VPMAX = P * 16;
+  static constexpr int XLD = C + 8;
+  static constexpr int CT = C / 16;
+  static constexpr int MAXT = (CT * (VPMAX / 16) + 3) / 4;
+};
+
+template <int C>
+__global__ __launch_bounds__(256) void tblock_bwd_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ dy, const float* __restrict__ gamma,
+    const float* __restrict__ mr, const float* __restrict__ lse, const bf16* __restrict__ wqkv,
+    const bf16* __restrict__ wqkv_t, const bf16* __restrict__ wout_t, const float* __restrict__ bias,
+    const float* __restrict__ rotg, bf16* __restrict__ dx, bf16* __restrict__ dqkv_out, bf16* __restrict__ o_out,
+    bf16* __restrict__ xn_out, float* __restrict__ dbias_part, float* __restrict__ dgamma_part, int F, int HW,
+    float scale) {
+  using T = TBB<C>;
+  __shared__ __attribute__((aligned(16))) bf16 xn[T::VPMAX * T::XLD];
+  __shared__ __attribute__((aligned(16))) bf16 dyl[T::VPMAX * T::XLD];
+  __shared__ __attribute__((aligned(16))) bf16 sq[T::VPMAX * HLD];
+  __shared__ __attribute__((aligned(16))) bf16 sk[T::VPMAX * HLD];
+  __shared__ __attribute__((aligned(16))) bf16 sv[T::VPMAX * HLD];
+  __shared__ __attribute__((aligned(16))) bf16 sdo[T::VPMAX * HLD];
+  __shared__ __attribute__((aligned(16))) bf16 sdq[T::VPMAX * HLD];
+  __shared__ __attribute__((aligned(16))) bf16 sdk[T::VPMAX * HLD];
+  __shared__ __attribute__((aligned(16))) bf16 sdv[T::VPMAX * HLD];
+  __shared__ float sb[NH * 16 * 16];
+  __shared__ float rot[16 * 32];
+  __shared__ float sLD[4][2][16];           // per wave: lse_i, D_i of the current pixel
+  __shared__ float red[T::CT * T::VPMAX * 2];  // LN-bwd per-voxel partial sums
+  __shared__ float sdb[NH * 16 * 16];        // block dbias accumulator (thread tid owns entries [h][tid])
+  __shared__ float sdw[4 * 256];             // per-wave dbias of the current head
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int b = blockIdx.y;
+  const int V = T::P * F;
+  const int NV = (V + 15) >> 4;
+  const int VP = NV * 16;
+  const int npg = (HW + T::P - 1) / T::P;
+
+  for (int e = tid; e < NH * F * F; e += 256) {
+    const int h = e / (F * F), r = e - h * F * F, i = r / F, j = r - i * F;
+    sb[(h * 16 + i) * 16 + j] = bias[e];
+  }
+  for (int e = tid; e < F * 32; e += 256) rot[e] = rotg[e];
+  for (int e = tid; e < NH * 256; e += 256) sdb[e] = 0.f;
+
+  float dgam[T::MAXT][4];
+#pragma unroll
+  for (int k = 0; k < T::MAXT; ++k)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dgam[k][r] = 0.f;
+  const int nty = T::CT * NV;
+
+  for (int pg = blockIdx.x; pg < npg; pg += gridDim.x) {
+    const int p0 = pg * T::P;
+    __syncthreads();  // previous group's LDS consumers done
+    // ---- stage xn (LN with saved stats) and dy
+    {
+      constexpr int L = C / 8;
+      constexpr int VPP = 256 / L;
+      const int sub = tid % L;
+      for (int v0 = 0; v0 < VP; v0 += VPP) {
+        const int v = v0 + tid / L;
+        bool ok = false;
+        int64_t row = 0;
+        if (v < V) {
+          const int pp = v / F, f = v - pp * F, p = p0 + pp;
+          if (p < HW) { ok = true; row = ((int64_t)b * F + f) * HW + p; }
+        }
+        float a[8], d[8];
+        if (ok) {
+          load8(x + row * C + sub * 8, a);
+          load8(dy + row * C + sub * 8, d);
+          const float mean = mr[row * 2], rstd = mr[row * 2 + 1];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) a[i] = (a[i] - mean) * rstd * gamma[sub * 8 + i];
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) { a[i] = 0.f; d[i] = 0.f; }
+        }
+        if (v < VP) {
+          store8(xn + v * T::XLD + sub * 8, a);
+          store8(dyl + v * T::XLD + sub * 8, d);
+        }
+        if (ok && xn_out) store8(xn_out + row * C + sub * 8, a);
+      }
+    }
+    __syncthreads();
+
+    f32x4 dxacc[T::MAXT];
+#pragma unroll
+    for (int k = 0; k < T::MAXT; ++k) dxacc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int h = 0; h < NH; ++h) {
+      // ---- recompute q',k',v (6 tiles per voxel tile) and dO_h (2 tiles)
+      for (int t = wid; t < 8 * NV; t += 4) {
+        const int ct = t / NV, vt = t - ct * NV;
+        const int v = vt * 16 + lr;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        if (ct < 6) {
+          const int kind = ct >> 1;
+          const int wrow = kind * INNER + h * DH + (ct & 1) * 16 + lr;
+#pragma unroll
+          for (int k0 = 0; k0 < C; k0 += 32) {
+            const bf16x8 a = *reinterpret_cast<const bf16x8*>(wqkv + (int64_t)wrow * C + k0 + lg * 8);
+            const bf16x8 bb = *reinterpret_cast<const bf16x8*>(xn + v * T::XLD + k0 + lg * 8);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb, acc, 0, 0, 0);
+          }
+          const int f = v % F;
+          const int d0 = (ct & 1) * 16 + lg * 4;
+          float o4[4] = {acc[0], acc[1], acc[2], acc[3]};
+          if (kind == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o4[r] *= scale;
+          }
+          if (kind < 2) {
+#pragma unroll
+            for (int pr = 0; pr < 2; ++pr) {
+              const int ri = (d0 >> 1) + pr;
+              const float c = rot[f * 32 + ri * 2], s = rot[f * 32 + ri * 2 + 1];
+              const float a0 = o4[2 * pr], a1 = o4[2 * pr + 1];
+              o4[2 * pr] = a0 * c - a1 * s;
+              o4[2 * pr + 1] = a1 * c + a0 * s;
+            }
+          }
+          store4((kind == 0 ? sq : (kind == 1 ? sk : sv)) + v * HLD + d0, o4);
+        } else {
+          const int wrow = h * DH + (ct - 6) * 16 + lr;  // row of W_out^T [256][C]
+#pragma unroll
+          for (int k0 = 0; k0 < C; k0 += 32) {
+            const bf16x8 a = *reinterpret_cast<const bf16x8*>(wout_t + (int64_t)wrow * C + k0 + lg * 8);
+            const bf16x8 bb = *reinterpret_cast<const bf16x8*>(dyl + v * T::XLD + k0 + lg * 8);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb, acc, 0, 0, 0);
+          }
+          float o4[4] = {acc[0], acc[1], acc[2], acc[3]};
+          store4(sdo + v * HLD + (ct - 6) * 16 + lg * 4, o4);
+        }
+      }
+      __syncthreads();
+      // ---- core backward per pixel
+      float dbr[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int pp = wid; pp < T::P; pp += 4) {
+        const int rb = pp * F;
+        const int p = p0 + pp;
+        const bool pix_ok = p < HW;
+        const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+        const float Li = (lr < F && pix_ok) ? lse[(((int64_t)b * NH + h) * HW + p) * F + lr] : 0.f;
+        // transposed orientation: lane col i = lr, rows j = 4lg + r
+        const bf16x8 kr = lr < F ? *reinterpret_cast<const bf16x8*>(sk + (rb + lr) * HLD + lg * 8) : zero8();
+        const bf16x8 qr = lr < F ? *reinterpret_cast<const bf16x8*>(sq + (rb + lr) * HLD + lg * 8) : zero8();
+        const bf16x8 vr = lr < F ? *reinterpret_cast<const bf16x8*>(sv + (rb + lr) * HLD + lg * 8) : zero8();
+        const bf16x8 dor = lr < F ? *reinterpret_cast<const bf16x8*>(sdo + (rb + lr) * HLD + lg * 8) : zero8();
+        const f32x4 st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kr, qr, z4, 0, 0, 0);    // S^T[j][i]
+        const f32x4 dpt = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vr, dor, z4, 0, 0, 0);  // dP^T[j][i]
+        float pt[4], D = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int j = lg * 4 + r;
+          const bool ok = j < F && lr < F;
+          pt[r] = ok ? expf(st[r] + sb[(h * 16 + lr) * 16 + j] - Li) : 0.f;
+          D = fmaf(pt[r], dpt[r], D);
+        }
+        D += __shfl_xor(D, 16, 64);
+        D += __shfl_xor(D, 32, 64);
+        if (lg == 0) { sLD[wid][0][lr] = Li; sLD[wid][1][lr] = D; }
+        bf16x8 dst_b = zero8(), pt_b = zero8();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float ds = pt[r] * (dpt[r] - D);
+          dbr[r] += ds;
+          dst_b[r] = (bf16)ds;
+          pt_b[r] = (bf16)pt[r];
+        }
+        // dQ'^T[d][i] = sum_j K'[j][d] dS^T[j][i] ; O^T[d][i] = sum_j V[j][d] P^T[j][i]
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          bf16x8 ka = zero8(), va = zero8();
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int j = lg * 4 + r;
+            if (j < F) {
+              ka[r] = sk[(rb + j) * HLD + half * 16 + lr];
+              va[r] = sv[(rb + j) * HLD + half * 16 + lr];
+            }
+          }
+          const f32x4 dqt = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, dst_b, z4, 0, 0, 0);
+          const f32x4 ot = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pt_b, z4, 0, 0, 0);
+          if (lr < F) {
+            // dq = scale * R_i^T dQ'
+            const int d0 = half * 16 + lg * 4;
+            float o4[4] = {dqt[0], dqt[1], dqt[2], dqt[3]};
+#pragma unroll
+            for (int pr = 0; pr < 2; ++pr) {
+              const int ri = (d0 >> 1) + pr;
+              const float c = rot[lr * 32 + ri * 2], s = -rot[lr * 32 + ri * 2 + 1];
+              const float a0 = o4[2 * pr], a1 = o4[2 * pr + 1];
+              o4[2 * pr] = (a0 * c - a1 * s) * scale;
+              o4[2 * pr + 1] = (a1 * c + a0 * s) * scale;
+            }
+            store4(sdq + (rb + lr) * HLD + d0, o4);
+            if (o_out && pix_ok) {
+              float oo[4] = {ot[0], ot[1], ot[2], ot[3]};
+              const int64_t row = ((int64_t)b * F + lr) * HW + p;
+              store4(o_out + row * INNER + h * DH + d0, oo);
+            }
+          }
+        }
+        // row-major orientation: lane col j = lr, rows i = 4lg + r
+        const f32x4 s_ = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qr, kr, z4, 0, 0, 0);   // S[i][j]
+        const f32x4 dp_ = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dor, vr, z4, 0, 0, 0); // dP[i][j]
+        bf16x8 ds_b = zero8(), p_b = zero8();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = lg * 4 + r;
+          const bool ok = i < F && lr < F;
+          const float pv = ok ? expf(s_[r] + sb[(h * 16 + i) * 16 + lr] - sLD[wid][0][i]) : 0.f;
+          p_b[r] = (bf16)pv;
+          ds_b[r] = (bf16)(ok ? pv * (dp_[r] - sLD[wid][1][i]) : 0.f);
+        }
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          bf16x8 qa = zero8(), doa = zero8();
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int i = lg * 4 + r;
+            if (i < F) {
+              qa[r] = sq[(rb + i) * HLD + half * 16 + lr];
+              doa[r] = sdo[(rb + i) * HLD + half * 16 + lr];
+            }
+          }
+          const f32x4 dkt = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, ds_b, z4, 0, 0, 0);   // dK'^T[d][j]
+          const f32x4 dvt = __builtin_amdgcn_mfma_f32_16x16x32_bf16(doa, p_b, z4, 0, 0, 0);   // dV^T[d][j]
+          if (lr < F) {
+            const int d0 = half * 16 + lg * 4;
+            float o4[4] = {dkt[0], dkt[1], dkt[2], dkt[3]};
+#pragma unroll
+            for (int pr = 0; pr < 2; ++pr) {
+              const int ri = (d0 >> 1) + pr;
+              const float c = rot[lr * 32 + ri * 2], s = -rot[lr * 32 + ri * 2 + 1];
+              const float a0 = o4[2 * pr], a1 = o4[2 * pr + 1];
+              o4[2 * pr] = a0 * c - a1 * s;
+              o4[2 * pr + 1] = a1 * c + a0 * s;
+            }
+            store4(sdk + (rb + lr) * HLD + d0, o4);
+            float v4[4] = {dvt[0], dvt[1], dvt[2], dvt[3]};
+            store4(sdv + (rb + lr) * HLD + d0, v4);
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sdw[wid * 256 + lr * 16 + lg * 4 + r] = dbr[r];
+      __syncthreads();
+      sdb[h * 256 + tid] += ((sdw[tid] + sdw[256 + tid]) + sdw[512 + tid]) + sdw[768 + tid];
+      // ---- dxn^T += W_qkv^T[:, h cols] . dqkv_h^T ; also emit dqkv_h
+#pragma unroll
+      for (int k = 0; k < T::MAXT; ++k) {
+        const int t = wid + 4 * k;
+        if (t < nty) {
+          const int ct = t / NV, vt = t - ct * NV;
+          const int v = vt * 16 + lr;
+#pragma unroll
+          for (int kind = 0; kind < 3; ++kind) {
+            const bf16* src = kind == 0 ? sdq : (kind == 1 ? sdk : sdv);
+            const bf16x8 a = *reinterpret_cast<const bf16x8*>(wqkv_t + (int64_t)(ct * 16 + lr) * QKV + kind * INNER +
+                                                              h * DH + lg * 8);
+            const bf16x8 bb = *reinterpret_cast<const bf16x8*>(src + v * HLD + lg * 8);
+            dxacc[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb, dxacc[k], 0, 0, 0);
+          }
+        }
+      }
+      if (dqkv_out) {
+        for (int e = tid; e < V * 12; e += 256) {   // V voxels x 3 kinds x 4 x 8-element chunks
+          const int v = e / 12, rem = e - v * 12, kind = rem >> 2, part = rem & 3;
+          const int pp = v / F, f = v - pp * F, p = p0 + pp;
+          if (p >= HW) continue;
+          const int64_t row = ((int64_t)b * F + f) * HW + p;
+          const bf16* src = kind == 0 ? sdq : (kind == 1 ? sdk : sdv);
+          *reinterpret_cast<bf16x8*>(dqkv_out + row * QKV + kind * INNER + h * DH + part * 8) =
+              *reinterpret_cast<const bf16x8*>(src + v * HLD + part * 8);
+        }
+      }
+      __syncthreads();  // sq/sk/sv/sdo/sdq/sdk/sdv reused by the next head
+    }
+    // ---- LN backward: g = dxn*gamma, dx = rstd*(g - mean(g) - xhat*mean(g*xhat)) + dy
+#pragma unroll
+    for (int k = 0; k < T::MAXT; ++k) {
+      const int t = wid + 4 * k;
+      float s1 = 0.f, s2 = 0.f;
+      if (t < nty) {
+        const int ct = t / NV, vt = t - ct * NV;
+        const int v = vt * 16 + lr;
+        bool ok = false;
+        int64_t row = 0;
+        if (v < V) {
+          const int pp = v / F, f = v - pp * F, p = p0 + pp;
+          if (p < HW) { ok = true; row = ((int64_t)b * F + f) * HW + p; }
+        }
+        const int co = ct * 16 + lg * 4;
+        if (ok) {
+          float xv[4];
+          load4(x + row * C + co, xv);
+          const float mean = mr[row * 2], rstd = mr[row * 2 + 1];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float xh = (xv[r] - mean) * rstd;
+            const float g = dxacc[k][r] * gamma[co + r];
+            s1 += g;
+            s2 = fmaf(g, xh, s2);
+            dgam[k][r] = fmaf(dxacc[k][r], xh, dgam[k][r]);
+          }
+        }
+        s1 += __shfl_xor(s1, 16, 64);
+        s1 += __shfl_xor(s1, 32, 64);
+        s2 += __shfl_xor(s2, 16, 64);
+        s2 += __shfl_xor(s2, 32, 64);
+        if (lg == 0) { red[(ct * T::VPMAX + v) * 2] = s1; red[(ct * T::VPMAX + v) * 2 + 1] = s2; }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < T::MAXT; ++k) {
+      const int t = wid + 4 * k;
+      if (t >= nty) continue;
+      const int ct = t / NV, vt = t - ct * NV;
+      const int v = vt * 16 + lr;
+      if (v >= V) continue;
+      const int pp = v / F, f = v - pp * F, p = p0 + pp;
+      if (p >= HW) continue;
+      const int64_t row = ((int64_t)b * F + f) * HW + p;
+      float S1 = 0.f, S2 = 0.f;
+      for (int c2 = 0; c2 < T::CT; ++c2) { S1 += red[(c2 * T::VPMAX + v) * 2]; S2 += red[(c2 * T::VPMAX + v) * 2 + 1]; }
+      S1 /= C;
+      S2 /= C;
+      const float mean = mr[row * 2], rstd = mr[row * 2 + 1];
+      const int co = ct * 16 + lg * 4;
+      float xv[4], o4[4];
+      load4(x + row * C + co, xv);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float xh = (xv[r] - mean) * rstd;
+        o4[r] = rstd * (dxacc[k][r] * gamma[co + r] - S1 - xh * S2) + (float)dyl[v * T::XLD + co + r];
+      }
+      store4(dx + row * C + co, o4);
+    }
+  }
+  // ---- block partials: dbias -> relpos layout [b][h][blk][F][F]
+  __syncthreads();
+  for (int e = tid; e < NH * F * F; e += 256) {
+    const int h = e / (F * F), r = e - h * F * F, i = r / F, j = r - i * F;
+    dbias_part[(((int64_t)b * NH + h) * gridDim.x + blockIdx.x) * F * F + r] = sdb[(h * 16 + i) * 16 + j];
+  }
+  // dgamma: reduce each lane's per-channel partials over the 16 voxel lanes, then tiles/waves in order
+#pragma unroll
+  for (int k = 0; k < T::MAXT; ++k)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) dgam[k][r] += __shfl_xor(dgam[k][r], o, 64);
+  float* sg = red;  // reuse: C floats
+  for (int e = tid; e < C; e += 256) sg[e] = 0.f;
+  __syncthreads();
+  for (int w = 0; w < 4; ++w) {
+    if (wid == w && lr == 0) {
+#pragma unroll
+      for (int k = 0; k < T::MAXT; ++k) {
+        const int t = wid + 4 * k;
+        if (t < nty) {
+          const int ct = t / NV;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sg[ct * 16 + lg * 4 + r] += dgam[k][r];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  for (int e = tid; e < C; e += 256) dgamma_part[((int64_t)b * gridDim.x + blockIdx.x) * C + e] = sg[e];
+}
+
+// ============================================================================================
+// Wave-private variants (C <= 256).  Each wave owns PW consecutive pixels x F frames (VW = PW*F
+// voxels, NVT = ceil(VW/16) voxel tiles) end to end, so there are no block barriers after the
+// table preload:
+//   * LN is evaluated on the MFMA B fragments in registers (lane (g, r): voxel r of the tile,
+//     channels ks*32 + 8g..8g+7); per-voxel sums via 16/32-lane shuffles;
+//   * per head, [q'|k'|v] (and dO in the backward) go to a wave-private LDS slice of NVT*16 rows;
+//   * each weight fragment is loaded once per head and reused for all NVT voxel tiles.
+// ============================================================================================
+template <int C, int NV = 1>
+struct TW {
+  static constexpr int PW = C <= 64 ? 4 : (C == 128 ? 2 : 1);  // pixels per wave
+  static constexpr int KS = C / 32;                            // k-steps of the C-deep GEMMs
+  static constexpr int CT = C / 16;                            // 16-channel output tiles
+  static constexpr int NVTM = NV;                              // voxel tiles of the wave (<= PW)
+};
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ bf16x8 ld16(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
+// rows of voxel v of the wave's pixel group
+__device__ __forceinline__ bool tw_row(int v, int VW, int F, int p0, int HW, int b, int64_t& row) {
+  if (v >= VW) return false;
+  const int pp = v / F, f = v - pp * F, p = p0 + pp;
+  if (p >= HW) return false;
+  row = ((int64_t)b * F + f) * HW + p;
+  return true;
+}
+
+// q'|k'|v tiles (and the RoPE/scale epilogue) of head h for the wave's NVT voxel tiles
+template <int C, int NV>
+__device__ __forceinline__ void tw_qkv(const bf16* __restrict__ wqkv, const bf16x8 (&xf)[TW<C, NV>::NVTM][TW<C, NV>::KS],
+                                       int h, int NVT, int F, float scale, const float* rot, bf16* sq, bf16* sk,
+                                       bf16* sv, int lr, int lg) {
+  using T = TW<C, NV>;
+#pragma unroll
+  for (int ct = 0; ct < 6; ++ct) {
+    const int kind = ct >> 1;
+    const int wrow = kind * INNER + h * DH + (ct & 1) * 16 + lr;
+    bf16x8 a[T::KS];
+#pragma unroll
+    for (int ks = 0; ks < T::KS; ++ks) a[ks] = ld16(wqkv + (int64_t)wrow * C + ks * 32 + lg * 8);
+    bf16* dst = kind == 0 ? sq : (kind == 1 ? sk : sv);
+    const int d0 = (ct & 1) * 16 + lg * 4;
+#pragma unroll
+    for (int vt = 0; vt < T::NVTM; ++vt) {
+      if (vt < NVT) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < T::KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], xf[vt][ks], acc, 0, 0, 0);
+        const int v = vt * 16 + lr;
+        const int f = v % F;
+        float o4[4] = {acc[0], acc[1], acc[2], acc[3]};
+        if (kind == 0) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o4[r] *= scale;
+        }
+        if (kind < 2) {
+#pragma unroll
+          for (int pr = 0; pr < 2; ++pr) {
+            const int ri = (d0 >> 1) + pr;
+            const float c = rot[f * 32 + ri * 2], sn = rot[f * 32 + ri * 2 + 1];
+            const float a0 = o4[2 * pr], a1 = o4[2 * pr + 1];
+            o4[2 * pr] = a0 * c - a1 * sn;
+            o4[2 * pr + 1] = a1 * c + a0 * sn;
+          }
+        }
+        store4(dst + v * HLD + d0, o4);
+      }
+    }
+  }
+}
+
+// LN of the wave's voxels on the B fragments.  use_saved: take (mean, rstd) from mr, else compute
+// them (and store them to mr when non-null).
+template <int C, int NV>
+__device__ __forceinline__ void tw_ln(const bf16* __restrict__ x, const float* __restrict__ gamma, float* mr_out,
+                                      const float* __restrict__ mr_in, bf16x8 (&xf)[TW<C, NV>::NVTM][TW<C, NV>::KS], int NVT,
+                                      int VW, int F, int p0, int HW, int b, float eps, int lr, int lg) {
+  using T = TW<C, NV>;
+#pragma unroll
+  for (int vt = 0; vt < T::NVTM; ++vt) {
+    if (vt >= NVT) break;
+    int64_t row = 0;
+    const bool ok = tw_row(vt * 16 + lr, VW, F, p0, HW, b, row);
+    float a[T::KS][8];
+#pragma unroll
+    for (int ks = 0; ks < T::KS; ++ks) {
+      if (ok) load8(x + row * C + ks * 32 + lg * 8, a[ks]);
+      else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[ks][i] = 0.f;
+      }
+    }
+    float mean, rstd;
+    if (mr_in) {
+      mean = ok ? mr_in[row * 2] : 0.f;
+      rstd = ok ? mr_in[row * 2 + 1] : 0.f;
+    } else {
+      float s = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < T::KS; ++ks)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s += a[ks][i];
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      mean = s / C;
+      float q = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < T::KS; ++ks)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { const float d = a[ks][i] - mean; q = fmaf(d, d, q); }
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      rstd = 1.f / sqrtf(q / C + eps);
+      if (ok && lg == 0 && mr_out) { mr_out[row * 2] = mean; mr_out[row * 2 + 1] = rstd; }
+    }
+#pragma unroll
+    for (int ks = 0; ks < T::KS; ++ks)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        xf[vt][ks][i] = (bf16)(ok ? (a[ks][i] - mean) * rstd * gamma[ks * 32 + lg * 8 + i] : 0.f);
+  }
+}
+
+template <int C, int NV>
+__global__ __launch_bounds__(256) void tw_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ gamma,
+                                                     const bf16* __restrict__ wqkv, const bf16* __restrict__ wout,
+                                                     const float* __restrict__ bias, const float* __restrict__ rotg,
+                                                     bf16* __restrict__ y, float* __restrict__ mr,
+                                                     float* __restrict__ lse, int F, int HW, float scale, float eps) {
+  using T = TW<C, NV>;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sb = smem;             // [8][F][F]
+  float* rot = smem + NH * 256; // [16][32]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int b = blockIdx.y;
+  const int VW = T::PW * F;
+  constexpr int NVT = NV;
+  const int R = NVT * 16;
+  bf16* sq = reinterpret_cast<bf16*>(rot + 512) + wid * 3 * R * HLD;
+  bf16* sk = sq + R * HLD;
+  bf16* sv = sk + R * HLD;
+  for (int e = tid; e < NH * F * F; e += 256) sb[e] = bias[e];
+  for (int e = tid; e < F * 32; e += 256) rot[e] = rotg[e];
+  __syncthreads();
+  const int p0 = (blockIdx.x * 4 + wid) * T::PW;
+  if (p0 >= HW) return;
+
+  bf16x8 xf[T::NVTM][T::KS];
+  tw_ln<C, NV>(x, gamma, mr, nullptr, xf, NVT, VW, F, p0, HW, b, eps, lr, lg);
+
+  f32x4 yacc[T::CT][T::NVTM];
+#pragma unroll
+  for (int ct = 0; ct < T::CT; ++ct)
+#pragma unroll
+    for (int vt = 0; vt < T::NVTM; ++vt) yacc[ct][vt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+
+  for (int h = 0; h < NH; ++h) {
+    tw_qkv<C, NV>(wqkv, xf, h, NVT, F, scale, rot, sq, sk, sv, lr, lg);
+    wave_lds_sync();
+    // attention core per pixel; O overwrites the pixel's own q rows
+    for (int pp = 0; pp < T::PW; ++pp) {
+      const int p = p0 + pp;
+      if (p >= HW) break;
+      const int rb = pp * F;
+      const bf16x8 ka = lr < F ? ld16(sk + (rb + lr) * HLD + lg * 8) : zero8();
+      const bf16x8 qb = lr < F ? ld16(sq + (rb + lr) * HLD + lg * 8) : zero8();
+      const f32x4 st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qb, z4, 0, 0, 0);
+      float sc[4];
+      float m = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = lg * 4 + r;
+        sc[r] = (j < F && lr < F) ? st[r] + sb[(h * F + lr) * F + j] : -INFINITY;
+        m = fmaxf(m, sc[r]);
+      }
+      m = fmaxf(m, __shfl_xor(m, 16, 64));
+      m = fmaxf(m, __shfl_xor(m, 32, 64));
+      float pr[4], l = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pr[r] = sc[r] == -INFINITY ? 0.f : expf(sc[r] - m);
+        l += pr[r];
+      }
+      l += __shfl_xor(l, 16, 64);
+      l += __shfl_xor(l, 32, 64);
+      if (lse && lg == 0 && lr < F) lse[(((int64_t)b * NH + h) * HW + p) * F + lr] = m + logf(l);
+      const float inv = lr < F ? 1.f / l : 0.f;
+      bf16x8 pb = zero8();
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pb[r] = (bf16)(pr[r] * inv);
+      bf16x8 va[2];
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        va[half] = zero8();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int j = lg * 4 + r;
+          if (j < F) va[half][r] = sv[(rb + j) * HLD + half * 16 + lr];
+        }
+      }
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const f32x4 ot = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va[half], pb, z4, 0, 0, 0);
+        if (lr < F) {
+          float o4[4] = {ot[0], ot[1], ot[2], ot[3]};
+          store4(sq + (rb + lr) * HLD + half * 16 + lg * 4, o4);
+        }
+      }
+    }
+    wave_lds_sync();
+    // y^T += W_out[:, h] . O_h^T
+    bf16x8 ob[T::NVTM];
+#pragma unroll
+    for (int vt = 0; vt < T::NVTM; ++vt) ob[vt] = vt < NVT ? ld16(sq + (vt * 16 + lr) * HLD + lg * 8) : zero8();
+#pragma unroll
+    for (int ct = 0; ct < T::CT; ++ct) {
+      const bf16x8 a = ld16(wout + (int64_t)(ct * 16 + lr) * INNER + h * DH + lg * 8);
+#pragma unroll
+      for (int vt = 0; vt < T::NVTM; ++vt)
+        if (vt < NVT) yacc[ct][vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ob[vt], yacc[ct][vt], 0, 0, 0);
+    }
+    wave_lds_sync();
+  }
+  // y = x + attn
+#pragma unroll
+  for (int vt = 0; vt < T::NVTM; ++vt) {
+    if (vt >= NVT) break;
+    int64_t row = 0;
+    if (!tw_row(vt * 16 + lr, VW, F, p0, HW, b, row)) continue;
+#pragma unroll
+    for (int ct = 0; ct < T::CT; ++ct) {
+      const int co = ct * 16 + lg * 4;
+      float xv[4];
+      load4(x + row * C + co, xv);
+      float o4[4] = {yacc[ct][vt][0] + xv[0], yacc[ct][vt][1] + xv[1], yacc[ct][vt][2] + xv[2], yacc[ct][vt][3] + xv[3]};
+      store4(y + row * C + co, o4);
+    }
+  }
+}
+
+template <int C, int NV>
+__global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ dy, const float* __restrict__ gamma,
+    const float* __restrict__ mr, const float* __restrict__ lse, const bf16* __restrict__ wqkv,
+    const bf16* __restrict__ wqkv_t, const bf16* __restrict__ wout_t, const float* __restrict__ bias,
+    const float* __restrict__ rotg, bf16* __restrict__ dx, bf16* __restrict__ dqkv_out, bf16* __restrict__ o_out,
+    bf16* __restrict__ xn_out, float* __restrict__ dbias_part, float* __restrict__ dgamma_part, int F, int HW,
+    float scale) {
+  using T = TW<C, NV>;
+  constexpr bool DG_REG = false;  // dgamma partials flushed per pixel group (LDS atomics)
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int FF = F * F;
+  float* sb = smem;                  // [8][F][F]
+  float* sdb = sb + NH * FF;         // [8][F][F] block dbias accumulator
+  float* sg = sdb + NH * FF;         // [C] block dgamma accumulator
+  float* rot = sg + C;               // [16][32]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int b = blockIdx.y;
+  const int VW = T::PW * F;
+  constexpr int NVT = NV;
+  const int R = NVT * 16;
+  bf16* sq = reinterpret_cast<bf16*>(rot + 512) + wid * 4 * R * HLD;
+  bf16* sk = sq + R * HLD;
+  bf16* sv = sk + R * HLD;
+  bf16* sdo = sv + R * HLD;
+  for (int e = tid; e < NH * FF; e += 256) { sb[e] = bias[e]; sdb[e] = 0.f; }
+  for (int e = tid; e < C; e += 256) sg[e] = 0.f;
+  for (int e = tid; e < F * 32; e += 256) rot[e] = rotg[e];
+  __syncthreads();
+
+  const int npg = (HW + T::PW - 1) / T::PW;
+  const int nw = gridDim.x * 4;
+  float dgam[DG_REG ? T::CT : 1][4];
+#pragma unroll
+  for (int ct = 0; ct < (DG_REG ? T::CT : 1); ++ct)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dgam[ct][r] = 0.f;
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+
+  for (int pg = blockIdx.x * 4 + wid; pg < npg; pg += nw) {
+    const int p0 = pg * T::PW;
+    bf16x8 xf[T::NVTM][T::KS];
+    tw_ln<C, NV>(x, gamma, nullptr, mr, xf, NVT, VW, F, p0, HW, b, 0.f, lr, lg);
+    int64_t vrow[T::NVTM];  // row of voxel (vt*16 + lane&15), -1 when outside the group
+#pragma unroll
+    for (int vt = 0; vt < T::NVTM; ++vt) {
+      int64_t row = 0;
+      vrow[vt] = tw_row(vt * 16 + lr, VW, F, p0, HW, b, row) ? row : -1;
+      if (vrow[vt] >= 0 && xn_out) {
+#pragma unroll
+        for (int ks = 0; ks < T::KS; ++ks) *reinterpret_cast<bf16x8*>(xn_out + row * C + ks * 32 + lg * 8) = xf[vt][ks];
+      }
+    }
+    f32x4 dxacc[T::CT][T::NVTM];
+#pragma unroll
+    for (int ct = 0; ct < T::CT; ++ct)
+#pragma unroll
+      for (int vt = 0; vt < T::NVTM; ++vt) dxacc[ct][vt] = z4;
+
+    for (int h = 0; h < NH; ++h) {
+      tw_qkv<C, NV>(wqkv, xf, h, NVT, F, scale, rot, sq, sk, sv, lr, lg);
+      // dO_h^T = W_out[:, h]^T . dy^T
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        bf16x8 a[T::KS];
+#pragma unroll
+        for (int ks = 0; ks < T::KS; ++ks) a[ks] = ld16(wout_t + (int64_t)(h * DH + dt * 16 + lr) * C + ks * 32 + lg * 8);
+#pragma unroll
+        for (int vt = 0; vt < T::NVTM; ++vt) {
+          if (vt < NVT) {
+            f32x4 acc = z4;
+#pragma unroll
+            for (int ks = 0; ks < T::KS; ++ks) {
+              const bf16x8 dyf = vrow[vt] >= 0 ? ld16(dy + vrow[vt] * C + ks * 32 + lg * 8) : zero8();
+              acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], dyf, acc, 0, 0, 0);
+            }
+            float o4[4] = {acc[0], acc[1], acc[2], acc[3]};
+            store4(sdo + (vt * 16 + lr) * HLD + dt * 16 + lg * 4, o4);
+          }
+        }
+      }
+      wave_lds_sync();
+      // core backward per pixel; dq/dk/dv overwrite the pixel's own q/k/v rows at the end
+      float dbr[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int pp = 0; pp < T::PW; ++pp) {
+        const int p = p0 + pp;
+        if (p >= HW) break;
+        const int rb = pp * F;
+        const float Li = lr < F ? lse[(((int64_t)b * NH + h) * HW + p) * F + lr] : 0.f;
+        const bf16x8 kr = lr < F ? ld16(sk + (rb + lr) * HLD + lg * 8) : zero8();
+        const bf16x8 qr = lr < F ? ld16(sq + (rb + lr) * HLD + lg * 8) : zero8();
+        const bf16x8 vr = lr < F ? ld16(sv + (rb + lr) * HLD + lg * 8) : zero8();
+        const bf16x8 dor = lr < F ? ld16(sdo + (rb + lr) * HLD + lg * 8) : zero8();
+        // -- transposed orientation: lane (g, i): entries (j = 4g + r, i)
+        float D = 0.f;
+        bf16x8 dst_b = zero8(), pt_b = zero8();
+        {
+          const f32x4 st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kr, qr, z4, 0, 0, 0);    // S^T[j][i]
+          const f32x4 dpt = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vr, dor, z4, 0, 0, 0);  // dP^T[j][i]
+          float pt[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int j = lg * 4 + r;
+            const bool ok = j < F && lr < F;
+            pt[r] = ok ? expf(st[r] + sb[(h * F + lr) * F + j] - Li) : 0.f;
+            D = fmaf(pt[r], dpt[r], D);
+          }
+          D += __shfl_xor(D, 16, 64);
+          D += __shfl_xor(D, 32, 64);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float ds = pt[r] * (dpt[r] - D);
+            dbr[r] += ds;
+            dst_b[r] = (bf16)ds;
+            pt_b[r] = (bf16)pt[r];
+          }
+        }
+        // k-slot gathers: slot (g, e<4) <-> frame 4g+e, column d = half*16 + (lane & 15)
+        f32x4 dqt[2];
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          bf16x8 kg = zero8(), vg = zero8();
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int j = lg * 4 + r;
+            if (j < F) {
+              const int o = (rb + j) * HLD + half * 16 + lr;
+              kg[r] = sk[o];
+              vg[r] = sv[o];
+            }
+          }
+          dqt[half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kg, dst_b, z4, 0, 0, 0);  // dQ'^T[d][i]
+          const f32x4 ot = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vg, pt_b, z4, 0, 0, 0);  // O^T[d][i]
+          if (o_out && lr < F) {
+            float oo[4] = {ot[0], ot[1], ot[2], ot[3]};
+            store4(o_out + (((int64_t)b * F + lr) * HW + p) * INNER + h * DH + half * 16 + lg * 4, oo);
+          }
+        }
+        // -- row-major orientation: lane (g, j): entries (i = 4g + r, j); L_i, D_i from lane i
+        bf16x8 ds_b = zero8(), p_b = zero8();
+        {
+          const f32x4 s_ = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qr, kr, z4, 0, 0, 0);    // S[i][j]
+          const f32x4 dp_ = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dor, vr, z4, 0, 0, 0);  // dP[i][j]
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int i = lg * 4 + r;
+            const float Lr = __shfl(Li, i, 64), Dr = __shfl(D, i, 64);
+            const bool ok = i < F && lr < F;
+            const float pv = ok ? expf(s_[r] + sb[(h * F + i) * F + lr] - Lr) : 0.f;
+            p_b[r] = (bf16)pv;
+            ds_b[r] = (bf16)(ok ? pv * (dp_[r] - Dr) : 0.f);
+          }
+        }
+        f32x4 dkt[2], dvt[2];
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          bf16x8 qg = zero8(), dog = zero8();
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int i = lg * 4 + r;
+            if (i < F) {
+              const int o = (rb + i) * HLD + half * 16 + lr;
+              qg[r] = sq[o];
+              dog[r] = sdo[o];
+            }
+          }
+          dkt[half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qg, ds_b, z4, 0, 0, 0);   // dK'^T[d][j]
+          dvt[half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dog, p_b, z4, 0, 0, 0);   // dV^T[d][j]
+        }
+        wave_lds_sync();  // all reads of this pixel's rows done before they are overwritten
+        if (lr < F) {
+#pragma unroll
+          for (int half = 0; half < 2; ++half) {
+            const int d0 = half * 16 + lg * 4;
+            float q4[4] = {dqt[half][0], dqt[half][1], dqt[half][2], dqt[half][3]};
+            float k4[4] = {dkt[half][0], dkt[half][1], dkt[half][2], dkt[half][3]};
+            float v4[4] = {dvt[half][0], dvt[half][1], dvt[half][2], dvt[half][3]};
+#pragma unroll
+            for (int pr = 0; pr < 2; ++pr) {  // dq = scale R^T dQ', dk = R^T dK' (frame lr)
+              const int ri = (d0 >> 1) + pr;
+              const float c = rot[lr * 32 + ri * 2], sn = rot[lr * 32 + ri * 2 + 1];
+              const float a0 = q4[2 * pr], a1 = q4[2 * pr + 1];
+              q4[2 * pr] = (a0 * c + a1 * sn) * scale;
+              q4[2 * pr + 1] = (a1 * c - a0 * sn) * scale;
+              const float b0 = k4[2 * pr], b1 = k4[2 * pr + 1];
+              k4[2 * pr] = b0 * c + b1 * sn;
+              k4[2 * pr + 1] = b1 * c - b0 * sn;
+            }
+            store4(sq + (rb + lr) * HLD + d0, q4);
+            store4(sk + (rb + lr) * HLD + d0, k4);
+            store4(sv + (rb + lr) * HLD + d0, v4);
+          }
+        }
+        wave_lds_sync();
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (lr < F && lg * 4 + r < F) atomicAdd(&sdb[(h * F + lr) * F + lg * 4 + r], dbr[r]);
+      wave_lds_sync();
+      // dxn^T += W_qkv[h rows]^T . [dq|dk|dv]_h^T ; emit dqkv_h
+#pragma unroll
+      for (int kind = 0; kind < 3; ++kind) {
+        const bf16* src = kind == 0 ? sq : (kind == 1 ? sk : sv);
+        bf16x8 bf[T::NVTM];
+#pragma unroll
+        for (int vt = 0; vt < T::NVTM; ++vt) bf[vt] = vt < NVT ? ld16(src + (vt * 16 + lr) * HLD + lg * 8) : zero8();
+#pragma unroll
+        for (int ct = 0; ct < T::CT; ++ct) {
+          const bf16x8 a = ld16(wqkv_t + (int64_t)(ct * 16 + lr) * QKV + kind * INNER + h * DH + lg * 8);
+#pragma unroll
+          for (int vt = 0; vt < T::NVTM; ++vt)
+            if (vt < NVT) dxacc[ct][vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bf[vt], dxacc[ct][vt], 0, 0, 0);
+        }
+        if (dqkv_out) {
+#pragma unroll
+          for (int vt = 0; vt < T::NVTM; ++vt) {
+            if (vt >= NVT) break;
+            int64_t row = 0;
+            if (tw_row(vt * 16 + lr, VW, F, p0, HW, b, row))
+              *reinterpret_cast<bf16x8*>(dqkv_out + row * QKV + kind * INNER + h * DH + lg * 8) = bf[vt];
+          }
+        }
+      }
+      wave_lds_sync();
+    }
+    // LN backward: dx = rstd*(g - mean(g) - xhat*mean(g*xhat)) + dy, g = dxn*gamma
+#pragma unroll
+    for (int vt = 0; vt < T::NVTM; ++vt) {
+      if (vt >= NVT) break;
+      int64_t row = 0;
+      const bool ok = tw_row(vt * 16 + lr, VW, F, p0, HW, b, row);
+      const float mean = ok ? mr[row * 2] : 0.f, rstd = ok ? mr[row * 2 + 1] : 0.f;
+      float s1 = 0.f, s2 = 0.f;
+      float xh[T::CT][4];
+#pragma unroll
+      for (int ct = 0; ct < T::CT; ++ct) {
+        const int co = ct * 16 + lg * 4;
+        float xv[4] = {0.f, 0.f, 0.f, 0.f};
+        if (ok) load4(x + row * C + co, xv);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          xh[ct][r] = ok ? (xv[r] - mean) * rstd : 0.f;
+          const float g = dxacc[ct][vt][r] * gamma[co + r];
+          s1 += g;
+          s2 = fmaf(g, xh[ct][r], s2);
+          if constexpr (DG_REG) dgam[ct][r] = fmaf(dxacc[ct][vt][r], xh[ct][r], dgam[ct][r]);
+        }
+      }
+      s1 += __shfl_xor(s1, 16, 64);
+      s1 += __shfl_xor(s1, 32, 64);
+      s2 += __shfl_xor(s2, 16, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      s1 /= C;
+      s2 /= C;
+#pragma unroll
+      for (int ct = 0; ct < T::CT; ++ct) {
+        const int co = ct * 16 + lg * 4;
+        if constexpr (!DG_REG) {
+          float d4[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            d4[r] = dxacc[ct][vt][r] * xh[ct][r];
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) d4[r] += __shfl_xor(d4[r], o, 64);
+          }
+          if (lr == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) atomicAdd(&sg[co + r], d4[r]);
+          }
+        }
+        if (ok) {
+          float dv[4], o4[4];
+          load4(dy + row * C + co, dv);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o4[r] = rstd * (dxacc[ct][vt][r] * gamma[co + r] - s1 - xh[ct][r] * s2) + dv[r];
+          store4(dx + row * C + co, o4);
+        }
+      }
+    }
+  }
+  if constexpr (DG_REG) {
+#pragma unroll
+    for (int ct = 0; ct < T::CT; ++ct)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = dgam[ct][r];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+        if (lr == 0) atomicAdd(&sg[ct * 16 + lg * 4 + r], v);
+      }
+  }
+  __syncthreads();
+  for (int e = tid; e < NH * FF; e += 256) {
+    const int h = e / FF, r = e - h * FF;
+    dbias_part[(((int64_t)b * NH + h) * gridDim.x + blockIdx.x) * FF + r] = sdb[e];
+  }
+  for (int e = tid; e < C; e += 256) dgamma_part[((int64_t)b * gridDim.x + blockIdx.x) * C + e] = sg[e];
+}
+
+__global__ void tb_sum_rows_kernel(const float* __restrict__ part, float* __restrict__ dst, int nrows, int C,
+                                   int accumulate) {
+  const int c = blockIdx.x;
+  float s = 0.f;
+  for (int k = threadIdx.x; k < nrows; k += 64) s += part[(int64_t)k * C + c];
+  s = wave_sum(s);
+  if (threadIdx.x == 0) dst[c] = accumulate ? dst[c] + s : s;
+}
+
+template <int C>
+static size_t tw_fwd_smem(int F) {  // NOLINT
+  const int R = ((TW<C>::PW * F + 15) / 16) * 16;
+  return (size_t)(NH * 256 + 512) * 4 + (size_t)4 * 3 * R * HLD * 2;
+}
+template <int C>
+static size_t tw_bwd_smem(int F) {
+  const int R = ((TW<C>::PW * F + 15) / 16) * 16;
+  return (size_t)(2 * NH * F * F + C + 512) * 4 + (size_t)4 * 4 * R * HLD * 2;
+}
+template <typename K>
+static void allow_smem(K kernel, size_t bytes) {
+  if (bytes > 65536) hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+template <int C, int NV>
+static void tw_fwd_launch_nv(const void* x, const float* gamma, const void* wqkv, const void* wout, const float* bias,
+                             const float* rot, void* y, float* mr, float* lse, int B, int F, int HW, float scale,
+                             float eps, hipStream_t stream) {
+  const int npg = (int)cdiv(HW, TW<C>::PW);
+  dim3 grid((unsigned)cdiv(npg, 4), B);
+  const size_t sm = tw_fwd_smem<C>(F);
+  allow_smem(tw_fwd_kernel<C, NV>, sm);
+  tw_fwd_kernel<C, NV><<<grid, 256, sm, stream>>>((const bf16*)x, gamma, (const bf16*)wqkv, (const bf16*)wout, bias,
+                                                  rot, (bf16*)y, mr, lse, F, HW, scale, eps);
+}
+
+template <int C>
+static int tw_fwd_launch(const void* x, const float* gamma, const void* wqkv, const void* wout, const float* bias,
+                         const float* rot, void* y, float* mr, float* lse, int B, int F, int HW, float scale, float eps,
+                         hipStream_t stream) {
+  const int nv = (TW<C>::PW * F + 15) / 16;
+  switch (nv) {
+    case 1: tw_fwd_launch_nv<C, 1>(x, gamma, wqkv, wout, bias, rot, y, mr, lse, B, F, HW, scale, eps, stream); break;
+    case 2:
+      if constexpr (TW<C>::PW >= 2) { tw_fwd_launch_nv<C, 2>(x, gamma, wqkv, wout, bias, rot, y, mr, lse, B, F, HW, scale, eps, stream); break; }
+      return CESM_EUNSUPPORTED;
+    case 3:
+      if constexpr (TW<C>::PW >= 3) { tw_fwd_launch_nv<C, 3>(x, gamma, wqkv, wout, bias, rot, y, mr, lse, B, F, HW, scale, eps, stream); break; }
+      return CESM_EUNSUPPORTED;
+    case 4:
+      if constexpr (TW<C>::PW >= 4) { tw_fwd_launch_nv<C, 4>(x, gamma, wqkv, wout, bias, rot, y, mr, lse, B, F, HW, scale, eps, stream); break; }
+      return CESM_EUNSUPPORTED;
+    default:
+      return CESM_EUNSUPPORTED;
+  }
+  return cesm_launch_status();
+}
+
+template <int C, int NV>
+static void tw_bwd_launch_nv(const void* x, const void* dy, const float* gamma, const float* mr, const float* lse,
+                             const void* wqkv, const void* wqkv_t, const void* wout_t, const float* bias,
+                             const float* rot, void* dx, void* dqkv, void* o, void* xn, float* dbias_part,
+                             float* dgamma_part, dim3 grid, int F, int HW, float scale, hipStream_t stream) {
+  const size_t sm = tw_bwd_smem<C>(F);
+  allow_smem(tw_bwd_kernel<C, NV>, sm);
+  tw_bwd_kernel<C, NV><<<grid, 256, sm, stream>>>((const bf16*)x, (const bf16*)dy, gamma, mr, lse, (const bf16*)wqkv,
+                                                  (const bf16*)wqkv_t, (const bf16*)wout_t, bias, rot, (bf16*)dx,
+                                                  (bf16*)dqkv, (bf16*)o, (bf16*)xn, dbias_part, dgamma_part, F, HW,
+                                                  scale);
+}
+
+template <int C>
+static int tw_bwd_launch(const void* x, const void* dy, const float* gamma, const float* mr, const float* lse,
+                         const void* wqkv, const void* wqkv_t, const void* wout_t, const float* bias, const float* rot,
+                         void* dx, void* dqkv, void* o, void* xn, float* dbias_part, float* dgamma_part, dim3 grid,
+                         int F, int HW, float scale, hipStream_t stream) {
+  const int nv = (TW<C>::PW * F + 15) / 16;
+#define TWB_ARGS x, dy, gamma, mr, lse, wqkv, wqkv_t, wout_t, bias, rot, dx, dqkv, o, xn, dbias_part, dgamma_part, grid, F, HW, scale, stream
+  switch (nv) {
+    case 1: tw_bwd_launch_nv<C, 1>(TWB_ARGS); break;
+    case 2:
+      if constexpr (TW<C>::PW >= 2) { tw_bwd_launch_nv<C, 2>(TWB_ARGS); break; }
+      return CESM_EUNSUPPORTED;
+    case 3:
+      if constexpr (TW<C>::PW >= 3) { tw_bwd_launch_nv<C, 3>(TWB_ARGS); break; }
+      return CESM_EUNSUPPORTED;
+    case 4:
+      if constexpr (TW<C>::PW >= 4) { tw_bwd_launch_nv<C, 4>(TWB_ARGS); break; }
+      return CESM_EUNSUPPORTED;
+    default:
+      return CESM_EUNSUPPORTED;
+  }
+#undef TWB_ARGS
+  return CESM_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -231,21 +1268,71 @@ int cesm_tblock_fwd(const void* x, const float* gamma, const void* wqkv, const v
                     float eps, hipStream_t stream) {
   if (F < 1 || F > 16) return CESM_EUNSUPPORTED;
   switch (C) {
-#define TB_CASE(CC)                                                                                            \
-  case CC: {                                                                                                   \
-    dim3 grid((unsigned)cdiv(HW, TB<CC>::P), B);                                                               \
-    tblock_fwd_kernel<CC><<<grid, 256, 0, stream>>>((const bf16*)x, gamma, (const bf16*)wqkv, (const bf16*)wout, \
-                                                    bias, rot, (bf16*)y, mr, lse, F, HW, scale, eps);          \
-    break;                                                                                                     \
-  }
-    TB_CASE(64)
-    TB_CASE(128)
-    TB_CASE(256)
-    TB_CASE(512)
-#undef TB_CASE
+    case 64: return tw_fwd_launch<64>(x, gamma, wqkv, wout, bias, rot, y, mr, lse, B, F, HW, scale, eps, stream);
+    case 128: return tw_fwd_launch<128>(x, gamma, wqkv, wout, bias, rot, y, mr, lse, B, F, HW, scale, eps, stream);
+    case 256: return tw_fwd_launch<256>(x, gamma, wqkv, wout, bias, rot, y, mr, lse, B, F, HW, scale, eps, stream);
+    case 512: {
+      dim3 grid((unsigned)cdiv(HW, TB<512>::P), B);
+      tblock_fwd_kernel<512><<<grid, 256, 0, stream>>>((const bf16*)x, gamma, (const bf16*)wqkv, (const bf16*)wout,
+                                                       bias, rot, (bf16*)y, mr, lse, F, HW, scale, eps);
+      break;
+    }
     default:
       return CESM_EUNSUPPORTED;
   }
+  return cesm_launch_status();
+}
+
+static int tb_bwd_P(int C) { return C >= 256 ? 1 : 256 / C; }
+
+// blocks per sample used by cesm_tblock_bwd (grid-stride over pixel groups)
+int cesm_tblock_bwd_nblk(int B, int F, int HW, int C) {
+  (void)F;
+  if (C <= 256) {
+    const int pw = C <= 64 ? 4 : (C == 128 ? 2 : 1);
+    const int nwg = (int)cdiv(cdiv(HW, pw), 4);  // 4 waves per block, one pixel group each
+    const int target = std::max(1, 512 / std::max(B, 1));
+    return std::min(nwg, target);
+  }
+  const int npg = (int)cdiv(HW, tb_bwd_P(C));
+  const int target = std::max(1, 1024 / std::max(B, 1));
+  return std::min(npg, target);
+}
+
+// Fused backward of the temporal-attention block (dx path). x, dy, dx [B*F*HW][C] bf16; gamma [C];
+// mr, lse from cesm_tblock_fwd; wqkv [768][C], wqkv_t [C][768], wout_t [256][C] packed bf16.
+// Emits (each may be null) dqkv [B*F*HW][768], o [B*F*HW][256], xn [B*F*HW][C] bf16 for the weight
+// gradients; dbias_part [B][8][nblk][F][F] (cesm_relpos_bwd layout); dgamma (+)= sum dxn*xhat
+// through dgamma_part [B*nblk][C].
+int cesm_tblock_bwd(const void* x, const void* dy, const float* gamma, const float* mr, const float* lse,
+                    const void* wqkv, const void* wqkv_t, const void* wout_t, const float* bias, const float* rot,
+                    void* dx, void* dqkv, void* o, void* xn, float* dbias_part, float* dgamma, float* dgamma_part,
+                    int nblk, int B, int F, int HW, int C, float scale, int accumulate, hipStream_t stream) {
+  if (F < 1 || F > 16 || nblk < 1) return CESM_EUNSUPPORTED;
+  dim3 grid(nblk, B);
+  switch (C) {
+    case 64:
+    case 128:
+    case 256: {
+      const int rc = C == 64 ? tw_bwd_launch<64>(x, dy, gamma, mr, lse, wqkv, wqkv_t, wout_t, bias, rot, dx, dqkv, o, xn,
+                                                 dbias_part, dgamma_part, grid, F, HW, scale, stream)
+                   : C == 128 ? tw_bwd_launch<128>(x, dy, gamma, mr, lse, wqkv, wqkv_t, wout_t, bias, rot, dx, dqkv, o, xn,
+                                                   dbias_part, dgamma_part, grid, F, HW, scale, stream)
+                              : tw_bwd_launch<256>(x, dy, gamma, mr, lse, wqkv, wqkv_t, wout_t, bias, rot, dx, dqkv, o, xn,
+                                                   dbias_part, dgamma_part, grid, F, HW, scale, stream);
+      if (rc) return rc;
+      break;
+    }
+    case 512:
+      tblock_bwd_kernel<512><<<grid, 256, 0, stream>>>(
+          (const bf16*)x, (const bf16*)dy, gamma, mr, lse, (const bf16*)wqkv, (const bf16*)wqkv_t,
+          (const bf16*)wout_t, bias, rot, (bf16*)dx, (bf16*)dqkv, (bf16*)o, (bf16*)xn, dbias_part, dgamma_part, F, HW,
+          scale);
+      break;
+    default:
+      return CESM_EUNSUPPORTED;
+  }
+  if (dgamma) tb_sum_rows_kernel<<<C, 64, 0, stream>>>(dgamma_part, dgamma, B * nblk, C, accumulate);
   return cesm_launch_status();
 }
 

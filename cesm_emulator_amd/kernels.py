@@ -257,6 +257,38 @@ def tblock_fwd(x, gamma, wqkv, wout, bias, rot, B, F, scale, save=True, eps=1e-5
     return y, mr, lse
 
 
+def tblock_bwd(x, dy, gamma, mr, lse, wqkv, wqkv_t, wout_t, bias, rot, dgamma, dtable, B, F, scale,
+               want_wgrad_inputs=True, num_buckets=32, max_distance=32):
+    """fused temporal-attention block backward, dx path (bf16).  Returns (dx, dqkv, o, xn); the last
+    three ([.., 768], [.., 256], [.., C] bf16) feed the to_qkv / to_out weight-gradient GEMMs."""
+    Nb, H, W, C = x.shape
+    HW = H * W
+    _chk(x, dtype=torch.bfloat16)
+    _chk(dy, x.shape, torch.bfloat16)
+    _chk(wqkv, (768, C), torch.bfloat16)
+    _chk(wqkv_t, (C, 768), torch.bfloat16)
+    _chk(wout_t, (256, C), torch.bfloat16)
+    if Nb != B * F or mr.shape != (Nb * HW, 2) or lse.shape != (B, 8, HW, F):
+        raise ValueError("tblock_bwd: saved statistics do not match x")
+    dev = x.device
+    dx = empty(x.shape, x.dtype, dev)
+    if want_wgrad_inputs:
+        dqkv = empty((Nb, H, W, 768), x.dtype, dev)
+        o = empty((Nb, H, W, 256), x.dtype, dev)
+        xn = empty(x.shape, x.dtype, dev)
+    else:
+        dqkv = o = xn = None
+    nblk = lib().cesm_tblock_bwd_nblk(B, F, HW, C)
+    dbp = empty((B, 8, nblk, F, F), torch.float32, dev)
+    dgp = empty((B * nblk, C), torch.float32, dev)
+    call("cesm_tblock_bwd", P(x), P(dy), P(gamma), P(mr), P(lse), P(wqkv), P(wqkv_t), P(wout_t), P(bias), P(rot),
+         P(dx), P(dqkv), P(o), P(xn), P(dbp), P(dgamma), P(dgp), nblk, B, F, HW, C, float(scale), 1, S())
+    if dtable is not None:
+        ws = empty((8, F, F), torch.float32, dev)
+        call("cesm_relpos_bwd", P(dbp), nblk, B, P(dtable), P(ws), F, 8, num_buckets, max_distance, 1, S())
+    return dx, dqkv, o, xn
+
+
 def sla_fwd(qkv, Nf, HW, scale):
     nchunk = lib().cesm_sla_nchunk(HW)
     out = empty((qkv.shape[0], 256), qkv.dtype, qkv.device)

@@ -14,6 +14,7 @@ Autograd sees the network as ONE node (`_NetFunction`): loss.backward() calls
 from __future__ import annotations
 
 import math
+import os
 from types import SimpleNamespace
 
 import torch
@@ -273,18 +274,33 @@ def resnet_bwd(rc, rb, st, dout):
     return dx  # tensor, or (dx1, dx2) for concat inputs
 
 
+FUSED_TBLOCK = os.environ.get("CESM_NO_FUSED_TBLOCK", "0") != "1"
+
+
+def _tblock_fused(rc, C):
+    return FUSED_TBLOCK and rc.cdt == torch.bfloat16 and rc.F <= 16 and C in K.TBLOCK_C
+
+
 def tattn_fwd(rc, res_mod, x):
-    """Residual(PreNorm(EinopsToAndFrom(Attention))) over frames (video_net.py:368-454)."""
+    """Residual(PreNorm(EinopsToAndFrom(Attention))) over frames (video_net.py:368-454).
+    bf16: one fused kernel (csrc/tblock.hip); fp32 parity mode: LN -> to_qkv -> core -> to_out."""
     pre = res_mod.fn
     attn = pre.fn.fn
+    Nb, H, W, C = x.shape
+    HW = H * W
+    if _tblock_fused(rc, C):
+        wq = rc.packed(attn.to_qkv.weight, 768, C, 1, 1, 0, 0)
+        wo = rc.packed(attn.to_out.weight, C, 256, 1, 1, 0, 0)
+        y, mr, lse = K.tblock_fwd(x, _flat(pre.norm.gamma), wq, wo, rc.bias, rc.rot, rc.B, rc.F, attn.scale,
+                                  save=rc.save, eps=pre.norm.eps)
+        st = SimpleNamespace(fused=True, x=x, mr=mr, lse=lse) if rc.save else None
+        return y, st
     n, mr = K.ln_fwd(x, _flat(pre.norm.gamma), save=rc.save, eps=pre.norm.eps)
     qspec, ospec = ConvSpec(attn.to_qkv), ConvSpec(attn.to_out)
     qkv, qst = conv_forward(rc, qspec, n)
-    Nb, H, W, _ = x.shape
-    HW = H * W
     o, lse = K.tattn_fwd(qkv.view(-1, 768), rc.bias, rc.rot, rc.B, rc.F, HW, attn.scale, save=rc.save)
     y, ost = conv_forward(rc, ospec, o.view(Nb, H, W, 256), None, res=x)
-    st = SimpleNamespace(x=x, mr=mr, qkv=qkv, o=o, lse=lse, qst=qst, ost=ost) if rc.save else None
+    st = SimpleNamespace(fused=False, x=x, mr=mr, qkv=qkv, o=o, lse=lse, qst=qst, ost=ost) if rc.save else None
     return y, st
 
 
@@ -292,6 +308,20 @@ def tattn_bwd(rc, res_mod, st, dy):
     pre = res_mod.fn
     attn = pre.fn.fn
     Nb, H, W, C = st.x.shape
+    if st.fused:
+        wq = rc.packed(attn.to_qkv.weight, 768, C, 1, 1, 0, 0)
+        wq_t = rc.packed(attn.to_qkv.weight, C, 768, 1, 1, 1, 1)
+        wo_t = rc.packed(attn.to_out.weight, 256, C, 1, 1, 1, 1)
+        dwq, dwo = gbuf(attn.to_qkv.weight), gbuf(attn.to_out.weight)
+        want = dwq is not None or dwo is not None
+        dx, dqkv, o, xn = K.tblock_bwd(st.x, dy, _flat(pre.norm.gamma), st.mr, st.lse, wq, wq_t, wo_t, rc.bias,
+                                       rc.rot, gbuf(pre.norm.gamma), rc.dtable, rc.B, rc.F, attn.scale,
+                                       want_wgrad_inputs=want)
+        if dwq is not None:
+            K.conv_wgrad(xn, None, dqkv, None, dwq, (H, W, 768, 1, 1, 1, 0, 1), 0, 0)
+        if dwo is not None:
+            K.conv_wgrad(o, None, dy, None, dwo, (H, W, C, 1, 1, 1, 0, 1), 0, 0)
+        return dx
     do = conv_backward(rc, ConvSpec(attn.to_out), st.ost, dy)
     dqkv = K.tattn_bwd(st.qkv.view(-1, 768), st.o, do.view(-1, 256), st.lse, rc.bias, rc.rot, rc.dtable, rc.B,
                        rc.F, H * W, attn.scale)

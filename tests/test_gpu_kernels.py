@@ -444,3 +444,59 @@ def test_fused_temporal_block_forward(dev, C, Fr):
     # saved LN stats match
     xv = q(x, torch.bfloat16).permute(0, 2, 3, 4, 1).reshape(-1, C)
     torch.testing.assert_close(mr[:, 0].cpu().double(), xv.mean(1), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("C", [64, 128, 256, 512])
+@pytest.mark.parametrize("Fr", [1, 5, 12])
+def test_fused_temporal_block_backward(dev, C, Fr):
+    """cesm_tblock_bwd (recompute + MFMA core backward + LN backward in one kernel) and the weight
+    gradients built from its dqkv/o/xn outputs vs float64 autograd through the reference block"""
+    torch.manual_seed(12)
+    B, H, W = 2, 5, 7
+    rot_mod = VN.RotaryEmbedding(32)
+    res_mod = VN.Residual(VN.PreNorm(C, VN.EinopsToAndFrom(VN.Attention(C, 8, 32, rot_mod)))).to(dev)
+    with torch.no_grad():
+        res_mod.fn.norm.gamma.uniform_(0.5, 1.5)
+    attn = res_mod.fn.fn.fn
+    x = q(torch.randn(B, C, Fr, H, W), torch.bfloat16)
+    g = q(torch.randn(B, C, Fr, H, W), torch.bfloat16)
+    table = torch.randn(32, 8)
+    rc = make_rc(B, Fr, torch.bfloat16)
+    rc.bias = K.relpos_fwd(table.to(dev), Fr)
+    rc.rot = K.rope_table(rot_mod.freqs.to(dev), Fr)
+    xd = to_cl(x).to(dev, torch.bfloat16)
+    gd = to_cl(g).to(dev, torch.bfloat16)
+    wqkv, wout = attn.to_qkv.weight.detach(), attn.to_out.weight.detach()
+    wq = K.conv_pack(wqkv, torch.bfloat16, 768, C, 1, 1, 0, 0)
+    wo = K.conv_pack(wout, torch.bfloat16, C, 256, 1, 1, 0, 0)
+    wq_t = K.conv_pack(wqkv, torch.bfloat16, C, 768, 1, 1, 1, 1)
+    wo_t = K.conv_pack(wout, torch.bfloat16, 256, C, 1, 1, 1, 1)
+    gamma = res_mod.fn.norm.gamma.detach().reshape(-1).contiguous()
+    _, mr, lse = K.tblock_fwd(xd, gamma, wq, wo, rc.bias, rc.rot, B, Fr, attn.scale)
+    dgamma = torch.zeros(C, device=dev)
+    dtable = torch.zeros(32, 8, device=dev)
+    dx, dqkv, o, xn = K.tblock_bwd(xd, gd, gamma, mr, lse, wq, wq_t, wo_t, rc.bias, rc.rot, dgamma, dtable, B, Fr,
+                                   attn.scale)
+    dwq = dqkv.reshape(-1, 768).double().t() @ xn.reshape(-1, C).double()
+    dwo = gd.reshape(-1, C).double().t() @ o.reshape(-1, 256).double()
+    # float64 reference
+    from oracle import ref_cpu as R
+    ref = R.Residual(R.PreNorm(C, R.EinopsToAndFrom(R.Attention(C, 8, 32, R.RotaryEmbedding(32))))).double()
+    ref.fn.norm.gamma.data.copy_(gamma.cpu().double().view_as(ref.fn.norm.gamma))
+    ref.fn.fn.fn.to_qkv.weight.data.copy_(wqkv.cpu().to(torch.bfloat16).double())
+    ref.fn.fn.fn.to_out.weight.data.copy_(wout.cpu().to(torch.bfloat16).double())
+    rp = R.RelativePositionBias(8, 32, 32).double()
+    rp.relative_attention_bias.weight.data.copy_(table.double())
+    xr = x.double().requires_grad_(True)
+    yr = ref(xr, pos_bias=rp(Fr))
+    (yr * g.double()).sum().backward()
+    errs = {
+        "dx": rel(from_cl(dx, B), xr.grad),
+        "dgamma": rel(dgamma.double(), ref.fn.norm.gamma.grad.reshape(-1)),
+        "dtable": rel(dtable.double(), rp.relative_attention_bias.weight.grad),
+        "dWqkv": rel(dwq, ref.fn.fn.fn.to_qkv.weight.grad),
+        "dWout": rel(dwo, ref.fn.fn.fn.to_out.weight.grad),
+    }
+    print(f"fused tblock bwd C={C} F={Fr}: " + " ".join(f"{k} {v:.2e}" for k, v in errs.items()))
+    for k, v in errs.items():
+        assert v < 3e-2, (k, v)
