@@ -4,6 +4,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 #define CESM_OK 0
 #define CESM_EINVAL -1
@@ -80,6 +81,22 @@ __device__ __forceinline__ float silu_p(float x) { return x / (1.f + expf(-x)); 
 __device__ __forceinline__ float dsilu_p(float x) {
   const float s = 1.f / (1.f + expf(-x));
   return s * (1.f + x * (1.f - s));
+}
+
+// storage-dtype dispatch: fp32 (parity mode) keeps expf + IEEE division, bf16 uses v_exp/v_rcp
+__device__ __forceinline__ float fast_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+template <typename T>
+__device__ __forceinline__ float silu_t(float x) {
+  if constexpr (std::is_same<T, float>::value) return silu_p(x);
+  else return x * fast_sigmoid(x);
+}
+template <typename T>
+__device__ __forceinline__ float dsilu_t(float x) {
+  if constexpr (std::is_same<T, float>::value) return dsilu_p(x);
+  else {
+    const float s = fast_sigmoid(x);
+    return s * (1.f + x * (1.f - s));
+  }
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

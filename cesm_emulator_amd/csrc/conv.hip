@@ -864,6 +864,115 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(const float* __restrict
   }
 }
 
+// bf16 stem dW on MFMA: dW[co][tap] = sum_px dy[px][co] * X[ci][y+ky-P][x+kx-P]  (tap = (ci,ky,kx)).
+// Block = 8x32-pixel tiles (grid-stride), 4 waves = 4 output-channel tiles of 16 (Co slice of 64);
+// each wave accumulates all <=7 tap tiles (98 taps padded to 112).  k-step = 32 pixels of one row.
+//   A = dy^T fragment via ds_read_b64_tr_b16 from the [256 px][64 co] bf16 tile (XOR-swizzled chunks)
+//   B = im2col fragment: 8 consecutive x of tap (ci,ky,kx) — read 16-B aligned from kx-shifted bf16
+//       copies tin_k[kx][ci][row][32] of the input halo (so every tap's 8-pixel run is aligned)
+constexpr int SW_TH = 8, SW_TW = 32;
+__device__ __forceinline__ int sw_dy_off(int px, int co) {  // bf16 index in the [256][64] dy tile
+  return px * 64 + ((((co >> 3) ^ (px & 7))) << 3) + (co & 7);
+}
+__global__ __launch_bounds__(256) void stem_wgrad_mfma_kernel(const float* __restrict__ xt, const float* __restrict__ cond,
+                                                              const bf16* __restrict__ dy, float* __restrict__ part,
+                                                              int F, int Fx, int Fc, int H, int W, int Co, int KS,
+                                                              int ntiles) {
+  const int PAD = KS / 2;
+  const int IH = SW_TH + KS - 1, IW = SW_TW + KS - 1;  // <= 14 x 38
+  const int NT = 2 * KS * KS;                          // taps (<= 98)
+  __shared__ float tin[2 * 14 * 38];
+  __shared__ __attribute__((aligned(16))) bf16 tink[7 * 2 * 14 * SW_TW];
+  __shared__ __attribute__((aligned(16))) bf16 tdy[SW_TH * SW_TW * 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int cog = blockIdx.y * 64;
+  // per-lane tap offsets into tink for each of the 7 tap tiles (-1: padded tap)
+  int toff[7];
+#pragma unroll
+  for (int nt = 0; nt < 7; ++nt) {
+    const int t = nt * 16 + lr;
+    if (t < NT) {
+      const int ci = t / (KS * KS), r = t - ci * KS * KS, ky = r / KS, kx = r - ky * KS;
+      toff[nt] = ((kx * 2 + ci) * 14 + ky) * SW_TW + lg * 8;
+    } else {
+      toff[nt] = -1;
+    }
+  }
+  f32x4 acc[7];
+#pragma unroll
+  for (int nt = 0; nt < 7; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int tx_tiles = (W + SW_TW - 1) / SW_TW, ty_tiles = (H + SW_TH - 1) / SW_TH;
+  const int per_img = tx_tiles * ty_tiles;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int n = tile / per_img;
+    const int rem = tile - n * per_img;
+    const int ty0 = (rem / tx_tiles) * SW_TH, tx0 = (rem % tx_tiles) * SW_TW;
+    const int b = n / F, f = n - b * F;
+    const float* s0 = xt + ((int64_t)b * Fx + (Fx == 1 ? 0 : f)) * H * W;
+    const float* s1 = cond + ((int64_t)b * Fc + (Fc == 1 ? 0 : f)) * H * W;
+    __syncthreads();  // previous tile's readers done
+    for (int e = tid; e < IH * IW; e += 256) {
+      const int yy = ty0 - PAD + e / IW, xx = tx0 - PAD + e % IW;
+      const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+      tin[e] = ok ? s0[(int64_t)yy * W + xx] : 0.f;
+      tin[IH * IW + e] = ok ? s1[(int64_t)yy * W + xx] : 0.f;
+    }
+    for (int e = tid; e < SW_TH * SW_TW * 8; e += 256) {  // dy: 256 px x 8 chunks of 8 co
+      const int px = e >> 3, ch = e & 7;
+      const int yy = ty0 + px / SW_TW, xx = tx0 + px % SW_TW;
+      bf16x8 v;
+      if (yy < H && xx < W) v = *reinterpret_cast<const bf16x8*>(dy + (((int64_t)n * H + yy) * W + xx) * Co + cog + ch * 8);
+      else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = (bf16)0.f;
+      }
+      *reinterpret_cast<bf16x8*>(tdy + sw_dy_off(px, ch * 8)) = v;
+    }
+    __syncthreads();
+    for (int e = tid; e < KS * 2 * IH * SW_TW; e += 256) {  // kx-shifted bf16 copies
+      const int x = e % SW_TW, r = e / SW_TW;
+      const int row = r % IH, r2 = r / IH, ci = r2 & 1, kx = r2 >> 1;
+      tink[((kx * 2 + ci) * 14 + row) * SW_TW + x] = (bf16)tin[ci * IH * IW + row * IW + x + kx];
+    }
+    __syncthreads();
+#pragma unroll 2
+    for (int py = 0; py < SW_TH; ++py) {
+      // A: dy^T[co = wid*16 + i][px = py*32 + 8g + e]
+      bf16x8 a;
+      const int q = (lane >> 2) & 3, p4 = (lane & 3) * 4;
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const int px = py * SW_TW + lg * 8 + hf * 4 + q;
+        const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tdy + sw_dy_off(px, wid * 16 + p4)));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a[hf * 4 + e] = __builtin_bit_cast(bf16, (short)v[e]);
+      }
+#pragma unroll
+      for (int nt = 0; nt < 7; ++nt) {
+        bf16x8 bb;
+        if (toff[nt] >= 0) bb = *reinterpret_cast<const bf16x8*>(tink + toff[nt] + py * SW_TW);
+        else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) bb[i] = (bf16)0.f;
+        }
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb, acc[nt], 0, 0, 0);
+      }
+    }
+  }
+  // D[co = wid*16 + 4g + r][tap = nt*16 + i]
+#pragma unroll
+  for (int nt = 0; nt < 7; ++nt) {
+    const int t = nt * 16 + lr;
+    if (t >= NT) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = cog + wid * 16 + lg * 4 + r;
+      part[((int64_t)blockIdx.x * Co + co) * NT + t] = acc[nt][r];
+    }
+  }
+}
+
 __global__ void sum_partials_kernel(const float* __restrict__ part, float* __restrict__ dst, int nsplit, int64_t n,
                                     int accumulate) {
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
@@ -1085,8 +1194,7 @@ int cesm_stem_wgrad(int dtype, const float* xt, const float* cond, const void* d
   const int ntiles = B * F * (int)cdiv(H, 8) * (int)cdiv(W, 32);
   dim3 grid(nblk, Co / 64);
   if (dtype == CESM_DT_BF16)
-    stem_wgrad_kernel<bf16><<<grid, 256, 0, stream>>>(xt, cond, (const bf16*)dy, part, B, F, Fx, Fc, H, W, Co, KS,
-                                                      ntiles);
+    stem_wgrad_mfma_kernel<<<grid, 256, 0, stream>>>(xt, cond, (const bf16*)dy, part, F, Fx, Fc, H, W, Co, KS, ntiles);
   else if (dtype == CESM_DT_F32)
     stem_wgrad_kernel<float><<<grid, 256, 0, stream>>>(xt, cond, (const float*)dy, part, B, F, Fx, Fc, H, W, Co, KS,
                                                        ntiles);

@@ -121,7 +121,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ y, 
     if (res) load8(res + off + r * C, rv);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const float a = silu_p(fmaf(v[i], A1[i], A0[i]));
+      const float a = silu_t<T>(fmaf(v[i], A1[i], A0[i]));
       v[i] = res ? a + rv[i] : a;
     }
     store8(out + off + r * C, v);
@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256) void gn_bwd_reduce_kernel(const T* __restrict_
       load8(dout + off + r * C, d);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const float da = d[i] * dsilu_p(fmaf(v[i], A1[i], A0[i]));
+        const float da = d[i] * dsilu_t<T>(fmaf(v[i], A1[i], A0[i]));
         s1[i] += da;
         s3[i] = fmaf(da, v[i], s3[i]);
       }
@@ -261,7 +261,7 @@ __global__ __launch_bounds__(256) void gn_bwd_apply_kernel(const T* __restrict__
     load8(dout + off + r * C, d);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const float da = d[i] * dsilu_p(fmaf(v[i], A1[i], A0[i]));
+      const float da = d[i] * dsilu_t<T>(fmaf(v[i], A1[i], A0[i]));
       d[i] = fmaf(da, E1[i], fmaf(v[i], E2[i], E3[i]));
     }
     store8(dy + off + r * C, d);

@@ -22,20 +22,33 @@ __global__ void sinusoidal_kernel(const int64_t* __restrict__ t, float* __restri
 }
 
 // y[r][o] = bias[o] + sum_i act(x[r][i]) * W[o][i]; act = silu if silu_in
+// one wave per output feature o (coalesced W row), rows r looped (R = batch, small)
 __global__ void linear_small_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                         const float* __restrict__ bias, float* __restrict__ y, int R, int I, int O,
                                         int silu_in) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= R * O) return;
-  const int r = t / O, o = t % O;
-  float s = bias ? bias[o] : 0.f;
-  const float* xr = x + (int64_t)r * I;
+  const int o = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (o >= O) return;
   const float* wr = w + (int64_t)o * I;
-  for (int i = 0; i < I; ++i) {
-    const float xv = silu_in ? silu_p(xr[i]) : xr[i];
-    s = fmaf(xv, wr[i], s);
+  for (int r0 = 0; r0 < R; r0 += 8) {
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int i = lane; i < I; i += 64) {
+      const float wv = wr[i];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if (r0 + k < R) {
+          const float xv = x[(int64_t)(r0 + k) * I + i];
+          s[k] = fmaf(silu_in ? silu_p(xv) : xv, wv, s[k]);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (r0 + k >= R) break;
+      const float t = wave_sum(s[k]);
+      if (lane == 0) y[(int64_t)(r0 + k) * O + o] = t + (bias ? bias[o] : 0.f);
+    }
   }
-  y[t] = s;
 }
 
 // dx[r][i] (+)= act'(x) * sum_o dy[r][o] W[o][i]
@@ -243,7 +256,7 @@ int cesm_sinusoidal(const int64_t* t, float* emb, int B, int dim, hipStream_t st
 
 int cesm_linear_small_fwd(const float* x, const float* w, const float* bias, float* y, int R, int I, int O,
                           int silu_in, hipStream_t stream) {
-  linear_small_fwd_kernel<<<(unsigned)cdiv(R * O, 256), 256, 0, stream>>>(x, w, bias, y, R, I, O, silu_in);
+  linear_small_fwd_kernel<<<(unsigned)cdiv(O, 4), 256, 0, stream>>>(x, w, bias, y, R, I, O, silu_in);
   return cesm_launch_status();
 }
 

@@ -636,6 +636,33 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 __device__ __forceinline__ bf16x8 ld16(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
+constexpr int RS = 36;  // RoPE table row stride (floats): 16-B aligned, spreads frames over banks
+constexpr float LOG2E = 1.4426950408889634f;
+
+// k-slot gather with the hardware transpose read: lane (g, i) gets tile[rb + 4g + e][c0 + i] in
+// element e (e < 4; elements 4..7 and rows >= F are zero).  Must run with EXEC all ones.
+__device__ __forceinline__ bf16x8 kslot_gather(const bf16* tile, int rb, int c0, int F, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tile + (rb + 4 * g + q) * HLD + c0 + 4 * p));
+  bf16x8 r = zero8();
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    if (4 * g + e < F) r[e] = __builtin_bit_cast(bf16, (short)v[e]);
+  return r;
+}
+
+// RoPE rotation of 4 consecutive head dims d0..d0+3 (two pairs) of frame f; sign=-1 applies R^T
+__device__ __forceinline__ void rope4(float* o4, const float* rot, int f, int d0, float sign) {
+  const f32x4 cs = *reinterpret_cast<const f32x4*>(rot + f * RS + d0);  // (c0, s0, c1, s1)
+#pragma unroll
+  for (int pr = 0; pr < 2; ++pr) {
+    const float c = cs[2 * pr], sn = sign * cs[2 * pr + 1];
+    const float a0 = o4[2 * pr], a1 = o4[2 * pr + 1];
+    o4[2 * pr] = a0 * c - a1 * sn;
+    o4[2 * pr + 1] = a1 * c + a0 * sn;
+  }
+}
+
 // rows of voxel v of the wave's pixel group
 __device__ __forceinline__ bool tw_row(int v, int VW, int F, int p0, int HW, int b, int64_t& row) {
   if (v >= VW) return false;
@@ -648,7 +675,7 @@ __device__ __forceinline__ bool tw_row(int v, int VW, int F, int p0, int HW, int
 // q'|k'|v tiles (and the RoPE/scale epilogue) of head h for the wave's NVT voxel tiles
 template <int C, int NV>
 __device__ __forceinline__ void tw_qkv(const bf16* __restrict__ wqkv, const bf16x8 (&xf)[TW<C, NV>::NVTM][TW<C, NV>::KS],
-                                       int h, int NVT, int F, float scale, const float* rot, bf16* sq, bf16* sk,
+                                       int h, const int (&fr)[NV], float scale, const float* rot, bf16* sq, bf16* sk,
                                        bf16* sv, int lr, int lg) {
   using T = TW<C, NV>;
 #pragma unroll
@@ -661,30 +688,17 @@ __device__ __forceinline__ void tw_qkv(const bf16* __restrict__ wqkv, const bf16
     bf16* dst = kind == 0 ? sq : (kind == 1 ? sk : sv);
     const int d0 = (ct & 1) * 16 + lg * 4;
 #pragma unroll
-    for (int vt = 0; vt < T::NVTM; ++vt) {
-      if (vt < NVT) {
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int vt = 0; vt < NV; ++vt) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int ks = 0; ks < T::KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], xf[vt][ks], acc, 0, 0, 0);
-        const int v = vt * 16 + lr;
-        const int f = v % F;
-        float o4[4] = {acc[0], acc[1], acc[2], acc[3]};
-        if (kind == 0) {
+      for (int ks = 0; ks < T::KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], xf[vt][ks], acc, 0, 0, 0);
+      float o4[4] = {acc[0], acc[1], acc[2], acc[3]};
+      if (kind == 0) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) o4[r] *= scale;
-        }
-        if (kind < 2) {
-#pragma unroll
-          for (int pr = 0; pr < 2; ++pr) {
-            const int ri = (d0 >> 1) + pr;
-            const float c = rot[f * 32 + ri * 2], sn = rot[f * 32 + ri * 2 + 1];
-            const float a0 = o4[2 * pr], a1 = o4[2 * pr + 1];
-            o4[2 * pr] = a0 * c - a1 * sn;
-            o4[2 * pr + 1] = a1 * c + a0 * sn;
-          }
-        }
-        store4(dst + v * HLD + d0, o4);
+        for (int r = 0; r < 4; ++r) o4[r] *= scale;
       }
+      if (kind < 2) rope4(o4, rot, fr[vt], d0, 1.f);
+      store4(dst + (vt * 16 + lr) * HLD + d0, o4);
     }
   }
 }
@@ -749,22 +763,25 @@ __global__ __launch_bounds__(256) void tw_fwd_kernel(const bf16* __restrict__ x,
                                                      float* __restrict__ lse, int F, int HW, float scale, float eps) {
   using T = TW<C, NV>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* sb = smem;             // [8][F][F]
-  float* rot = smem + NH * 256; // [16][32]
+  float* sb = smem;             // [8][F][F], pre-scaled by log2(e)
+  float* rot = smem + NH * 256; // [16][RS]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const int b = blockIdx.y;
   const int VW = T::PW * F;
   constexpr int NVT = NV;
   const int R = NVT * 16;
-  bf16* sq = reinterpret_cast<bf16*>(rot + 512) + wid * 3 * R * HLD;
+  bf16* sq = reinterpret_cast<bf16*>(rot + 16 * RS) + wid * 3 * R * HLD;
   bf16* sk = sq + R * HLD;
   bf16* sv = sk + R * HLD;
-  for (int e = tid; e < NH * F * F; e += 256) sb[e] = bias[e];
-  for (int e = tid; e < F * 32; e += 256) rot[e] = rotg[e];
+  for (int e = tid; e < NH * F * F; e += 256) sb[e] = bias[e] * LOG2E;
+  for (int e = tid; e < F * 32; e += 256) rot[(e >> 5) * RS + (e & 31)] = rotg[e];
   __syncthreads();
   const int p0 = (blockIdx.x * 4 + wid) * T::PW;
   if (p0 >= HW) return;
+  int fr[NV];
+#pragma unroll
+  for (int vt = 0; vt < NV; ++vt) fr[vt] = (vt * 16 + lr) % F;
 
   bf16x8 xf[T::NVTM][T::KS];
   tw_ln<C, NV>(x, gamma, mr, nullptr, xf, NVT, VW, F, p0, HW, b, eps, lr, lg);
@@ -777,9 +794,9 @@ __global__ __launch_bounds__(256) void tw_fwd_kernel(const bf16* __restrict__ x,
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
 
   for (int h = 0; h < NH; ++h) {
-    tw_qkv<C, NV>(wqkv, xf, h, NVT, F, scale, rot, sq, sk, sv, lr, lg);
+    tw_qkv<C, NV>(wqkv, xf, h, fr, scale, rot, sq, sk, sv, lr, lg);
     wave_lds_sync();
-    // attention core per pixel; O overwrites the pixel's own q rows
+    // attention core per pixel (base-2 softmax); O overwrites the pixel's own q rows
     for (int pp = 0; pp < T::PW; ++pp) {
       const int p = p0 + pp;
       if (p >= HW) break;
@@ -792,7 +809,7 @@ __global__ __launch_bounds__(256) void tw_fwd_kernel(const bf16* __restrict__ x,
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int j = lg * 4 + r;
-        sc[r] = (j < F && lr < F) ? st[r] + sb[(h * F + lr) * F + j] : -INFINITY;
+        sc[r] = (j < F && lr < F) ? fmaf(st[r], LOG2E, sb[(h * F + lr) * F + j]) : -INFINITY;
         m = fmaxf(m, sc[r]);
       }
       m = fmaxf(m, __shfl_xor(m, 16, 64));
@@ -800,26 +817,19 @@ __global__ __launch_bounds__(256) void tw_fwd_kernel(const bf16* __restrict__ x,
       float pr[4], l = 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        pr[r] = sc[r] == -INFINITY ? 0.f : expf(sc[r] - m);
+        pr[r] = sc[r] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(sc[r] - m);
         l += pr[r];
       }
       l += __shfl_xor(l, 16, 64);
       l += __shfl_xor(l, 32, 64);
-      if (lse && lg == 0 && lr < F) lse[(((int64_t)b * NH + h) * HW + p) * F + lr] = m + logf(l);
+      if (lse && lg == 0 && lr < F) lse[(((int64_t)b * NH + h) * HW + p) * F + lr] = m + log2f(l);  // log2 units
       const float inv = lr < F ? 1.f / l : 0.f;
       bf16x8 pb = zero8();
 #pragma unroll
       for (int r = 0; r < 4; ++r) pb[r] = (bf16)(pr[r] * inv);
       bf16x8 va[2];
 #pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        va[half] = zero8();
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int j = lg * 4 + r;
-          if (j < F) va[half][r] = sv[(rb + j) * HLD + half * 16 + lr];
-        }
-      }
+      for (int half = 0; half < 2; ++half) va[half] = kslot_gather(sv, rb, half * 16, F, lane);
 #pragma unroll
       for (int half = 0; half < 2; ++half) {
         const f32x4 ot = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va[half], pb, z4, 0, 0, 0);
@@ -875,20 +885,20 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
   float* sb = smem;                  // [8][F][F]
   float* sdb = sb + NH * FF;         // [8][F][F] block dbias accumulator
   float* sg = sdb + NH * FF;         // [C] block dgamma accumulator
-  float* rot = sg + C;               // [16][32]
+  float* rot = sg + C;               // [16][RS]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const int b = blockIdx.y;
   const int VW = T::PW * F;
   constexpr int NVT = NV;
   const int R = NVT * 16;
-  bf16* sq = reinterpret_cast<bf16*>(rot + 512) + wid * 4 * R * HLD;
+  bf16* sq = reinterpret_cast<bf16*>(rot + 16 * RS) + wid * 4 * R * HLD;
   bf16* sk = sq + R * HLD;
   bf16* sv = sk + R * HLD;
   bf16* sdo = sv + R * HLD;
-  for (int e = tid; e < NH * FF; e += 256) { sb[e] = bias[e]; sdb[e] = 0.f; }
+  for (int e = tid; e < NH * FF; e += 256) { sb[e] = bias[e] * LOG2E; sdb[e] = 0.f; }
   for (int e = tid; e < C; e += 256) sg[e] = 0.f;
-  for (int e = tid; e < F * 32; e += 256) rot[e] = rotg[e];
+  for (int e = tid; e < F * 32; e += 256) rot[(e >> 5) * RS + (e & 31)] = rotg[e];
   __syncthreads();
 
   const int npg = (HW + T::PW - 1) / T::PW;
@@ -899,6 +909,9 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
 #pragma unroll
     for (int r = 0; r < 4; ++r) dgam[ct][r] = 0.f;
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  int fr[NV];
+#pragma unroll
+  for (int vt = 0; vt < NV; ++vt) fr[vt] = (vt * 16 + lr) % F;
 
   for (int pg = blockIdx.x * 4 + wid; pg < npg; pg += nw) {
     const int p0 = pg * T::PW;
@@ -921,7 +934,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
       for (int vt = 0; vt < T::NVTM; ++vt) dxacc[ct][vt] = z4;
 
     for (int h = 0; h < NH; ++h) {
-      tw_qkv<C, NV>(wqkv, xf, h, NVT, F, scale, rot, sq, sk, sv, lr, lg);
+      tw_qkv<C, NV>(wqkv, xf, h, fr, scale, rot, sq, sk, sv, lr, lg);
       // dO_h^T = W_out[:, h]^T . dy^T
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
@@ -965,7 +978,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
           for (int r = 0; r < 4; ++r) {
             const int j = lg * 4 + r;
             const bool ok = j < F && lr < F;
-            pt[r] = ok ? expf(st[r] + sb[(h * F + lr) * F + j] - Li) : 0.f;
+            pt[r] = ok ? __builtin_amdgcn_exp2f(fmaf(st[r], LOG2E, sb[(h * F + lr) * F + j]) - Li) : 0.f;
             D = fmaf(pt[r], dpt[r], D);
           }
           D += __shfl_xor(D, 16, 64);
@@ -982,16 +995,8 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
         f32x4 dqt[2];
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
-          bf16x8 kg = zero8(), vg = zero8();
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int j = lg * 4 + r;
-            if (j < F) {
-              const int o = (rb + j) * HLD + half * 16 + lr;
-              kg[r] = sk[o];
-              vg[r] = sv[o];
-            }
-          }
+          const bf16x8 kg = kslot_gather(sk, rb, half * 16, F, lane);
+          const bf16x8 vg = kslot_gather(sv, rb, half * 16, F, lane);
           dqt[half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kg, dst_b, z4, 0, 0, 0);  // dQ'^T[d][i]
           const f32x4 ot = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vg, pt_b, z4, 0, 0, 0);  // O^T[d][i]
           if (o_out && lr < F) {
@@ -1009,7 +1014,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
             const int i = lg * 4 + r;
             const float Lr = __shfl(Li, i, 64), Dr = __shfl(D, i, 64);
             const bool ok = i < F && lr < F;
-            const float pv = ok ? expf(s_[r] + sb[(h * F + i) * F + lr] - Lr) : 0.f;
+            const float pv = ok ? __builtin_amdgcn_exp2f(fmaf(s_[r], LOG2E, sb[(h * F + i) * F + lr]) - Lr) : 0.f;
             p_b[r] = (bf16)pv;
             ds_b[r] = (bf16)(ok ? pv * (dp_[r] - Dr) : 0.f);
           }
@@ -1017,16 +1022,8 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
         f32x4 dkt[2], dvt[2];
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
-          bf16x8 qg = zero8(), dog = zero8();
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int i = lg * 4 + r;
-            if (i < F) {
-              const int o = (rb + i) * HLD + half * 16 + lr;
-              qg[r] = sq[o];
-              dog[r] = sdo[o];
-            }
-          }
+          const bf16x8 qg = kslot_gather(sq, rb, half * 16, F, lane);
+          const bf16x8 dog = kslot_gather(sdo, rb, half * 16, F, lane);
           dkt[half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qg, ds_b, z4, 0, 0, 0);   // dK'^T[d][j]
           dvt[half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dog, p_b, z4, 0, 0, 0);   // dV^T[d][j]
         }
@@ -1038,17 +1035,10 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
             float q4[4] = {dqt[half][0], dqt[half][1], dqt[half][2], dqt[half][3]};
             float k4[4] = {dkt[half][0], dkt[half][1], dkt[half][2], dkt[half][3]};
             float v4[4] = {dvt[half][0], dvt[half][1], dvt[half][2], dvt[half][3]};
+            rope4(q4, rot, lr, d0, -1.f);  // dq = scale R^T dQ', dk = R^T dK' (frame lr)
+            rope4(k4, rot, lr, d0, -1.f);
 #pragma unroll
-            for (int pr = 0; pr < 2; ++pr) {  // dq = scale R^T dQ', dk = R^T dK' (frame lr)
-              const int ri = (d0 >> 1) + pr;
-              const float c = rot[lr * 32 + ri * 2], sn = rot[lr * 32 + ri * 2 + 1];
-              const float a0 = q4[2 * pr], a1 = q4[2 * pr + 1];
-              q4[2 * pr] = (a0 * c + a1 * sn) * scale;
-              q4[2 * pr + 1] = (a1 * c - a0 * sn) * scale;
-              const float b0 = k4[2 * pr], b1 = k4[2 * pr + 1];
-              k4[2 * pr] = b0 * c + b1 * sn;
-              k4[2 * pr + 1] = b1 * c - b0 * sn;
-            }
+            for (int r = 0; r < 4; ++r) q4[r] *= scale;
             store4(sq + (rb + lr) * HLD + d0, q4);
             store4(sk + (rb + lr) * HLD + d0, k4);
             store4(sv + (rb + lr) * HLD + d0, v4);
@@ -1172,12 +1162,12 @@ __global__ void tb_sum_rows_kernel(const float* __restrict__ part, float* __rest
 template <int C>
 static size_t tw_fwd_smem(int F) {  // NOLINT
   const int R = ((TW<C>::PW * F + 15) / 16) * 16;
-  return (size_t)(NH * 256 + 512) * 4 + (size_t)4 * 3 * R * HLD * 2;
+  return (size_t)(NH * 256 + 16 * RS) * 4 + (size_t)4 * 3 * R * HLD * 2;
 }
 template <int C>
 static size_t tw_bwd_smem(int F) {
   const int R = ((TW<C>::PW * F + 15) / 16) * 16;
-  return (size_t)(2 * NH * F * F + C + 512) * 4 + (size_t)4 * 4 * R * HLD * 2;
+  return (size_t)(2 * NH * F * F + C + 16 * RS) * 4 + (size_t)4 * 4 * R * HLD * 2;
 }
 template <typename K>
 static void allow_smem(K kernel, size_t bytes) {
