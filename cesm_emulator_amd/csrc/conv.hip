@@ -534,6 +534,156 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const T* __restrict__ x
 }
 
 // ----------------------------------------------------------------------------------------
+// bf16 weight gradient with wide output tiles: BM output channels x 64 K-columns (one tap, 64 input
+// channels) per block, pixels split over grid.z.  Same MFMA scheme as conv_wgrad_kernel (pixels are
+// the MFMA K axis, both operands read with ds_read_b64_tr_b16), but
+//   * BM = 128/256 rows amortise each input tile over 2-4x more output channels (fewer x re-reads);
+//   * the input pixel coordinates are advanced incrementally (no 64-bit div/mod per load);
+//   * wave w owns rows [w*BM/4, +BM/4) x all 64 columns.
+// ----------------------------------------------------------------------------------------
+template <int BM>
+__device__ __forceinline__ int wgb_swz(int r) {  // XOR on 4-element chunk index of a BM-wide row
+  if constexpr (BM == 64) return (((r >> 1) & 1) << 2) | (((r >> 3) & 1) << 3);
+  else return 4 * ((r & 3) | (((r >> 3) & 1) << 2));
+}
+
+template <int BM>
+__global__ __launch_bounds__(256) void wgrad_wide_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
+                                                         const bf16* __restrict__ dy1, const bf16* __restrict__ dy2,
+                                                         float* __restrict__ slab, ConvGeom g, int M, int px_per_split) {
+  constexpr int VPRY = BM / 8, RPPY = 256 / VPRY, NPY = WG_BP / RPPY;
+  constexpr int MT = BM / 64;  // 16-row co tiles per wave
+  __shared__ __attribute__((aligned(16))) bf16 tY[2][WG_BP * BM];
+  __shared__ __attribute__((aligned(16))) bf16 tX[2][WG_BP * 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int Cin = g.C1 + g.C2;
+  const int co0 = blockIdx.x * BM;
+  const int kcol0 = blockIdx.y * 64;
+  const int tap = kcol0 / Cin;
+  const int ci0 = kcol0 - tap * Cin;
+  const int ky = tap / g.KW, kx = tap - ky * g.KW;
+  const int pbeg = blockIdx.z * px_per_split;
+  const int pend = min(M, pbeg + px_per_split);
+  const bf16* xs; int xcs, xcc;
+  if (ci0 < g.C1) { xs = x1; xcs = g.C1; xcc = ci0; } else { xs = x2; xcs = g.C2; xcc = ci0 - g.C1; }
+  const bf16* ys; int ycs, ycc;
+  const int Co2 = g.Cout - g.Co1;
+  if (co0 < g.Co1) { ys = dy1; ycs = g.Co1; ycc = co0; } else { ys = dy2; ycs = Co2; ycc = co0 - g.Co1; }
+
+  // x-tile role: one 8-channel vector of one pixel row per thread; its output coordinates advance by
+  // WG_BP pixels per step
+  const int xrow = tid >> 3, xcol = (tid & 7) * 8;
+  int m = pbeg + xrow;
+  int ox, oy, on;
+  {
+    const int hw = g.Ho * g.Wo;
+    on = m / hw;
+    const int rem = m - on * hw;
+    oy = rem / g.Wo;
+    ox = rem - oy * g.Wo;
+  }
+  const int yrow0 = tid / VPRY, ycol = (tid % VPRY) * 8;
+
+  bf16x8 xr, yr[NPY];
+  auto gload = [&](int p0) {
+#pragma unroll
+    for (int p = 0; p < NPY; ++p) {
+      const int mm = p0 + yrow0 + p * RPPY;
+      if (mm < pend) yr[p] = *reinterpret_cast<const bf16x8*>(ys + (int64_t)mm * ycs + ycc + ycol);
+      else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) yr[p][i] = (bf16)0.f;
+      }
+    }
+    int iy, ix;
+    if (m < pend && tap_src(g, oy, ox, ky, kx, iy, ix))
+      xr = *reinterpret_cast<const bf16x8*>(xs + (((int64_t)on * g.Hi + iy) * g.Wi + ix) * xcs + xcc + xcol);
+    else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) xr[i] = (bf16)0.f;
+    }
+    // advance this thread's pixel by one step
+    m += WG_BP;
+    ox += WG_BP;
+    while (ox >= g.Wo) {
+      ox -= g.Wo;
+      if (++oy >= g.Ho) { oy = 0; ++on; }
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int p = 0; p < NPY; ++p) {
+      const int r = yrow0 + p * RPPY;
+      const int ch = (ycol >> 2) ^ wgb_swz<BM>(r);
+      *reinterpret_cast<bf16x8*>(tY[buf] + r * BM + ch * 4) = yr[p];
+    }
+    const int ch = (xcol >> 2) ^ wgb_swz<64>(xrow);
+    *reinterpret_cast<bf16x8*>(tX[buf] + xrow * 64 + ch * 4) = xr;
+  };
+
+  f32x4 acc[MT][4];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nsteps = (pend - pbeg + WG_BP - 1) / WG_BP;
+  if (nsteps > 0) {
+    gload(pbeg);
+    sstore(0);
+  }
+  __syncthreads();
+  const int q = lr >> 2, pp = lr & 3;
+  for (int s = 0; s < nsteps; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nsteps) gload(pbeg + (s + 1) * WG_BP);
+    bf16x8 af[MT], bfr[4];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const int c0 = wid * (BM / 4) + i * 16;
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const int r = lg * 8 + half * 4 + q;
+        const int ch = ((c0 >> 2) + pp) ^ wgb_swz<BM>(r);
+        const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tY[buf] + r * BM + ch * 4));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) af[i][half * 4 + e] = __builtin_bit_cast(bf16, (short)v[e]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const int r = lg * 8 + half * 4 + q;
+        const int ch = ((j * 16 >> 2) + pp) ^ wgb_swz<64>(r);
+        const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tX[buf] + r * 64 + ch * 4));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bfr[j][half * 4 + e] = __builtin_bit_cast(bf16, (short)v[e]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    if (s + 1 < nsteps) sstore(buf ^ 1);
+    __syncthreads();
+  }
+  const int K = g.KH * g.KW * Cin;
+  float* out = slab + (int64_t)blockIdx.z * g.Cout * K;
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int kc = kcol0 + j * 16 + lr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wid * (BM / 4) + i * 16 + lg * 4 + r;
+        out[(int64_t)co * K + kc] = acc[i][j][r];
+      }
+    }
+}
+
+// ----------------------------------------------------------------------------------------
 // 3x3 / stride 1 / pad 1 weight gradient (bf16), halo-tiled.  Block = (64 co) x (32 ci chunk) x
 // all 9 taps, looping over 8x32-pixel tiles (its share of the split-K over pixels).  Per tile the
 // dY tile [256 px][64 co] and the input halo [10x34 px][32 ci] are staged in LDS; pixels are the
@@ -670,22 +820,31 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_bf16_kernel(const bf16* __res
 // sum slabs over splits (fixed order) and scatter into the PyTorch weight layout
 // dst[((d0*D1 + d1)*KH + kyt)*KW + kxt], with (d0,d1) = swap ? (ci,co) : (co,ci) and
 // (kyt,kxt) = flip ? (KH-1-ky, KW-1-kx) : (ky,kx).
-__global__ void conv_wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ dst, int nsplit,
-                                         int Cout, int Cin, int KH, int KW, int swap, int flip, int accumulate) {
+// dst (+)= sum over the nsplit slabs, remapped to the PyTorch layout.  Block = 64 consecutive slab
+// elements x 4 split-groups (coalesced 256-B rows per split), fixed-order combine in LDS.
+__global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ dst,
+                                                                int nsplit, int Cout, int Cin, int KH, int KW, int swap,
+                                                                int flip, int accumulate) {
   const int64_t K = (int64_t)KH * KW * Cin;
   const int64_t total = (int64_t)Cout * K;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int k = 0; k < nsplit; ++k) s += slab[(int64_t)k * total + e];
-    const int co = (int)(e / K);
-    const int kc = (int)(e - (int64_t)co * K);
-    const int tap = kc / Cin, ci = kc - tap * Cin;
-    int ky = tap / KW, kx = tap - ky * KW;
-    if (flip) { ky = KH - 1 - ky; kx = KW - 1 - kx; }
-    const int d0 = swap ? ci : co, d1 = swap ? co : ci, D1 = swap ? Cout : Cin;
-    const int64_t di = (((int64_t)d0 * D1 + d1) * KH + ky) * KW + kx;
-    dst[di] = accumulate ? dst[di] + s : s;
-  }
+  const int64_t e = blockIdx.x * 64ll + (threadIdx.x & 63);
+  const int grp = threadIdx.x >> 6;
+  float s = 0.f;
+  if (e < total)
+    for (int k = grp; k < nsplit; k += 4) s += slab[(int64_t)k * total + e];
+  __shared__ float red[4][64];
+  red[grp][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (grp != 0 || e >= total) return;
+  s = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+  const int co = (int)(e / K);
+  const int kc = (int)(e - (int64_t)co * K);
+  const int tap = kc / Cin, ci = kc - tap * Cin;
+  int ky = tap / KW, kx = tap - ky * KW;
+  if (flip) { ky = KH - 1 - ky; kx = KW - 1 - kx; }
+  const int d0 = swap ? ci : co, d1 = swap ? co : ci, D1 = swap ? Cout : Cin;
+  const int64_t di = (((int64_t)d0 * D1 + d1) * KH + ky) * KW + kx;
+  dst[di] = accumulate ? dst[di] + s : s;
 }
 
 // pack a PyTorch conv weight into the GEMM layout Wp[co][tap][ci] (cast to T)
@@ -1132,6 +1291,19 @@ int cesm_conv_wgrad(int dtype, const void* x1, const void* x2, const void* dy1, 
     wgrad3x3_bf16_kernel<<<g3, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
                                                  (const bf16*)dy2, slab, g, tx, ntiles);
     nsplit = (int)g3.z;
+  } else if (dtype == CESM_DT_BF16 && M < (1ll << 31) && !getenv_flag("CESM_NO_WIDE_WGRAD")) {
+    // wide-tile kernel; nsplit from the caller sized the slab for 64-row tiles, keep it
+    const int bm = (Cout % 256 == 0 && Co1 % 256 == 0) ? 256 : ((Cout % 128 == 0 && Co1 % 128 == 0) ? 128 : 64);
+    dim3 gw(Cout / bm, K / 64, nsplit);
+    if (bm == 256)
+      wgrad_wide_kernel<256><<<gw, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
+                                                     (const bf16*)dy2, slab, g, (int)M, (int)pps);
+    else if (bm == 128)
+      wgrad_wide_kernel<128><<<gw, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
+                                                     (const bf16*)dy2, slab, g, (int)M, (int)pps);
+    else
+      wgrad_wide_kernel<64><<<gw, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
+                                                    (const bf16*)dy2, slab, g, (int)M, (int)pps);
   } else if (dtype == CESM_DT_BF16)
     conv_wgrad_kernel<bf16><<<grid, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
                                                       (const bf16*)dy2, slab, g, M, pps);
@@ -1141,8 +1313,8 @@ int cesm_conv_wgrad(int dtype, const void* x1, const void* x2, const void* dy1, 
   else
     return CESM_EINVAL;
   const int64_t total = (int64_t)Cout * K;
-  conv_wgrad_reduce_kernel<<<(unsigned)std::min<int64_t>(cdiv(total, 256), 2048), 256, 0, stream>>>(
-      slab, dw, nsplit, Cout, Cin, KH, KW, swap, flip, accumulate);
+  conv_wgrad_reduce_kernel<<<(unsigned)cdiv(total, 64), 256, 0, stream>>>(slab, dw, nsplit, Cout, Cin, KH, KW, swap,
+                                                                          flip, accumulate);
   return cesm_launch_status();
 }
 

@@ -636,6 +636,20 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 __device__ __forceinline__ bf16x8 ld16(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
+// sum / max over the 4 lanes {l, l^16, l^32, l^48} with v_permlane{16,32}_swap (VALU, no LDS)
+__device__ __forceinline__ float grp4_sum(float v) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float grp4_max(float v) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
 constexpr int RS = 36;  // RoPE table row stride (floats): 16-B aligned, spreads frames over banks
 constexpr float LOG2E = 1.4426950408889634f;
 
@@ -674,24 +688,32 @@ __device__ __forceinline__ bool tw_row(int v, int VW, int F, int p0, int HW, int
 
 // q'|k'|v tiles (and the RoPE/scale epilogue) of head h for the wave's NVT voxel tiles
 template <int C, int NV>
-__device__ __forceinline__ void tw_qkv(const bf16* __restrict__ wqkv, const bf16x8 (&xf)[TW<C, NV>::NVTM][TW<C, NV>::KS],
-                                       int h, const int (&fr)[NV], float scale, const float* rot, bf16* sq, bf16* sk,
-                                       bf16* sv, int lr, int lg) {
+__device__ __forceinline__ void tw_load_wq(bf16x8 (&a)[6][C / 32], const bf16* __restrict__ wqkv, int h, int lr,
+                                           int lg) {
+#pragma unroll
+  for (int ct = 0; ct < 6; ++ct) {
+    const int wrow = (ct >> 1) * INNER + h * DH + (ct & 1) * 16 + lr;
+#pragma unroll
+    for (int ks = 0; ks < TW<C, NV>::KS; ++ks) a[ct][ks] = ld16(wqkv + (int64_t)wrow * C + ks * 32 + lg * 8);
+  }
+}
+
+// q'|k'|v tiles (RoPE/scale epilogue) of one head from preloaded weight fragments a[6][KS]
+template <int C, int NV>
+__device__ __forceinline__ void tw_qkv_pre(const bf16x8 (&a)[6][C / 32],
+                                           const bf16x8 (&xf)[TW<C, NV>::NVTM][TW<C, NV>::KS], const int (&fr)[NV],
+                                           float scale, const float* rot, bf16* sq, bf16* sk, bf16* sv, int lr, int lg) {
   using T = TW<C, NV>;
 #pragma unroll
   for (int ct = 0; ct < 6; ++ct) {
     const int kind = ct >> 1;
-    const int wrow = kind * INNER + h * DH + (ct & 1) * 16 + lr;
-    bf16x8 a[T::KS];
-#pragma unroll
-    for (int ks = 0; ks < T::KS; ++ks) a[ks] = ld16(wqkv + (int64_t)wrow * C + ks * 32 + lg * 8);
     bf16* dst = kind == 0 ? sq : (kind == 1 ? sk : sv);
     const int d0 = (ct & 1) * 16 + lg * 4;
 #pragma unroll
     for (int vt = 0; vt < NV; ++vt) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < T::KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], xf[vt][ks], acc, 0, 0, 0);
+      for (int ks = 0; ks < T::KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ct][ks], xf[vt][ks], acc, 0, 0, 0);
       float o4[4] = {acc[0], acc[1], acc[2], acc[3]};
       if (kind == 0) {
 #pragma unroll
@@ -701,6 +723,15 @@ __device__ __forceinline__ void tw_qkv(const bf16* __restrict__ wqkv, const bf16
       store4(dst + (vt * 16 + lr) * HLD + d0, o4);
     }
   }
+}
+
+template <int C, int NV>
+__device__ __forceinline__ void tw_qkv(const bf16* __restrict__ wqkv, const bf16x8 (&xf)[TW<C, NV>::NVTM][TW<C, NV>::KS],
+                                       int h, const int (&fr)[NV], float scale, const float* rot, bf16* sq, bf16* sk,
+                                       bf16* sv, int lr, int lg) {
+  bf16x8 a[6][C / 32];
+  tw_load_wq<C, NV>(a, wqkv, h, lr, lg);
+  tw_qkv_pre<C, NV>(a, xf, fr, scale, rot, sq, sk, sv, lr, lg);
 }
 
 // LN of the wave's voxels on the B fragments.  use_saved: take (mean, rstd) from mr, else compute
@@ -734,16 +765,14 @@ __device__ __forceinline__ void tw_ln(const bf16* __restrict__ x, const float* _
       for (int ks = 0; ks < T::KS; ++ks)
 #pragma unroll
         for (int i = 0; i < 8; ++i) s += a[ks][i];
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
+      s = grp4_sum(s);
       mean = s / C;
       float q = 0.f;
 #pragma unroll
       for (int ks = 0; ks < T::KS; ++ks)
 #pragma unroll
         for (int i = 0; i < 8; ++i) { const float d = a[ks][i] - mean; q = fmaf(d, d, q); }
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
+      q = grp4_sum(q);
       rstd = 1.f / sqrtf(q / C + eps);
       if (ok && lg == 0 && mr_out) { mr_out[row * 2] = mean; mr_out[row * 2 + 1] = rstd; }
     }
@@ -756,7 +785,7 @@ __device__ __forceinline__ void tw_ln(const bf16* __restrict__ x, const float* _
 }
 
 template <int C, int NV>
-__global__ __launch_bounds__(256) void tw_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ gamma,
+__global__ __launch_bounds__(256, 2) void tw_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ gamma,
                                                      const bf16* __restrict__ wqkv, const bf16* __restrict__ wout,
                                                      const float* __restrict__ bias, const float* __restrict__ rotg,
                                                      bf16* __restrict__ y, float* __restrict__ mr,
@@ -793,8 +822,26 @@ __global__ __launch_bounds__(256) void tw_fwd_kernel(const bf16* __restrict__ x,
     for (int vt = 0; vt < T::NVTM; ++vt) yacc[ct][vt] = f32x4{0.f, 0.f, 0.f, 0.f};
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
 
+  constexpr bool PREF = C <= 64;  // next head's QKV weights prefetched into registers (48 VGPRs at C=64)
+  bf16x8 wq[6][PREF ? T::KS : 1];
+  if constexpr (PREF) tw_load_wq<C, NV>(wq, wqkv, 0, lr, lg);
   for (int h = 0; h < NH; ++h) {
-    tw_qkv<C, NV>(wqkv, xf, h, fr, scale, rot, sq, sk, sv, lr, lg);
+    bf16x8 wo[T::CT];
+#pragma unroll
+    for (int ct = 0; ct < T::CT; ++ct) wo[ct] = ld16(wout + (int64_t)(ct * 16 + lr) * INNER + h * DH + lg * 8);
+    if constexpr (PREF) {
+      tw_qkv_pre<C, NV>(wq, xf, fr, scale, rot, sq, sk, sv, lr, lg);
+      if (h + 1 < NH) tw_load_wq<C, NV>(wq, wqkv, h + 1, lr, lg);  // in flight during the core
+    } else {
+      tw_qkv<C, NV>(wqkv, xf, h, fr, scale, rot, sq, sk, sv, lr, lg);
+    }
+    // bias (log2 units) of this lane's 4 entries (i = lr, j = 4g + r); -inf masks padding frames
+    float bt[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = lg * 4 + r;
+      bt[r] = (j < F && lr < F) ? sb[(h * F + lr) * F + j] : -INFINITY;
+    }
     wave_lds_sync();
     // attention core per pixel (base-2 softmax); O overwrites the pixel's own q rows
     for (int pp = 0; pp < T::PW; ++pp) {
@@ -808,22 +855,19 @@ __global__ __launch_bounds__(256) void tw_fwd_kernel(const bf16* __restrict__ x,
       float m = -INFINITY;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int j = lg * 4 + r;
-        sc[r] = (j < F && lr < F) ? fmaf(st[r], LOG2E, sb[(h * F + lr) * F + j]) : -INFINITY;
+        sc[r] = fmaf(st[r], LOG2E, bt[r]);
         m = fmaxf(m, sc[r]);
       }
-      m = fmaxf(m, __shfl_xor(m, 16, 64));
-      m = fmaxf(m, __shfl_xor(m, 32, 64));
+      m = grp4_max(m);
       float pr[4], l = 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         pr[r] = sc[r] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(sc[r] - m);
         l += pr[r];
       }
-      l += __shfl_xor(l, 16, 64);
-      l += __shfl_xor(l, 32, 64);
+      l = grp4_sum(l);
       if (lse && lg == 0 && lr < F) lse[(((int64_t)b * NH + h) * HW + p) * F + lr] = m + log2f(l);  // log2 units
-      const float inv = lr < F ? 1.f / l : 0.f;
+      const float inv = lr < F ? __builtin_amdgcn_rcpf(l) : 0.f;
       bf16x8 pb = zero8();
 #pragma unroll
       for (int r = 0; r < 4; ++r) pb[r] = (bf16)(pr[r] * inv);
@@ -846,10 +890,9 @@ __global__ __launch_bounds__(256) void tw_fwd_kernel(const bf16* __restrict__ x,
     for (int vt = 0; vt < T::NVTM; ++vt) ob[vt] = vt < NVT ? ld16(sq + (vt * 16 + lr) * HLD + lg * 8) : zero8();
 #pragma unroll
     for (int ct = 0; ct < T::CT; ++ct) {
-      const bf16x8 a = ld16(wout + (int64_t)(ct * 16 + lr) * INNER + h * DH + lg * 8);
 #pragma unroll
       for (int vt = 0; vt < T::NVTM; ++vt)
-        if (vt < NVT) yacc[ct][vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ob[vt], yacc[ct][vt], 0, 0, 0);
+        if (vt < NVT) yacc[ct][vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wo[ct], ob[vt], yacc[ct][vt], 0, 0, 0);
     }
     wave_lds_sync();
   }
@@ -896,6 +939,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
   bf16* sk = sq + R * HLD;
   bf16* sv = sk + R * HLD;
   bf16* sdo = sv + R * HLD;
+  float* sld = reinterpret_cast<float*>(reinterpret_cast<bf16*>(rot + 16 * RS) + 4 * 4 * R * HLD) + wid * 32;
   for (int e = tid; e < NH * FF; e += 256) { sb[e] = bias[e] * LOG2E; sdb[e] = 0.f; }
   for (int e = tid; e < C; e += 256) sg[e] = 0.f;
   for (int e = tid; e < F * 32; e += 256) rot[(e >> 5) * RS + (e & 31)] = rotg[e];
@@ -955,6 +999,15 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
           }
         }
       }
+      // biases (log2 units): transposed entries (i = lr, j = 4g + r) and row-major (i = 4g + r, j = lr)
+      float bt[4], brm[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = lg * 4 + r;
+        const bool ok = c < F && lr < F;
+        bt[r] = ok ? sb[(h * F + lr) * F + c] : 0.f;
+        brm[r] = ok ? sb[(h * F + c) * F + lr] : 0.f;
+      }
       wave_lds_sync();
       // core backward per pixel; dq/dk/dv overwrite the pixel's own q/k/v rows at the end
       float dbr[4] = {0.f, 0.f, 0.f, 0.f};
@@ -978,11 +1031,11 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
           for (int r = 0; r < 4; ++r) {
             const int j = lg * 4 + r;
             const bool ok = j < F && lr < F;
-            pt[r] = ok ? __builtin_amdgcn_exp2f(fmaf(st[r], LOG2E, sb[(h * F + lr) * F + j]) - Li) : 0.f;
+            pt[r] = ok ? __builtin_amdgcn_exp2f(fmaf(st[r], LOG2E, bt[r]) - Li) : 0.f;
             D = fmaf(pt[r], dpt[r], D);
           }
-          D += __shfl_xor(D, 16, 64);
-          D += __shfl_xor(D, 32, 64);
+          D = grp4_sum(D);
+          if (lg == 0) { sld[lr] = Li; sld[16 + lr] = D; }
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float ds = pt[r] * (dpt[r] - D);
@@ -1009,12 +1062,15 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
         {
           const f32x4 s_ = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qr, kr, z4, 0, 0, 0);    // S[i][j]
           const f32x4 dp_ = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dor, vr, z4, 0, 0, 0);  // dP[i][j]
+          wave_lds_sync();
+          const f32x4 L4 = *reinterpret_cast<const f32x4*>(sld + lg * 4);
+          const f32x4 D4 = *reinterpret_cast<const f32x4*>(sld + 16 + lg * 4);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int i = lg * 4 + r;
-            const float Lr = __shfl(Li, i, 64), Dr = __shfl(D, i, 64);
+            const float Lr = L4[r], Dr = D4[r];
             const bool ok = i < F && lr < F;
-            const float pv = ok ? __builtin_amdgcn_exp2f(fmaf(s_[r], LOG2E, sb[(h * F + i) * F + lr]) - Lr) : 0.f;
+            const float pv = ok ? __builtin_amdgcn_exp2f(fmaf(s_[r], LOG2E, brm[r]) - Lr) : 0.f;
             p_b[r] = (bf16)pv;
             ds_b[r] = (bf16)(ok ? pv * (dp_[r] - Dr) : 0.f);
           }
@@ -1099,10 +1155,8 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
           if constexpr (DG_REG) dgam[ct][r] = fmaf(dxacc[ct][vt][r], xh[ct][r], dgam[ct][r]);
         }
       }
-      s1 += __shfl_xor(s1, 16, 64);
-      s1 += __shfl_xor(s1, 32, 64);
-      s2 += __shfl_xor(s2, 16, 64);
-      s2 += __shfl_xor(s2, 32, 64);
+      s1 = grp4_sum(s1);
+      s2 = grp4_sum(s2);
       s1 /= C;
       s2 /= C;
 #pragma unroll
@@ -1167,7 +1221,7 @@ static size_t tw_fwd_smem(int F) {  // NOLINT
 template <int C>
 static size_t tw_bwd_smem(int F) {
   const int R = ((TW<C>::PW * F + 15) / 16) * 16;
-  return (size_t)(2 * NH * F * F + C + 16 * RS) * 4 + (size_t)4 * 4 * R * HLD * 2;
+  return (size_t)(2 * NH * F * F + C + 16 * RS) * 4 + (size_t)4 * 4 * R * HLD * 2 + 4 * 32 * 4;
 }
 template <typename K>
 static void allow_smem(K kernel, size_t bytes) {

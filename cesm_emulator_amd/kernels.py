@@ -76,11 +76,22 @@ def conv_fwd(x1, x2, wp, bias, geom, res=None, res2=None, out_split=None):
     return y1 if y2 is None else (y1, y2)
 
 
-def _wgrad_nsplit(M, cout, K):
-    tiles = (cout // 64) * (K // 64)
-    n = max(1, 2048 // max(1, tiles))
+def _wgrad_nsplit(M, cout, K, bm=64):
+    """pixel splits of the weight-gradient GEMM: ~2048 blocks of (bm x 64) tiles, >= 256 pixels each"""
+    tiles = max(1, cout // bm) * max(1, K // 64)
+    n = max(1, 2048 // tiles)
     n = min(n, max(1, M // 256))
     return n
+
+
+def _wgrad_bm(x, cout, co1):
+    if x.dtype != torch.bfloat16:
+        return 64
+    if cout % 256 == 0 and co1 % 256 == 0:
+        return 256
+    if cout % 128 == 0 and co1 % 128 == 0:
+        return 128
+    return 64
 
 
 def conv_wgrad(x1, x2, dy1, dy2, dw, geom, swap, flip, accumulate=True):
@@ -93,7 +104,8 @@ def conv_wgrad(x1, x2, dy1, dy2, dw, geom, swap, flip, accumulate=True):
     _chk(dw, dtype=torch.float32)
     K = KH * KW * (C1 + C2)
     M = Nb * Ho * Wo
-    nsplit = _wgrad_nsplit(M, Cout, K)
+    halo3 = KH == 3 and KW == 3 and St == 1 and Pd == 1 and U == 1  # wgrad3x3 kernel: 64-row tiles
+    nsplit = _wgrad_nsplit(M, Cout, K, 64 if halo3 else _wgrad_bm(x1, Cout, Co1))
     slab = empty((nsplit, Cout, K), torch.float32, x1.device)
     call("cesm_conv_wgrad", dtcode(x1), P(x1), P(x2), P(dy1), P(dy2), P(dw), P(slab), nsplit, Nb, Hi, Wi, C1, C2,
          Ho, Wo, Cout, Co1, KH, KW, St, Pd, U, int(swap), int(flip), int(accumulate), S())
