@@ -1,0 +1,921 @@
+// Fused spatial linear attention block (bf16, C = 64): Residual(PreNorm(SpatialLinearAttention))
+// (video_net.py:313-347, :69-98).  Per frame n, head h (8 x 32):
+//   xn = LN(x);  q,k,v = W_{q,k,v} xn
+//   q~[d,p] = scale * softmax_d(q)[d,p]      k~[d,p] = softmax_p(k)[d,p] = exp(k - M_d) / Z_d
+//   ctx[d,e] = sum_p k~[d,p] v[e,p]          o[e,p] = sum_d ctx[d,e] q~[d,p]
+//   y = x + W_o o + b_o
+// Forward = three launches, none of which writes a per-pixel intermediate:
+//   slaf_stats   (8 waves = 8 heads, xn tile in LDS): online-softmax partials per block:
+//                m_d, s_d = sum exp(k - m), u^T[e][d] = sum_p v[e,p] exp(k[d,p] - m_d)
+//   slaf_combine per (frame, head): M, Z, ctx; ctx also written as ready-to-load MFMA A fragments
+//   slaf_out     (wave = 64 pixels, all heads): LN -> q -> softmax_d -> o = ctx^T q~ -> y, with q~ and o
+//                kept in registers: the MFMA D layout (lane (g, i): rows 4g..4g+3 of a 16-row tile,
+//                column i) is fed back as a B operand through the k-slot map
+//                slot (g, j<4) <-> k = 4g + j,  slot (g, 4+j) <-> k = 16 + 4g + j.
+#include "common.h"
+
+namespace {
+
+constexpr int NH = 8, DH = 32, INNER = 256, QKV = 768;
+constexpr float LOG2E = 1.4426950408889634f;
+
+__device__ __forceinline__ bf16x8 zero8() {
+  bf16x8 z;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) z[i] = (bf16)0.f;
+  return z;
+}
+__device__ __forceinline__ bf16x8 ld16(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+__device__ __forceinline__ float grp4_sum(float v) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float grp4_max(float v) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+// k index of slot (g, j) of the k-slot map
+__device__ __forceinline__ int kslot(int g, int j) { return j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4); }
+// B/A operand from two D-layout 16-row tiles (rows 0..15 -> slots 0..3, rows 16..31 -> slots 4..7)
+__device__ __forceinline__ bf16x8 pack_kslot(const float* t0, const float* t1) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    r[j] = (bf16)t0[j];
+    r[4 + j] = (bf16)t1[j];
+  }
+  return r;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// slaf_stats: grid (nblk, Nf), 512 threads (wave h = head h).  Block b of frame n handles 64-pixel
+// sub-chunks [b*spb, (b+1)*spb).  Partial layout per (n, b, h): m[32] | s[32] | uT[32 e][32 d].
+// ---------------------------------------------------------------------------------------------------
+template <int C>
+__global__ __launch_bounds__(512) void slaf_stats_kernel(const bf16* __restrict__ x, const float* __restrict__ gamma,
+                                                         const bf16* __restrict__ wqkv, float* __restrict__ part,
+                                                         int HW, int spb, float eps) {
+  constexpr int KS = C / 32, XLD = C + 8, L = C / 8, PPP = 512 / L;  // LN lanes per pixel, pixels per pass
+  __shared__ __attribute__((aligned(16))) bf16 xs[64 * XLD];
+  const int tid = threadIdx.x, lane = tid & 63, h = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int n = blockIdx.y;
+  const int nsc = (HW + 63) / 64;
+  const int sc0 = blockIdx.x * spb, sc1 = min(nsc, sc0 + spb);
+  const bf16* xf = x + (int64_t)n * HW * C;
+
+  // B fragments W[ch][ci] of this head's k and v rows
+  bf16x8 wk[2][KS], wv[2][KS];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      wk[t][ks] = ld16(wqkv + (int64_t)(INNER + h * DH + t * 16 + lr) * C + ks * 32 + lg * 8);
+      wv[t][ks] = ld16(wqkv + (int64_t)(2 * INNER + h * DH + t * 16 + lr) * C + ks * 32 + lg * 8);
+    }
+  float m[2] = {-INFINITY, -INFINITY}, s[2] = {0.f, 0.f};  // d = t*16 + lr
+  f32x4 uT[2][2];                                           // [e tile][d tile]
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) uT[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+
+  for (int sc = sc0; sc < sc1; ++sc) {
+    const int p0 = sc * 64;
+    __syncthreads();
+    // LN of 64 pixels into xs (rows beyond HW zero)
+    {
+      const int sub = tid % L;
+#pragma unroll
+      for (int pp0 = 0; pp0 < 64; pp0 += PPP) {
+        const int pl = pp0 + tid / L;
+        const int p = p0 + pl;
+        float a[8];
+        if (p < HW) load8(xf + (int64_t)p * C + sub * 8, a);
+        else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) a[i] = 0.f;
+        }
+        float sm = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sm += a[i];
+        sm = group_sum(sm, L);
+        const float mean = sm / C;
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { const float d = a[i] - mean; q = fmaf(d, d, q); }
+        q = group_sum(q, L);
+        const float rstd = 1.f / sqrtf(q / C + eps);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] = p < HW ? (a[i] - mean) * rstd * gamma[sub * 8 + i] : 0.f;
+        store8(xs + pl * XLD + sub * 8, a);
+      }
+    }
+    __syncthreads();
+    // k, v of this head for 64 pixels: D[px = vt*16 + 4g + r][ch = t*16 + i]
+    f32x4 kk[4][2], vv[4][2];
+#pragma unroll
+    for (int vt = 0; vt < 4; ++vt) {
+      bf16x8 af[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) af[ks] = ld16(xs + (vt * 16 + lr) * XLD + ks * 32 + lg * 8);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        f32x4 ak = z4, av = z4;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          ak = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks], wk[t][ks], ak, 0, 0, 0);
+          av = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks], wv[t][ks], av, 0, 0, 0);
+        }
+        kk[vt][t] = ak;
+        vv[vt][t] = av;
+      }
+    }
+    // online softmax over pixels, per d = t*16 + lr
+    float corr[2], mn[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      float lm = -INFINITY;
+#pragma unroll
+      for (int vt = 0; vt < 4; ++vt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (p0 + vt * 16 + lg * 4 + r < HW) lm = fmaxf(lm, kk[vt][t][r]);
+      lm = grp4_max(lm);
+      mn[t] = fmaxf(m[t], lm);
+      corr[t] = m[t] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m[t] - mn[t]) * LOG2E);
+    }
+    float pe[4][2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      float ps = 0.f;
+#pragma unroll
+      for (int vt = 0; vt < 4; ++vt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool ok = p0 + vt * 16 + lg * 4 + r < HW;
+          pe[vt][t][r] = ok ? __builtin_amdgcn_exp2f((kk[vt][t][r] - mn[t]) * LOG2E) : 0.f;
+          ps += pe[vt][t][r];
+        }
+      ps = grp4_sum(ps);
+      s[t] = s[t] * corr[t] + ps;
+      m[t] = mn[t];
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) uT[e][t][r] *= corr[t];
+    }
+    // uT[e][d] += sum_p v[p][e] p[p][d]   (two 32-pixel k-steps from tile pairs (0,1), (2,3))
+#pragma unroll
+    for (int kp = 0; kp < 2; ++kp) {
+      const int va = 2 * kp, vb = 2 * kp + 1;
+      bf16x8 Av[2], Bp[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        float a0[4] = {vv[va][t][0], vv[va][t][1], vv[va][t][2], vv[va][t][3]};
+        float a1[4] = {vv[vb][t][0], vv[vb][t][1], vv[vb][t][2], vv[vb][t][3]};
+        Av[t] = pack_kslot(a0, a1);
+        Bp[t] = pack_kslot(pe[va][t], pe[vb][t]);
+      }
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) uT[e][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Av[e], Bp[t], uT[e][t], 0, 0, 0);
+    }
+  }
+  float* o = part + (((int64_t)n * gridDim.x + blockIdx.x) * NH + h) * (64 + 1024);
+  if (lg == 0) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      o[t * 16 + lr] = m[t];
+      o[32 + t * 16 + lr] = s[t];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 2; ++e)
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[64 + (e * 16 + lg * 4 + r) * 32 + t * 16 + lr] = uT[e][t][r];
+}
+
+// ---------------------------------------------------------------------------------------------------
+// slaf_combine: grid (Nf * 8), 256 threads.  mz[n][h][d] = (M, Z); ctx32[n][h][d][e];
+// A-fragment images (bf16, [n][h][tile][lane][8]):  actT rows e / k = d  (o = ctx^T q~),
+//                                                     actx rows d / k = e  (dq~ = ctx do).
+// ---------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void slaf_combine_kernel(const float* __restrict__ part, int nblk,
+                                                           float* __restrict__ mz, float* __restrict__ ctx32,
+                                                           bf16* __restrict__ actT, bf16* __restrict__ actx) {
+  __shared__ float sM[32], sZ[32];
+  __shared__ float sc[32][33];  // [d][e]
+  const int nh = blockIdx.x, n = nh / NH, h = nh % NH;
+  const int tid = threadIdx.x;
+  const float* pb = part + ((int64_t)n * nblk * NH + h) * (64 + 1024);
+  const int64_t bstride = (int64_t)NH * (64 + 1024);
+  if (tid < 32) {
+    float M = -INFINITY;
+    for (int b = 0; b < nblk; ++b) M = fmaxf(M, pb[b * bstride + tid]);
+    float Z = 0.f;
+    for (int b = 0; b < nblk; ++b) {
+      const float mb = pb[b * bstride + tid];
+      if (mb != -INFINITY) Z += expf(mb - M) * pb[b * bstride + 32 + tid];
+    }
+    sM[tid] = M;
+    sZ[tid] = Z;
+    mz[((int64_t)nh * 32 + tid) * 2] = M;
+    mz[((int64_t)nh * 32 + tid) * 2 + 1] = Z;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = tid * 4 + i;  // (e, d) = (idx / 32, idx % 32)
+    const int e = idx >> 5, d = idx & 31;
+    float U = 0.f;
+    for (int b = 0; b < nblk; ++b) {
+      const float mb = pb[b * bstride + d];
+      if (mb != -INFINITY) U += expf(mb - sM[d]) * pb[b * bstride + 64 + idx];
+    }
+    const float c = sZ[d] > 0.f ? U / sZ[d] : 0.f;
+    sc[d][e] = c;
+    ctx32[((int64_t)nh * 32 + d) * 32 + e] = c;
+  }
+  __syncthreads();
+  // fragment images: 2 tiles x 64 lanes x 8
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = tid + i * 256;  // (tile, lane, j) over 2*64*4 pairs of slots
+    const int tile = idx >> 8, lane = (idx >> 2) & 63, jp = idx & 3;
+    const int g = lane >> 4, l16 = lane & 15;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int j = jp * 2 + jj;
+      const int k = kslot(g, j);
+      const int row = tile * 16 + l16;
+      const int64_t o = (((int64_t)nh * 2 + tile) * 64 + lane) * 8 + j;
+      actT[o] = (bf16)sc[k][row];  // rows e, k = d
+      actx[o] = (bf16)sc[row][k];  // rows d, k = e
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// slaf_out: wave = 16*NV pixels of one frame, all heads; grid (cdiv(HW, 64*NV), Nf), 256 threads.
+// ---------------------------------------------------------------------------------------------------
+template <int C, int NV>
+__global__ __launch_bounds__(256) void slaf_out_kernel(const bf16* __restrict__ x, const float* __restrict__ gamma,
+                                                       const bf16* __restrict__ wqkv, const bf16* __restrict__ wout,
+                                                       const float* __restrict__ bout, const bf16* __restrict__ actT,
+                                                       bf16* __restrict__ y, int HW, float scale, float eps) {
+  constexpr int KS = C / 32, CT = C / 16;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int n = blockIdx.y;
+  const int p0 = (blockIdx.x * 4 + wid) * 16 * NV;
+  if (p0 >= HW) return;
+  const bf16* xb = x + (int64_t)n * HW * C;
+  // LN on the B fragments: lane (g, i) holds pixel p0 + vt*16 + i, channels ks*32 + 8g..8g+7
+  bf16x8 xf[NV][KS];
+#pragma unroll
+  for (int vt = 0; vt < NV; ++vt) {
+    const int p = p0 + vt * 16 + lr;
+    const bool ok = p < HW;
+    float a[KS][8];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ok) load8(xb + (int64_t)p * C + ks * 32 + lg * 8, a[ks]);
+      else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[ks][i] = 0.f;
+      }
+    }
+    float sm = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) sm += a[ks][i];
+    const float mean = grp4_sum(sm) / C;
+    float q = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { const float d = a[ks][i] - mean; q = fmaf(d, d, q); }
+    const float rstd = 1.f / sqrtf(grp4_sum(q) / C + eps);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) xf[vt][ks][i] = (bf16)(ok ? (a[ks][i] - mean) * rstd * gamma[ks * 32 + lg * 8 + i] : 0.f);
+  }
+  f32x4 yacc[CT][NV];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+    for (int vt = 0; vt < NV; ++vt) yacc[ct][vt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  const bf16* actn = actT + (int64_t)n * NH * 2 * 64 * 8;
+
+  for (int h = 0; h < NH; ++h) {
+    bf16x8 wq[2][KS];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) wq[t][ks] = ld16(wqkv + (int64_t)(h * DH + t * 16 + lr) * C + ks * 32 + lg * 8);
+    bf16x8 at[2];
+#pragma unroll
+    for (int et = 0; et < 2; ++et) at[et] = ld16(actn + ((h * 2 + et) * 64 + lane) * 8);
+    // W_o[co][h*32 + kslot(g, j)] fragments
+    bf16x8 wo[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const bf16* src = wout + (int64_t)(ct * 16 + lr) * INNER + h * DH + lg * 4;
+      const s16x4 lo = *reinterpret_cast<const s16x4*>(src);
+      const s16x4 hi = *reinterpret_cast<const s16x4*>(src + 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        wo[ct][j] = __builtin_bit_cast(bf16, (short)lo[j]);
+        wo[ct][4 + j] = __builtin_bit_cast(bf16, (short)hi[j]);
+      }
+    }
+#pragma unroll
+    for (int vt = 0; vt < NV; ++vt) {
+      float qv[2][4];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        f32x4 a = z4;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wq[t][ks], xf[vt][ks], a, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) qv[t][r] = a[r];
+      }
+      // softmax over d (rows t*16 + 4g + r) for pixel lr
+      float mx = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, qv[t][r]);
+      mx = grp4_max(mx);
+      float sm = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          qv[t][r] = __builtin_amdgcn_exp2f((qv[t][r] - mx) * LOG2E);
+          sm += qv[t][r];
+        }
+      const float inv = scale * __builtin_amdgcn_rcpf(grp4_sum(sm));
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) qv[t][r] *= inv;
+      const bf16x8 qb = pack_kslot(qv[0], qv[1]);
+      // o^T = ctx^T q~  -> rows e
+      float ov[2][4];
+#pragma unroll
+      for (int et = 0; et < 2; ++et) {
+        const f32x4 o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[et], qb, z4, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ov[et][r] = o[r];
+      }
+      const bf16x8 ob = pack_kslot(ov[0], ov[1]);
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) yacc[ct][vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wo[ct], ob, yacc[ct][vt], 0, 0, 0);
+    }
+  }
+  // y = x + W_o o + b_o
+#pragma unroll
+  for (int vt = 0; vt < NV; ++vt) {
+    const int p = p0 + vt * 16 + lr;
+    if (p >= HW) continue;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int co = ct * 16 + lg * 4;
+      float xv[4];
+      load4(xb + (int64_t)p * C + co, xv);
+      float o4[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o4[r] = xv[r] + yacc[ct][vt][r] + bout[co + r];
+      store4(y + ((int64_t)n * HW + p) * C + co, o4);
+    }
+  }
+}
+
+// ===================================================================================================
+// Backward.  With do = W_o^T dy:
+//   dq~ = ctx do,  dctx = sum_p q~ do^T,  dq = scale sm (dq~ - sum_d sm dq~)       (sm = softmax_d q)
+//   dk~ = dctx v,  dv = dctx^T k~,       dk = k~ (dk~ - G),  G_d = sum_p k~ dk~ = sum_e dctx[d,e] ctx[d,e]
+//   dxn = W_q^T dq + W_k^T dk + W_v^T dv -> LN backward (+ dy residual)
+// slab_dctx (8 waves = heads, non-transposed tiles) -> slab_combine -> slab_dx (per wave, all heads).
+// ===================================================================================================
+
+// max / sum over the 16 lanes of a row with DPP (quad_perm xor1, xor2, row_half_mirror, row_mirror)
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false)));
+  return v;
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));
+  return v;
+}
+
+// grid (nblk, Nf), 512 threads; partial per (n, b, h): dctx[32 d][32 e]
+template <int C>
+__global__ __launch_bounds__(512) void slab_dctx_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                        const float* __restrict__ gamma, const bf16* __restrict__ wqkv,
+                                                        const bf16* __restrict__ wout_t, float* __restrict__ part,
+                                                        int HW, int spb, float scale, float eps) {
+  constexpr int KS = C / 32, XLD = C + 8, L = C / 8, PPP = 512 / L;
+  __shared__ __attribute__((aligned(16))) bf16 xs[64 * XLD];
+  __shared__ __attribute__((aligned(16))) bf16 ds[64 * XLD];
+  const int tid = threadIdx.x, lane = tid & 63, h = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int n = blockIdx.y;
+  const int nsc = (HW + 63) / 64;
+  const int sc0 = blockIdx.x * spb, sc1 = min(nsc, sc0 + spb);
+  const bf16* xb = x + (int64_t)n * HW * C;
+  const bf16* db = dy + (int64_t)n * HW * C;
+  bf16x8 wq[2][KS], wo[2][KS];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      wq[t][ks] = ld16(wqkv + (int64_t)(h * DH + t * 16 + lr) * C + ks * 32 + lg * 8);
+      wo[t][ks] = ld16(wout_t + (int64_t)(h * DH + t * 16 + lr) * C + ks * 32 + lg * 8);
+    }
+  f32x4 dc[2][2];  // [d tile][e tile]
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) dc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  for (int sc = sc0; sc < sc1; ++sc) {
+    const int p0 = sc * 64;
+    __syncthreads();
+    {
+      const int sub = tid % L;
+#pragma unroll
+      for (int pp0 = 0; pp0 < 64; pp0 += PPP) {
+        const int pl = pp0 + tid / L;
+        const int p = p0 + pl;
+        float a[8], d8[8];
+        if (p < HW) {
+          load8(xb + (int64_t)p * C + sub * 8, a);
+          load8(db + (int64_t)p * C + sub * 8, d8);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) { a[i] = 0.f; d8[i] = 0.f; }
+        }
+        float sm = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sm += a[i];
+        sm = group_sum(sm, L);
+        const float mean = sm / C;
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { const float d = a[i] - mean; q = fmaf(d, d, q); }
+        q = group_sum(q, L);
+        const float rstd = 1.f / sqrtf(q / C + eps);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] = p < HW ? (a[i] - mean) * rstd * gamma[sub * 8 + i] : 0.f;
+        store8(xs + pl * XLD + sub * 8, a);
+        store8(ds + pl * XLD + sub * 8, d8);
+      }
+    }
+    __syncthreads();
+    float qt[4][2][4], dv[4][2][4];  // q~ [px tile][d tile][r], do [px tile][e tile][r]
+#pragma unroll
+    for (int vt = 0; vt < 4; ++vt) {
+      bf16x8 ax[KS], ad[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        ax[ks] = ld16(xs + (vt * 16 + lr) * XLD + ks * 32 + lg * 8);
+        ad[ks] = ld16(ds + (vt * 16 + lr) * XLD + ks * 32 + lg * 8);
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        f32x4 aq = z4, ao = z4;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          aq = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[ks], wq[t][ks], aq, 0, 0, 0);
+          ao = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ad[ks], wo[t][ks], ao, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { qt[vt][t][r] = aq[r]; dv[vt][t][r] = ao[r]; }
+      }
+      // softmax over d (lanes of the row x 2 tiles) for pixel vt*16 + 4g + r
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float mx = row16_max(fmaxf(qt[vt][0][r], qt[vt][1][r]));
+        const float e0 = __builtin_amdgcn_exp2f((qt[vt][0][r] - mx) * LOG2E);
+        const float e1 = __builtin_amdgcn_exp2f((qt[vt][1][r] - mx) * LOG2E);
+        const float inv = scale * __builtin_amdgcn_rcpf(row16_sum(e0 + e1));
+        qt[vt][0][r] = e0 * inv;
+        qt[vt][1][r] = e1 * inv;
+      }
+    }
+#pragma unroll
+    for (int kp = 0; kp < 2; ++kp) {
+      const int va = 2 * kp, vb = 2 * kp + 1;
+      bf16x8 Aq[2], Bd[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        Aq[t] = pack_kslot(qt[va][t], qt[vb][t]);
+        Bd[t] = pack_kslot(dv[va][t], dv[vb][t]);
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) dc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Aq[a], Bd[b], dc[a][b], 0, 0, 0);
+    }
+  }
+  float* o = part + (((int64_t)n * gridDim.x + blockIdx.x) * NH + h) * 1024;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[(a * 16 + lg * 4 + r) * 32 + b * 16 + lr] = dc[a][b][r];
+}
+
+// grid (Nf * 8), 256 threads: dctx = sum of partials; G; A-fragment images adc (rows d / k = e) and
+// adcT (rows e / k = d)
+__global__ __launch_bounds__(256) void slab_combine_kernel(const float* __restrict__ part, int nblk,
+                                                           const float* __restrict__ ctx32, float* __restrict__ G,
+                                                           bf16* __restrict__ adc, bf16* __restrict__ adcT) {
+  __shared__ float sd[32][33];
+  __shared__ float sg[32][9];
+  const int nh = blockIdx.x, n = nh / NH, h = nh % NH;
+  const int tid = threadIdx.x;
+  const float* pb = part + ((int64_t)n * nblk * NH + h) * 1024;
+  const int64_t bstride = (int64_t)NH * 1024;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = tid * 4 + i, d = idx >> 5, e = idx & 31;
+    float a = 0.f;
+    for (int b = 0; b < nblk; ++b) a += pb[b * bstride + idx];
+    sd[d][e] = a;
+  }
+  __syncthreads();
+  {  // G_d = sum_e dctx[d][e] ctx[d][e]: thread (d, 8 groups of 4 e)
+    const int d = tid >> 3, eg = tid & 7;
+    float a = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a += sd[d][eg * 4 + j] * ctx32[((int64_t)nh * 32 + d) * 32 + eg * 4 + j];
+    sg[d][eg] = a;
+  }
+  __syncthreads();
+  if (tid < 32) {
+    float a = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a += sg[tid][j];
+    G[(int64_t)nh * 32 + tid] = a;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = tid + i * 256;
+    const int tile = idx >> 8, lane = (idx >> 2) & 63, jp = idx & 3;
+    const int g = lane >> 4, l16 = lane & 15;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int j = jp * 2 + jj;
+      const int k = kslot(g, j);
+      const int row = tile * 16 + l16;
+      const int64_t o = (((int64_t)nh * 2 + tile) * 64 + lane) * 8 + j;
+      adc[o] = (bf16)sd[row][k];   // rows d, k = e
+      adcT[o] = (bf16)sd[k][row];  // rows e, k = d
+    }
+  }
+}
+
+// slab_dx: wave = 16*NV pixels of one frame, all heads.  grid (cdiv(HW, 64*NV), Nf), 256 threads,
+// dynamic LDS: 4 waves x [16*NV][DQLD] bf16 (this head's dq|dk|dv) + C floats (dgamma).
+constexpr int DQLD = 104;
+template <int C, int NV>
+__global__ __launch_bounds__(256, 2) void slab_dx_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ dy, const float* __restrict__ gamma,
+    const bf16* __restrict__ wqkv, const bf16* __restrict__ wqkv_t, const bf16* __restrict__ wout_t,
+    const float* __restrict__ mz, const float* __restrict__ G, const bf16* __restrict__ actT,
+    const bf16* __restrict__ actx, const bf16* __restrict__ adc, const bf16* __restrict__ adcT,
+    bf16* __restrict__ dx, bf16* __restrict__ dqkv_out, bf16* __restrict__ o_out, bf16* __restrict__ xn_out,
+    float* __restrict__ dgamma_part, int HW, float scale, float eps) {
+  constexpr int KS = C / 32, CT = C / 16;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sg = smem;  // [C]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  bf16* sq = reinterpret_cast<bf16*>(smem + C) + wid * 16 * NV * DQLD;
+  for (int e = tid; e < C; e += 256) sg[e] = 0.f;
+  __syncthreads();
+  const int n = blockIdx.y;
+  const int p0 = (blockIdx.x * 4 + wid) * 16 * NV;
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  if (p0 < HW) {
+    const int64_t rb = (int64_t)n * HW;
+    bf16x8 xf[NV][KS];
+    float mean[NV], rstd[NV];
+#pragma unroll
+    for (int vt = 0; vt < NV; ++vt) {
+      const int p = p0 + vt * 16 + lr;
+      const bool ok = p < HW;
+      float a[KS][8];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        if (ok) load8(x + (rb + p) * C + ks * 32 + lg * 8, a[ks]);
+        else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) a[ks][i] = 0.f;
+        }
+      }
+      float sm = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sm += a[ks][i];
+      mean[vt] = grp4_sum(sm) / C;
+      float q = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { const float d = a[ks][i] - mean[vt]; q = fmaf(d, d, q); }
+      rstd[vt] = 1.f / sqrtf(grp4_sum(q) / C + eps);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          xf[vt][ks][i] = (bf16)(ok ? (a[ks][i] - mean[vt]) * rstd[vt] * gamma[ks * 32 + lg * 8 + i] : 0.f);
+        if (ok && xn_out) *reinterpret_cast<bf16x8*>(xn_out + (rb + p) * C + ks * 32 + lg * 8) = xf[vt][ks];
+      }
+    }
+    f32x4 dxacc[CT][NV];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+      for (int vt = 0; vt < NV; ++vt) dxacc[ct][vt] = z4;
+
+    for (int h = 0; h < NH; ++h) {
+      const int64_t fo = ((int64_t)(n * NH + h) * 2) * 64 * 8;
+      bf16x8 aT[2], ax[2], ad[2], adT[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        aT[t] = ld16(actT + fo + (t * 64 + lane) * 8);
+        ax[t] = ld16(actx + fo + (t * 64 + lane) * 8);
+        ad[t] = ld16(adc + fo + (t * 64 + lane) * 8);
+        adT[t] = ld16(adcT + fo + (t * 64 + lane) * 8);
+      }
+      // per-lane softmax stats of k and G for d = t*16 + 4g + r
+      float Mk[2][4], iZ[2][4], Gd[2][4];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int d = t * 16 + lg * 4 + r;
+          const int64_t i = (int64_t)(n * NH + h) * 32 + d;
+          Mk[t][r] = mz[i * 2];
+          iZ[t][r] = 1.f / mz[i * 2 + 1];
+          Gd[t][r] = G[i];
+        }
+#pragma unroll
+      for (int vt = 0; vt < NV; ++vt) {
+        const int p = p0 + vt * 16 + lr;
+        const bool ok = p < HW;
+        bf16x8 dyf[KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) dyf[ks] = ok ? ld16(dy + (rb + p) * C + ks * 32 + lg * 8) : zero8();
+        // q, k, v (rows d/e = t*16 + 4g + r, column pixel lr) and do
+        float qv[2][4], kv[2][4], vv[2][4], dov[2][4];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          f32x4 aq = z4, ak = z4, av = z4, ao = z4;
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) {
+            const int off = ks * 32 + lg * 8;
+            aq = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld16(wqkv + (int64_t)(h * DH + t * 16 + lr) * C + off), xf[vt][ks], aq, 0, 0, 0);
+            ak = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld16(wqkv + (int64_t)(INNER + h * DH + t * 16 + lr) * C + off), xf[vt][ks], ak, 0, 0, 0);
+            av = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld16(wqkv + (int64_t)(2 * INNER + h * DH + t * 16 + lr) * C + off), xf[vt][ks], av, 0, 0, 0);
+            ao = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld16(wout_t + (int64_t)(h * DH + t * 16 + lr) * C + off), dyf[ks], ao, 0, 0, 0);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) { qv[t][r] = aq[r]; kv[t][r] = ak[r]; vv[t][r] = av[r]; dov[t][r] = ao[r]; }
+        }
+        // sm = softmax_d(q); q~ = scale sm
+        float mx = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mx = fmaxf(mx, qv[t][r]);
+        mx = grp4_max(mx);
+        float ssum = 0.f;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            qv[t][r] = __builtin_amdgcn_exp2f((qv[t][r] - mx) * LOG2E);
+            ssum += qv[t][r];
+          }
+        const float inv = __builtin_amdgcn_rcpf(grp4_sum(ssum));
+        float qs[2][4], kt[2][4];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            qv[t][r] *= inv;              // sm
+            qs[t][r] = qv[t][r] * scale;  // q~
+            kt[t][r] = __builtin_amdgcn_exp2f((kv[t][r] - Mk[t][r]) * LOG2E) * iZ[t][r];  // k~
+          }
+        const bf16x8 qb = pack_kslot(qs[0], qs[1]);
+        const bf16x8 kb = pack_kslot(kt[0], kt[1]);
+        const bf16x8 vb = pack_kslot(vv[0], vv[1]);
+        const bf16x8 dob = pack_kslot(dov[0], dov[1]);
+        float dq[2][4], dk[2][4], dvv[2][4];
+        float sdq = 0.f;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const f32x4 oT = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aT[t], qb, z4, 0, 0, 0);
+          const f32x4 dqt = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[t], dob, z4, 0, 0, 0);
+          const f32x4 dkt = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ad[t], vb, z4, 0, 0, 0);
+          const f32x4 dvt = __builtin_amdgcn_mfma_f32_16x16x32_bf16(adT[t], kb, z4, 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            dq[t][r] = dqt[r];
+            sdq = fmaf(qv[t][r], dqt[r], sdq);
+            dk[t][r] = kt[t][r] * (dkt[r] - Gd[t][r]);
+            dvv[t][r] = dvt[r];
+          }
+          if (ok && o_out) {
+            float o4[4] = {oT[0], oT[1], oT[2], oT[3]};
+            store4(o_out + (rb + p) * INNER + h * DH + t * 16 + lg * 4, o4);
+          }
+        }
+        sdq = grp4_sum(sdq);
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dq[t][r] = scale * qv[t][r] * (dq[t][r] - sdq);
+        // stage dq | dk | dv of this pixel tile: row = pixel, column kind*32 + d
+        bf16* row = sq + (vt * 16 + lr) * DQLD;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          store4(row + t * 16 + lg * 4, dq[t]);
+          store4(row + 32 + t * 16 + lg * 4, dk[t]);
+          store4(row + 64 + t * 16 + lg * 4, dvv[t]);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // dxn^T += W_qkv[h rows]^T [dq|dk|dv]^T ; emit dqkv
+#pragma unroll
+      for (int kind = 0; kind < 3; ++kind) {
+        bf16x8 bq[NV];
+#pragma unroll
+        for (int vt = 0; vt < NV; ++vt) bq[vt] = ld16(sq + (vt * 16 + lr) * DQLD + kind * 32 + lg * 8);
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          const bf16x8 a = ld16(wqkv_t + (int64_t)(ct * 16 + lr) * QKV + kind * INNER + h * DH + lg * 8);
+#pragma unroll
+          for (int vt = 0; vt < NV; ++vt) dxacc[ct][vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq[vt], dxacc[ct][vt], 0, 0, 0);
+        }
+        if (dqkv_out) {
+#pragma unroll
+          for (int vt = 0; vt < NV; ++vt) {
+            const int p = p0 + vt * 16 + lr;
+            if (p < HW) *reinterpret_cast<bf16x8*>(dqkv_out + (rb + p) * QKV + kind * INNER + h * DH + lg * 8) = bq[vt];
+          }
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    // LN backward + residual; dgamma partial
+#pragma unroll
+    for (int vt = 0; vt < NV; ++vt) {
+      const int p = p0 + vt * 16 + lr;
+      const bool ok = p < HW;
+      float s1 = 0.f, s2 = 0.f;
+      float xh[CT][4];
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        const int co = ct * 16 + lg * 4;
+        float xv[4] = {0.f, 0.f, 0.f, 0.f};
+        if (ok) load4(x + (rb + p) * C + co, xv);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          xh[ct][r] = ok ? (xv[r] - mean[vt]) * rstd[vt] : 0.f;
+          const float g = dxacc[ct][vt][r] * gamma[co + r];
+          s1 += g;
+          s2 = fmaf(g, xh[ct][r], s2);
+        }
+      }
+      s1 = grp4_sum(s1) / C;
+      s2 = grp4_sum(s2) / C;
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        const int co = ct * 16 + lg * 4;
+        float d4[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          d4[r] = dxacc[ct][vt][r] * xh[ct][r];
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) d4[r] += __shfl_xor(d4[r], o, 64);
+        }
+        if (lr == 0) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) atomicAdd(&sg[co + r], d4[r]);
+        }
+        if (ok) {
+          float dv4[4], o4[4];
+          load4(dy + (rb + p) * C + co, dv4);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o4[r] = rstd[vt] * (dxacc[ct][vt][r] * gamma[co + r] - s1 - xh[ct][r] * s2) + dv4[r];
+          store4(dx + (rb + p) * C + co, o4);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < C; e += 256)
+    dgamma_part[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * C + e] = sg[e];
+}
+
+__global__ void slaf_sum_rows_kernel(const float* __restrict__ part, float* __restrict__ dst, int nrows, int C,
+                                     int accumulate) {
+  const int c = blockIdx.x;
+  float s = 0.f;
+  for (int k = threadIdx.x; k < nrows; k += 64) s += part[(int64_t)k * C + c];
+  s = wave_sum(s);
+  if (threadIdx.x == 0) dst[c] = accumulate ? dst[c] + s : s;
+}
+
+}  // namespace
+
+extern "C" {
+
+// blocks per frame used by the stats / dctx kernels (each covers spb 64-pixel sub-chunks)
+int cesm_slaf_nblk(int Nf, int HW) {
+  const int nsc = (HW + 63) / 64;
+  int nblk = std::max(1, 1024 / std::max(1, Nf));
+  nblk = std::min(nblk, nsc);
+  const int spb = (nsc + nblk - 1) / nblk;
+  return (nsc + spb - 1) / spb;
+}
+
+// Fused SLA block forward (bf16, C = 64).  x, y [Nf*HW][C]; wqkv [768][C], wout [C][256] packed bf16;
+// saved for the backward: mz [Nf][8][32][2] (softmax max / normaliser of k over pixels),
+// ctx32 [Nf][8][32][32] fp32, actT / actx [Nf][8][2][64][8] bf16 (ctx as MFMA A fragments).
+// ws: cesm_slaf_nblk(Nf, HW) * Nf * 8 * 1088 floats.
+int cesm_slaf_fwd(const void* x, const float* gamma, const void* wqkv, const void* wout, const float* bout, void* y,
+                  float* mz, float* ctx32, void* actT, void* actx, float* ws, int Nf, int HW, int C, float scale,
+                  float eps, hipStream_t stream) {
+  if (C != 64 || Nf < 1 || HW < 1) return CESM_EUNSUPPORTED;
+  const int nsc = (HW + 63) / 64;
+  const int nblk = cesm_slaf_nblk(Nf, HW);
+  const int spb = (nsc + nblk - 1) / nblk;
+  slaf_stats_kernel<64><<<dim3(nblk, Nf), 512, 0, stream>>>((const bf16*)x, gamma, (const bf16*)wqkv, ws, HW, spb, eps);
+  slaf_combine_kernel<<<Nf * NH, 256, 0, stream>>>(ws, nblk, mz, ctx32, (bf16*)actT, (bf16*)actx);
+  constexpr int NV = 4;
+  slaf_out_kernel<64, NV><<<dim3((unsigned)cdiv(HW, 64 * NV), Nf), 256, 0, stream>>>(
+      (const bf16*)x, gamma, (const bf16*)wqkv, (const bf16*)wout, bout, (const bf16*)actT, (bf16*)y, HW, scale, eps);
+  return cesm_launch_status();
+}
+
+// Fused SLA block backward (bf16, C = 64), dx path: dx (+ dy residual), dgamma (+)=, and for the weight
+// gradients dqkv [Nf*HW][768], o [Nf*HW][256], xn [Nf*HW][C] (each nullable).  mz/ctx32/actT/actx from
+// cesm_slaf_fwd; wqkv_t [C][768] and wout_t [256][C] swap-packed.  ws: max(nblk*Nf*8*1024, ...) floats
+// + Nf*8*(32 + 2*2*64*8/2) + grid*C (see kernels.slaf_bwd for the carve-up).
+int cesm_slaf_bwd(const void* x, const void* dy, const float* gamma, const void* wqkv, const void* wqkv_t,
+                  const void* wout_t, const float* mz, const float* ctx32, const void* actT, const void* actx,
+                  void* dx, void* dqkv, void* o, void* xn, float* dgamma, float* part, float* G, void* adc, void* adcT,
+                  float* dgp, int Nf, int HW, int C, float scale, float eps, int accumulate, hipStream_t stream) {
+  if (C != 64 || Nf < 1 || HW < 1) return CESM_EUNSUPPORTED;
+  const int nsc = (HW + 63) / 64;
+  const int nblk = cesm_slaf_nblk(Nf, HW);
+  const int spb = (nsc + nblk - 1) / nblk;
+  slab_dctx_kernel<64><<<dim3(nblk, Nf), 512, 0, stream>>>((const bf16*)x, (const bf16*)dy, gamma, (const bf16*)wqkv,
+                                                           (const bf16*)wout_t, part, HW, spb, scale, eps);
+  slab_combine_kernel<<<Nf * NH, 256, 0, stream>>>(part, nblk, ctx32, G, (bf16*)adc, (bf16*)adcT);
+  constexpr int NV = 2;
+  dim3 grid((unsigned)cdiv(HW, 64 * NV), Nf);
+  const size_t sm = (size_t)64 * 4 + (size_t)4 * 16 * NV * DQLD * 2;
+  slab_dx_kernel<64, NV><<<grid, 256, sm, stream>>>(
+      (const bf16*)x, (const bf16*)dy, gamma, (const bf16*)wqkv, (const bf16*)wqkv_t, (const bf16*)wout_t, mz, G,
+      (const bf16*)actT, (const bf16*)actx, (const bf16*)adc, (const bf16*)adcT, (bf16*)dx, (bf16*)dqkv, (bf16*)o,
+      (bf16*)xn, dgp, HW, scale, eps);
+  if (dgamma) slaf_sum_rows_kernel<<<C, 64, 0, stream>>>(dgp, dgamma, (int)(grid.x * grid.y), C, accumulate);
+  return cesm_launch_status();
+}
+
+// grid blocks of cesm_slaf_bwd's dx kernel (rows of its dgamma partial)
+int cesm_slaf_bwd_nblk(int Nf, int HW) { return (int)cdiv(HW, 128) * Nf; }
+
+}  // extern "C"

@@ -301,6 +301,59 @@ def tblock_bwd(x, dy, gamma, mr, lse, wqkv, wqkv_t, wout_t, bias, rot, dgamma, d
     return dx, dqkv, o, xn
 
 
+SLAF_C = (64,)
+
+
+def slaf_fwd(x, gamma, wqkv, wout, bout, scale, eps=1e-5):
+    """fused spatial-linear-attention block forward (bf16, C=64); x [Nf, H, W, C].
+    Returns y and the saved state (mz, ctx32, actT, actx) for slaf_bwd."""
+    Nf, H, W, C = x.shape
+    HW = H * W
+    _chk(x, dtype=torch.bfloat16)
+    _chk(wqkv, (768, C), torch.bfloat16)
+    _chk(wout, (C, 256), torch.bfloat16)
+    dev = x.device
+    y = empty(x.shape, x.dtype, dev)
+    mz = empty((Nf, 8, 32, 2), torch.float32, dev)
+    ctx32 = empty((Nf, 8, 32, 32), torch.float32, dev)
+    actT = empty((Nf, 8, 2, 64, 8), torch.bfloat16, dev)
+    actx = empty((Nf, 8, 2, 64, 8), torch.bfloat16, dev)
+    nblk = lib().cesm_slaf_nblk(Nf, HW)
+    ws = empty((nblk * Nf * 8 * 1088,), torch.float32, dev)
+    call("cesm_slaf_fwd", P(x), P(gamma), P(wqkv), P(wout), P(bout), P(y), P(mz), P(ctx32), P(actT), P(actx), P(ws),
+         Nf, HW, C, float(scale), float(eps), S())
+    return y, (mz, ctx32, actT, actx)
+
+
+def slaf_bwd(x, dy, gamma, wqkv, wqkv_t, wout_t, state, dgamma, scale, want_wgrad_inputs=True, eps=1e-5):
+    """fused SLA block backward, dx path (bf16, C=64).  Returns (dx, dqkv, o, xn); the last three feed the
+    to_qkv / to_out weight-gradient GEMMs."""
+    Nf, H, W, C = x.shape
+    HW = H * W
+    mz, ctx32, actT, actx = state
+    _chk(dy, x.shape, torch.bfloat16)
+    _chk(wqkv_t, (C, 768), torch.bfloat16)
+    _chk(wout_t, (256, C), torch.bfloat16)
+    dev = x.device
+    dx = empty(x.shape, x.dtype, dev)
+    if want_wgrad_inputs:
+        dqkv = empty((Nf, H, W, 768), x.dtype, dev)
+        o = empty((Nf, H, W, 256), x.dtype, dev)
+        xn = empty(x.shape, x.dtype, dev)
+    else:
+        dqkv = o = xn = None
+    nblk = lib().cesm_slaf_nblk(Nf, HW)
+    part = empty((nblk * Nf * 8 * 1024,), torch.float32, dev)
+    G = empty((Nf, 8, 32), torch.float32, dev)
+    adc = empty((Nf, 8, 2, 64, 8), torch.bfloat16, dev)
+    adcT = empty((Nf, 8, 2, 64, 8), torch.bfloat16, dev)
+    dgp = empty((lib().cesm_slaf_bwd_nblk(Nf, HW), C), torch.float32, dev)
+    call("cesm_slaf_bwd", P(x), P(dy), P(gamma), P(wqkv), P(wqkv_t), P(wout_t), P(mz), P(ctx32), P(actT), P(actx),
+         P(dx), P(dqkv), P(o), P(xn), P(dgamma), P(part), P(G), P(adc), P(adcT), P(dgp), Nf, HW, C, float(scale),
+         float(eps), 1, S())
+    return dx, dqkv, o, xn
+
+
 def sla_fwd(qkv, Nf, HW, scale):
     nchunk = lib().cesm_sla_nchunk(HW)
     out = empty((qkv.shape[0], 256), qkv.dtype, qkv.device)

@@ -275,10 +275,15 @@ def resnet_bwd(rc, rb, st, dout):
 
 
 FUSED_TBLOCK = os.environ.get("CESM_NO_FUSED_TBLOCK", "0") != "1"
+# widest channel count routed to the fused kernels: below it the 768-channel qkv intermediate is what
+# costs (HBM); above it the level is small and the unfused GEMMs are cheaper than per-pixel-group
+# weight re-reads
+FUSED_TBLOCK_MAXC = int(os.environ.get("CESM_TBLOCK_MAXC", "64"))
 
 
 def _tblock_fused(rc, C):
-    return FUSED_TBLOCK and rc.cdt == torch.bfloat16 and rc.F <= 16 and C in K.TBLOCK_C
+    return (FUSED_TBLOCK and rc.cdt == torch.bfloat16 and rc.F <= 16 and C in K.TBLOCK_C
+            and C <= FUSED_TBLOCK_MAXC)
 
 
 def tattn_fwd(rc, res_mod, x):
@@ -329,16 +334,30 @@ def tattn_bwd(rc, res_mod, st, dy):
     return K.ln_bwd(dn, st.x, st.mr, _flat(pre.norm.gamma), gbuf(pre.norm.gamma), dres=dy)
 
 
+FUSED_SLA = os.environ.get("CESM_NO_FUSED_SLA", "0") != "1"
+
+
+def _sla_fused(rc, C):
+    return FUSED_SLA and rc.cdt == torch.bfloat16 and C in K.SLAF_C
+
+
 def sla_fwd(rc, res_mod, x):
-    """Residual(PreNorm(SpatialLinearAttention)) per frame (video_net.py:313-347)."""
+    """Residual(PreNorm(SpatialLinearAttention)) per frame (video_net.py:313-347).
+    bf16, C=64: fused kernels (csrc/sla_fused.hip); otherwise LN -> to_qkv -> core -> to_out."""
     pre = res_mod.fn
     sla = pre.fn
+    Nb, H, W, C = x.shape
+    if _sla_fused(rc, C):
+        wq = rc.packed(sla.to_qkv.weight, 768, C, 1, 1, 0, 0)
+        wo = rc.packed(sla.to_out.weight, C, 256, 1, 1, 0, 0)
+        y, state = K.slaf_fwd(x, _flat(pre.norm.gamma), wq, wo, sla.to_out.bias, sla.scale, eps=pre.norm.eps)
+        st = SimpleNamespace(fused=True, x=x, state=state) if rc.save else None
+        return y, st
     n, mr = K.ln_fwd(x, _flat(pre.norm.gamma), save=rc.save, eps=pre.norm.eps)
     qkv, qst = conv_forward(rc, ConvSpec(sla.to_qkv), n)
-    Nb, H, W, _ = x.shape
     o, ctx, ml = K.sla_fwd(qkv.view(-1, 768), Nb, H * W, sla.scale)
     y, ost = conv_forward(rc, ConvSpec(sla.to_out), o.view(Nb, H, W, 256), None, res=x)
-    st = SimpleNamespace(x=x, mr=mr, qkv=qkv, ctx=ctx, ml=ml, qst=qst, ost=ost) if rc.save else None
+    st = SimpleNamespace(fused=False, x=x, mr=mr, qkv=qkv, ctx=ctx, ml=ml, qst=qst, ost=ost) if rc.save else None
     return y, st
 
 
@@ -346,6 +365,21 @@ def sla_bwd(rc, res_mod, st, dy):
     pre = res_mod.fn
     sla = pre.fn
     Nb, H, W, C = st.x.shape
+    if st.fused:
+        wq = rc.packed(sla.to_qkv.weight, 768, C, 1, 1, 0, 0)
+        wq_t = rc.packed(sla.to_qkv.weight, C, 768, 1, 1, 1, 1)
+        wo_t = rc.packed(sla.to_out.weight, 256, C, 1, 1, 1, 1)
+        dwq, dwo, dbo = gbuf(sla.to_qkv.weight), gbuf(sla.to_out.weight), gbuf(sla.to_out.bias)
+        dx, dqkv, o, xn = K.slaf_bwd(st.x, dy, _flat(pre.norm.gamma), wq, wq_t, wo_t, st.state,
+                                     gbuf(pre.norm.gamma), sla.scale,
+                                     want_wgrad_inputs=dwq is not None or dwo is not None, eps=pre.norm.eps)
+        if dwq is not None:
+            K.conv_wgrad(xn, None, dqkv, None, dwq, (H, W, 768, 1, 1, 1, 0, 1), 0, 0)
+        if dwo is not None:
+            K.conv_wgrad(o, None, dy, None, dwo, (H, W, C, 1, 1, 1, 0, 1), 0, 0)
+        if dbo is not None:
+            K.colsum(dy, dbo)
+        return dx
     do = conv_backward(rc, ConvSpec(sla.to_out), st.ost, dy)
     dqkv = K.sla_bwd(st.qkv.view(-1, 768), do.view(-1, 256), st.ctx, st.ml, Nb, H * W, sla.scale)
     dn = conv_backward(rc, ConvSpec(sla.to_qkv), st.qst, dqkv.view(Nb, H, W, 768))

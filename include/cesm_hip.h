@@ -117,6 +117,26 @@ int cesm_sla_fwd(int dtype, const void* qkv, void* out, float* ctx, float* ml, f
 int cesm_sla_bwd(int dtype, const void* qkv, const void* dout, const float* ctx, const float* ml, void* dqkv,
                  float* ws, int Nf, int HW, float scale, hipStream_t stream);
 
+/* Fused spatial-linear-attention block (bf16, C = 64; csrc/sla_fused.hip): y = x + Residual(PreNorm(
+ * SpatialLinearAttention)) (video_net.py:313-347) without per-pixel intermediates in HBM: online-softmax
+ * context partials -> combine -> output.  Saves mz [Nf][8][32][2] (max, normaliser of k over pixels),
+ * ctx32 [Nf][8][32][32] and the context as MFMA A fragments actT/actx [Nf][8][2][64][8] bf16.
+ * ws: cesm_slaf_nblk(Nf, HW) * Nf * 8 * 1088 floats. */
+int cesm_slaf_nblk(int Nf, int HW);
+int cesm_slaf_fwd(const void* x, const float* gamma, const void* wqkv, const void* wout, const float* bout, void* y,
+                  float* mz, float* ctx32, void* actT, void* actx, float* ws, int Nf, int HW, int C, float scale,
+                  float eps, hipStream_t stream);
+
+/* Fused SLA block backward, dx path (bf16, C = 64): dctx partials -> combine (G_d = sum_e dctx ctx, dctx as
+ * A fragments adc/adcT) -> dx (+ dy residual), dgamma (+)=; emits (nullable) dqkv [..][768], o [..][256],
+ * xn [..][C] for the to_qkv / to_out weight gradients.  part: nblk*Nf*8*1024 floats, G: Nf*8*32 floats,
+ * adc/adcT: Nf*8*2*64*8 bf16, dgp: cesm_slaf_bwd_nblk(Nf, HW)*C floats. */
+int cesm_slaf_bwd(const void* x, const void* dy, const float* gamma, const void* wqkv, const void* wqkv_t,
+                  const void* wout_t, const float* mz, const float* ctx32, const void* actT, const void* actx,
+                  void* dx, void* dqkv, void* o, void* xn, float* dgamma, float* part, float* G, void* adc, void* adcT,
+                  float* dgp, int Nf, int HW, int C, float scale, float eps, int accumulate, hipStream_t stream);
+int cesm_slaf_bwd_nblk(int Nf, int HW);
+
 /* ---- small ops, loss, optimizer, data (csrc/misc.hip) ------------------------------------- */
 /* SinusoidalPosEmb (video_net.py:101-113) */
 int cesm_sinusoidal(const int64_t* t, float* emb, int B, int dim, hipStream_t stream);

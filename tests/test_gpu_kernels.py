@@ -500,3 +500,94 @@ def test_fused_temporal_block_backward(dev, C, Fr):
     print(f"fused tblock bwd C={C} F={Fr}: " + " ".join(f"{k} {v:.2e}" for k, v in errs.items()))
     for k, v in errs.items():
         assert v < 3e-2, (k, v)
+
+
+def _sla_block(C, dev):
+    res = VN.Residual(VN.PreNorm(C, VN.SpatialLinearAttention(C, 8, 32))).to(dev)
+    with torch.no_grad():
+        res.fn.norm.gamma.uniform_(0.5, 1.5)
+        res.fn.fn.to_out.bias.uniform_(-0.1, 0.1)
+    return res
+
+
+def _sla_block_ref(res, C):
+    from oracle import ref_cpu as R
+    ref = R.Residual(R.PreNorm(C, R.SpatialLinearAttention(C, heads=8, dim_head=32))).double()
+    sla = res.fn.fn
+    ref.fn.norm.gamma.data.copy_(res.fn.norm.gamma.detach().cpu().double())
+    ref.fn.fn.to_qkv.weight.data.copy_(sla.to_qkv.weight.detach().cpu().to(torch.bfloat16).double())
+    ref.fn.fn.to_out.weight.data.copy_(sla.to_out.weight.detach().cpu().to(torch.bfloat16).double())
+    ref.fn.fn.to_out.bias.data.copy_(sla.to_out.bias.detach().cpu().double())
+    return ref
+
+
+@pytest.mark.parametrize("H,W", [(8, 8), (12, 20), (37, 29)])
+def test_fused_sla_forward(dev, H, W):
+    """cesm_slaf_fwd (LN + online-softmax context + output projection, no per-pixel intermediates)
+    vs a float64 evaluation of the reference block on bf16-rounded inputs/weights"""
+    torch.manual_seed(13)
+    B, Fr, C = 2, 3, 64
+    res = _sla_block(C, dev)
+    sla = res.fn.fn
+    x = q(torch.randn(B, C, Fr, H, W), torch.bfloat16)
+    xd = to_cl(x).to(dev, torch.bfloat16)
+    wq = K.conv_pack(sla.to_qkv.weight.detach().reshape(768, C), torch.bfloat16, 768, C, 1, 1, 0, 0)
+    wo = K.conv_pack(sla.to_out.weight.detach().reshape(C, 256), torch.bfloat16, C, 256, 1, 1, 0, 0)
+    y, st = K.slaf_fwd(xd, res.fn.norm.gamma.detach().reshape(-1).contiguous(), wq, wo, sla.to_out.bias.detach(),
+                       sla.scale)
+    ref = _sla_block_ref(res, C)
+    with torch.no_grad():
+        yr = ref(x)
+    err = rel(from_cl(y, B), yr)
+    # the context itself: ctx[n][h][d][e]
+    xr = x.permute(0, 2, 1, 3, 4).reshape(B * Fr, C, H * W)
+    mu = xr.mean(1, keepdim=True)
+    var = xr.var(1, unbiased=False, keepdim=True)
+    xn = (xr - mu) / (var + 1e-5).sqrt() * ref.fn.norm.gamma.reshape(1, C, 1)
+    qkv = torch.einsum("oc,ncp->nop", ref.fn.fn.to_qkv.weight.reshape(768, C), xn)
+    k = qkv[:, 256:512].reshape(B * Fr, 8, 32, H * W).softmax(-1)
+    v = qkv[:, 512:].reshape(B * Fr, 8, 32, H * W)
+    ctx = torch.einsum("nhdp,nhep->nhde", k, v)
+    cerr = rel(st[1], ctx)
+    print(f"fused sla fwd HxW={H}x{W}: y rel {err:.2e} ctx rel {cerr:.2e}")
+    assert cerr < 2e-2
+    assert err < 2e-2
+
+
+@pytest.mark.parametrize("H,W", [(8, 8), (12, 20), (37, 29)])
+def test_fused_sla_backward(dev, H, W):
+    """cesm_slaf_bwd (+ weight gradients from its dqkv/o/xn outputs) vs float64 autograd through the
+    reference SpatialLinearAttention block"""
+    torch.manual_seed(14)
+    B, Fr, C = 2, 3, 64
+    res = _sla_block(C, dev)
+    sla = res.fn.fn
+    x = q(torch.randn(B, C, Fr, H, W), torch.bfloat16)
+    g = q(torch.randn(B, C, Fr, H, W), torch.bfloat16)
+    xd = to_cl(x).to(dev, torch.bfloat16)
+    gd = to_cl(g).to(dev, torch.bfloat16)
+    wqkv = sla.to_qkv.weight.detach().reshape(768, C)
+    wout = sla.to_out.weight.detach().reshape(C, 256)
+    wq = K.conv_pack(wqkv, torch.bfloat16, 768, C, 1, 1, 0, 0)
+    wo = K.conv_pack(wout, torch.bfloat16, C, 256, 1, 1, 0, 0)
+    wq_t = K.conv_pack(wqkv, torch.bfloat16, C, 768, 1, 1, 1, 1)
+    wo_t = K.conv_pack(wout, torch.bfloat16, 256, C, 1, 1, 1, 1)
+    gamma = res.fn.norm.gamma.detach().reshape(-1).contiguous()
+    _, st = K.slaf_fwd(xd, gamma, wq, wo, sla.to_out.bias.detach(), sla.scale)
+    dgamma = torch.zeros(C, device=dev)
+    dx, dqkv, o, xn = K.slaf_bwd(xd, gd, gamma, wq, wq_t, wo_t, st, dgamma, sla.scale)
+    dwq = dqkv.reshape(-1, 768).double().t() @ xn.reshape(-1, C).double()
+    dwo = gd.reshape(-1, C).double().t() @ o.reshape(-1, 256).double()
+    ref = _sla_block_ref(res, C)
+    xr = x.double().requires_grad_(True)
+    yr = ref(xr)
+    (yr * g.double()).sum().backward()
+    errs = {
+        "dx": rel(from_cl(dx, B), xr.grad),
+        "dgamma": rel(dgamma.double(), ref.fn.norm.gamma.grad.reshape(-1)),
+        "dWqkv": rel(dwq, ref.fn.fn.to_qkv.weight.grad.reshape(768, C)),
+        "dWout": rel(dwo, ref.fn.fn.to_out.weight.grad.reshape(C, 256)),
+    }
+    print(f"fused sla bwd HxW={H}x{W}: " + " ".join(f"{k} {v:.2e}" for k, v in errs.items()))
+    for k, v in errs.items():
+        assert v < 3e-2, (k, v)
