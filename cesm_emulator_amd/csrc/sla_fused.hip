@@ -550,10 +550,12 @@ __global__ __launch_bounds__(512) void slab_dctx_kernel(const bf16* __restrict__
 // grid (Nf * 8), 256 threads: dctx = sum of partials; G; A-fragment images adc (rows d / k = e) and
 // adcT (rows e / k = d)
 __global__ __launch_bounds__(256) void slab_combine_kernel(const float* __restrict__ part, int nblk,
-                                                           const float* __restrict__ ctx32, float* __restrict__ G,
-                                                           bf16* __restrict__ adc, bf16* __restrict__ adcT) {
+                                                           const float* __restrict__ ctx32, const float* __restrict__ mz,
+                                                           float* __restrict__ kimg, bf16* __restrict__ adc,
+                                                           bf16* __restrict__ adcT) {
   __shared__ float sd[32][33];
   __shared__ float sg[32][9];
+  __shared__ float sG[32];
   const int nh = blockIdx.x, n = nh / NH, h = nh % NH;
   const int tid = threadIdx.x;
   const float* pb = part + ((int64_t)n * nblk * NH + h) * 1024;
@@ -578,7 +580,22 @@ __global__ __launch_bounds__(256) void slab_combine_kernel(const float* __restri
     float a = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) a += sg[tid][j];
-    G[(int64_t)nh * 32 + tid] = a;
+    sG[tid] = a;
+  }
+  __syncthreads();
+  // per-lane image for slab_dx: lane (g, i), d = t*16 + 4g + r:
+  //   [t*4 + r] = M_d log2(e) + log2(Z_d)  (k~ = exp2(k log2(e) - it)),  [8 + t*4 + r] = G_d
+  if (tid < 64) {
+    const int g = tid >> 4;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int d = t * 16 + 4 * g + r;
+        const float M = mz[((int64_t)nh * 32 + d) * 2], Z = mz[((int64_t)nh * 32 + d) * 2 + 1];
+        kimg[((int64_t)nh * 64 + tid) * 16 + t * 4 + r] = M * LOG2E + log2f(Z);
+        kimg[((int64_t)nh * 64 + tid) * 16 + 8 + t * 4 + r] = sG[d];
+      }
   }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -604,7 +621,7 @@ template <int C, int NV>
 __global__ __launch_bounds__(256, 2) void slab_dx_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ dy, const float* __restrict__ gamma,
     const bf16* __restrict__ wqkv, const bf16* __restrict__ wqkv_t, const bf16* __restrict__ wout_t,
-    const float* __restrict__ mz, const float* __restrict__ G, const bf16* __restrict__ actT,
+    const float* __restrict__ kimg, const bf16* __restrict__ actT,
     const bf16* __restrict__ actx, const bf16* __restrict__ adc, const bf16* __restrict__ adcT,
     bf16* __restrict__ dx, bf16* __restrict__ dqkv_out, bf16* __restrict__ o_out, bf16* __restrict__ xn_out,
     float* __restrict__ dgamma_part, int HW, float scale, float eps) {
@@ -672,17 +689,24 @@ __global__ __launch_bounds__(256, 2) void slab_dx_kernel(
         ad[t] = ld16(adc + fo + (t * 64 + lane) * 8);
         adT[t] = ld16(adcT + fo + (t * 64 + lane) * 8);
       }
-      // per-lane softmax stats of k and G for d = t*16 + 4g + r
-      float Mk[2][4], iZ[2][4], Gd[2][4];
+      // per-lane k-softmax offsets and G for d = t*16 + 4g + r (16-B loads of the combine's lane image)
+      float Kofs[2][4], Gd[2][4];
+      {
+        const f32x4* ki = reinterpret_cast<const f32x4*>(kimg + ((int64_t)(n * NH + h) * 64 + lane) * 16);
+        const f32x4 k0 = ki[0], k1 = ki[1], g0 = ki[2], g1 = ki[3];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { Kofs[0][r] = k0[r]; Kofs[1][r] = k1[r]; Gd[0][r] = g0[r]; Gd[1][r] = g1[r]; }
+      }
+      bf16x8 wh[4][2][KS];  // this head's q, k, v rows of W_qkv and do rows of W_out^T
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int d = t * 16 + lg * 4 + r;
-          const int64_t i = (int64_t)(n * NH + h) * 32 + d;
-          Mk[t][r] = mz[i * 2];
-          iZ[t][r] = 1.f / mz[i * 2 + 1];
-          Gd[t][r] = G[i];
+        for (int ks = 0; ks < KS; ++ks) {
+          const int off = ks * 32 + lg * 8;
+#pragma unroll
+          for (int kind = 0; kind < 3; ++kind)
+            wh[kind][t][ks] = ld16(wqkv + (int64_t)(kind * INNER + h * DH + t * 16 + lr) * C + off);
+          wh[3][t][ks] = ld16(wout_t + (int64_t)(h * DH + t * 16 + lr) * C + off);
         }
 #pragma unroll
       for (int vt = 0; vt < NV; ++vt) {
@@ -698,11 +722,10 @@ __global__ __launch_bounds__(256, 2) void slab_dx_kernel(
           f32x4 aq = z4, ak = z4, av = z4, ao = z4;
 #pragma unroll
           for (int ks = 0; ks < KS; ++ks) {
-            const int off = ks * 32 + lg * 8;
-            aq = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld16(wqkv + (int64_t)(h * DH + t * 16 + lr) * C + off), xf[vt][ks], aq, 0, 0, 0);
-            ak = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld16(wqkv + (int64_t)(INNER + h * DH + t * 16 + lr) * C + off), xf[vt][ks], ak, 0, 0, 0);
-            av = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld16(wqkv + (int64_t)(2 * INNER + h * DH + t * 16 + lr) * C + off), xf[vt][ks], av, 0, 0, 0);
-            ao = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld16(wout_t + (int64_t)(h * DH + t * 16 + lr) * C + off), dyf[ks], ao, 0, 0, 0);
+            aq = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[0][t][ks], xf[vt][ks], aq, 0, 0, 0);
+            ak = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[1][t][ks], xf[vt][ks], ak, 0, 0, 0);
+            av = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[2][t][ks], xf[vt][ks], av, 0, 0, 0);
+            ao = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[3][t][ks], dyf[ks], ao, 0, 0, 0);
           }
 #pragma unroll
           for (int r = 0; r < 4; ++r) { qv[t][r] = aq[r]; kv[t][r] = ak[r]; vv[t][r] = av[r]; dov[t][r] = ao[r]; }
@@ -730,7 +753,7 @@ __global__ __launch_bounds__(256, 2) void slab_dx_kernel(
           for (int r = 0; r < 4; ++r) {
             qv[t][r] *= inv;              // sm
             qs[t][r] = qv[t][r] * scale;  // q~
-            kt[t][r] = __builtin_amdgcn_exp2f((kv[t][r] - Mk[t][r]) * LOG2E) * iZ[t][r];  // k~
+            kt[t][r] = __builtin_amdgcn_exp2f(fmaf(kv[t][r], LOG2E, -Kofs[t][r]));  // k~
           }
         const bf16x8 qb = pack_kslot(qs[0], qs[1]);
         const bf16x8 kb = pack_kslot(kt[0], kt[1]);
@@ -848,13 +871,19 @@ __global__ __launch_bounds__(256, 2) void slab_dx_kernel(
     dgamma_part[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * C + e] = sg[e];
 }
 
-__global__ void slaf_sum_rows_kernel(const float* __restrict__ part, float* __restrict__ dst, int nrows, int C,
-                                     int accumulate) {
+__global__ __launch_bounds__(256) void slaf_sum_rows_kernel(const float* __restrict__ part, float* __restrict__ dst,
+                                                            int nrows, int C, int accumulate) {
+  __shared__ float red[4];
   const int c = blockIdx.x;
   float s = 0.f;
-  for (int k = threadIdx.x; k < nrows; k += 64) s += part[(int64_t)k * C + c];
+  for (int k = threadIdx.x; k < nrows; k += 256) s += part[(int64_t)k * C + c];
   s = wave_sum(s);
-  if (threadIdx.x == 0) dst[c] = accumulate ? dst[c] + s : s;
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    s = ((red[0] + red[1]) + red[2]) + red[3];
+    dst[c] = accumulate ? dst[c] + s : s;
+  }
 }
 
 }  // namespace
@@ -903,15 +932,15 @@ int cesm_slaf_bwd(const void* x, const void* dy, const float* gamma, const void*
   const int spb = (nsc + nblk - 1) / nblk;
   slab_dctx_kernel<64><<<dim3(nblk, Nf), 512, 0, stream>>>((const bf16*)x, (const bf16*)dy, gamma, (const bf16*)wqkv,
                                                            (const bf16*)wout_t, part, HW, spb, scale, eps);
-  slab_combine_kernel<<<Nf * NH, 256, 0, stream>>>(part, nblk, ctx32, G, (bf16*)adc, (bf16*)adcT);
+  slab_combine_kernel<<<Nf * NH, 256, 0, stream>>>(part, nblk, ctx32, mz, G, (bf16*)adc, (bf16*)adcT);
   constexpr int NV = 2;
   dim3 grid((unsigned)cdiv(HW, 64 * NV), Nf);
   const size_t sm = (size_t)64 * 4 + (size_t)4 * 16 * NV * DQLD * 2;
   slab_dx_kernel<64, NV><<<grid, 256, sm, stream>>>(
-      (const bf16*)x, (const bf16*)dy, gamma, (const bf16*)wqkv, (const bf16*)wqkv_t, (const bf16*)wout_t, mz, G,
+      (const bf16*)x, (const bf16*)dy, gamma, (const bf16*)wqkv, (const bf16*)wqkv_t, (const bf16*)wout_t, G,
       (const bf16*)actT, (const bf16*)actx, (const bf16*)adc, (const bf16*)adcT, (bf16*)dx, (bf16*)dqkv, (bf16*)o,
       (bf16*)xn, dgp, HW, scale, eps);
-  if (dgamma) slaf_sum_rows_kernel<<<C, 64, 0, stream>>>(dgp, dgamma, (int)(grid.x * grid.y), C, accumulate);
+  if (dgamma) slaf_sum_rows_kernel<<<C, 256, 0, stream>>>(dgp, dgamma, (int)(grid.x * grid.y), C, accumulate);
   return cesm_launch_status();
 }
 

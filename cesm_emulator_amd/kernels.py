@@ -344,7 +344,7 @@ def slaf_bwd(x, dy, gamma, wqkv, wqkv_t, wout_t, state, dgamma, scale, want_wgra
         dqkv = o = xn = None
     nblk = lib().cesm_slaf_nblk(Nf, HW)
     part = empty((nblk * Nf * 8 * 1024,), torch.float32, dev)
-    G = empty((Nf, 8, 32), torch.float32, dev)
+    G = empty((Nf, 8, 64, 16), torch.float32, dev)  # per-lane k-softmax offsets + G image
     adc = empty((Nf, 8, 2, 64, 8), torch.bfloat16, dev)
     adcT = empty((Nf, 8, 2, 64, 8), torch.bfloat16, dev)
     dgp = empty((lib().cesm_slaf_bwd_nblk(Nf, HW), C), torch.float32, dev)

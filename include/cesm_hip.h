@@ -129,7 +129,7 @@ int cesm_slaf_fwd(const void* x, const float* gamma, const void* wqkv, const voi
 
 /* Fused SLA block backward, dx path (bf16, C = 64): dctx partials -> combine (G_d = sum_e dctx ctx, dctx as
  * A fragments adc/adcT) -> dx (+ dy residual), dgamma (+)=; emits (nullable) dqkv [..][768], o [..][256],
- * xn [..][C] for the to_qkv / to_out weight gradients.  part: nblk*Nf*8*1024 floats, G: Nf*8*32 floats,
+ * xn [..][C] for the to_qkv / to_out weight gradients.  part: nblk*Nf*8*1024 floats, G: Nf*8*64*16 floats,
  * adc/adcT: Nf*8*2*64*8 bf16, dgp: cesm_slaf_bwd_nblk(Nf, HW)*C floats. */
 int cesm_slaf_bwd(const void* x, const void* dy, const float* gamma, const void* wqkv, const void* wqkv_t,
                   const void* wout_t, const float* mz, const float* ctx32, const void* actT, const void* actx,
