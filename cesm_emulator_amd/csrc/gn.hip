@@ -5,16 +5,20 @@
 // contiguous [rows][C] block of the channels-last activation.  Everything after the statistics
 // is folded into per-(sample, channel) affine coefficients computed once per call:
 //   forward   a = y*A1[b,c] + A0[b,c],  out = silu(a) + res
-//   backward  da = dout * silu'(a),  S1 = sum da,  S3 = sum da*y   (per b,c; xhat never stored)
-//             dy = da*E1[b,c] + y*E2[b,c] + E3[b,c]
+//   backward  da = dout * silu'(a),  S1 = sum da,  S3 = sum da*y,  Sy = sum y  (per b,c; xhat never
+//             stored);  dy = da*E1[b,c] + y*E2[b,c] + E3[b,c], so the producing conv's bias gradient
+//             sum dy = E1 S1 + E2 Sy + rows E3 comes out of the reduction without another pass over dy
 // so the streaming kernels keep a thread on one 8-channel group (coefficients in registers)
 // and touch HBM only for the activations.
 #include "common.h"
 
 namespace {
 
-static int gn_nchunk(int64_t rows_b) {
-  int64_t n = rows_b / 2048;
+// row chunks per sample for the reduction kernels: >= ~8 row-iterations per thread, <= 256 chunks
+// (small levels still get ~1000 blocks in total)
+static int gn_nchunk(int64_t rows_b, int C) {
+  const int rl = 256 / (C / 8);
+  int64_t n = rows_b / (rl * 8);
   if (n < 1) n = 1;
   if (n > 256) n = 256;
   return (int)n;
@@ -57,18 +61,20 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const T* __restrict__ y, 
   }
 }
 
-// stats[b][g] = (mean, rstd)
-__global__ void gn_finalize_kernel(const double* __restrict__ part, float* __restrict__ stats, int B, int G,
-                                   int nchunk, double count, float eps) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= B * G) return;
+// stats[b][g] = (mean, rstd); one wave per (b, g)
+__global__ __launch_bounds__(64) void gn_finalize_kernel(const double* __restrict__ part, float* __restrict__ stats,
+                                                         int B, int G, int nchunk, double count, float eps) {
+  const int i = blockIdx.x;
   const int b = i / G, g = i - b * G;
   double a = 0.0, q = 0.0;
-  for (int k = 0; k < nchunk; ++k) {
+  for (int k = threadIdx.x; k < nchunk; k += 64) {
     const double* p = part + (((int64_t)b * nchunk + k) * G + g) * 2;
     a += p[0];
     q += p[1];
   }
+  a = wave_sum_d(a);
+  q = wave_sum_d(q);
+  if (threadIdx.x) return;
   const double mean = a / count;
   double var = q / count - mean * mean;
   if (var < 0) var = 0;
@@ -128,7 +134,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ y, 
   }
 }
 
-// part[b][chunk][c] = (S1 = sum da, S3 = sum da*y)
+// part[b][chunk][c] = (S1 = sum da, S3 = sum da*y, Sy = sum y)
 template <typename T>
 __global__ __launch_bounds__(256) void gn_bwd_reduce_kernel(const T* __restrict__ dout, const T* __restrict__ y,
                                                             const float* __restrict__ coef, float* __restrict__ part,
@@ -143,7 +149,7 @@ __global__ __launch_bounds__(256) void gn_bwd_reduce_kernel(const T* __restrict_
   const int64_t rpc = (rows_b + nchunk - 1) / nchunk;
   const int64_t r0 = chunk * rpc, r1 = min(rows_b, r0 + rpc);
   const int64_t off = (int64_t)b * rows_b * C + c8 * 8;
-  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s3[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sy[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (rr < rl) {
 #pragma unroll 4
     for (int64_t r = r0 + rr; r < r1; r += rl) {
@@ -155,86 +161,130 @@ __global__ __launch_bounds__(256) void gn_bwd_reduce_kernel(const T* __restrict_
         const float da = d[i] * dsilu_t<T>(fmaf(v[i], A1[i], A0[i]));
         s1[i] += da;
         s3[i] = fmaf(da, v[i], s3[i]);
+        sy[i] += v[i];
       }
     }
   }
-  __shared__ float red[256][17];
+  // reduce over the lanes of a wave that share c8 (lane stride cv), then over the row groups in a
+  // fixed order (deterministic)
+  for (int o = cv; o < 64; o <<= 1) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) { red[tid][i] = s1[i]; red[tid][8 + i] = s3[i]; }
-  __syncthreads();
-  if (tid < cv) {
-    float a[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int k = 0; k < rl; ++k)
+    for (int i = 0; i < 8; ++i) {
+      s1[i] += __shfl_xor(s1[i], o, 64);
+      s3[i] += __shfl_xor(s3[i], o, 64);
+      sy[i] += __shfl_xor(sy[i], o, 64);
+    }
+  }
+  __shared__ float red[3][1024];
+  const int lane = tid & 63, wv = tid >> 6;
+  const bool owner = lane < (cv < 64 ? cv : 64);          // holds the wave's sums for c8 = tid % cv
+  const int ngroup = cv <= 64 ? 4 : 256 / cv;              // row groups left per c8
+  const int grp = cv <= 64 ? wv : rr;
+  for (int k = 0; k < ngroup; ++k) {
+    if (owner && grp == k) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) { a[i] += red[k * cv + tid][i]; q[i] += red[k * cv + tid][8 + i]; }
-    float* o = part + (((int64_t)b * nchunk + chunk) * C + tid * 8) * 2;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) { o[i * 2] = a[i]; o[i * 2 + 1] = q[i]; }
+      for (int i = 0; i < 8; ++i) {
+        const int c = c8 * 8 + i;
+        if (k == 0) { red[0][c] = s1[i]; red[1][c] = s3[i]; red[2][c] = sy[i]; }
+        else { red[0][c] += s1[i]; red[1][c] += s3[i]; red[2][c] += sy[i]; }
+      }
+    }
+    __syncthreads();
+  }
+  float* o = part + ((int64_t)b * nchunk + chunk) * C * 3;
+  for (int c = tid; c < C; c += 256) {
+    o[c * 3] = red[0][c];
+    o[c * 3 + 1] = red[1][c];
+    o[c * 3 + 2] = red[2][c];
   }
 }
 
-// per sample b (one block): S1, S2 = rstd*(S3 - mean*S1) -> dss[b] (d scale | d shift), param
-// contributions pb[b][c] = ((1+scale)*S2, (1+scale)*S1), and the apply coefficients
-// E[b][0..2][c]:  dy = da*E1 + y*E2 + E3
+// grid (B, C/64), 256 threads = 64 channels x 4 chunk groups.  Per (b, c): S1, S3, Sy over the chunk
+// partials; S2 = rstd*(S3 - mean*S1) = sum da*xhat -> dss[b] (d scale | d shift), parameter
+// contributions pb[b][c] = ((1+scale)*S2, (1+scale)*S1, conv-bias sum dy), apply coefficients
+// E[b][0..2][c]:  dy = da*E1 + y*E2 + E3.  Groups (C/G <= 64 channels) never straddle blocks.
 __global__ __launch_bounds__(256) void gn_bwd_finalize_kernel(const float* __restrict__ part,
                                                               const float* __restrict__ stats,
                                                               const float* __restrict__ gamma,
                                                               const float* __restrict__ beta,
                                                               const float* __restrict__ ss, float* __restrict__ dss,
                                                               float* __restrict__ pb, float* __restrict__ E, int C,
-                                                              int G, int nchunk, double count) {
+                                                              int G, int nchunk, double count, float rows_b) {
   const int b = blockIdx.x;
-  __shared__ float ga_[1024], gb_[1024];
+  const int cl = threadIdx.x & 63, kg = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + cl;
+  __shared__ float red[4][3][64];
+  __shared__ float ga_[64], gb_[64];
   __shared__ float gA[64], gB[64];
   const int gsz = C / G;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float s1 = 0.f, s3 = 0.f;
-    for (int k = 0; k < nchunk; ++k) {
-      const float* p = part + (((int64_t)b * nchunk + k) * C + c) * 2;
+  float s1 = 0.f, s3 = 0.f, sy = 0.f;
+  if (c < C)
+    for (int k = kg; k < nchunk; k += 4) {
+      const float* p = part + (((int64_t)b * nchunk + k) * C + c) * 3;
       s1 += p[0];
       s3 += p[1];
+      sy += p[2];
     }
+  red[kg][0][cl] = s1;
+  red[kg][1][cl] = s3;
+  red[kg][2][cl] = sy;
+  __syncthreads();
+  float mean = 0.f, rstd = 0.f, sc = 1.f;
+  if (kg == 0 && c < C) {
+    s1 = ((red[0][0][cl] + red[1][0][cl]) + red[2][0][cl]) + red[3][0][cl];
+    s3 = ((red[0][1][cl] + red[1][1][cl]) + red[2][1][cl]) + red[3][1][cl];
+    sy = ((red[0][2][cl] + red[1][2][cl]) + red[2][2][cl]) + red[3][2][cl];
     const int g = c / gsz;
-    const float mean = stats[(b * G + g) * 2], rstd = stats[(b * G + g) * 2 + 1];
+    mean = stats[(b * G + g) * 2];
+    rstd = stats[(b * G + g) * 2 + 1];
     const float s2 = rstd * (s3 - mean * s1);  // sum da * xhat
-    const float sc = ss ? ss[(int64_t)b * 2 * C + c] + 1.f : 1.f;
+    sc = ss ? ss[(int64_t)b * 2 * C + c] + 1.f : 1.f;
     if (dss) {
       dss[(int64_t)b * 2 * C + c] = gamma[c] * s2 + beta[c] * s1;  // d scale
       dss[(int64_t)b * 2 * C + C + c] = s1;                        // d shift
     }
-    pb[((int64_t)b * C + c) * 2] = sc * s2;      // dgamma contribution
-    pb[((int64_t)b * C + c) * 2 + 1] = sc * s1;  // dbeta contribution
-    ga_[c] = gamma[c] * sc * s1;
-    gb_[c] = gamma[c] * sc * s2;
+    pb[((int64_t)b * C + c) * 3] = sc * s2;      // dgamma contribution
+    pb[((int64_t)b * C + c) * 3 + 1] = sc * s1;  // dbeta contribution
+    ga_[cl] = gamma[c] * sc * s1;
+    gb_[cl] = gamma[c] * sc * s2;
   }
   __syncthreads();
-  if ((int)threadIdx.x < G) {
+  const int ng = 64 / gsz;  // groups in this block (gsz <= 64)
+  if ((int)threadIdx.x < ng && blockIdx.y * 64 + threadIdx.x * gsz < C) {
     double a = 0.0, q = 0.0;
-    for (int c = threadIdx.x * gsz; c < (int)(threadIdx.x + 1) * gsz; ++c) { a += ga_[c]; q += gb_[c]; }
+    for (int j = threadIdx.x * gsz; j < (int)(threadIdx.x + 1) * gsz; ++j) { a += ga_[j]; q += gb_[j]; }
     gA[threadIdx.x] = (float)(a / count);
     gB[threadIdx.x] = (float)(q / count);
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    const int g = c / gsz;
-    const float mean = stats[(b * G + g) * 2], rstd = stats[(b * G + g) * 2 + 1];
-    const float sc = ss ? ss[(int64_t)b * 2 * C + c] + 1.f : 1.f;
+  if (kg == 0 && c < C) {
+    const int gl = cl / gsz;
     // dy = rstd*(da*sc*gamma - A - (y-mean)*rstd*Bg)
-    E[((int64_t)b * 3) * C + c] = rstd * sc * gamma[c];
-    E[((int64_t)b * 3 + 1) * C + c] = -rstd * rstd * gB[g];
-    E[((int64_t)b * 3 + 2) * C + c] = rstd * (mean * rstd * gB[g] - gA[g]);
+    const float e1 = rstd * sc * gamma[c];
+    const float e2 = -rstd * rstd * gB[gl];
+    const float e3 = rstd * (mean * rstd * gB[gl] - gA[gl]);
+    E[((int64_t)b * 3) * C + c] = e1;
+    E[((int64_t)b * 3 + 1) * C + c] = e2;
+    E[((int64_t)b * 3 + 2) * C + c] = e3;
+    pb[((int64_t)b * C + c) * 3 + 2] = e1 * s1 + e2 * sy + rows_b * e3;  // sum over rows of dy
   }
 }
 
-// dgamma/dbeta (+)= sum_b pb[b]
+// dgamma/dbeta/dbias (+)= sum_b pb[b]
 __global__ void gn_param_grad_kernel(const float* __restrict__ pb, float* __restrict__ dgamma,
-                                     float* __restrict__ dbeta, int B, int C, int accumulate) {
+                                     float* __restrict__ dbeta, float* __restrict__ dbias, int B, int C,
+                                     int accumulate) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  float a = 0.f, q = 0.f;
-  for (int b = 0; b < B; ++b) { a += pb[((int64_t)b * C + c) * 2]; q += pb[((int64_t)b * C + c) * 2 + 1]; }
+  float a = 0.f, q = 0.f, w = 0.f;
+  for (int b = 0; b < B; ++b) {
+    a += pb[((int64_t)b * C + c) * 3];
+    q += pb[((int64_t)b * C + c) * 3 + 1];
+    w += pb[((int64_t)b * C + c) * 3 + 2];
+  }
   if (dgamma) dgamma[c] = accumulate ? dgamma[c] + a : a;
   if (dbeta) dbeta[c] = accumulate ? dbeta[c] + q : q;
+  if (dbias) dbias[c] = accumulate ? dbias[c] + w : w;
 }
 
 template <typename T>
@@ -292,15 +342,14 @@ extern "C" {
 int cesm_gn_stats(int dtype, const void* y, float* stats, double* ws, int B, int64_t rows_b, int C, int G, float eps,
                   hipStream_t stream) {
   if (C % 8 || C / 8 > 256 || C % G || (C / G) % 8) return CESM_EINVAL;
-  const int nchunk = gn_nchunk(rows_b);
+  const int nchunk = gn_nchunk(rows_b, C);
   dim3 grid(nchunk, B);
   int rc = dispatch_dt(dtype, [&](auto* tp) {
     using T = std::remove_pointer_t<decltype(tp)>;
     gn_stats_kernel<T><<<grid, 256, 0, stream>>>((const T*)y, ws, rows_b, C, G, nchunk);
   });
   if (rc) return rc;
-  gn_finalize_kernel<<<(unsigned)cdiv(B * G, 64), 64, 0, stream>>>(ws, stats, B, G, nchunk,
-                                                                   (double)rows_b * (C / G), eps);
+  gn_finalize_kernel<<<B * G, 64, 0, stream>>>(ws, stats, B, G, nchunk, (double)rows_b * (C / G), eps);
   return cesm_launch_status();
 }
 
@@ -320,15 +369,16 @@ int cesm_gn_apply(int dtype, const void* y, const float* stats, const float* gam
 }
 
 // Backward of out = silu(GN(y)*(1+scale)+shift) (+res).  Writes dy, dss [B][2C] (if non-null),
-// dgamma/dbeta (accumulate flag).  ws: float workspace >= B*256*C*2 + B*C*2 + B*C*5 floats.
+// dgamma/dbeta and the producing conv's bias gradient dbias = sum dy (each nullable; accumulate flag).
+// ws: float workspace >= B*256*C*3 + B*C*3 + B*C*5 floats.
 int cesm_gn_bwd(int dtype, const void* dout, const void* y, const float* stats, const float* gamma,
-                const float* beta, const float* ss, void* dy, float* dss, float* dgamma, float* dbeta, float* ws,
-                int B, int64_t rows_b, int C, int G, int accumulate, hipStream_t stream) {
-  if (C % 8 || C / 8 > 256 || C % G || C > 1024 || G > 64) return CESM_EINVAL;
-  const int nchunk = gn_nchunk(rows_b);
+                const float* beta, const float* ss, void* dy, float* dss, float* dgamma, float* dbeta, float* dbias,
+                float* ws, int B, int64_t rows_b, int C, int G, int accumulate, hipStream_t stream) {
+  if (C % 8 || C / 8 > 128 || C % G || C / G > 64 || 64 % (C / G) || G > 64) return CESM_EINVAL;
+  const int nchunk = gn_nchunk(rows_b, C);
   float* part = ws;
-  float* pb = part + (int64_t)B * nchunk * C * 2;
-  float* coef = pb + (int64_t)B * C * 2;
+  float* pb = part + (int64_t)B * nchunk * C * 3;
+  float* coef = pb + (int64_t)B * C * 3;
   float* E = coef + (int64_t)B * C * 2;
   const double count = (double)rows_b * (C / G);
   gn_coef_kernel<<<(unsigned)cdiv(B * C, 256), 256, 0, stream>>>(stats, gamma, beta, ss, coef, B, C, G);
@@ -337,12 +387,13 @@ int cesm_gn_bwd(int dtype, const void* dout, const void* y, const float* stats, 
     using T = std::remove_pointer_t<decltype(tp)>;
     gn_bwd_reduce_kernel<T><<<dim3(nchunk, B), 256, 0, stream>>>((const T*)dout, (const T*)y, coef, part, rows_b, C,
                                                                  nchunk);
-    gn_bwd_finalize_kernel<<<B, 256, 0, stream>>>(part, stats, gamma, beta, ss, dss, pb, E, C, G, nchunk, count);
+    gn_bwd_finalize_kernel<<<dim3(B, (unsigned)cdiv(C, 64)), 256, 0, stream>>>(part, stats, gamma, beta, ss, dss, pb,
+                                                                               E, C, G, nchunk, count, (float)rows_b);
     gn_bwd_apply_kernel<T><<<dim3(nch, B), 256, 0, stream>>>((const T*)dout, (const T*)y, coef, E, (T*)dy, rows_b, C,
                                                              nch);
   });
   if (rc) return rc;
-  gn_param_grad_kernel<<<(unsigned)cdiv(C, 256), 256, 0, stream>>>(pb, dgamma, dbeta, B, C, accumulate);
+  gn_param_grad_kernel<<<(unsigned)cdiv(C, 256), 256, 0, stream>>>(pb, dgamma, dbeta, dbias, B, C, accumulate);
   return cesm_launch_status();
 }
 

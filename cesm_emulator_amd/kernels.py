@@ -179,14 +179,15 @@ def gn_apply(y, stats, gamma, beta, ss, res, B, G):
     return out
 
 
-def gn_bwd(dout, y, stats, gamma, beta, ss, dgamma, dbeta, B, G, want_dss):
+def gn_bwd(dout, y, stats, gamma, beta, ss, dgamma, dbeta, B, G, want_dss, dbias=None):
+    """GroupNorm(+scale/shift, SiLU) backward; dbias (+)= sum of dy over rows (the producing conv's bias)"""
     C = y.shape[-1]
     rows_b = y.numel() // (C * B)
     dy = empty(y.shape, y.dtype, y.device)
     dss = empty((B, 2 * C), torch.float32, y.device) if want_dss else None
-    ws = empty((B * 256 * C * 2 + B * C * 2 + B * C * 5,), torch.float32, y.device)
+    ws = empty((B * 256 * C * 3 + B * C * 3 + B * C * 5,), torch.float32, y.device)
     call("cesm_gn_bwd", dtcode(y), P(dout), P(y), P(stats), P(gamma), P(beta), P(ss), P(dy), P(dss), P(dgamma),
-         P(dbeta), P(ws), B, rows_b, C, G, 1, S())
+         P(dbeta), P(dbias), P(ws), B, rows_b, C, G, 1, S())
     return dy, dss
 
 

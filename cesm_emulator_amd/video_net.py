@@ -96,14 +96,15 @@ def conv_forward(rc, spec, x1, x2=None, res=None):
     return y, st
 
 
-def conv_backward(rc, spec, st, dy, need_dx=True, dres1=None, dres2=None):
-    """Param grads of the conv + (optionally) dX (split for concat inputs) + fused residual grads."""
+def conv_backward(rc, spec, st, dy, need_dx=True, dres1=None, dres2=None, bias_done=False):
+    """Param grads of the conv + (optionally) dX (split for concat inputs) + fused residual grads.
+    bias_done: the bias gradient was already produced (by the GroupNorm backward's reduction)."""
     w, b = spec.mod.weight, spec.mod.bias
     dw = gbuf(w)
     if dw is not None:
         K.conv_wgrad(st.x1, st.x2, dy, None, dw, st.geom, st.swap, st.flip)
     db = gbuf(b)
-    if db is not None:
+    if db is not None and not bias_done:
         K.colsum(dy, db)
     if not need_dx:
         return None
@@ -237,8 +238,8 @@ def block_fwd(rc, blk, x1, x2, ss, res):
 def block_bwd(rc, blk, st, dout, want_dss, dres1=None, dres2=None):
     G = blk.norm.num_groups
     dy, dss = K.gn_bwd(dout, st.y, st.stats, blk.norm.weight, blk.norm.bias, st.ss, gbuf(blk.norm.weight),
-                       gbuf(blk.norm.bias), rc.B, G, want_dss)
-    dx = conv_backward(rc, st.spec, st.cst, dy, True, dres1, dres2)
+                       gbuf(blk.norm.bias), rc.B, G, want_dss, dbias=gbuf(blk.proj.bias))
+    dx = conv_backward(rc, st.spec, st.cst, dy, True, dres1, dres2, bias_done=True)
     return dx, dss
 
 

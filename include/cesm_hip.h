@@ -68,9 +68,11 @@ int cesm_gn_stats(int dtype, const void* y, float* stats, double* ws, int B, int
 int cesm_gn_apply(int dtype, const void* y, const float* stats, const float* gamma, const float* beta,
                   const float* ss, const void* res, void* out, float* ws, int B, int64_t rows_b, int C, int G,
                   hipStream_t stream);
+/* backward; also writes the producing conv's bias gradient dbias (+)= sum dy (nullable) without another
+ * pass over dy.  ws >= B*256*C*3 + B*C*3 + B*C*5 floats. */
 int cesm_gn_bwd(int dtype, const void* dout, const void* y, const float* stats, const float* gamma,
-                const float* beta, const float* ss, void* dy, float* dss, float* dgamma, float* dbeta, float* ws,
-                int B, int64_t rows_b, int C, int G, int accumulate, hipStream_t stream);
+                const float* beta, const float* ss, void* dy, float* dss, float* dgamma, float* dbeta, float* dbias,
+                float* ws, int B, int64_t rows_b, int C, int G, int accumulate, hipStream_t stream);
 /* channel LayerNorm (biased var, gamma only): video_net.py:78-87 */
 int cesm_ln_fwd(int dtype, const void* x, const float* gamma, void* out, float* mr, int64_t V, int C, float eps,
                 hipStream_t stream);

@@ -137,10 +137,12 @@ def test_conv_concat_split_and_residual(dev, cdt):
 
 @pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("with_ss", [True, False])
-def test_block_groupnorm(dev, cdt, with_ss):
-    """Block: conv -> GroupNorm(8) -> x*(scale+1)+shift -> SiLU (+residual), fwd and bwd"""
+@pytest.mark.parametrize("cout", [128, 512])
+def test_block_groupnorm(dev, cdt, with_ss, cout):
+    """Block: conv -> GroupNorm(8) -> x*(scale+1)+shift -> SiLU (+residual), fwd and bwd (incl. the conv
+    bias gradient produced by the GroupNorm backward's reduction)"""
     torch.manual_seed(2)
-    B, Fr, H, W, cin, cout = 2, 3, 8, 12, 64, 128
+    B, Fr, H, W, cin = 2, 3, 8, 12, 64
     blk = VN.Block(cin, cout).to(dev)
     with torch.no_grad():
         blk.norm.weight.uniform_(0.5, 1.5)
@@ -172,6 +174,8 @@ def test_block_groupnorm(dev, cdt, with_ss):
     tol = TOL[cdt] * (5 if cdt == torch.bfloat16 else 10)
     assert rel(blk.norm.weight.grad, gam.grad) < tol
     assert rel(blk.norm.bias.grad, bet.grad) < tol
+    ref_db = bconv.grad if cdt == torch.float32 else y.grad.sum((0, 2, 3, 4))
+    assert rel(blk.proj.bias.grad, ref_db) < tol
     if ssr is not None:
         assert rel(dss, ssr.grad) < tol
     if cdt == torch.float32:
