@@ -23,6 +23,18 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 
 #define LDS_PTR(T) __attribute__((address_space(3))) T*
 
+// compute units of the current device (cached; 256 on MI355X)
+static inline int cesm_num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
 static inline int cesm_launch_status() {
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? CESM_OK : CESM_ELAUNCH;

@@ -232,9 +232,8 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const T* __restrict__ x1,
 // halo (9x fewer input loads than im2col).  The next chunk is prefetched into registers while the
 // current one is consumed.  4 waves = 2 (co halves) x 2 (pixel halves of 4 rows).
 // ----------------------------------------------------------------------------------------
-constexpr int H3_TH = 8, H3_TW = 32;
-constexpr int H3_HH = H3_TH + 2, H3_HW = H3_TW + 2;
-constexpr int H3_NPIX = H3_HH * H3_HW;   // 340 halo pixels
+constexpr int H3_TH = 8, H3_TW = 32;     // default tile (TH x TW is chosen per level, see c2_tile)
+constexpr int H3_NPIX = 384;             // max halo pixels (TH+2)(TW+2)
 constexpr int H3_LD = 40;                // bf16 per LDS row (32 ch + 8 pad = 80 B)
 constexpr int H3_BN = 64;
 constexpr int H3_HVEC = H3_NPIX * 4;     // 16-B vectors in the halo tile
@@ -242,18 +241,21 @@ constexpr int H3_WVEC = 9 * H3_BN * 4;   // 16-B vectors in the weight tile
 constexpr int H3_HPT = (H3_HVEC + 255) / 256;
 constexpr int H3_WPT = H3_WVEC / 256;
 
+template <int TW>
 __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
                                                               const bf16* __restrict__ w, const float* __restrict__ bias,
                                                               const bf16* __restrict__ res, const bf16* __restrict__ res2,
                                                               bf16* __restrict__ y1, bf16* __restrict__ y2, ConvGeom g,
-                                                              int tiles_x) {
+                                                              int tiles_x, int TH) {
   __shared__ __attribute__((aligned(16))) bf16 sh[H3_NPIX * H3_LD];
   __shared__ __attribute__((aligned(16))) bf16 sw[9 * H3_BN * H3_LD];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
   const int n = blockIdx.y;
   const int ty = blockIdx.x / tiles_x, tx = blockIdx.x - ty * tiles_x;
-  const int y0 = ty * H3_TH, x0 = tx * H3_TW;
+  const int y0 = ty * TH, x0 = tx * TW;
+  constexpr int HWd = TW + 2;
+  const int HP = (TH + 2) * HWd;
   const int n0 = blockIdx.z * H3_BN;
   const int Cin = g.C1 + g.C2;
   const int nchunk = Cin / 32;
@@ -270,9 +272,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
     for (int k = 0; k < H3_HPT; ++k) {
       const int e = tid + k * 256;
       bf16x8 v = {};
-      if (e < H3_HVEC) {
+      if (e < HP * 4) {
         const int hp = e >> 2, part = e & 3;
-        const int r = hp / H3_HW, c = hp - r * H3_HW;
+        const int r = hp / HWd, c = hp - r * HWd;
         const int iy = y0 - 1 + r, ix = x0 - 1 + c;
         if ((unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi)
           v = *reinterpret_cast<const bf16x8*>(src + (((int64_t)n * g.Hi + iy) * g.Wi + ix) * cs + cc + part * 8);
@@ -289,7 +291,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
 #pragma unroll
     for (int k = 0; k < H3_HPT; ++k) {
       const int e = tid + k * 256;
-      if (e < H3_HVEC) *reinterpret_cast<bf16x8*>(sh + (e >> 2) * H3_LD + (e & 3) * 8) = hreg[k];
+      if (e < HP * 4) *reinterpret_cast<bf16x8*>(sh + (e >> 2) * H3_LD + (e & 3) * 8) = hreg[k];
     }
 #pragma unroll
     for (int k = 0; k < H3_WPT; ++k) {
@@ -305,6 +307,24 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int lr = lane & 15, lg = lane >> 4;
+  // pixel group j of this wave: tile pixel p = wc*128 + j*16 + lr -> halo row of tap (0,0)
+  int hoff[8], pyx[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    int py, px;
+    if constexpr (TW == 32) {  // rows of two 16-pixel groups: compile-time offsets per j
+      py = wc * 4 + (j >> 1);
+      px = (j & 1) * 16 + lr;
+    } else {
+      const int p = wc * 128 + j * 16 + lr;
+      py = p / TW;
+      px = p - py * TW;
+    }
+    const bool in = py < TH;
+    // TW == 32: rows past TH stay inside the LDS halo buffer (results discarded), no select needed
+    hoff[j] = (TW == 32 || in) ? py * HWd + px : 0;
+    pyx[j] = in ? (py << 16) | px : -1;
+  }
   for (int ch = 0; ch < nchunk; ++ch) {
     if (ch) __syncthreads();  // previous chunk fully consumed
     stage(ch);
@@ -318,9 +338,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
         af[i] = *reinterpret_cast<const bf16x8*>(sw + (tap * H3_BN + wr * 32 + i * 16 + lr) * H3_LD + lg * 8);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int py = wc * 4 + (j >> 1), px = (j & 1) * 16 + lr;
-        const bf16x8 bfr =
-            *reinterpret_cast<const bf16x8*>(sh + ((py + ky) * H3_HW + px + kx) * H3_LD + lg * 8);
+        const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(sh + (hoff[j] + ky * HWd + kx) * H3_LD + lg * 8);
         acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bfr, acc[0][j], 0, 0, 0);
         acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bfr, acc[1][j], 0, 0, 0);
       }
@@ -330,7 +348,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
   const int Co2 = g.Cout - g.Co1;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const int oy = y0 + wc * 4 + (j >> 1), ox = x0 + (j & 1) * 16 + lr;
+    if (pyx[j] < 0) continue;
+    const int oy = y0 + (pyx[j] >> 16), ox = x0 + (pyx[j] & 0xffff);
     if (oy >= g.Ho || ox >= g.Wo) continue;
     const int64_t m = ((int64_t)n * g.Ho + oy) * g.Wo + ox;
 #pragma unroll
@@ -358,6 +377,200 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
         }
         store4(y2 + m * Co2 + (co - g.Co1), v);
       }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// 3x3 / stride 1 / pad 1 conv (bf16), v2: persistent, software-pipelined halo conv.
+// Work item = (TH x TW pixel tile of one image, 64 output channels); a block streams the
+// (item, 32-channel chunk) sequence through two LDS stages filled by global_load_lds (LDS-DMA, no
+// VGPR staging): the loads of step s+2 are issued as soon as step s's stage is released and stay in
+// flight across the raw barriers (counted s_waitcnt vmcnt).  Stage = halo [(TH+2)(TW+2) <= 384 px]
+// [32 ch] + weights [9 taps x 64 co][32 ci], 64-B rows with the 16-B chunk index XORed by
+// (row >> 2) & 3 (conflict-free fragment reads).  Generic TW lets W = 36 / 72 / 144 levels use
+// 36-wide tiles instead of wasting 25-44 % of a 32-wide tiling.  4 waves = 2 (co halves) x 2
+// (pixel halves); wave tile 32 co x 128 px, 16 MFMA per tap.
+// ----------------------------------------------------------------------------------------
+constexpr int C2_HROWS = 384;                 // halo rows per stage (>= (TH+2)(TW+2))
+constexpr int C2_HALO_B = C2_HROWS * 64;      // 24 KiB
+constexpr int C2_W_B = 9 * 64 * 64;           // 36 KiB
+constexpr int C2_STAGE_B = C2_HALO_B + C2_W_B;
+constexpr int C2_NI = C2_HROWS / 16 + 9 * 64 / 16;  // wave-instructions per stage (60)
+constexpr int C2_NPW = C2_NI / 4;                   // per wave (15)
+static_assert(C2_NI % 4 == 0, "glds instructions must split evenly over the 4 waves");
+__device__ __attribute__((aligned(16))) bf16 c2_zero_page[8] = {};
+
+__device__ __forceinline__ int c2_swz(int row) { return (row >> 2) & 3; }
+
+__global__ __launch_bounds__(256, 1) void conv3x3v2_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
+                                                           const bf16* __restrict__ w, const float* __restrict__ bias,
+                                                           const bf16* __restrict__ res, const bf16* __restrict__ res2,
+                                                           bf16* __restrict__ y1, bf16* __restrict__ y2, ConvGeom g,
+                                                           int TH, int TW, int tiles_x, int tiles_y, int ncob,
+                                                           int nitems) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * C2_STAGE_B];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int Cin = g.C1 + g.C2;
+  const int nchunk = Cin / 32;
+  const int HWd = TW + 2, HP = (TH + 2) * HWd;
+  const int per_img = tiles_x * tiles_y;
+  // this block's items: contiguous range (neighbouring tiles share halo rows and weights in L2)
+  const int ipb = (nitems + gridDim.x - 1) / gridDim.x;
+  const int it0 = blockIdx.x * ipb, it1 = min(nitems, it0 + ipb);
+  const int nsteps = (it1 > it0 ? it1 - it0 : 0) * nchunk;
+
+  // per-lane pixel offsets of the 8 B-fragment groups (independent of the item)
+  int hoff[8];
+  int pyx[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int p = wc * 128 + j * 16 + lr;
+    const int py = p / TW, px = p - (p / TW) * TW;
+    const bool in = p < TH * TW;
+    hoff[j] = in ? py * HWd + px : 0;
+    pyx[j] = in ? (py << 16) | px : -1;
+  }
+
+  auto item_geo = [&](int it, int& n, int& y0, int& x0, int& n0) {
+    const int cob = it % ncob, t = it / ncob;
+    n = t / per_img;
+    const int r = t - n * per_img;
+    y0 = (r / tiles_x) * TH;
+    x0 = (r % tiles_x) * TW;
+    n0 = cob * 64;
+  };
+  auto issue = [&](int s) {  // glds for step s into stage s & 1
+    const int it = it0 + s / nchunk, ch = s % nchunk;
+    int n, y0, x0, n0;
+    item_geo(it, n, y0, x0, n0);
+    const int c0 = ch * 32;
+    const bf16* src;
+    int cs, cc;
+    if (c0 < g.C1) { src = x1; cs = g.C1; cc = c0; } else { src = x2; cs = g.C2; cc = c0 - g.C1; }
+    char* base = lds + (s & 1) * C2_STAGE_B;
+#pragma unroll
+    for (int k = 0; k < C2_NPW; ++k) {
+      const int i = k * 4 + wid;
+      const int rsub = lane >> 2, slot = lane & 3;
+      const bf16* gp;
+      if (i < C2_HROWS / 16) {
+        const int row = i * 16 + rsub;
+        const int chunk = slot ^ c2_swz(row);
+        gp = c2_zero_page;
+        if (row < HP) {
+          const int hy = row / HWd, hx = row - (row / HWd) * HWd;
+          const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
+          if ((unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi)
+            gp = src + (((int64_t)n * g.Hi + iy) * g.Wi + ix) * cs + cc + chunk * 8;
+        }
+      } else {
+        const int row = (i - C2_HROWS / 16) * 16 + rsub;  // tap*64 + co
+        const int chunk = slot ^ c2_swz(row);
+        const int tap = row >> 6, co = row & 63;
+        gp = w + ((int64_t)(n0 + co) * 9 + tap) * Cin + c0 + chunk * 8;
+      }
+      __builtin_amdgcn_global_load_lds((const void*)gp, (__attribute__((address_space(3))) void*)(base + i * 1024), 16,
+                                       0, 0);
+    }
+  };
+
+  f32x4 acc[2][8];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nsteps > 0) issue(0);
+  if (nsteps > 1) issue(1);
+  for (int s = 0; s < nsteps; ++s) {
+    if (s + 1 < nsteps) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");  // step s landed, s+1 in flight
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const char* hb = lds + (s & 1) * C2_STAGE_B;
+    const char* wb = hb + C2_HALO_B;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int ky = tap / 3, kx = tap - ky * 3;
+      bf16x8 af[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = tap * 64 + wr * 32 + i * 16 + lr;
+        af[i] = *reinterpret_cast<const bf16x8*>(wb + row * 64 + ((lg ^ c2_swz(row)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int row = hoff[j] + ky * HWd + kx;
+        const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(hb + row * 64 + ((lg ^ c2_swz(row)) << 4));
+        acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bfr, acc[0][j], 0, 0, 0);
+        acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bfr, acc[1][j], 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // stage (s & 1) released
+    if (s + 2 < nsteps) issue(s + 2);
+    if ((s % nchunk) == nchunk - 1) {
+      // epilogue of the item: lane holds co = n0 + wr*32 + i*16 + 4*lg + r of pixel group j
+      int n, y0, x0, n0;
+      item_geo(it0 + s / nchunk, n, y0, x0, n0);
+      const int Co2 = g.Cout - g.Co1;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (pyx[j] < 0) continue;
+        const int oy = y0 + (pyx[j] >> 16), ox = x0 + (pyx[j] & 0xffff);
+        if (oy < g.Ho && ox < g.Wo) {
+          const int64_t m = ((int64_t)n * g.Ho + oy) * g.Wo + ox;
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const int co = n0 + wr * 32 + i * 16 + lg * 4;
+            float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+            if (bias) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] += bias[co + r];
+            }
+            if (co < g.Co1) {
+              if (res) {
+                float rv[4];
+                load4(res + m * g.Co1 + co, rv);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] += rv[r];
+              }
+              store4(y1 + m * g.Co1 + co, v);
+            } else {
+              if (res2) {
+                float rv[4];
+                load4(res2 + m * Co2 + (co - g.Co1), rv);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] += rv[r];
+              }
+              store4(y2 + m * Co2 + (co - g.Co1), v);
+            }
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  }
+}
+
+// tile shape for an Ho x Wo image: TW in {32, 36, 48}, TH*TW <= 256, (TH+2)(TW+2) <= 384; maximise
+// useful / computed pixels (fewest tiles on ties)
+static void c2_tile(int Ho, int Wo, int& TH, int& TW, bool only_32_36 = false) {
+  double best = -1.0;
+  int bt = 1 << 30;
+  const int cands[3] = {32, 36, 48};
+  for (int c = 0; c < (only_32_36 ? 2 : 3); ++c) {
+    const int tw = cands[c];
+    for (int th = 1; th * tw <= 256; ++th) {
+      if ((th + 2) * (tw + 2) > C2_HROWS) break;
+      const int ntile = (int)(cdiv(Ho, th) * cdiv(Wo, tw));
+      const double util = (double)Ho * Wo / ((double)ntile * 256);
+      // a non-32 width must buy > 10 % utilisation (32-wide tiles align with the fragment rows)
+      const double u = tw == 32 ? util + 0.10 : util;
+      if (u > best + 1e-9 || (u > best - 1e-9 && ntile < bt)) { best = u; bt = ntile; TH = th; TW = tw; }
     }
   }
 }
@@ -1242,11 +1455,29 @@ int cesm_conv_fwd(int dtype, const void* x1, const void* x2, const void* wp, con
   dim3 grid(Cout / BN, (unsigned)cdiv(M, BMP));
   const bool halo3 = dtype == CESM_DT_BF16 && KH == 3 && KW == 3 && S == 1 && P == 1 && U == 1 && Ho == Hi &&
                      Wo == Wi && (Co1 % H3_BN) == 0 && !getenv_flag("CESM_NO_HALO");
-  if (halo3) {
-    const int tx = (int)cdiv(Wo, H3_TW), ty = (int)cdiv(Ho, H3_TH);
+  if (halo3 && getenv_flag("CESM_CONV3X3_V2")) {
+    int TH = 8, TW = 32;
+    c2_tile(Ho, Wo, TH, TW);
+    const int tx = (int)cdiv(Wo, TW), ty = (int)cdiv(Ho, TH);
+    const int ncob = Cout / 64;
+    const int nitems = Nb * tx * ty * ncob;
+    const int nblk = std::min(nitems, cesm_num_cus());
+    conv3x3v2_kernel<<<nblk, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
+                                               (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, TH, TW,
+                                               tx, ty, ncob, nitems);
+  } else if (halo3) {
+    int TH = H3_TH, TW = H3_TW;
+    if (!getenv_flag("CESM_CONV3X3_FIXED_TILE")) c2_tile(Ho, Wo, TH, TW, true);
+    const int tx = (int)cdiv(Wo, TW), ty = (int)cdiv(Ho, TH);
     dim3 g3(tx * ty, Nb, Cout / H3_BN);
-    conv3x3_bf16_kernel<<<g3, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
-                                                (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, tx);
+    if (TW == 36)
+      conv3x3_bf16_kernel<36><<<g3, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
+                                                      (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, tx,
+                                                      TH);
+    else
+      conv3x3_bf16_kernel<32><<<g3, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
+                                                      (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, tx,
+                                                      TH);
   } else if (dtype == CESM_DT_BF16) {
     if (BN == 128)
       conv_fwd_kernel<bf16, 128><<<grid, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,

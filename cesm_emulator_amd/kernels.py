@@ -7,6 +7,8 @@ instead of faulting on the GPU.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ._lib import call, lib
@@ -73,7 +75,13 @@ def conv_fwd(x1, x2, wp, bias, geom, res=None, res2=None, out_split=None):
     _chk(res2, (Nb, Ho, Wo, Cout - Co1), x1.dtype)
     call("cesm_conv_fwd", dtcode(x1), P(x1), P(x2), P(wp), P(bias), P(res), P(res2), P(y1), P(y2), Nb, Hi, Wi, C1,
          C2, Ho, Wo, Cout, Co1, KH, KW, St, Pd, U, S())
+    if CONV_TRACE is not None:
+        CONV_TRACE.append(("fwd", Nb, Hi, Wi, C1 + C2, Ho, Wo, Cout, KH, KW, St, Pd, U))
     return y1 if y2 is None else (y1, y2)
+
+
+# shape log of conv launches (set CESM_TRACE_CONV=1; tools/conv_shapes.py prints it)
+CONV_TRACE = [] if os.environ.get("CESM_TRACE_CONV") else None
 
 
 def _wgrad_nsplit(M, cout, K, bm=64):
@@ -107,6 +115,8 @@ def conv_wgrad(x1, x2, dy1, dy2, dw, geom, swap, flip, accumulate=True):
     halo3 = KH == 3 and KW == 3 and St == 1 and Pd == 1 and U == 1  # wgrad3x3 kernel: 64-row tiles
     nsplit = _wgrad_nsplit(M, Cout, K, 64 if halo3 else _wgrad_bm(x1, Cout, Co1))
     slab = empty((nsplit, Cout, K), torch.float32, x1.device)
+    if CONV_TRACE is not None:
+        CONV_TRACE.append(("wgrad", Nb, Hi, Wi, C1 + C2, Ho, Wo, Cout, KH, KW, St, Pd, U))
     call("cesm_conv_wgrad", dtcode(x1), P(x1), P(x2), P(dy1), P(dy2), P(dw), P(slab), nsplit, Nb, Hi, Wi, C1, C2,
          Ho, Wo, Cout, Co1, KH, KW, St, Pd, U, int(swap), int(flip), int(accumulate), S())
 
