@@ -112,8 +112,12 @@ def conv_wgrad(x1, x2, dy1, dy2, dw, geom, swap, flip, accumulate=True):
     _chk(dw, dtype=torch.float32)
     K = KH * KW * (C1 + C2)
     M = Nb * Ho * Wo
-    halo3 = KH == 3 and KW == 3 and St == 1 and Pd == 1 and U == 1  # wgrad3x3 kernel: 64-row tiles
-    nsplit = _wgrad_nsplit(M, Cout, K, 64 if halo3 else _wgrad_bm(x1, Cout, Co1))
+    halo3 = KH == 3 and KW == 3 and St == 1 and Pd == 1 and U == 1
+    if halo3 and x1.dtype == torch.bfloat16:
+        # wgrad3x3 kernel: blocks of 64 co x 32 ci (all 9 taps), split over pixel tiles
+        nsplit = max(1, min(2048 // max(1, (Cout // 64) * ((C1 + C2) // 32)), max(1, M // 256)))
+    else:
+        nsplit = _wgrad_nsplit(M, Cout, K, _wgrad_bm(x1, Cout, Co1))
     slab = empty((nsplit, Cout, K), torch.float32, x1.device)
     if CONV_TRACE is not None:
         CONV_TRACE.append(("wgrad", Nb, Hi, Wi, C1 + C2, Ho, Wo, Cout, KH, KW, St, Pd, U))
