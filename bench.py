@@ -88,6 +88,17 @@ class KernelProbe:
         return avg_ms, avg_flops, len(ms)
 
 
+def pmc_traffic():
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
+    (tools/gpu_round.sh step 4 -> tools/traffic.py; FETCH_SIZE/WRITE_SIZE calibrated on a known copy)."""
+    f = os.path.join(ROOT, "profiles", "r1_conv3x3_traffic.json")
+    if not os.path.exists(f):
+        return None, None
+    with open(f) as fh:
+        d = json.load(fh)
+    return d["traffic_bytes_per_launch"], d["algorithmic_bytes_per_launch"]
+
+
 def cpu_baseline(cfg_unet, F, H, W, crop):
     """Oracle fp32 train step (B=1) on the host cores, on a 1/crop spatial sample."""
     from oracle import ref_cpu as R
@@ -189,8 +200,12 @@ def main():
     if ps is not None:
         avg_ms, avg_flops, n = ps
         ach = avg_flops / (avg_ms * 1e-3) / 1e12
+        traffic, alg_bytes = pmc_traffic() if a.dtype == "bf16" else (None, None)
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(ach / peak, 4), "traffic": None,
+                "frac": round(ach / peak, 4), "traffic": traffic,
+                "traffic_note": None if traffic is None else
+                f"HBM bytes/launch (PMC FETCH_SIZE+WRITE_SIZE, profiles/r1_conv3x3_traffic.json) vs "
+                f"{alg_bytes:.3g} algorithmic (input read + output write)",
                 "kernel": "conv3x3_bf16_kernel (level-0 3x3 conv 64->64, fwd+dgrad)" if a.dtype == "bf16" else
                           "conv_fwd_kernel<float,64>", "launches": n, "avg_us": round(avg_ms * 1e3, 2),
                 "flop_per_launch": avg_flops}

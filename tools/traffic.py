@@ -1,0 +1,51 @@
+"""HBM bytes per launch of the dominant kernel from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE)
+over tools/conv_micro.py.
+
+Calibration (MI355X_MICROARCH.md, HBM section): FETCH_SIZE under-reports wide streaming reads by 2x
+on gfx950 and the counter unit is not bytes.  The micro run ends with one device copy of a known
+byte count N (read N, write N); its FETCH_SIZE / WRITE_SIZE give the counter->byte factors, which are
+applied to the conv dispatches.  usage: python tools/traffic.py <pmc_fetch_dir> <pmc_write_dir>
+"""
+import glob
+import json
+import re
+import sqlite3
+import sys
+
+KERNEL = "conv3x3"
+COPY_BYTES = 48 * 192 * 288 * 64 * 2
+
+
+def per_dispatch(d, counter):
+    out = []
+    for db in glob.glob(d + "/**/*.db", recursive=True):
+        c = sqlite3.connect(db)
+        q = ("select kernel_name, dispatch_id, sum(value) from counters_collection "
+             "where counter_name = ? group by dispatch_id order by dispatch_id")
+        out += [(re.sub(r"\(.*", "", k), v) for k, _, v in c.execute(q, (counter,))]
+    return out
+
+
+def main():
+    fd, wd = sys.argv[1], sys.argv[2]
+    res = {}
+    for d, cn in ((fd, "FETCH_SIZE"), (wd, "WRITE_SIZE")):
+        rows = per_dispatch(d, cn)
+        conv = [v for k, v in rows if KERNEL in k]
+        copy = [v for k, v in rows if "elementwise" in k.lower()]
+        if not conv or not copy:
+            raise SystemExit(f"{cn}: conv dispatches {len(conv)}, copy dispatches {len(copy)}")
+        factor = COPY_BYTES / copy[-1]
+        res[cn] = {"conv_counter_avg": sum(conv) / len(conv), "copy_counter": copy[-1],
+                   "bytes_per_unit": factor, "conv_bytes": sum(conv) / len(conv) * factor,
+                   "dispatches": len(conv)}
+    alg = 2 * COPY_BYTES  # input read once + output written once (weights 74 KB)
+    total = res["FETCH_SIZE"]["conv_bytes"] + res["WRITE_SIZE"]["conv_bytes"]
+    res["traffic_bytes_per_launch"] = total
+    res["algorithmic_bytes_per_launch"] = alg
+    res["traffic_over_algorithmic"] = total / alg
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
