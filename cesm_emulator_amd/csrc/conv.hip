@@ -50,12 +50,16 @@ template <typename T> struct KCfg;
 template <> struct KCfg<bf16> { static constexpr int VEC = 8; static constexpr int LDW = 40; };   // 80-B rows
 template <> struct KCfg<float> { static constexpr int VEC = 4; static constexpr int LDW = 36; };  // 144-B rows
 
-template <typename T, int BN>
+// PAR (U = 2, S = 1, even KH/KW, even Ho/Wo): parity-blocked transposed conv.  Output pixels with
+// (oy, ox) = (2a + py, 2b + px) only receive taps ky = (P - py) mod 2 + 2i, kx = (P - px) mod 2 + 2j,
+// so each block holds pixels of ONE parity class (blockIdx.y = parity * bpp + tile; M = pixels per
+// class) and loops over its KH*KW/4 live taps instead of all KH*KW (3/4 of which gather zeros).
+template <typename T, int BN, bool PAR = false>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(const T* __restrict__ x1, const T* __restrict__ x2,
                                                        const T* __restrict__ w, const float* __restrict__ bias,
                                                        const T* __restrict__ res, const T* __restrict__ res2,
                                                        T* __restrict__ y1, T* __restrict__ y2, ConvGeom g,
-                                                       int64_t M) {
+                                                       int64_t M, int bpp = 0) {
   constexpr int VEC = KCfg<T>::VEC;
   constexpr int LDW = KCfg<T>::LDW;
   constexpr int VPR = BK / VEC;          // vectors per row
@@ -73,11 +77,17 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const T* __restrict__ x1,
   const int wr = wid >> 1, wc = wid & 1;
   // grid.x = output-channel tile (fast): the Cout/BN blocks sharing one pixel tile run adjacently,
   // so the im2col tile is re-read from L2 instead of HBM
-  const int64_t m0 = (int64_t)blockIdx.y * BMP;
+  const int par = PAR ? (int)blockIdx.y / bpp : 0;
+  const int py = par >> 1, px = par & 1;
+  const int64_t m0 = (int64_t)(PAR ? (int)blockIdx.y - par * bpp : (int)blockIdx.y) * BMP;
   const int n0 = blockIdx.x * BN;
   const int Cin = g.C1 + g.C2;
   const int csteps = Cin / BK;
-  const int ksteps = g.KH * g.KW * csteps;
+  const int ntap = PAR ? (g.KH / 2) * (g.KW / 2) : g.KH * g.KW;
+  const int ksteps = ntap * csteps;
+  const int ky0 = PAR ? (((g.P - py) % 2) + 2) % 2 : 0;
+  const int kx0 = PAR ? (((g.P - px) % 2) + 2) % 2 : 0;
+  const int Wg = PAR ? g.Wo / 2 : g.Wo, Hg = PAR ? g.Ho / 2 : g.Ho;  // pixel grid enumerated by m
 
   // per-thread staging rows
   const int vrow = tid / VPR, vk = (tid % VPR) * VEC;
@@ -88,19 +98,32 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const T* __restrict__ x1,
     const int64_t m = m0 + vrow + p * RPP;
     pval[p] = m < M;
     const int64_t mm = pval[p] ? m : 0;
-    pox[p] = (int)(mm % g.Wo);
-    const int64_t t = mm / g.Wo;
-    poy[p] = (int)(t % g.Ho);
-    pn[p] = (int)(t / g.Ho);
+    pox[p] = (int)(mm % Wg);
+    const int64_t t = mm / Wg;
+    poy[p] = (int)(t % Hg);
+    pn[p] = (int)(t / Hg);
+    if constexpr (PAR) {
+      poy[p] = 2 * poy[p] + py;
+      pox[p] = 2 * pox[p] + px;
+    }
   }
 
   float xr[PX_PASS][VEC];
   float wreg[W_PASS][VEC];
 
   auto gload = [&](int ks) {
-    const int tap = ks / csteps;
-    const int c0 = (ks - tap * csteps) * BK;
-    const int ky = tap / g.KW, kx = tap - ky * g.KW;
+    const int t = ks / csteps;
+    const int c0 = (ks - t * csteps) * BK;
+    int ky, kx;
+    if constexpr (PAR) {
+      const int hw = g.KW / 2;
+      ky = ky0 + 2 * (t / hw);
+      kx = kx0 + 2 * (t - (t / hw) * hw);
+    } else {
+      ky = t / g.KW;
+      kx = t - ky * g.KW;
+    }
+    const int tap = ky * g.KW + kx;
     const T* src;
     int cs, cc;
     if (c0 < g.C1) { src = x1; cs = g.C1; cc = c0; } else { src = x2; cs = g.C2; cc = c0 - g.C1; }
@@ -194,8 +217,12 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const T* __restrict__ x1,
   const int Co2 = g.Cout - g.Co1;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int64_t m = m0 + wc * 64 + j * 16 + lr;
+    int64_t m = m0 + wc * 64 + j * 16 + lr;
     if (m >= M) continue;
+    if constexpr (PAR) {  // class-local index -> output pixel
+      const int64_t b = m % Wg, t = m / Wg, a = t % Hg, n = t / Hg;
+      m = (n * g.Ho + 2 * a + py) * g.Wo + 2 * b + px;
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int co = n0 + wr * (BN / 2) + i * 16 + lg * 4;
@@ -1478,6 +1505,19 @@ int cesm_conv_fwd(int dtype, const void* x1, const void* x2, const void* wp, con
       conv3x3_bf16_kernel<32><<<g3, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
                                                       (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, tx,
                                                       TH);
+  } else if (dtype == CESM_DT_BF16 && U == 2 && S == 1 && KH % 2 == 0 && KW % 2 == 0 && Ho % 2 == 0 &&
+             Wo % 2 == 0 && !getenv_flag("CESM_NO_PARITY_TCONV")) {
+    const int64_t Mp = (int64_t)Nb * (Ho / 2) * (Wo / 2);
+    const int bpp = (int)cdiv(Mp, BMP);
+    dim3 gp(Cout / BN, 4 * bpp);
+    if (BN == 128)
+      conv_fwd_kernel<bf16, 128, true><<<gp, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp,
+                                                               bias, (const bf16*)res, (const bf16*)res2, (bf16*)y1,
+                                                               (bf16*)y2, g, Mp, bpp);
+    else
+      conv_fwd_kernel<bf16, 64, true><<<gp, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp,
+                                                              bias, (const bf16*)res, (const bf16*)res2, (bf16*)y1,
+                                                              (bf16*)y2, g, Mp, bpp);
   } else if (dtype == CESM_DT_BF16) {
     if (BN == 128)
       conv_fwd_kernel<bf16, 128><<<grid, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,

@@ -84,10 +84,16 @@ def conv_fwd(x1, x2, wp, bias, geom, res=None, res2=None, out_split=None):
 CONV_TRACE = [] if os.environ.get("CESM_TRACE_CONV") else None
 
 
-def _wgrad_nsplit(M, cout, K, bm=64):
-    """pixel splits of the weight-gradient GEMM: ~2048 blocks of (bm x 64) tiles, >= 256 pixels each"""
+# target block count of the split-K weight-gradient launches: every split writes a full fp32
+# [Cout][K] slab that conv_wgrad_reduce reads back, so more blocks than ~2-4 per CU only adds slab
+# traffic (override: CESM_WGRAD_BLOCKS)
+WGRAD_BLOCKS = int(os.environ.get("CESM_WGRAD_BLOCKS", "1024"))
+
+
+def _wgrad_nsplit(M, cout, K, bm=64, blocks=None):
+    """pixel splits of the weight-gradient GEMM: ~`blocks` blocks of (bm x 64) tiles, >= 256 pixels each"""
     tiles = max(1, cout // bm) * max(1, K // 64)
-    n = max(1, 2048 // tiles)
+    n = max(1, (blocks or WGRAD_BLOCKS) // tiles)
     n = min(n, max(1, M // 256))
     return n
 
@@ -115,9 +121,11 @@ def conv_wgrad(x1, x2, dy1, dy2, dw, geom, swap, flip, accumulate=True):
     halo3 = KH == 3 and KW == 3 and St == 1 and Pd == 1 and U == 1
     if halo3 and x1.dtype == torch.bfloat16:
         # wgrad3x3 kernel: blocks of 64 co x 32 ci (all 9 taps), split over pixel tiles
-        nsplit = max(1, min(2048 // max(1, (Cout // 64) * ((C1 + C2) // 32)), max(1, M // 256)))
+        nb = WGRAD_BLOCKS // 2
+        nsplit = max(1, min(nb // max(1, (Cout // 64) * ((C1 + C2) // 32)), max(1, M // 256)))
     else:
-        nsplit = _wgrad_nsplit(M, Cout, K, _wgrad_bm(x1, Cout, Co1))
+        bm = _wgrad_bm(x1, Cout, Co1)
+        nsplit = _wgrad_nsplit(M, Cout, K, bm, WGRAD_BLOCKS // 2 if bm == 256 else WGRAD_BLOCKS)
     slab = empty((nsplit, Cout, K), torch.float32, x1.device)
     if CONV_TRACE is not None:
         CONV_TRACE.append(("wgrad", Nb, Hi, Wi, C1 + C2, Ho, Wo, Cout, KH, KW, St, Pd, U))

@@ -102,7 +102,16 @@ def conv_backward(rc, spec, st, dy, need_dx=True, dres1=None, dres2=None, bias_d
     w, b = spec.mod.weight, spec.mod.bias
     dw = gbuf(w)
     if dw is not None:
-        K.conv_wgrad(st.x1, st.x2, dy, None, dw, st.geom, st.swap, st.flip)
+        if spec.transposed:
+            # the transposed conv's weight gradient sum_{a,b} x[a,b] (x) dOut[S*a - P + ky, S*b - P + kx] is the
+            # weight gradient of the plain strided conv dOut -> x-grid (GEMM co = x channels = torch dim 0,
+            # taps unflipped: lands in the [in, out, 1, k, k] layout with swap = flip = 0); every tap is live,
+            # unlike the U = S gather form where 3/4 of the (pixel, tap) pairs are zero
+            assert st.x2 is None
+            Hx, Wx = st.x1.shape[1], st.x1.shape[2]
+            K.conv_wgrad(dy, None, st.x1, None, dw, (Hx, Wx, spec.cin, spec.k, spec.k, spec.stride, spec.pad, 1), 0, 0)
+        else:
+            K.conv_wgrad(st.x1, st.x2, dy, None, dw, st.geom, st.swap, st.flip)
     db = gbuf(b)
     if db is not None and not bias_done:
         K.colsum(dy, db)

@@ -1,5 +1,5 @@
 """Level-0 sized fused SLA fwd+bwd launches (for rocprofv3 counter passes).
-usage: python tools/sla_micro.py [reps]"""
+usage: python tools/sla_micro.py [reps] [emit 0|1]"""
 import sys
 
 import torch
@@ -10,6 +10,7 @@ from cesm_emulator_amd import kernels as K  # noqa: E402
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    emit = (sys.argv[2] != '0') if len(sys.argv) > 2 else True
     Nf, H, W, C = 48, 192, 288, 64
     dev = torch.device("cuda")
     torch.manual_seed(0)
@@ -26,7 +27,7 @@ def main():
     dgamma = torch.zeros(C, device=dev)
     for _ in range(reps):
         y, st = K.slaf_fwd(x, gamma, wq, wo, bout, 32 ** -0.5)
-        K.slaf_bwd(x, dy, gamma, wq, wq_t, wo_t, st, dgamma, 32 ** -0.5)
+        K.slaf_bwd(x, dy, gamma, wq, wq_t, wo_t, st, dgamma, 32 ** -0.5, want_wgrad_inputs=emit)
     torch.cuda.synchronize()
     print("ok", float(y.float().abs().mean()))
 

@@ -1,5 +1,5 @@
 """Level-0 sized fused temporal-block fwd+bwd launches (for rocprofv3 counter passes).
-usage: python tools/tblock_micro.py [C] [reps]"""
+usage: python tools/tblock_micro.py [C] [reps] [emit 0|1]"""
 import sys
 
 import torch
@@ -11,6 +11,7 @@ from cesm_emulator_amd import kernels as K  # noqa: E402
 def main():
     C = int(sys.argv[1]) if len(sys.argv) > 1 else 64
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+    emit = (sys.argv[3] != '0') if len(sys.argv) > 3 else True
     B, F = 4, 12
     H, W = {64: (192, 288), 128: (96, 144), 256: (48, 72), 512: (24, 36)}[C]
     dev = torch.device("cuda")
@@ -30,7 +31,8 @@ def main():
     dtable = torch.zeros(32, 8, device=dev)
     for _ in range(reps):
         y, mr, lse = K.tblock_fwd(x, gamma, wq, wo, bias, rot, B, F, 32 ** -0.5)
-        K.tblock_bwd(x, dy, gamma, mr, lse, wq, wq_t, wo_t, bias, rot, dgamma, dtable, B, F, 32 ** -0.5)
+        K.tblock_bwd(x, dy, gamma, mr, lse, wq, wq_t, wo_t, bias, rot, dgamma, dtable, B, F, 32 ** -0.5,
+                      want_wgrad_inputs=emit)
     torch.cuda.synchronize()
     print("ok", float(y.float().abs().mean()))
 
