@@ -409,6 +409,421 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
 }
 
 // ----------------------------------------------------------------------------------------
+// 3x3 / stride 1 / pad 1 conv (bf16), v3 "wide wave": block = TH x TW (<= 512) output pixels of one
+// image x 64 output channels; 4 waves, wave w owns tile pixels [128w, 128w + 128) (8 fragment groups
+// of 16) x ALL 64 channels (32 accumulators): per tap 4 A + 8 B ds_read_b128 feed 32 MFMA (0.375
+// reads / MFMA vs 0.625 for the 32-co wave tile of conv3x3_bf16_kernel), and the block's 512 pixels
+// halve the weight staging per pixel.  Per 32-channel chunk the (TH+2)(TW+2) halo and the 9 x 64 x 32
+// weight tile are staged by LDS-DMA (global_load_lds, no VGPR round trip) into 64-B rows whose
+// 16-B chunk index is XORed with (row >> 1) & 2 - conflict-free for ds_read_b128 over any 16
+// consecutive rows (exhaustive check over the four lane groups); the weight-fragment addresses are
+// compile-time + lane constants.  76 KiB LDS -> two blocks per CU: one stages while the other
+// computes.
+// ----------------------------------------------------------------------------------------
+constexpr int CW_HROWS = 640;                       // max halo rows (TH+2)(TW+2)
+constexpr int CW_WROWS = 9 * 64;                    // weight rows (tap*64 + co)
+constexpr int CW_HPIECE = CW_HROWS / 16;            // 1-KiB glds pieces
+constexpr int CW_WPIECE = CW_WROWS / 16;
+constexpr int CW_HPW = CW_HPIECE / 4;               // halo pieces per wave (10)
+constexpr int CW_WPW = CW_WPIECE / 4;               // weight pieces per wave (9)
+__device__ __attribute__((aligned(64))) bf16 cw_zero_page[32] = {};
+
+__device__ __forceinline__ int cw_swz(int row) { return (row >> 1) & 2; }
+__device__ __forceinline__ bf16x8 zero8_bf16() {
+  bf16x8 z;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) z[i] = (bf16)0.f;
+  return z;
+}
+// byte offset of 16-B chunk c (8 channels) of row `row`
+__device__ __forceinline__ int cw_off(int row, int c) { return (row << 6) + ((c ^ cw_swz(row)) << 4); }
+
+// the 9 taps of one staged 32-channel chunk: 4 A + 8 B fragments per tap, software-pipelined one
+// tap ahead in registers (the reads of tap t+1 are issued before tap t's 32 MFMAs; sched_barrier
+// pins the order so the scheduler cannot hoist every tap's reads and blow the register budget)
+template <int TW>
+__device__ __forceinline__ void cw_taps(const char* sh, const char* sw, const int (&hoff)[8], int lr, int lg,
+                                        f32x4 (&acc)[4][8]) {
+  constexpr int HWd = TW + 2;
+  bf16x8 af[2][4], bfr[2][8];
+  // weight rows tap*64 + i*16 + lr: swizzle bit = bit 2 of lr -> compile-time offset + a lane constant
+  const int a_lane = (lr << 6) + ((lg ^ cw_swz(lr)) << 4);
+  // opaque copies: keeps the (non-linear, swizzled) halo addresses from being hoisted out of the
+  // chunk loop as 72 loop-invariant VGPRs
+  int ho[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ho[j] = hoff[j];
+    asm volatile("" : "+v"(ho[j]));
+  }
+  auto load = [&](int tap, int b) {
+    const int ky = tap / 3, kx = tap - ky * 3;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[b][i] = *reinterpret_cast<const bf16x8*>(sw + a_lane + (tap * 64 + i * 16) * 64);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bfr[b][j] = *reinterpret_cast<const bf16x8*>(sh + cw_off(ho[j] + ky * HWd + kx, lg));
+  };
+  load(0, 0);
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int b = tap & 1;
+    if (tap + 1 < 9) load(tap + 1, b ^ 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[b][i], bfr[b][j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+template <int TW>
+__global__ __launch_bounds__(256, 2) void conv3x3w_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
+                                                          const bf16* __restrict__ w, const float* __restrict__ bias,
+                                                          const bf16* __restrict__ res, const bf16* __restrict__ res2,
+                                                          bf16* __restrict__ y1, bf16* __restrict__ y2, ConvGeom g,
+                                                          int tiles_x, int TH) {
+  __shared__ __attribute__((aligned(1024))) char lds[(CW_HROWS + CW_WROWS) * 64];
+  char* sh = lds;
+  char* sw = lds + CW_HROWS * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int n = blockIdx.y;
+  const int ty = blockIdx.x / tiles_x, tx = blockIdx.x - ty * tiles_x;
+  const int y0 = ty * TH, x0 = tx * TW;
+  constexpr int HWd = TW + 2;
+  const int HP = (TH + 2) * HWd;
+  const int n0 = blockIdx.z * 64;
+  const int Cin = g.C1 + g.C2;
+  const int nchunk = Cin / 32;
+
+  // LDS-DMA through buffer descriptors (32-bit per-lane offsets, out-of-range -> zeros): halo piece
+  // k of wave w = rows 16*(w + 4k) + lane/4, 16-B slot lane&3 of each row
+  const int prow = lane >> 2, pslot = lane & 3;
+  const int hpieces = (HP + 15) >> 4;
+  int hpix[CW_HPW];  // source pixel (iy*Wi + ix) of this lane's row in halo piece k, -1 = zero row
+#pragma unroll
+  for (int k = 0; k < CW_HPW; ++k) {
+    const int row = 16 * (wid + 4 * k) + prow;
+    const int hy = row / HWd, hx = row - (row / HWd) * HWd;
+    const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
+    hpix[k] = (row < HP && (unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi) ? iy * g.Wi + ix : -1;
+  }
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(w + (int64_t)n0 * 9 * Cin), (short)0, 64 * 9 * Cin * 2, 0x00020000);
+
+  auto stage = [&](int ch) {
+    const int c0 = ch * 32;
+    const bf16* src;
+    int cs, cc;
+    if (c0 < g.C1) { src = x1; cs = g.C1; cc = c0; } else { src = x2; cs = g.C2; cc = c0 - g.C1; }
+    const int64_t img_elems = (int64_t)g.Hi * g.Wi * cs;
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(src + (int64_t)n * img_elems + cc), (short)0, (int)(img_elems * 2 - cc * 2), 0x00020000);
+#pragma unroll
+    for (int k = 0; k < CW_HPW; ++k) {
+      const int q = wid + 4 * k;
+      if (q < hpieces) {  // wave-uniform
+        const int chunk = pslot ^ cw_swz(16 * q + prow);
+        const int vo = hpix[k] >= 0 ? (hpix[k] * cs + chunk * 8) * 2 : 0x7ffffff0;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)(sh + q * 1024), 16, vo,
+                                                 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < CW_WPW; ++k) {
+      const int q = wid + 4 * k;
+      const int row = 16 * q + prow;  // tap*64 + co
+      const int chunk = pslot ^ cw_swz(row);
+      const int vo = (((row & 63) * 9 + (row >> 6)) * Cin + c0 + chunk * 8) * 2;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(sw + q * 1024), 16, vo, 0,
+                                               0, 0);
+    }
+  };
+
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // halo row of tap (0,0) for fragment group j (pixels past TH*TW read row 0; results discarded)
+  int hoff[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int p = wid * 128 + j * 16 + lr;
+    const int py = p / TW, px = p - (p / TW) * TW;
+    hoff[j] = p < TH * TW ? py * HWd + px : 0;
+  }
+  for (int ch = 0; ch < nchunk; ++ch) {
+    if (ch) __syncthreads();  // all fragment reads of the previous chunk done before the DMA overwrites
+    stage(ch);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    cw_taps<TW>(sh, sw, hoff, lr, lg, acc);
+  }
+  // epilogue: lane holds co = n0 + i*16 + 4*lg + r of tile pixel wid*128 + j*16 + lr
+  const int Co2 = g.Cout - g.Co1;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int p = wid * 128 + j * 16 + lr;
+    if (p >= TH * TW) continue;
+    const int oy = y0 + p / TW, ox = x0 + (p - (p / TW) * TW);
+    if (oy >= g.Ho || ox >= g.Wo) continue;
+    const int64_t m = ((int64_t)n * g.Ho + oy) * g.Wo + ox;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = n0 + i * 16 + lg * 4;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (bias) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += bias[co + r];
+      }
+      if (co < g.Co1) {
+        if (res) {
+          float rv[4];
+          load4(res + m * g.Co1 + co, rv);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += rv[r];
+        }
+        store4(y1 + m * g.Co1 + co, v);
+      } else {
+        if (res2) {
+          float rv[4];
+          load4(res2 + m * Co2 + (co - g.Co1), rv);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += rv[r];
+        }
+        store4(y2 + m * Co2 + (co - g.Co1), v);
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// 3x3 conv (bf16), v4 "pipelined wide wave": the conv3x3w tile / wave layout / LDS image, but
+// persistent (one block per CU) with TWO LDS stages: the buffer-LDS-DMA of step s+1 (next 32-channel
+// chunk, or the next item's first chunk) is issued right after the barrier that opens step s and
+// lands while step s's 288 MFMAs per wave run.  Steps run over the block's items (it = blockIdx.x +
+// k * gridDim.x; item = (image, tile, 64-channel co block), co block fastest so the co blocks of a
+// tile run concurrently and share its halo in L2).
+// ----------------------------------------------------------------------------------------
+constexpr int CP_STAGE = (CW_HROWS + CW_WROWS) * 64;  // 76 KiB
+constexpr int CP_NST = 16;                            // epilogue buffer stores per wave (vmcnt count)
+constexpr int CP_ELD = 68;                            // epilogue tile row (bf16): 136 B, conflict-free 8-B writes
+
+template <int TW>
+__global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
+                                                          const bf16* __restrict__ w, const float* __restrict__ bias,
+                                                          const bf16* __restrict__ res, const bf16* __restrict__ res2,
+                                                          bf16* __restrict__ y1, bf16* __restrict__ y2, ConvGeom g,
+                                                          int tiles_x, int tiles_per_img, int TH, int ncob, int nitems,
+                                                          int dbg) {
+  // one LDS array (a second __shared__ object can make hipcc drain the DMA before ds_reads):
+  // 2 stages | bias [Cout <= 1024] fp32
+  __shared__ __attribute__((aligned(1024))) char lds[2 * CP_STAGE + 4096];
+  float* sbias = reinterpret_cast<float*>(lds + 2 * CP_STAGE);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  constexpr int HWd = TW + 2;
+  const int HP = (TH + 2) * HWd;
+  for (int c = tid; c < g.Cout; c += 256) sbias[c] = bias ? bias[c] : 0.f;
+  const int hpieces = (HP + 15) >> 4;
+  const int Cin = g.C1 + g.C2;
+  const int nchunk = Cin / 32;
+  const int prow = lane >> 2, pslot = lane & 3;
+  const int nmine = nitems > (int)blockIdx.x ? (nitems - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int nsteps = nmine * nchunk;
+
+  // per-lane halo row -> tile-relative (hy, hx) of piece k (item independent)
+  int hrel[CW_HPW];
+#pragma unroll
+  for (int k = 0; k < CW_HPW; ++k) {
+    const int row = 16 * (wid + 4 * k) + prow;
+    const int hy = row / HWd, hx = row - (row / HWd) * HWd;
+    hrel[k] = row < HP ? (hy << 16) | hx : -1;
+  }
+  // fragment-group halo rows of tap (0,0)
+  int hoff[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int p = wid * 128 + j * 16 + lr;
+    hoff[j] = p < TH * TW ? (p / TW) * HWd + (p - (p / TW) * TW) : 0;
+  }
+
+  auto item_geo = [&](int it, int& n, int& y0, int& x0, int& cob) {
+    cob = it % ncob;
+    const int t = it / ncob;
+    n = t / tiles_per_img;
+    const int r = t - n * tiles_per_img;
+    const int ty = r / tiles_x;
+    y0 = ty * TH;
+    x0 = (r - ty * tiles_x) * TW;
+  };
+  auto issue = [&](int s) {
+    const int it = (int)blockIdx.x + (s / nchunk) * (int)gridDim.x, ch = s % nchunk;
+    int n, y0, x0, cob;
+    item_geo(it, n, y0, x0, cob);
+    const int c0 = ch * 32;
+    const bf16* src;
+    int cs, cc;
+    if (c0 < g.C1) { src = x1; cs = g.C1; cc = c0; } else { src = x2; cs = g.C2; cc = c0 - g.C1; }
+    const int64_t img_elems = (int64_t)g.Hi * g.Wi * cs;
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(src + (int64_t)n * img_elems + cc), (short)0, (int)(img_elems * 2 - cc * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(w + (int64_t)cob * 64 * 9 * Cin + c0), (short)0, 64 * 9 * Cin * 2 - c0 * 2, 0x00020000);
+    char* sh = lds + (s & 1) * CP_STAGE;
+    char* sw = sh + CW_HROWS * 64;
+#pragma unroll
+    for (int k = 0; k < CW_HPW; ++k) {
+      const int q = wid + 4 * k;
+      if (q < hpieces) {  // wave-uniform
+        const int chunk = pslot ^ cw_swz(16 * q + prow);
+        const int iy = y0 - 1 + (hrel[k] >> 16), ix = x0 - 1 + (hrel[k] & 0xffff);
+        const bool in = hrel[k] >= 0 && (unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi;
+        const int vo = in ? ((iy * g.Wi + ix) * cs + chunk * 8) * 2 : 0x7ffffff0;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)(sh + q * 1024), 16, vo,
+                                                 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < CW_WPW; ++k) {
+      const int q = wid + 4 * k;
+      const int row = 16 * q + prow;  // tap*64 + co
+      const int chunk = pslot ^ cw_swz(row);
+      const int vo = (((row & 63) * 9 + (row >> 6)) * Cin + chunk * 8) * 2;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(sw + q * 1024), 16, vo, 0,
+                                               0, 0);
+    }
+  };
+
+  if (nsteps > 0) issue(0);
+  int s = 0;
+  bool epi = false;
+  for (int k = 0; k < nmine; ++k) {
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int ch = 0; ch < nchunk; ++ch, ++s) {
+      // step s landed: after an epilogue only its CP_NST stores are younger than step s's DMA
+      if (epi) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      epi = false;
+      __builtin_amdgcn_s_barrier();                     // ... for every wave; step s-1's reads are done
+      if (s + 1 < nsteps && !(dbg & 1)) issue(s + 1);     // into the stage step s-1 used
+      const char* sh = lds + (s & 1) * CP_STAGE;
+      if (!(dbg & 2)) cw_taps<TW>(sh, sh + CW_HROWS * 64, hoff, lr, lg, acc);
+    }
+    int n, y0, x0, cob;
+    item_geo((int)blockIdx.x + k * (int)gridDim.x, n, y0, x0, cob);
+    const int n0 = cob * 64;
+    if (dbg & 4) {  // debug: no epilogue (keep the accumulators live)
+      float sacc = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sacc += acc[i][j][0];
+      if (sacc == 12345.f) y1[0] = (bf16)sacc;
+      continue;
+    }
+    // epilogue through LDS: (acc + bias) -> bf16 tile [512 px][CP_ELD] in the stage just consumed
+    // (every wave is past its taps: barrier), then 8 lanes per pixel write full 128-B rows
+    // (+ residual read the same way) with 16-B accesses
+    __builtin_amdgcn_s_barrier();
+    bf16* so = reinterpret_cast<bf16*>(lds + ((s - 1) & 1) * CP_STAGE);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = i * 16 + lg * 4;
+      const f32x4 bv = *reinterpret_cast<const f32x4*>(sbias + n0 + co);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int p = wid * 128 + j * 16 + lr;
+        float v[4] = {acc[i][j][0] + bv[0], acc[i][j][1] + bv[1], acc[i][j][2] + bv[2], acc[i][j][3] + bv[3]};
+        store4(so + p * CP_ELD + co, v);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    {
+      // the 64-channel block lies wholly in y1 or y2 (Co1 % 64 == 0); 32-bit offsets within image n.
+      // Exactly CP_NST buffer stores per wave (rows outside the image -> out-of-range offset, dropped)
+      // so the next step can wait for its DMA with vmcnt(CP_NST) instead of draining these stores.
+      const bool first = n0 < g.Co1;
+      const int cstride = first ? g.Co1 : g.Cout - g.Co1;
+      const int cofs = (first ? n0 : n0 - g.Co1) + (lane & 7) * 8;
+      const int64_t img = (int64_t)n * g.Ho * g.Wo * cstride;
+      const int img_bytes = g.Ho * g.Wo * cstride * 2;
+      const __amdgpu_buffer_rsrc_t yrs =
+          __builtin_amdgcn_make_buffer_rsrc((void*)((first ? y1 : y2) + img), (short)0, img_bytes, 0x00020000);
+      const bf16* rsrc = first ? res : res2;
+      auto row_off = [&](int it2, bool& ok) {
+        const int p = wid * 128 + it2 * 8 + (lane >> 3);
+        const int oy = y0 + p / TW, ox = x0 + (p - (p / TW) * TW);
+        ok = p < TH * TW && oy < g.Ho && ox < g.Wo;
+        return (ok ? oy * g.Wo + ox : 0) * cstride + cofs;  // invalid rows read row 0, never store
+      };
+      auto tile_row = [&](int it2) {
+        return *reinterpret_cast<const bf16x8*>(so + (wid * 128 + it2 * 8 + (lane >> 3)) * CP_ELD + (lane & 7) * 8);
+      };
+      if (rsrc) {
+        const __amdgpu_buffer_rsrc_t rrs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(rsrc + img), (short)0, img_bytes, 0x00020000);
+#pragma unroll
+        for (int b4 = 0; b4 < 4; ++b4) {
+          int off[4];
+          bool ok[4];
+          u32x4 rv[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            off[u] = row_off(b4 * 4 + u, ok[u]);
+            rv[u] = __builtin_amdgcn_raw_buffer_load_b128(rrs, off[u] * 2, 0, 0);
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            bf16x8 v = tile_row(b4 * 4 + u);
+            const bf16x8 r = __builtin_bit_cast(bf16x8, rv[u]);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = (bf16)((float)v[e] + (float)r[e]);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yrs, ok[u] ? off[u] * 2 : 0x7ffffff0,
+                                                   0, 0);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int it2 = 0; it2 < 16; ++it2) {
+          bool ok;
+          const int off = row_off(it2, ok);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, tile_row(it2)), yrs, ok ? off * 2 : 0x7ffffff0,
+                                                 0, 0);
+        }
+      }
+      epi = true;
+    }
+  }
+}
+
+// tile of the wide-wave conv: TW in {32, 36}, TH*TW <= 512, (TH+2)(TW+2) <= 640; maximise useful /
+// computed pixels (computed = 512 per tile), fewest tiles on ties
+static void cw_tile(int Ho, int Wo, int& TH, int& TW) {
+  double best = -1.0;
+  int bt = 1 << 30;
+  const int cands[2] = {32, 36};
+  for (int c = 0; c < 2; ++c) {
+    const int tw = cands[c];
+    for (int th = 1; th * tw <= 512; ++th) {
+      if ((th + 2) * (tw + 2) > CW_HROWS) break;
+      const int ntile = (int)(cdiv(Ho, th) * cdiv(Wo, tw));
+      const double util = (double)Ho * Wo / ((double)ntile * 512);
+      if (util > best + 1e-9 || (util > best - 1e-9 && ntile < bt)) { best = util; bt = ntile; TH = th; TW = tw; }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------
 // 3x3 / stride 1 / pad 1 conv (bf16), v2: persistent, software-pipelined halo conv.
 // Work item = (TH x TW pixel tile of one image, 64 output channels); a block streams the
 // (item, 32-channel chunk) sequence through two LDS stages filled by global_load_lds (LDS-DMA, no
@@ -1482,7 +1897,35 @@ int cesm_conv_fwd(int dtype, const void* x1, const void* x2, const void* wp, con
   dim3 grid(Cout / BN, (unsigned)cdiv(M, BMP));
   const bool halo3 = dtype == CESM_DT_BF16 && KH == 3 && KW == 3 && S == 1 && P == 1 && U == 1 && Ho == Hi &&
                      Wo == Wi && (Co1 % H3_BN) == 0 && !getenv_flag("CESM_NO_HALO");
-  if (halo3 && getenv_flag("CESM_CONV3X3_V2")) {
+  if (halo3 && getenv_flag("CESM_CONV3X3_V4")) {
+    const int dbg = (getenv_flag("CESM_DBG_NODMA") ? 1 : 0) | (getenv_flag("CESM_DBG_NOMFMA") ? 2 : 0) |
+                    (getenv_flag("CESM_DBG_NOEPI") ? 4 : 0);
+    int TH = 16, TW = 32;
+    cw_tile(Ho, Wo, TH, TW);
+    const int tx = (int)cdiv(Wo, TW), ty = (int)cdiv(Ho, TH);
+    const int ncob = Cout / 64;
+    const int nitems = Nb * tx * ty * ncob;
+    const int nblk = std::min(nitems, cesm_num_cus());
+    if (TW == 36)
+      conv3x3p_kernel<36><<<nblk, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
+                                                    (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, tx,
+                                                    tx * ty, TH, ncob, nitems, dbg);
+    else
+      conv3x3p_kernel<32><<<nblk, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
+                                                    (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, tx,
+                                                    tx * ty, TH, ncob, nitems, dbg);
+  } else if (halo3 && getenv_flag("CESM_CONV3X3_V3")) {
+    int TH = 16, TW = 32;
+    cw_tile(Ho, Wo, TH, TW);
+    const int tx = (int)cdiv(Wo, TW), ty = (int)cdiv(Ho, TH);
+    dim3 g3(tx * ty, Nb, Cout / 64);
+    if (TW == 36)
+      conv3x3w_kernel<36><<<g3, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
+                                                  (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, tx, TH);
+    else
+      conv3x3w_kernel<32><<<g3, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
+                                                  (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, tx, TH);
+  } else if (halo3 && getenv_flag("CESM_CONV3X3_V2")) {
     int TH = 8, TW = 32;
     c2_tile(Ho, Wo, TH, TW);
     const int tx = (int)cdiv(Wo, TW), ty = (int)cdiv(Ho, TH);
