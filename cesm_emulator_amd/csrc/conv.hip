@@ -610,24 +610,74 @@ __global__ __launch_bounds__(256, 2) void conv3x3w_kernel(const bf16* __restrict
 // tile run concurrently and share its halo in L2).
 // ----------------------------------------------------------------------------------------
 constexpr int CP_STAGE = (CW_HROWS + CW_WROWS) * 64;  // 76 KiB
-constexpr int CP_NST = 16;                            // epilogue buffer stores per wave (vmcnt count)
 constexpr int CP_ELD = 68;                            // epilogue tile row (bf16): 136 B, conflict-free 8-B writes
+constexpr int CP_PITCH = 40;                          // halo row pitch (pixels): multiple of 8
+constexpr int CP_TH = 14;                             // max tile rows: (14 + 2) * 40 = 640 halo rows
 
-template <int TW>
+// taps of one staged chunk for NG fragment groups per wave.  Halo rows use a pitch of 40 pixels, so a
+// ky step (+40 rows) keeps bits 0..2 of the row and with them the chunk swizzle: the B address of
+// (group j, ky, kx) = bad[j][kx] + ky * 40 * 64 -> immediate offsets, no per-read VALU.  Fragment reads
+// of tap t+1 are interleaved with tap t's MFMAs (sched_group_barrier: 1 ds_read, 2 MFMA, ...).
+template <int NG>
+__device__ __forceinline__ void cp_taps(const char* sh, const char* sw, const int (&bad)[NG][3], int a_lane,
+                                        f32x4 (&acc)[4][NG]) {
+  bf16x8 af[2][4], bfr[2][NG];
+  auto load = [&](int tap, int b) {
+    const int ky = tap / 3, kx = tap - ky * 3;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[b][i] = *reinterpret_cast<const bf16x8*>(sw + a_lane + (tap * 64 + i * 16) * 64);
+#pragma unroll
+    for (int j = 0; j < NG; ++j)
+      bfr[b][j] = *reinterpret_cast<const bf16x8*>(sh + bad[j][kx] + ky * CP_PITCH * 64);
+  };
+  load(0, 0);
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int b = tap & 1;
+    __builtin_amdgcn_sched_barrier(0);
+    if (tap + 1 < 9) load(tap + 1, b ^ 1);
+#pragma unroll
+    for (int j = 0; j < NG; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[b][i], bfr[b][j], acc[i][j], 0, 0, 0);
+    if (tap + 1 < 9) {
+#pragma unroll
+      for (int q = 0; q < 4 + NG; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 4 * NG - 2 * (4 + NG), 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+// ----------------------------------------------------------------------------------------
+// 3x3 conv (bf16), v4 "pipelined wide wave": persistent (one block per CU) with TWO LDS stages:
+// the buffer-LDS-DMA of step s+1 (next 32-channel chunk, or the next item's first chunk) is issued
+// right after the barrier that opens step s and lands while step s's MFMAs run.  Steps run over
+// the block's items (it = blockIdx.x + k * gridDim.x; item = (image, TH x TW tile, 64-channel co
+// block), co block fastest so a tile's co blocks run concurrently and share its halo in L2).
+// Wave w owns tile pixels [16*NG*w, 16*NG*(w+1)) x all 64 co.  The epilogue stages (acc + bias) as
+// bf16 in the stage just consumed and writes full 128-B pixel rows (+ residual) with exactly 2*NG
+// buffer stores per wave, so the next step waits for its DMA with vmcnt(2*NG), not for the stores.
+// ----------------------------------------------------------------------------------------
+template <int TW, int NG>
 __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
                                                           const bf16* __restrict__ w, const float* __restrict__ bias,
                                                           const bf16* __restrict__ res, const bf16* __restrict__ res2,
                                                           bf16* __restrict__ y1, bf16* __restrict__ y2, ConvGeom g,
                                                           int tiles_x, int tiles_per_img, int TH, int ncob, int nitems,
                                                           int dbg) {
+  static_assert(TW + 2 <= CP_PITCH && 4 * 16 * NG >= CP_TH * TW - 16 * 4 && NG <= 8, "tile geometry");
   // one LDS array (a second __shared__ object can make hipcc drain the DMA before ds_reads):
   // 2 stages | bias [Cout <= 1024] fp32
   __shared__ __attribute__((aligned(1024))) char lds[2 * CP_STAGE + 4096];
   float* sbias = reinterpret_cast<float*>(lds + 2 * CP_STAGE);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
-  constexpr int HWd = TW + 2;
-  const int HP = (TH + 2) * HWd;
+  const int HP = (TH + 2) * CP_PITCH;
   for (int c = tid; c < g.Cout; c += 256) sbias[c] = bias ? bias[c] : 0.f;
   const int hpieces = (HP + 15) >> 4;
   const int Cin = g.C1 + g.C2;
@@ -636,21 +686,24 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
   const int nmine = nitems > (int)blockIdx.x ? (nitems - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
   const int nsteps = nmine * nchunk;
 
-  // per-lane halo row -> tile-relative (hy, hx) of piece k (item independent)
+  // per-lane halo row -> tile-relative (hy, hx) of piece k (item independent); -1: zero row
   int hrel[CW_HPW];
 #pragma unroll
   for (int k = 0; k < CW_HPW; ++k) {
     const int row = 16 * (wid + 4 * k) + prow;
-    const int hy = row / HWd, hx = row - (row / HWd) * HWd;
-    hrel[k] = row < HP ? (hy << 16) | hx : -1;
+    const int hy = row / CP_PITCH, hx = row - (row / CP_PITCH) * CP_PITCH;
+    hrel[k] = (row < HP && hx < TW + 2) ? (hy << 16) | hx : -1;
   }
-  // fragment-group halo rows of tap (0,0)
-  int hoff[8];
+  // B-fragment addresses of tap (0, kx) per group; A lane constant
+  int bad[NG][3];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int p = wid * 128 + j * 16 + lr;
-    hoff[j] = p < TH * TW ? (p / TW) * HWd + (p - (p / TW) * TW) : 0;
+  for (int j = 0; j < NG; ++j) {
+    const int p = wid * 16 * NG + j * 16 + lr;
+    const int h0 = p < TH * TW ? (p / TW) * CP_PITCH + (p - (p / TW) * TW) : 0;
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) bad[j][kx] = cw_off(h0 + kx, lg);
   }
+  const int a_lane = (lr << 6) + ((lg ^ cw_swz(lr)) << 4);
 
   auto item_geo = [&](int it, int& n, int& y0, int& x0, int& cob) {
     cob = it % ncob;
@@ -703,20 +756,24 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
   int s = 0;
   bool epi = false;
   for (int k = 0; k < nmine; ++k) {
-    f32x4 acc[4][8];
+    f32x4 acc[4][NG];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NG; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int ch = 0; ch < nchunk; ++ch, ++s) {
-      // step s landed: after an epilogue only its CP_NST stores are younger than step s's DMA
-      if (epi) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // step s landed: after an epilogue only its 2*NG stores are younger than step s's DMA
+      if (epi) {
+        if constexpr (NG == 8) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       epi = false;
       __builtin_amdgcn_s_barrier();                     // ... for every wave; step s-1's reads are done
       if (s + 1 < nsteps && !(dbg & 1)) issue(s + 1);     // into the stage step s-1 used
       const char* sh = lds + (s & 1) * CP_STAGE;
-      if (!(dbg & 2)) cw_taps<TW>(sh, sh + CW_HROWS * 64, hoff, lr, lg, acc);
+      if (!(dbg & 2)) cp_taps<NG>(sh, sh + CW_HROWS * 64, bad, a_lane, acc);
     }
     int n, y0, x0, cob;
     item_geo((int)blockIdx.x + k * (int)gridDim.x, n, y0, x0, cob);
@@ -724,15 +781,14 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
     if (dbg & 4) {  // debug: no epilogue (keep the accumulators live)
       float sacc = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
+      for (int j = 0; j < NG; ++j)
 #pragma unroll
         for (int i = 0; i < 4; ++i) sacc += acc[i][j][0];
       if (sacc == 12345.f) y1[0] = (bf16)sacc;
       continue;
     }
-    // epilogue through LDS: (acc + bias) -> bf16 tile [512 px][CP_ELD] in the stage just consumed
+    // epilogue through LDS: (acc + bias) -> bf16 tile [64*NG px][CP_ELD] in the stage just consumed
     // (every wave is past its taps: barrier), then 8 lanes per pixel write full 128-B rows
-    // (+ residual read the same way) with 16-B accesses
     __builtin_amdgcn_s_barrier();
     bf16* so = reinterpret_cast<bf16*>(lds + ((s - 1) & 1) * CP_STAGE);
 #pragma unroll
@@ -740,8 +796,8 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
       const int co = i * 16 + lg * 4;
       const f32x4 bv = *reinterpret_cast<const f32x4*>(sbias + n0 + co);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int p = wid * 128 + j * 16 + lr;
+      for (int j = 0; j < NG; ++j) {
+        const int p = wid * 16 * NG + j * 16 + lr;
         float v[4] = {acc[i][j][0] + bv[0], acc[i][j][1] + bv[1], acc[i][j][2] + bv[2], acc[i][j][3] + bv[3]};
         store4(so + p * CP_ELD + co, v);
       }
@@ -750,8 +806,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
     __builtin_amdgcn_s_barrier();
     {
       // the 64-channel block lies wholly in y1 or y2 (Co1 % 64 == 0); 32-bit offsets within image n.
-      // Exactly CP_NST buffer stores per wave (rows outside the image -> out-of-range offset, dropped)
-      // so the next step can wait for its DMA with vmcnt(CP_NST) instead of draining these stores.
+      // rows outside the image -> out-of-range buffer offset (store dropped), so the count is exact
       const bool first = n0 < g.Co1;
       const int cstride = first ? g.Co1 : g.Cout - g.Co1;
       const int cofs = (first ? n0 : n0 - g.Co1) + (lane & 7) * 8;
@@ -761,30 +816,30 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
           __builtin_amdgcn_make_buffer_rsrc((void*)((first ? y1 : y2) + img), (short)0, img_bytes, 0x00020000);
       const bf16* rsrc = first ? res : res2;
       auto row_off = [&](int it2, bool& ok) {
-        const int p = wid * 128 + it2 * 8 + (lane >> 3);
+        const int p = wid * 16 * NG + it2 * 8 + (lane >> 3);
         const int oy = y0 + p / TW, ox = x0 + (p - (p / TW) * TW);
         ok = p < TH * TW && oy < g.Ho && ox < g.Wo;
         return (ok ? oy * g.Wo + ox : 0) * cstride + cofs;  // invalid rows read row 0, never store
       };
       auto tile_row = [&](int it2) {
-        return *reinterpret_cast<const bf16x8*>(so + (wid * 128 + it2 * 8 + (lane >> 3)) * CP_ELD + (lane & 7) * 8);
+        return *reinterpret_cast<const bf16x8*>(so + (wid * 16 * NG + it2 * 8 + (lane >> 3)) * CP_ELD + (lane & 7) * 8);
       };
       if (rsrc) {
         const __amdgpu_buffer_rsrc_t rrs =
             __builtin_amdgcn_make_buffer_rsrc((void*)(rsrc + img), (short)0, img_bytes, 0x00020000);
 #pragma unroll
-        for (int b4 = 0; b4 < 4; ++b4) {
+        for (int b2 = 0; b2 < NG / 2; ++b2) {
           int off[4];
           bool ok[4];
           u32x4 rv[4];
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            off[u] = row_off(b4 * 4 + u, ok[u]);
+            off[u] = row_off(b2 * 4 + u, ok[u]);
             rv[u] = __builtin_amdgcn_raw_buffer_load_b128(rrs, off[u] * 2, 0, 0);
           }
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            bf16x8 v = tile_row(b4 * 4 + u);
+            bf16x8 v = tile_row(b2 * 4 + u);
             const bf16x8 r = __builtin_bit_cast(bf16x8, rv[u]);
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = (bf16)((float)v[e] + (float)r[e]);
@@ -792,9 +847,22 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
                                                    0, 0);
           }
         }
+        if constexpr (NG % 2) {
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            bool ok;
+            const int off = row_off(2 * NG - 2 + u, ok);
+            const u32x4 rv = __builtin_amdgcn_raw_buffer_load_b128(rrs, off * 2, 0, 0);
+            bf16x8 v = tile_row(2 * NG - 2 + u);
+            const bf16x8 r = __builtin_bit_cast(bf16x8, rv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = (bf16)((float)v[e] + (float)r[e]);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yrs, ok ? off * 2 : 0x7ffffff0, 0, 0);
+          }
+        }
       } else {
 #pragma unroll
-        for (int it2 = 0; it2 < 16; ++it2) {
+        for (int it2 = 0; it2 < 2 * NG; ++it2) {
           bool ok;
           const int off = row_off(it2, ok);
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, tile_row(it2)), yrs, ok ? off * 2 : 0x7ffffff0,
@@ -1897,23 +1965,32 @@ int cesm_conv_fwd(int dtype, const void* x1, const void* x2, const void* wp, con
   dim3 grid(Cout / BN, (unsigned)cdiv(M, BMP));
   const bool halo3 = dtype == CESM_DT_BF16 && KH == 3 && KW == 3 && S == 1 && P == 1 && U == 1 && Ho == Hi &&
                      Wo == Wi && (Co1 % H3_BN) == 0 && !getenv_flag("CESM_NO_HALO");
-  if (halo3 && getenv_flag("CESM_CONV3X3_V4")) {
+  if (halo3 && getenv_flag("CESM_CONV3X3_V4") && Cout <= 1024) {
     const int dbg = (getenv_flag("CESM_DBG_NODMA") ? 1 : 0) | (getenv_flag("CESM_DBG_NOMFMA") ? 2 : 0) |
                     (getenv_flag("CESM_DBG_NOEPI") ? 4 : 0);
-    int TH = 16, TW = 32;
-    cw_tile(Ho, Wo, TH, TW);
+    // TW = 32 -> TH = 14 (448 px = 4 waves x 7 groups); TW = 36 -> TH <= 14 (<= 504 px, 8 groups)
+    const bool w36 = (Wo % 32) != 0 && (Wo % 36) == 0;
+    const int TW = w36 ? 36 : 32;
+    int TH = CP_TH;
+    if (w36) {  // fewest tiles, then least padding
+      int best = 1 << 30;
+      for (int th = CP_TH; th >= 8; --th) {
+        const int nt = (int)cdiv(Ho, th);
+        if (nt * th < best) { best = nt * th; TH = th; }
+      }
+    }
     const int tx = (int)cdiv(Wo, TW), ty = (int)cdiv(Ho, TH);
     const int ncob = Cout / 64;
     const int nitems = Nb * tx * ty * ncob;
     const int nblk = std::min(nitems, cesm_num_cus());
-    if (TW == 36)
-      conv3x3p_kernel<36><<<nblk, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
-                                                    (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, tx,
-                                                    tx * ty, TH, ncob, nitems, dbg);
+    if (w36)
+      conv3x3p_kernel<36, 8><<<nblk, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
+                                                       (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, tx,
+                                                       tx * ty, TH, ncob, nitems, dbg);
     else
-      conv3x3p_kernel<32><<<nblk, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
-                                                    (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, tx,
-                                                    tx * ty, TH, ncob, nitems, dbg);
+      conv3x3p_kernel<32, 7><<<nblk, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
+                                                       (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, tx,
+                                                       tx * ty, TH, ncob, nitems, dbg);
   } else if (halo3 && getenv_flag("CESM_CONV3X3_V3")) {
     int TH = 16, TW = 32;
     cw_tile(Ho, Wo, TH, TW);

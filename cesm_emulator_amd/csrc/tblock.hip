@@ -976,6 +976,15 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
     for (int ct = 0; ct < T::CT; ++ct)
 #pragma unroll
       for (int vt = 0; vt < T::NVTM; ++vt) dxacc[ct][vt] = z4;
+    // dy fragments of the wave's voxels, loaded once (not once per head)
+    constexpr bool DYREG = C <= 64;
+    bf16x8 dyr[DYREG ? T::NVTM : 1][DYREG ? T::KS : 1];
+    if constexpr (DYREG) {
+#pragma unroll
+      for (int vt = 0; vt < T::NVTM; ++vt)
+#pragma unroll
+        for (int ks = 0; ks < T::KS; ++ks) dyr[vt][ks] = vrow[vt] >= 0 ? ld16(dy + vrow[vt] * C + ks * 32 + lg * 8) : zero8();
+    }
 
     for (int h = 0; h < NH; ++h) {
       tw_qkv<C, NV>(wqkv, xf, h, fr, scale, rot, sq, sk, sv, lr, lg);
@@ -991,7 +1000,9 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
             f32x4 acc = z4;
 #pragma unroll
             for (int ks = 0; ks < T::KS; ++ks) {
-              const bf16x8 dyf = vrow[vt] >= 0 ? ld16(dy + vrow[vt] * C + ks * 32 + lg * 8) : zero8();
+              bf16x8 dyf;
+              if constexpr (DYREG) dyf = dyr[vt][ks];
+              else dyf = vrow[vt] >= 0 ? ld16(dy + vrow[vt] * C + ks * 32 + lg * 8) : zero8();
               acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], dyf, acc, 0, 0, 0);
             }
             float o4[4] = {acc[0], acc[1], acc[2], acc[3]};
