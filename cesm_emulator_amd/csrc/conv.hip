@@ -874,6 +874,133 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
   }
 }
 
+// ----------------------------------------------------------------------------------------
+// 1x1 conv (bf16) as a GEMM: Y[m][co] = bias[co] + res[m][co] + sum_k X[m][k] W[co][k], X = [x1 | x2]
+// concatenated on channels, Y = [y1 | y2] split at Co1.  Block = 128 pixels x BN output channels
+// (grid.x = co blocks, fast, so a pixel tile's co blocks share its X rows in L2); K in steps of 64
+// through two LDS stages filled by buffer-LDS-DMA (128-B rows, 16-B chunk index XORed with row & 7,
+// out-of-range rows -> zeros); 4 waves = 2 (co halves) x 2 (64-pixel halves).  The epilogue stages
+// (acc + bias) as bf16 pixel rows in LDS and writes them (+ residual) with coalesced 16-B accesses.
+// Replaces the generic implicit-GEMM path for every 1x1 conv: attention projections at levels with
+// C >= 128, res_conv, and their data gradients.
+// ----------------------------------------------------------------------------------------
+constexpr int G1_BM = 128;
+__device__ __forceinline__ int g1_off(int row, int chunk) { return (row << 7) + ((chunk ^ (row & 7)) << 4); }
+
+template <int BN>
+__global__ __launch_bounds__(256, 2) void gemm1x1_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
+                                                         const bf16* __restrict__ w, const float* __restrict__ bias,
+                                                         const bf16* __restrict__ res, const bf16* __restrict__ res2,
+                                                         bf16* __restrict__ y1, bf16* __restrict__ y2, int M, int C1,
+                                                         int C2, int Cout, int Co1) {
+  constexpr int STAGE = (G1_BM + BN) * 128;  // bytes
+  constexpr int TM = BN / 32;                // 16-co fragments per wave
+  constexpr int ELD = BN + 8;                // epilogue row (bf16)
+  static_assert(G1_BM * ELD * 2 <= 2 * STAGE, "epilogue tile fits the stages");
+  __shared__ __attribute__((aligned(1024))) char lds[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int K = C1 + C2, nk = K / 64;
+  const int m0 = blockIdx.y * G1_BM, n0 = blockIdx.x * BN;
+  const int prow = lane >> 3, pslot = lane & 7;
+
+  auto issue = [&](int ks) {
+    const int c0 = ks * 64;
+    const bf16* src;
+    int cs, cc;
+    if (c0 < C1) { src = x1; cs = C1; cc = c0; } else { src = x2; cs = C2; cc = c0 - C1; }
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(src + (int64_t)m0 * cs + cc), (short)0, (int)((int64_t)(M - m0) * cs * 2 - cc * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(w + (int64_t)n0 * K + c0), (short)0, BN * K * 2 - c0 * 2, 0x00020000);
+    char* sx = lds + (ks & 1) * STAGE;
+    char* sw = sx + G1_BM * 128;
+#pragma unroll
+    for (int k = 0; k < G1_BM / 32; ++k) {  // 8-row pieces, 4 per wave
+      const int q = wid + 4 * k, row = 8 * q + prow;
+      const int chunk = pslot ^ (row & 7);
+      const int vo = m0 + row < M ? (row * cs + chunk * 8) * 2 : 0x7ffffff0;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)(sx + q * 1024), 16, vo, 0,
+                                               0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < BN / 32; ++k) {
+      const int q = wid + 4 * k, row = 8 * q + prow;
+      const int chunk = pslot ^ (row & 7);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(sw + q * 1024), 16,
+                                               (row * K + chunk * 8) * 2, 0, 0, 0);
+    }
+  };
+
+  f32x4 acc[TM][4];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue(0);
+  for (int ks = 0; ks < nk; ++ks) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // stage ks landed for all waves; stage ks+1's previous reads (step ks-1) are done
+    if (ks + 1 < nk) issue(ks + 1);
+    const char* sx = lds + (ks & 1) * STAGE;
+    const char* sw = sx + G1_BM * 128;
+#pragma unroll
+    for (int k32 = 0; k32 < 2; ++k32) {
+      const int chunk = k32 * 4 + lg;
+      bf16x8 af[TM], bfr[4];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(sw + g1_off(wr * (BN / 2) + i * 16 + lr, chunk));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(sx + g1_off(wc * 64 + j * 16 + lr, chunk));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();  // all fragment reads done: reuse the stages for the output tile
+  bf16* so = reinterpret_cast<bf16*>(lds);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int co = wr * (BN / 2) + i * 16 + lg * 4;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (bias) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[r] = bias[n0 + co + r];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int p = wc * 64 + j * 16 + lr;
+      float v[4] = {acc[i][j][0] + bv[0], acc[i][j][1] + bv[1], acc[i][j][2] + bv[2], acc[i][j][3] + bv[3]};
+      store4(so + p * ELD + co, v);
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = BN / 8;  // 16-B chunks per pixel row
+  const int Co2 = Cout - Co1;
+#pragma unroll
+  for (int it = 0; it < G1_BM * CPR / 256; ++it) {
+    const int e = it * 256 + tid;
+    const int p = e / CPR, c = e - p * CPR;
+    const int m = m0 + p;
+    if (m >= M) continue;
+    bf16x8 v = *reinterpret_cast<const bf16x8*>(so + p * ELD + c * 8);
+    const int co = n0 + c * 8;
+    bf16* dst;
+    const bf16* rs;
+    if (co < Co1) { dst = y1 + (int64_t)m * Co1 + co; rs = res ? res + (int64_t)m * Co1 + co : nullptr; }
+    else { dst = y2 + (int64_t)m * Co2 + (co - Co1); rs = res2 ? res2 + (int64_t)m * Co2 + (co - Co1) : nullptr; }
+    if (rs) {
+      const bf16x8 rv = *reinterpret_cast<const bf16x8*>(rs);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = (bf16)((float)v[q] + (float)rv[q]);
+    }
+    *reinterpret_cast<bf16x8*>(dst) = v;
+  }
+}
+
 // tile of the wide-wave conv: TW in {32, 36}, TH*TW <= 512, (TH+2)(TW+2) <= 640; maximise useful /
 // computed pixels (computed = 512 per tile), fewest tiles on ties
 static void cw_tile(int Ho, int Wo, int& TH, int& TW) {
@@ -1965,7 +2092,22 @@ int cesm_conv_fwd(int dtype, const void* x1, const void* x2, const void* wp, con
   dim3 grid(Cout / BN, (unsigned)cdiv(M, BMP));
   const bool halo3 = dtype == CESM_DT_BF16 && KH == 3 && KW == 3 && S == 1 && P == 1 && U == 1 && Ho == Hi &&
                      Wo == Wi && (Co1 % H3_BN) == 0 && !getenv_flag("CESM_NO_HALO");
-  if (halo3 && getenv_flag("CESM_CONV3X3_V4") && Cout <= 1024) {
+  const bool g1x1 = dtype == CESM_DT_BF16 && KH == 1 && KW == 1 && S == 1 && P == 0 && U == 1 && Ho == Hi &&
+                    Wo == Wi && (C1 % 64) == 0 && (C2 % 64) == 0 && (Co1 % 8) == 0 && M < (1ll << 31) &&
+                    M * (C1 > C2 ? C1 : C2) * 2 < (1ll << 31) && !getenv_flag("CESM_NO_GEMM1X1");
+  if (g1x1) {
+    if (Cout % 128 == 0) {
+      dim3 gg(Cout / 128, (unsigned)cdiv(M, G1_BM));
+      gemm1x1_kernel<128><<<gg, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
+                                                  (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, (int)M, C1,
+                                                  C2, Cout, Co1);
+    } else {
+      dim3 gg(Cout / 64, (unsigned)cdiv(M, G1_BM));
+      gemm1x1_kernel<64><<<gg, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
+                                                 (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, (int)M, C1,
+                                                 C2, Cout, Co1);
+    }
+  } else if (halo3 && getenv_flag("CESM_CONV3X3_V4") && Cout <= 1024) {
     const int dbg = (getenv_flag("CESM_DBG_NODMA") ? 1 : 0) | (getenv_flag("CESM_DBG_NOMFMA") ? 2 : 0) |
                     (getenv_flag("CESM_DBG_NOEPI") ? 4 : 0);
     // TW = 32 -> TH = 14 (448 px = 4 waves x 7 groups); TW = 36 -> TH <= 14 (<= 504 px, 8 groups)
