@@ -1667,6 +1667,141 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_bf16_kernel(const bf16* __res
     }
 }
 
+// Same weight gradient on 8 x 36 pixel tiles (288 px = 9 K-chunks of 32 flat pixels): every U-Net
+// level's width (288/144/72/36) is a multiple of 36, so no tile column is wasted (the 8 x 32 tiles
+// above compute 36-px rows as two 32-px tiles: 56 % useful at 24 x 36).  A K-chunk may span two
+// image rows: each lane derives its own halo row per chunk (the transposed ds_read takes per-lane
+// addresses).
+constexpr int W36_TH = 8, W36_TW = 36, W36_HW = W36_TW + 2, W36_NPIX = (W36_TH + 2) * W36_HW;  // 380 halo px
+constexpr int W36_NP = W36_TH * W36_TW;                                                          // 288 px
+
+__global__ __launch_bounds__(256, 2) void wgrad3x3w36_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
+                                                             const bf16* __restrict__ dy1, const bf16* __restrict__ dy2,
+                                                             float* __restrict__ slab, ConvGeom g, int tiles_x,
+                                                             int ntiles) {
+  __shared__ __attribute__((aligned(16))) bf16 sdy[W36_NP * 64];     // 36 KB, 128-B rows
+  __shared__ __attribute__((aligned(16))) bf16 shx[W36_NPIX * 32];   // 23.75 KB, 64-B rows
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int cot0 = (wid >> 1) * 2, cit = wid & 1;
+  const int co0 = blockIdx.x * 64, ci0 = blockIdx.y * 32;
+  const int Cin = g.C1 + g.C2;
+  const bf16* xs; int xcs, xcc;
+  if (ci0 < g.C1) { xs = x1; xcs = g.C1; xcc = ci0; } else { xs = x2; xcs = g.C2; xcc = ci0 - g.C1; }
+  const bf16* ys; int ycs, ycc;
+  const int Co2 = g.Cout - g.Co1;
+  if (co0 < g.Co1) { ys = dy1; ycs = g.Co1; ycc = co0; } else { ys = dy2; ycs = Co2; ycc = co0 - g.Co1; }
+  const int tiles_per_img = tiles_x * ((g.Ho + W36_TH - 1) / W36_TH);
+
+  f32x4 acc[2][9];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int lr = lane & 15, lg = lane >> 4, q = lr >> 2, pp = lr & 3;
+  for (int tile = blockIdx.z; tile < ntiles; tile += gridDim.z) {
+    const int n = tile / tiles_per_img;
+    const int rem = tile - n * tiles_per_img;
+    const int ty = rem / tiles_x, tx = rem - ty * tiles_x;
+    const int y0 = ty * W36_TH, x0 = tx * W36_TW;
+    __syncthreads();
+    {
+      bf16x8 yv[9], hv[6];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {       // dY: 288 px x 8 vectors
+        const int e = tid + k * 256;
+        const int p = e >> 3, part = e & 7;
+        const int oy = y0 + p / W36_TW, ox = x0 + (p - (p / W36_TW) * W36_TW);
+        bf16x8 v = {};
+        if (oy < g.Ho && ox < g.Wo)
+          v = *reinterpret_cast<const bf16x8*>(ys + (((int64_t)n * g.Ho + oy) * g.Wo + ox) * ycs + ycc + part * 8);
+        yv[k] = v;
+      }
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {       // halo: 380 px x 4 vectors
+        const int e = tid + k * 256;
+        bf16x8 v = {};
+        if (e < W36_NPIX * 4) {
+          const int hp = e >> 2, part = e & 3;
+          const int r = hp / W36_HW, c = hp - r * W36_HW;
+          const int iy = y0 - 1 + r, ix = x0 - 1 + c;
+          if ((unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi)
+            v = *reinterpret_cast<const bf16x8*>(xs + (((int64_t)n * g.Hi + iy) * g.Wi + ix) * xcs + xcc + part * 8);
+        }
+        hv[k] = v;
+      }
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const int e = tid + k * 256;
+        const int p = e >> 3, part = e & 7;
+        const int ch = (part * 2) ^ w3_swz_dy(p);
+        *reinterpret_cast<bf16x8*>(sdy + p * 64 + ch * 4) = yv[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const int e = tid + k * 256;
+        if (e < W36_NPIX * 4) {
+          const int hp = e >> 2, part = e & 3;
+          const int ch = (part * 2) ^ w3_swz_x(hp);
+          *reinterpret_cast<bf16x8*>(shx + hp * 32 + ch * 4) = hv[k];
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int kc = 0; kc < W36_NP / 32; ++kc) {
+      // A = dY^T (rows co, K = flat pixels kc*32 .. +31): tr reads
+      bf16x8 af[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const int r = kc * 32 + lg * 8 + half * 4 + q;
+          const int ch = ((cot0 + i) * 4 + pp) ^ w3_swz_dy(r);
+          const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(sdy + r * 64 + ch * 4));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) af[i][half * 4 + e] = __builtin_bit_cast(bf16, (short)v[e]);
+        }
+      }
+      // halo row of tap (0,0) for this lane's two 4-pixel groups
+      int hb[2];
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const int P = kc * 32 + lg * 8 + half * 4 + q;
+        hb[half] = (P / W36_TW) * W36_HW + (P - (P / W36_TW) * W36_TW);
+      }
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int ky = tap / 3, kx = tap - ky * 3;
+        bf16x8 bfr;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const int r = hb[half] + ky * W36_HW + kx;
+          const int ch = (cit * 4 + pp) ^ w3_swz_x(r);
+          const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(shx + r * 32 + ch * 4));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bfr[half * 4 + e] = __builtin_bit_cast(bf16, (short)v[e]);
+        }
+        acc[0][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bfr, acc[0][tap], 0, 0, 0);
+        acc[1][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bfr, acc[1][tap], 0, 0, 0);
+      }
+    }
+  }
+  const int K = 9 * Cin;
+  float* out = slab + (int64_t)blockIdx.z * g.Cout * K;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int ci = ci0 + cit * 16 + lr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + (cot0 + i) * 16 + lg * 4 + r;
+        out[(int64_t)co * K + tap * Cin + ci] = acc[i][tap][r];
+      }
+    }
+}
+
 // sum slabs over splits (fixed order) and scatter into the PyTorch weight layout
 // dst[((d0*D1 + d1)*KH + kyt)*KW + kxt], with (d0,d1) = swap ? (ci,co) : (co,ci) and
 // (kyt,kxt) = flip ? (KH-1-ky, KW-1-kx) : (ky,kx).
@@ -2217,7 +2352,16 @@ int cesm_conv_wgrad(int dtype, const void* x1, const void* x2, const void* dy1, 
   dim3 grid(Cout / 64, K / 64, nsplit);
   const bool halo3 = dtype == CESM_DT_BF16 && KH == 3 && KW == 3 && S == 1 && P == 1 && U == 1 && Ho == Hi &&
                      Wo == Wi && !getenv_flag("CESM_NO_HALO");
-  if (halo3) {
+  // 8 x 36 tiles only where 32-wide tiles waste >= 20 % of the columns (W = 36, 72); at W = 144 / 288
+  // the 8 x 32 kernel's row-aligned K chunks are faster despite the partial last tile
+  if (halo3 && (Wo % W36_TW) == 0 && 5 * Wo <= 4 * (int)cdiv(Wo, W3_TW) * W3_TW && !getenv_flag("CESM_NO_WGRAD36")) {
+    const int tx = Wo / W36_TW;
+    const int ntiles = Nb * tx * (int)cdiv(Ho, W36_TH);
+    dim3 g3(Cout / 64, Cin / 32, std::min(nsplit, ntiles));
+    wgrad3x3w36_kernel<<<g3, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
+                                               (const bf16*)dy2, slab, g, tx, ntiles);
+    nsplit = (int)g3.z;
+  } else if (halo3) {
     const int tx = (int)cdiv(Wo, W3_TW);
     const int ntiles = Nb * tx * (int)cdiv(Ho, W3_TH);
     dim3 g3(Cout / 64, Cin / 32, std::min(nsplit, ntiles));

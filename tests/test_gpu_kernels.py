@@ -104,6 +104,35 @@ def test_conv_fwd_bwd(dev, cdt, case):
     assert rel(mod_dev.bias.grad, br2.grad) < TOL[cdt]
 
 
+@pytest.mark.parametrize("H,W,cin,cout", [(12, 72, 64, 64), (8, 36, 128, 64), (6, 36, 64, 128)])
+def test_conv3x3_tile_shapes_bf16(dev, H, W, cin, cout):
+    """widths that are multiples of 36 take the 36-wide halo tiles (fwd/dgrad) and the 8 x 36 weight-
+    gradient tiles; heights that are not tile multiples leave partial tile rows"""
+    torch.manual_seed(3)
+    cdt = torch.bfloat16
+    B, Fr = 2, 2
+    mod = nn.Conv3d(cin, cout, (1, 3, 3), (1, 1, 1), (0, 1, 1))
+    mod_dev = nn.Conv3d(cin, cout, (1, 3, 3), (1, 1, 1), (0, 1, 1)).to(dev)
+    mod_dev.load_state_dict(mod.state_dict())
+    x = torch.randn(B, cin, Fr, H, W)
+    rc = make_rc(B, Fr, cdt)
+    spec = VN.ConvSpec(mod_dev)
+    y, st = VN.conv_forward(rc, spec, to_cl(x).to(dev, cdt))
+    xr = q(x, cdt).requires_grad_(True)
+    wr = mod.weight.detach().to(cdt).double().requires_grad_(True)
+    br = mod.bias.detach().double().requires_grad_(True)
+    yr = F.conv3d(xr, wr, br, 1, (0, 1, 1))
+    assert rel(from_cl(y, B), yr) < TOL[cdt]
+    g = torch.randn_like(yr)
+    gq = q(g, cdt)
+    yr.backward(gq)
+    dx = VN.conv_backward(rc, spec, st, to_cl(g.float()).to(dev, cdt), True)
+    torch.cuda.synchronize()
+    assert rel(from_cl(dx, B), xr.grad) < TOL[cdt]
+    assert rel(mod_dev.weight.grad, wr.grad) < TOL[cdt]
+    assert rel(mod_dev.bias.grad, br.grad) < TOL[cdt]
+
+
 @pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
 def test_conv_concat_split_and_residual(dev, cdt):
     """two-source input (torch.cat fused into the loader), split dgrad + fused residual grads"""
