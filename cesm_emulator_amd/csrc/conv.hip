@@ -1849,6 +1849,27 @@ __global__ void conv_pack_kernel(const float* __restrict__ src, T* __restrict__ 
   }
 }
 
+// batched repack after an optimizer step: job j = int64[8] {src, dst, Cout, Cin, KH, KW, swap, flip};
+// blockIdx.y = job, grid-stride over its elements in x (one launch for every cached pack)
+template <typename T>
+__global__ void conv_pack_batch_kernel(const int64_t* __restrict__ jobs) {
+  const int64_t* jb = jobs + (int64_t)blockIdx.y * 8;
+  const float* src = reinterpret_cast<const float*>(jb[0]);
+  T* dst = reinterpret_cast<T*>(jb[1]);
+  const int Cout = (int)jb[2], Cin = (int)jb[3], KH = (int)jb[4], KW = (int)jb[5], swap = (int)jb[6], flip = (int)jb[7];
+  const int64_t K = (int64_t)KH * KW * Cin;
+  const int64_t total = (int64_t)Cout * K;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int co = (int)(e / K);
+    const int kc = (int)(e - (int64_t)co * K);
+    const int tap = kc / Cin, ci = kc - tap * Cin;
+    int ky = tap / KW, kx = tap - ky * KW;
+    if (flip) { ky = KH - 1 - ky; kx = KW - 1 - kx; }
+    const int d0 = swap ? ci : co, d1 = swap ? co : ci, D1 = swap ? Cout : Cin;
+    dst[e] = from_f<T>(src[(((int64_t)d0 * D1 + d1) * KH + ky) * KW + kx]);
+  }
+}
+
 // per-channel column sum over rows of a channels-last matrix: partial[split][c]
 template <typename T>
 __global__ void colsum_partial_kernel(const T* __restrict__ x, float* __restrict__ part, int64_t rows, int C,
@@ -2403,6 +2424,18 @@ int cesm_conv_pack(int dtype, const float* w, void* wp, int Cout, int Cin, int K
     conv_pack_kernel<bf16><<<grid, 256, 0, stream>>>(w, (bf16*)wp, Cout, Cin, KH, KW, swap, flip);
   else if (dtype == CESM_DT_F32)
     conv_pack_kernel<float><<<grid, 256, 0, stream>>>(w, (float*)wp, Cout, Cin, KH, KW, swap, flip);
+  else
+    return CESM_EINVAL;
+  return cesm_launch_status();
+}
+
+int cesm_conv_pack_batch(int dtype, const int64_t* jobs, int njobs, int blocks_per_job, hipStream_t stream) {
+  if (njobs <= 0) return CESM_OK;
+  dim3 grid((unsigned)std::max(1, blocks_per_job), (unsigned)njobs);
+  if (dtype == CESM_DT_BF16)
+    conv_pack_batch_kernel<bf16><<<grid, 256, 0, stream>>>(jobs);
+  else if (dtype == CESM_DT_F32)
+    conv_pack_batch_kernel<float><<<grid, 256, 0, stream>>>(jobs);
   else
     return CESM_EINVAL;
   return cesm_launch_status();

@@ -203,7 +203,8 @@ __global__ __launch_bounds__(256) void gn_bwd_reduce_kernel(const T* __restrict_
 // partials; S2 = rstd*(S3 - mean*S1) = sum da*xhat -> dss[b] (d scale | d shift), parameter
 // contributions pb[b][c] = ((1+scale)*S2, (1+scale)*S1, conv-bias sum dy), apply coefficients
 // E[b][0..2][c]:  dy = da*E1 + y*E2 + E3.  Groups (C/G <= 64 channels) never straddle blocks.
-__global__ __launch_bounds__(256) void gn_bwd_finalize_kernel(const float* __restrict__ part,
+constexpr int GNF_KG = 16;  // chunk groups of the bwd finalize (1024 threads: short partial-sum chains)
+__global__ __launch_bounds__(1024) void gn_bwd_finalize_kernel(const float* __restrict__ part,
                                                               const float* __restrict__ stats,
                                                               const float* __restrict__ gamma,
                                                               const float* __restrict__ beta,
@@ -213,13 +214,13 @@ __global__ __launch_bounds__(256) void gn_bwd_finalize_kernel(const float* __res
   const int b = blockIdx.x;
   const int cl = threadIdx.x & 63, kg = threadIdx.x >> 6;
   const int c = blockIdx.y * 64 + cl;
-  __shared__ float red[4][3][64];
+  __shared__ float red[GNF_KG][3][64];
   __shared__ float ga_[64], gb_[64];
   __shared__ float gA[64], gB[64];
   const int gsz = C / G;
   float s1 = 0.f, s3 = 0.f, sy = 0.f;
   if (c < C)
-    for (int k = kg; k < nchunk; k += 4) {
+    for (int k = kg; k < nchunk; k += GNF_KG) {
       const float* p = part + (((int64_t)b * nchunk + k) * C + c) * 3;
       s1 += p[0];
       s3 += p[1];
@@ -231,9 +232,13 @@ __global__ __launch_bounds__(256) void gn_bwd_finalize_kernel(const float* __res
   __syncthreads();
   float mean = 0.f, rstd = 0.f, sc = 1.f;
   if (kg == 0 && c < C) {
-    s1 = ((red[0][0][cl] + red[1][0][cl]) + red[2][0][cl]) + red[3][0][cl];
-    s3 = ((red[0][1][cl] + red[1][1][cl]) + red[2][1][cl]) + red[3][1][cl];
-    sy = ((red[0][2][cl] + red[1][2][cl]) + red[2][2][cl]) + red[3][2][cl];
+    s1 = s3 = sy = 0.f;
+#pragma unroll
+    for (int k = 0; k < GNF_KG; ++k) {  // fixed order (deterministic)
+      s1 += red[k][0][cl];
+      s3 += red[k][1][cl];
+      sy += red[k][2][cl];
+    }
     const int g = c / gsz;
     mean = stats[(b * G + g) * 2];
     rstd = stats[(b * G + g) * 2 + 1];
@@ -387,7 +392,7 @@ int cesm_gn_bwd(int dtype, const void* dout, const void* y, const float* stats, 
     using T = std::remove_pointer_t<decltype(tp)>;
     gn_bwd_reduce_kernel<T><<<dim3(nchunk, B), 256, 0, stream>>>((const T*)dout, (const T*)y, coef, part, rows_b, C,
                                                                  nchunk);
-    gn_bwd_finalize_kernel<<<dim3(B, (unsigned)cdiv(C, 64)), 256, 0, stream>>>(part, stats, gamma, beta, ss, dss, pb,
+    gn_bwd_finalize_kernel<<<dim3(B, (unsigned)cdiv(C, 64)), 64 * GNF_KG, 0, stream>>>(part, stats, gamma, beta, ss, dss, pb,
                                                                                E, C, G, nchunk, count, (float)rows_b);
     gn_bwd_apply_kernel<T><<<dim3(nch, B), 256, 0, stream>>>((const T*)dout, (const T*)y, coef, E, (T*)dy, rows_b, C,
                                                              nch);

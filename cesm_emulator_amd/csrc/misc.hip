@@ -53,20 +53,24 @@ __global__ void linear_small_fwd_kernel(const float* __restrict__ x, const float
 
 // dx[r][i] (+)= act'(x) * sum_o dy[r][o] W[o][i]
 // block = 4 waves x 64 lanes: lane <-> i (64 consecutive), wave <-> quarter of the o range
-__global__ void linear_small_dx_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                       const float* __restrict__ dy, float* __restrict__ dx, int R, int I, int O,
-                                       int silu_in, int accumulate) {
-  __shared__ float red[4][64];
+__global__ __launch_bounds__(256) void linear_small_dx_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                              const float* __restrict__ dy, float* __restrict__ dx,
+                                                              int R, int I, int O, int silu_in, int accumulate) {
+  // block = 16 inputs i x 16 slices of the O reduction (short dependent chains: O/16 FMAs per thread);
+  // the 16 i of a slice read 64 consecutive bytes of each W row
+  __shared__ float red[16][17];
   const int r = blockIdx.y;
-  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int wv = threadIdx.x >> 6;
+  const int il = threadIdx.x & 15, os = threadIdx.x >> 4;
+  const int i = blockIdx.x * 16 + il;
   float s = 0.f;
   if (i < I)
-    for (int o = wv; o < O; o += 4) s = fmaf(dy[(int64_t)r * O + o], w[(int64_t)o * I + i], s);
-  red[wv][threadIdx.x & 63] = s;
+    for (int o = os; o < O; o += 16) s = fmaf(dy[(int64_t)r * O + o], w[(int64_t)o * I + i], s);
+  red[os][il] = s;
   __syncthreads();
-  if (wv == 0 && i < I) {
-    s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+  if (os == 0 && i < I) {
+    s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[k][il];
     const int64_t t = (int64_t)r * I + i;
     if (silu_in) s *= dsilu_p(x[t]);
     dx[t] = accumulate ? dx[t] + s : s;
@@ -263,7 +267,7 @@ int cesm_linear_small_fwd(const float* x, const float* w, const float* bias, flo
 int cesm_linear_small_bwd(const float* x, const float* w, const float* dy, float* dx, float* dw, float* db, int R,
                           int I, int O, int silu_in, int accumulate_dx, int accumulate_w, hipStream_t stream) {
   if (dx)
-    linear_small_dx_kernel<<<dim3((unsigned)cdiv(I, 64), R), 256, 0, stream>>>(x, w, dy, dx, R, I, O, silu_in,
+    linear_small_dx_kernel<<<dim3((unsigned)cdiv(I, 16), R), 256, 0, stream>>>(x, w, dy, dx, R, I, O, silu_in,
                                                                                accumulate_dx);
   if (dw)
     linear_small_dw_kernel<<<(unsigned)cdiv((int64_t)O * I, 256), 256, 0, stream>>>(x, dy, dw, db, R, I, O, silu_in,

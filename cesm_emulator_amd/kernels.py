@@ -57,6 +57,18 @@ def conv_pack(w: torch.Tensor, dtype, cout, cin, kh, kw, swap, flip):
     return out
 
 
+def conv_pack_into(w, out, cout, cin, kh, kw, swap, flip):
+    """re-pack into an existing GEMM-layout buffer"""
+    _chk(w, dtype=torch.float32)
+    call("cesm_conv_pack", _DT[out.dtype], P(w), P(out), cout, cin, kh, kw, int(swap), int(flip), S())
+    return out
+
+
+def conv_pack_batch(jobs_dev, njobs, dtype, blocks_per_job=512):
+    """one launch re-packing every job of a device int64 [njobs, 8] table (see cesm_conv_pack_batch)"""
+    call("cesm_conv_pack_batch", _DT[dtype], P(jobs_dev), int(njobs), int(blocks_per_job), S())
+
+
 def conv_fwd(x1, x2, wp, bias, geom, res=None, res2=None, out_split=None):
     """geom = (Ho, Wo, Cout, KH, KW, S, P, U).  Returns y (or (y1, y2) when out_split=Co1)."""
     Ho, Wo, Cout, KH, KW, St, Pd, U = geom

@@ -459,6 +459,7 @@ class UNetModel3D(nn.Module):
         self.out_conv = nn.Sequential(ResnetBlock(model_dim * 2, model_dim, groups=resnet_groups),
                                       nn.Conv3d(model_dim, n_vars, 1))
         self._pack_cache = {}
+        self._pack_tables = {}  # dtype -> device int64 job table of the cached packs
         self._weights_epoch = 0
         self._tape = None
 
@@ -467,16 +468,44 @@ class UNetModel3D(nn.Module):
         """Called after any in-place parameter update made through raw pointers (optimizer)."""
         self._weights_epoch += 1
         self._pack_cache.clear()
+        self._pack_tables.clear()
 
     def _packed(self, w, cdt, cout, cin, kh, kw, swap, flip):
-        key = (w.data_ptr(), w._version, self._weights_epoch, _PARAM_EPOCH[0], cdt, cout, cin, kh, kw, swap, flip)
-        hit = self._pack_cache.get(key)
-        if hit is None:
-            if len(self._pack_cache) > 4096:
-                self._pack_cache.clear()
-            hit = K.conv_pack(w.detach().reshape(w.shape), cdt, cout, cin, kh, kw, swap, flip)
-            self._pack_cache[key] = hit
-        return hit
+        """GEMM-layout copy of conv weight w (cesm_conv_pack).  Packs persist across steps: after an
+        optimizer step (epoch change) the first request re-packs EVERY cached weight in one batched
+        launch (cesm_conv_pack_batch) instead of ~180 small ones."""
+        key = (w.data_ptr(), cdt, cout, cin, kh, kw, swap, flip)
+        ep = (self._weights_epoch, _PARAM_EPOCH[0])
+        e = self._pack_cache.get(key)
+        if e is not None and e.epoch == ep and e.version == w._version:
+            return e.out
+        if e is None:
+            out = K.conv_pack(w.detach().reshape(w.shape), cdt, cout, cin, kh, kw, swap, flip)
+            self._pack_cache[key] = SimpleNamespace(w=w, out=out, geo=(cout, cin, kh, kw, swap, flip), epoch=ep,
+                                                    version=w._version)
+            self._pack_tables.clear()
+            return out
+        if e.epoch != ep:
+            self._repack_all(ep)
+        if e.version != w._version:  # in-place update through torch (version counter), this weight only
+            K.conv_pack_into(w.detach(), e.out, *e.geo)
+            e.version = w._version
+        e.epoch = ep
+        return e.out
+
+    def _repack_all(self, ep):
+        for cdt in (torch.bfloat16, torch.float32):
+            ents = [e for e in self._pack_cache.values() if e.out.dtype == cdt]
+            if not ents:
+                continue
+            tab = self._pack_tables.get(cdt)
+            if tab is None:
+                rows = [[e.w.data_ptr(), e.out.data_ptr(), *e.geo] for e in ents]
+                tab = torch.tensor(rows, dtype=torch.int64).to(ents[0].out.device)
+                self._pack_tables[cdt] = tab
+            K.conv_pack_batch(tab, len(ents), cdt)
+            for e in ents:
+                e.epoch, e.version = ep, e.w._version
 
     # ---------------------------------------------------------------- executor
     def run_forward(self, x_t, cond, t, save):

@@ -46,6 +46,9 @@ int cesm_conv_wgrad(int dtype, const void* x1, const void* x2, const void* dy1, 
  * the torch tensor (transposed conv forward / conv dgrad); flip: taps reversed. */
 int cesm_conv_pack(int dtype, const float* w, void* wp, int Cout, int Cin, int KH, int KW, int swap, int flip,
                    hipStream_t stream);
+/* every cached pack of one dtype redone in ONE launch after an optimizer step: jobs = device
+ * int64[njobs][8] {src fp32 ptr, dst ptr, Cout, Cin, KH, KW, swap, flip} (cesm_conv_pack semantics). */
+int cesm_conv_pack_batch(int dtype, const int64_t* jobs, int njobs, int blocks_per_job, hipStream_t stream);
 /* dst[c] (+)= sum over rows of x[r][c]  (conv bias gradients) ; part: nsplit*C floats */
 int cesm_colsum(int dtype, const void* x, float* dst, float* part, int nsplit, int64_t rows, int C, int accumulate,
                 hipStream_t stream);
