@@ -206,7 +206,7 @@ def main():
                 "traffic_note": None if traffic is None else
                 f"HBM bytes/launch (PMC FETCH_SIZE+WRITE_SIZE, profiles/r1_conv3x3_traffic.json) vs "
                 f"{alg_bytes:.3g} algorithmic (input read + output write)",
-                "kernel": "conv3x3_bf16_kernel (level-0 3x3 conv 64->64, fwd+dgrad)" if a.dtype == "bf16" else
+                "kernel": "conv3x3p_kernel (level-0 3x3 conv 64->64, fwd+dgrad; persistent, resident weights)" if a.dtype == "bf16" else
                           "conv_fwd_kernel<float,64>", "launches": n, "avg_us": round(avg_ms * 1e3, 2),
                 "flop_per_launch": avg_flops}
     out = {

@@ -618,9 +618,13 @@ constexpr int CP_TH = 14;                             // max tile rows: (14 + 2)
 // ky step (+40 rows) keeps bits 0..2 of the row and with them the chunk swizzle: the B address of
 // (group j, ky, kx) = bad[j][kx] + ky * 40 * 64 -> immediate offsets, no per-read VALU.  Fragment reads
 // of tap t+1 are interleaved with tap t's MFMAs (sched_group_barrier: 1 ds_read, 2 MFMA, ...).
-template <int NG>
+struct NoHook {
+  __device__ __forceinline__ void operator()(int) const {}
+};
+
+template <int NG, typename Hook = NoHook>
 __device__ __forceinline__ void cp_taps(const char* sh, const char* sw, const int (&bad)[NG][3], int a_lane,
-                                        f32x4 (&acc)[4][NG]) {
+                                        f32x4 (&acc)[4][NG], const Hook& hook = Hook()) {
   bf16x8 af[2][4], bfr[2][NG];
   auto load = [&](int tap, int b) {
     const int ky = tap / 3, kx = tap - ky * 3;
@@ -634,6 +638,8 @@ __device__ __forceinline__ void cp_taps(const char* sh, const char* sw, const in
 #pragma unroll
   for (int tap = 0; tap < 9; ++tap) {
     const int b = tap & 1;
+    __builtin_amdgcn_sched_barrier(0);
+    hook(tap);  // e.g. this tap's share of the next step's LDS-DMA, spread over the MFMA phase
     __builtin_amdgcn_sched_barrier(0);
     if (tap + 1 < 9) load(tap + 1, b ^ 1);
 #pragma unroll
@@ -663,7 +669,7 @@ __device__ __forceinline__ void cp_taps(const char* sh, const char* sw, const in
 // bf16 in the stage just consumed and writes full 128-B pixel rows (+ residual) with exactly 2*NG
 // buffer stores per wave, so the next step waits for its DMA with vmcnt(2*NG), not for the stores.
 // ----------------------------------------------------------------------------------------
-template <int TW, int NG>
+template <int TW, int NG, bool RW>
 __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
                                                           const bf16* __restrict__ w, const float* __restrict__ bias,
                                                           const bf16* __restrict__ res, const bf16* __restrict__ res2,
@@ -672,9 +678,13 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
                                                           int dbg) {
   static_assert(TW + 2 <= CP_PITCH && 4 * 16 * NG >= CP_TH * TW - 16 * 4 && NG <= 8, "tile geometry");
   // one LDS array (a second __shared__ object can make hipcc drain the DMA before ds_reads):
-  // 2 stages | bias [Cout <= 1024] fp32
-  __shared__ __attribute__((aligned(1024))) char lds[2 * CP_STAGE + 4096];
-  float* sbias = reinterpret_cast<float*>(lds + 2 * CP_STAGE);
+  // 2 stages | [RW: resident weights, all chunks] | bias [Cout <= 1024] fp32.  RW (Cin = Cout = 64):
+  // a stage holds only the halo and the 2 x 36 KiB weight chunks are loaded once per block
+  constexpr int STG = RW ? CW_HROWS * 64 : CP_STAGE;
+  constexpr int WRES = RW ? 2 * CW_WROWS * 64 : 0;
+  __shared__ __attribute__((aligned(1024))) char lds[2 * STG + WRES + 4096];
+  char* wres = lds + 2 * STG;
+  float* sbias = reinterpret_cast<float*>(lds + 2 * STG + WRES);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const int HP = (TH + 2) * CP_PITCH;
@@ -714,43 +724,67 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
     y0 = ty * TH;
     x0 = (r - ty * tiles_x) * TW;
   };
-  auto issue = [&](int s) {
+  // LDS-DMA of step s, piece by piece: piece k < CW_HPW = halo piece, else (!RW) weight piece.
+  // Source descriptors of the step being prefetched (set by step_src):
+  __amdgpu_buffer_rsrc_t dxrs, dwrs;
+  int dcs = 0, dy0 = 0, dx0 = 0;
+  char* dsh = lds;
+  auto step_src = [&](int s) {
     const int it = (int)blockIdx.x + (s / nchunk) * (int)gridDim.x, ch = s % nchunk;
-    int n, y0, x0, cob;
-    item_geo(it, n, y0, x0, cob);
+    int n, cob;
+    item_geo(it, n, dy0, dx0, cob);
     const int c0 = ch * 32;
     const bf16* src;
-    int cs, cc;
-    if (c0 < g.C1) { src = x1; cs = g.C1; cc = c0; } else { src = x2; cs = g.C2; cc = c0 - g.C1; }
-    const int64_t img_elems = (int64_t)g.Hi * g.Wi * cs;
-    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(src + (int64_t)n * img_elems + cc), (short)0, (int)(img_elems * 2 - cc * 2), 0x00020000);
-    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(w + (int64_t)cob * 64 * 9 * Cin + c0), (short)0, 64 * 9 * Cin * 2 - c0 * 2, 0x00020000);
-    char* sh = lds + (s & 1) * CP_STAGE;
-    char* sw = sh + CW_HROWS * 64;
-#pragma unroll
-    for (int k = 0; k < CW_HPW; ++k) {
+    int cc;
+    if (c0 < g.C1) { src = x1; dcs = g.C1; cc = c0; } else { src = x2; dcs = g.C2; cc = c0 - g.C1; }
+    const int64_t img_elems = (int64_t)g.Hi * g.Wi * dcs;
+    dxrs = __builtin_amdgcn_make_buffer_rsrc((void*)(src + (int64_t)n * img_elems + cc), (short)0,
+                                             (int)(img_elems * 2 - cc * 2), 0x00020000);
+    dwrs = __builtin_amdgcn_make_buffer_rsrc((void*)(w + (int64_t)cob * 64 * 9 * Cin + c0), (short)0,
+                                             64 * 9 * Cin * 2 - c0 * 2, 0x00020000);
+    dsh = lds + (s & 1) * STG;
+  };
+  auto issue_piece = [&](int k) {
+    if (k < CW_HPW) {
       const int q = wid + 4 * k;
       if (q < hpieces) {  // wave-uniform
         const int chunk = pslot ^ cw_swz(16 * q + prow);
-        const int iy = y0 - 1 + (hrel[k] >> 16), ix = x0 - 1 + (hrel[k] & 0xffff);
+        const int iy = dy0 - 1 + (hrel[k] >> 16), ix = dx0 - 1 + (hrel[k] & 0xffff);
         const bool in = hrel[k] >= 0 && (unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi;
-        const int vo = in ? ((iy * g.Wi + ix) * cs + chunk * 8) * 2 : 0x7ffffff0;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)(sh + q * 1024), 16, vo,
-                                                 0, 0, 0);
+        const int vo = in ? ((iy * g.Wi + ix) * dcs + chunk * 8) * 2 : 0x7ffffff0;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(dxrs, (__attribute__((address_space(3))) void*)(dsh + q * 1024), 16,
+                                                 vo, 0, 0, 0);
       }
-    }
-#pragma unroll
-    for (int k = 0; k < CW_WPW; ++k) {
-      const int q = wid + 4 * k;
+    } else if constexpr (!RW) {
+      const int q = wid + 4 * (k - CW_HPW);
       const int row = 16 * q + prow;  // tap*64 + co
       const int chunk = pslot ^ cw_swz(row);
       const int vo = (((row & 63) * 9 + (row >> 6)) * Cin + chunk * 8) * 2;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(sw + q * 1024), 16, vo, 0,
-                                               0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(dwrs,
+                                               (__attribute__((address_space(3))) void*)(dsh + CW_HROWS * 64 + q * 1024),
+                                               16, vo, 0, 0, 0);
     }
   };
+  constexpr int NPIECE = RW ? CW_HPW : CW_HPW + CW_WPW;  // per wave per step
+  auto issue = [&](int s) {
+    step_src(s);
+#pragma unroll
+    for (int k = 0; k < NPIECE; ++k) issue_piece(k);
+  };
+  if constexpr (RW) {  // the whole (64 co x 9 taps x 64 ci) weight, chunk-major, waited for by step 0
+    const __amdgpu_buffer_rsrc_t wrs0 = __builtin_amdgcn_make_buffer_rsrc((void*)w, (short)0, 64 * 9 * 64 * 2, 0x00020000);
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+      for (int k = 0; k < CW_WPW; ++k) {
+        const int q = wid + 4 * k;
+        const int row = 16 * q + prow;
+        const int chunk = pslot ^ cw_swz(row);
+        const int vo = (((row & 63) * 9 + (row >> 6)) * 64 + ch * 32 + chunk * 8) * 2;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            wrs0, (__attribute__((address_space(3))) void*)(wres + ch * CW_WROWS * 64 + q * 1024), 16, vo, 0, 0, 0);
+      }
+  }
 
   if (nsteps > 0) issue(0);
   int s = 0;
@@ -771,9 +805,24 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
       }
       epi = false;
       __builtin_amdgcn_s_barrier();                     // ... for every wave; step s-1's reads are done
-      if (s + 1 < nsteps && !(dbg & 1)) issue(s + 1);     // into the stage step s-1 used
-      const char* sh = lds + (s & 1) * CP_STAGE;
-      if (!(dbg & 2)) cp_taps<NG>(sh, sh + CW_HROWS * 64, bad, a_lane, acc);
+      const char* sh = lds + (s & 1) * STG;
+      const char* sw = RW ? wres + ch * CW_WROWS * 64 : sh + CW_HROWS * 64;
+      const bool pf = s + 1 < nsteps && !(dbg & 1);
+      if ((dbg & 2) || !RW) {  // spreading the 19-piece (!RW) DMA over the taps spills at NG = 8
+        if (pf) issue(s + 1);
+      } else if (pf) {
+        // step s+1's DMA into the stage step s-1 used, spread over this step's taps (issuing all of it
+        // up front stalls the wave on the vector-memory queue before its first MFMA)
+        step_src(s + 1);
+        auto hook = [&](int tap) {
+#pragma unroll
+          for (int k = 0; k < NPIECE; ++k)
+            if (k * 9 / NPIECE == tap) issue_piece(k);
+        };
+        cp_taps<NG>(sh, sw, bad, a_lane, acc, hook);
+      } else {
+        cp_taps<NG>(sh, sw, bad, a_lane, acc);
+      }
     }
     int n, y0, x0, cob;
     item_geo((int)blockIdx.x + k * (int)gridDim.x, n, y0, x0, cob);
@@ -787,90 +836,62 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
       if (sacc == 12345.f) y1[0] = (bf16)sacc;
       continue;
     }
-    // epilogue through LDS: (acc + bias) -> bf16 tile [64*NG px][CP_ELD] in the stage just consumed
-    // (every wave is past its taps: barrier), then 8 lanes per pixel write full 128-B rows
+    // epilogue through LDS, wave-private, in rounds of up to 4 fragment groups (64 px): (acc + bias)
+    // -> bf16 rows [64 px][CP_ELD] in this wave's slice of the stage just consumed (barrier: every wave
+    // is past its taps), then 8 lanes per pixel write full 128-B rows with 16-B buffer stores (+
+    // residual read the same way); exactly 2*NG stores per wave (rows outside the image -> out-of-range
+    // offset, dropped) so the next step waits for its DMA with vmcnt(2*NG), not for these stores
     __builtin_amdgcn_s_barrier();
-    bf16* so = reinterpret_cast<bf16*>(lds + ((s - 1) & 1) * CP_STAGE);
+    bf16* so = reinterpret_cast<bf16*>(lds + ((s - 1) & 1) * STG) + wid * 64 * CP_ELD;
+    const bool first = n0 < g.Co1;
+    const int cstride = first ? g.Co1 : g.Cout - g.Co1;
+    const int cofs = (first ? n0 : n0 - g.Co1) + (lane & 7) * 8;
+    const int64_t img = (int64_t)n * g.Ho * g.Wo * cstride;
+    const int img_bytes = g.Ho * g.Wo * cstride * 2;
+    const __amdgpu_buffer_rsrc_t yrs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)((first ? y1 : y2) + img), (short)0, img_bytes, 0x00020000);
+    const bf16* rsrc = first ? res : res2;
+    const __amdgpu_buffer_rsrc_t rrs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)((rsrc ? rsrc : y1) + img), (short)0, img_bytes, 0x00020000);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int co = i * 16 + lg * 4;
-      const f32x4 bv = *reinterpret_cast<const f32x4*>(sbias + n0 + co);
+    for (int r0 = 0; r0 < NG; r0 += 4) {
+      constexpr int dummy = 0;
+      (void)dummy;
+      const int nj = NG - r0 < 4 ? NG - r0 : 4;
 #pragma unroll
-      for (int j = 0; j < NG; ++j) {
-        const int p = wid * 16 * NG + j * 16 + lr;
-        float v[4] = {acc[i][j][0] + bv[0], acc[i][j][1] + bv[1], acc[i][j][2] + bv[2], acc[i][j][3] + bv[3]};
-        store4(so + p * CP_ELD + co, v);
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    {
-      // the 64-channel block lies wholly in y1 or y2 (Co1 % 64 == 0); 32-bit offsets within image n.
-      // rows outside the image -> out-of-range buffer offset (store dropped), so the count is exact
-      const bool first = n0 < g.Co1;
-      const int cstride = first ? g.Co1 : g.Cout - g.Co1;
-      const int cofs = (first ? n0 : n0 - g.Co1) + (lane & 7) * 8;
-      const int64_t img = (int64_t)n * g.Ho * g.Wo * cstride;
-      const int img_bytes = g.Ho * g.Wo * cstride * 2;
-      const __amdgpu_buffer_rsrc_t yrs =
-          __builtin_amdgcn_make_buffer_rsrc((void*)((first ? y1 : y2) + img), (short)0, img_bytes, 0x00020000);
-      const bf16* rsrc = first ? res : res2;
-      auto row_off = [&](int it2, bool& ok) {
-        const int p = wid * 16 * NG + it2 * 8 + (lane >> 3);
-        const int oy = y0 + p / TW, ox = x0 + (p - (p / TW) * TW);
-        ok = p < TH * TW && oy < g.Ho && ox < g.Wo;
-        return (ok ? oy * g.Wo + ox : 0) * cstride + cofs;  // invalid rows read row 0, never store
-      };
-      auto tile_row = [&](int it2) {
-        return *reinterpret_cast<const bf16x8*>(so + (wid * 16 * NG + it2 * 8 + (lane >> 3)) * CP_ELD + (lane & 7) * 8);
-      };
-      if (rsrc) {
-        const __amdgpu_buffer_rsrc_t rrs =
-            __builtin_amdgcn_make_buffer_rsrc((void*)(rsrc + img), (short)0, img_bytes, 0x00020000);
+      for (int i = 0; i < 4; ++i) {
+        const int co = i * 16 + lg * 4;
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(sbias + n0 + co);
 #pragma unroll
-        for (int b2 = 0; b2 < NG / 2; ++b2) {
-          int off[4];
-          bool ok[4];
-          u32x4 rv[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            off[u] = row_off(b2 * 4 + u, ok[u]);
-            rv[u] = __builtin_amdgcn_raw_buffer_load_b128(rrs, off[u] * 2, 0, 0);
+        for (int jj = 0; jj < 4; ++jj) {
+          if (jj < nj) {
+            const int j = r0 + jj;
+            float v[4] = {acc[i][j][0] + bv[0], acc[i][j][1] + bv[1], acc[i][j][2] + bv[2], acc[i][j][3] + bv[3]};
+            store4(so + (jj * 16 + lr) * CP_ELD + co, v);
           }
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            bf16x8 v = tile_row(b2 * 4 + u);
-            const bf16x8 r = __builtin_bit_cast(bf16x8, rv[u]);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = (bf16)((float)v[e] + (float)r[e]);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yrs, ok[u] ? off[u] * 2 : 0x7ffffff0,
-                                                   0, 0);
-          }
-        }
-        if constexpr (NG % 2) {
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            bool ok;
-            const int off = row_off(2 * NG - 2 + u, ok);
-            const u32x4 rv = __builtin_amdgcn_raw_buffer_load_b128(rrs, off * 2, 0, 0);
-            bf16x8 v = tile_row(2 * NG - 2 + u);
-            const bf16x8 r = __builtin_bit_cast(bf16x8, rv);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = (bf16)((float)v[e] + (float)r[e]);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yrs, ok ? off * 2 : 0x7ffffff0, 0, 0);
-          }
-        }
-      } else {
-#pragma unroll
-        for (int it2 = 0; it2 < 2 * NG; ++it2) {
-          bool ok;
-          const int off = row_off(it2, ok);
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, tile_row(it2)), yrs, ok ? off * 2 : 0x7ffffff0,
-                                                 0, 0);
         }
       }
-      epi = true;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own writes visible to the wave's other lanes
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (u < 2 * nj) {
+          const int pl = u * 8 + (lane >> 3);  // row of the round
+          const int p = wid * 16 * NG + r0 * 16 + pl;
+          const int oy = y0 + p / TW, ox = x0 + (p - (p / TW) * TW);
+          const bool ok = p < TH * TW && oy < g.Ho && ox < g.Wo;
+          const int off = (ok ? oy * g.Wo + ox : 0) * cstride + cofs;
+          bf16x8 v = *reinterpret_cast<const bf16x8*>(so + pl * CP_ELD + (lane & 7) * 8);
+          if (rsrc) {
+            const bf16x8 rv = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rrs, off * 2, 0, 0));
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = (bf16)((float)v[e] + (float)rv[e]);
+          }
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yrs, ok ? off * 2 : 0x7ffffff0, 0, 0);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next round overwrites
     }
+    epi = true;
   }
 }
 
@@ -2263,7 +2284,10 @@ int cesm_conv_fwd(int dtype, const void* x1, const void* x2, const void* wp, con
                                                  (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, (int)M, C1,
                                                  C2, Cout, Co1);
     }
-  } else if (halo3 && getenv_flag("CESM_CONV3X3_V4") && Cout <= 1024) {
+  } else if (halo3 && Cout <= 1024 && !getenv_flag("CESM_CONV3X3_V1") &&
+             (getenv_flag("CESM_CONV3X3_V4") || ((C1 + C2) == 64 && Cout == 64 && (Wo % 32) == 0))) {
+    // v4 (persistent, resident weights) for the level-0 64 -> 64 convs by default;
+    // CESM_CONV3X3_V4=1 forces it for every 3x3 conv, CESM_CONV3X3_V1=1 disables it
     const int dbg = (getenv_flag("CESM_DBG_NODMA") ? 1 : 0) | (getenv_flag("CESM_DBG_NOMFMA") ? 2 : 0) |
                     (getenv_flag("CESM_DBG_NOEPI") ? 4 : 0);
     // TW = 32 -> TH = 14 (448 px = 4 waves x 7 groups); TW = 36 -> TH <= 14 (<= 504 px, 8 groups)
@@ -2281,14 +2305,23 @@ int cesm_conv_fwd(int dtype, const void* x1, const void* x2, const void* wp, con
     const int ncob = Cout / 64;
     const int nitems = Nb * tx * ty * ncob;
     const int nblk = std::min(nitems, cesm_num_cus());
-    if (w36)
-      conv3x3p_kernel<36, 8><<<nblk, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
-                                                       (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, tx,
-                                                       tx * ty, TH, ncob, nitems, dbg);
+    const bool rw = (C1 + C2) == 64 && Cout == 64 && !getenv_flag("CESM_NO_RESIDENT_W");
+    if (w36 && rw)
+      conv3x3p_kernel<36, 8, true><<<nblk, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
+                                                             (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g,
+                                                             tx, tx * ty, TH, ncob, nitems, dbg);
+    else if (w36)
+      conv3x3p_kernel<36, 8, false><<<nblk, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
+                                                              (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2,
+                                                              g, tx, tx * ty, TH, ncob, nitems, dbg);
+    else if (rw)
+      conv3x3p_kernel<32, 7, true><<<nblk, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
+                                                             (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g,
+                                                             tx, tx * ty, TH, ncob, nitems, dbg);
     else
-      conv3x3p_kernel<32, 7><<<nblk, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
-                                                       (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, tx,
-                                                       tx * ty, TH, ncob, nitems, dbg);
+      conv3x3p_kernel<32, 7, false><<<nblk, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
+                                                              (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2,
+                                                              g, tx, tx * ty, TH, ncob, nitems, dbg);
   } else if (halo3 && getenv_flag("CESM_CONV3X3_V3")) {
     int TH = 16, TW = 32;
     cw_tile(Ho, Wo, TH, TW);

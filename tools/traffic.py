@@ -12,7 +12,7 @@ import re
 import sqlite3
 import sys
 
-KERNEL = "conv3x3"
+KERNEL = "conv3x3"  # matches conv3x3p_kernel (default level-0 path) and conv3x3_bf16_kernel
 COPY_BYTES = 48 * 192 * 288 * 64 * 2
 
 
