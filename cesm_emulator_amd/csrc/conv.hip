@@ -669,27 +669,32 @@ __device__ __forceinline__ void cp_taps(const char* sh, const char* sw, const in
 // bf16 in the stage just consumed and writes full 128-B pixel rows (+ residual) with exactly 2*NG
 // buffer stores per wave, so the next step waits for its DMA with vmcnt(2*NG), not for the stores.
 // ----------------------------------------------------------------------------------------
-template <int TW, int NG, bool RW>
+template <int TW, int NG, bool RW, int NST = 2, int HPW = CW_HPW>
 __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
                                                           const bf16* __restrict__ w, const float* __restrict__ bias,
                                                           const bf16* __restrict__ res, const bf16* __restrict__ res2,
                                                           bf16* __restrict__ y1, bf16* __restrict__ y2, ConvGeom g,
                                                           int tiles_x, int tiles_per_img, int TH, int ncob, int nitems,
                                                           int dbg) {
-  static_assert(TW + 2 <= CP_PITCH && 4 * 16 * NG >= CP_TH * TW - 16 * 4 && NG <= 8, "tile geometry");
+  static_assert(TW + 2 <= CP_PITCH && NG <= 8 && HPW <= CW_HPW, "tile geometry");
+  static_assert(NST == 2 || (NST == 3 && RW), "3 stages only with resident weights");
   // one LDS array (a second __shared__ object can make hipcc drain the DMA before ds_reads):
   // 2 stages | [RW: resident weights, all chunks] | bias [Cout <= 1024] fp32.  RW (Cin = Cout = 64):
   // a stage holds only the halo and the 2 x 36 KiB weight chunks are loaded once per block
-  constexpr int STG = RW ? CW_HROWS * 64 : CP_STAGE;
+  // NST = 3 (RW, short tiles): every wave issues exactly HPW halo pieces per step (rows past the halo
+  // load zeros) so the step-start wait can leave the next step's pieces and the epilogue stores in
+  // flight: vmcnt(HPW + 2*NG)
+  constexpr int STG = RW ? HPW * 4 * 1024 : CP_STAGE;
   constexpr int WRES = RW ? 2 * CW_WROWS * 64 : 0;
-  __shared__ __attribute__((aligned(1024))) char lds[2 * STG + WRES + 4096];
-  char* wres = lds + 2 * STG;
-  float* sbias = reinterpret_cast<float*>(lds + 2 * STG + WRES);
+  constexpr int BIASB = RW ? 256 : 4096;
+  __shared__ __attribute__((aligned(1024))) char lds[NST * STG + WRES + BIASB];
+  char* wres = lds + NST * STG;
+  float* sbias = reinterpret_cast<float*>(lds + NST * STG + WRES);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const int HP = (TH + 2) * CP_PITCH;
   for (int c = tid; c < g.Cout; c += 256) sbias[c] = bias ? bias[c] : 0.f;
-  const int hpieces = (HP + 15) >> 4;
+  const int hpieces = NST == 3 ? 4 * HPW : (HP + 15) >> 4;
   const int Cin = g.C1 + g.C2;
   const int nchunk = Cin / 32;
   const int prow = lane >> 2, pslot = lane & 3;
@@ -697,9 +702,9 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
   const int nsteps = nmine * nchunk;
 
   // per-lane halo row -> tile-relative (hy, hx) of piece k (item independent); -1: zero row
-  int hrel[CW_HPW];
+  int hrel[HPW];
 #pragma unroll
-  for (int k = 0; k < CW_HPW; ++k) {
+  for (int k = 0; k < HPW; ++k) {
     const int row = 16 * (wid + 4 * k) + prow;
     const int hy = row / CP_PITCH, hx = row - (row / CP_PITCH) * CP_PITCH;
     hrel[k] = (row < HP && hx < TW + 2) ? (hy << 16) | hx : -1;
@@ -742,10 +747,10 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
                                              (int)(img_elems * 2 - cc * 2), 0x00020000);
     dwrs = __builtin_amdgcn_make_buffer_rsrc((void*)(w + (int64_t)cob * 64 * 9 * Cin + c0), (short)0,
                                              64 * 9 * Cin * 2 - c0 * 2, 0x00020000);
-    dsh = lds + (s & 1) * STG;
+    dsh = lds + (s % NST) * STG;
   };
   auto issue_piece = [&](int k) {
-    if (k < CW_HPW) {
+    if (k < HPW) {
       const int q = wid + 4 * k;
       if (q < hpieces) {  // wave-uniform
         const int chunk = pslot ^ cw_swz(16 * q + prow);
@@ -756,7 +761,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
                                                  vo, 0, 0, 0);
       }
     } else if constexpr (!RW) {
-      const int q = wid + 4 * (k - CW_HPW);
+      const int q = wid + 4 * (k - HPW);
       const int row = 16 * q + prow;  // tap*64 + co
       const int chunk = pslot ^ cw_swz(row);
       const int vo = (((row & 63) * 9 + (row >> 6)) * Cin + chunk * 8) * 2;
@@ -765,7 +770,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
                                                16, vo, 0, 0, 0);
     }
   };
-  constexpr int NPIECE = RW ? CW_HPW : CW_HPW + CW_WPW;  // per wave per step
+  constexpr int NPIECE = RW ? HPW : HPW + CW_WPW;  // per wave per step
   auto issue = [&](int s) {
     step_src(s);
 #pragma unroll
@@ -786,7 +791,9 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
       }
   }
 
-  if (nsteps > 0) issue(0);
+#pragma unroll
+  for (int q = 0; q < NST - 1; ++q)
+    if (q < nsteps) issue(q);
   int s = 0;
   bool epi = false;
   for (int k = 0; k < nmine; ++k) {
@@ -797,7 +804,13 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
       for (int j = 0; j < NG; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int ch = 0; ch < nchunk; ++ch, ++s) {
       // step s landed: after an epilogue only its 2*NG stores are younger than step s's DMA
-      if (epi) {
+      if constexpr (NST == 3) {
+        // steady state (nchunk == 2): younger than step s's DMA are step s+1's HPW pieces and one
+        // epilogue's 2*NG stores; the first two and the last two steps drain completely
+        static_assert(HPW + 2 * NG == 15, "vmcnt immediate below");
+        if (s >= 2 && s + 1 < nsteps && nchunk == 2) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else if (epi) {
         if constexpr (NG == 8) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
       } else {
@@ -805,15 +818,17 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
       }
       epi = false;
       __builtin_amdgcn_s_barrier();                     // ... for every wave; step s-1's reads are done
-      const char* sh = lds + (s & 1) * STG;
+      const char* sh = lds + (s % NST) * STG;
       const char* sw = RW ? wres + ch * CW_WROWS * 64 : sh + CW_HROWS * 64;
-      const bool pf = s + 1 < nsteps && !(dbg & 1);
+      const int sp = s + NST - 1;  // step prefetched now, into the stage step s-1 used
+      const bool pf = sp < nsteps && !(dbg & 1);
       if ((dbg & 2) || !RW) {  // spreading the 19-piece (!RW) DMA over the taps spills at NG = 8
-        if (pf) issue(s + 1);
+        if (pf) issue(sp);
+        if (!(dbg & 2)) cp_taps<NG>(sh, sw, bad, a_lane, acc);
       } else if (pf) {
-        // step s+1's DMA into the stage step s-1 used, spread over this step's taps (issuing all of it
-        // up front stalls the wave on the vector-memory queue before its first MFMA)
-        step_src(s + 1);
+        // the prefetch DMA spread over this step's taps (issuing all of it up front stalls the wave on
+        // the vector-memory queue before its first MFMA)
+        step_src(sp);
         auto hook = [&](int tap) {
 #pragma unroll
           for (int k = 0; k < NPIECE; ++k)
@@ -842,7 +857,8 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
     // residual read the same way); exactly 2*NG stores per wave (rows outside the image -> out-of-range
     // offset, dropped) so the next step waits for its DMA with vmcnt(2*NG), not for these stores
     __builtin_amdgcn_s_barrier();
-    bf16* so = reinterpret_cast<bf16*>(lds + ((s - 1) & 1) * STG) + wid * 64 * CP_ELD;
+    constexpr int RG = (4 * 16 * CP_ELD * 2 * 4 <= STG) ? 4 : 2;  // groups per epilogue round (fits the stage)
+    bf16* so = reinterpret_cast<bf16*>(lds + ((s - 1) % NST) * STG) + wid * RG * 16 * CP_ELD;
     const bool first = n0 < g.Co1;
     const int cstride = first ? g.Co1 : g.Cout - g.Co1;
     const int cofs = (first ? n0 : n0 - g.Co1) + (lane & 7) * 8;
@@ -854,16 +870,14 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
     const __amdgpu_buffer_rsrc_t rrs =
         __builtin_amdgcn_make_buffer_rsrc((void*)((rsrc ? rsrc : y1) + img), (short)0, img_bytes, 0x00020000);
 #pragma unroll
-    for (int r0 = 0; r0 < NG; r0 += 4) {
-      constexpr int dummy = 0;
-      (void)dummy;
-      const int nj = NG - r0 < 4 ? NG - r0 : 4;
+    for (int r0 = 0; r0 < NG; r0 += RG) {
+      const int nj = NG - r0 < RG ? NG - r0 : RG;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int co = i * 16 + lg * 4;
         const f32x4 bv = *reinterpret_cast<const f32x4*>(sbias + n0 + co);
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
+        for (int jj = 0; jj < RG; ++jj) {
           if (jj < nj) {
             const int j = r0 + jj;
             float v[4] = {acc[i][j][0] + bv[0], acc[i][j][1] + bv[1], acc[i][j][2] + bv[2], acc[i][j][3] + bv[3]};
@@ -873,7 +887,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own writes visible to the wave's other lanes
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < 2 * RG; ++u) {
         if (u < 2 * nj) {
           const int pl = u * 8 + (lane >> 3);  // row of the round
           const int p = wid * 16 * NG + r0 * 16 + pl;
@@ -2289,7 +2303,7 @@ int cesm_conv_fwd(int dtype, const void* x1, const void* x2, const void* wp, con
     // v4 (persistent, resident weights) for the level-0 64 -> 64 convs by default;
     // CESM_CONV3X3_V4=1 forces it for every 3x3 conv, CESM_CONV3X3_V1=1 disables it
     const int dbg = (getenv_flag("CESM_DBG_NODMA") ? 1 : 0) | (getenv_flag("CESM_DBG_NOMFMA") ? 2 : 0) |
-                    (getenv_flag("CESM_DBG_NOEPI") ? 4 : 0);
+                    (getenv_flag("CESM_DBG_NOEPI") ? 4 : 0) | (getenv_flag("CESM_DBG_CLOCK") ? 16 : 0);
     // TW = 32 -> TH = 14 (448 px = 4 waves x 7 groups); TW = 36 -> TH <= 14 (<= 504 px, 8 groups)
     const bool w36 = (Wo % 32) != 0 && (Wo % 36) == 0;
     const int TW = w36 ? 36 : 32;
@@ -2314,7 +2328,16 @@ int cesm_conv_fwd(int dtype, const void* x1, const void* x2, const void* wp, con
       conv3x3p_kernel<36, 8, false><<<nblk, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
                                                               (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2,
                                                               g, tx, tx * ty, TH, ncob, nitems, dbg);
-    else if (rw)
+    else if (rw && getenv_flag("CESM_CONV3X3_3STAGE")) {
+      // experimental: 8 x 32 tiles, 3 LDS stages (two steps of DMA in flight) - measured slower than
+      // 2 stages of 14 x 32 tiles (345 vs 315 us): the level-0 conv is HBM-bound (block-0 stamps: 2.2 GHz,
+      // DMA-only 175 us vs MFMA-only 166 us per launch), deeper prefetch does not add overlap
+      const int th8 = 8, ty8 = (int)cdiv(Ho, 8);
+      const int nit8 = Nb * tx * ty8;
+      conv3x3p_kernel<32, 4, true, 3, 7><<<std::min(nit8, cesm_num_cus()), 256, 0, stream>>>(
+          (const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias, (const bf16*)res, (const bf16*)res2, (bf16*)y1,
+          (bf16*)y2, g, tx, tx * ty8, th8, 1, nit8, dbg);
+    } else if (rw)
       conv3x3p_kernel<32, 7, true><<<nblk, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
                                                              (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g,
                                                              tx, tx * ty, TH, ncob, nitems, dbg);
