@@ -135,6 +135,30 @@ __device__ __forceinline__ float group_sum(float v, int width) {
 
 static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+namespace {
+// A-operand fragment image of a row-major bf16 matrix A[M][K] (M % 16 == 0, K % 32 == 0) for
+// v_mfma_f32_16x16x32_bf16: img[((mt * K/32 + kt) * 64 + lane) * 8 + e] = A[mt*16 + lane%16][kt*32 + (lane/16)*8 + e].
+// A wave's fragment load from the image is one contiguous 1-KiB line (vs 16 rows x 64 B from A itself):
+// half the vector-memory address work for the per-head weight reloads of slab_dx.
+__global__ void frag_image_kernel(const bf16* __restrict__ A, bf16* __restrict__ img, int M, int K) {
+  const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;  // 16-B vector of the image
+  if (v >= (int64_t)M * K / 8) return;
+  const int lane = (int)(v & 63);
+  const int64_t tile = v >> 6;
+  const int KT = K / 32;
+  const int kt = (int)(tile % KT), mt = (int)(tile / KT);
+  *reinterpret_cast<bf16x8*>(img + v * 8) =
+      *reinterpret_cast<const bf16x8*>(A + (int64_t)(mt * 16 + (lane & 15)) * K + kt * 32 + (lane >> 4) * 8);
+}
+__device__ __forceinline__ bf16x8 ld_img(const bf16* img, int mt, int KT, int kt, int lane) {
+  return *reinterpret_cast<const bf16x8*>(img + (((int64_t)mt * KT + kt) * 64 + lane) * 8);
+}
+
+static inline void frag_image(const void* A, void* img, int M, int K, hipStream_t stream) {
+  frag_image_kernel<<<(unsigned)cdiv((int64_t)M * K / 8, 256), 256, 0, stream>>>((const bf16*)A, (bf16*)img, M, K);
+}
+}  // namespace
+
 // host-side switch for A/B runs of kernel variants (read once per process)
 #include <cstdlib>
 #include <cstring>

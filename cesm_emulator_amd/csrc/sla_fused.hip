@@ -678,6 +678,14 @@ __global__ __launch_bounds__(256, 2) void slab_dx_kernel(
     for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
       for (int vt = 0; vt < NV; ++vt) dxacc[ct][vt] = z4;
+    // dy fragments, loaded once (not once per head)
+    bf16x8 dyr[NV][KS];
+#pragma unroll
+    for (int vt = 0; vt < NV; ++vt) {
+      const int p = p0 + vt * 16 + lr;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) dyr[vt][ks] = p < HW ? ld16(dy + (rb + p) * C + ks * 32 + lg * 8) : zero8();
+    }
 
     for (int h = 0; h < NH; ++h) {
       const int64_t fo = ((int64_t)(n * NH + h) * 2) * 64 * 8;
@@ -697,24 +705,20 @@ __global__ __launch_bounds__(256, 2) void slab_dx_kernel(
 #pragma unroll
         for (int r = 0; r < 4; ++r) { Kofs[0][r] = k0[r]; Kofs[1][r] = k1[r]; Gd[0][r] = g0[r]; Gd[1][r] = g1[r]; }
       }
-      bf16x8 wh[4][2][KS];  // this head's q, k, v rows of W_qkv and do rows of W_out^T
+      bf16x8 wh[4][2][KS];  // this head's q, k, v rows of W_qkv and do rows of W_out^T (fragment images)
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-          const int off = ks * 32 + lg * 8;
 #pragma unroll
-          for (int kind = 0; kind < 3; ++kind)
-            wh[kind][t][ks] = ld16(wqkv + (int64_t)(kind * INNER + h * DH + t * 16 + lr) * C + off);
-          wh[3][t][ks] = ld16(wout_t + (int64_t)(h * DH + t * 16 + lr) * C + off);
+          for (int kind = 0; kind < 3; ++kind) wh[kind][t][ks] = ld_img(wqkv, kind * 16 + h * 2 + t, KS, ks, lane);
+          wh[3][t][ks] = ld_img(wout_t, h * 2 + t, KS, ks, lane);
         }
 #pragma unroll
       for (int vt = 0; vt < NV; ++vt) {
         const int p = p0 + vt * 16 + lr;
         const bool ok = p < HW;
-        bf16x8 dyf[KS];
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) dyf[ks] = ok ? ld16(dy + (rb + p) * C + ks * 32 + lg * 8) : zero8();
+        const bf16x8 (&dyf)[KS] = dyr[vt];
         // q, k, v (rows d/e = t*16 + 4g + r, column pixel lr) and do
         float qv[2][4], kv[2][4], vv[2][4], dov[2][4];
 #pragma unroll
@@ -804,7 +808,7 @@ __global__ __launch_bounds__(256, 2) void slab_dx_kernel(
         for (int vt = 0; vt < NV; ++vt) bq[vt] = ld16(sq + (vt * 16 + lr) * DQLD + kind * 32 + lg * 8);
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
-          const bf16x8 a = ld16(wqkv_t + (int64_t)(ct * 16 + lr) * QKV + kind * INNER + h * DH + lg * 8);
+          const bf16x8 a = ld_img(wqkv_t, ct, QKV / 32, kind * 8 + h, lane);
 #pragma unroll
           for (int vt = 0; vt < NV; ++vt) dxacc[ct][vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq[vt], dxacc[ct][vt], 0, 0, 0);
         }
@@ -906,15 +910,21 @@ int cesm_slaf_nblk(int Nf, int HW) {
 int cesm_slaf_fwd(const void* x, const float* gamma, const void* wqkv, const void* wout, const float* bout, void* y,
                   float* mz, float* ctx32, void* actT, void* actx, float* ws, int Nf, int HW, int C, float scale,
                   float eps, hipStream_t stream) {
-  if (C != 64 || Nf < 1 || HW < 1) return CESM_EUNSUPPORTED;
+  if ((C != 64 && C != 128) || Nf < 1 || HW < 1) return CESM_EUNSUPPORTED;
   const int nsc = (HW + 63) / 64;
   const int nblk = cesm_slaf_nblk(Nf, HW);
   const int spb = (nsc + nblk - 1) / nblk;
-  slaf_stats_kernel<64><<<dim3(nblk, Nf), 512, 0, stream>>>((const bf16*)x, gamma, (const bf16*)wqkv, ws, HW, spb, eps);
+  if (C == 64)
+    slaf_stats_kernel<64><<<dim3(nblk, Nf), 512, 0, stream>>>((const bf16*)x, gamma, (const bf16*)wqkv, ws, HW, spb, eps);
+  else
+    slaf_stats_kernel<128><<<dim3(nblk, Nf), 512, 0, stream>>>((const bf16*)x, gamma, (const bf16*)wqkv, ws, HW, spb, eps);
   slaf_combine_kernel<<<Nf * NH, 256, 0, stream>>>(ws, nblk, mz, ctx32, (bf16*)actT, (bf16*)actx);
-  constexpr int NV = 4;
-  slaf_out_kernel<64, NV><<<dim3((unsigned)cdiv(HW, 64 * NV), Nf), 256, 0, stream>>>(
-      (const bf16*)x, gamma, (const bf16*)wqkv, (const bf16*)wout, bout, (const bf16*)actT, (bf16*)y, HW, scale, eps);
+  if (C == 64)
+    slaf_out_kernel<64, 4><<<dim3((unsigned)cdiv(HW, 64 * 4), Nf), 256, 0, stream>>>(
+        (const bf16*)x, gamma, (const bf16*)wqkv, (const bf16*)wout, bout, (const bf16*)actT, (bf16*)y, HW, scale, eps);
+  else
+    slaf_out_kernel<128, 2><<<dim3((unsigned)cdiv(HW, 64 * 2), Nf), 256, 0, stream>>>(
+        (const bf16*)x, gamma, (const bf16*)wqkv, (const bf16*)wout, bout, (const bf16*)actT, (bf16*)y, HW, scale, eps);
   return cesm_launch_status();
 }
 
@@ -925,26 +935,46 @@ int cesm_slaf_fwd(const void* x, const float* gamma, const void* wqkv, const voi
 int cesm_slaf_bwd(const void* x, const void* dy, const float* gamma, const void* wqkv, const void* wqkv_t,
                   const void* wout_t, const float* mz, const float* ctx32, const void* actT, const void* actx,
                   void* dx, void* dqkv, void* o, void* xn, float* dgamma, float* part, float* G, void* adc, void* adcT,
-                  float* dgp, int Nf, int HW, int C, float scale, float eps, int accumulate, hipStream_t stream) {
-  if (C != 64 || Nf < 1 || HW < 1) return CESM_EUNSUPPORTED;
+                  float* dgp, void* wimg, int Nf, int HW, int C, float scale, float eps, int accumulate,
+                  hipStream_t stream) {
+  if ((C != 64 && C != 128) || Nf < 1 || HW < 1) return CESM_EUNSUPPORTED;
+  // fragment images of W_qkv [768][C], W_qkv^T [C][768], W_out^T [256][C] for slab_dx
+  bf16* img_q = (bf16*)wimg;
+  bf16* img_qt = img_q + 768 * C;
+  bf16* img_ot = img_qt + 768 * C;
+  frag_image(wqkv, img_q, 768, C, stream);
+  frag_image(wqkv_t, img_qt, C, 768, stream);
+  frag_image(wout_t, img_ot, 256, C, stream);
   const int nsc = (HW + 63) / 64;
   const int nblk = cesm_slaf_nblk(Nf, HW);
   const int spb = (nsc + nblk - 1) / nblk;
-  slab_dctx_kernel<64><<<dim3(nblk, Nf), 512, 0, stream>>>((const bf16*)x, (const bf16*)dy, gamma, (const bf16*)wqkv,
-                                                           (const bf16*)wout_t, part, HW, spb, scale, eps);
+  if (C == 64)
+    slab_dctx_kernel<64><<<dim3(nblk, Nf), 512, 0, stream>>>((const bf16*)x, (const bf16*)dy, gamma, (const bf16*)wqkv,
+                                                             (const bf16*)wout_t, part, HW, spb, scale, eps);
+  else
+    slab_dctx_kernel<128><<<dim3(nblk, Nf), 512, 0, stream>>>((const bf16*)x, (const bf16*)dy, gamma,
+                                                              (const bf16*)wqkv, (const bf16*)wout_t, part, HW, spb,
+                                                              scale, eps);
   slab_combine_kernel<<<Nf * NH, 256, 0, stream>>>(part, nblk, ctx32, mz, G, (bf16*)adc, (bf16*)adcT);
-  constexpr int NV = 2;
-  dim3 grid((unsigned)cdiv(HW, 64 * NV), Nf);
-  const size_t sm = (size_t)64 * 4 + (size_t)4 * 16 * NV * DQLD * 2;
-  slab_dx_kernel<64, NV><<<grid, 256, sm, stream>>>(
-      (const bf16*)x, (const bf16*)dy, gamma, (const bf16*)wqkv, (const bf16*)wqkv_t, (const bf16*)wout_t, G,
-      (const bf16*)actT, (const bf16*)actx, (const bf16*)adc, (const bf16*)adcT, (bf16*)dx, (bf16*)dqkv, (bf16*)o,
-      (bf16*)xn, dgp, HW, scale, eps);
+  // NV = 16-pixel tiles per wave: 2 at C = 64, 1 at C = 128 (registers); dgp rows = grid blocks
+  const int NVr = C == 64 ? 2 : 1;
+  dim3 grid((unsigned)cdiv(HW, 64 * NVr), Nf);
+  const size_t sm = (size_t)C * 4 + (size_t)4 * 16 * NVr * DQLD * 2;
+  if (C == 64)
+    slab_dx_kernel<64, 2><<<grid, 256, sm, stream>>>(
+        (const bf16*)x, (const bf16*)dy, gamma, img_q, img_qt, img_ot, G,
+        (const bf16*)actT, (const bf16*)actx, (const bf16*)adc, (const bf16*)adcT, (bf16*)dx, (bf16*)dqkv, (bf16*)o,
+        (bf16*)xn, dgp, HW, scale, eps);
+  else
+    slab_dx_kernel<128, 1><<<grid, 256, sm, stream>>>(
+        (const bf16*)x, (const bf16*)dy, gamma, img_q, img_qt, img_ot, G,
+        (const bf16*)actT, (const bf16*)actx, (const bf16*)adc, (const bf16*)adcT, (bf16*)dx, (bf16*)dqkv, (bf16*)o,
+        (bf16*)xn, dgp, HW, scale, eps);
   if (dgamma) slaf_sum_rows_kernel<<<C, 256, 0, stream>>>(dgp, dgamma, (int)(grid.x * grid.y), C, accumulate);
   return cesm_launch_status();
 }
 
 // grid blocks of cesm_slaf_bwd's dx kernel (rows of its dgamma partial)
-int cesm_slaf_bwd_nblk(int Nf, int HW) { return (int)cdiv(HW, 128) * Nf; }
+int cesm_slaf_bwd_nblk(int Nf, int HW, int C) { return (int)cdiv(HW, C == 64 ? 128 : 64) * Nf; }
 
 }  // extern "C"

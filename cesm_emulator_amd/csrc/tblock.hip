@@ -690,11 +690,12 @@ __device__ __forceinline__ bool tw_row(int v, int VW, int F, int p0, int HW, int
 template <int C, int NV>
 __device__ __forceinline__ void tw_load_wq(bf16x8 (&a)[6][C / 32], const bf16* __restrict__ wqkv, int h, int lr,
                                            int lg) {
+  // wqkv = A-fragment image of W_qkv [768][C] (frag_image): 1-KiB line per fragment
 #pragma unroll
   for (int ct = 0; ct < 6; ++ct) {
-    const int wrow = (ct >> 1) * INNER + h * DH + (ct & 1) * 16 + lr;
+    const int mt = (ct >> 1) * 16 + h * 2 + (ct & 1);
 #pragma unroll
-    for (int ks = 0; ks < TW<C, NV>::KS; ++ks) a[ct][ks] = ld16(wqkv + (int64_t)wrow * C + ks * 32 + lg * 8);
+    for (int ks = 0; ks < TW<C, NV>::KS; ++ks) a[ct][ks] = ld_img(wqkv, mt, TW<C, NV>::KS, ks, lg * 16 + lr);
   }
 }
 
@@ -828,7 +829,7 @@ __global__ __launch_bounds__(256, 2) void tw_fwd_kernel(const bf16* __restrict__
   for (int h = 0; h < NH; ++h) {
     bf16x8 wo[T::CT];
 #pragma unroll
-    for (int ct = 0; ct < T::CT; ++ct) wo[ct] = ld16(wout + (int64_t)(ct * 16 + lr) * INNER + h * DH + lg * 8);
+    for (int ct = 0; ct < T::CT; ++ct) wo[ct] = ld_img(wout, ct, INNER / 32, h, lane);  // image of W_out [C][256]
     if constexpr (PREF) {
       tw_qkv_pre<C, NV>(wq, xf, fr, scale, rot, sq, sk, sv, lr, lg);
       if (h + 1 < NH) tw_load_wq<C, NV>(wq, wqkv, h + 1, lr, lg);  // in flight during the core
@@ -993,7 +994,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
       for (int dt = 0; dt < 2; ++dt) {
         bf16x8 a[T::KS];
 #pragma unroll
-        for (int ks = 0; ks < T::KS; ++ks) a[ks] = ld16(wout_t + (int64_t)(h * DH + dt * 16 + lr) * C + ks * 32 + lg * 8);
+        for (int ks = 0; ks < T::KS; ++ks) a[ks] = ld_img(wout_t, h * 2 + dt, T::KS, ks, lane);  // image of W_out^T
 #pragma unroll
         for (int vt = 0; vt < T::NVTM; ++vt) {
           if (vt < NVT) {
@@ -1126,7 +1127,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
         for (int vt = 0; vt < T::NVTM; ++vt) bf[vt] = vt < NVT ? ld16(src + (vt * 16 + lr) * HLD + lg * 8) : zero8();
 #pragma unroll
         for (int ct = 0; ct < T::CT; ++ct) {
-          const bf16x8 a = ld16(wqkv_t + (int64_t)(ct * 16 + lr) * QKV + kind * INNER + h * DH + lg * 8);
+          const bf16x8 a = ld_img(wqkv_t, ct, QKV / 32, kind * 8 + h, lane);  // image of W_qkv^T [C][768]
 #pragma unroll
           for (int vt = 0; vt < T::NVTM; ++vt)
             if (vt < NVT) dxacc[ct][vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bf[vt], dxacc[ct][vt], 0, 0, 0);
@@ -1319,9 +1320,17 @@ extern "C" {
 // wqkv [768][C] / wout [C][256] packed bf16, bias [8][F][F], rot [F][16][2].
 // mr [B*F*HW][2] (LN mean, rstd) and lse [B][8][HW][F] are saved for the backward (may be null).
 int cesm_tblock_fwd(const void* x, const float* gamma, const void* wqkv, const void* wout, const float* bias,
-                    const float* rot, void* y, float* mr, float* lse, int B, int F, int HW, int C, float scale,
-                    float eps, hipStream_t stream) {
+                    const float* rot, void* y, float* mr, float* lse, void* wimg, int B, int F, int HW, int C,
+                    float scale, float eps, hipStream_t stream) {
   if (F < 1 || F > 16) return CESM_EUNSUPPORTED;
+  if (C <= 256) {  // the wave-private kernels read weight fragments from images (1-KiB lines)
+    bf16* iq = (bf16*)wimg;
+    bf16* io = iq + 768 * C;
+    frag_image(wqkv, iq, 768, C, stream);
+    frag_image(wout, io, C, INNER, stream);
+    wqkv = iq;
+    wout = io;
+  }
   switch (C) {
     case 64: return tw_fwd_launch<64>(x, gamma, wqkv, wout, bias, rot, y, mr, lse, B, F, HW, scale, eps, stream);
     case 128: return tw_fwd_launch<128>(x, gamma, wqkv, wout, bias, rot, y, mr, lse, B, F, HW, scale, eps, stream);
@@ -1362,9 +1371,21 @@ int cesm_tblock_bwd_nblk(int B, int F, int HW, int C) {
 int cesm_tblock_bwd(const void* x, const void* dy, const float* gamma, const float* mr, const float* lse,
                     const void* wqkv, const void* wqkv_t, const void* wout_t, const float* bias, const float* rot,
                     void* dx, void* dqkv, void* o, void* xn, float* dbias_part, float* dgamma, float* dgamma_part,
-                    int nblk, int B, int F, int HW, int C, float scale, int accumulate, hipStream_t stream) {
+                    void* wimg, int nblk, int B, int F, int HW, int C, float scale, int accumulate,
+                    hipStream_t stream) {
   if (F < 1 || F > 16 || nblk < 1) return CESM_EUNSUPPORTED;
   dim3 grid(nblk, B);
+  if (C <= 256) {
+    bf16* iq = (bf16*)wimg;
+    bf16* iqt = iq + 768 * C;
+    bf16* iot = iqt + 768 * C;
+    frag_image(wqkv, iq, 768, C, stream);
+    frag_image(wqkv_t, iqt, C, QKV, stream);
+    frag_image(wout_t, iot, INNER, C, stream);
+    wqkv = iq;
+    wqkv_t = iqt;
+    wout_t = iot;
+  }
   switch (C) {
     case 64:
     case 128:

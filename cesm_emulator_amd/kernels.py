@@ -299,8 +299,9 @@ def tblock_fwd(x, gamma, wqkv, wout, bias, rot, B, F, scale, save=True, eps=1e-5
     y = empty(x.shape, x.dtype, x.device)
     mr = empty((Nb * H * W, 2), torch.float32, x.device) if save else None
     lse = empty((B, 8, H * W, F), torch.float32, x.device) if save else None
-    call("cesm_tblock_fwd", P(x), P(gamma), P(wqkv), P(wout), P(bias), P(rot), P(y), P(mr), P(lse), B, F, H * W, C,
-         float(scale), float(eps), S())
+    wimg = empty(((768 + 256) * C,), torch.bfloat16, x.device)  # weight fragment images (rebuilt per call)
+    call("cesm_tblock_fwd", P(x), P(gamma), P(wqkv), P(wout), P(bias), P(rot), P(y), P(mr), P(lse), P(wimg), B, F,
+         H * W, C, float(scale), float(eps), S())
     return y, mr, lse
 
 
@@ -328,15 +329,16 @@ def tblock_bwd(x, dy, gamma, mr, lse, wqkv, wqkv_t, wout_t, bias, rot, dgamma, d
     nblk = lib().cesm_tblock_bwd_nblk(B, F, HW, C)
     dbp = empty((B, 8, nblk, F, F), torch.float32, dev)
     dgp = empty((B * nblk, C), torch.float32, dev)
+    wimg = empty(((2 * 768 + 256) * C,), torch.bfloat16, dev)  # weight fragment images (rebuilt per call)
     call("cesm_tblock_bwd", P(x), P(dy), P(gamma), P(mr), P(lse), P(wqkv), P(wqkv_t), P(wout_t), P(bias), P(rot),
-         P(dx), P(dqkv), P(o), P(xn), P(dbp), P(dgamma), P(dgp), nblk, B, F, HW, C, float(scale), 1, S())
+         P(dx), P(dqkv), P(o), P(xn), P(dbp), P(dgamma), P(dgp), P(wimg), nblk, B, F, HW, C, float(scale), 1, S())
     if dtable is not None:
         ws = empty((8, F, F), torch.float32, dev)
         call("cesm_relpos_bwd", P(dbp), nblk, B, P(dtable), P(ws), F, 8, num_buckets, max_distance, 1, S())
     return dx, dqkv, o, xn
 
 
-SLAF_C = (64,)
+SLAF_C = (64, 128) if os.environ.get("CESM_SLAF_C128") else (64,)  # C=128 fused: slower (slab_dx spills)
 
 
 def slaf_fwd(x, gamma, wqkv, wout, bout, scale, eps=1e-5):
@@ -382,10 +384,11 @@ def slaf_bwd(x, dy, gamma, wqkv, wqkv_t, wout_t, state, dgamma, scale, want_wgra
     G = empty((Nf, 8, 64, 16), torch.float32, dev)  # per-lane k-softmax offsets + G image
     adc = empty((Nf, 8, 2, 64, 8), torch.bfloat16, dev)
     adcT = empty((Nf, 8, 2, 64, 8), torch.bfloat16, dev)
-    dgp = empty((lib().cesm_slaf_bwd_nblk(Nf, HW), C), torch.float32, dev)
+    dgp = empty((lib().cesm_slaf_bwd_nblk(Nf, HW, C), C), torch.float32, dev)
+    wimg = empty(((2 * 768 + 256) * C,), torch.bfloat16, dev)
     call("cesm_slaf_bwd", P(x), P(dy), P(gamma), P(wqkv), P(wqkv_t), P(wout_t), P(mz), P(ctx32), P(actT), P(actx),
-         P(dx), P(dqkv), P(o), P(xn), P(dgamma), P(part), P(G), P(adc), P(adcT), P(dgp), Nf, HW, C, float(scale),
-         float(eps), 1, S())
+         P(dx), P(dqkv), P(o), P(xn), P(dgamma), P(part), P(G), P(adc), P(adcT), P(dgp), P(wimg), Nf, HW, C,
+         float(scale), float(eps), 1, S())
     return dx, dqkv, o, xn
 
 

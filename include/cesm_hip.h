@@ -103,7 +103,7 @@ int cesm_tattn_bwd(int dtype, const void* qkv, const void* o, const void* dout, 
  * [B*F*HW][C], wqkv [768][C], wout [C][256] packed bf16; saves mr [B*F*HW][2] and lse [B][8][HW][F].
  * F <= 16, C in {64,128,256,512}. */
 int cesm_tblock_fwd(const void* x, const float* gamma, const void* wqkv, const void* wout, const float* bias,
-                    const float* rot, void* y, float* mr, float* lse, int B, int F, int HW, int C, float scale,
+                    const float* rot, void* y, float* mr, float* lse, void* wimg, int B, int F, int HW, int C, float scale,
                     float eps, hipStream_t stream);
 /* Fused temporal-attention block backward, dx path (bf16): recomputes LN/QKV/RoPE/softmax from mr and
  * lse, dO = dy.W_out, MFMA core backward, dxn = dqkv.W_qkv, LN backward + residual -> dx.  Emits
@@ -113,7 +113,7 @@ int cesm_tblock_fwd(const void* x, const float* gamma, const void* wqkv, const v
 int cesm_tblock_bwd_nblk(int B, int F, int HW, int C);
 int cesm_tblock_bwd(const void* x, const void* dy, const float* gamma, const float* mr, const float* lse,
                     const void* wqkv, const void* wqkv_t, const void* wout_t, const float* bias, const float* rot,
-                    void* dx, void* dqkv, void* o, void* xn, float* dbias_part, float* dgamma, float* dgamma_part,
+                    void* dx, void* dqkv, void* o, void* xn, float* dbias_part, float* dgamma, float* dgamma_part, void* wimg,
                     int nblk, int B, int F, int HW, int C, float scale, int accumulate, hipStream_t stream);
 /* spatial linear attention core (video_net.py:335-345 between to_qkv and to_out) */
 int cesm_sla_nchunk(int HW);
@@ -135,12 +135,14 @@ int cesm_slaf_fwd(const void* x, const float* gamma, const void* wqkv, const voi
 /* Fused SLA block backward, dx path (bf16, C = 64): dctx partials -> combine (G_d = sum_e dctx ctx, dctx as
  * A fragments adc/adcT) -> dx (+ dy residual), dgamma (+)=; emits (nullable) dqkv [..][768], o [..][256],
  * xn [..][C] for the to_qkv / to_out weight gradients.  part: nblk*Nf*8*1024 floats, G: Nf*8*64*16 floats,
- * adc/adcT: Nf*8*2*64*8 bf16, dgp: cesm_slaf_bwd_nblk(Nf, HW)*C floats. */
+ * adc/adcT: Nf*8*2*64*8 bf16, dgp: cesm_slaf_bwd_nblk(Nf, HW, C)*C floats;
+ * wimg: (2*768 + 256)*C bf16 (fragment images of the three weights, rebuilt per call). */
 int cesm_slaf_bwd(const void* x, const void* dy, const float* gamma, const void* wqkv, const void* wqkv_t,
                   const void* wout_t, const float* mz, const float* ctx32, const void* actT, const void* actx,
                   void* dx, void* dqkv, void* o, void* xn, float* dgamma, float* part, float* G, void* adc, void* adcT,
-                  float* dgp, int Nf, int HW, int C, float scale, float eps, int accumulate, hipStream_t stream);
-int cesm_slaf_bwd_nblk(int Nf, int HW);
+                  float* dgp, void* wimg, int Nf, int HW, int C, float scale, float eps, int accumulate,
+                  hipStream_t stream);
+int cesm_slaf_bwd_nblk(int Nf, int HW, int C);
 
 /* ---- small ops, loss, optimizer, data (csrc/misc.hip) ------------------------------------- */
 /* SinusoidalPosEmb (video_net.py:101-113) */

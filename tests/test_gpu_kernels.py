@@ -554,12 +554,13 @@ def _sla_block_ref(res, C):
     return ref
 
 
+@pytest.mark.parametrize("C", [64, 128])
 @pytest.mark.parametrize("H,W", [(8, 8), (12, 20), (37, 29)])
-def test_fused_sla_forward(dev, H, W):
+def test_fused_sla_forward(dev, H, W, C):
     """cesm_slaf_fwd (LN + online-softmax context + output projection, no per-pixel intermediates)
     vs a float64 evaluation of the reference block on bf16-rounded inputs/weights"""
     torch.manual_seed(13)
-    B, Fr, C = 2, 3, 64
+    B, Fr = 2, 3
     res = _sla_block(C, dev)
     sla = res.fn.fn
     x = q(torch.randn(B, C, Fr, H, W), torch.bfloat16)
@@ -587,12 +588,13 @@ def test_fused_sla_forward(dev, H, W):
     assert err < 2e-2
 
 
+@pytest.mark.parametrize("C", [64, 128])
 @pytest.mark.parametrize("H,W", [(8, 8), (12, 20), (37, 29)])
-def test_fused_sla_backward(dev, H, W):
+def test_fused_sla_backward(dev, H, W, C):
     """cesm_slaf_bwd (+ weight gradients from its dqkv/o/xn outputs) vs float64 autograd through the
     reference SpatialLinearAttention block"""
     torch.manual_seed(14)
-    B, Fr, C = 2, 3, 64
+    B, Fr = 2, 3
     res = _sla_block(C, dev)
     sla = res.fn.fn
     x = q(torch.randn(B, C, Fr, H, W), torch.bfloat16)
