@@ -12,7 +12,10 @@ from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
 HEADER = PKG.parent / "include" / "cesm_hip.h"
-LIBPATH = PKG / "libcesm_hip.so"
+import os
+
+# CESM_HIP_LIB selects a diagnostic build (tools/build_diag.sh); default: the in-tree product library
+LIBPATH = Path(os.environ["CESM_HIP_LIB"]) if os.environ.get("CESM_HIP_LIB") else PKG / "libcesm_hip.so"
 
 _CTYPE = {"int": ctypes.c_int, "int64_t": ctypes.c_int64, "float": ctypes.c_float, "double": ctypes.c_double}
 

@@ -650,6 +650,26 @@ __device__ __forceinline__ float grp4_max(float v) {
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
+// Diagnostic phase stamps (build with -DCESM_TW_STAMPS only): per-wave cycle sums of the tw_bwd
+// phases, written to g_tw_stamps[wave][8] at kernel end.
+#ifdef CESM_TW_STAMPS
+__device__ unsigned long long g_tw_stamps[4096 * 8];
+__device__ __forceinline__ unsigned long long tw_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define TW_ST_DECL unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long st_t = tw_stamp();
+#define TW_ST(i) { const unsigned long long st_n = tw_stamp(); st_acc[i] += st_n - st_t; st_t = st_n; }
+#define TW_ST_FLUSH(w) { if ((threadIdx.x & 63) == 0) for (int i = 0; i < 8; ++i) g_tw_stamps[(w) * 8 + i] = st_acc[i]; }
+#else
+#define TW_ST_DECL
+#define TW_ST(i)
+#define TW_ST_FLUSH(w)
+#endif
+
 constexpr int RS = 36;  // RoPE table row stride (floats): 16-B aligned, spreads frames over banks
 constexpr float LOG2E = 1.4426950408889634f;
 
@@ -958,6 +978,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
 #pragma unroll
   for (int vt = 0; vt < NV; ++vt) fr[vt] = (vt * 16 + lr) % F;
 
+  TW_ST_DECL
   for (int pg = blockIdx.x * 4 + wid; pg < npg; pg += nw) {
     const int p0 = pg * T::PW;
     bf16x8 xf[T::NVTM][T::KS];
@@ -969,7 +990,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
       vrow[vt] = tw_row(vt * 16 + lr, VW, F, p0, HW, b, row) ? row : -1;
       if (vrow[vt] >= 0 && xn_out) {
 #pragma unroll
-        for (int ks = 0; ks < T::KS; ++ks) *reinterpret_cast<bf16x8*>(xn_out + row * C + ks * 32 + lg * 8) = xf[vt][ks];
+        for (int ks = 0; ks < T::KS; ++ks) stnt16(xn_out + row * C + ks * 32 + lg * 8, xf[vt][ks]);
       }
     }
     f32x4 dxacc[T::CT][T::NVTM];
@@ -984,11 +1005,19 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
 #pragma unroll
       for (int vt = 0; vt < T::NVTM; ++vt)
 #pragma unroll
-        for (int ks = 0; ks < T::KS; ++ks) dyr[vt][ks] = vrow[vt] >= 0 ? ld16(dy + vrow[vt] * C + ks * 32 + lg * 8) : zero8();
+        for (int ks = 0; ks < T::KS; ++ks) dyr[vt][ks] = vrow[vt] >= 0 ? ldnt16(dy + vrow[vt] * C + ks * 32 + lg * 8) : zero8();
     }
 
+    TW_ST(0)
     for (int h = 0; h < NH; ++h) {
+      // issued ahead of the q/k/v GEMMs so its latency hides behind them: this head's log-sum-exp
+      // of the wave's pixels (one per frame row lr)
+      float Lp[T::PW];
+#pragma unroll
+      for (int pp = 0; pp < T::PW; ++pp)
+        Lp[pp] = (lr < F && p0 + pp < HW) ? lse[(((int64_t)b * NH + h) * HW + p0 + pp) * F + lr] : 0.f;
       tw_qkv<C, NV>(wqkv, xf, h, fr, scale, rot, sq, sk, sv, lr, lg);
+      TW_ST(1)
       // dO_h^T = W_out[:, h]^T . dy^T
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
@@ -1021,13 +1050,16 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
         brm[r] = ok ? sb[(h * F + c) * F + lr] : 0.f;
       }
       wave_lds_sync();
+      TW_ST(2)
       // core backward per pixel; dq/dk/dv overwrite the pixel's own q/k/v rows at the end
       float dbr[4] = {0.f, 0.f, 0.f, 0.f};
       for (int pp = 0; pp < T::PW; ++pp) {
         const int p = p0 + pp;
         if (p >= HW) break;
         const int rb = pp * F;
-        const float Li = lr < F ? lse[(((int64_t)b * NH + h) * HW + p) * F + lr] : 0.f;
+        float Li = Lp[0];
+#pragma unroll
+        for (int q = 1; q < T::PW; ++q) Li = pp == q ? Lp[q] : Li;
         const bf16x8 kr = lr < F ? ld16(sk + (rb + lr) * HLD + lg * 8) : zero8();
         const bf16x8 qr = lr < F ? ld16(sq + (rb + lr) * HLD + lg * 8) : zero8();
         const bf16x8 vr = lr < F ? ld16(sv + (rb + lr) * HLD + lg * 8) : zero8();
@@ -1066,7 +1098,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
           const f32x4 ot = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vg, pt_b, z4, 0, 0, 0);  // O^T[d][i]
           if (o_out && lr < F) {
             float oo[4] = {ot[0], ot[1], ot[2], ot[3]};
-            store4(o_out + (((int64_t)b * F + lr) * HW + p) * INNER + h * DH + half * 16 + lg * 4, oo);
+            stnt4(o_out + (((int64_t)b * F + lr) * HW + p) * INNER + h * DH + half * 16 + lg * 4, oo);
           }
         }
         // -- row-major orientation: lane (g, j): entries (i = 4g + r, j); L_i, D_i from lane i
@@ -1118,6 +1150,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
       for (int r = 0; r < 4; ++r)
         if (lr < F && lg * 4 + r < F) atomicAdd(&sdb[(h * F + lr) * F + lg * 4 + r], dbr[r]);
       wave_lds_sync();
+      TW_ST(3)
       // dxn^T += W_qkv[h rows]^T . [dq|dk|dv]_h^T ; emit dqkv_h
 #pragma unroll
       for (int kind = 0; kind < 3; ++kind) {
@@ -1138,11 +1171,12 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
             if (vt >= NVT) break;
             int64_t row = 0;
             if (tw_row(vt * 16 + lr, VW, F, p0, HW, b, row))
-              *reinterpret_cast<bf16x8*>(dqkv_out + row * QKV + kind * INNER + h * DH + lg * 8) = bf[vt];
+              stnt16(dqkv_out + row * QKV + kind * INNER + h * DH + lg * 8, bf[vt]);
           }
         }
       }
       wave_lds_sync();
+      TW_ST(4)
     }
     // LN backward: dx = rstd*(g - mean(g) - xhat*mean(g*xhat)) + dy, g = dxn*gamma
 #pragma unroll
@@ -1157,7 +1191,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
       for (int ct = 0; ct < T::CT; ++ct) {
         const int co = ct * 16 + lg * 4;
         float xv[4] = {0.f, 0.f, 0.f, 0.f};
-        if (ok) load4(x + row * C + co, xv);
+        if (ok) ldnt4(x + row * C + co, xv);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           xh[ct][r] = ok ? (xv[r] - mean) * rstd : 0.f;
@@ -1189,14 +1223,16 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
         }
         if (ok) {
           float dv[4], o4[4];
-          load4(dy + row * C + co, dv);
+          ldnt4(dy + row * C + co, dv);
 #pragma unroll
           for (int r = 0; r < 4; ++r) o4[r] = rstd * (dxacc[ct][vt][r] * gamma[co + r] - s1 - xh[ct][r] * s2) + dv[r];
-          store4(dx + row * C + co, o4);
+          stnt4(dx + row * C + co, o4);
         }
       }
     }
+    TW_ST(5)
   }
+  TW_ST_FLUSH(blockIdx.x * 4 + wid)
   if constexpr (DG_REG) {
 #pragma unroll
     for (int ct = 0; ct < T::CT; ++ct)
@@ -1313,6 +1349,11 @@ static int tw_bwd_launch(const void* x, const void* dy, const float* gamma, cons
 }
 
 }  // namespace
+#ifdef CESM_TW_STAMPS
+extern "C" int cesm_diag_tw_stamps(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tw_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -3;
+}
+#endif
 
 extern "C" {
 
