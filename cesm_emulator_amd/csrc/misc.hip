@@ -110,6 +110,26 @@ __global__ void q_sample_kernel(const float* __restrict__ x0, const float* __res
   }
 }
 
+// DDPM ancestral step (model.py:168-183), fused:
+//   x_{t-1} = r_t (x_t - (b_t / s1_t) eps) + sqrt(pv_t) z
+// with the reference's operation order and no contraction (agrees with the eager torch expression to
+// fp32 rounding).  pv_0 = 0 (alphas_cumprod_prev[0] = 1), so the t = 0 step adds no noise either way;
+// z == nullptr skips the noise term (the reference's `(t == 0).all()` branch).  out may alias x.
+__global__ void ddpm_step_kernel(const float* __restrict__ x, const float* __restrict__ eps,
+                                 const float* __restrict__ z, const int64_t* __restrict__ t,
+                                 const float* __restrict__ sra, const float* __restrict__ betas,
+                                 const float* __restrict__ s1a, const float* __restrict__ pv, float* out, int B,
+                                 int64_t HW) {
+  const int64_t n = (int64_t)B * HW;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t ti = t[e / HW];
+    const float c = __fdiv_rn(betas[ti], s1a[ti]);
+    float m = __fmul_rn(sra[ti], __fsub_rn(x[e], __fmul_rn(c, eps[e])));
+    if (z) m = __fadd_rn(m, __fmul_rn(__fsqrt_rn(pv[ti]), z[e]));
+    out[e] = m;
+  }
+}
+
 // loss partials: part[blk] = sum (pred - noise)^2
 __global__ void mse_partial_kernel(const float* __restrict__ pred, const float* __restrict__ tgt,
                                    float* __restrict__ part, int64_t n) {
@@ -279,6 +299,16 @@ int cesm_q_sample(const float* x0, const float* noise, const int64_t* t, const f
                   float* xt, int B, int64_t HW, hipStream_t stream) {
   const unsigned grid = (unsigned)std::min<int64_t>(cdiv((int64_t)B * HW, 256), 4096);
   q_sample_kernel<<<grid, 256, 0, stream>>>(x0, noise, t, sa, s1a, xt, B, HW);
+  return cesm_launch_status();
+}
+
+int cesm_ddpm_step(const float* x, const float* eps, const float* z, const int64_t* t, const float* sqrt_recip_alphas,
+                   const float* betas, const float* sqrt_one_minus_ac, const float* posterior_variance, float* out,
+                   int B, int64_t HW, hipStream_t stream) {
+  if (B < 1 || HW < 1) return CESM_EINVAL;
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv((int64_t)B * HW, 256), 4096);
+  ddpm_step_kernel<<<grid, 256, 0, stream>>>(x, eps, z, t, sqrt_recip_alphas, betas, sqrt_one_minus_ac,
+                                             posterior_variance, out, B, HW);
   return cesm_launch_status();
 }
 

@@ -209,41 +209,73 @@ __global__ __launch_bounds__(512) void slaf_stats_kernel(const bf16* __restrict_
 // A-fragment images (bf16, [n][h][tile][lane][8]):  actT rows e / k = d  (o = ctx^T q~),
 //                                                     actx rows d / k = e  (dq~ = ctx do).
 // ---------------------------------------------------------------------------------------------------
+constexpr int SLAF_NBLK_MAX = 128;  // partial blocks per frame (cesm_slaf_nblk caps it)
+
 __global__ __launch_bounds__(256) void slaf_combine_kernel(const float* __restrict__ part, int nblk,
                                                            float* __restrict__ mz, float* __restrict__ ctx32,
                                                            bf16* __restrict__ actT, bf16* __restrict__ actx) {
   __shared__ float sM[32], sZ[32];
+  __shared__ float red[8][33];
+  __shared__ __attribute__((aligned(16))) float sw[SLAF_NBLK_MAX][32];  // exp(m_b[d] - M[d])
   __shared__ float sc[32][33];  // [d][e]
   const int nh = blockIdx.x, n = nh / NH, h = nh % NH;
   const int tid = threadIdx.x;
   const float* pb = part + ((int64_t)n * nblk * NH + h) * (64 + 1024);
   const int64_t bstride = (int64_t)NH * (64 + 1024);
+  // M_d = max_b m_b[d], Z_d = sum_b exp(m_b[d] - M_d) s_b[d]: thread (d, slice of 8 over b)
+  const int d = tid & 31, sl = tid >> 5;
+  float M = -INFINITY;
+  for (int b = sl; b < nblk; b += 8) M = fmaxf(M, pb[b * bstride + d]);
+  red[sl][d] = M;
+  __syncthreads();
   if (tid < 32) {
-    float M = -INFINITY;
-    for (int b = 0; b < nblk; ++b) M = fmaxf(M, pb[b * bstride + tid]);
-    float Z = 0.f;
-    for (int b = 0; b < nblk; ++b) {
-      const float mb = pb[b * bstride + tid];
-      if (mb != -INFINITY) Z += expf(mb - M) * pb[b * bstride + 32 + tid];
-    }
-    sM[tid] = M;
-    sZ[tid] = Z;
-    mz[((int64_t)nh * 32 + tid) * 2] = M;
-    mz[((int64_t)nh * 32 + tid) * 2 + 1] = Z;
+    float m = red[0][tid];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) m = fmaxf(m, red[k][tid]);
+    sM[tid] = m;
   }
   __syncthreads();
+  M = sM[d];
+  float Z = 0.f;
+  for (int b = sl; b < nblk; b += 8) {
+    const float mb = pb[b * bstride + d];
+    const float w = mb == -INFINITY ? 0.f : expf(mb - M);
+    sw[b][d] = w;
+    Z = fmaf(w, pb[b * bstride + 32 + d], Z);
+  }
+  __syncthreads();
+  red[sl][d] = Z;
+  __syncthreads();
+  if (tid < 32) {
+    float z = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) z += red[k][tid];
+    sZ[tid] = z;
+    mz[((int64_t)nh * 32 + tid) * 2] = sM[tid];
+    mz[((int64_t)nh * 32 + tid) * 2 + 1] = z;
+  }
+  __syncthreads();
+  // U[e][d] = sum_b w_b[d] u_b[e][d]: thread owns idx = 4 tid .. 4 tid + 3 (e = idx / 32, d = idx % 32)
+  const int e = (tid * 4) >> 5, d0 = (tid * 4) & 31;
+  f32x4 U = {0.f, 0.f, 0.f, 0.f};
+  int b = 0;
+  for (; b + 4 <= nblk; b += 4) {
+    f32x4 u[4], w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      u[k] = *reinterpret_cast<const f32x4*>(pb + (b + k) * bstride + 64 + tid * 4);
+      w[k] = *reinterpret_cast<const f32x4*>(&sw[b + k][d0]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) U += w[k] * u[k];
+  }
+  for (; b < nblk; ++b) U += *reinterpret_cast<const f32x4*>(&sw[b][d0]) * *reinterpret_cast<const f32x4*>(pb + b * bstride + 64 + tid * 4);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int idx = tid * 4 + i;  // (e, d) = (idx / 32, idx % 32)
-    const int e = idx >> 5, d = idx & 31;
-    float U = 0.f;
-    for (int b = 0; b < nblk; ++b) {
-      const float mb = pb[b * bstride + d];
-      if (mb != -INFINITY) U += expf(mb - sM[d]) * pb[b * bstride + 64 + idx];
-    }
-    const float c = sZ[d] > 0.f ? U / sZ[d] : 0.f;
-    sc[d][e] = c;
-    ctx32[((int64_t)nh * 32 + d) * 32 + e] = c;
+    const float zd = sZ[d0 + i];
+    const float c = zd > 0.f ? U[i] / zd : 0.f;
+    sc[d0 + i][e] = c;
+    ctx32[((int64_t)nh * 32 + d0 + i) * 32 + e] = c;
   }
   __syncthreads();
   // fragment images: 2 tiles x 64 lanes x 8
@@ -897,7 +929,7 @@ extern "C" {
 // blocks per frame used by the stats / dctx kernels (each covers spb 64-pixel sub-chunks)
 int cesm_slaf_nblk(int Nf, int HW) {
   const int nsc = (HW + 63) / 64;
-  int nblk = std::max(1, 1024 / std::max(1, Nf));
+  int nblk = std::min(std::max(1, 1024 / std::max(1, Nf)), SLAF_NBLK_MAX);  // combine reduces <= 128 partials
   nblk = std::min(nblk, nsc);
   const int spb = (nsc + nblk - 1) / nblk;
   return (nsc + spb - 1) / spb;

@@ -439,6 +439,19 @@ def q_sample(x0, noise, t, sa, s1a):
     return xt
 
 
+def ddpm_step(x, eps, z, t, sra, betas, s1a, pv, out=None):
+    """Fused DDPM ancestral update (model.py:168-183); z=None drops the noise term; out may be x."""
+    B = x.shape[0]
+    _chk(x, dtype=torch.float32)
+    _chk(eps, x.shape, torch.float32)
+    if z is not None:
+        _chk(z, x.shape, torch.float32)
+    if out is None:
+        out = empty(x.shape, torch.float32, x.device)
+    call("cesm_ddpm_step", P(x), P(eps), P(z), P(t), P(sra), P(betas), P(s1a), P(pv), P(out), B, x.numel() // B, S())
+    return out
+
+
 def mse(pred, tgt):
     loss = empty((), torch.float32, pred.device)
     part = empty((512,), torch.float32, pred.device)

@@ -10,6 +10,8 @@ the CPU fp32 reference within 1e-5 relative L2).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -131,28 +133,81 @@ class Diffusion(nn.Module):
         eps = self.model(x_t, cond, t)
         return _MSE.apply(eps, noise.float().contiguous())
 
-    @torch.no_grad()
-    def p_sample(self, x_t, cond, t, noise=None):
-        """model.py:168-183 (DDPM ancestral step)."""
-        with torch.inference_mode():
-            b = self.betas[t].view(-1, 1, 1, 1)
-            s1 = self.sqrt_one_minus_alphas_cumprod[t].view(-1, 1, 1, 1)
-            r = self.sqrt_recip_alphas[t].view(-1, 1, 1, 1)
-            eps = self.model(x_t, cond, t)
-            mean = r * (x_t - b / s1 * eps)
-            if (t == 0).all():
-                return mean
-            if noise is None:
-                noise = torch.randn_like(x_t)
-            return mean + torch.sqrt(self.posterior_variance[t].view(-1, 1, 1, 1)) * noise
+    def _coefs(self):
+        return self.sqrt_recip_alphas, self.betas, self.sqrt_one_minus_alphas_cumprod, self.posterior_variance
 
     @torch.no_grad()
-    def sample(self, cond, shape, device):
-        """model.py:186-194."""
+    def p_sample(self, x_t, cond, t, noise=None):
+        """model.py:168-183 (DDPM ancestral step): model evaluation + one fused update kernel."""
+        with torch.inference_mode():
+            x_t = x_t.float().contiguous()
+            t = t.to(device=x_t.device, dtype=torch.long).contiguous()
+            eps = self.model(x_t, cond, t).float().contiguous()
+            if (t == 0).all():
+                return K.ddpm_step(x_t, eps, None, t, *self._coefs())
+            if noise is None:
+                noise = torch.randn_like(x_t)
+            return K.ddpm_step(x_t, eps, noise.float().contiguous(), t, *self._coefs())
+
+    @torch.no_grad()
+    def sample(self, cond, shape, device, use_graph=None, x_T=None, noise_seq=None):
+        """model.py:186-194.  On the GPU every p_sample step is ONE replay of a captured HIP graph (the
+        F=1 network forward + the fused update); the host only sets t and draws the step noise.  RNG use
+        is the reference's: randn(shape) for x_T, then randn_like(x) for every step with t > 0, drawn
+        outside the graph on the default generator, so the result equals the eager loop.  Test hooks:
+        x_T (initial state) and noise_seq ([T, *shape], noise of step i = noise_seq[i], i = 0 for t = T-1)
+        replace the draws.  use_graph=False (or CESM_SAMPLE_GRAPH=0) runs the eager loop."""
         with torch.inference_mode():
             B = shape[0]
-            x = torch.randn(shape, device=device)
-            for tt in reversed(range(self.T)):
-                t_tensor = torch.full((B,), tt, device=device, dtype=torch.long)
-                x = self.p_sample(x, cond, t_tensor)
-            return x
+            x = torch.randn(shape, device=device) if x_T is None else x_T.to(device).float().clone()
+            if use_graph is None:
+                use_graph = os.environ.get("CESM_SAMPLE_GRAPH", "1") != "0"
+            if not use_graph:
+                for i, tt in enumerate(reversed(range(self.T))):
+                    t_tensor = torch.full((B,), tt, device=device, dtype=torch.long)
+                    nz = None if noise_seq is None or tt == 0 else noise_seq[i].to(device)
+                    x = self.p_sample(x, cond, t_tensor, noise=nz)
+                return x
+            step = GraphSampleStep(self, cond, x)
+            for i, tt in enumerate(reversed(range(self.T))):
+                if tt == 0:
+                    step.z.zero_()
+                elif noise_seq is not None:
+                    step.z.copy_(noise_seq[i])
+                else:
+                    step.z.normal_()
+                step.run(tt)
+            return step.x
+
+
+class GraphSampleStep:
+    """One DDPM sampling step (model eval + fused update, in place on a static x) captured as a HIP graph
+    (torch.cuda.graph drives hipStreamBeginCapture; every kernel launches on the capturing stream).
+    Static inputs: x [B,1,H,W] fp32 (updated in place), cond, t [B] int64, z (step noise; zero at t=0,
+    where posterior_variance[0] = 0 makes the noise term vanish as in the reference's t=0 branch)."""
+
+    def __init__(self, diffusion, cond, x):
+        self.d = diffusion
+        self.x = x.float().contiguous()
+        self.cond = cond.float().contiguous()
+        self.t = torch.zeros(x.shape[0], dtype=torch.long, device=x.device)
+        self.z = torch.zeros_like(self.x)
+        x0 = self.x.clone()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):  # warm-up: weight packs, lazily built tables, allocator pools
+            for _ in range(2):
+                self._step()
+        torch.cuda.current_stream().wait_stream(side)
+        self.x.copy_(x0)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self._step()
+
+    def _step(self):
+        eps = self.d.model(self.x, self.cond, self.t).float().contiguous()
+        K.ddpm_step(self.x, eps, self.z, self.t, *self.d._coefs(), out=self.x)
+
+    def run(self, tt):
+        self.t.fill_(tt)
+        self.graph.replay()

@@ -303,6 +303,15 @@ def tattn_fwd(rc, res_mod, x):
     attn = pre.fn.fn
     Nb, H, W, C = x.shape
     HW = H * W
+    if rc.F == 1 and not rc.save:
+        # single frame (the sampler's F = 1 forward, inference.py:229): softmax over one key is exactly 1,
+        # so the block is x + to_out(v) — q, k, RoPE and the rel-pos bias drop out.
+        # LN -> v rows of to_qkv (1x1 GEMM) -> to_out with the residual fused.
+        n, _ = K.ln_fwd(x, _flat(pre.norm.gamma), save=False, eps=pre.norm.eps)
+        wv = rc.packed(attn.to_qkv.weight[512:768], 256, C, 1, 1, 0, 0)
+        v = K.conv_fwd(n, None, wv, None, (H, W, 256, 1, 1, 1, 0, 1))
+        wo = rc.packed(attn.to_out.weight, C, 256, 1, 1, 0, 0)
+        return K.conv_fwd(v, None, wo, None, (H, W, C, 1, 1, 1, 0, 1), res=x), None
     if _tblock_fused(rc, C):
         wq = rc.packed(attn.to_qkv.weight, 768, C, 1, 1, 0, 0)
         wo = rc.packed(attn.to_out.weight, C, 256, 1, 1, 0, 0)

@@ -155,6 +155,12 @@ int cesm_linear_small_bwd(const float* x, const float* w, const float* dy, float
 /* Diffusion.q_sample (model.py:196-201) and F.mse_loss (model.py:208) */
 int cesm_q_sample(const float* x0, const float* noise, const int64_t* t, const float* sa, const float* s1a,
                   float* xt, int B, int64_t HW, hipStream_t stream);
+/* Diffusion.p_sample DDPM update (model.py:168-183), fused: out = r_t (x - b_t/s1_t eps) + sqrt(pv_t) z,
+ * coefficients gathered on device from the schedule buffers by t[B]; z may be null (no noise term);
+ * out may alias x.  x, eps, z, out: [B][HW] fp32. */
+int cesm_ddpm_step(const float* x, const float* eps, const float* z, const int64_t* t, const float* sqrt_recip_alphas,
+                   const float* betas, const float* sqrt_one_minus_ac, const float* posterior_variance, float* out,
+                   int B, int64_t HW, hipStream_t stream);
 int cesm_mse(const float* pred, const float* tgt, float* loss, float* part, int64_t n, hipStream_t stream);
 int cesm_mse_bwd(const float* pred, const float* tgt, const float* gscale, float* dpred, int64_t n,
                  hipStream_t stream);

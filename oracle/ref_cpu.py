@@ -417,6 +417,16 @@ class Diffusion(nn.Module):
             noise = torch.randn_like(x_t)
         return mean + torch.sqrt(self.posterior_variance[t].view(-1, 1, 1, 1)) * noise
 
+    @torch.no_grad()
+    def sample(self, cond, shape, device, x_T=None, noise_seq=None):
+        """model.py:186-194; x_T / noise_seq ([T, *shape], step i <-> t = T-1-i) replace the draws."""
+        B = shape[0]
+        x = torch.randn(shape, device=device) if x_T is None else x_T.clone()
+        for i, tt in enumerate(reversed(range(self.T))):
+            t = torch.full((B,), tt, device=device, dtype=torch.long)
+            x = self.p_sample(x, cond, t, None if noise_seq is None or tt == 0 else noise_seq[i])
+        return x
+
 
 def train_step(diffusion, optimizer, x0, cond, t=None, noise=None, max_grad_norm=1.0):
     """train.py:868-880 (fp32 branch): zero_grad → loss → isfinite → backward → clip → step."""
