@@ -260,13 +260,21 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const T* __restrict__ x1,
 // current one is consumed.  4 waves = 2 (co halves) x 2 (pixel halves of 4 rows).
 // ----------------------------------------------------------------------------------------
 constexpr int H3_TH = 8, H3_TW = 32;     // default tile (TH x TW is chosen per level, see c2_tile)
-constexpr int H3_NPIX = 384;             // max halo pixels (TH+2)(TW+2)
-constexpr int H3_LD = 40;                // bf16 per LDS row (32 ch + 8 pad = 80 B)
+constexpr int H3_NPIX = 384;             // max halo pixels (TH+2)(TW+2) actually staged
+constexpr int H3_P = 40;                 // LDS halo row pitch (pixels): >= TW+2, multiple of 8 (see below)
+constexpr int H3_NROW = 10 * H3_P;       // LDS halo rows ((TH+2) <= 10 tile rows of H3_P pixels)
+constexpr int H3_LD = 32;                // bf16 per LDS row: 32 channels = 64 B, no padding
 constexpr int H3_BN = 64;
 constexpr int H3_HVEC = H3_NPIX * 4;     // 16-B vectors in the halo tile
 constexpr int H3_WVEC = 9 * H3_BN * 4;   // 16-B vectors in the weight tile
 constexpr int H3_HPT = (H3_HVEC + 255) / 256;
 constexpr int H3_WPT = H3_WVEC / 256;
+// element offset of 16-B chunk `ch` (8 channels) of LDS row `row`: 64-B rows, chunk index XORed with
+// bit 2 of the row.  ds_read_b128 of 16 rows r0..r0+15 (lane = row, lane group = chunk) is then
+// bank-conflict free for any r0 (the 80-B padded rows it replaces ran 2-3-way conflicted: PMC
+// SQ_LDS_BANK_CONFLICT = 51 % of LDS cycles at level 3).  Steps of 8 rows keep the swizzle, so the
+// tap offsets ky * H3_P and tap * 64 stay immediate.
+__device__ __forceinline__ int h3_off(int row, int ch) { return row * H3_LD + ((ch ^ ((row >> 1) & 2)) << 3); }
 
 template <int TW>
 __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
@@ -274,7 +282,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
                                                               const bf16* __restrict__ res, const bf16* __restrict__ res2,
                                                               bf16* __restrict__ y1, bf16* __restrict__ y2, ConvGeom g,
                                                               int tiles_x, int TH) {
-  __shared__ __attribute__((aligned(16))) bf16 sh[H3_NPIX * H3_LD];
+  __shared__ __attribute__((aligned(16))) bf16 sh[H3_NROW * H3_LD];
   __shared__ __attribute__((aligned(16))) bf16 sw[9 * H3_BN * H3_LD];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
@@ -318,12 +326,15 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
 #pragma unroll
     for (int k = 0; k < H3_HPT; ++k) {
       const int e = tid + k * 256;
-      if (e < HP * 4) *reinterpret_cast<bf16x8*>(sh + (e >> 2) * H3_LD + (e & 3) * 8) = hreg[k];
+      if (e < HP * 4) {
+        const int hp = e >> 2, r = hp / HWd, c = hp - r * HWd;
+        *reinterpret_cast<bf16x8*>(sh + h3_off(r * H3_P + c, e & 3)) = hreg[k];
+      }
     }
 #pragma unroll
     for (int k = 0; k < H3_WPT; ++k) {
       const int e = tid + k * 256;
-      *reinterpret_cast<bf16x8*>(sw + (e >> 2) * H3_LD + (e & 3) * 8) = wreg[k];
+      *reinterpret_cast<bf16x8*>(sw + h3_off(e >> 2, e & 3)) = wreg[k];
     }
   };
 
@@ -349,9 +360,17 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
     }
     const bool in = py < TH;
     // TW == 32: rows past TH stay inside the LDS halo buffer (results discarded), no select needed
-    hoff[j] = (TW == 32 || in) ? py * HWd + px : 0;
+    hoff[j] = (TW == 32 || in) ? py * H3_P + px : 0;
     pyx[j] = in ? (py << 16) | px : -1;
   }
+  // fragment addresses for ky = 0 / tap = 0; the other taps add immediates (swizzle-preserving steps)
+  int boff[8][3], aoff[2];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) boff[j][kx] = h3_off(hoff[j] + kx, lg);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) aoff[i] = h3_off(wr * 32 + i * 16 + lr, lg);
   for (int ch = 0; ch < nchunk; ++ch) {
     if (ch) __syncthreads();  // previous chunk fully consumed
     stage(ch);
@@ -362,10 +381,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
       bf16x8 af[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(sw + (tap * H3_BN + wr * 32 + i * 16 + lr) * H3_LD + lg * 8);
+        af[i] = *reinterpret_cast<const bf16x8*>(sw + aoff[i] + tap * H3_BN * H3_LD);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(sh + (hoff[j] + ky * HWd + kx) * H3_LD + lg * 8);
+        const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(sh + boff[j][kx] + ky * H3_P * H3_LD);
         acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bfr, acc[0][j], 0, 0, 0);
         acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bfr, acc[1][j], 0, 0, 0);
       }

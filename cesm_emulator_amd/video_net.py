@@ -288,7 +288,7 @@ FUSED_TBLOCK = os.environ.get("CESM_NO_FUSED_TBLOCK", "0") != "1"
 # widest channel count routed to the fused kernels: below it the 768-channel qkv intermediate is what
 # costs (HBM); above it the level is small and the unfused GEMMs are cheaper than per-pixel-group
 # weight re-reads
-FUSED_TBLOCK_MAXC = int(os.environ.get("CESM_TBLOCK_MAXC", "64"))
+FUSED_TBLOCK_MAXC = int(os.environ.get("CESM_TBLOCK_MAXC", "128"))  # C = 256/512: unfused measured faster
 
 
 def _tblock_fused(rc, C):
