@@ -66,6 +66,12 @@ class FusedAdamW:
     """torch.optim.AdamW-compatible surface (step / zero_grad / state_dict / param_groups)."""
 
     def __init__(self, params, lr=2e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-4, max_grad_norm=None):
+        params = list(params)
+        # every parameter passed in, frozen ones included: torch.optim indexes its state_dict by this order
+        self.all_params = params
+        self._index = {}
+        for i, p in enumerate(params):
+            self._index.setdefault(id(p), i)
         self.flat = FlatParams(params)
         self.lr, self.betas, self.eps, self.weight_decay = float(lr), tuple(betas), float(eps), float(weight_decay)
         self.max_grad_norm = max_grad_norm
@@ -103,11 +109,62 @@ class FusedAdamW:
         bump_param_epoch()
 
     def state_dict(self):
-        return {"step": self.step_count, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
-                "param_groups": [{k: v for k, v in self.param_groups[0].items() if k != "params"}]}
+        """torch.optim.AdamW layout — what train.py:1164 stores under "optimizer" — so checkpoints
+        round-trip with the reference: state[i] for the i-th parameter passed in (frozen ones, e.g. the
+        rotary freqs, carry no state), group keys as the installed torch's AdamW writes them."""
+        state = {}
+        if self.step_count > 0:
+            for p, off in zip(self.flat.params, self.flat.offsets):
+                n = p.numel()
+                state[self._index[id(p)]] = {
+                    "step": torch.tensor(float(self.step_count)),
+                    "exp_avg": self.exp_avg[off:off + n].view_as(p).clone(),
+                    "exp_avg_sq": self.exp_avg_sq[off:off + n].view_as(p).clone()}
+        group = dict(_adamw_group_defaults())
+        group.update({k: v for k, v in self.param_groups[0].items() if k != "params"})
+        group["betas"] = tuple(group["betas"])
+        group["params"] = list(range(len(self.all_params)))
+        return {"state": state, "param_groups": [group]}
 
     def load_state_dict(self, sd):
-        self.step_count = int(sd["step"])
-        self.exp_avg.copy_(sd["exp_avg"])
-        self.exp_avg_sq.copy_(sd["exp_avg_sq"])
-        self.param_groups[0].update(sd["param_groups"][0])
+        """Accepts torch.optim.AdamW state dicts (reference checkpoints) and the flat form of earlier
+        versions of this class."""
+        if "state" not in sd:  # flat form
+            self.step_count = int(sd["step"])
+            self.exp_avg.copy_(sd["exp_avg"])
+            self.exp_avg_sq.copy_(sd["exp_avg_sq"])
+            self.param_groups[0].update(sd["param_groups"][0])
+            return
+        g = sd["param_groups"][0]
+        if len(g["params"]) != len(self.all_params):
+            raise ValueError(f"optimizer state has {len(g['params'])} parameters, model has {len(self.all_params)}")
+        for k in ("lr", "betas", "eps", "weight_decay"):
+            if k in g:
+                self.param_groups[0][k] = tuple(g[k]) if k == "betas" else g[k]
+        self.exp_avg.zero_()
+        self.exp_avg_sq.zero_()
+        steps = set()
+        with torch.no_grad():
+            for p, off in zip(self.flat.params, self.flat.offsets):
+                st = sd["state"].get(self._index[id(p)], sd["state"].get(str(self._index[id(p)])))
+                if not st:
+                    continue
+                n = p.numel()
+                self.exp_avg[off:off + n].copy_(st["exp_avg"].reshape(-1))
+                self.exp_avg_sq[off:off + n].copy_(st["exp_avg_sq"].reshape(-1))
+                steps.add(int(float(st["step"])))
+        if len(steps) > 1:
+            raise ValueError(f"per-parameter step counts differ ({sorted(steps)}); the fused step needs one")
+        self.step_count = steps.pop() if steps else 0
+
+
+_GROUP_DEFAULTS = None
+
+
+def _adamw_group_defaults():
+    """param_group keys/defaults of the installed torch.optim.AdamW (the de-facto pinned version)."""
+    global _GROUP_DEFAULTS
+    if _GROUP_DEFAULTS is None:
+        g = torch.optim.AdamW([torch.zeros(1, requires_grad=True)]).param_groups[0]
+        _GROUP_DEFAULTS = {k: v for k, v in g.items() if k != "params"}
+    return _GROUP_DEFAULTS
