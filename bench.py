@@ -62,12 +62,12 @@ class KernelProbe:
         self.active = False
         self._orig = kernels_mod.conv_fwd
 
-        def wrapped(x1, x2, wp, bias, geom, res=None, res2=None, out_split=None):
+        def wrapped(x1, x2, wp, bias, geom, **kw):
             hit = self.active and self.match(x1, x2, geom)
             if hit:
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
-            y = self._orig(x1, x2, wp, bias, geom, res=res, res2=res2, out_split=out_split)
+            y = self._orig(x1, x2, wp, bias, geom, **kw)
             if hit:
                 e.record()
                 Ho, Wo, Cout, KH, KW = geom[:5]
