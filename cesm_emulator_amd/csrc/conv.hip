@@ -253,6 +253,185 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const T* __restrict__ x1,
 }
 
 // ----------------------------------------------------------------------------------------
+// bf16 generic implicit GEMM (strided down-sampling convs, transposed up-sampling convs in parity
+// blocks, their data gradients, every conv the halo / 1x1 kernels do not take).  Same tiling and
+// tap/parity enumeration as conv_fwd_kernel, but
+//   * the im2col and weight tiles stay bf16 in registers (raw 16-B loads: no f32 round trip) and
+//     are loaded TWO K-steps ahead (each step is only 16 MFMAs per wave, far shorter than a global
+//     load's latency);
+//   * LDS rows are 64 B with the 16-B chunk index XORed with bit 2 of the row (conflict-free
+//     ds_read_b128 over any 16 consecutive rows; the 80-B padded rows ran 2-3-way conflicted).
+// ----------------------------------------------------------------------------------------
+__device__ __forceinline__ int gx_off(int row, int ch) { return row * 32 + ((ch ^ ((row >> 1) & 2)) << 3); }
+
+template <int BN, bool PAR = false>
+__global__ __launch_bounds__(256) void conv_fwd_bf16_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
+                                                            const bf16* __restrict__ w, const float* __restrict__ bias,
+                                                            const bf16* __restrict__ res, const bf16* __restrict__ res2,
+                                                            bf16* __restrict__ y1, bf16* __restrict__ y2, ConvGeom g,
+                                                            int64_t M, int bpp = 0) {
+  constexpr int VPR = BK / 8;            // 16-B vectors per 32-channel row
+  constexpr int RPP = 256 / VPR;         // rows per pass
+  constexpr int PX_PASS = BMP / RPP;
+  constexpr int W_PASS = BN / RPP;
+  constexpr int TM = BN / 32;
+  constexpr int TN = 4;
+  __shared__ __attribute__((aligned(16))) bf16 lds[2][(BMP + BN) * 32];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int par = PAR ? (int)blockIdx.y / bpp : 0;
+  const int py = par >> 1, px = par & 1;
+  const int64_t m0 = (int64_t)(PAR ? (int)blockIdx.y - par * bpp : (int)blockIdx.y) * BMP;
+  const int n0 = blockIdx.x * BN;
+  const int Cin = g.C1 + g.C2;
+  const int csteps = Cin / BK;
+  const int ntap = PAR ? (g.KH / 2) * (g.KW / 2) : g.KH * g.KW;
+  const int ksteps = ntap * csteps;
+  const int ky0 = PAR ? (((g.P - py) % 2) + 2) % 2 : 0;
+  const int kx0 = PAR ? (((g.P - px) % 2) + 2) % 2 : 0;
+  const int Wg = PAR ? g.Wo / 2 : g.Wo, Hg = PAR ? g.Ho / 2 : g.Ho;
+
+  const int vrow = tid / VPR, vch = tid % VPR;
+  int pn[PX_PASS], poy[PX_PASS], pox[PX_PASS];
+  bool pval[PX_PASS];
+#pragma unroll
+  for (int p = 0; p < PX_PASS; ++p) {
+    const int64_t m = m0 + vrow + p * RPP;
+    pval[p] = m < M;
+    const int64_t mm = pval[p] ? m : 0;
+    pox[p] = (int)(mm % Wg);
+    const int64_t t = mm / Wg;
+    poy[p] = (int)(t % Hg);
+    pn[p] = (int)(t / Hg);
+    if constexpr (PAR) {
+      poy[p] = 2 * poy[p] + py;
+      pox[p] = 2 * pox[p] + px;
+    }
+  }
+
+  bf16x8 xr[2][PX_PASS], wreg[2][W_PASS];  // two K-steps in flight
+  auto gload = [&](int ks, int slot) {
+    const int t = ks / csteps;
+    const int c0 = (ks - t * csteps) * BK;
+    int ky, kx;
+    if constexpr (PAR) {
+      const int hw = g.KW / 2;
+      ky = ky0 + 2 * (t / hw);
+      kx = kx0 + 2 * (t - (t / hw) * hw);
+    } else {
+      ky = t / g.KW;
+      kx = t - ky * g.KW;
+    }
+    const int tap = ky * g.KW + kx;
+    const bf16* src;
+    int cs, cc;
+    if (c0 < g.C1) { src = x1; cs = g.C1; cc = c0; } else { src = x2; cs = g.C2; cc = c0 - g.C1; }
+#pragma unroll
+    for (int p = 0; p < PX_PASS; ++p) {
+      int iy, ix;
+      bf16x8 v = {};
+      if (pval[p] && tap_src(g, poy[p], pox[p], ky, kx, iy, ix))
+        v = *reinterpret_cast<const bf16x8*>(src + ((((int64_t)pn[p] * g.Hi + iy) * g.Wi + ix) * cs + cc + vch * 8));
+      xr[slot][p] = v;
+    }
+#pragma unroll
+    for (int p = 0; p < W_PASS; ++p) {
+      const int co = n0 + vrow + p * RPP;
+      wreg[slot][p] = *reinterpret_cast<const bf16x8*>(w + ((int64_t)co * (g.KH * g.KW) + tap) * Cin + c0 + vch * 8);
+    }
+  };
+  auto sstore = [&](int buf, int slot) {
+    bf16* A = lds[buf];            // weights [BN][32]
+    bf16* B = lds[buf] + BN * 32;  // pixels  [BMP][32]
+#pragma unroll
+    for (int p = 0; p < W_PASS; ++p) *reinterpret_cast<bf16x8*>(A + gx_off(vrow + p * RPP, vch)) = wreg[slot][p];
+#pragma unroll
+    for (int p = 0; p < PX_PASS; ++p) *reinterpret_cast<bf16x8*>(B + gx_off(vrow + p * RPP, vch)) = xr[slot][p];
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int lr = lane & 15, lg = lane >> 4;
+  int aoff[TM], boff[TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) aoff[i] = gx_off(wr * (BN / 2) + i * 16 + lr, lg);
+#pragma unroll
+  for (int j = 0; j < TN; ++j) boff[j] = BN * 32 + gx_off(wc * 64 + j * 16 + lr, lg);
+
+  // K-steps in pairs so the register slots / LDS buffers are compile-time (a runtime slot index would
+  // put the staging arrays in scratch memory)
+  auto step = [&](int ks, auto bufc) {
+    constexpr int buf = decltype(bufc)::value;
+    // registers: slot buf held step ks (already in LDS), slot buf^1 holds step ks+1
+    if (ks + 2 < ksteps) gload(ks + 2, buf);
+    const bf16* L = lds[buf];
+    bf16x8 af[TM], bfr[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(L + aoff[i]);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(L + boff[j]);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    if (ks + 1 < ksteps) sstore(buf ^ 1, buf ^ 1);
+    __syncthreads();
+  };
+  gload(0, 0);
+  if (ksteps > 1) gload(1, 1);
+  sstore(0, 0);
+  __syncthreads();
+  for (int ks = 0; ks < ksteps; ks += 2) {
+    step(ks, std::integral_constant<int, 0>{});
+    if (ks + 1 < ksteps) step(ks + 1, std::integral_constant<int, 1>{});
+  }
+
+  const int Co2 = g.Cout - g.Co1;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    int64_t m = m0 + wc * 64 + j * 16 + lr;
+    if (m >= M) continue;
+    if constexpr (PAR) {
+      const int64_t b = m % Wg, t = m / Wg, a = t % Hg, n = t / Hg;
+      m = (n * g.Ho + 2 * a + py) * g.Wo + 2 * b + px;
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int co = n0 + wr * (BN / 2) + i * 16 + lg * 4;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (bias) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += bias[co + r];
+      }
+      if (co < g.Co1) {
+        if (res) {
+          float rv[4];
+          load4(res + m * g.Co1 + co, rv);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += rv[r];
+        }
+        store4(y1 + m * g.Co1 + co, v);
+      } else {
+        if (res2) {
+          float rv[4];
+          load4(res2 + m * Co2 + (co - g.Co1), rv);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += rv[r];
+        }
+        store4(y2 + m * Co2 + (co - g.Co1), v);
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------
 // 3x3 / stride 1 / pad 1 conv (bf16): halo-tiled implicit GEMM.  Block = 8 x 32 output pixels of
 // one image x 64 output channels.  Per 32-channel input chunk the (8+2) x (32+2) input halo and
 // the 9 taps x 64 co weights are staged in LDS once and all 9 taps read shifted windows of the
@@ -2491,19 +2670,19 @@ int cesm_conv_fwd(int dtype, const void* x1, const void* x2, const void* wp, con
     const int bpp = (int)cdiv(Mp, BMP);
     dim3 gp(Cout / BN, 4 * bpp);
     if (BN == 128)
-      conv_fwd_kernel<bf16, 128, true><<<gp, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp,
+      conv_fwd_bf16_kernel<128, true><<<gp, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp,
                                                                bias, (const bf16*)res, (const bf16*)res2, (bf16*)y1,
                                                                (bf16*)y2, g, Mp, bpp);
     else
-      conv_fwd_kernel<bf16, 64, true><<<gp, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp,
+      conv_fwd_bf16_kernel<64, true><<<gp, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp,
                                                               bias, (const bf16*)res, (const bf16*)res2, (bf16*)y1,
                                                               (bf16*)y2, g, Mp, bpp);
   } else if (dtype == CESM_DT_BF16) {
     if (BN == 128)
-      conv_fwd_kernel<bf16, 128><<<grid, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
+      conv_fwd_bf16_kernel<128><<<grid, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
                                                            (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, M);
     else
-      conv_fwd_kernel<bf16, 64><<<grid, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
+      conv_fwd_bf16_kernel<64><<<grid, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
                                                           (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, M);
   } else if (dtype == CESM_DT_F32) {
     if (BN == 128)
