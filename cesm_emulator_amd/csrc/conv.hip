@@ -1668,8 +1668,11 @@ __global__ __launch_bounds__(256) void wgrad_wide_kernel(const bf16* __restrict_
   }
   const int yrow0 = tid / VPRY, ycol = (tid % VPRY) * 8;
 
-  bf16x8 xr, yr[NPY];
-  auto gload = [&](int p0) {
+  bf16x8 xr2[2], yr2[2][NPY];  // two steps in flight (register slot = step parity)
+  auto gload = [&](int p0, auto slotc) {
+    constexpr int slot = decltype(slotc)::value;
+    bf16x8& xr = xr2[slot];
+    bf16x8 (&yr)[NPY] = yr2[slot];
 #pragma unroll
     for (int p = 0; p < NPY; ++p) {
       const int mm = p0 + yrow0 + p * RPPY;
@@ -1694,7 +1697,10 @@ __global__ __launch_bounds__(256) void wgrad_wide_kernel(const bf16* __restrict_
       if (++oy >= g.Ho) { oy = 0; ++on; }
     }
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](auto bufc) {
+    constexpr int buf = decltype(bufc)::value;
+    const bf16x8& xr = xr2[buf];
+    const bf16x8 (&yr)[NPY] = yr2[buf];
 #pragma unroll
     for (int p = 0; p < NPY; ++p) {
       const int r = yrow0 + p * RPPY;
@@ -1711,15 +1717,19 @@ __global__ __launch_bounds__(256) void wgrad_wide_kernel(const bf16* __restrict_
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nsteps = (pend - pbeg + WG_BP - 1) / WG_BP;
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
   if (nsteps > 0) {
-    gload(pbeg);
-    sstore(0);
+    gload(pbeg, I0{});
+    if (nsteps > 1) gload(pbeg + WG_BP, I1{});
+    sstore(I0{});
   }
   __syncthreads();
   const int q = lr >> 2, pp = lr & 3;
-  for (int s = 0; s < nsteps; ++s) {
-    const int buf = s & 1;
-    if (s + 1 < nsteps) gload(pbeg + (s + 1) * WG_BP);
+  // steps in pairs: LDS buffer and register slot are compile-time; step s+2 is loaded while step s runs
+  auto step = [&](int s, auto bufc) {
+    constexpr int buf = decltype(bufc)::value;
+    if (s + 2 < nsteps) gload(pbeg + (s + 2) * WG_BP, bufc);
     bf16x8 af[MT], bfr[4];
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
@@ -1748,8 +1758,12 @@ __global__ __launch_bounds__(256) void wgrad_wide_kernel(const bf16* __restrict_
     for (int i = 0; i < MT; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    if (s + 1 < nsteps) sstore(buf ^ 1);
+    if (s + 1 < nsteps) sstore(std::integral_constant<int, buf ^ 1>{});
     __syncthreads();
+  };
+  for (int s = 0; s < nsteps; s += 2) {
+    step(s, I0{});
+    if (s + 1 < nsteps) step(s + 1, I1{});
   }
   const int K = g.KH * g.KW * Cin;
   float* out = slab + (int64_t)blockIdx.z * g.Cout * K;
