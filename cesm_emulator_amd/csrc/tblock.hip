@@ -750,9 +750,44 @@ template <int C, int NV>
 __device__ __forceinline__ void tw_qkv(const bf16* __restrict__ wqkv, const bf16x8 (&xf)[TW<C, NV>::NVTM][TW<C, NV>::KS],
                                        int h, const int (&fr)[NV], float scale, const float* rot, bf16* sq, bf16* sk,
                                        bf16* sv, int lr, int lg) {
-  bf16x8 a[6][C / 32];
-  tw_load_wq<C, NV>(a, wqkv, h, lr, lg);
-  tw_qkv_pre<C, NV>(a, xf, fr, scale, rot, sq, sk, sv, lr, lg);
+  if constexpr (C <= 64) {
+    bf16x8 a[6][C / 32];
+    tw_load_wq<C, NV>(a, wqkv, h, lr, lg);
+    tw_qkv_pre<C, NV>(a, xf, fr, scale, rot, sq, sk, sv, lr, lg);
+  } else {
+    // wider C: the six 16-row tiles' fragments (24 x 16 B at C = 128) in two-tile batches, which keeps
+    // the backward kernel within its 256 registers
+    using T = TW<C, NV>;
+#pragma unroll
+    for (int c2 = 0; c2 < 6; c2 += 2) {
+      bf16x8 a[2][T::KS];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int ct = c2 + u, mt = (ct >> 1) * 16 + h * 2 + (ct & 1);
+#pragma unroll
+        for (int ks = 0; ks < T::KS; ++ks) a[u][ks] = ld_img(wqkv, mt, T::KS, ks, lg * 16 + lr);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int ct = c2 + u, kind = ct >> 1;
+        bf16* dst = kind == 0 ? sq : (kind == 1 ? sk : sv);
+        const int d0 = (ct & 1) * 16 + lg * 4;
+#pragma unroll
+        for (int vt = 0; vt < NV; ++vt) {
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < T::KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][ks], xf[vt][ks], acc, 0, 0, 0);
+          float o4[4] = {acc[0], acc[1], acc[2], acc[3]};
+          if (kind == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o4[r] *= scale;
+          }
+          if (kind < 2) rope4(o4, rot, fr[vt], d0, 1.f);
+          store4(dst + (vt * 16 + lr) * HLD + d0, o4);
+        }
+      }
+    }
+  }
 }
 
 // LN of the wave's voxels on the B fragments.  use_saved: take (mean, rstd) from mr, else compute
@@ -1012,10 +1047,11 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
     for (int h = 0; h < NH; ++h) {
       // issued ahead of the q/k/v GEMMs so its latency hides behind them: this head's log-sum-exp
       // of the wave's pixels (one per frame row lr)
+      constexpr bool LPF = C <= 64;  // at C = 128 the 2 extra registers cost spills
       float Lp[T::PW];
 #pragma unroll
       for (int pp = 0; pp < T::PW; ++pp)
-        Lp[pp] = (lr < F && p0 + pp < HW) ? lse[(((int64_t)b * NH + h) * HW + p0 + pp) * F + lr] : 0.f;
+        Lp[pp] = (LPF && lr < F && p0 + pp < HW) ? lse[(((int64_t)b * NH + h) * HW + p0 + pp) * F + lr] : 0.f;
       tw_qkv<C, NV>(wqkv, xf, h, fr, scale, rot, sq, sk, sv, lr, lg);
       TW_ST(1)
       // dO_h^T = W_out[:, h]^T . dy^T
@@ -1058,8 +1094,12 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
         if (p >= HW) break;
         const int rb = pp * F;
         float Li = Lp[0];
+        if constexpr (LPF) {
 #pragma unroll
-        for (int q = 1; q < T::PW; ++q) Li = pp == q ? Lp[q] : Li;
+          for (int q = 1; q < T::PW; ++q) Li = pp == q ? Lp[q] : Li;
+        } else {
+          Li = lr < F ? lse[(((int64_t)b * NH + h) * HW + p) * F + lr] : 0.f;
+        }
         const bf16x8 kr = lr < F ? ld16(sk + (rb + lr) * HLD + lg * 8) : zero8();
         const bf16x8 qr = lr < F ? ld16(sq + (rb + lr) * HLD + lg * 8) : zero8();
         const bf16x8 vr = lr < F ? ld16(sv + (rb + lr) * HLD + lg * 8) : zero8();
