@@ -647,7 +647,7 @@ __global__ __launch_bounds__(256) void slab_combine_kernel(const float* __restri
 }
 
 // slab_dx: wave = 16*NV pixels of one frame, all heads.  grid (cdiv(HW, 64*NV), Nf), 256 threads,
-// dynamic LDS: 4 waves x [16*NV][DQLD] bf16 (this head's dq|dk|dv) + C floats (dgamma).
+// dynamic LDS: 2C floats (dgamma accumulator, LN gamma) + 4 waves x [16*NV][DQLD] bf16 (this head's dq|dk|dv).
 constexpr int DQLD = 104;
 template <int C, int NV>
 __global__ __launch_bounds__(256, 2) void slab_dx_kernel(
@@ -659,11 +659,12 @@ __global__ __launch_bounds__(256, 2) void slab_dx_kernel(
     float* __restrict__ dgamma_part, int HW, float scale, float eps) {
   constexpr int KS = C / 32, CT = C / 16;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* sg = smem;  // [C]
+  float* sg = smem;      // [C] dgamma accumulator
+  float* sgm = smem + C;  // [C] LN gamma (LDS reads do not queue behind the emission stores)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
-  bf16* sq = reinterpret_cast<bf16*>(smem + C) + wid * 16 * NV * DQLD;
-  for (int e = tid; e < C; e += 256) sg[e] = 0.f;
+  bf16* sq = reinterpret_cast<bf16*>(smem + 2 * C) + wid * 16 * NV * DQLD;
+  for (int e = tid; e < C; e += 256) { sg[e] = 0.f; sgm[e] = gamma[e]; }
   __syncthreads();
   const int n = blockIdx.y;
   const int p0 = (blockIdx.x * 4 + wid) * 16 * NV;
@@ -701,7 +702,7 @@ __global__ __launch_bounds__(256, 2) void slab_dx_kernel(
       for (int ks = 0; ks < KS; ++ks) {
 #pragma unroll
         for (int i = 0; i < 8; ++i)
-          xf[vt][ks][i] = (bf16)(ok ? (a[ks][i] - mean[vt]) * rstd[vt] * gamma[ks * 32 + lg * 8 + i] : 0.f);
+          xf[vt][ks][i] = (bf16)(ok ? (a[ks][i] - mean[vt]) * rstd[vt] * sgm[ks * 32 + lg * 8 + i] : 0.f);
         if (ok && xn_out) *reinterpret_cast<bf16x8*>(xn_out + (rb + p) * C + ks * 32 + lg * 8) = xf[vt][ks];
       }
     }
@@ -871,7 +872,7 @@ __global__ __launch_bounds__(256, 2) void slab_dx_kernel(
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           xh[ct][r] = ok ? (xv[r] - mean[vt]) * rstd[vt] : 0.f;
-          const float g = dxacc[ct][vt][r] * gamma[co + r];
+          const float g = dxacc[ct][vt][r] * sgm[co + r];
           s1 += g;
           s2 = fmaf(g, xh[ct][r], s2);
         }
@@ -896,7 +897,7 @@ __global__ __launch_bounds__(256, 2) void slab_dx_kernel(
           float dv4[4], o4[4];
           load4(dy + (rb + p) * C + co, dv4);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) o4[r] = rstd[vt] * (dxacc[ct][vt][r] * gamma[co + r] - s1 - xh[ct][r] * s2) + dv4[r];
+          for (int r = 0; r < 4; ++r) o4[r] = rstd[vt] * (dxacc[ct][vt][r] * sgm[co + r] - s1 - xh[ct][r] * s2) + dv4[r];
           store4(dx + (rb + p) * C + co, o4);
         }
       }
@@ -991,7 +992,7 @@ int cesm_slaf_bwd(const void* x, const void* dy, const float* gamma, const void*
   // NV = 16-pixel tiles per wave: 2 at C = 64, 1 at C = 128 (registers); dgp rows = grid blocks
   const int NVr = C == 64 ? 2 : 1;
   dim3 grid((unsigned)cdiv(HW, 64 * NVr), Nf);
-  const size_t sm = (size_t)C * 4 + (size_t)4 * 16 * NVr * DQLD * 2;
+  const size_t sm = (size_t)C * 8 + (size_t)4 * 16 * NVr * DQLD * 2;
   if (C == 64)
     slab_dx_kernel<64, 2><<<grid, 256, sm, stream>>>(
         (const bf16*)x, (const bf16*)dy, gamma, img_q, img_qt, img_ot, G,

@@ -984,7 +984,8 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
   float* sb = smem;                  // [8][F][F]
   float* sdb = sb + NH * FF;         // [8][F][F] block dbias accumulator
   float* sg = sdb + NH * FF;         // [C] block dgamma accumulator
-  float* rot = sg + C;               // [16][RS]
+  float* sgm = sg + C;               // [C] LN gamma (LDS reads do not queue behind the emission stores)
+  float* rot = sgm + C;              // [16][RS]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const int b = blockIdx.y;
@@ -997,7 +998,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
   bf16* sdo = sv + R * HLD;
   float* sld = reinterpret_cast<float*>(reinterpret_cast<bf16*>(rot + 16 * RS) + 4 * 4 * R * HLD) + wid * 32;
   for (int e = tid; e < NH * FF; e += 256) { sb[e] = bias[e] * LOG2E; sdb[e] = 0.f; }
-  for (int e = tid; e < C; e += 256) sg[e] = 0.f;
+  for (int e = tid; e < C; e += 256) { sg[e] = 0.f; sgm[e] = gamma[e]; }
   for (int e = tid; e < F * 32; e += 256) rot[(e >> 5) * RS + (e & 31)] = rotg[e];
   __syncthreads();
 
@@ -1017,7 +1018,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
   for (int pg = blockIdx.x * 4 + wid; pg < npg; pg += nw) {
     const int p0 = pg * T::PW;
     bf16x8 xf[T::NVTM][T::KS];
-    tw_ln<C, NV>(x, gamma, nullptr, mr, xf, NVT, VW, F, p0, HW, b, 0.f, lr, lg);
+    tw_ln<C, NV>(x, sgm, nullptr, mr, xf, NVT, VW, F, p0, HW, b, 0.f, lr, lg);
     int64_t vrow[T::NVTM];  // row of voxel (vt*16 + lane&15), -1 when outside the group
 #pragma unroll
     for (int vt = 0; vt < T::NVTM; ++vt) {
@@ -1235,7 +1236,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           xh[ct][r] = ok ? (xv[r] - mean) * rstd : 0.f;
-          const float g = dxacc[ct][vt][r] * gamma[co + r];
+          const float g = dxacc[ct][vt][r] * sgm[co + r];
           s1 += g;
           s2 = fmaf(g, xh[ct][r], s2);
           if constexpr (DG_REG) dgam[ct][r] = fmaf(dxacc[ct][vt][r], xh[ct][r], dgam[ct][r]);
@@ -1265,7 +1266,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
           float dv[4], o4[4];
           ldnt4(dy + row * C + co, dv);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) o4[r] = rstd * (dxacc[ct][vt][r] * gamma[co + r] - s1 - xh[ct][r] * s2) + dv[r];
+          for (int r = 0; r < 4; ++r) o4[r] = rstd * (dxacc[ct][vt][r] * sgm[co + r] - s1 - xh[ct][r] * s2) + dv[r];
           stnt4(dx + row * C + co, o4);
         }
       }
@@ -1309,7 +1310,7 @@ static size_t tw_fwd_smem(int F) {  // NOLINT
 template <int C>
 static size_t tw_bwd_smem(int F) {
   const int R = ((TW<C>::PW * F + 15) / 16) * 16;
-  return (size_t)(2 * NH * F * F + C + 16 * RS) * 4 + (size_t)4 * 4 * R * HLD * 2 + 4 * 32 * 4;
+  return (size_t)(2 * NH * F * F + 2 * C + 16 * RS) * 4 + (size_t)4 * 4 * R * HLD * 2 + 4 * 32 * 4;
 }
 template <typename K>
 static void allow_smem(K kernel, size_t bytes) {
