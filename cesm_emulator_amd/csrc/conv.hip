@@ -1789,6 +1789,12 @@ __global__ __launch_bounds__(256) void wgrad_wide_kernel(const bf16* __restrict_
 // ----------------------------------------------------------------------------------------
 constexpr int W3_TH = 8, W3_TW = 32;
 constexpr int W3_HW = W3_TW + 2, W3_NPIX = (W3_TH + 2) * (W3_TW + 2);
+// LDS pitch (pixels) of the input-halo rows of both 3x3 weight-gradient kernels: a multiple of 16, so
+// a step of whole halo rows keeps bit 3 of the LDS row and with it the chunk swizzle (w3_swz_x) —
+// the transposed fragment reads of all nine taps then share six per-lane offsets plus immediates
+// instead of recomputing a swizzled address per read (the kernels were VALU-issue bound: 6-10 VALU
+// per MFMA, mostly that address arithmetic).
+constexpr int W3_P = 48;
 
 __device__ __forceinline__ int w3_swz_dy(int r) { return (((r >> 1) & 1) << 2) | (((r >> 3) & 1) << 3); }
 __device__ __forceinline__ int w3_swz_x(int r) { return ((r >> 3) & 1) << 2; }
@@ -1798,7 +1804,7 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_bf16_kernel(const bf16* __res
                                                                float* __restrict__ slab, ConvGeom g, int tiles_x,
                                                                int ntiles) {
   __shared__ __attribute__((aligned(16))) bf16 sdy[W3_TH * W3_TW * 64];   // 32 KB, 128-B rows
-  __shared__ __attribute__((aligned(16))) bf16 shx[W3_NPIX * 32];         // 21.3 KB, 64-B rows
+  __shared__ __attribute__((aligned(16))) bf16 shx[(W3_TH + 2) * W3_P * 32];  // 30 KB, 64-B rows
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int cot0 = (wid >> 1) * 2, cit = wid & 1;
   const int co0 = blockIdx.x * 64, ci0 = blockIdx.y * 32;
@@ -1817,6 +1823,16 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_bf16_kernel(const bf16* __res
     for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int lr = lane & 15, lg = lane >> 4, q = lr >> 2, pp = lr & 3;
+  // per-lane fragment offsets (elements); row steps of 32 dY pixels / W3_P halo pixels keep the swizzles
+  int aoff[2][2], boff[2][3];
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const int r = lg * 8 + half * 4 + q;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) aoff[i][half] = r * 64 + ((((cot0 + i) * 4 + pp) ^ w3_swz_dy(r)) * 4);
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) boff[half][kx] = (r + kx) * 32 + (((cit * 4 + pp) ^ w3_swz_x(r + kx)) * 4);
+  }
   for (int tile = blockIdx.z; tile < ntiles; tile += gridDim.z) {
     const int n = tile / tiles_per_img;
     const int rem = tile - n * tiles_per_img;
@@ -1860,8 +1876,9 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_bf16_kernel(const bf16* __res
         const int e = tid + k * 256;
         if (e < W3_NPIX * 4) {
           const int hp = e >> 2, part = e & 3;
-          const int ch = (part * 2) ^ w3_swz_x(hp);
-          *reinterpret_cast<bf16x8*>(shx + hp * 32 + ch * 4) = hv[k];
+          const int r = hp / W3_HW, row = r * W3_P + (hp - r * W3_HW);
+          const int ch = (part * 2) ^ w3_swz_x(row);
+          *reinterpret_cast<bf16x8*>(shx + row * 32 + ch * 4) = hv[k];
         }
       }
     }
@@ -1874,9 +1891,7 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_bf16_kernel(const bf16* __res
       for (int i = 0; i < 2; ++i) {
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
-          const int r = py * 32 + lg * 8 + half * 4 + q;
-          const int ch = ((cot0 + i) * 4 + pp) ^ w3_swz_dy(r);
-          const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(sdy + r * 64 + ch * 4));
+          const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(sdy + aoff[i][half] + py * 32 * 64));
 #pragma unroll
           for (int e = 0; e < 4; ++e) af[i][half * 4 + e] = __builtin_bit_cast(bf16, (short)v[e]);
         }
@@ -1887,9 +1902,8 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_bf16_kernel(const bf16* __res
         bf16x8 bfr;
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
-          const int r = (py + ky) * W3_HW + lg * 8 + half * 4 + q + kx;
-          const int ch = (cit * 4 + pp) ^ w3_swz_x(r);
-          const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(shx + r * 32 + ch * 4));
+          const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (LDS_PTR(s16x4))(shx + boff[half][kx] + (py + ky) * W3_P * 32));
 #pragma unroll
           for (int e = 0; e < 4; ++e) bfr[half * 4 + e] = __builtin_bit_cast(bf16, (short)v[e]);
         }
@@ -1927,7 +1941,7 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3w36_kernel(const bf16* __restr
                                                              float* __restrict__ slab, ConvGeom g, int tiles_x,
                                                              int ntiles) {
   __shared__ __attribute__((aligned(16))) bf16 sdy[W36_NP * 64];     // 36 KB, 128-B rows
-  __shared__ __attribute__((aligned(16))) bf16 shx[W36_NPIX * 32];   // 23.75 KB, 64-B rows
+  __shared__ __attribute__((aligned(16))) bf16 shx[(W36_TH + 2) * W3_P * 32];  // 30 KB, 64-B rows
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int cot0 = (wid >> 1) * 2, cit = wid & 1;
   const int co0 = blockIdx.x * 64, ci0 = blockIdx.y * 32;
@@ -1946,6 +1960,13 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3w36_kernel(const bf16* __restr
     for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int lr = lane & 15, lg = lane >> 4, q = lr >> 2, pp = lr & 3;
+  int aoff[2][2];  // dY fragment offsets for K-chunk 0 (chunk kc adds kc*32 rows: swizzle-invariant)
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const int r = lg * 8 + half * 4 + q;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) aoff[i][half] = r * 64 + ((((cot0 + i) * 4 + pp) ^ w3_swz_dy(r)) * 4);
+  }
   for (int tile = blockIdx.z; tile < ntiles; tile += gridDim.z) {
     const int n = tile / tiles_per_img;
     const int rem = tile - n * tiles_per_img;
@@ -1989,33 +2010,40 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3w36_kernel(const bf16* __restr
         const int e = tid + k * 256;
         if (e < W36_NPIX * 4) {
           const int hp = e >> 2, part = e & 3;
-          const int ch = (part * 2) ^ w3_swz_x(hp);
-          *reinterpret_cast<bf16x8*>(shx + hp * 32 + ch * 4) = hv[k];
+          const int r = hp / W36_HW, row = r * W3_P + (hp - r * W36_HW);
+          const int ch = (part * 2) ^ w3_swz_x(row);
+          *reinterpret_cast<bf16x8*>(shx + row * 32 + ch * 4) = hv[k];
         }
       }
     }
     __syncthreads();
+    // flat pixel of this lane's two 4-pixel groups in K-chunk kc: P = kc*32 + r0[half]; (row, col) of
+    // it in the 36-wide tile advance incrementally (32 < 36: at most one wrap per chunk)
+    int prow[2], pcol[2];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) { prow[half] = 0; pcol[half] = lg * 8 + half * 4 + q; }
 #pragma unroll 1
     for (int kc = 0; kc < W36_NP / 32; ++kc) {
-      // A = dY^T (rows co, K = flat pixels kc*32 .. +31): tr reads
+      // A = dY^T (rows co, K = flat pixels kc*32 .. +31): tr reads (swizzle invariant under kc*32)
       bf16x8 af[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
-          const int r = kc * 32 + lg * 8 + half * 4 + q;
-          const int ch = ((cot0 + i) * 4 + pp) ^ w3_swz_dy(r);
-          const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(sdy + r * 64 + ch * 4));
+          const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(sdy + aoff[i][half] + kc * 32 * 64));
 #pragma unroll
           for (int e = 0; e < 4; ++e) af[i][half * 4 + e] = __builtin_bit_cast(bf16, (short)v[e]);
         }
       }
-      // halo row of tap (0,0) for this lane's two 4-pixel groups
-      int hb[2];
+      // halo row of tap (0,0) for each 4-pixel group -> offsets of kx = 0..2 (ky adds whole W3_P rows)
+      int bo[2][3];
 #pragma unroll
       for (int half = 0; half < 2; ++half) {
-        const int P = kc * 32 + lg * 8 + half * 4 + q;
-        hb[half] = (P / W36_TW) * W36_HW + (P - (P / W36_TW) * W36_TW);
+        const int hb = prow[half] * W3_P + pcol[half];
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) bo[half][kx] = (hb + kx) * 32 + (((cit * 4 + pp) ^ w3_swz_x(hb + kx)) * 4);
+        pcol[half] += 32;
+        if (pcol[half] >= W36_TW) { pcol[half] -= W36_TW; ++prow[half]; }
       }
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
@@ -2023,9 +2051,7 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3w36_kernel(const bf16* __restr
         bf16x8 bfr;
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
-          const int r = hb[half] + ky * W36_HW + kx;
-          const int ch = (cit * 4 + pp) ^ w3_swz_x(r);
-          const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(shx + r * 32 + ch * 4));
+          const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(shx + bo[half][kx] + ky * W3_P * 32));
 #pragma unroll
           for (int e = 0; e < 4; ++e) bfr[half * 4 + e] = __builtin_bit_cast(bf16, (short)v[e]);
         }
