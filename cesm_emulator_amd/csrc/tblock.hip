@@ -845,7 +845,8 @@ __global__ __launch_bounds__(256, 2) void tw_fwd_kernel(const bf16* __restrict__
                                                      const bf16* __restrict__ wqkv, const bf16* __restrict__ wout,
                                                      const float* __restrict__ bias, const float* __restrict__ rotg,
                                                      bf16* __restrict__ y, float* __restrict__ mr,
-                                                     float* __restrict__ lse, int F, int HW, float scale, float eps) {
+                                                     float* __restrict__ lse, bf16* __restrict__ o_out, int F, int HW,
+                                                     float scale, float eps) {
   using T = TW<C, NV>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* sb = smem;             // [8][F][F], pre-scaled by log2(e)
@@ -944,6 +945,14 @@ __global__ __launch_bounds__(256, 2) void tw_fwd_kernel(const bf16* __restrict__
     bf16x8 ob[T::NVTM];
 #pragma unroll
     for (int vt = 0; vt < T::NVTM; ++vt) ob[vt] = vt < NVT ? ld16(sq + (vt * 16 + lr) * HLD + lg * 8) : zero8();
+    if (o_out) {  // O_h for the to_out weight gradient (the backward then skips its emission)
+#pragma unroll
+      for (int vt = 0; vt < T::NVTM; ++vt) {
+        int64_t row = 0;
+        if (vt < NVT && tw_row(vt * 16 + lr, VW, F, p0, HW, b, row))
+          stnt16(o_out + row * INNER + h * DH + lg * 8, ob[vt]);
+      }
+    }
 #pragma unroll
     for (int ct = 0; ct < T::CT; ++ct) {
 #pragma unroll
@@ -1136,8 +1145,9 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
           const bf16x8 kg = kslot_gather(sk, rb, half * 16, F, lane);
           const bf16x8 vg = kslot_gather(sv, rb, half * 16, F, lane);
           dqt[half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kg, dst_b, z4, 0, 0, 0);  // dQ'^T[d][i]
+          if (!o_out) continue;  // O written by the forward (cesm_tblock_fwd o)
           const f32x4 ot = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vg, pt_b, z4, 0, 0, 0);  // O^T[d][i]
-          if (o_out && lr < F) {
+          if (lr < F) {
             float oo[4] = {ot[0], ot[1], ot[2], ot[3]};
             stnt4(o_out + (((int64_t)b * F + lr) * HW + p) * INNER + h * DH + half * 16 + lg * 4, oo);
           }
@@ -1319,31 +1329,31 @@ static void allow_smem(K kernel, size_t bytes) {
 
 template <int C, int NV>
 static void tw_fwd_launch_nv(const void* x, const float* gamma, const void* wqkv, const void* wout, const float* bias,
-                             const float* rot, void* y, float* mr, float* lse, int B, int F, int HW, float scale,
-                             float eps, hipStream_t stream) {
+                             const float* rot, void* y, float* mr, float* lse, void* o, int B, int F, int HW,
+                             float scale, float eps, hipStream_t stream) {
   const int npg = (int)cdiv(HW, TW<C>::PW);
   dim3 grid((unsigned)cdiv(npg, 4), B);
   const size_t sm = tw_fwd_smem<C>(F);
   allow_smem(tw_fwd_kernel<C, NV>, sm);
   tw_fwd_kernel<C, NV><<<grid, 256, sm, stream>>>((const bf16*)x, gamma, (const bf16*)wqkv, (const bf16*)wout, bias,
-                                                  rot, (bf16*)y, mr, lse, F, HW, scale, eps);
+                                                  rot, (bf16*)y, mr, lse, (bf16*)o, F, HW, scale, eps);
 }
 
 template <int C>
 static int tw_fwd_launch(const void* x, const float* gamma, const void* wqkv, const void* wout, const float* bias,
-                         const float* rot, void* y, float* mr, float* lse, int B, int F, int HW, float scale, float eps,
-                         hipStream_t stream) {
+                         const float* rot, void* y, float* mr, float* lse, void* o, int B, int F, int HW, float scale,
+                         float eps, hipStream_t stream) {
   const int nv = (TW<C>::PW * F + 15) / 16;
   switch (nv) {
-    case 1: tw_fwd_launch_nv<C, 1>(x, gamma, wqkv, wout, bias, rot, y, mr, lse, B, F, HW, scale, eps, stream); break;
+    case 1: tw_fwd_launch_nv<C, 1>(x, gamma, wqkv, wout, bias, rot, y, mr, lse, o, B, F, HW, scale, eps, stream); break;
     case 2:
-      if constexpr (TW<C>::PW >= 2) { tw_fwd_launch_nv<C, 2>(x, gamma, wqkv, wout, bias, rot, y, mr, lse, B, F, HW, scale, eps, stream); break; }
+      if constexpr (TW<C>::PW >= 2) { tw_fwd_launch_nv<C, 2>(x, gamma, wqkv, wout, bias, rot, y, mr, lse, o, B, F, HW, scale, eps, stream); break; }
       return CESM_EUNSUPPORTED;
     case 3:
-      if constexpr (TW<C>::PW >= 3) { tw_fwd_launch_nv<C, 3>(x, gamma, wqkv, wout, bias, rot, y, mr, lse, B, F, HW, scale, eps, stream); break; }
+      if constexpr (TW<C>::PW >= 3) { tw_fwd_launch_nv<C, 3>(x, gamma, wqkv, wout, bias, rot, y, mr, lse, o, B, F, HW, scale, eps, stream); break; }
       return CESM_EUNSUPPORTED;
     case 4:
-      if constexpr (TW<C>::PW >= 4) { tw_fwd_launch_nv<C, 4>(x, gamma, wqkv, wout, bias, rot, y, mr, lse, B, F, HW, scale, eps, stream); break; }
+      if constexpr (TW<C>::PW >= 4) { tw_fwd_launch_nv<C, 4>(x, gamma, wqkv, wout, bias, rot, y, mr, lse, o, B, F, HW, scale, eps, stream); break; }
       return CESM_EUNSUPPORTED;
     default:
       return CESM_EUNSUPPORTED;
@@ -1402,9 +1412,10 @@ extern "C" {
 // wqkv [768][C] / wout [C][256] packed bf16, bias [8][F][F], rot [F][16][2].
 // mr [B*F*HW][2] (LN mean, rstd) and lse [B][8][HW][F] are saved for the backward (may be null).
 int cesm_tblock_fwd(const void* x, const float* gamma, const void* wqkv, const void* wout, const float* bias,
-                    const float* rot, void* y, float* mr, float* lse, void* wimg, int B, int F, int HW, int C,
+                    const float* rot, void* y, float* mr, float* lse, void* o, void* wimg, int B, int F, int HW, int C,
                     float scale, float eps, hipStream_t stream) {
   if (F < 1 || F > 16) return CESM_EUNSUPPORTED;
+  if (o && C > 256) return CESM_EUNSUPPORTED;  // only the wave-private kernels write O
   if (C <= 256) {  // the wave-private kernels read weight fragments from images (1-KiB lines)
     bf16* iq = (bf16*)wimg;
     bf16* io = iq + 768 * C;
@@ -1414,9 +1425,9 @@ int cesm_tblock_fwd(const void* x, const float* gamma, const void* wqkv, const v
     wout = io;
   }
   switch (C) {
-    case 64: return tw_fwd_launch<64>(x, gamma, wqkv, wout, bias, rot, y, mr, lse, B, F, HW, scale, eps, stream);
-    case 128: return tw_fwd_launch<128>(x, gamma, wqkv, wout, bias, rot, y, mr, lse, B, F, HW, scale, eps, stream);
-    case 256: return tw_fwd_launch<256>(x, gamma, wqkv, wout, bias, rot, y, mr, lse, B, F, HW, scale, eps, stream);
+    case 64: return tw_fwd_launch<64>(x, gamma, wqkv, wout, bias, rot, y, mr, lse, o, B, F, HW, scale, eps, stream);
+    case 128: return tw_fwd_launch<128>(x, gamma, wqkv, wout, bias, rot, y, mr, lse, o, B, F, HW, scale, eps, stream);
+    case 256: return tw_fwd_launch<256>(x, gamma, wqkv, wout, bias, rot, y, mr, lse, o, B, F, HW, scale, eps, stream);
     case 512: {
       dim3 grid((unsigned)cdiv(HW, TB<512>::P), B);
       tblock_fwd_kernel<512><<<grid, 256, 0, stream>>>((const bf16*)x, gamma, (const bf16*)wqkv, (const bf16*)wout,

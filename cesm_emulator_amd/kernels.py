@@ -290,8 +290,10 @@ def tattn_bwd(qkv, o, dout, lse, bias, rot, dtable, B, F, HW, scale, num_buckets
 TBLOCK_C = (64, 128, 256, 512)
 
 
-def tblock_fwd(x, gamma, wqkv, wout, bias, rot, B, F, scale, save=True, eps=1e-5):
-    """fused temporal-attention block forward (bf16); x [B*F, H, W, C]"""
+def tblock_fwd(x, gamma, wqkv, wout, bias, rot, B, F, scale, save=True, eps=1e-5, save_o=False):
+    """fused temporal-attention block forward (bf16); x [B*F, H, W, C].  Returns (y, mr, lse, o); o (the
+    attention output before to_out, [B*F, H, W, 256]) only with save_o (C <= 256), for the to_out weight
+    gradient, so the backward need not emit it."""
     Nb, H, W, C = x.shape
     _chk(x, dtype=torch.bfloat16)
     _chk(wqkv, (768, C), torch.bfloat16)
@@ -299,14 +301,15 @@ def tblock_fwd(x, gamma, wqkv, wout, bias, rot, B, F, scale, save=True, eps=1e-5
     y = empty(x.shape, x.dtype, x.device)
     mr = empty((Nb * H * W, 2), torch.float32, x.device) if save else None
     lse = empty((B, 8, H * W, F), torch.float32, x.device) if save else None
+    o = empty((Nb, H, W, 256), x.dtype, x.device) if save_o else None
     wimg = empty(((768 + 256) * C,), torch.bfloat16, x.device)  # weight fragment images (rebuilt per call)
-    call("cesm_tblock_fwd", P(x), P(gamma), P(wqkv), P(wout), P(bias), P(rot), P(y), P(mr), P(lse), P(wimg), B, F,
-         H * W, C, float(scale), float(eps), S())
-    return y, mr, lse
+    call("cesm_tblock_fwd", P(x), P(gamma), P(wqkv), P(wout), P(bias), P(rot), P(y), P(mr), P(lse), P(o), P(wimg),
+         B, F, H * W, C, float(scale), float(eps), S())
+    return y, mr, lse, o
 
 
 def tblock_bwd(x, dy, gamma, mr, lse, wqkv, wqkv_t, wout_t, bias, rot, dgamma, dtable, B, F, scale,
-               want_wgrad_inputs=True, num_buckets=32, max_distance=32):
+               want_wgrad_inputs=True, num_buckets=32, max_distance=32, emit_o=True):
     """fused temporal-attention block backward, dx path (bf16).  Returns (dx, dqkv, o, xn); the last
     three ([.., 768], [.., 256], [.., C] bf16) feed the to_qkv / to_out weight-gradient GEMMs."""
     Nb, H, W, C = x.shape
@@ -322,7 +325,7 @@ def tblock_bwd(x, dy, gamma, mr, lse, wqkv, wqkv_t, wout_t, bias, rot, dgamma, d
     dx = empty(x.shape, x.dtype, dev)
     if want_wgrad_inputs:
         dqkv = empty((Nb, H, W, 768), x.dtype, dev)
-        o = empty((Nb, H, W, 256), x.dtype, dev)
+        o = empty((Nb, H, W, 256), x.dtype, dev) if emit_o else None
         xn = empty(x.shape, x.dtype, dev)
     else:
         dqkv = o = xn = None

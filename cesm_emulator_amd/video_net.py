@@ -285,6 +285,7 @@ def resnet_bwd(rc, rb, st, dout):
 
 
 FUSED_TBLOCK = os.environ.get("CESM_NO_FUSED_TBLOCK", "0") != "1"
+TW_FWD_O = os.environ.get("CESM_TW_FWD_O", "1") != "0"  # forward writes O for dW_out (else the backward emits it)
 # widest channel count routed to the fused kernels: below it the 768-channel qkv intermediate is what
 # costs (HBM); above it the level is small and the unfused GEMMs are cheaper than per-pixel-group
 # weight re-reads
@@ -315,9 +316,11 @@ def tattn_fwd(rc, res_mod, x):
     if _tblock_fused(rc, C):
         wq = rc.packed(attn.to_qkv.weight, 768, C, 1, 1, 0, 0)
         wo = rc.packed(attn.to_out.weight, C, 256, 1, 1, 0, 0)
-        y, mr, lse = K.tblock_fwd(x, _flat(pre.norm.gamma), wq, wo, rc.bias, rc.rot, rc.B, rc.F, attn.scale,
-                                  save=rc.save, eps=pre.norm.eps)
-        st = SimpleNamespace(fused=True, x=x, mr=mr, lse=lse) if rc.save else None
+        # training: the forward also writes O (to_out's input) so the backward does not emit it
+        save_o = rc.save and C <= 256 and TW_FWD_O
+        y, mr, lse, o = K.tblock_fwd(x, _flat(pre.norm.gamma), wq, wo, rc.bias, rc.rot, rc.B, rc.F, attn.scale,
+                                     save=rc.save, eps=pre.norm.eps, save_o=save_o)
+        st = SimpleNamespace(fused=True, x=x, mr=mr, lse=lse, o=o) if rc.save else None
         return y, st
     n, mr = K.ln_fwd(x, _flat(pre.norm.gamma), save=rc.save, eps=pre.norm.eps)
     qspec, ospec = ConvSpec(attn.to_qkv), ConvSpec(attn.to_out)
@@ -340,7 +343,9 @@ def tattn_bwd(rc, res_mod, st, dy):
         want = dwq is not None or dwo is not None
         dx, dqkv, o, xn = K.tblock_bwd(st.x, dy, _flat(pre.norm.gamma), st.mr, st.lse, wq, wq_t, wo_t, rc.bias,
                                        rc.rot, gbuf(pre.norm.gamma), rc.dtable, rc.B, rc.F, attn.scale,
-                                       want_wgrad_inputs=want)
+                                       want_wgrad_inputs=want, emit_o=st.o is None)
+        if st.o is not None:
+            o = st.o
         if dwq is not None:
             K.conv_wgrad(xn, None, dqkv, None, dwq, (H, W, 768, 1, 1, 1, 0, 1), 0, 0)
         if dwo is not None:

@@ -103,14 +103,16 @@ int cesm_tattn_bwd(int dtype, const void* qkv, const void* o, const void* dout, 
  * [B*F*HW][C], wqkv [768][C], wout [C][256] packed bf16; saves mr [B*F*HW][2] and lse [B][8][HW][F].
  * F <= 16, C in {64,128,256,512}. */
 int cesm_tblock_fwd(const void* x, const float* gamma, const void* wqkv, const void* wout, const float* bias,
-                    const float* rot, void* y, float* mr, float* lse, void* wimg, int B, int F, int HW, int C, float scale,
-                    float eps, hipStream_t stream);
+                    const float* rot, void* y, float* mr, float* lse, void* o, void* wimg, int B, int F, int HW, int C,
+                    float scale, float eps, hipStream_t stream);
 /* Fused temporal-attention block backward, dx path (bf16): recomputes LN/QKV/RoPE/softmax from mr and
  * lse, dO = dy.W_out, MFMA core backward, dxn = dqkv.W_qkv, LN backward + residual -> dx.  Emits
  * (nullable) dqkv [..][768], o [..][256], xn [..][C] bf16 for the to_qkv/to_out weight gradients,
  * dbias_part [B][8][nblk][F][F] (cesm_relpos_bwd layout) and dgamma (+)= sum dxn*xhat.
  * wqkv_t [C][768] and wout_t [256][C] are the swap-packed weights; nblk from cesm_tblock_bwd_nblk. */
 int cesm_tblock_bwd_nblk(int B, int F, int HW, int C);
+/* (cesm_tblock_fwd's o, nullable, C <= 256: the attention output O [..][256] bf16 before to_out, written
+ * by the forward for the to_out weight gradient; the backward's o is then passed null.) */
 int cesm_tblock_bwd(const void* x, const void* dy, const float* gamma, const float* mr, const float* lse,
                     const void* wqkv, const void* wqkv_t, const void* wout_t, const float* bias, const float* rot,
                     void* dx, void* dqkv, void* o, void* xn, float* dbias_part, float* dgamma, float* dgamma_part, void* wimg,

@@ -460,7 +460,7 @@ def test_fused_temporal_block_forward(dev, C, Fr):
     xd = to_cl(x).to(dev, torch.bfloat16)
     wq = K.conv_pack(attn.to_qkv.weight.detach(), torch.bfloat16, 768, C, 1, 1, 0, 0)
     wo = K.conv_pack(attn.to_out.weight.detach(), torch.bfloat16, C, 256, 1, 1, 0, 0)
-    y, mr, lse = K.tblock_fwd(xd, res_mod.fn.norm.gamma.reshape(-1), wq, wo, rc.bias, rc.rot, B, Fr, attn.scale)
+    y, mr, lse, _ = K.tblock_fwd(xd, res_mod.fn.norm.gamma.reshape(-1), wq, wo, rc.bias, rc.rot, B, Fr, attn.scale)
     # float64 reference (oracle module) on bf16-rounded x and weights
     from oracle import ref_cpu as R
     ref = R.Residual(R.PreNorm(C, R.EinopsToAndFrom(R.Attention(C, 8, 32, R.RotaryEmbedding(32))))).double()
@@ -505,11 +505,25 @@ def test_fused_temporal_block_backward(dev, C, Fr):
     wq_t = K.conv_pack(wqkv, torch.bfloat16, C, 768, 1, 1, 1, 1)
     wo_t = K.conv_pack(wout, torch.bfloat16, 256, C, 1, 1, 1, 1)
     gamma = res_mod.fn.norm.gamma.detach().reshape(-1).contiguous()
-    _, mr, lse = K.tblock_fwd(xd, gamma, wq, wo, rc.bias, rc.rot, B, Fr, attn.scale)
+    save_o = C <= 256
+    _, mr, lse, o_fwd = K.tblock_fwd(xd, gamma, wq, wo, rc.bias, rc.rot, B, Fr, attn.scale, save_o=save_o)
     dgamma = torch.zeros(C, device=dev)
     dtable = torch.zeros(32, 8, device=dev)
     dx, dqkv, o, xn = K.tblock_bwd(xd, gd, gamma, mr, lse, wq, wq_t, wo_t, rc.bias, rc.rot, dgamma, dtable, B, Fr,
                                    attn.scale)
+    if save_o:  # the forward's O (what training uses for dW_out) == the backward's recomputed emission
+        assert rel(o_fwd, o) < 1e-2
+        # and the backward without the O emission gives the same dx / dqkv
+        dg2, dt2 = torch.zeros(C, device=dev), torch.zeros(32, 8, device=dev)
+        dx2, dqkv2, o2, _ = K.tblock_bwd(xd, gd, gamma, mr, lse, wq, wq_t, wo_t, rc.bias, rc.rot, dg2, dt2, B, Fr,
+                                         attn.scale, emit_o=False)
+        dg3, dt3 = torch.zeros(C, device=dev), torch.zeros(32, 8, device=dev)
+        dx3, dqkv3, _, _ = K.tblock_bwd(xd, gd, gamma, mr, lse, wq, wq_t, wo_t, rc.bias, rc.rot, dg3, dt3, B, Fr,
+                                        attn.scale)
+        print("rerun identical:", torch.equal(dx3, dx), torch.equal(dqkv3, dqkv), " no-emit identical:",
+              torch.equal(dx2, dx), torch.equal(dqkv2, dqkv), " max |ddx|", (dx2.float() - dx.float()).abs().max().item())
+        assert o2 is None and rel(dx2, dx) < 1e-2 and rel(dqkv2, dqkv) < 1e-2
+        o = o_fwd
     dwq = dqkv.reshape(-1, 768).double().t() @ xn.reshape(-1, C).double()
     dwo = gd.reshape(-1, C).double().t() @ o.reshape(-1, 256).double()
     # float64 reference

@@ -30,7 +30,7 @@ def main():
     dgamma = torch.zeros(C, device=dev)
     dtable = torch.zeros(32, 8, device=dev)
     for _ in range(reps):
-        y, mr, lse = K.tblock_fwd(x, gamma, wq, wo, bias, rot, B, F, 32 ** -0.5)
+        y, mr, lse, _ = K.tblock_fwd(x, gamma, wq, wo, bias, rot, B, F, 32 ** -0.5)
         K.tblock_bwd(x, dy, gamma, mr, lse, wq, wq_t, wo_t, bias, rot, dgamma, dtable, B, F, 32 ** -0.5,
                       want_wgrad_inputs=emit)
     torch.cuda.synchronize()
