@@ -12,7 +12,7 @@ cd /tmp && export TMPDIR=/tmp
 cd "$root"
 mkdir -p gpurun_out
 if [ "$2" != "skip-tests" ]; then
-  timeout -k 10 900 python3 -m pytest tests -m gpu -x -q > "gpurun_out/${tag}_pytest.log" 2>&1
+  timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "gpurun_out/${tag}_pytest.log" 2>&1
 fi
 timeout -k 10 420 python3 bench.py > "gpurun_out/${tag}_bench.json" 2> "gpurun_out/${tag}_bench.err"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "gpurun_out/${tag}_prof" -o run -- \
