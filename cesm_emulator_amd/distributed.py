@@ -6,9 +6,17 @@ train independent replicas; here gradients ARE averaged, making an N-rank step e
 step on the concatenated batch (per-sample GroupNorm/LayerNorm => no cross-sample statistics).
 
 Gradients live in ONE flat fp32 buffer (FusedAdamW / FlatParams), so the exchange is a few large
-bucketed all-reduces issued on a dedicated communication stream (ordered after the backward with
-an event), sized for xGMI's point-to-point rings (64 MB default buckets: 35 M params = 140 MB ->
-3 buckets).  The average is folded into the all-reduce via pre-scaling by 1/world (no extra pass).
+bucketed all-reduces issued on a dedicated communication stream, sized for xGMI's point-to-point
+rings (32 MB buckets: 35 M params = 140 MB -> 5 buckets).  The average is folded into the
+all-reduce via pre-scaling the bucket by 1/world on the communication stream.
+
+Overlap with the backward: `arm()` hands the network a readiness hook.
+The HIP backward walks the modules in reverse construction order, which is also reverse flat-buffer
+order, and calls the hook after each level.  Once every parameter at or above a bucket's start
+offset is final, that bucket's all-reduce is enqueued on the communication stream behind an event
+on the compute stream, so RCCL moves the deep levels' gradients while the shallow levels' backward
+still runs.  The shared accumulators (time MLP, rel-pos table) sit at the front of the buffer and
+go last, in `finish()`.
 """
 from __future__ import annotations
 
@@ -44,11 +52,12 @@ def is_dist():
 class GradAllReducer:
     """Bucketed average of a flat gradient buffer across ranks."""
 
-    def __init__(self, bucket_bytes=64 << 20, use_side_stream=True):
+    def __init__(self, bucket_bytes=32 << 20, use_side_stream=True):
         self.world = dist.get_world_size() if is_dist() else 1
         self.bucket_elems = max(1, bucket_bytes // 4)
         self.side = use_side_stream
         self._stream = None
+        self._armed = None
 
     def buckets(self, n):
         return [(s, min(n, s + self.bucket_elems)) for s in range(0, n, self.bucket_elems)]
@@ -76,3 +85,71 @@ class GradAllReducer:
         """Initial replica sync (what DDP's constructor does at train.py:1076)."""
         if self.world > 1:
             dist.broadcast(flat_params, src=src)
+
+    # ------------------------------------------------------------------ overlapped path
+    def _comm(self, device):
+        if self._stream is None:
+            self._stream = torch.cuda.Stream(device=device)
+        return self._stream
+
+    def arm(self, net, flat):
+        """Reduce buckets during the coming backward.  `net` is the module whose backward calls
+        `net._grad_ready(params, extra_stream)`; `flat` has .params / .offsets / .grad (FlatParams).
+        Buckets are cut from the END of the buffer, the order the backward finalises it."""
+        if self.world == 1:
+            return
+        g = flat.grad
+        ends = {}
+        for p, off in zip(flat.params, flat.offsets):
+            ends[id(p)] = off + p.numel()
+        self._armed = dict(grad=g, total=g.numel(), ends=ends, pending=set(ends), lo=g.numel(), works=[])
+        net._grad_ready = self.ready
+
+    def _issue(self, a, b, streams):
+        st = self._armed
+        chunk = st["grad"][a:b]
+        if chunk.is_cuda and self.side:
+            comm = self._comm(chunk.device)
+            comm.wait_stream(torch.cuda.current_stream(chunk.device))
+            for s in streams:
+                if s is not None:
+                    comm.wait_stream(s)
+            with torch.cuda.stream(comm):
+                chunk.mul_(1.0 / self.world)
+                st["works"].append(dist.all_reduce(chunk, op=dist.ReduceOp.SUM, async_op=True))
+        else:
+            chunk.mul_(1.0 / self.world)
+            dist.all_reduce(chunk, op=dist.ReduceOp.SUM)
+
+    def ready(self, params, extra_stream=None):
+        """Hook: `params` have final gradients (enqueued on the current stream / extra_stream)."""
+        st = self._armed
+        if st is None:
+            return
+        for p in params:
+            st["pending"].discard(id(p))
+        ready_from = max((st["ends"][i] for i in st["pending"]), default=0)
+        streams = (extra_stream,)
+        while st["lo"] > 0:
+            b = st["lo"]
+            a = max(0, b - self.bucket_elems)
+            if a < ready_from:
+                break
+            self._issue(a, b, streams)
+            st["lo"] = a
+
+    def finish(self, net=None, extra_stream=None):
+        """Reduce whatever is left, then order the compute stream after every bucket."""
+        st = self._armed
+        if st is None:
+            return
+        st["pending"].clear()
+        self.ready((), extra_stream)
+        for w in st["works"]:
+            w.wait()
+        g = st["grad"]
+        if g.is_cuda and self.side and self._stream is not None:
+            torch.cuda.current_stream(g.device).wait_stream(self._stream)
+        self._armed = None
+        if net is not None and getattr(net, "_grad_ready", None) is not None:
+            net._grad_ready = None

@@ -6,7 +6,8 @@ Differences from the reference, all deliberate:
   * the isfinite(loss) guard runs on device (the AdamW kernel skips a non-finite step) and is
     raised on the host when the loss is read, instead of forcing a sync before backward;
   * data-parallel gradient averaging is actually performed (the reference's DDP reducer is never
-    armed): `dp.allreduce_grads()` after backward.
+    armed): bucketed all-reduces overlapped with the backward (`dp.arm` /
+    `dp.finish`, distributed.py).
 """
 from __future__ import annotations
 
@@ -35,9 +36,15 @@ def make_optimizer(diffusion, train_cfg):
 def train_step(diffusion, optimizer, x0, cond, max_grad_norm=1.0, dp=None, t=None, noise=None):
     """One optimizer step; returns the loss as a device tensor (no host sync)."""
     optimizer.zero_grad(set_to_none=True)
+    net = diffusion.model.net
+    overlap = dp is not None and getattr(dp, "overlap", True)
+    if overlap:
+        dp.arm(net, optimizer.flat)  # bucket all-reduces issued during the backward
     loss = diffusion.loss(x0, cond, t=t, noise=noise)
     loss.backward()
-    if dp is not None:
+    if overlap:
+        dp.finish(net)
+    elif dp is not None:
         dp.allreduce_grads(optimizer.flat.grad)
     optimizer.max_grad_norm = max_grad_norm
     optimizer.step(loss=loss.detach())

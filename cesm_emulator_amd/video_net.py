@@ -33,6 +33,52 @@ def bump_param_epoch():
 
 
 # ============================================================================ run context
+# Weight gradients off the critical path: the backward's dX chain stays on the current stream and every
+# parameter-gradient GEMM (conv / 1x1 / qkv wgrads, bias column sums, stem wgrad) is enqueued on a second
+# HIP stream ordered after the kernel that produced its inputs.  The wgrads are HBM-bound (the level-0 qkv
+# wgrad streams 4.4 GB) while the dX kernels are MFMA/latency-bound, so the two co-run on the CUs.
+# "0": off, "attn": only the fused attention blocks' wgrads, "1": every wgrad
+WGRAD_STREAM = os.environ.get("CESM_WGRAD_STREAM", "0")
+_WSTREAMS = {}
+
+
+def _wgrad_stream(device):
+    s = _WSTREAMS.get(device)
+    if s is None:
+        s = _WSTREAMS[device] = torch.cuda.Stream(device=device)
+    return s
+
+
+class _Side:
+    """Context: enqueue on the wgrad stream after everything already on the current stream; the
+    tensors read there are recorded on it so the caching allocator does not hand their memory to
+    the current stream before the wgrad kernels are done."""
+
+    def __init__(self, rc, tensors):
+        self.rc, self.tensors = rc, tensors
+
+    def __enter__(self):
+        ws = self.rc.wstream
+        if ws is None:
+            return
+        ws.wait_stream(torch.cuda.current_stream())
+        self._ctx = torch.cuda.stream(ws)
+        self._ctx.__enter__()
+
+    def __exit__(self, *exc):
+        ws = self.rc.wstream
+        if ws is None:
+            return False
+        self._ctx.__exit__(*exc)
+        for t in self.tensors:
+            if t is not None:
+                t.record_stream(ws)
+        return False
+
+
+_NOSIDE = SimpleNamespace(wstream=None)
+
+
 class RunCtx:
     """Per-call state: compute dtype, batch geometry, shared tables, weight-pack cache."""
 
@@ -40,9 +86,18 @@ class RunCtx:
         self.net, self.B, self.F, self.cdt, self.save = net, B, F, cdt, save
         self.dt = None      # grad of the time embedding (allocated in backward)
         self.dtable = None  # grad of the rel-pos embedding table
+        self.wstream = None  # weight-gradient stream (set by the backward when WGRAD_STREAM)
 
     def packed(self, w, cout, cin, kh, kw, swap, flip):
         return self.net._packed(w, self.cdt, cout, cin, kh, kw, swap, flip)
+
+    def side(self, *tensors, attn=False):
+        return _Side(self if (attn or WGRAD_STREAM == "1") else _NOSIDE, tensors)
+
+    def join(self):
+        """current stream waits for every weight gradient enqueued so far"""
+        if self.wstream is not None:
+            torch.cuda.current_stream().wait_stream(self.wstream)
 
 
 def gbuf(p):
@@ -96,11 +151,8 @@ def conv_forward(rc, spec, x1, x2=None, res=None):
     return y, st
 
 
-def conv_backward(rc, spec, st, dy, need_dx=True, dres1=None, dres2=None, bias_done=False):
-    """Param grads of the conv + (optionally) dX (split for concat inputs) + fused residual grads.
-    bias_done: the bias gradient was already produced (by the GroupNorm backward's reduction)."""
-    w, b = spec.mod.weight, spec.mod.bias
-    dw = gbuf(w)
+def conv_param_grads(spec, st, dy, dw, db):
+    """dW (+ dbias) of one conv (called on the weight-gradient stream)."""
     if dw is not None:
         if spec.transposed:
             # the transposed conv's weight gradient sum_{a,b} x[a,b] (x) dOut[S*a - P + ky, S*b - P + kx] is the
@@ -112,9 +164,18 @@ def conv_backward(rc, spec, st, dy, need_dx=True, dres1=None, dres2=None, bias_d
             K.conv_wgrad(dy, None, st.x1, None, dw, (Hx, Wx, spec.cin, spec.k, spec.k, spec.stride, spec.pad, 1), 0, 0)
         else:
             K.conv_wgrad(st.x1, st.x2, dy, None, dw, st.geom, st.swap, st.flip)
-    db = gbuf(b)
-    if db is not None and not bias_done:
+    if db is not None:
         K.colsum(dy, db)
+
+
+def conv_backward(rc, spec, st, dy, need_dx=True, dres1=None, dres2=None, bias_done=False):
+    """Param grads of the conv + (optionally) dX (split for concat inputs) + fused residual grads.
+    bias_done: the bias gradient was already produced (by the GroupNorm backward's reduction)."""
+    w, b = spec.mod.weight, spec.mod.bias
+    dw = gbuf(w)
+    db = gbuf(b)
+    with rc.side(dy, st.x1, st.x2):
+        conv_param_grads(spec, st, dy, dw, None if bias_done else db)
     if not need_dx:
         return None
     k = spec.k
@@ -346,10 +407,11 @@ def tattn_bwd(rc, res_mod, st, dy):
                                        want_wgrad_inputs=want, emit_o=st.o is None)
         if st.o is not None:
             o = st.o
-        if dwq is not None:
-            K.conv_wgrad(xn, None, dqkv, None, dwq, (H, W, 768, 1, 1, 1, 0, 1), 0, 0)
-        if dwo is not None:
-            K.conv_wgrad(o, None, dy, None, dwo, (H, W, C, 1, 1, 1, 0, 1), 0, 0)
+        with rc.side(xn, dqkv, o, dy, attn=True):
+            if dwq is not None:
+                K.conv_wgrad(xn, None, dqkv, None, dwq, (H, W, 768, 1, 1, 1, 0, 1), 0, 0)
+            if dwo is not None:
+                K.conv_wgrad(o, None, dy, None, dwo, (H, W, C, 1, 1, 1, 0, 1), 0, 0)
         return dx
     do = conv_backward(rc, ConvSpec(attn.to_out), st.ost, dy)
     dqkv = K.tattn_bwd(st.qkv.view(-1, 768), st.o, do.view(-1, 256), st.lse, rc.bias, rc.rot, rc.dtable, rc.B,
@@ -397,12 +459,13 @@ def sla_bwd(rc, res_mod, st, dy):
         dx, dqkv, o, xn = K.slaf_bwd(st.x, dy, _flat(pre.norm.gamma), wq, wq_t, wo_t, st.state,
                                      gbuf(pre.norm.gamma), sla.scale,
                                      want_wgrad_inputs=dwq is not None or dwo is not None, eps=pre.norm.eps)
-        if dwq is not None:
-            K.conv_wgrad(xn, None, dqkv, None, dwq, (H, W, 768, 1, 1, 1, 0, 1), 0, 0)
-        if dwo is not None:
-            K.conv_wgrad(o, None, dy, None, dwo, (H, W, C, 1, 1, 1, 0, 1), 0, 0)
-        if dbo is not None:
-            K.colsum(dy, dbo)
+        with rc.side(xn, dqkv, o, dy, attn=True):
+            if dwq is not None:
+                K.conv_wgrad(xn, None, dqkv, None, dwq, (H, W, 768, 1, 1, 1, 0, 1), 0, 0)
+            if dwo is not None:
+                K.conv_wgrad(o, None, dy, None, dwo, (H, W, C, 1, 1, 1, 0, 1), 0, 0)
+            if dbo is not None:
+                K.colsum(dy, dbo)
         return dx
     do = conv_backward(rc, ConvSpec(sla.to_out), st.ost, dy)
     dqkv = K.sla_bwd(st.qkv.view(-1, 768), do.view(-1, 256), st.ctx, st.ml, Nb, H * W, sla.scale)
@@ -584,6 +647,13 @@ class UNetModel3D(nn.Module):
         self._tape = None
         rc = tape.rc
         dev = dout.device
+        hook = getattr(self, "_grad_ready", None)
+
+        def done(*mods):  # data-parallel overlap: these modules' gradients are final (distributed.arm)
+            if hook is not None:
+                hook([p for m in mods for p in m.parameters()], rc.wstream)
+        if WGRAD_STREAM != "0" and dout.is_cuda:
+            rc.wstream = _wgrad_stream(dev)
         rc.dt = torch.zeros((rc.B, self.time_mlp[1].out_features), dtype=torch.float32, device=dev)
         rc.dtable = gbuf(self.time_rel_pos_bias.relative_attention_bias.weight)
         head = self.out_conv[1]
@@ -591,6 +661,7 @@ class UNetModel3D(nn.Module):
         dx = K.head_bwd(dout.contiguous(), tape.head_in, head.weight.reshape(-1),
                         None if hw is None else hw.view(-1), hb, rc.B, rc.F)
         dx, dr = resnet_bwd(rc, self.out_conv[0], tape.out_rb, dx)
+        done(self.out_conv)
         nres = len(self.downs)
         dskips = [None] * nres
         for j in reversed(range(len(self.ups))):
@@ -604,9 +675,11 @@ class UNetModel3D(nn.Module):
             dx = resnet_bwd(rc, b2, s.b2, dx)
             dx, dskip = resnet_bwd(rc, b1, s.b1, dx)
             dskips[nres - 1 - j] = dskip
+            done(self.ups[j])
         dx = resnet_bwd(rc, self.mid_block2, tape.mid2, dx)
         dx = tattn_bwd(rc, self.mid_temporal_attn, tape.mid_attn, dx)
         dx = resnet_bwd(rc, self.mid_block1, tape.mid1, dx)
+        done(self.mid_block1, self.mid_temporal_attn, self.mid_block2)
         for i in reversed(range(nres)):
             b1, b2, sa, ta, down = self.downs[i]
             s = tape.downs[i]
@@ -619,18 +692,21 @@ class UNetModel3D(nn.Module):
                 dx = sla_bwd(rc, sa, s.sa, dx)
             dx = resnet_bwd(rc, b2, s.b2, dx)
             dx = resnet_bwd(rc, b1, s.b1, dx)
+            done(self.downs[i])
         dx = K.add(dx, dr)
         dx = tattn_bwd(rc, self.input_temp_op, tape.in_attn, dx)
         wi, bi = gbuf(self.input_conv.weight), gbuf(self.input_conv.bias)
-        if wi is not None:
-            K.stem_wgrad(tape.x_t, tape.cond, dx, wi, rc.F)
-        if bi is not None:
-            K.colsum(dx, bi)
+        with rc.side(tape.x_t, tape.cond, dx):
+            if wi is not None:
+                K.stem_wgrad(tape.x_t, tape.cond, dx, wi, rc.F)
+            if bi is not None:
+                K.colsum(dx, bi)
         # time MLP: temb = Lin3(SiLU(Lin1(emb)))
         l1, l3 = self.time_mlp[1], self.time_mlp[3]
         dh1 = torch.empty_like(tape.h1)
         K.linear_small_bwd(tape.h1, l3.weight, rc.dt, dh1, gbuf(l3.weight), gbuf(l3.bias), True, False)
         K.linear_small_bwd(tape.emb, l1.weight, dh1, None, gbuf(l1.weight), gbuf(l1.bias), False, False)
+        rc.join()
 
 
 class _NetFunction(torch.autograd.Function):

@@ -86,3 +86,58 @@ def test_bucketing_covers_buffer():
     b = r.buckets(95)
     assert b[0] == (0, 10) and b[-1] == (90, 95)
     assert sum(e - s for s, e in b) == 95
+
+
+def _overlap_worker(rank, world, port, out_path):
+    """The overlapped path: buckets are reduced from the end of the flat buffer as the backward
+    reports parameter groups final (reverse construction order), the rest in finish()."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from types import SimpleNamespace
+    from cesm_emulator_amd import distributed as D
+    D.setup(backend="gloo")
+    sizes = [7, 130, 64, 300, 5, 90]
+    offs, o = [], 0
+    for n in sizes:
+        offs.append(o)
+        o += (n + 63) // 64 * 64
+    g = torch.zeros(o)
+    params = [torch.nn.Parameter(torch.zeros(n)) for n in sizes]
+    gen = torch.Generator().manual_seed(100 + rank)
+    for n, off in zip(sizes, offs):
+        g[off:off + n] = torch.randn(n, generator=gen)
+    flat = SimpleNamespace(params=params, offsets=offs, grad=g)
+    net = SimpleNamespace(_grad_ready=None)
+    red = D.GradAllReducer(bucket_bytes=4 * 100)
+    red.arm(net, flat)
+    issued = []
+    for grp in ([5], [4, 3], [2], [1]):  # reverse construction order; param 0 is the shared one
+        net._grad_ready([params[i] for i in grp])
+        issued.append(red._armed["lo"])
+    red.finish(net)
+    torch.save({"g": g, "issued": torch.tensor(issued)}, out_path + f".{rank}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_overlapped_allreduce_matches_average(tmp_path):
+    out = str(tmp_path / "ov.pt")
+    mp.spawn(_overlap_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    r0 = torch.load(out + ".0", weights_only=True)
+    r1 = torch.load(out + ".1", weights_only=True)
+    torch.testing.assert_close(r0["g"], r1["g"])
+    sizes = [7, 130, 64, 300, 5, 90]
+    offs, o = [], 0
+    for n in sizes:
+        offs.append(o)
+        o += (n + 63) // 64 * 64
+    exp = torch.zeros(o)
+    for rank in (0, 1):
+        gen = torch.Generator().manual_seed(100 + rank)
+        for n, off in zip(sizes, offs):
+            exp[off:off + n] += torch.randn(n, generator=gen) / 2
+    torch.testing.assert_close(r0["g"], exp)
+    lo = r0["issued"].tolist()
+    # buckets went out before finish(): after the last group only the shared param's bucket is left
+    assert lo[0] < o and lo[-1] <= 64 and lo == sorted(lo, reverse=True), lo
