@@ -91,16 +91,16 @@ __global__ __launch_bounds__(512) void slaf_stats_kernel(const bf16* __restrict_
     // LN of 64 pixels into xs (rows beyond HW zero)
     {
       const int sub = tid % L;
+      float gm8[8];
+      load8(gamma + sub * 8, gm8);
 #pragma unroll
       for (int pp0 = 0; pp0 < 64; pp0 += PPP) {
         const int pl = pp0 + tid / L;
         const int p = p0 + pl;
         float a[8];
-        if (p < HW) load8(xf + (int64_t)p * C + sub * 8, a);
-        else {
+        load8(xf + (int64_t)(p < HW ? p : 0) * C + sub * 8, a);  // unpredicated (row 0 past HW), selected
 #pragma unroll
-          for (int i = 0; i < 8; ++i) a[i] = 0.f;
-        }
+        for (int i = 0; i < 8; ++i) a[i] = p < HW ? a[i] : 0.f;
         float sm = 0.f;
 #pragma unroll
         for (int i = 0; i < 8; ++i) sm += a[i];
@@ -112,7 +112,7 @@ __global__ __launch_bounds__(512) void slaf_stats_kernel(const bf16* __restrict_
         q = group_sum(q, L);
         const float rstd = 1.f / sqrtf(q / C + eps);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) a[i] = p < HW ? (a[i] - mean) * rstd * gamma[sub * 8 + i] : 0.f;
+        for (int i = 0; i < 8; ++i) a[i] = p < HW ? (a[i] - mean) * rstd * gm8[i] : 0.f;
         store8(xs + pl * XLD + sub * 8, a);
       }
     }
@@ -312,6 +312,9 @@ __global__ __launch_bounds__(256) void slaf_out_kernel(const bf16* __restrict__ 
   if (p0 >= HW) return;
   const bf16* xb = x + (int64_t)n * HW * C;
   // LN on the B fragments: lane (g, i) holds pixel p0 + vt*16 + i, channels ks*32 + 8g..8g+7
+  float gm[KS][8];  // gamma hoisted: under the lane predicate each element was its own load + vmcnt(0)
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) load8(gamma + ks * 32 + lg * 8, gm[ks]);
   bf16x8 xf[NV][KS];
 #pragma unroll
   for (int vt = 0; vt < NV; ++vt) {
@@ -319,12 +322,10 @@ __global__ __launch_bounds__(256) void slaf_out_kernel(const bf16* __restrict__ 
     const bool ok = p < HW;
     float a[KS][8];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      if (ok) load8(xb + (int64_t)p * C + ks * 32 + lg * 8, a[ks]);
-      else {
+    for (int ks = 0; ks < KS; ++ks) {  // unpredicated loads (row 0 past HW), then selected
+      load8(xb + (int64_t)(ok ? p : 0) * C + ks * 32 + lg * 8, a[ks]);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) a[ks][i] = 0.f;
-      }
+      for (int i = 0; i < 8; ++i) a[ks][i] = ok ? a[ks][i] : 0.f;
     }
     float sm = 0.f;
 #pragma unroll
@@ -341,7 +342,7 @@ __global__ __launch_bounds__(256) void slaf_out_kernel(const bf16* __restrict__ 
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) xf[vt][ks][i] = (bf16)(ok ? (a[ks][i] - mean) * rstd * gamma[ks * 32 + lg * 8 + i] : 0.f);
+      for (int i = 0; i < 8; ++i) xf[vt][ks][i] = (bf16)(ok ? (a[ks][i] - mean) * rstd * gm[ks][i] : 0.f);
   }
   f32x4 yacc[CT][NV];
 #pragma unroll
@@ -495,18 +496,18 @@ __global__ __launch_bounds__(512) void slab_dctx_kernel(const bf16* __restrict__
     __syncthreads();
     {
       const int sub = tid % L;
+      float gm8[8];
+      load8(gamma + sub * 8, gm8);
 #pragma unroll
       for (int pp0 = 0; pp0 < 64; pp0 += PPP) {
         const int pl = pp0 + tid / L;
         const int p = p0 + pl;
         float a[8], d8[8];
-        if (p < HW) {
-          load8(xb + (int64_t)p * C + sub * 8, a);
-          load8(db + (int64_t)p * C + sub * 8, d8);
-        } else {
+        const int64_t ps = p < HW ? p : 0;  // unpredicated loads (row 0 past HW), then selected
+        load8(xb + ps * C + sub * 8, a);
+        load8(db + ps * C + sub * 8, d8);
 #pragma unroll
-          for (int i = 0; i < 8; ++i) { a[i] = 0.f; d8[i] = 0.f; }
-        }
+        for (int i = 0; i < 8; ++i) { a[i] = p < HW ? a[i] : 0.f; d8[i] = p < HW ? d8[i] : 0.f; }
         float sm = 0.f;
 #pragma unroll
         for (int i = 0; i < 8; ++i) sm += a[i];
@@ -518,7 +519,7 @@ __global__ __launch_bounds__(512) void slab_dctx_kernel(const bf16* __restrict__
         q = group_sum(q, L);
         const float rstd = 1.f / sqrtf(q / C + eps);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) a[i] = p < HW ? (a[i] - mean) * rstd * gamma[sub * 8 + i] : 0.f;
+        for (int i = 0; i < 8; ++i) a[i] = p < HW ? (a[i] - mean) * rstd * gm8[i] : 0.f;
         store8(xs + pl * XLD + sub * 8, a);
         store8(ds + pl * XLD + sub * 8, d8);
       }
@@ -679,12 +680,10 @@ __global__ __launch_bounds__(256, 2) void slab_dx_kernel(
       const bool ok = p < HW;
       float a[KS][8];
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        if (ok) load8(x + (rb + p) * C + ks * 32 + lg * 8, a[ks]);
-        else {
+      for (int ks = 0; ks < KS; ++ks) {  // unpredicated loads (row 0 past HW), then selected
+        load8(x + (rb + (ok ? p : 0)) * C + ks * 32 + lg * 8, a[ks]);
 #pragma unroll
-          for (int i = 0; i < 8; ++i) a[ks][i] = 0.f;
-        }
+        for (int i = 0; i < 8; ++i) a[ks][i] = ok ? a[ks][i] : 0.f;
       }
       float sm = 0.f;
 #pragma unroll
@@ -717,7 +716,10 @@ __global__ __launch_bounds__(256, 2) void slab_dx_kernel(
     for (int vt = 0; vt < NV; ++vt) {
       const int p = p0 + vt * 16 + lr;
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) dyr[vt][ks] = p < HW ? ld16(dy + (rb + p) * C + ks * 32 + lg * 8) : zero8();
+      for (int ks = 0; ks < KS; ++ks) {  // unpredicated (row 0 past HW), then selected
+        const bf16x8 v = ld16(dy + (rb + (p < HW ? p : 0)) * C + ks * 32 + lg * 8);
+        dyr[vt][ks] = p < HW ? v : zero8();
+      }
     }
 
     for (int h = 0; h < NH; ++h) {
@@ -867,8 +869,8 @@ __global__ __launch_bounds__(256, 2) void slab_dx_kernel(
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
         const int co = ct * 16 + lg * 4;
-        float xv[4] = {0.f, 0.f, 0.f, 0.f};
-        if (ok) load4(x + (rb + p) * C + co, xv);
+        float xv[4];
+        load4(x + (rb + (ok ? p : 0)) * C + co, xv);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           xh[ct][r] = ok ? (xv[r] - mean[vt]) * rstd[vt] : 0.f;
@@ -893,9 +895,10 @@ __global__ __launch_bounds__(256, 2) void slab_dx_kernel(
 #pragma unroll
           for (int r = 0; r < 4; ++r) atomicAdd(&sg[co + r], d4[r]);
         }
+        float dv4[4];
+        load4(dy + (rb + (ok ? p : 0)) * C + co, dv4);
         if (ok) {
-          float dv4[4], o4[4];
-          load4(dy + (rb + p) * C + co, dv4);
+          float o4[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) o4[r] = rstd[vt] * (dxacc[ct][vt][r] * sgm[co + r] - s1 - xh[ct][r] * s2) + dv4[r];
           store4(dx + (rb + p) * C + co, o4);

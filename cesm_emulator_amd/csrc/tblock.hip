@@ -670,6 +670,9 @@ __device__ __forceinline__ unsigned long long tw_stamp() {
 #define TW_ST_FLUSH(w)
 #endif
 
+#ifndef TW_FWD_PG
+#define TW_FWD_PG 1  // pixels per interleaved attention-core group in tw_fwd (2 / 4 measured neutral)
+#endif
 constexpr int RS = 36;  // RoPE table row stride (floats): 16-B aligned, spreads frames over banks
 constexpr float LOG2E = 1.4426950408889634f;
 
@@ -696,6 +699,8 @@ __device__ __forceinline__ void rope4(float* o4, const float* rot, int f, int d0
     o4[2 * pr + 1] = a1 * c + a0 * sn;
   }
 }
+
+__device__ __forceinline__ bf16x8 sel8(bool ok, bf16x8 v) { return ok ? v : zero8(); }
 
 // rows of voxel v of the wave's pixel group
 __device__ __forceinline__ bool tw_row(int v, int VW, int F, int p0, int HW, int b, int64_t& row) {
@@ -746,11 +751,11 @@ __device__ __forceinline__ void tw_qkv_pre(const bf16x8 (&a)[6][C / 32],
   }
 }
 
-template <int C, int NV>
+template <int C, int NV, bool FULL = (C <= 64)>
 __device__ __forceinline__ void tw_qkv(const bf16* __restrict__ wqkv, const bf16x8 (&xf)[TW<C, NV>::NVTM][TW<C, NV>::KS],
                                        int h, const int (&fr)[NV], float scale, const float* rot, bf16* sq, bf16* sk,
                                        bf16* sv, int lr, int lg) {
-  if constexpr (C <= 64) {
+  if constexpr (FULL) {
     bf16x8 a[6][C / 32];
     tw_load_wq<C, NV>(a, wqkv, h, lr, lg);
     tw_qkv_pre<C, NV>(a, xf, fr, scale, rot, sq, sk, sv, lr, lg);
@@ -797,24 +802,36 @@ __device__ __forceinline__ void tw_ln(const bf16* __restrict__ x, const float* _
                                       const float* __restrict__ mr_in, bf16x8 (&xf)[TW<C, NV>::NVTM][TW<C, NV>::KS], int NVT,
                                       int VW, int F, int p0, int HW, int b, float eps, int lr, int lg) {
   using T = TW<C, NV>;
+  // every load is unconditional (invalid voxels read row 0 and are zeroed by a select): a load under a
+  // lane predicate becomes a branch with its own vmcnt(0), which serialised the 16 gamma and 2 x loads
+  // of every voxel tile
+  float gm[T::KS][8];
+#pragma unroll
+  for (int ks = 0; ks < T::KS; ++ks) load8(gamma + ks * 32 + lg * 8, gm[ks]);
+  bf16x8 raw[T::NVTM][T::KS];
+  bool okv[T::NVTM];
+  int64_t rows[T::NVTM];
 #pragma unroll
   for (int vt = 0; vt < T::NVTM; ++vt) {
-    if (vt >= NVT) break;
     int64_t row = 0;
-    const bool ok = tw_row(vt * 16 + lr, VW, F, p0, HW, b, row);
+    okv[vt] = vt < NVT && tw_row(vt * 16 + lr, VW, F, p0, HW, b, row);
+    rows[vt] = okv[vt] ? row : 0;
+#pragma unroll
+    for (int ks = 0; ks < T::KS; ++ks) raw[vt][ks] = ld16(x + rows[vt] * C + ks * 32 + lg * 8);
+  }
+#pragma unroll
+  for (int vt = 0; vt < T::NVTM; ++vt) {
+    const bool ok = okv[vt];
     float a[T::KS][8];
 #pragma unroll
-    for (int ks = 0; ks < T::KS; ++ks) {
-      if (ok) load8(x + row * C + ks * 32 + lg * 8, a[ks]);
-      else {
+    for (int ks = 0; ks < T::KS; ++ks)
 #pragma unroll
-        for (int i = 0; i < 8; ++i) a[ks][i] = 0.f;
-      }
-    }
+      for (int i = 0; i < 8; ++i) a[ks][i] = ok ? (float)raw[vt][ks][i] : 0.f;
     float mean, rstd;
     if (mr_in) {
-      mean = ok ? mr_in[row * 2] : 0.f;
-      rstd = ok ? mr_in[row * 2 + 1] : 0.f;
+      const float m0 = mr_in[rows[vt] * 2], r0 = mr_in[rows[vt] * 2 + 1];
+      mean = ok ? m0 : 0.f;
+      rstd = ok ? r0 : 0.f;
     } else {
       float s = 0.f;
 #pragma unroll
@@ -830,18 +847,24 @@ __device__ __forceinline__ void tw_ln(const bf16* __restrict__ x, const float* _
         for (int i = 0; i < 8; ++i) { const float d = a[ks][i] - mean; q = fmaf(d, d, q); }
       q = grp4_sum(q);
       rstd = 1.f / sqrtf(q / C + eps);
-      if (ok && lg == 0 && mr_out) { mr_out[row * 2] = mean; mr_out[row * 2 + 1] = rstd; }
+      if (ok && lg == 0 && mr_out) { mr_out[rows[vt] * 2] = mean; mr_out[rows[vt] * 2 + 1] = rstd; }
     }
 #pragma unroll
     for (int ks = 0; ks < T::KS; ++ks)
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-        xf[vt][ks][i] = (bf16)(ok ? (a[ks][i] - mean) * rstd * gamma[ks * 32 + lg * 8 + i] : 0.f);
+      for (int i = 0; i < 8; ++i) xf[vt][ks][i] = (bf16)(ok ? (a[ks][i] - mean) * rstd * gm[ks][i] : 0.f);
   }
 }
 
+// waves per SIMD of tw_fwd: at C = 64 LDS-bound (per-wave q/k/v slices + tables: 3 blocks of 53 KB);
+// at C >= 128 register-bound (the out-projection accumulators spill below 256 VGPRs)
+#ifndef TW_FWD_OCC64
+#define TW_FWD_OCC64 3
+#endif
+template <int C>
+constexpr int tw_fwd_occ() { return C <= 64 ? TW_FWD_OCC64 : 2; }
 template <int C, int NV>
-__global__ __launch_bounds__(256, 2) void tw_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ gamma,
+__global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ gamma,
                                                      const bf16* __restrict__ wqkv, const bf16* __restrict__ wout,
                                                      const float* __restrict__ bias, const float* __restrict__ rotg,
                                                      bf16* __restrict__ y, float* __restrict__ mr,
@@ -849,8 +872,8 @@ __global__ __launch_bounds__(256, 2) void tw_fwd_kernel(const bf16* __restrict__
                                                      float scale, float eps) {
   using T = TW<C, NV>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* sb = smem;             // [8][F][F], pre-scaled by log2(e)
-  float* rot = smem + NH * 256; // [16][RS]
+  float* sb = smem;                              // [8][F][F], pre-scaled by log2(e)
+  float* rot = smem + ((NH * F * F + 3) & ~3);   // [16][RS]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const int b = blockIdx.y;
@@ -879,18 +902,22 @@ __global__ __launch_bounds__(256, 2) void tw_fwd_kernel(const bf16* __restrict__
     for (int vt = 0; vt < T::NVTM; ++vt) yacc[ct][vt] = f32x4{0.f, 0.f, 0.f, 0.f};
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
 
-  constexpr bool PREF = C <= 64;  // next head's QKV weights prefetched into registers (48 VGPRs at C=64)
+  // next head's QKV weights prefetched into registers (48 VGPRs at C=64): only at 2 waves / SIMD, where
+  // the register budget has room and there is no third wave to hide the weight loads
+  constexpr bool PREF = C <= 64 && tw_fwd_occ<C>() <= 2;
   bf16x8 wq[6][PREF ? T::KS : 1];
   if constexpr (PREF) tw_load_wq<C, NV>(wq, wqkv, 0, lr, lg);
   for (int h = 0; h < NH; ++h) {
     bf16x8 wo[T::CT];
+    if constexpr (PREF) {
 #pragma unroll
-    for (int ct = 0; ct < T::CT; ++ct) wo[ct] = ld_img(wout, ct, INNER / 32, h, lane);  // image of W_out [C][256]
+      for (int ct = 0; ct < T::CT; ++ct) wo[ct] = ld_img(wout, ct, INNER / 32, h, lane);  // image of W_out [C][256]
+    }
     if constexpr (PREF) {
       tw_qkv_pre<C, NV>(wq, xf, fr, scale, rot, sq, sk, sv, lr, lg);
       if (h + 1 < NH) tw_load_wq<C, NV>(wq, wqkv, h + 1, lr, lg);  // in flight during the core
     } else {
-      tw_qkv<C, NV>(wqkv, xf, h, fr, scale, rot, sq, sk, sv, lr, lg);
+      tw_qkv<C, NV, false>(wqkv, xf, h, fr, scale, rot, sq, sk, sv, lr, lg);  // two-tile weight batches
     }
     // bias (log2 units) of this lane's 4 entries (i = lr, j = 4g + r); -inf masks padding frames
     float bt[4];
@@ -900,45 +927,68 @@ __global__ __launch_bounds__(256, 2) void tw_fwd_kernel(const bf16* __restrict__
       bt[r] = (j < F && lr < F) ? sb[(h * F + lr) * F + j] : -INFINITY;
     }
     wave_lds_sync();
-    // attention core per pixel (base-2 softmax); O overwrites the pixel's own q rows
-    for (int pp = 0; pp < T::PW; ++pp) {
-      const int p = p0 + pp;
-      if (p >= HW) break;
-      const int rb = pp * F;
-      const bf16x8 ka = lr < F ? ld16(sk + (rb + lr) * HLD + lg * 8) : zero8();
-      const bf16x8 qb = lr < F ? ld16(sq + (rb + lr) * HLD + lg * 8) : zero8();
-      const f32x4 st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qb, z4, 0, 0, 0);
-      float sc[4];
-      float m = -INFINITY;
+    // attention core, base-2 softmax; O overwrites the pixel's own q rows.  Pixels go in groups of PG
+    // with each phase issued for the whole group (independent MFMA -> softmax -> MFMA chains
+    // interleave instead of serialising on the MFMA result latency).  Pixels past HW hold zero rows
+    // (their LN input is masked): computing them is harmless, only the lse store is guarded.
+    constexpr int PG = TW_FWD_PG < T::PW ? TW_FWD_PG : T::PW;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        sc[r] = fmaf(st[r], LOG2E, bt[r]);
-        m = fmaxf(m, sc[r]);
+    for (int pg = 0; pg < T::PW; pg += PG) {
+      f32x4 st[PG];
+#pragma unroll
+      for (int u = 0; u < PG; ++u) {
+        const int rb = (pg + u) * F;
+        const int rr = rb + (lr < F ? lr : 0);  // unpredicated LDS reads, zeroed after
+        const bf16x8 ka = sel8(lr < F, ld16(sk + rr * HLD + lg * 8));
+        const bf16x8 qb = sel8(lr < F, ld16(sq + rr * HLD + lg * 8));
+        st[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qb, z4, 0, 0, 0);
       }
-      m = grp4_max(m);
-      float pr[4], l = 0.f;
+      bf16x8 va[PG][2];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        pr[r] = sc[r] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(sc[r] - m);
-        l += pr[r];
+      for (int u = 0; u < PG; ++u)
+#pragma unroll
+        for (int half = 0; half < 2; ++half) va[u][half] = kslot_gather(sv, (pg + u) * F, half * 16, F, lane);
+      bf16x8 pb[PG];
+#pragma unroll
+      for (int u = 0; u < PG; ++u) {
+        const int p = p0 + pg + u;
+        float sc[4];
+        float m = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          sc[r] = fmaf(st[u][r], LOG2E, bt[r]);
+          m = fmaxf(m, sc[r]);
+        }
+        m = grp4_max(m);
+        float pr[4], l = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pr[r] = sc[r] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(sc[r] - m);
+          l += pr[r];
+        }
+        l = grp4_sum(l);
+        if (lse && lg == 0 && lr < F && p < HW) lse[(((int64_t)b * NH + h) * HW + p) * F + lr] = m + log2f(l);  // log2 units
+        const float inv = lr < F ? __builtin_amdgcn_rcpf(l) : 0.f;
+        pb[u] = zero8();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pb[u][r] = (bf16)(pr[r] * inv);
       }
-      l = grp4_sum(l);
-      if (lse && lg == 0 && lr < F) lse[(((int64_t)b * NH + h) * HW + p) * F + lr] = m + log2f(l);  // log2 units
-      const float inv = lr < F ? __builtin_amdgcn_rcpf(l) : 0.f;
-      bf16x8 pb = zero8();
 #pragma unroll
-      for (int r = 0; r < 4; ++r) pb[r] = (bf16)(pr[r] * inv);
-      bf16x8 va[2];
+      for (int u = 0; u < PG; ++u) {
+        const int rb = (pg + u) * F;
 #pragma unroll
-      for (int half = 0; half < 2; ++half) va[half] = kslot_gather(sv, rb, half * 16, F, lane);
-#pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        const f32x4 ot = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va[half], pb, z4, 0, 0, 0);
-        if (lr < F) {
-          float o4[4] = {ot[0], ot[1], ot[2], ot[3]};
-          store4(sq + (rb + lr) * HLD + half * 16 + lg * 4, o4);
+        for (int half = 0; half < 2; ++half) {
+          const f32x4 ot = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va[u][half], pb[u], z4, 0, 0, 0);
+          if (lr < F) {
+            float o4[4] = {ot[0], ot[1], ot[2], ot[3]};
+            store4(sq + (rb + lr) * HLD + half * 16 + lg * 4, o4);
+          }
         }
       }
+    }
+    if constexpr (!PREF) {  // issued after the core: keeps the 16 registers out of the qkv phase
+#pragma unroll
+      for (int ct = 0; ct < T::CT; ++ct) wo[ct] = ld_img(wout, ct, INNER / 32, h, lane);
     }
     wave_lds_sync();
     // y^T += W_out[:, h] . O_h^T
@@ -1050,7 +1100,8 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
 #pragma unroll
       for (int vt = 0; vt < T::NVTM; ++vt)
 #pragma unroll
-        for (int ks = 0; ks < T::KS; ++ks) dyr[vt][ks] = vrow[vt] >= 0 ? ldnt16(dy + vrow[vt] * C + ks * 32 + lg * 8) : zero8();
+        for (int ks = 0; ks < T::KS; ++ks)  // unconditional load (row 0 when outside), then select
+          dyr[vt][ks] = sel8(vrow[vt] >= 0, ldnt16(dy + (vrow[vt] >= 0 ? vrow[vt] : 0) * C + ks * 32 + lg * 8));
     }
 
     TW_ST(0)
@@ -1060,8 +1111,15 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
       constexpr bool LPF = C <= 64;  // at C = 128 the 2 extra registers cost spills
       float Lp[T::PW];
 #pragma unroll
-      for (int pp = 0; pp < T::PW; ++pp)
-        Lp[pp] = (LPF && lr < F && p0 + pp < HW) ? lse[(((int64_t)b * NH + h) * HW + p0 + pp) * F + lr] : 0.f;
+      for (int pp = 0; pp < T::PW; ++pp) {
+        if constexpr (LPF) {
+          const bool ok = lr < F && p0 + pp < HW;
+          const float v = lse[(((int64_t)b * NH + h) * HW + (ok ? p0 + pp : 0)) * F + (ok ? lr : 0)];
+          Lp[pp] = ok ? v : 0.f;
+        } else {
+          Lp[pp] = 0.f;
+        }
+      }
       tw_qkv<C, NV>(wqkv, xf, h, fr, scale, rot, sq, sk, sv, lr, lg);
       TW_ST(1)
       // dO_h^T = W_out[:, h]^T . dy^T
@@ -1078,7 +1136,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
             for (int ks = 0; ks < T::KS; ++ks) {
               bf16x8 dyf;
               if constexpr (DYREG) dyf = dyr[vt][ks];
-              else dyf = vrow[vt] >= 0 ? ld16(dy + vrow[vt] * C + ks * 32 + lg * 8) : zero8();
+              else dyf = sel8(vrow[vt] >= 0, ld16(dy + (vrow[vt] >= 0 ? vrow[vt] : 0) * C + ks * 32 + lg * 8));
               acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], dyf, acc, 0, 0, 0);
             }
             float o4[4] = {acc[0], acc[1], acc[2], acc[3]};
@@ -1108,12 +1166,14 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
 #pragma unroll
           for (int q = 1; q < T::PW; ++q) Li = pp == q ? Lp[q] : Li;
         } else {
-          Li = lr < F ? lse[(((int64_t)b * NH + h) * HW + p) * F + lr] : 0.f;
+          const float v = lse[(((int64_t)b * NH + h) * HW + p) * F + (lr < F ? lr : 0)];
+          Li = lr < F ? v : 0.f;
         }
-        const bf16x8 kr = lr < F ? ld16(sk + (rb + lr) * HLD + lg * 8) : zero8();
-        const bf16x8 qr = lr < F ? ld16(sq + (rb + lr) * HLD + lg * 8) : zero8();
-        const bf16x8 vr = lr < F ? ld16(sv + (rb + lr) * HLD + lg * 8) : zero8();
-        const bf16x8 dor = lr < F ? ld16(sdo + (rb + lr) * HLD + lg * 8) : zero8();
+        const int rr = rb + (lr < F ? lr : 0);  // LDS reads unpredicated: a row of this pixel, zeroed after
+        const bf16x8 kr = sel8(lr < F, ld16(sk + rr * HLD + lg * 8));
+        const bf16x8 qr = sel8(lr < F, ld16(sq + rr * HLD + lg * 8));
+        const bf16x8 vr = sel8(lr < F, ld16(sv + rr * HLD + lg * 8));
+        const bf16x8 dor = sel8(lr < F, ld16(sdo + rr * HLD + lg * 8));
         // -- transposed orientation: lane (g, i): entries (j = 4g + r, i)
         float D = 0.f;
         bf16x8 dst_b = zero8(), pt_b = zero8();
@@ -1235,14 +1295,16 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
       if (vt >= NVT) break;
       int64_t row = 0;
       const bool ok = tw_row(vt * 16 + lr, VW, F, p0, HW, b, row);
-      const float mean = ok ? mr[row * 2] : 0.f, rstd = ok ? mr[row * 2 + 1] : 0.f;
+      row = ok ? row : 0;  // loads unpredicated (row 0 outside the group), results selected
+      const float m0 = mr[row * 2], r0 = mr[row * 2 + 1];
+      const float mean = ok ? m0 : 0.f, rstd = ok ? r0 : 0.f;
       float s1 = 0.f, s2 = 0.f;
       float xh[T::CT][4];
 #pragma unroll
       for (int ct = 0; ct < T::CT; ++ct) {
         const int co = ct * 16 + lg * 4;
-        float xv[4] = {0.f, 0.f, 0.f, 0.f};
-        if (ok) ldnt4(x + row * C + co, xv);
+        float xv[4];
+        ldnt4(x + row * C + co, xv);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           xh[ct][r] = ok ? (xv[r] - mean) * rstd : 0.f;
@@ -1272,9 +1334,10 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
             for (int r = 0; r < 4; ++r) atomicAdd(&sg[co + r], d4[r]);
           }
         }
+        float dv[4];
+        ldnt4(dy + row * C + co, dv);
         if (ok) {
-          float dv[4], o4[4];
-          ldnt4(dy + row * C + co, dv);
+          float o4[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) o4[r] = rstd * (dxacc[ct][vt][r] * sgm[co + r] - s1 - xh[ct][r] * s2) + dv[r];
           stnt4(dx + row * C + co, o4);
@@ -1315,7 +1378,7 @@ __global__ void tb_sum_rows_kernel(const float* __restrict__ part, float* __rest
 template <int C>
 static size_t tw_fwd_smem(int F) {  // NOLINT
   const int R = ((TW<C>::PW * F + 15) / 16) * 16;
-  return (size_t)(NH * 256 + 16 * RS) * 4 + (size_t)4 * 3 * R * HLD * 2;
+  return (size_t)(((NH * F * F + 3) & ~3) + 16 * RS) * 4 + (size_t)4 * 3 * R * HLD * 2;
 }
 template <int C>
 static size_t tw_bwd_smem(int F) {

@@ -1,0 +1,75 @@
+"""HIP-event timing of the level-0 fused temporal / SLA block kernels (A/B of variant libraries:
+CESM_HIP_LIB=... python tools/tblock_time.py [C] [reps])."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from cesm_emulator_amd import kernels as K  # noqa: E402
+
+
+def timed(fn, reps):
+    fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps * 1e3
+
+
+def main():
+    C = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    B, F = 4, 12
+    H, W = {64: (192, 288), 128: (96, 144)}[C]
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    x = torch.randn(B * F, H, W, C, device=dev).to(torch.bfloat16)
+    dy = torch.randn_like(x)
+    gamma = torch.ones(C, device=dev)
+    wqkv = torch.randn(768, C, device=dev) * C ** -0.5
+    wout = torch.randn(C, 256, device=dev) * 256 ** -0.5
+    wq = K.conv_pack(wqkv, torch.bfloat16, 768, C, 1, 1, 0, 0)
+    wo = K.conv_pack(wout, torch.bfloat16, C, 256, 1, 1, 0, 0)
+    wq_t = K.conv_pack(wqkv, torch.bfloat16, C, 768, 1, 1, 1, 1)
+    wo_t = K.conv_pack(wout, torch.bfloat16, 256, C, 1, 1, 1, 1)
+    bias = K.relpos_fwd(torch.randn(32, 8, device=dev), F)
+    rot = K.rope_table(1.0 / (10000 ** (torch.arange(0, 32, 2, device=dev).float() / 32)), F)
+    dgamma = torch.zeros(C, device=dev)
+    dtable = torch.zeros(32, 8, device=dev)
+    st = {}
+
+    def fwd():
+        st["r"] = K.tblock_fwd(x, gamma, wq, wo, bias, rot, B, F, 32 ** -0.5, save_o=True)
+
+    tf = timed(fwd, reps)
+    y, mr, lse, o = st["r"]
+
+    def bwd():
+        K.tblock_bwd(x, dy, gamma, mr, lse, wq, wq_t, wo_t, bias, rot, dgamma, dtable, B, F, 32 ** -0.5,
+                     want_wgrad_inputs=True, emit_o=False)
+
+    tb = timed(bwd, reps)
+    bout = torch.randn(C, device=dev) * 0.1
+
+    def sfwd():
+        st["s"] = K.slaf_fwd(x, gamma, wq, wo, bout, 32 ** -0.5)
+
+    sf = timed(sfwd, reps)
+    ys, sst = st["s"]
+
+    def sbwd():
+        K.slaf_bwd(x, dy, gamma, wq, wq_t, wo_t, sst, dgamma, 32 ** -0.5, want_wgrad_inputs=True)
+
+    sb = timed(sbwd, reps)
+    lib = os.environ.get("CESM_HIP_LIB", "default")
+    print(f"{lib}: C={C} tw_fwd {tf:.1f} us  tw_bwd {tb:.1f} us  sla_fwd {sf:.1f} us  sla_bwd {sb:.1f} us  "
+          f"y {float(y.float().abs().mean()):.6f} ys {float(ys.float().abs().mean()):.6f}")
+
+
+if __name__ == "__main__":
+    main()
