@@ -253,6 +253,32 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const T* __restrict__ x1,
 }
 
 // ----------------------------------------------------------------------------------------
+// Conv epilogue loads, issued together and unpredicated.  Under lane predicates (pixel valid,
+// channel half, residual present) every bias / residual load became a branch with its own
+// vmcnt(0), i.e. one full memory round trip per (pixel group, channel tile) in sequence.
+// ----------------------------------------------------------------------------------------
+__device__ __forceinline__ void epi_bias(const float* __restrict__ bias, int co, float (&bv)[4]) {
+  if (bias) {  // uniform (kernel argument)
+    load4(bias + co, bv);
+  } else {
+    bv[0] = bv[1] = bv[2] = bv[3] = 0.f;
+  }
+}
+// residual of output pixel m (ok: inside the image), channels co..co+3, from res (co < Co1) or res2;
+// kept as raw bf16 (2 registers) until the epilogue adds it
+__device__ __forceinline__ bf16x4 epi_res(const bf16* __restrict__ res, const bf16* __restrict__ res2, int64_t m, int co,
+                                          int Co1, int Co2, bool ok) {
+  const bool first = co < Co1;
+  const bf16* rp = first ? res : res2;
+  const bool use = ok && rp != nullptr;
+  const bf16* base = use ? rp : (res ? res : res2);  // some valid address; the value is discarded
+  const int64_t off = use ? (first ? m * Co1 + co : m * Co2 + (co - Co1)) : 0;
+  const bf16x4 t = *reinterpret_cast<const bf16x4*>(base + off);
+  return use ? t : bf16x4{};
+}
+__device__ __forceinline__ float b2f(bf16x4 v, int r) { return (float)v[r]; }
+
+// ----------------------------------------------------------------------------------------
 // bf16 generic implicit GEMM (strided down-sampling convs, transposed up-sampling convs in parity
 // blocks, their data gradients, every conv the halo / 1x1 kernels do not take).  Same tiling and
 // tap/parity enumeration as conv_fwd_kernel, but
@@ -571,37 +597,41 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
   }
   // epilogue: lane holds co = n0 + wr*32 + i*16 + 4*lg + r of pixel (py, px)
   const int Co2 = g.Cout - g.Co1;
+  float bv[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) epi_bias(bias, n0 + wr * 32 + i * 16 + lg * 4, bv[i]);
+  int64_t mj[8];
+  bool okj[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    if (pyx[j] < 0) continue;
     const int oy = y0 + (pyx[j] >> 16), ox = x0 + (pyx[j] & 0xffff);
-    if (oy >= g.Ho || ox >= g.Wo) continue;
-    const int64_t m = ((int64_t)n * g.Ho + oy) * g.Wo + ox;
+    okj[j] = pyx[j] >= 0 && oy < g.Ho && ox < g.Wo;
+    mj[j] = okj[j] ? ((int64_t)n * g.Ho + oy) * g.Wo + ox : 0;
+  }
+  bf16x4 rv[8][2];
+  if (res || res2) {  // uniform
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) rv[j][i] = epi_res(res, res2, mj[j], n0 + wr * 32 + i * 16 + lg * 4, g.Co1, Co2, okj[j]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) rv[j][i] = bf16x4{};
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (!okj[j]) continue;
+    const int64_t m = mj[j];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int co = n0 + wr * 32 + i * 16 + lg * 4;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (bias) {
+      float v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += bias[co + r];
-      }
-      if (co < g.Co1) {
-        if (res) {
-          float rv[4];
-          load4(res + m * g.Co1 + co, rv);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] += rv[r];
-        }
-        store4(y1 + m * g.Co1 + co, v);
-      } else {
-        if (res2) {
-          float rv[4];
-          load4(res2 + m * Co2 + (co - g.Co1), rv);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] += rv[r];
-        }
-        store4(y2 + m * Co2 + (co - g.Co1), v);
-      }
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bv[i][r] + b2f(rv[j][i], r);
+      if (co < g.Co1) store4(y1 + m * g.Co1 + co, v);
+      else store4(y2 + m * Co2 + (co - g.Co1), v);
     }
   }
 }
