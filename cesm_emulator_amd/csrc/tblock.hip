@@ -670,6 +670,9 @@ __device__ __forceinline__ unsigned long long tw_stamp() {
 #define TW_ST_FLUSH(w)
 #endif
 
+#ifndef TW_EMIT_LATE
+#define TW_EMIT_LATE 1  // tw_bwd: dqkv emission after the head's dxn GEMMs (see there)
+#endif
 #ifndef TW_FWD_PG
 #define TW_FWD_PG 1  // pixels per interleaved attention-core group in tw_fwd (2 / 4 measured neutral)
 #endif
@@ -1276,13 +1279,28 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
           for (int vt = 0; vt < T::NVTM; ++vt)
             if (vt < NVT) dxacc[ct][vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bf[vt], dxacc[ct][vt], 0, 0, 0);
         }
-        if (dqkv_out) {
+        if (dqkv_out && !TW_EMIT_LATE) {
 #pragma unroll
           for (int vt = 0; vt < T::NVTM; ++vt) {
             if (vt >= NVT) break;
             int64_t row = 0;
             if (tw_row(vt * 16 + lr, VW, F, p0, HW, b, row))
               stnt16(dqkv_out + row * QKV + kind * INNER + h * DH + lg * 8, bf[vt]);
+          }
+        }
+      }
+      // emission after all of the head's weight loads: a load issued behind a store waits for it
+      // (vmcnt counts both in issue order), so storing between the kinds stalled the next kind's W^T loads
+      if (dqkv_out && TW_EMIT_LATE) {
+#pragma unroll
+        for (int kind = 0; kind < 3; ++kind) {
+          const bf16* src = kind == 0 ? sq : (kind == 1 ? sk : sv);
+#pragma unroll
+          for (int vt = 0; vt < T::NVTM; ++vt) {
+            if (vt >= NVT) break;
+            int64_t row = 0;
+            if (tw_row(vt * 16 + lr, VW, F, p0, HW, b, row))
+              stnt16(dqkv_out + row * QKV + kind * INNER + h * DH + lg * 8, ld16(src + (vt * 16 + lr) * HLD + lg * 8));
           }
         }
       }
