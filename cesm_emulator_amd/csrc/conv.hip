@@ -1114,22 +1114,53 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own writes visible to the wave's other lanes
+      // residual rows of the round in batches of CP_RB loads issued back to back (one load -> wait ->
+      // add -> store chain per row made the residual-fused dgrads 1.7x slower than the plain ones);
+      // the plain path keeps its own loop (uniform branch)
+      constexpr int CP_RB = 4;
+      if (!rsrc) {
 #pragma unroll
-      for (int u = 0; u < 2 * RG; ++u) {
-        if (u < 2 * nj) {
+        for (int u = 0; u < 2 * RG; ++u) {
+          if (u < 2 * nj) {
+            const int pl = u * 8 + (lane >> 3);  // row of the round
+            const int p = wid * 16 * NG + r0 * 16 + pl;
+            const int oy = y0 + p / TW, ox = x0 + (p - (p / TW) * TW);
+            const bool ok = p < TH * TW && oy < g.Ho && ox < g.Wo;
+            const int off = (ok ? oy * g.Wo + ox : 0) * cstride + cofs;
+            const bf16x8 v = *reinterpret_cast<const bf16x8*>(so + pl * CP_ELD + (lane & 7) * 8);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yrs, ok ? off * 2 : 0x7ffffff0, 0, 0);
+          }
+        }
+      } else {
+#pragma unroll
+      for (int u0 = 0; u0 < 2 * RG; u0 += CP_RB) {
+        int offs[CP_RB];
+        bool oks[CP_RB];
+        bf16x8 rv[CP_RB];
+#pragma unroll
+        for (int uu = 0; uu < CP_RB; ++uu) {
+          const int u = u0 + uu;
           const int pl = u * 8 + (lane >> 3);  // row of the round
           const int p = wid * 16 * NG + r0 * 16 + pl;
           const int oy = y0 + p / TW, ox = x0 + (p - (p / TW) * TW);
-          const bool ok = p < TH * TW && oy < g.Ho && ox < g.Wo;
-          const int off = (ok ? oy * g.Wo + ox : 0) * cstride + cofs;
-          bf16x8 v = *reinterpret_cast<const bf16x8*>(so + pl * CP_ELD + (lane & 7) * 8);
-          if (rsrc) {
-            const bf16x8 rv = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rrs, off * 2, 0, 0));
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = (bf16)((float)v[e] + (float)rv[e]);
-          }
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yrs, ok ? off * 2 : 0x7ffffff0, 0, 0);
+          oks[uu] = u < 2 * nj && p < TH * TW && oy < g.Ho && ox < g.Wo;
+          offs[uu] = (oks[uu] ? oy * g.Wo + ox : 0) * cstride + cofs;
+          if (u < 2 * nj)
+            rv[uu] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rrs, offs[uu] * 2, 0, 0));
         }
+#pragma unroll
+        for (int uu = 0; uu < CP_RB; ++uu) {
+          const int u = u0 + uu;
+          if (u < 2 * nj) {
+            const int pl = u * 8 + (lane >> 3);
+            bf16x8 v = *reinterpret_cast<const bf16x8*>(so + pl * CP_ELD + (lane & 7) * 8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = (bf16)((float)v[e] + (float)rv[uu][e]);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yrs, oks[uu] ? offs[uu] * 2 : 0x7ffffff0,
+                                                   0, 0);
+          }
+        }
+      }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next round overwrites
     }
@@ -1242,23 +1273,37 @@ __global__ __launch_bounds__(256, 2) void gemm1x1_kernel(const bf16* __restrict_
   }
   __syncthreads();
   constexpr int CPR = BN / 8;  // 16-B chunks per pixel row
+  constexpr int NIT = G1_BM * CPR / 256;
   const int Co2 = Cout - Co1;
+  // residual vectors of every iteration issued together, unpredicated (clamped address, selected
+  // after): under the lane predicates each was a branch with its own vmcnt(0)
+  bf16x8 rv[NIT];
+  if (res || res2) {  // uniform
 #pragma unroll
-  for (int it = 0; it < G1_BM * CPR / 256; ++it) {
+    for (int it = 0; it < NIT; ++it) {
+      const int e = it * 256 + tid;
+      const int p = e / CPR, c = e - p * CPR;
+      const int m = m0 + p, co = n0 + c * 8;
+      const bool first = co < Co1;
+      const bf16* rp = first ? res : res2;
+      const bool use = m < M && rp != nullptr;
+      const int64_t off = use ? (first ? (int64_t)m * Co1 + co : (int64_t)m * Co2 + (co - Co1)) : 0;
+      const bf16x8 t = *reinterpret_cast<const bf16x8*>((use ? rp : (res ? res : res2)) + off);
+      rv[it] = use ? t : bf16x8{};
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
     const int e = it * 256 + tid;
     const int p = e / CPR, c = e - p * CPR;
     const int m = m0 + p;
     if (m >= M) continue;
     bf16x8 v = *reinterpret_cast<const bf16x8*>(so + p * ELD + c * 8);
     const int co = n0 + c * 8;
-    bf16* dst;
-    const bf16* rs;
-    if (co < Co1) { dst = y1 + (int64_t)m * Co1 + co; rs = res ? res + (int64_t)m * Co1 + co : nullptr; }
-    else { dst = y2 + (int64_t)m * Co2 + (co - Co1); rs = res2 ? res2 + (int64_t)m * Co2 + (co - Co1) : nullptr; }
-    if (rs) {
-      const bf16x8 rv = *reinterpret_cast<const bf16x8*>(rs);
+    bf16* dst = co < Co1 ? y1 + (int64_t)m * Co1 + co : y2 + (int64_t)m * Co2 + (co - Co1);
+    if (res || res2) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = (bf16)((float)v[q] + (float)rv[q]);
+      for (int q = 0; q < 8; ++q) v[q] = (bf16)((float)v[q] + (float)rv[it][q]);
     }
     *reinterpret_cast<bf16x8*>(dst) = v;
   }
