@@ -303,7 +303,7 @@ template <int C, int NV>
 __global__ __launch_bounds__(256) void slaf_out_kernel(const bf16* __restrict__ x, const float* __restrict__ gamma,
                                                        const bf16* __restrict__ wqkv, const bf16* __restrict__ wout,
                                                        const float* __restrict__ bout, const bf16* __restrict__ actT,
-                                                       bf16* __restrict__ y, int HW, float scale, float eps) {
+                                                       bf16* __restrict__ y, bf16* __restrict__ o_out, int HW, float scale, float eps) {
   constexpr int KS = C / 32, CT = C / 16;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
@@ -417,6 +417,13 @@ __global__ __launch_bounds__(256) void slaf_out_kernel(const bf16* __restrict__ 
       const bf16x8 ob = pack_kslot(ov[0], ov[1]);
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) yacc[ct][vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wo[ct], ob, yacc[ct][vt], 0, 0, 0);
+      if (o_out) {  // O for the to_out weight gradient (the backward then skips its emission)
+        const int p = p0 + vt * 16 + lr;
+        if (p < HW) {
+#pragma unroll
+          for (int et = 0; et < 2; ++et) stnt4(o_out + ((int64_t)n * HW + p) * INNER + h * DH + et * 16 + lg * 4, ov[et]);
+        }
+      }
     }
   }
   // y = x + W_o o + b_o
@@ -944,8 +951,8 @@ int cesm_slaf_nblk(int Nf, int HW) {
 // ctx32 [Nf][8][32][32] fp32, actT / actx [Nf][8][2][64][8] bf16 (ctx as MFMA A fragments).
 // ws: cesm_slaf_nblk(Nf, HW) * Nf * 8 * 1088 floats.
 int cesm_slaf_fwd(const void* x, const float* gamma, const void* wqkv, const void* wout, const float* bout, void* y,
-                  float* mz, float* ctx32, void* actT, void* actx, float* ws, int Nf, int HW, int C, float scale,
-                  float eps, hipStream_t stream) {
+                  void* o, float* mz, float* ctx32, void* actT, void* actx, float* ws, int Nf, int HW, int C,
+                  float scale, float eps, hipStream_t stream) {
   if ((C != 64 && C != 128) || Nf < 1 || HW < 1) return CESM_EUNSUPPORTED;
   const int nsc = (HW + 63) / 64;
   const int nblk = cesm_slaf_nblk(Nf, HW);
@@ -957,10 +964,10 @@ int cesm_slaf_fwd(const void* x, const float* gamma, const void* wqkv, const voi
   slaf_combine_kernel<<<Nf * NH, 256, 0, stream>>>(ws, nblk, mz, ctx32, (bf16*)actT, (bf16*)actx);
   if (C == 64)
     slaf_out_kernel<64, 4><<<dim3((unsigned)cdiv(HW, 64 * 4), Nf), 256, 0, stream>>>(
-        (const bf16*)x, gamma, (const bf16*)wqkv, (const bf16*)wout, bout, (const bf16*)actT, (bf16*)y, HW, scale, eps);
+        (const bf16*)x, gamma, (const bf16*)wqkv, (const bf16*)wout, bout, (const bf16*)actT, (bf16*)y, (bf16*)o, HW, scale, eps);
   else
     slaf_out_kernel<128, 2><<<dim3((unsigned)cdiv(HW, 64 * 2), Nf), 256, 0, stream>>>(
-        (const bf16*)x, gamma, (const bf16*)wqkv, (const bf16*)wout, bout, (const bf16*)actT, (bf16*)y, HW, scale, eps);
+        (const bf16*)x, gamma, (const bf16*)wqkv, (const bf16*)wout, bout, (const bf16*)actT, (bf16*)y, (bf16*)o, HW, scale, eps);
   return cesm_launch_status();
 }
 

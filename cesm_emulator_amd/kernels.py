@@ -346,9 +346,10 @@ def tblock_bwd(x, dy, gamma, mr, lse, wqkv, wqkv_t, wout_t, bias, rot, dgamma, d
 SLAF_C = (64,) if os.environ.get("CESM_SLAF_C64_ONLY") else (64, 128)
 
 
-def slaf_fwd(x, gamma, wqkv, wout, bout, scale, eps=1e-5):
-    """fused spatial-linear-attention block forward (bf16, C=64); x [Nf, H, W, C].
-    Returns y and the saved state (mz, ctx32, actT, actx) for slaf_bwd."""
+def slaf_fwd(x, gamma, wqkv, wout, bout, scale, eps=1e-5, save_o=False):
+    """fused spatial-linear-attention block forward (bf16, C=64/128); x [Nf, H, W, C].
+    Returns y and the saved state (mz, ctx32, actT, actx, o) for slaf_bwd; o (the attention output before
+    to_out, [Nf, H, W, 256]) only with save_o, for the to_out weight gradient."""
     Nf, H, W, C = x.shape
     HW = H * W
     _chk(x, dtype=torch.bfloat16)
@@ -362,17 +363,19 @@ def slaf_fwd(x, gamma, wqkv, wout, bout, scale, eps=1e-5):
     actx = empty((Nf, 8, 2, 64, 8), torch.bfloat16, dev)
     nblk = lib().cesm_slaf_nblk(Nf, HW)
     ws = empty((nblk * Nf * 8 * 1088,), torch.float32, dev)
-    call("cesm_slaf_fwd", P(x), P(gamma), P(wqkv), P(wout), P(bout), P(y), P(mz), P(ctx32), P(actT), P(actx), P(ws),
-         Nf, HW, C, float(scale), float(eps), S())
-    return y, (mz, ctx32, actT, actx)
+    o = empty((Nf, H, W, 256), x.dtype, dev) if save_o else None
+    call("cesm_slaf_fwd", P(x), P(gamma), P(wqkv), P(wout), P(bout), P(y), P(o), P(mz), P(ctx32), P(actT), P(actx),
+         P(ws), Nf, HW, C, float(scale), float(eps), S())
+    return y, (mz, ctx32, actT, actx, o)
 
 
 def slaf_bwd(x, dy, gamma, wqkv, wqkv_t, wout_t, state, dgamma, scale, want_wgrad_inputs=True, eps=1e-5):
     """fused SLA block backward, dx path (bf16, C=64).  Returns (dx, dqkv, o, xn); the last three feed the
-    to_qkv / to_out weight-gradient GEMMs."""
+    to_qkv / to_out weight-gradient GEMMs.  When the forward saved o (slaf_fwd save_o), that o is returned
+    and the backward does not emit it."""
     Nf, H, W, C = x.shape
     HW = H * W
-    mz, ctx32, actT, actx = state
+    mz, ctx32, actT, actx, o_fwd = state
     _chk(dy, x.shape, torch.bfloat16)
     _chk(wqkv_t, (C, 768), torch.bfloat16)
     _chk(wout_t, (256, C), torch.bfloat16)
@@ -380,7 +383,7 @@ def slaf_bwd(x, dy, gamma, wqkv, wqkv_t, wout_t, state, dgamma, scale, want_wgra
     dx = empty(x.shape, x.dtype, dev)
     if want_wgrad_inputs:
         dqkv = empty((Nf, H, W, 768), x.dtype, dev)
-        o = empty((Nf, H, W, 256), x.dtype, dev)
+        o = empty((Nf, H, W, 256), x.dtype, dev) if o_fwd is None else None
         xn = empty(x.shape, x.dtype, dev)
     else:
         dqkv = o = xn = None
@@ -394,6 +397,8 @@ def slaf_bwd(x, dy, gamma, wqkv, wqkv_t, wout_t, state, dgamma, scale, want_wgra
     call("cesm_slaf_bwd", P(x), P(dy), P(gamma), P(wqkv), P(wqkv_t), P(wout_t), P(mz), P(ctx32), P(actT), P(actx),
          P(dx), P(dqkv), P(o), P(xn), P(dgamma), P(part), P(G), P(adc), P(adcT), P(dgp), P(wimg), Nf, HW, C,
          float(scale), float(eps), 1, S())
+    if want_wgrad_inputs and o_fwd is not None:
+        o = o_fwd
     return dx, dqkv, o, xn
 
 

@@ -421,6 +421,7 @@ def tattn_bwd(rc, res_mod, st, dy):
 
 
 FUSED_SLA = os.environ.get("CESM_NO_FUSED_SLA", "0") != "1"
+SLA_FWD_O = os.environ.get("CESM_SLA_FWD_O", "1") != "0"  # forward writes O for dW_out (else the backward emits it)
 
 
 def _sla_fused(rc, C):
@@ -436,7 +437,9 @@ def sla_fwd(rc, res_mod, x):
     if _sla_fused(rc, C):
         wq = rc.packed(sla.to_qkv.weight, 768, C, 1, 1, 0, 0)
         wo = rc.packed(sla.to_out.weight, C, 256, 1, 1, 0, 0)
-        y, state = K.slaf_fwd(x, _flat(pre.norm.gamma), wq, wo, sla.to_out.bias, sla.scale, eps=pre.norm.eps)
+        # training: the forward also writes O (to_out's input) so the backward does not emit it
+        y, state = K.slaf_fwd(x, _flat(pre.norm.gamma), wq, wo, sla.to_out.bias, sla.scale, eps=pre.norm.eps,
+                              save_o=rc.save and SLA_FWD_O)
         st = SimpleNamespace(fused=True, x=x, state=state) if rc.save else None
         return y, st
     n, mr = K.ln_fwd(x, _flat(pre.norm.gamma), save=rc.save, eps=pre.norm.eps)

@@ -128,11 +128,13 @@ int cesm_sla_bwd(int dtype, const void* qkv, const void* dout, const float* ctx,
  * SpatialLinearAttention)) (video_net.py:313-347) without per-pixel intermediates in HBM: online-softmax
  * context partials -> combine -> output.  Saves mz [Nf][8][32][2] (max, normaliser of k over pixels),
  * ctx32 [Nf][8][32][32] and the context as MFMA A fragments actT/actx [Nf][8][2][64][8] bf16.
+ * o (nullable): the attention output before to_out [Nf][HW][256] bf16, for the to_out weight gradient
+ * (training; the backward then need not emit it).
  * ws: cesm_slaf_nblk(Nf, HW) * Nf * 8 * 1088 floats. */
 int cesm_slaf_nblk(int Nf, int HW);
 int cesm_slaf_fwd(const void* x, const float* gamma, const void* wqkv, const void* wout, const float* bout, void* y,
-                  float* mz, float* ctx32, void* actT, void* actx, float* ws, int Nf, int HW, int C, float scale,
-                  float eps, hipStream_t stream);
+                  void* o, float* mz, float* ctx32, void* actT, void* actx, float* ws, int Nf, int HW, int C,
+                  float scale, float eps, hipStream_t stream);
 
 /* Fused SLA block backward, dx path (bf16, C = 64): dctx partials -> combine (G_d = sum_e dctx ctx, dctx as
  * A fragments adc/adcT) -> dx (+ dy residual), dgamma (+)=; emits (nullable) dqkv [..][768], o [..][256],

@@ -602,11 +602,12 @@ def test_fused_sla_forward(dev, H, W, C):
     assert err < 2e-2
 
 
+@pytest.mark.parametrize("save_o", [False, True])
 @pytest.mark.parametrize("C", [64, 128])
 @pytest.mark.parametrize("H,W", [(8, 8), (12, 20), (37, 29)])
-def test_fused_sla_backward(dev, H, W, C):
+def test_fused_sla_backward(dev, H, W, C, save_o):
     """cesm_slaf_bwd (+ weight gradients from its dqkv/o/xn outputs) vs float64 autograd through the
-    reference SpatialLinearAttention block"""
+    reference SpatialLinearAttention block; save_o: O written by the forward instead of the backward"""
     torch.manual_seed(14)
     B, Fr = 2, 3
     res = _sla_block(C, dev)
@@ -622,9 +623,13 @@ def test_fused_sla_backward(dev, H, W, C):
     wq_t = K.conv_pack(wqkv, torch.bfloat16, C, 768, 1, 1, 1, 1)
     wo_t = K.conv_pack(wout, torch.bfloat16, 256, C, 1, 1, 1, 1)
     gamma = res.fn.norm.gamma.detach().reshape(-1).contiguous()
-    _, st = K.slaf_fwd(xd, gamma, wq, wo, sla.to_out.bias.detach(), sla.scale)
+    _, st = K.slaf_fwd(xd, gamma, wq, wo, sla.to_out.bias.detach(), sla.scale, save_o=save_o)
     dgamma = torch.zeros(C, device=dev)
     dx, dqkv, o, xn = K.slaf_bwd(xd, gd, gamma, wq, wq_t, wo_t, st, dgamma, sla.scale)
+    if save_o:  # the forward's O equals the one the backward emits (same bf16 rounding up to 1 ulp)
+        _, st2 = K.slaf_fwd(xd, gamma, wq, wo, sla.to_out.bias.detach(), sla.scale)
+        _, _, o_bwd, _ = K.slaf_bwd(xd, gd, gamma, wq, wq_t, wo_t, st2, torch.zeros(C, device=dev), sla.scale)
+        assert rel(o, o_bwd) < 1e-2
     dwq = dqkv.reshape(-1, 768).double().t() @ xn.reshape(-1, C).double()
     dwo = gd.reshape(-1, C).double().t() @ o.reshape(-1, 256).double()
     ref = _sla_block_ref(res, C)

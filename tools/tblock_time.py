@@ -57,7 +57,7 @@ def main():
     bout = torch.randn(C, device=dev) * 0.1
 
     def sfwd():
-        st["s"] = K.slaf_fwd(x, gamma, wq, wo, bout, 32 ** -0.5)
+        st["s"] = K.slaf_fwd(x, gamma, wq, wo, bout, 32 ** -0.5, save_o=True)
 
     sf = timed(sfwd, reps)
     ys, sst = st["s"]
