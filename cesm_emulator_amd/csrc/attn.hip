@@ -71,8 +71,9 @@ template <typename T>
 __global__ __launch_bounds__(TA_T) void tattn_fwd_kernel(const T* __restrict__ qkv, const float* __restrict__ bias,
                                                          const float* __restrict__ rotg, T* __restrict__ out,
                                                          float* __restrict__ lse, int F, int HW, float scale) {
-  __shared__ float rot[32 * 32];
-  __shared__ float sb[32 * 32];
+  extern __shared__ __attribute__((aligned(16))) float ta_dyn[];  // tables sized by F (ta_fwd_smem)
+  float* rot = ta_dyn;        // [F][32]
+  float* sb = rot + F * 32;   // [F][F]
   __shared__ __attribute__((aligned(16))) float sk[TA_T * TA_LD];
   const int b = blockIdx.y / NH, h = blockIdx.y % NH;
   for (int e = threadIdx.x; e < F * 32; e += blockDim.x) rot[e] = rotg[e];
@@ -140,20 +141,22 @@ __global__ __launch_bounds__(TA_T) void tattn_bwd_kernel(const T* __restrict__ q
                                                          const float* __restrict__ rotg, T* __restrict__ dqkv,
                                                          float* __restrict__ dbias_part, int F, int HW,
                                                          float scale) {
-  __shared__ float rot[32 * 32];
-  __shared__ float sb[32 * 32];
+  extern __shared__ __attribute__((aligned(16))) float ta_dyn[];  // tables sized by F (ta_bwd_smem)
+  const int AS = F + 1;                 // dbias row stride (odd: conflict-free column walks)
+  float* rot = ta_dyn;                  // [F][32]
+  float* sb = rot + F * 32;             // [F][F]
+  float* sacc = sb + F * F;             // [TA_T][F + 1] per-lane dbias rows
   __shared__ __attribute__((aligned(16))) float sv[TA_T * TA_LD];  // k' (phase 1) / q' (phase 2)
   __shared__ float sD[TA_T], sL[TA_T];
-  __shared__ float sacc[TA_T * 33];
   const int b = blockIdx.y / NH, h = blockIdx.y % NH;
   for (int e = threadIdx.x; e < F * 32; e += blockDim.x) rot[e] = rotg[e];
   for (int e = threadIdx.x; e < F * F; e += blockDim.x) sb[e] = bias[h * F * F + e];
-  for (int e = threadIdx.x; e < TA_T * 33; e += blockDim.x) sacc[e] = 0.f;
+  for (int e = threadIdx.x; e < TA_T * AS; e += blockDim.x) sacc[e] = 0.f;
   __syncthreads();
   const int G = TA_T / F;
   const int g = threadIdx.x / F, i = threadIdx.x % F;
   const bool lane_ok = g < G;
-  float* myacc = sacc + threadIdx.x * 33;
+  float* myacc = sacc + threadIdx.x * AS;
   const int npb = (HW + G - 1) / G;
   for (int pb = blockIdx.x; pb < npb; pb += gridDim.x) {
     const int p = pb * G + g;
@@ -249,7 +252,7 @@ __global__ __launch_bounds__(TA_T) void tattn_bwd_kernel(const T* __restrict__ q
   for (int t = threadIdx.x; t < F * F; t += blockDim.x) {
     const int ii = t / F, j = t % F;
     float s = 0.f;
-    for (int gg = 0; gg < G; ++gg) s += sacc[(gg * F + ii) * 33 + j];
+    for (int gg = 0; gg < G; ++gg) s += sacc[(gg * F + ii) * AS + j];
     outp[t] = s;
   }
 }
@@ -598,12 +601,23 @@ static int sla_chunk(int HW) {
   return c;
 }
 
+// dynamic LDS of the unfused temporal-attention kernels: RoPE table [F][32] + bias [F][F] (+ per-lane
+// dbias rows [TA_T][F+1] in the backward).  F <= 32 fits the old static tables; long windows (the
+// decadal F = 120 of BASELINE config 4) take one block per CU.
+constexpr size_t TA_LDS_MAX = 160 * 1024;
+static size_t ta_fwd_smem(int F) { return (size_t)(F * 32 + F * F) * 4; }
+static size_t ta_bwd_smem(int F) { return (size_t)(F * 32 + F * F + TA_T * (F + 1)) * 4; }
+template <typename K>
+static void ta_allow_smem(K kernel, size_t bytes) {
+  if (bytes > 48 * 1024) (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
 }  // namespace
 
 extern "C" {
 
 int cesm_rope_table(const float* freqs, float* rot, int F, hipStream_t stream) {
-  if (F > 32) return CESM_EINVAL;
+  if (F < 1 || F > TA_T) return CESM_EINVAL;
   rope_table_kernel<<<(unsigned)cdiv(F * 16, 256), 256, 0, stream>>>(freqs, rot, F);
   return cesm_launch_status();
 }
@@ -632,11 +646,13 @@ int cesm_tattn_nblk(int F, int HW) {
 
 int cesm_tattn_fwd(int dtype, const void* qkv, const float* bias, const float* rot, void* out, float* lse, int B,
                    int F, int HW, float scale, hipStream_t stream) {
-  if (F < 1 || F > 32) return CESM_EUNSUPPORTED;
+  const size_t sm = ta_fwd_smem(F);
+  if (F < 1 || F > TA_T || sm + TA_T * TA_LD * 4 > TA_LDS_MAX) return CESM_EUNSUPPORTED;
   dim3 grid(cesm_tattn_nblk(F, HW), B * NH);
   return dispatch_dt(dtype, [&](auto* tp) {
     using T = std::remove_pointer_t<decltype(tp)>;
-    tattn_fwd_kernel<T><<<grid, TA_T, 0, stream>>>((const T*)qkv, bias, rot, (T*)out, lse, F, HW, scale);
+    ta_allow_smem(tattn_fwd_kernel<T>, sm);
+    tattn_fwd_kernel<T><<<grid, TA_T, sm, stream>>>((const T*)qkv, bias, rot, (T*)out, lse, F, HW, scale);
   }) ?: cesm_launch_status();
 }
 
@@ -644,11 +660,13 @@ int cesm_tattn_fwd(int dtype, const void* qkv, const float* bias, const float* r
 int cesm_tattn_bwd(int dtype, const void* qkv, const void* o, const void* dout, const float* lse, const float* bias,
                    const float* rot, void* dqkv, float* dbias_part, int B, int F, int HW, float scale,
                    hipStream_t stream) {
-  if (F < 1 || F > 32) return CESM_EUNSUPPORTED;
+  const size_t sm = ta_bwd_smem(F);
+  if (F < 1 || F > TA_T || sm + (TA_T * TA_LD + 2 * TA_T) * 4 > TA_LDS_MAX) return CESM_EUNSUPPORTED;
   dim3 grid(cesm_tattn_nblk(F, HW), B * NH);
   return dispatch_dt(dtype, [&](auto* tp) {
     using T = std::remove_pointer_t<decltype(tp)>;
-    tattn_bwd_kernel<T><<<grid, TA_T, 0, stream>>>((const T*)qkv, (const T*)o, (const T*)dout, lse, bias, rot,
+    ta_allow_smem(tattn_bwd_kernel<T>, sm);
+    tattn_bwd_kernel<T><<<grid, TA_T, sm, stream>>>((const T*)qkv, (const T*)o, (const T*)dout, lse, bias, rot,
                                                    (T*)dqkv, dbias_part, F, HW, scale);
   }) ?: cesm_launch_status();
 }

@@ -256,10 +256,11 @@ def _tattn_ref(qkv, bias, freqs, B, Fr, HW, scale):
 
 
 @pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("Fr", [1, 3, 12])
+@pytest.mark.parametrize("Fr", [1, 3, 12, 33, 64, 120])
 def test_temporal_attention_core(dev, cdt, Fr):
+    """unfused temporal attention; F > 32 exercises the F-sized LDS tables (decadal window F = 120)"""
     torch.manual_seed(4)
-    B, HW = 2, 77
+    B, HW = 2, (77 if Fr <= 32 else 13)
     qkv = torch.randn(B * Fr * HW, 768)
     table = torch.randn(32, 8)
     freqs = 1.0 / (10000 ** (torch.arange(0, 32, 2).float() / 32))

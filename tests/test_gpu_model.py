@@ -48,7 +48,7 @@ def test_state_dict_keys_match_reference_layout():
 
 
 @pytest.mark.parametrize("mults,Fr,H,W", [((1, 2, 4), 8, 32, 48), ((1, 2, 4, 8), 3, 32, 48),
-                                          ((1, 2, 4), 1, 16, 24)])
+                                          ((1, 2, 4), 1, 16, 24), ((1, 2, 4), 40, 16, 24)])
 def test_forward_parity_fp32(dev, mults, Fr, H, W):
     ref, prod = build_pair(mults)
     prod = prod.to(dev)
@@ -192,3 +192,45 @@ def test_overlapped_allreduce_hook_order(dev, monkeypatch):
     assert rel(opt.flat.grad, ref * 0.5) < 1e-6  # (split-K reductions may reorder fp32 sums)
     print(f"buckets {len(calls)}, issued during backward {early[0]}")
     assert early[0] >= len(calls) // 2
+
+
+def test_decadal_window_backward_parity_fp32(dev):
+    """F = 120 (BASELINE config 4, the decadal window): loss and every gradient against the oracle on a
+    small grid; the temporal attention runs on the F-sized-LDS unfused kernels"""
+    ref, prod = build_pair((1, 2))
+    prod = prod.to(dev)
+    prod.compute_dtype = torch.float32
+    dref, dprod = R.Diffusion(ref), Diffusion(prod).to(dev)
+    x0, cond, t, noise = inputs(1, 120, 8, 16, seed=21)
+    lr_ = dref.loss(x0, cond, t=t, noise=noise)
+    lr_.backward()
+    lp = dprod.loss(x0.to(dev), cond.to(dev), t=t.to(dev), noise=noise.to(dev))
+    lp.backward()
+    assert abs(lp.item() - lr_.item()) / abs(lr_.item()) < 1e-5
+    pr = dict(prod.named_parameters())
+    worst = 0.0
+    for name, p in ref.named_parameters():
+        if p.requires_grad:
+            e = rel(pr[name].grad, p.grad)
+            worst = max(worst, e)
+            assert e < 1e-4, (name, e)
+    print(f"F=120 worst grad rel err: {worst:.3e}")
+
+
+def test_decadal_window_bf16_step(dev):
+    """the bf16 throughput path at F = 120 (unfused temporal blocks) trains: finite, decreasing loss"""
+    torch.manual_seed(0)
+    prod = UNet(ch_mults=(1, 2)).to(dev)
+    d = Diffusion(prod).to(dev)
+    opt = FusedAdamW(d.parameters(), lr=1e-3, max_grad_norm=1.0)
+    x0, cond, t, noise = inputs(1, 120, 16, 24, seed=22)
+    x0, cond, t, noise = x0.to(dev), cond.to(dev), t.to(dev), noise.to(dev)
+    losses = []
+    for _ in range(4):
+        opt.zero_grad()
+        l = d.loss(x0, cond, t=t, noise=noise)
+        l.backward()
+        opt.step(loss=l.detach())
+        losses.append(l.item())
+    print("F=120 bf16 losses", losses)
+    assert all(map(lambda v: v == v, losses)) and losses[-1] < losses[0]
