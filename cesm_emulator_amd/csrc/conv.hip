@@ -1705,10 +1705,15 @@ __device__ __forceinline__ int wgb_swz(int r) {  // XOR on 4-element chunk index
   else return 4 * ((r & 3) | (((r >> 3) & 1) << 2));
 }
 
+// bslab (nullable): the conv bias gradient sum_px dY[px][co] comes out of the same K loop — the blocks
+// of the first K tile multiply their dY fragments by a ones operand (MT extra MFMAs per step, no extra
+// memory traffic) and write per-split partials bslab[z][co] (replaces a separate column-sum pass
+// over dY, which re-read the whole tensor).
 template <int BM>
 __global__ __launch_bounds__(256) void wgrad_wide_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
                                                          const bf16* __restrict__ dy1, const bf16* __restrict__ dy2,
-                                                         float* __restrict__ slab, ConvGeom g, int M, int px_per_split) {
+                                                         float* __restrict__ slab, float* __restrict__ bslab, ConvGeom g,
+                                                         int M, int px_per_split) {
   constexpr int VPRY = BM / 8, RPPY = 256 / VPRY, NPY = WG_BP / RPPY;
   constexpr int MT = BM / 64;  // 16-row co tiles per wave
   __shared__ __attribute__((aligned(16))) bf16 tY[2][WG_BP * BM];
@@ -1791,6 +1796,13 @@ __global__ __launch_bounds__(256) void wgrad_wide_kernel(const bf16* __restrict_
   for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool bias_blk = bslab != nullptr && blockIdx.y == 0;  // uniform
+  f32x4 bacc[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) bacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.f;
   const int nsteps = (pend - pbeg + WG_BP - 1) / WG_BP;
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
@@ -1833,12 +1845,22 @@ __global__ __launch_bounds__(256) void wgrad_wide_kernel(const bf16* __restrict_
     for (int i = 0; i < MT; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    if (bias_blk) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i) bacc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, bacc[i], 0, 0, 0);
+    }
     if (s + 1 < nsteps) sstore(std::integral_constant<int, buf ^ 1>{});
     __syncthreads();
   };
   for (int s = 0; s < nsteps; s += 2) {
     step(s, I0{});
     if (s + 1 < nsteps) step(s + 1, I1{});
+  }
+  if (bias_blk && lr == 0) {  // every output column holds the row sum: column 0 writes it
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bslab[(int64_t)blockIdx.z * g.Cout + co0 + wid * (BM / 4) + i * 16 + lg * 4 + r] = bacc[i][r];
   }
   const int K = g.KH * g.KW * Cin;
   float* out = slab + (int64_t)blockIdx.z * g.Cout * K;
@@ -2817,9 +2839,10 @@ int cesm_conv_fwd(int dtype, const void* x1, const void* x2, const void* wp, con
 // Result accumulated/written into the PyTorch weight tensor `dw` ([D0][D1][1][KH][KW] with the
 // (swap, flip) mapping of the pack).  `slab` is an fp32 workspace of nsplit*Cout*K floats.
 int cesm_conv_wgrad(int dtype, const void* x1, const void* x2, const void* dy1, const void* dy2, float* dw,
-                    float* slab, int nsplit, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout,
-                    int Co1, int KH, int KW, int S, int P, int U, int swap, int flip, int accumulate,
+                    float* slab, float* db, float* bslab, int nsplit, int Nb, int Hi, int Wi, int C1, int C2, int Ho,
+                    int Wo, int Cout, int Co1, int KH, int KW, int S, int P, int U, int swap, int flip, int accumulate,
                     hipStream_t stream) {
+  if (db && !bslab) return CESM_EINVAL;
   const int Cin = C1 + C2;
   if ((Cin % 64) || (C1 % 64) || (Cout % 64) || (Co1 % 64) || nsplit <= 0) return CESM_EINVAL;
   ConvGeom g{Nb, Hi, Wi, Ho, Wo, C1, C2, Cout, Co1, KH, KW, S, P, U};
@@ -2849,15 +2872,19 @@ int cesm_conv_wgrad(int dtype, const void* x1, const void* x2, const void* dy1, 
     // wide-tile kernel; nsplit from the caller sized the slab for 64-row tiles, keep it
     const int bm = (Cout % 256 == 0 && Co1 % 256 == 0) ? 256 : ((Cout % 128 == 0 && Co1 % 128 == 0) ? 128 : 64);
     dim3 gw(Cout / bm, K / 64, nsplit);
+    float* bs = db ? bslab : nullptr;
     if (bm == 256)
       wgrad_wide_kernel<256><<<gw, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
-                                                     (const bf16*)dy2, slab, g, (int)M, (int)pps);
+                                                     (const bf16*)dy2, slab, bs, g, (int)M, (int)pps);
     else if (bm == 128)
       wgrad_wide_kernel<128><<<gw, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
-                                                     (const bf16*)dy2, slab, g, (int)M, (int)pps);
+                                                     (const bf16*)dy2, slab, bs, g, (int)M, (int)pps);
     else
       wgrad_wide_kernel<64><<<gw, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
-                                                    (const bf16*)dy2, slab, g, (int)M, (int)pps);
+                                                    (const bf16*)dy2, slab, bs, g, (int)M, (int)pps);
+    if (db) colsum_final_kernel<<<Cout, 64, 0, stream>>>(bslab, db, nsplit, Cout, 1);
+  } else if (db) {
+    return CESM_EUNSUPPORTED;  // the bias gradient rides only on the wide kernel (callers use cesm_colsum)
   } else if (dtype == CESM_DT_BF16)
     conv_wgrad_kernel<bf16><<<grid, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
                                                       (const bf16*)dy2, slab, g, M, pps);

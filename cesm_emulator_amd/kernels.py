@@ -120,7 +120,9 @@ def _wgrad_bm(x, cout, co1):
     return 64
 
 
-def conv_wgrad(x1, x2, dy1, dy2, dw, geom, swap, flip, accumulate=True):
+def conv_wgrad(x1, x2, dy1, dy2, dw, geom, swap, flip, accumulate=True, db=None):
+    """dW of a conv (split-K over pixels + reduce).  db: also the bias gradient (+=) in the same pass when
+    the bf16 wide-tile kernel runs; returns True if db was produced (else the caller runs colsum)."""
     Ho, Wo, Cout, KH, KW, St, Pd, U = geom
     Nb, Hi, Wi, C1 = x1.shape
     C2 = 0 if x2 is None else x2.shape[3]
@@ -141,8 +143,20 @@ def conv_wgrad(x1, x2, dy1, dy2, dw, geom, swap, flip, accumulate=True):
     slab = empty((nsplit, Cout, K), torch.float32, x1.device)
     if CONV_TRACE is not None:
         CONV_TRACE.append(("wgrad", Nb, Hi, Wi, C1 + C2, Ho, Wo, Cout, KH, KW, St, Pd, U))
-    call("cesm_conv_wgrad", dtcode(x1), P(x1), P(x2), P(dy1), P(dy2), P(dw), P(slab), nsplit, Nb, Hi, Wi, C1, C2,
-         Ho, Wo, Cout, Co1, KH, KW, St, Pd, U, int(swap), int(flip), int(accumulate), S())
+    # the bias rides on the wide-tile kernel only (same dispatch condition as cesm_conv_wgrad)
+    wide = (x1.dtype == torch.bfloat16 and not halo3 and M < (1 << 31) and dy2 is None
+            and os.environ.get("CESM_NO_WIDE_WGRAD", "0") in ("", "0") and FUSED_BIAS_GRAD)
+    if db is not None and wide:
+        _chk(db, (Cout,), torch.float32)
+        bslab = empty((nsplit, Cout), torch.float32, x1.device)
+    else:
+        db = bslab = None
+    call("cesm_conv_wgrad", dtcode(x1), P(x1), P(x2), P(dy1), P(dy2), P(dw), P(slab), P(db), P(bslab), nsplit, Nb,
+         Hi, Wi, C1, C2, Ho, Wo, Cout, Co1, KH, KW, St, Pd, U, int(swap), int(flip), int(accumulate), S())
+    return db is not None
+
+
+FUSED_BIAS_GRAD = os.environ.get("CESM_NO_FUSED_BIAS_GRAD", "0") != "1"
 
 
 def colsum(x, dst, accumulate=True):

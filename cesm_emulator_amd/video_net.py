@@ -152,7 +152,8 @@ def conv_forward(rc, spec, x1, x2=None, res=None):
 
 
 def conv_param_grads(spec, st, dy, dw, db):
-    """dW (+ dbias) of one conv (called on the weight-gradient stream)."""
+    """dW (+ dbias) of one conv (called on the weight-gradient stream).  The bias gradient rides on the
+    weight-gradient pass when its kernel supports it (bf16 wide-tile wgrad), else a column sum of dY."""
     if dw is not None:
         if spec.transposed:
             # the transposed conv's weight gradient sum_{a,b} x[a,b] (x) dOut[S*a - P + ky, S*b - P + kx] is the
@@ -163,7 +164,8 @@ def conv_param_grads(spec, st, dy, dw, db):
             Hx, Wx = st.x1.shape[1], st.x1.shape[2]
             K.conv_wgrad(dy, None, st.x1, None, dw, (Hx, Wx, spec.cin, spec.k, spec.k, spec.stride, spec.pad, 1), 0, 0)
         else:
-            K.conv_wgrad(st.x1, st.x2, dy, None, dw, st.geom, st.swap, st.flip)
+            if K.conv_wgrad(st.x1, st.x2, dy, None, dw, st.geom, st.swap, st.flip, db=db):
+                db = None
     if db is not None:
         K.colsum(dy, db)
 
@@ -465,8 +467,8 @@ def sla_bwd(rc, res_mod, st, dy):
         with rc.side(xn, dqkv, o, dy, attn=True):
             if dwq is not None:
                 K.conv_wgrad(xn, None, dqkv, None, dwq, (H, W, 768, 1, 1, 1, 0, 1), 0, 0)
-            if dwo is not None:
-                K.conv_wgrad(o, None, dy, None, dwo, (H, W, C, 1, 1, 1, 0, 1), 0, 0)
+            if dwo is not None and K.conv_wgrad(o, None, dy, None, dwo, (H, W, C, 1, 1, 1, 0, 1), 0, 0, db=dbo):
+                dbo = None
             if dbo is not None:
                 K.colsum(dy, dbo)
         return dx

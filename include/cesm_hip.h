@@ -37,10 +37,12 @@ int cesm_conv_fwd(int dtype, const void* x1, const void* x2, const void* wp, con
                   const void* res2, void* y1, void* y2, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout, int Co1,
                   int KH, int KW, int S, int P, int U, hipStream_t stream);
 /* weight gradient of a cesm_conv_fwd launch; written in PyTorch layout [D0][D1][1][KH][KW] with the
- * (swap, flip) mapping of cesm_conv_pack.  slab: nsplit*Cout*KH*KW*(C1+C2) floats. */
+ * (swap, flip) mapping of cesm_conv_pack.  slab: nsplit*Cout*KH*KW*(C1+C2) floats.
+ * db (nullable): the conv bias gradient sum_px dY (+=), computed in the same pass (bslab: nsplit*Cout
+ * floats); only on the bf16 wide-tile path (non-3x3, no dy2) — CESM_EUNSUPPORTED otherwise. */
 int cesm_conv_wgrad(int dtype, const void* x1, const void* x2, const void* dy1, const void* dy2, float* dw,
-                    float* slab, int nsplit, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout,
-                    int Co1, int KH, int KW, int S, int P, int U, int swap, int flip, int accumulate,
+                    float* slab, float* db, float* bslab, int nsplit, int Nb, int Hi, int Wi, int C1, int C2, int Ho,
+                    int Wo, int Cout, int Co1, int KH, int KW, int S, int P, int U, int swap, int flip, int accumulate,
                     hipStream_t stream);
 /* PyTorch conv weight (fp32) -> GEMM layout Wp[co][tap][ci] in dtype.  swap: GEMM co is dim 1 of
  * the torch tensor (transposed conv forward / conv dgrad); flip: taps reversed. */

@@ -104,6 +104,27 @@ def test_conv_fwd_bwd(dev, cdt, case):
     assert rel(mod_dev.bias.grad, br2.grad) < TOL[cdt]
 
 
+@pytest.mark.parametrize("cin,cout,k,st", [(256, 64, 1, 1), (64, 768, 1, 1), (64, 64, 4, 2), (128, 256, 1, 1)])
+def test_wgrad_fused_bias(dev, cin, cout, k, st):
+    """bias gradient produced inside the bf16 wide-tile wgrad (ones-operand MFMA, split-K partials) ==
+    column sum of dY; the weight gradient is unchanged by it"""
+    torch.manual_seed(9)
+    Nb, H, W = 6, 37, 41
+    pd = (k - 1) // 2 if k != 4 else 1
+    Ho, Wo = (H + 2 * pd - k) // st + 1, (W + 2 * pd - k) // st + 1
+    x = torch.randn(Nb, H, W, cin, device=dev).to(torch.bfloat16)
+    dy = torch.randn(Nb, Ho, Wo, cout, device=dev).to(torch.bfloat16)
+    geom = (Ho, Wo, cout, k, k, st, pd, 1)
+    dw1 = torch.zeros(cout, cin, 1, k, k, device=dev)
+    dw2 = torch.zeros_like(dw1)
+    db = torch.full((cout,), 0.5, device=dev)  # accumulates (+=)
+    assert K.conv_wgrad(x, None, dy, None, dw1, geom, 0, 0, db=db)
+    K.conv_wgrad(x, None, dy, None, dw2, geom, 0, 0)
+    ref = dy.double().reshape(-1, cout).sum(0) + 0.5
+    assert rel(db, ref) < 1e-5
+    assert torch.equal(dw1, dw2)
+
+
 @pytest.mark.parametrize("H,W,cin,cout", [(12, 72, 64, 64), (8, 36, 128, 64), (6, 36, 64, 128)])
 def test_conv3x3_tile_shapes_bf16(dev, H, W, cin, cout):
     """widths that are multiples of 36 take the 36-wide halo tiles (fwd/dgrad) and the 8 x 36 weight-
