@@ -3,7 +3,8 @@
 //
 // Statistics are per sample over (C/G channels x F frames x H x W); the sample's voxels are a
 // contiguous [rows][C] block of the channels-last activation.  Everything after the statistics
-// is folded into per-(sample, channel) affine coefficients computed once per call:
+// is folded into per-(sample, channel) affine coefficients (computed in each streaming kernel's prologue
+// for the thread's 8 channels):
 //   forward   a = y*A1[b,c] + A0[b,c],  out = silu(a) + res
 //   backward  da = dout * silu'(a),  S1 = sum da,  S3 = sum da*y,  Sy = sum y  (per b,c; xhat never
 //             stored);  dy = da*E1[b,c] + y*E2[b,c] + E3[b,c], so the producing conv's bias gradient
@@ -82,22 +83,7 @@ __global__ __launch_bounds__(64) void gn_finalize_kernel(const double* __restric
   stats[i * 2 + 1] = (float)(1.0 / sqrt(var + (double)eps));
 }
 
-// coef[b][0][c] = A1, coef[b][1][c] = A0 :  a = y*A1 + A0
-__global__ void gn_coef_kernel(const float* __restrict__ stats, const float* __restrict__ gamma,
-                               const float* __restrict__ beta, const float* __restrict__ ss, float* __restrict__ coef,
-                               int B, int C, int G) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= B * C) return;
-  const int b = i / C, c = i - b * C;
-  const int g = c / (C / G);
-  const float mean = stats[(b * G + g) * 2], rstd = stats[(b * G + g) * 2 + 1];
-  const float sc = ss ? ss[(int64_t)b * 2 * C + c] + 1.f : 1.f;
-  const float sh = ss ? ss[(int64_t)b * 2 * C + C + c] : 0.f;
-  const float k = rstd * gamma[c];
-  coef[((int64_t)b * 2) * C + c] = k * sc;
-  coef[((int64_t)b * 2 + 1) * C + c] = (beta[c] - mean * k) * sc + sh;
-}
-
+// coefficients: A1[b][c], A0[b][c] with a = y*A1 + A0 (gn_coef8 below)
 __device__ __forceinline__ void load_coef8(const float* p, float* v) {
   const f32x4 a = *reinterpret_cast<const f32x4*>(p);
   const f32x4 b = *reinterpret_cast<const f32x4*>(p + 4);
@@ -105,9 +91,41 @@ __device__ __forceinline__ void load_coef8(const float* p, float* v) {
   v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
 }
 
+// The same coefficients computed in the streaming kernels' prologue for the thread's 8 channels (one
+// group: C/G is a multiple of 8), which saves the coefficient kernel's launch per GroupNorm call.
+struct GnAffine {
+  const float* stats;  // [B][G][2] (mean, rstd)
+  const float* gamma;
+  const float* beta;
+  const float* ss;     // [B][2C] (scale | shift) or null
+  int G;
+};
+__device__ __forceinline__ void gn_coef8(const GnAffine& q, int b, int c0, int C, float* A1, float* A0) {
+  const int g = c0 / (C / q.G);
+  const float mean = q.stats[(b * q.G + g) * 2], rstd = q.stats[(b * q.G + g) * 2 + 1];
+  float gm[8], bt[8], sc[8], sh[8];
+  load_coef8(q.gamma + c0, gm);
+  load_coef8(q.beta + c0, bt);
+  if (q.ss) {
+    load_coef8(q.ss + (int64_t)b * 2 * C + c0, sc);
+    load_coef8(q.ss + (int64_t)b * 2 * C + C + c0, sh);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sc[i] += 1.f;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { sc[i] = 1.f; sh[i] = 0.f; }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const float k = rstd * gm[i];
+    A1[i] = k * sc[i];
+    A0[i] = (bt[i] - mean * k) * sc[i] + sh[i];
+  }
+}
+
 // grid (nchunk, B): thread = (8-channel group c8, row lane rr), rows strided by 256/(C/8)
 template <typename T>
-__global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ y, const float* __restrict__ coef,
+__global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ y, const GnAffine coef,
                                                        const T* __restrict__ res, T* __restrict__ out, int64_t rows_b,
                                                        int C, int nchunk) {
   const int b = blockIdx.y, chunk = blockIdx.x;
@@ -115,8 +133,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ y, 
   const int c8 = threadIdx.x % cv, rr = threadIdx.x / cv;
   if (rr >= rl) return;
   float A1[8], A0[8];
-  load_coef8(coef + ((int64_t)b * 2) * C + c8 * 8, A1);
-  load_coef8(coef + ((int64_t)b * 2 + 1) * C + c8 * 8, A0);
+  gn_coef8(coef, b, c8 * 8, C, A1, A0);
   const int64_t rpc = (rows_b + nchunk - 1) / nchunk;
   const int64_t r0 = chunk * rpc, r1 = min(rows_b, r0 + rpc);
   const int64_t off = (int64_t)b * rows_b * C + c8 * 8;
@@ -137,15 +154,14 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ y, 
 // part[b][chunk][c] = (S1 = sum da, S3 = sum da*y, Sy = sum y)
 template <typename T>
 __global__ __launch_bounds__(256) void gn_bwd_reduce_kernel(const T* __restrict__ dout, const T* __restrict__ y,
-                                                            const float* __restrict__ coef, float* __restrict__ part,
+                                                            const GnAffine coef, float* __restrict__ part,
                                                             int64_t rows_b, int C, int nchunk) {
   const int b = blockIdx.y, chunk = blockIdx.x;
   const int cv = C / 8, rl = 256 / cv;
   const int tid = threadIdx.x;
   const int c8 = tid % cv, rr = tid / cv;
   float A1[8], A0[8];
-  load_coef8(coef + ((int64_t)b * 2) * C + c8 * 8, A1);
-  load_coef8(coef + ((int64_t)b * 2 + 1) * C + c8 * 8, A0);
+  gn_coef8(coef, b, c8 * 8, C, A1, A0);
   const int64_t rpc = (rows_b + nchunk - 1) / nchunk;
   const int64_t r0 = chunk * rpc, r1 = min(rows_b, r0 + rpc);
   const int64_t off = (int64_t)b * rows_b * C + c8 * 8;
@@ -294,15 +310,14 @@ __global__ void gn_param_grad_kernel(const float* __restrict__ pb, float* __rest
 
 template <typename T>
 __global__ __launch_bounds__(256) void gn_bwd_apply_kernel(const T* __restrict__ dout, const T* __restrict__ y,
-                                                           const float* __restrict__ coef, const float* __restrict__ E,
+                                                           const GnAffine coef, const float* __restrict__ E,
                                                            T* __restrict__ dy, int64_t rows_b, int C, int nchunk) {
   const int b = blockIdx.y, chunk = blockIdx.x;
   const int cv = C / 8, rl = 256 / cv;
   const int c8 = threadIdx.x % cv, rr = threadIdx.x / cv;
   if (rr >= rl) return;
   float A1[8], A0[8], E1[8], E2[8], E3[8];
-  load_coef8(coef + ((int64_t)b * 2) * C + c8 * 8, A1);
-  load_coef8(coef + ((int64_t)b * 2 + 1) * C + c8 * 8, A0);
+  gn_coef8(coef, b, c8 * 8, C, A1, A0);
   load_coef8(E + ((int64_t)b * 3) * C + c8 * 8, E1);
   load_coef8(E + ((int64_t)b * 3 + 1) * C + c8 * 8, E2);
   load_coef8(E + ((int64_t)b * 3 + 2) * C + c8 * 8, E3);
@@ -363,11 +378,12 @@ int cesm_gn_apply(int dtype, const void* y, const float* stats, const float* gam
                   const float* ss, const void* res, void* out, float* ws, int B, int64_t rows_b, int C, int G,
                   hipStream_t stream) {
   if (C % 8 || C / 8 > 256 || C % G) return CESM_EINVAL;
-  gn_coef_kernel<<<(unsigned)cdiv(B * C, 256), 256, 0, stream>>>(stats, gamma, beta, ss, ws, B, C, G);
+  const GnAffine aff{stats, gamma, beta, ss, G};
+  (void)ws;
   const int nch = gn_apply_chunks(rows_b, C);
   int rc = dispatch_dt(dtype, [&](auto* tp) {
     using T = std::remove_pointer_t<decltype(tp)>;
-    gn_apply_kernel<T><<<dim3(nch, B), 256, 0, stream>>>((const T*)y, ws, (const T*)res, (T*)out, rows_b, C, nch);
+    gn_apply_kernel<T><<<dim3(nch, B), 256, 0, stream>>>((const T*)y, aff, (const T*)res, (T*)out, rows_b, C, nch);
   });
   if (rc) return rc;
   return cesm_launch_status();
@@ -386,15 +402,15 @@ int cesm_gn_bwd(int dtype, const void* dout, const void* y, const float* stats, 
   float* coef = pb + (int64_t)B * C * 3;
   float* E = coef + (int64_t)B * C * 2;
   const double count = (double)rows_b * (C / G);
-  gn_coef_kernel<<<(unsigned)cdiv(B * C, 256), 256, 0, stream>>>(stats, gamma, beta, ss, coef, B, C, G);
+  const GnAffine aff{stats, gamma, beta, ss, G};
   const int nch = gn_apply_chunks(rows_b, C);
   int rc = dispatch_dt(dtype, [&](auto* tp) {
     using T = std::remove_pointer_t<decltype(tp)>;
-    gn_bwd_reduce_kernel<T><<<dim3(nchunk, B), 256, 0, stream>>>((const T*)dout, (const T*)y, coef, part, rows_b, C,
+    gn_bwd_reduce_kernel<T><<<dim3(nchunk, B), 256, 0, stream>>>((const T*)dout, (const T*)y, aff, part, rows_b, C,
                                                                  nchunk);
     gn_bwd_finalize_kernel<<<dim3(B, (unsigned)cdiv(C, 64)), 64 * GNF_KG, 0, stream>>>(part, stats, gamma, beta, ss, dss, pb,
                                                                                E, C, G, nchunk, count, (float)rows_b);
-    gn_bwd_apply_kernel<T><<<dim3(nch, B), 256, 0, stream>>>((const T*)dout, (const T*)y, coef, E, (T*)dy, rows_b, C,
+    gn_bwd_apply_kernel<T><<<dim3(nch, B), 256, 0, stream>>>((const T*)dout, (const T*)y, aff, E, (T*)dy, rows_b, C,
                                                              nch);
   });
   if (rc) return rc;
