@@ -1709,7 +1709,9 @@ __device__ __forceinline__ int wgb_swz(int r) {  // XOR on 4-element chunk index
 // of the first K tile multiply their dY fragments by a ones operand (MT extra MFMAs per step, no extra
 // memory traffic) and write per-split partials bslab[z][co] (replaces a separate column-sum pass
 // over dY, which re-read the whole tensor).
-template <int BM>
+// (BIAS: compile-time, so the plain instantiation keeps its register count — the bias accumulators
+// pushed the BM = 256 kernel past 128 VGPRs, a wave per SIMD fewer and 43 % slower.)
+template <int BM, bool BIAS = false>
 __global__ __launch_bounds__(256) void wgrad_wide_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
                                                          const bf16* __restrict__ dy1, const bf16* __restrict__ dy2,
                                                          float* __restrict__ slab, float* __restrict__ bslab, ConvGeom g,
@@ -1796,10 +1798,10 @@ __global__ __launch_bounds__(256) void wgrad_wide_kernel(const bf16* __restrict_
   for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bool bias_blk = bslab != nullptr && blockIdx.y == 0;  // uniform
-  f32x4 bacc[MT];
+  const bool bias_blk = BIAS && blockIdx.y == 0;  // uniform
+  f32x4 bacc[BIAS ? MT : 1];
 #pragma unroll
-  for (int i = 0; i < MT; ++i) bacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < (BIAS ? MT : 1); ++i) bacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 ones;
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.f;
@@ -1845,9 +1847,11 @@ __global__ __launch_bounds__(256) void wgrad_wide_kernel(const bf16* __restrict_
     for (int i = 0; i < MT; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    if (bias_blk) {
+    if constexpr (BIAS) {
+      if (bias_blk) {
 #pragma unroll
-      for (int i = 0; i < MT; ++i) bacc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, bacc[i], 0, 0, 0);
+        for (int i = 0; i < MT; ++i) bacc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, bacc[i], 0, 0, 0);
+      }
     }
     if (s + 1 < nsteps) sstore(std::integral_constant<int, buf ^ 1>{});
     __syncthreads();
@@ -1856,9 +1860,9 @@ __global__ __launch_bounds__(256) void wgrad_wide_kernel(const bf16* __restrict_
     step(s, I0{});
     if (s + 1 < nsteps) step(s + 1, I1{});
   }
-  if (bias_blk && lr == 0) {  // every output column holds the row sum: column 0 writes it
+  if (BIAS && bias_blk && lr == 0) {  // every output column holds the row sum: column 0 writes it
 #pragma unroll
-    for (int i = 0; i < MT; ++i)
+    for (int i = 0; i < (BIAS ? MT : 1); ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) bslab[(int64_t)blockIdx.z * g.Cout + co0 + wid * (BM / 4) + i * 16 + lg * 4 + r] = bacc[i][r];
   }
@@ -2872,16 +2876,17 @@ int cesm_conv_wgrad(int dtype, const void* x1, const void* x2, const void* dy1, 
     // wide-tile kernel; nsplit from the caller sized the slab for 64-row tiles, keep it
     const int bm = (Cout % 256 == 0 && Co1 % 256 == 0) ? 256 : ((Cout % 128 == 0 && Co1 % 128 == 0) ? 128 : 64);
     dim3 gw(Cout / bm, K / 64, nsplit);
-    float* bs = db ? bslab : nullptr;
-    if (bm == 256)
-      wgrad_wide_kernel<256><<<gw, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
-                                                     (const bf16*)dy2, slab, bs, g, (int)M, (int)pps);
-    else if (bm == 128)
-      wgrad_wide_kernel<128><<<gw, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
-                                                     (const bf16*)dy2, slab, bs, g, (int)M, (int)pps);
-    else
-      wgrad_wide_kernel<64><<<gw, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
-                                                    (const bf16*)dy2, slab, bs, g, (int)M, (int)pps);
+    auto launch = [&](auto bmc, auto biasc) {
+      constexpr int BMv = decltype(bmc)::value;
+      constexpr bool Bv = decltype(biasc)::value;
+      wgrad_wide_kernel<BMv, Bv><<<gw, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
+                                                         (const bf16*)dy2, slab, bslab, g, (int)M, (int)pps);
+    };
+    using T0 = std::false_type;
+    using T1 = std::true_type;
+    if (bm == 256) { if (db) launch(std::integral_constant<int, 256>{}, T1{}); else launch(std::integral_constant<int, 256>{}, T0{}); }
+    else if (bm == 128) { if (db) launch(std::integral_constant<int, 128>{}, T1{}); else launch(std::integral_constant<int, 128>{}, T0{}); }
+    else { if (db) launch(std::integral_constant<int, 64>{}, T1{}); else launch(std::integral_constant<int, 64>{}, T0{}); }
     if (db) colsum_final_kernel<<<Cout, 64, 0, stream>>>(bslab, db, nsplit, Cout, 1);
   } else if (db) {
     return CESM_EUNSUPPORTED;  // the bias gradient rides only on the wide kernel (callers use cesm_colsum)
