@@ -17,9 +17,6 @@
 namespace {
 
 constexpr int NH = 8, DH = 32, INNER = 256, QKV = 768;
-#ifndef SLAB_EMIT_LATE
-#define SLAB_EMIT_LATE 0  // slab_dx: dqkv emission after the head's dxn GEMMs
-#endif
 constexpr float LOG2E = 1.4426950408889634f;
 
 __device__ __forceinline__ bf16x8 zero8() {
@@ -812,7 +809,7 @@ __global__ __launch_bounds__(256, 2) void slab_dx_kernel(
         float sdq = 0.f;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          const f32x4 oT = o_out ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(aT[t], qb, z4, 0, 0, 0) : z4;
+          const f32x4 oT = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aT[t], qb, z4, 0, 0, 0);
           const f32x4 dqt = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[t], dob, z4, 0, 0, 0);
           const f32x4 dkt = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ad[t], vb, z4, 0, 0, 0);
           const f32x4 dvt = __builtin_amdgcn_mfma_f32_16x16x32_bf16(adT[t], kb, z4, 0, 0, 0);
@@ -857,26 +854,13 @@ __global__ __launch_bounds__(256, 2) void slab_dx_kernel(
 #pragma unroll
           for (int vt = 0; vt < NV; ++vt) dxacc[ct][vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq[vt], dxacc[ct][vt], 0, 0, 0);
         }
-        if (dqkv_out && !SLAB_EMIT_LATE) {
+        if (dqkv_out) {
 #pragma unroll
           for (int vt = 0; vt < NV; ++vt) {
             const int p = p0 + vt * 16 + lr;
             if (p < HW) *reinterpret_cast<bf16x8*>(dqkv_out + (rb + p) * QKV + kind * INNER + h * DH + lg * 8) = bq[vt];
           }
         }
-      }
-      // late emission: after all of the head's W^T loads (a load issued behind a store waits for it: vmcnt
-      // counts both in issue order), re-read from the LDS tile
-      if (dqkv_out && SLAB_EMIT_LATE) {
-#pragma unroll
-        for (int kind = 0; kind < 3; ++kind)
-#pragma unroll
-          for (int vt = 0; vt < NV; ++vt) {
-            const int p = p0 + vt * 16 + lr;
-            if (p < HW)
-              *reinterpret_cast<bf16x8*>(dqkv_out + (rb + p) * QKV + kind * INNER + h * DH + lg * 8) =
-                  ld16(sq + (vt * 16 + lr) * DQLD + kind * 32 + lg * 8);
-          }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
