@@ -67,13 +67,16 @@ __device__ __forceinline__ void rope(float* v, const float* rot, float sign) {
 }
 
 // grid: x = pixel-block (grid-stride), y = b*NH + h.  Block = G = TA_T/F groups of F lanes.
-template <typename T>
+// VLDS (long windows, F > 32): the pixel's v rows are staged in LDS next to k, so the per-key v read is
+// an LDS broadcast instead of the same global row loaded by all F lanes
+template <typename T, bool VLDS = false>
 __global__ __launch_bounds__(TA_T) void tattn_fwd_kernel(const T* __restrict__ qkv, const float* __restrict__ bias,
                                                          const float* __restrict__ rotg, T* __restrict__ out,
                                                          float* __restrict__ lse, int F, int HW, float scale) {
   extern __shared__ __attribute__((aligned(16))) float ta_dyn[];  // tables sized by F (ta_fwd_smem)
   float* rot = ta_dyn;        // [F][32]
   float* sb = rot + F * 32;   // [F][F]
+  float* svl = ta_dyn + ((F * 32 + F * F + 3) & ~3);  // VLDS: [TA_T][TA_LD] v rows
   __shared__ __attribute__((aligned(16))) float sk[TA_T * TA_LD];
   const int b = blockIdx.y / NH, h = blockIdx.y % NH;
   for (int e = threadIdx.x; e < F * 32; e += blockDim.x) rot[e] = rotg[e];
@@ -93,6 +96,11 @@ __global__ __launch_bounds__(TA_T) void tattn_fwd_kernel(const T* __restrict__ q
       load32(qkv + vi * QKV + INNER + h * DH, k);
       rope(k, rot + i * 32, 1.f);
       lds_store32(sk + threadIdx.x * TA_LD, k);
+      if constexpr (VLDS) {
+        float vv[32];
+        load32(qkv + vi * QKV + 2 * INNER + h * DH, vv);
+        lds_store32(svl + threadIdx.x * TA_LD, vv);
+      }
       load32(qkv + vi * QKV + h * DH, q);
 #pragma unroll
       for (int d = 0; d < 32; ++d) q[d] *= scale;
@@ -111,8 +119,12 @@ __global__ __launch_bounds__(TA_T) void tattn_fwd_kernel(const T* __restrict__ q
 #pragma unroll
         for (int d = 0; d < 32; ++d) s = fmaf(q[d], k[d], s);
         s += sb[i * F + j];
-        const int64_t vj = ((int64_t)b * F + j) * HW + p;
-        load32(qkv + vj * QKV + 2 * INNER + h * DH, v);
+        if constexpr (VLDS) {
+          lds_load32(svl + (g * F + j) * TA_LD, v);
+        } else {
+          const int64_t vj = ((int64_t)b * F + j) * HW + p;
+          load32(qkv + vj * QKV + 2 * INNER + h * DH, v);
+        }
         const float mn = fmaxf(m, s);
         const float corr = expf(m - mn);
         const float pj = expf(s - mn);
@@ -646,13 +658,19 @@ int cesm_tattn_nblk(int F, int HW) {
 
 int cesm_tattn_fwd(int dtype, const void* qkv, const float* bias, const float* rot, void* out, float* lse, int B,
                    int F, int HW, float scale, hipStream_t stream) {
-  const size_t sm = ta_fwd_smem(F);
+  const bool vlds = F > 32;
+  const size_t sm = vlds ? (size_t)((F * 32 + F * F + 3) & ~3) * 4 + (size_t)TA_T * TA_LD * 4 : ta_fwd_smem(F);
   if (F < 1 || F > TA_T || sm + TA_T * TA_LD * 4 > TA_LDS_MAX) return CESM_EUNSUPPORTED;
   dim3 grid(cesm_tattn_nblk(F, HW), B * NH);
   return dispatch_dt(dtype, [&](auto* tp) {
     using T = std::remove_pointer_t<decltype(tp)>;
-    ta_allow_smem(tattn_fwd_kernel<T>, sm);
-    tattn_fwd_kernel<T><<<grid, TA_T, sm, stream>>>((const T*)qkv, bias, rot, (T*)out, lse, F, HW, scale);
+    if (vlds) {
+      ta_allow_smem(tattn_fwd_kernel<T, true>, sm);
+      tattn_fwd_kernel<T, true><<<grid, TA_T, sm, stream>>>((const T*)qkv, bias, rot, (T*)out, lse, F, HW, scale);
+    } else {
+      ta_allow_smem(tattn_fwd_kernel<T>, sm);
+      tattn_fwd_kernel<T><<<grid, TA_T, sm, stream>>>((const T*)qkv, bias, rot, (T*)out, lse, F, HW, scale);
+    }
   }) ?: cesm_launch_status();
 }
 
