@@ -146,7 +146,10 @@ __global__ __launch_bounds__(TA_T) void tattn_fwd_kernel(const T* __restrict__ q
 // backward.  Phase 1 (lane = query i): D_i, dq_i, dbias row accumulation (k' rows in LDS).
 //            Phase 2 (lane = key j):   dk_j, dv_j (q' rows in LDS).
 // dbias partials: part[blockIdx.y][blockIdx.x][i][j] (the block's sum over its pixels)
-template <typename T>
+// VLDS (long windows, F > 32): the bias is read from global memory (cached) instead of an [F][F] LDS
+// table, and that LDS holds the pixel's v rows (phase 1) / dO rows (phase 2) instead, so the per-key
+// row read is an LDS broadcast rather than the same global row loaded by all F lanes
+template <typename T, bool VLDS = false>
 __global__ __launch_bounds__(TA_T) void tattn_bwd_kernel(const T* __restrict__ qkv, const T* __restrict__ o,
                                                          const T* __restrict__ dout, const float* __restrict__ lse,
                                                          const float* __restrict__ bias,
@@ -156,13 +159,15 @@ __global__ __launch_bounds__(TA_T) void tattn_bwd_kernel(const T* __restrict__ q
   extern __shared__ __attribute__((aligned(16))) float ta_dyn[];  // tables sized by F (ta_bwd_smem)
   const int AS = F + 1;                 // dbias row stride (odd: conflict-free column walks)
   float* rot = ta_dyn;                  // [F][32]
-  float* sb = rot + F * 32;             // [F][F]
-  float* sacc = sb + F * F;             // [TA_T][F + 1] per-lane dbias rows
+  float* sb = rot + F * 32;             // [F][F] (VLDS: v / dO rows [TA_T][TA_LD])
+  float* sacc = sb + (VLDS ? TA_T * TA_LD : F * F);  // [TA_T][F + 1] per-lane dbias rows
+  const float* gbias = bias + (int64_t)(blockIdx.y % NH) * F * F;
   __shared__ __attribute__((aligned(16))) float sv[TA_T * TA_LD];  // k' (phase 1) / q' (phase 2)
   __shared__ float sD[TA_T], sL[TA_T];
   const int b = blockIdx.y / NH, h = blockIdx.y % NH;
   for (int e = threadIdx.x; e < F * 32; e += blockDim.x) rot[e] = rotg[e];
-  for (int e = threadIdx.x; e < F * F; e += blockDim.x) sb[e] = bias[h * F * F + e];
+  if constexpr (!VLDS)
+    for (int e = threadIdx.x; e < F * F; e += blockDim.x) sb[e] = bias[h * F * F + e];
   for (int e = threadIdx.x; e < TA_T * AS; e += blockDim.x) sacc[e] = 0.f;
   __syncthreads();
   const int G = TA_T / F;
@@ -181,6 +186,11 @@ __global__ __launch_bounds__(TA_T) void tattn_bwd_kernel(const T* __restrict__ q
       load32(qkv + vi * QKV + INNER + h * DH, k);
       rope(k, rot + i * 32, 1.f);
       lds_store32(sv + threadIdx.x * TA_LD, k);
+      if constexpr (VLDS) {
+        float vv[32];
+        load32(qkv + vi * QKV + 2 * INNER + h * DH, vv);
+        lds_store32(sb + threadIdx.x * TA_LD, vv);
+      }
     }
     __syncthreads();
     if (ok) {
@@ -200,12 +210,16 @@ __global__ __launch_bounds__(TA_T) void tattn_bwd_kernel(const T* __restrict__ q
       for (int j = 0; j < F; ++j) {
         float k[32], v[32];
         lds_load32(sv + (g * F + j) * TA_LD, k);
-        const int64_t vj = ((int64_t)b * F + j) * HW + p;
-        load32(qkv + vj * QKV + 2 * INNER + h * DH, v);
+        if constexpr (VLDS) {
+          lds_load32(sb + (g * F + j) * TA_LD, v);
+        } else {
+          const int64_t vj = ((int64_t)b * F + j) * HW + p;
+          load32(qkv + vj * QKV + 2 * INNER + h * DH, v);
+        }
         float s = 0.f, dp = 0.f;
 #pragma unroll
         for (int d = 0; d < 32; ++d) { s = fmaf(q[d], k[d], s); dp = fmaf(dO[d], v[d], dp); }
-        s += sb[i * F + j];
+        s += VLDS ? gbias[i * F + j] : sb[i * F + j];
         const float P = expf(s - L);
         const float dS = P * (dp - D);
         myacc[j] += dS;
@@ -228,6 +242,11 @@ __global__ __launch_bounds__(TA_T) void tattn_bwd_kernel(const T* __restrict__ q
       for (int d = 0; d < 32; ++d) q[d] *= scale;
       rope(q, rot + i * 32, 1.f);
       lds_store32(sv + threadIdx.x * TA_LD, q);
+      if constexpr (VLDS) {
+        float dd[32];
+        load32(dout + vi * INNER + h * DH, dd);
+        lds_store32(sb + threadIdx.x * TA_LD, dd);
+      }
     }
     __syncthreads();
     if (ok) {
@@ -241,12 +260,16 @@ __global__ __launch_bounds__(TA_T) void tattn_bwd_kernel(const T* __restrict__ q
       for (int ii = 0; ii < F; ++ii) {
         float q[32], dO[32];
         lds_load32(sv + (g * F + ii) * TA_LD, q);
-        const int64_t vq = ((int64_t)b * F + ii) * HW + p;
-        load32(dout + vq * INNER + h * DH, dO);
+        if constexpr (VLDS) {
+          lds_load32(sb + (g * F + ii) * TA_LD, dO);
+        } else {
+          const int64_t vq = ((int64_t)b * F + ii) * HW + p;
+          load32(dout + vq * INNER + h * DH, dO);
+        }
         float s = 0.f, dp = 0.f;
 #pragma unroll
         for (int d = 0; d < 32; ++d) { s = fmaf(q[d], k[d], s); dp = fmaf(dO[d], v[d], dp); }
-        s += sb[ii * F + j];
+        s += VLDS ? gbias[ii * F + j] : sb[ii * F + j];
         const int t2 = g * F + ii;
         const float P = expf(s - sL[t2]);
         const float dS = P * (dp - sD[t2]);
@@ -678,14 +701,21 @@ int cesm_tattn_fwd(int dtype, const void* qkv, const float* bias, const float* r
 int cesm_tattn_bwd(int dtype, const void* qkv, const void* o, const void* dout, const float* lse, const float* bias,
                    const float* rot, void* dqkv, float* dbias_part, int B, int F, int HW, float scale,
                    hipStream_t stream) {
-  const size_t sm = ta_bwd_smem(F);
+  const bool vlds = F > 32;
+  const size_t sm = vlds ? (size_t)(F * 32 + TA_T * TA_LD + TA_T * (F + 1)) * 4 : ta_bwd_smem(F);
   if (F < 1 || F > TA_T || sm + (TA_T * TA_LD + 2 * TA_T) * 4 > TA_LDS_MAX) return CESM_EUNSUPPORTED;
   dim3 grid(cesm_tattn_nblk(F, HW), B * NH);
   return dispatch_dt(dtype, [&](auto* tp) {
     using T = std::remove_pointer_t<decltype(tp)>;
-    ta_allow_smem(tattn_bwd_kernel<T>, sm);
-    tattn_bwd_kernel<T><<<grid, TA_T, sm, stream>>>((const T*)qkv, (const T*)o, (const T*)dout, lse, bias, rot,
-                                                   (T*)dqkv, dbias_part, F, HW, scale);
+    if (vlds) {
+      ta_allow_smem(tattn_bwd_kernel<T, true>, sm);
+      tattn_bwd_kernel<T, true><<<grid, TA_T, sm, stream>>>((const T*)qkv, (const T*)o, (const T*)dout, lse, bias, rot,
+                                                            (T*)dqkv, dbias_part, F, HW, scale);
+    } else {
+      ta_allow_smem(tattn_bwd_kernel<T>, sm);
+      tattn_bwd_kernel<T><<<grid, TA_T, sm, stream>>>((const T*)qkv, (const T*)o, (const T*)dout, lse, bias, rot,
+                                                     (T*)dqkv, dbias_part, F, HW, scale);
+    }
   }) ?: cesm_launch_status();
 }
 
