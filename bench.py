@@ -34,7 +34,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=4, help="samples per GPU per step")
+    ap.add_argument("--batch", type=int, default=8, help="samples per GPU per step (8 x 8 GPUs = config/more_blocks batch_size 64)")
     ap.add_argument("--frames", type=int, default=12)
     ap.add_argument("--height", type=int, default=192)
     ap.add_argument("--width", type=int, default=288)
@@ -201,11 +201,13 @@ def main():
         avg_ms, avg_flops, n = ps
         ach = avg_flops / (avg_ms * 1e-3) / 1e12
         traffic, alg_bytes = pmc_traffic() if a.dtype == "bf16" else (None, None)
+        if traffic is not None:  # PMC passes run tools/conv_micro.py at B = 4; per-launch bytes scale with B
+            traffic, alg_bytes = traffic * a.batch / 4, alg_bytes * a.batch / 4
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(ach / peak, 4), "traffic": traffic,
                 "traffic_note": None if traffic is None else
-                f"HBM bytes/launch (PMC FETCH_SIZE+WRITE_SIZE, profiles/r1_conv3x3_traffic.json) vs "
-                f"{alg_bytes:.3g} algorithmic (input read + output write)",
+                f"HBM bytes/launch (PMC FETCH_SIZE+WRITE_SIZE at B=4, profiles/r1_conv3x3_traffic.json, scaled "
+                f"to B={a.batch}) vs {alg_bytes:.3g} algorithmic (input read + output write)",
                 "kernel": "conv3x3p_kernel (level-0 3x3 conv 64->64, fwd+dgrad; persistent, resident weights)" if a.dtype == "bf16" else
                           "conv_fwd_kernel<float,64>", "launches": n, "avg_us": round(avg_ms * 1e3, 2),
                 "flop_per_launch": avg_flops}
