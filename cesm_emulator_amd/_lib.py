@@ -21,12 +21,13 @@ _CTYPE = {"int": ctypes.c_int, "int64_t": ctypes.c_int64, "float": ctypes.c_floa
 
 
 def parse_header(path: Path = HEADER):
-    """Return {name: (restype, [argtypes])} for every `int cesm_*(...)` declaration."""
+    """Return {name: (restype, [argtypes])} for every `int cesm_*(...)` / `const char* cesm_*(...)`
+    declaration (the latter: host-only queries returning a static string)."""
     text = path.read_text()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     decls = {}
-    for m in re.finditer(r"\bint\s+(cesm_\w+)\s*\(([^)]*)\)\s*;", text, flags=re.S):
-        name, args = m.group(1), m.group(2)
+    for m in re.finditer(r"\b(int|const\s+char\s*\*)\s*(cesm_\w+)\s*\(([^)]*)\)\s*;", text, flags=re.S):
+        ret, name, args = m.group(1), m.group(2), m.group(3)
         types = []
         for a in args.split(","):
             a = " ".join(a.replace("const", " ").split())
@@ -37,7 +38,7 @@ def parse_header(path: Path = HEADER):
             else:
                 base = a.rsplit(" ", 1)[0]
                 types.append(_CTYPE[base])
-        decls[name] = (ctypes.c_int, types)
+        decls[name] = (ctypes.c_int if ret == "int" else ctypes.c_char_p, types)
     return decls
 
 

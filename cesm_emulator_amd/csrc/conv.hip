@@ -2689,6 +2689,83 @@ __global__ void head_reduce_kernel(const float* __restrict__ part, float* __rest
   }
 }
 
+// Kernel selection of cesm_conv_fwd (host only, no GPU work): every launch and the
+// cesm_conv_fwd_variant query go through this one function, so tests can assert which kernel a shape reaches.
+enum ConvFwdVariant {
+  CFV_INVALID = -1,
+  CFV_GEMM1X1_128 = 0, CFV_GEMM1X1_64, CFV_P36_RW, CFV_P36, CFV_P32_3STAGE, CFV_P32_RW, CFV_P32, CFV_W36, CFV_W32,
+  CFV_V2, CFV_HALO36, CFV_HALO32, CFV_TCONV_PAR_128, CFV_TCONV_PAR_64, CFV_GEN_BF16_128, CFV_GEN_BF16_64,
+  CFV_GEN_F32_128, CFV_GEN_F32_64, CFV_COUNT
+};
+static const char* const kConvFwdVariantName[CFV_COUNT] = {
+    "gemm1x1_kernel<128>", "gemm1x1_kernel<64>", "conv3x3p_kernel<36,8,true>", "conv3x3p_kernel<36,8,false>",
+    "conv3x3p_kernel<32,4,true,3,7>", "conv3x3p_kernel<32,7,true>", "conv3x3p_kernel<32,7,false>",
+    "conv3x3w_kernel<36>", "conv3x3w_kernel<32>", "conv3x3v2_kernel", "conv3x3_bf16_kernel<36>",
+    "conv3x3_bf16_kernel<32>", "conv_fwd_bf16_kernel<128,true>", "conv_fwd_bf16_kernel<64,true>",
+    "conv_fwd_bf16_kernel<128>", "conv_fwd_bf16_kernel<64>", "conv_fwd_kernel<float,128>",
+    "conv_fwd_kernel<float,64>"};
+
+struct ConvFwdPlan {
+  ConvFwdVariant v = CFV_INVALID;
+  int TH = 0, TW = 0;  // halo tile (conv3x3p / conv3x3w / v2 / halo kernels)
+};
+
+static ConvFwdPlan conv_fwd_plan(int dtype, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout, int Co1,
+                                 int KH, int KW, int S, int P, int U) {
+  ConvFwdPlan pl;
+  if ((C1 % BK) || (C2 % BK) || (Cout % 64) || (Co1 % 16) || Co1 > Cout || C1 <= 0) return pl;
+  if (dtype != CESM_DT_BF16 && dtype != CESM_DT_F32) return pl;
+  const int64_t M = (int64_t)Nb * Ho * Wo;
+  const int BN = (Cout % 128 == 0) ? 128 : 64;
+  const bool halo3 = dtype == CESM_DT_BF16 && KH == 3 && KW == 3 && S == 1 && P == 1 && U == 1 && Ho == Hi &&
+                     Wo == Wi && (Co1 % H3_BN) == 0 && !getenv_flag("CESM_NO_HALO");
+  const bool g1x1 = dtype == CESM_DT_BF16 && KH == 1 && KW == 1 && S == 1 && P == 0 && U == 1 && Ho == Hi &&
+                    Wo == Wi && (C1 % 64) == 0 && (C2 % 64) == 0 && (Co1 % 8) == 0 && M < (1ll << 31) &&
+                    M * (C1 > C2 ? C1 : C2) * 2 < (1ll << 31) && !getenv_flag("CESM_NO_GEMM1X1");
+  if (g1x1) {
+    pl.v = (Cout % 128 == 0) ? CFV_GEMM1X1_128 : CFV_GEMM1X1_64;
+  } else if (halo3 && Cout <= 1024 && !getenv_flag("CESM_CONV3X3_V1") &&
+             (getenv_flag("CESM_CONV3X3_V4") || ((C1 + C2) == 64 && Cout == 64 && (Wo % 32) == 0))) {
+    // v4 (persistent, resident weights) for the level-0 64 -> 64 convs by default;
+    // CESM_CONV3X3_V4=1 forces it for every 3x3 conv, CESM_CONV3X3_V1=1 disables it
+    // TW = 32 -> TH = 14 (448 px = 4 waves x 7 groups); TW = 36 -> TH <= 14 (<= 504 px, 8 groups)
+    const bool w36 = (Wo % 32) != 0 && (Wo % 36) == 0;
+    pl.TW = w36 ? 36 : 32;
+    pl.TH = CP_TH;
+    if (w36) {  // fewest tiles, then least padding
+      int best = 1 << 30;
+      for (int th = CP_TH; th >= 8; --th) {
+        const int nt = (int)cdiv(Ho, th);
+        if (nt * th < best) { best = nt * th; pl.TH = th; }
+      }
+    }
+    const bool rw = (C1 + C2) == 64 && Cout == 64 && !getenv_flag("CESM_NO_RESIDENT_W");
+    if (w36) pl.v = rw ? CFV_P36_RW : CFV_P36;
+    else if (rw && getenv_flag("CESM_CONV3X3_3STAGE")) { pl.v = CFV_P32_3STAGE; pl.TH = 8; }
+    else pl.v = rw ? CFV_P32_RW : CFV_P32;
+  } else if (halo3 && getenv_flag("CESM_CONV3X3_V3")) {
+    pl.TH = 16; pl.TW = 32;
+    cw_tile(Ho, Wo, pl.TH, pl.TW);
+    pl.v = pl.TW == 36 ? CFV_W36 : CFV_W32;
+  } else if (halo3 && getenv_flag("CESM_CONV3X3_V2")) {
+    pl.TH = 8; pl.TW = 32;
+    c2_tile(Ho, Wo, pl.TH, pl.TW);
+    pl.v = CFV_V2;
+  } else if (halo3) {
+    pl.TH = H3_TH; pl.TW = H3_TW;
+    if (!getenv_flag("CESM_CONV3X3_FIXED_TILE")) c2_tile(Ho, Wo, pl.TH, pl.TW, true);
+    pl.v = pl.TW == 36 ? CFV_HALO36 : CFV_HALO32;
+  } else if (dtype == CESM_DT_BF16 && U == 2 && S == 1 && KH % 2 == 0 && KW % 2 == 0 && Ho % 2 == 0 &&
+             Wo % 2 == 0 && !getenv_flag("CESM_NO_PARITY_TCONV")) {
+    pl.v = BN == 128 ? CFV_TCONV_PAR_128 : CFV_TCONV_PAR_64;
+  } else if (dtype == CESM_DT_BF16) {
+    pl.v = BN == 128 ? CFV_GEN_BF16_128 : CFV_GEN_BF16_64;
+  } else {
+    pl.v = BN == 128 ? CFV_GEN_F32_128 : CFV_GEN_F32_64;
+  }
+  return pl;
+}
+
 }  // namespace
 
 // ========================================================================================
@@ -2696,146 +2773,168 @@ __global__ void head_reduce_kernel(const float* __restrict__ part, float* __rest
 // ========================================================================================
 extern "C" {
 
+const char* cesm_conv_fwd_variant(int dtype, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout,
+                                  int Co1, int KH, int KW, int S, int P, int U) {
+  const ConvFwdPlan pl = conv_fwd_plan(dtype, Nb, Hi, Wi, C1, C2, Ho, Wo, Cout, Co1, KH, KW, S, P, U);
+  return pl.v == CFV_INVALID ? "invalid" : kConvFwdVariantName[pl.v];
+}
+
 // Generic implicit-GEMM conv / dgrad.  Shapes: x1 [Nb][Hi][Wi][C1], x2 [Nb][Hi][Wi][C2] (may be
 // null if C2 == 0), wp [Cout][KH*KW][C1+C2] packed, y1 [Nb][Ho][Wo][Co1], y2 [..][Cout-Co1].
 int cesm_conv_fwd(int dtype, const void* x1, const void* x2, const void* wp, const float* bias, const void* res,
                   const void* res2, void* y1, void* y2, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout, int Co1,
                   int KH, int KW, int S, int P, int U, hipStream_t stream) {
   if (Nb <= 0 || Ho <= 0 || Wo <= 0) return CESM_OK;
-  if ((C1 % BK) || (C2 % BK) || (Cout % 64) || (Co1 % 16) || Co1 > Cout || C1 <= 0) return CESM_EINVAL;
+  const ConvFwdPlan pl = conv_fwd_plan(dtype, Nb, Hi, Wi, C1, C2, Ho, Wo, Cout, Co1, KH, KW, S, P, U);
+  if (pl.v == CFV_INVALID) return CESM_EINVAL;
   ConvGeom g{Nb, Hi, Wi, Ho, Wo, C1, C2, Cout, Co1, KH, KW, S, P, U};
   const int64_t M = (int64_t)Nb * Ho * Wo;
   const int BN = (Cout % 128 == 0) ? 128 : 64;
   dim3 grid(Cout / BN, (unsigned)cdiv(M, BMP));
-  const bool halo3 = dtype == CESM_DT_BF16 && KH == 3 && KW == 3 && S == 1 && P == 1 && U == 1 && Ho == Hi &&
-                     Wo == Wi && (Co1 % H3_BN) == 0 && !getenv_flag("CESM_NO_HALO");
-  const bool g1x1 = dtype == CESM_DT_BF16 && KH == 1 && KW == 1 && S == 1 && P == 0 && U == 1 && Ho == Hi &&
-                    Wo == Wi && (C1 % 64) == 0 && (C2 % 64) == 0 && (Co1 % 8) == 0 && M < (1ll << 31) &&
-                    M * (C1 > C2 ? C1 : C2) * 2 < (1ll << 31) && !getenv_flag("CESM_NO_GEMM1X1");
-  if (g1x1) {
-    if (Cout % 128 == 0) {
-      dim3 gg(Cout / 128, (unsigned)cdiv(M, G1_BM));
-      gemm1x1_kernel<128><<<gg, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
-                                                  (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, (int)M, C1,
-                                                  C2, Cout, Co1);
-    } else {
-      dim3 gg(Cout / 64, (unsigned)cdiv(M, G1_BM));
-      gemm1x1_kernel<64><<<gg, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
-                                                 (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, (int)M, C1,
-                                                 C2, Cout, Co1);
-    }
-  } else if (halo3 && Cout <= 1024 && !getenv_flag("CESM_CONV3X3_V1") &&
-             (getenv_flag("CESM_CONV3X3_V4") || ((C1 + C2) == 64 && Cout == 64 && (Wo % 32) == 0))) {
-    // v4 (persistent, resident weights) for the level-0 64 -> 64 convs by default;
-    // CESM_CONV3X3_V4=1 forces it for every 3x3 conv, CESM_CONV3X3_V1=1 disables it
-    const int dbg = (getenv_flag("CESM_DBG_NODMA") ? 1 : 0) | (getenv_flag("CESM_DBG_NOMFMA") ? 2 : 0) |
-                    (getenv_flag("CESM_DBG_NOEPI") ? 4 : 0) | (getenv_flag("CESM_DBG_CLOCK") ? 16 : 0);
-    // TW = 32 -> TH = 14 (448 px = 4 waves x 7 groups); TW = 36 -> TH <= 14 (<= 504 px, 8 groups)
-    const bool w36 = (Wo % 32) != 0 && (Wo % 36) == 0;
-    const int TW = w36 ? 36 : 32;
-    int TH = CP_TH;
-    if (w36) {  // fewest tiles, then least padding
-      int best = 1 << 30;
-      for (int th = CP_TH; th >= 8; --th) {
-        const int nt = (int)cdiv(Ho, th);
-        if (nt * th < best) { best = nt * th; TH = th; }
+  const bf16 *bx1 = (const bf16*)x1, *bx2 = (const bf16*)x2, *bwp = (const bf16*)wp, *br = (const bf16*)res,
+             *br2 = (const bf16*)res2;
+  bf16 *by1 = (bf16*)y1, *by2 = (bf16*)y2;
+  const int TH = pl.TH, TW = pl.TW;
+  switch (pl.v) {
+    case CFV_GEMM1X1_128:
+    case CFV_GEMM1X1_64: {
+      if (pl.v == CFV_GEMM1X1_128) {
+        dim3 gg(Cout / 128, (unsigned)cdiv(M, G1_BM));
+        gemm1x1_kernel<128><<<gg, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, (int)M, C1, C2, Cout, Co1);
+      } else {
+        dim3 gg(Cout / 64, (unsigned)cdiv(M, G1_BM));
+        gemm1x1_kernel<64><<<gg, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, (int)M, C1, C2, Cout, Co1);
       }
+      break;
     }
-    const int tx = (int)cdiv(Wo, TW), ty = (int)cdiv(Ho, TH);
-    const int ncob = Cout / 64;
-    const int nitems = Nb * tx * ty * ncob;
-    const int nblk = std::min(nitems, cesm_num_cus());
-    const bool rw = (C1 + C2) == 64 && Cout == 64 && !getenv_flag("CESM_NO_RESIDENT_W");
-    if (w36 && rw)
-      conv3x3p_kernel<36, 8, true><<<nblk, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
-                                                             (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g,
-                                                             tx, tx * ty, TH, ncob, nitems, dbg);
-    else if (w36)
-      conv3x3p_kernel<36, 8, false><<<nblk, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
-                                                              (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2,
-                                                              g, tx, tx * ty, TH, ncob, nitems, dbg);
-    else if (rw && getenv_flag("CESM_CONV3X3_3STAGE")) {
-      // experimental: 8 x 32 tiles, 3 LDS stages (two steps of DMA in flight) - measured slower than
-      // 2 stages of 14 x 32 tiles (345 vs 315 us): the level-0 conv is HBM-bound (block-0 stamps: 2.2 GHz,
-      // DMA-only 175 us vs MFMA-only 166 us per launch), deeper prefetch does not add overlap
-      const int th8 = 8, ty8 = (int)cdiv(Ho, 8);
-      const int nit8 = Nb * tx * ty8;
-      conv3x3p_kernel<32, 4, true, 3, 7><<<std::min(nit8, cesm_num_cus()), 256, 0, stream>>>(
-          (const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias, (const bf16*)res, (const bf16*)res2, (bf16*)y1,
-          (bf16*)y2, g, tx, tx * ty8, th8, 1, nit8, dbg);
-    } else if (rw)
-      conv3x3p_kernel<32, 7, true><<<nblk, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
-                                                             (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g,
-                                                             tx, tx * ty, TH, ncob, nitems, dbg);
-    else
-      conv3x3p_kernel<32, 7, false><<<nblk, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
-                                                              (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2,
-                                                              g, tx, tx * ty, TH, ncob, nitems, dbg);
-  } else if (halo3 && getenv_flag("CESM_CONV3X3_V3")) {
-    int TH = 16, TW = 32;
-    cw_tile(Ho, Wo, TH, TW);
-    const int tx = (int)cdiv(Wo, TW), ty = (int)cdiv(Ho, TH);
-    dim3 g3(tx * ty, Nb, Cout / 64);
-    if (TW == 36)
-      conv3x3w_kernel<36><<<g3, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
-                                                  (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, tx, TH);
-    else
-      conv3x3w_kernel<32><<<g3, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
-                                                  (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, tx, TH);
-  } else if (halo3 && getenv_flag("CESM_CONV3X3_V2")) {
-    int TH = 8, TW = 32;
-    c2_tile(Ho, Wo, TH, TW);
-    const int tx = (int)cdiv(Wo, TW), ty = (int)cdiv(Ho, TH);
-    const int ncob = Cout / 64;
-    const int nitems = Nb * tx * ty * ncob;
-    const int nblk = std::min(nitems, cesm_num_cus());
-    conv3x3v2_kernel<<<nblk, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
-                                               (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, TH, TW,
-                                               tx, ty, ncob, nitems);
-  } else if (halo3) {
-    int TH = H3_TH, TW = H3_TW;
-    if (!getenv_flag("CESM_CONV3X3_FIXED_TILE")) c2_tile(Ho, Wo, TH, TW, true);
-    const int tx = (int)cdiv(Wo, TW), ty = (int)cdiv(Ho, TH);
-    dim3 g3(tx * ty, Nb, Cout / H3_BN);
-    if (TW == 36)
-      conv3x3_bf16_kernel<36><<<g3, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
-                                                      (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, tx,
-                                                      TH);
-    else
-      conv3x3_bf16_kernel<32><<<g3, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
-                                                      (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, tx,
-                                                      TH);
-  } else if (dtype == CESM_DT_BF16 && U == 2 && S == 1 && KH % 2 == 0 && KW % 2 == 0 && Ho % 2 == 0 &&
-             Wo % 2 == 0 && !getenv_flag("CESM_NO_PARITY_TCONV")) {
-    const int64_t Mp = (int64_t)Nb * (Ho / 2) * (Wo / 2);
-    const int bpp = (int)cdiv(Mp, BMP);
-    dim3 gp(Cout / BN, 4 * bpp);
-    if (BN == 128)
-      conv_fwd_bf16_kernel<128, true><<<gp, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp,
-                                                               bias, (const bf16*)res, (const bf16*)res2, (bf16*)y1,
-                                                               (bf16*)y2, g, Mp, bpp);
-    else
-      conv_fwd_bf16_kernel<64, true><<<gp, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp,
-                                                              bias, (const bf16*)res, (const bf16*)res2, (bf16*)y1,
-                                                              (bf16*)y2, g, Mp, bpp);
-  } else if (dtype == CESM_DT_BF16) {
-    if (BN == 128)
-      conv_fwd_bf16_kernel<128><<<grid, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
-                                                           (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, M);
-    else
-      conv_fwd_bf16_kernel<64><<<grid, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)wp, bias,
-                                                          (const bf16*)res, (const bf16*)res2, (bf16*)y1, (bf16*)y2, g, M);
-  } else if (dtype == CESM_DT_F32) {
-    if (BN == 128)
+    case CFV_P36_RW:
+    case CFV_P36:
+    case CFV_P32_3STAGE:
+    case CFV_P32_RW:
+    case CFV_P32: {
+      const int dbg = (getenv_flag("CESM_DBG_NODMA") ? 1 : 0) | (getenv_flag("CESM_DBG_NOMFMA") ? 2 : 0) |
+                      (getenv_flag("CESM_DBG_NOEPI") ? 4 : 0) | (getenv_flag("CESM_DBG_CLOCK") ? 16 : 0);
+      const int tx = (int)cdiv(Wo, TW), ty = (int)cdiv(Ho, TH);
+      const int ncob = Cout / 64;
+      const int nitems = Nb * tx * ty * ncob;
+      const int nblk = std::min(nitems, cesm_num_cus());
+      if (pl.v == CFV_P36_RW)
+        conv3x3p_kernel<36, 8, true><<<nblk, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, tx * ty,
+                                                               TH, ncob, nitems, dbg);
+      else if (pl.v == CFV_P36)
+        conv3x3p_kernel<36, 8, false><<<nblk, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx,
+                                                                tx * ty, TH, ncob, nitems, dbg);
+      else if (pl.v == CFV_P32_3STAGE)
+        // experimental: 8 x 32 tiles, 3 LDS stages (two steps of DMA in flight) - measured slower than
+        // 2 stages of 14 x 32 tiles (345 vs 315 us): the level-0 conv is HBM-bound (block-0 stamps: 2.2 GHz,
+        // DMA-only 175 us vs MFMA-only 166 us per launch), deeper prefetch does not add overlap
+        conv3x3p_kernel<32, 4, true, 3, 7><<<std::min(nitems, cesm_num_cus()), 256, 0, stream>>>(
+            bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, tx * ty, TH, 1, Nb * tx * ty, dbg);
+      else if (pl.v == CFV_P32_RW)
+        conv3x3p_kernel<32, 7, true><<<nblk, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, tx * ty,
+                                                               TH, ncob, nitems, dbg);
+      else
+        conv3x3p_kernel<32, 7, false><<<nblk, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx,
+                                                                tx * ty, TH, ncob, nitems, dbg);
+      break;
+    }
+    case CFV_W36:
+    case CFV_W32: {
+      const int tx = (int)cdiv(Wo, TW), ty = (int)cdiv(Ho, TH);
+      dim3 g3(tx * ty, Nb, Cout / 64);
+      if (pl.v == CFV_W36)
+        conv3x3w_kernel<36><<<g3, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, TH);
+      else
+        conv3x3w_kernel<32><<<g3, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, TH);
+      break;
+    }
+    case CFV_V2: {
+      const int tx = (int)cdiv(Wo, TW), ty = (int)cdiv(Ho, TH);
+      const int ncob = Cout / 64;
+      const int nitems = Nb * tx * ty * ncob;
+      const int nblk = std::min(nitems, cesm_num_cus());
+      conv3x3v2_kernel<<<nblk, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, TH, TW, tx, ty, ncob,
+                                                 nitems);
+      break;
+    }
+    case CFV_HALO36:
+    case CFV_HALO32: {
+      const int tx = (int)cdiv(Wo, TW), ty = (int)cdiv(Ho, TH);
+      dim3 g3(tx * ty, Nb, Cout / H3_BN);
+      if (pl.v == CFV_HALO36)
+        conv3x3_bf16_kernel<36><<<g3, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, TH);
+      else
+        conv3x3_bf16_kernel<32><<<g3, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, TH);
+      break;
+    }
+    case CFV_TCONV_PAR_128:
+    case CFV_TCONV_PAR_64: {
+      const int64_t Mp = (int64_t)Nb * (Ho / 2) * (Wo / 2);
+      const int bpp = (int)cdiv(Mp, BMP);
+      dim3 gp(Cout / BN, 4 * bpp);
+      if (pl.v == CFV_TCONV_PAR_128)
+        conv_fwd_bf16_kernel<128, true><<<gp, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, Mp, bpp);
+      else
+        conv_fwd_bf16_kernel<64, true><<<gp, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, Mp, bpp);
+      break;
+    }
+    case CFV_GEN_BF16_128:
+      conv_fwd_bf16_kernel<128><<<grid, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, M);
+      break;
+    case CFV_GEN_BF16_64:
+      conv_fwd_bf16_kernel<64><<<grid, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, M);
+      break;
+    case CFV_GEN_F32_128:
       conv_fwd_kernel<float, 128><<<grid, 256, 0, stream>>>((const float*)x1, (const float*)x2, (const float*)wp,
-                                                            bias, (const float*)res, (const float*)res2, (float*)y1, (float*)y2, g, M);
-    else
+                                                            bias, (const float*)res, (const float*)res2, (float*)y1,
+                                                            (float*)y2, g, M);
+      break;
+    case CFV_GEN_F32_64:
       conv_fwd_kernel<float, 64><<<grid, 256, 0, stream>>>((const float*)x1, (const float*)x2, (const float*)wp,
-                                                           bias, (const float*)res, (const float*)res2, (float*)y1, (float*)y2, g, M);
-  } else {
-    return CESM_EINVAL;
+                                                           bias, (const float*)res, (const float*)res2, (float*)y1,
+                                                           (float*)y2, g, M);
+      break;
+    default:
+      return CESM_EINVAL;
   }
   return cesm_launch_status();
+}
+
+}  // extern "C"
+
+namespace {
+// Kernel selection of cesm_conv_wgrad (host only)
+enum WgradVariant { WGV_W36 = 0, WGV_W32, WGV_WIDE, WGV_GEN };
+static int wgrad_plan(int dtype, int64_t M, int Hi, int Wi, int Ho, int Wo, int KH, int KW, int S, int P, int U) {
+  const bool halo3 = dtype == CESM_DT_BF16 && KH == 3 && KW == 3 && S == 1 && P == 1 && U == 1 && Ho == Hi &&
+                     Wo == Wi && !getenv_flag("CESM_NO_HALO");
+  // 8 x 36 tiles only where 32-wide tiles waste >= 20 % of the columns (W = 36, 72); at W = 144 / 288
+  // the 8 x 32 kernel's row-aligned K chunks are faster despite the partial last tile
+  if (halo3 && (Wo % W36_TW) == 0 && 5 * Wo <= 4 * (int)cdiv(Wo, W3_TW) * W3_TW && !getenv_flag("CESM_NO_WGRAD36"))
+    return WGV_W36;
+  if (halo3) return WGV_W32;
+  if (dtype == CESM_DT_BF16 && M < (1ll << 31) && !getenv_flag("CESM_NO_WIDE_WGRAD")) return WGV_WIDE;
+  return WGV_GEN;
+}
+}  // namespace
+
+extern "C" {
+
+const char* cesm_conv_wgrad_variant(int dtype, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout,
+                                    int Co1, int KH, int KW, int S, int P, int U, int with_bias) {
+  const int64_t M = (int64_t)Nb * Ho * Wo;
+  switch (wgrad_plan(dtype, M, Hi, Wi, Ho, Wo, KH, KW, S, P, U)) {
+    case WGV_W36: return "wgrad3x3w36_kernel";
+    case WGV_W32: return "wgrad3x3_bf16_kernel";
+    case WGV_WIDE: {
+      const int bm = (Cout % 256 == 0 && Co1 % 256 == 0) ? 256 : ((Cout % 128 == 0 && Co1 % 128 == 0) ? 128 : 64);
+      static const char* const names[6] = {"wgrad_wide_kernel<64, false>", "wgrad_wide_kernel<64, true>",
+                                           "wgrad_wide_kernel<128, false>", "wgrad_wide_kernel<128, true>",
+                                           "wgrad_wide_kernel<256, false>", "wgrad_wide_kernel<256, true>"};
+      return names[(bm == 256 ? 4 : bm == 128 ? 2 : 0) + (with_bias ? 1 : 0)];
+    }
+    default: return dtype == CESM_DT_BF16 ? "conv_wgrad_kernel<bf16>" : "conv_wgrad_kernel<float>";
+  }
 }
 
 // Weight gradient of the conv whose forward launch had geometry (…, KH, KW, S, P, U).
@@ -2854,25 +2953,22 @@ int cesm_conv_wgrad(int dtype, const void* x1, const void* x2, const void* dy1, 
   const int64_t pps = cdiv(cdiv(M, nsplit), WG_BP) * WG_BP;
   const int K = KH * KW * Cin;
   dim3 grid(Cout / 64, K / 64, nsplit);
-  const bool halo3 = dtype == CESM_DT_BF16 && KH == 3 && KW == 3 && S == 1 && P == 1 && U == 1 && Ho == Hi &&
-                     Wo == Wi && !getenv_flag("CESM_NO_HALO");
-  // 8 x 36 tiles only where 32-wide tiles waste >= 20 % of the columns (W = 36, 72); at W = 144 / 288
-  // the 8 x 32 kernel's row-aligned K chunks are faster despite the partial last tile
-  if (halo3 && (Wo % W36_TW) == 0 && 5 * Wo <= 4 * (int)cdiv(Wo, W3_TW) * W3_TW && !getenv_flag("CESM_NO_WGRAD36")) {
+  const int wv = wgrad_plan(dtype, M, Hi, Wi, Ho, Wo, KH, KW, S, P, U);
+  if (wv == WGV_W36) {
     const int tx = Wo / W36_TW;
     const int ntiles = Nb * tx * (int)cdiv(Ho, W36_TH);
     dim3 g3(Cout / 64, Cin / 32, std::min(nsplit, ntiles));
     wgrad3x3w36_kernel<<<g3, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
                                                (const bf16*)dy2, slab, g, tx, ntiles);
     nsplit = (int)g3.z;
-  } else if (halo3) {
+  } else if (wv == WGV_W32) {
     const int tx = (int)cdiv(Wo, W3_TW);
     const int ntiles = Nb * tx * (int)cdiv(Ho, W3_TH);
     dim3 g3(Cout / 64, Cin / 32, std::min(nsplit, ntiles));
     wgrad3x3_bf16_kernel<<<g3, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
                                                  (const bf16*)dy2, slab, g, tx, ntiles);
     nsplit = (int)g3.z;
-  } else if (dtype == CESM_DT_BF16 && M < (1ll << 31) && !getenv_flag("CESM_NO_WIDE_WGRAD")) {
+  } else if (wv == WGV_WIDE) {
     // wide-tile kernel; nsplit from the caller sized the slab for 64-row tiles, keep it
     const int bm = (Cout % 256 == 0 && Co1 % 256 == 0) ? 256 : ((Cout % 128 == 0 && Co1 % 128 == 0) ? 128 : 64);
     dim3 gw(Cout / bm, K / 64, nsplit);

@@ -194,11 +194,24 @@ __global__ void clip_coef_kernel(const double* __restrict__ part, int nblk, floa
   info[2] = fin ? 1.f : 0.f;
 }
 
+// step counter kept on the device: advanced only when the step is finite (info[2]), so a skipped step
+// leaves the bias corrections and the saved "step" consistent with exp_avg / exp_avg_sq (as
+// torch.optim.AdamW, which never sees a skipped step).  info[3] = the step number this update uses.
+__global__ void adamw_step_kernel(float* __restrict__ info, int* __restrict__ step) {
+  if (threadIdx.x != 0) return;
+  const int s = step[0] + ((info[2] != 0.f) ? 1 : 0);
+  step[0] = s;
+  info[3] = (float)s;
+}
+
 __global__ void adamw_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                              float* __restrict__ v, const float* __restrict__ info, int64_t n, float lr, float b1,
-                             float b2, float eps, float wd, float bc1, float bc2_sqrt, int use_clip) {
-  if (info && info[2] == 0.f) return;  // non-finite loss/grad: no update (train step raises)
-  const float coef = (use_clip && info) ? info[1] : 1.f;
+                             float b2, float eps, float wd, int use_clip) {
+  if (info[2] == 0.f) return;  // non-finite loss/grad: no update (train step raises)
+  const float coef = use_clip ? info[1] : 1.f;
+  const float st = info[3];
+  const float bc1 = 1.f - powf(b1, st);
+  const float bc2_sqrt = sqrtf(1.f - powf(b2, st));
   const float step_size = lr / bc1;
   const float decay = 1.f - lr * wd;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
@@ -336,12 +349,12 @@ int cesm_grad_norm(const float* g, int64_t n, float max_norm, const float* loss,
   return cesm_launch_status();
 }
 
-int cesm_adamw(float* p, float* g, float* m, float* v, const float* info, int64_t n, float lr, float b1, float b2,
-               float eps, float wd, int step, int use_clip, hipStream_t stream) {
-  const float bc1 = 1.f - powf(b1, (float)step);
-  const float bc2 = 1.f - powf(b2, (float)step);
+int cesm_adamw(float* p, float* g, float* m, float* v, float* info, int* step, int64_t n, float lr, float b1,
+               float b2, float eps, float wd, int use_clip, hipStream_t stream) {
+  if (!info || !step) return CESM_EINVAL;
+  adamw_step_kernel<<<1, 64, 0, stream>>>(info, step);
   const unsigned grid = (unsigned)std::min<int64_t>(cdiv(n, 256), 8192);
-  adamw_kernel<<<grid, 256, 0, stream>>>(p, g, m, v, info, n, lr, b1, b2, eps, wd, bc1, sqrtf(bc2), use_clip);
+  adamw_kernel<<<grid, 256, 0, stream>>>(p, g, m, v, info, n, lr, b1, b2, eps, wd, use_clip);
   return cesm_launch_status();
 }
 

@@ -496,9 +496,11 @@ def grad_norm(flat_grad, max_norm, loss=None):
     return info
 
 
-def adamw(p, g, m, v, info, lr, b1, b2, eps, wd, step, use_clip):
-    call("cesm_adamw", P(p), P(g), P(m), P(v), P(info), p.numel(), float(lr), float(b1), float(b2), float(eps),
-         float(wd), int(step), int(use_clip), S())
+def adamw(p, g, m, v, info, lr, b1, b2, eps, wd, step_dev, use_clip):
+    """step_dev: device int32 [1] step counter (advanced on device when the step is finite)"""
+    _chk(step_dev, (1,), torch.int32)
+    call("cesm_adamw", P(p), P(g), P(m), P(v), P(info), P(step_dev), p.numel(), float(lr), float(b1), float(b2),
+         float(eps), float(wd), int(use_clip), S())
 
 
 def cast(x, dtype):
@@ -514,3 +516,14 @@ def window_gather(cond, tgt, items, K, h, w, center):
     x0 = empty((n, 1, h, w), torch.float32, items.device)
     call("cesm_window_gather", P(cond), P(tgt), P(items), P(cwin), P(x0), n, K, M, H, W, h, w, int(center), S())
     return cwin, x0
+
+
+def conv_fwd_variant(dtype, Nb, Hi, Wi, C1, C2, Ho, Wo, Cout, Co1, KH, KW, S, P, U):
+    """name of the kernel cesm_conv_fwd selects for these arguments (host-only query)"""
+    return lib().cesm_conv_fwd_variant(_DT[dtype], Nb, Hi, Wi, C1, C2, Ho, Wo, Cout, Co1, KH, KW, S, P, U).decode()
+
+
+def conv_wgrad_variant(dtype, Nb, Hi, Wi, C1, C2, Ho, Wo, Cout, Co1, KH, KW, S, P, U, with_bias=False):
+    """name of the kernel cesm_conv_wgrad selects (host-only query)"""
+    return lib().cesm_conv_wgrad_variant(_DT[dtype], Nb, Hi, Wi, C1, C2, Ho, Wo, Cout, Co1, KH, KW, S, P, U,
+                                         int(bool(with_bias))).decode()

@@ -114,6 +114,10 @@ class Diffusion(nn.Module):
         self.register_buffer("sqrt_one_minus_alphas_cumprod", torch.sqrt(1.0 - ac))
         self.register_buffer("sqrt_recip_alphas", torch.sqrt(1.0 / alphas))
         self.register_buffer("posterior_variance", betas * (1.0 - acp) / (1.0 - ac))
+        # draws of t / eps in loss(): None = the default generator (as model.py:205-206); data-parallel
+        # training gives every rank its own stream (train.rank_generator) so ranks do not draw identical
+        # t / eps for their different samples
+        self.generator = None
 
     def q_sample(self, x0, t, noise=None):
         if noise is None:
@@ -125,10 +129,11 @@ class Diffusion(nn.Module):
     def loss(self, x0, cond, t=None, noise=None):
         """model.py:203-208; optional t / noise make the draw reproducible for parity tests."""
         B = x0.size(0)
+        g = self.generator
         if t is None:
-            t = torch.randint(0, self.T, (B,), device=x0.device).long()
+            t = torch.randint(0, self.T, (B,), device=x0.device, generator=g).long()
         if noise is None:
-            noise = torch.randn_like(x0)
+            noise = torch.randn(x0.shape, device=x0.device, dtype=x0.dtype, generator=g)
         x_t, noise = self.q_sample(x0, t, noise)
         eps = self.model(x_t, cond, t)
         return _MSE.apply(eps, noise.float().contiguous())

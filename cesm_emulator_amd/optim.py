@@ -77,7 +77,9 @@ class FusedAdamW:
         self.max_grad_norm = max_grad_norm
         self.exp_avg = torch.zeros_like(self.flat.data)
         self.exp_avg_sq = torch.zeros_like(self.flat.data)
-        self.step_count = 0
+        # step counter on the device: the AdamW launch advances it only for a finite step, so a skipped
+        # (non-finite) step leaves bias corrections and the saved "step" consistent with exp_avg/exp_avg_sq
+        self._step_dev = torch.zeros(1, dtype=torch.int32, device=self.flat.data.device)
         self.last_info = None  # device tensor: [norm, clip coef, finite, -]
         self.param_groups = [dict(params=self.flat.params, lr=self.lr, betas=self.betas, eps=self.eps,
                                   weight_decay=self.weight_decay)]
@@ -101,23 +103,32 @@ class FusedAdamW:
         if self.last_info is None or loss is not None:
             self.last_info = K.grad_norm(self.flat.grad, self.max_grad_norm or 0.0, loss)
         use_clip = bool(self.max_grad_norm)
-        self.step_count += 1
         K.adamw(self.flat.data, self.flat.grad, self.exp_avg, self.exp_avg_sq, self.last_info, lr, b1, b2,
-                g["eps"], g["weight_decay"], self.step_count, use_clip)
+                g["eps"], g["weight_decay"], self._step_dev, use_clip)
         self.last_info = None
         # parameters changed behind autograd's back: invalidate cached packed (bf16 / GEMM-layout) weights
         bump_param_epoch()
+
+    @property
+    def step_count(self):
+        """number of applied (finite) steps; reading it synchronises with the device"""
+        return int(self._step_dev.item())
+
+    @step_count.setter
+    def step_count(self, n):
+        self._step_dev.fill_(int(n))
 
     def state_dict(self):
         """torch.optim.AdamW layout — what train.py:1164 stores under "optimizer" — so checkpoints
         round-trip with the reference: state[i] for the i-th parameter passed in (frozen ones, e.g. the
         rotary freqs, carry no state), group keys as the installed torch's AdamW writes them."""
         state = {}
-        if self.step_count > 0:
+        nstep = self.step_count
+        if nstep > 0:
             for p, off in zip(self.flat.params, self.flat.offsets):
                 n = p.numel()
                 state[self._index[id(p)]] = {
-                    "step": torch.tensor(float(self.step_count)),
+                    "step": torch.tensor(float(nstep)),
                     "exp_avg": self.exp_avg[off:off + n].view_as(p).clone(),
                     "exp_avg_sq": self.exp_avg_sq[off:off + n].view_as(p).clone()}
         group = dict(_adamw_group_defaults())

@@ -26,6 +26,15 @@ def build_model_from_config(cfg_unet):
                 dropout=cfg_unet.get("dropout", 0.0))
 
 
+def rank_generator(device, seed=2, rank=0):
+    """per-rank t / eps stream for Diffusion.generator: seed + rank (SURVEY.md §8(e) E1 — the reference
+    draws from the default generator, model.py:205-206, which is identical on every rank after the same
+    manual_seed)."""
+    g = torch.Generator(device=device)
+    g.manual_seed(int(seed) + int(rank))
+    return g
+
+
 def make_optimizer(diffusion, train_cfg):
     """train.py:1077-1083 (+ the clip of :865 folded into the fused step)."""
     opt = train_cfg.get("optimizer", {})
@@ -55,6 +64,8 @@ def train_one_epoch(diffusion, dl, optimizer, device, max_grad_norm=1.0, use_amp
     """train.py:808-911; returns the epoch's mean loss."""
     diffusion.train()
     diffusion.model.compute_dtype = torch.bfloat16 if use_amp else torch.float32
+    if dp is not None and getattr(dp, "world", 1) > 1 and diffusion.generator is None:
+        diffusion.generator = rank_generator(device, 2, torch.distributed.get_rank())
     total, steps = 0.0, 0
     for step, (cond, x0) in enumerate(dl, start=1):
         cond = cond.to(device, non_blocking=True)

@@ -543,7 +543,6 @@ class UNetModel3D(nn.Module):
         self._pack_cache = {}
         self._pack_tables = {}  # dtype -> device int64 job table of the cached packs
         self._weights_epoch = 0
-        self._tape = None
 
     # ---------------------------------------------------------------- weight packing cache
     def invalidate_packed(self):
@@ -641,15 +640,13 @@ class UNetModel3D(nn.Module):
         head = self.out_conv[1]
         out = K.head_fwd(x, head.weight.reshape(-1), head.bias, B, F)
         tape.head_in = x
-        if save:
-            self._tape = tape
-        return out
+        return (out, tape) if save else out
 
-    def backward_from(self, dout):
-        tape = self._tape
+    def backward_from(self, dout, tape):
+        """backward of the forward that recorded `tape` (held by that forward's autograd node, so several
+        grad-enabled forwards may be in flight and each backward replays its own activations)."""
         if tape is None:
-            raise RuntimeError("backward called without a saved forward")
-        self._tape = None
+            raise RuntimeError("backward called twice for one forward (its tape was already consumed)")
         rc = tape.rc
         dev = dout.device
         hook = getattr(self, "_grad_ready", None)
@@ -718,11 +715,13 @@ class _NetFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, net, x_t, cond, t, anchor):
         ctx.net = net
-        return net.run_forward(x_t, cond, t, save=True)
+        out, ctx.tape = net.run_forward(x_t, cond, t, save=True)
+        return out
 
     @staticmethod
     def backward(ctx, dout):
-        ctx.net.backward_from(dout)
+        tape, ctx.tape = ctx.tape, None  # activations freed as soon as the backward has run
+        ctx.net.backward_from(dout, tape)
         return None, None, None, None, None
 
 

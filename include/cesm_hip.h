@@ -36,6 +36,13 @@ extern "C" {
 int cesm_conv_fwd(int dtype, const void* x1, const void* x2, const void* wp, const float* bias, const void* res,
                   const void* res2, void* y1, void* y2, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout, int Co1,
                   int KH, int KW, int S, int P, int U, hipStream_t stream);
+/* name of the kernel cesm_conv_fwd launches for these arguments (host-only query, no GPU work; the
+ * launcher itself selects through the same function).  "invalid" if cesm_conv_fwd would return EINVAL. */
+const char* cesm_conv_fwd_variant(int dtype, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout,
+                                  int Co1, int KH, int KW, int S, int P, int U);
+/* name of the kernel cesm_conv_wgrad launches (host-only query; with_bias: db != NULL) */
+const char* cesm_conv_wgrad_variant(int dtype, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout,
+                                    int Co1, int KH, int KW, int S, int P, int U, int with_bias);
 /* weight gradient of a cesm_conv_fwd launch; written in PyTorch layout [D0][D1][1][KH][KW] with the
  * (swap, flip) mapping of cesm_conv_pack.  slab: nsplit*Cout*KH*KW*(C1+C2) floats.
  * db (nullable): the conv bias gradient sum_px dY (+=), computed in the same pass (bslab: nsplit*Cout
@@ -175,9 +182,11 @@ int cesm_mse_bwd(const float* pred, const float* tgt, const float* gscale, float
 int cesm_grad_norm(const float* g, int64_t n, float max_norm, const float* loss, double* part, float* info,
                    hipStream_t stream);
 /* AdamW step (train.py:1077-1083, torch/optim/adam.py:417-547) over flat buffers; skipped on device
- * when info[2] == 0 (non-finite), applies the clip coefficient info[1] when use_clip. */
-int cesm_adamw(float* p, float* g, float* m, float* v, const float* info, int64_t n, float lr, float b1, float b2,
-               float eps, float wd, int step, int use_clip, hipStream_t stream);
+ * when info[2] == 0 (non-finite), applies the clip coefficient info[1] when use_clip.  step: device int
+ * step counter, advanced on device only for a finite step (info[3] <- the step number used for the bias
+ * corrections), so a skipped step leaves the count consistent with exp_avg / exp_avg_sq. */
+int cesm_adamw(float* p, float* g, float* m, float* v, float* info, int* step, int64_t n, float lr, float b1,
+               float b2, float eps, float wd, int use_clip, hipStream_t stream);
 /* out = a + b (gradient sums at residual / skip fan-outs) */
 int cesm_add(int dtype, const void* a, const void* b, void* out, int64_t n, hipStream_t stream);
 int cesm_cast(int dtype_in, int dtype_out, const void* x, void* y, int64_t n, hipStream_t stream);

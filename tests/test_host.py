@@ -128,3 +128,36 @@ def test_flop_count_reconciles_with_survey():
     # SURVEY omitted (64*64*9 + 128*64 = 45,056 MAC/voxel) and the tiny time-MLP linears
     survey = 1_816_256 + 1_880 * 12
     assert abs(per_voxel - (survey + 45_056)) < 5
+
+
+# ------------------------------------------------------------------ kernel dispatch (host-only queries)
+def test_bench_shape_dispatch_table():
+    """which kernel each bench-shape conv reaches (more_blocks 192x288, B*F = 96; cesm_conv_*_variant
+    runs the launchers' own selection on the host).  tests/test_gpu_prod_parity.py covers these."""
+    from cesm_emulator_amd import kernels as K
+    bf = torch.bfloat16
+    N = 96
+    fv = lambda *a: K.conv_fwd_variant(bf, N, *a)  # noqa: E731
+    wv = lambda *a, **k: K.conv_wgrad_variant(bf, N, *a, **k)  # noqa: E731
+    # level 0, 64 -> 64 3x3 (fwd and dgrad): the persistent resident-weight kernel
+    assert fv(192, 288, 64, 0, 192, 288, 64, 64, 3, 3, 1, 1, 1) == "conv3x3p_kernel<32,7,true>"
+    assert wv(192, 288, 64, 0, 192, 288, 64, 64, 3, 3, 1, 1, 1) == "wgrad3x3_bf16_kernel"
+    # level-0 concat inputs (up path / out_conv: 64 + 64 -> 64)
+    assert fv(192, 288, 64, 64, 192, 288, 64, 64, 3, 3, 1, 1, 1) == "conv3x3_bf16_kernel<32>"
+    # levels 1-3 (144, 72, 36 wide)
+    assert fv(96, 144, 128, 0, 96, 144, 128, 128, 3, 3, 1, 1, 1) == "conv3x3_bf16_kernel<32>"
+    assert fv(48, 72, 256, 0, 48, 72, 256, 256, 3, 3, 1, 1, 1) == "conv3x3_bf16_kernel<36>"
+    assert fv(24, 36, 512, 0, 24, 36, 512, 512, 3, 3, 1, 1, 1) == "conv3x3_bf16_kernel<36>"
+    assert wv(24, 36, 512, 0, 24, 36, 512, 512, 3, 3, 1, 1, 1) == "wgrad3x3w36_kernel"
+    # 768-channel qkv weight gradient of the fused attention blocks; the SLA to_out with its bias
+    assert wv(192, 288, 64, 0, 192, 288, 768, 768, 1, 1, 1, 0, 1) == "wgrad_wide_kernel<256, false>"
+    assert wv(192, 288, 256, 0, 192, 288, 64, 64, 1, 1, 1, 0, 1, with_bias=True) == "wgrad_wide_kernel<64, true>"
+    # 1x1 res_conv / to_qkv GEMMs, down- and up-sampling
+    assert fv(192, 288, 64, 0, 192, 288, 768, 768, 1, 1, 1, 0, 1) == "gemm1x1_kernel<128>"
+    assert fv(192, 288, 64, 0, 96, 144, 64, 64, 4, 4, 2, 1, 1) == "conv_fwd_bf16_kernel<64>"
+    assert fv(96, 144, 64, 0, 192, 288, 64, 64, 4, 4, 1, 2, 2) == "conv_fwd_bf16_kernel<64,true>"
+    # fp32 parity mode: the generic kernels
+    assert K.conv_fwd_variant(torch.float32, N, 192, 288, 64, 0, 192, 288, 64, 64, 3, 3, 1, 1, 1) == \
+        "conv_fwd_kernel<float,64>"
+    # arguments cesm_conv_fwd rejects
+    assert K.conv_fwd_variant(bf, N, 8, 8, 48, 0, 8, 8, 64, 64, 3, 3, 1, 1, 1) == "invalid"
