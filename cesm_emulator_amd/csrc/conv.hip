@@ -2928,12 +2928,12 @@ const char* cesm_conv_wgrad_variant(int dtype, int Nb, int Hi, int Wi, int C1, i
     case WGV_W32: return "wgrad3x3_bf16_kernel";
     case WGV_WIDE: {
       const int bm = (Cout % 256 == 0 && Co1 % 256 == 0) ? 256 : ((Cout % 128 == 0 && Co1 % 128 == 0) ? 128 : 64);
-      static const char* const names[6] = {"wgrad_wide_kernel<64, false>", "wgrad_wide_kernel<64, true>",
-                                           "wgrad_wide_kernel<128, false>", "wgrad_wide_kernel<128, true>",
-                                           "wgrad_wide_kernel<256, false>", "wgrad_wide_kernel<256, true>"};
+      static const char* const names[6] = {"wgrad_wide_kernel<64,false>", "wgrad_wide_kernel<64,true>",
+                                           "wgrad_wide_kernel<128,false>", "wgrad_wide_kernel<128,true>",
+                                           "wgrad_wide_kernel<256,false>", "wgrad_wide_kernel<256,true>"};
       return names[(bm == 256 ? 4 : bm == 128 ? 2 : 0) + (with_bias ? 1 : 0)];
     }
-    default: return dtype == CESM_DT_BF16 ? "conv_wgrad_kernel<bf16>" : "conv_wgrad_kernel<float>";
+    default: return dtype == CESM_DT_BF16 ? "conv_wgrad_kernel<__bf16>" : "conv_wgrad_kernel<float>";
   }
 }
 

@@ -150,8 +150,8 @@ def test_bench_shape_dispatch_table():
     assert fv(24, 36, 512, 0, 24, 36, 512, 512, 3, 3, 1, 1, 1) == "conv3x3_bf16_kernel<36>"
     assert wv(24, 36, 512, 0, 24, 36, 512, 512, 3, 3, 1, 1, 1) == "wgrad3x3w36_kernel"
     # 768-channel qkv weight gradient of the fused attention blocks; the SLA to_out with its bias
-    assert wv(192, 288, 64, 0, 192, 288, 768, 768, 1, 1, 1, 0, 1) == "wgrad_wide_kernel<256, false>"
-    assert wv(192, 288, 256, 0, 192, 288, 64, 64, 1, 1, 1, 0, 1, with_bias=True) == "wgrad_wide_kernel<64, true>"
+    assert wv(192, 288, 64, 0, 192, 288, 768, 768, 1, 1, 1, 0, 1) == "wgrad_wide_kernel<256,false>"
+    assert wv(192, 288, 256, 0, 192, 288, 64, 64, 1, 1, 1, 0, 1, with_bias=True) == "wgrad_wide_kernel<64,true>"
     # 1x1 res_conv / to_qkv GEMMs, down- and up-sampling
     assert fv(192, 288, 64, 0, 192, 288, 768, 768, 1, 1, 1, 0, 1) == "gemm1x1_kernel<128>"
     assert fv(192, 288, 64, 0, 96, 144, 64, 64, 4, 4, 2, 1, 1) == "conv_fwd_bf16_kernel<64>"
