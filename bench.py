@@ -146,6 +146,23 @@ class KernelProbe:
                 b += v * (768 * 2 + C * 2 + (512 if emit_o else 0))
             return lab, v * tw_core_flop(C, F), float(b)
 
+        def tblock_fwd_fold(x, gamma, wqkv_f32, wout, bias, rot, B, F, scale, save=True, eps=1e-5, save_o=False):
+            Nb, H, W, C = x.shape
+            v = Nb * H * W
+            nv = (4 * F + 15) // 16
+            b = v * (2 * C * 2 + (40 if save else 0) + (512 if save_o else 0))
+            return f"tw_fwd_kernel<{C},{nv},true>", v * tw_core_flop(C, F), float(b)
+
+        def tblock_bwd_dw(x, dy, mr, lse, wqkv_f32, gamma, wout_t, bias, rot, dwqkv, dgamma, dtable, B, F, scale,
+                          num_buckets=32, max_distance=32):
+            Nb, H, W, C = x.shape
+            v = Nb * H * W
+            nv = (4 * F + 15) // 16
+            # dgrad-equivalent work (the forward's FLOPs) + the in-kernel to_qkv weight gradient (2 * 768 * C per
+            # voxel); bytes: x, dy, mr / lse read, dx written (no per-voxel intermediates)
+            return (f"twh_bwd_kernel<{nv}> (+ dW / dgamma / dbias reductions)",
+                    v * (tw_core_flop(C, F) + 2.0 * 768 * C), float(v * (3 * C * 2 + 40)))
+
         def sla_flop(C):  # per voxel: to_qkv + to_out + context k v^T and context^T q (8 heads, 32 x 32)
             return 2.0 * 768 * C + 2.0 * 256 * C + 2.0 * 2 * 32 * 32 * 8
 
@@ -186,6 +203,7 @@ class KernelProbe:
             return "add_kernel", 0.0, float(a.numel() * es_of(a) * 3)
 
         for name, fn in dict(conv_fwd=conv_fwd, conv_wgrad=conv_wgrad, tblock_fwd=tblock_fwd, tblock_bwd=tblock_bwd,
+                             tblock_fwd_fold=tblock_fwd_fold, tblock_bwd_dw=tblock_bwd_dw,
                              slaf_fwd=slaf_fwd, slaf_bwd=slaf_bwd, gn_stats=gn_stats, gn_apply=gn_apply, gn_bwd=gn_bwd,
                              ln_fwd=ln_fwd, ln_bwd=ln_bwd, adamw=adamw, add=add).items():
             self._wrap(name, fn)

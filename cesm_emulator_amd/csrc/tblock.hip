@@ -691,6 +691,17 @@ __device__ __forceinline__ bf16x8 kslot_gather(const bf16* tile, int rb, int c0,
   return r;
 }
 
+// kslot_gather for a tile of row stride ld (bf16 elements)
+__device__ __forceinline__ bf16x8 kslot_gather_ld(const bf16* tile, int ld, int rb, int c0, int F, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tile + (rb + 4 * g + q) * ld + c0 + 4 * p));
+  bf16x8 r = zero8();
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    if (4 * g + e < F) r[e] = __builtin_bit_cast(bf16, (short)v[e]);
+  return r;
+}
+
 // RoPE rotation of 4 consecutive head dims d0..d0+3 (two pairs) of frame f; sign=-1 applies R^T
 __device__ __forceinline__ void rope4(float* o4, const float* rot, int f, int d0, float sign) {
   const f32x4 cs = *reinterpret_cast<const f32x4*>(rot + f * RS + d0);  // (c0, s0, c1, s1)
@@ -800,7 +811,7 @@ __device__ __forceinline__ void tw_qkv(const bf16* __restrict__ wqkv, const bf16
 
 // LN of the wave's voxels on the B fragments.  use_saved: take (mean, rstd) from mr, else compute
 // them (and store them to mr when non-null).
-template <int C, int NV>
+template <int C, int NV, bool GAM = true>
 __device__ __forceinline__ void tw_ln(const bf16* __restrict__ x, const float* __restrict__ gamma, float* mr_out,
                                       const float* __restrict__ mr_in, bf16x8 (&xf)[TW<C, NV>::NVTM][TW<C, NV>::KS], int NVT,
                                       int VW, int F, int p0, int HW, int b, float eps, int lr, int lg) {
@@ -810,7 +821,12 @@ __device__ __forceinline__ void tw_ln(const bf16* __restrict__ x, const float* _
   // of every voxel tile
   float gm[T::KS][8];
 #pragma unroll
-  for (int ks = 0; ks < T::KS; ++ks) load8(gamma + ks * 32 + lg * 8, gm[ks]);
+  for (int ks = 0; ks < T::KS; ++ks) {
+    if constexpr (GAM) load8(gamma + ks * 32 + lg * 8, gm[ks]);
+    else
+#pragma unroll
+      for (int i = 0; i < 8; ++i) gm[ks][i] = 1.f;  // gamma folded into the weights (xf = xhat)
+  }
   bf16x8 raw[T::NVTM][T::KS];
   bool okv[T::NVTM];
   int64_t rows[T::NVTM];
@@ -866,7 +882,7 @@ __device__ __forceinline__ void tw_ln(const bf16* __restrict__ x, const float* _
 #endif
 template <int C>
 constexpr int tw_fwd_occ() { return C <= 64 ? TW_FWD_OCC64 : 2; }
-template <int C, int NV>
+template <int C, int NV, bool FOLD = false>
 __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ gamma,
                                                      const bf16* __restrict__ wqkv, const bf16* __restrict__ wout,
                                                      const float* __restrict__ bias, const float* __restrict__ rotg,
@@ -896,7 +912,9 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
   for (int vt = 0; vt < NV; ++vt) fr[vt] = (vt * 16 + lr) % F;
 
   bf16x8 xf[T::NVTM][T::KS];
-  tw_ln<C, NV>(x, gamma, mr, nullptr, xf, NVT, VW, F, p0, HW, b, eps, lr, lg);
+  // FOLD: wqkv is the image of W diag(gamma) and the B fragments hold xhat (twh_bwd_kernel recomputes
+  // q/k/v the same way, so forward and backward see identical bf16 operands)
+  tw_ln<C, NV, !FOLD>(x, gamma, mr, nullptr, xf, NVT, VW, F, p0, HW, b, eps, lr, lg);
 
   f32x4 yacc[T::CT][T::NVTM];
 #pragma unroll
@@ -1308,6 +1326,20 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
       TW_ST(4)
     }
     // LN backward: dx = rstd*(g - mean(g) - xhat*mean(g*xhat)) + dy, g = dxn*gamma
+#if defined(TWB_ABL_LNB) && TWB_ABL_LNB == 0
+    // ablation (diagnostic builds only): dx = dxn, no LN-backward loads / reductions
+#pragma unroll
+    for (int vt = 0; vt < T::NVTM; ++vt) {
+      int64_t row = 0;
+      if (vt < NVT && tw_row(vt * 16 + lr, VW, F, p0, HW, b, row))
+#pragma unroll
+        for (int ct = 0; ct < T::CT; ++ct) {
+          float o4[4] = {dxacc[ct][vt][0], dxacc[ct][vt][1], dxacc[ct][vt][2], dxacc[ct][vt][3]};
+          stnt4(dx + row * C + ct * 16 + lg * 4, o4);
+        }
+    }
+    if (false)
+#endif
 #pragma unroll
     for (int vt = 0; vt < T::NVTM; ++vt) {
       if (vt >= NVT) break;
@@ -1408,16 +1440,16 @@ static void allow_smem(K kernel, size_t bytes) {
   if (bytes > 65536) hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
-template <int C, int NV>
+template <int C, int NV, bool FOLD = false>
 static void tw_fwd_launch_nv(const void* x, const float* gamma, const void* wqkv, const void* wout, const float* bias,
                              const float* rot, void* y, float* mr, float* lse, void* o, int B, int F, int HW,
                              float scale, float eps, hipStream_t stream) {
   const int npg = (int)cdiv(HW, TW<C>::PW);
   dim3 grid((unsigned)cdiv(npg, 4), B);
   const size_t sm = tw_fwd_smem<C>(F);
-  allow_smem(tw_fwd_kernel<C, NV>, sm);
-  tw_fwd_kernel<C, NV><<<grid, 256, sm, stream>>>((const bf16*)x, gamma, (const bf16*)wqkv, (const bf16*)wout, bias,
-                                                  rot, (bf16*)y, mr, lse, (bf16*)o, F, HW, scale, eps);
+  allow_smem(tw_fwd_kernel<C, NV, FOLD>, sm);
+  tw_fwd_kernel<C, NV, FOLD><<<grid, 256, sm, stream>>>((const bf16*)x, gamma, (const bf16*)wqkv, (const bf16*)wout,
+                                                        bias, rot, (bf16*)y, mr, lse, (bf16*)o, F, HW, scale, eps);
 }
 
 template <int C>
@@ -1486,6 +1518,445 @@ extern "C" int cesm_diag_tw_stamps(unsigned long long* out, int n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tw_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -3;
 }
 #endif
+
+// ============================================================================================
+// Head-parallel fused backward with in-kernel weight gradients (C = 64, 4*F <= 48).
+//
+// A block of 8 waves processes one pixel group (4 pixels x F frames) at a time, wave h owning head h:
+// LN (block-cooperative, xhat and dy tiles in LDS) -> per wave: q/k/v_h and dO_h GEMMs, the attention-core
+// backward, dxn_h = W'_h^T dqkv_h (partial over heads) and dW'_h += dqkv_h^T xhat (MFMA accumulators that
+// stay in registers for the whole kernel) -> the 8 partial dxn summed through LDS -> LN backward -> dx.
+// Nothing per voxel is written but dx: the 768-channel dqkv and xn tensors of the wave-private kernel
+// (1.8 KB per voxel, re-read by the weight-gradient GEMM) do not exist on this path.
+// gamma is folded into the weights: W' = W diag(gamma) (images built from the fp32 master weight), so the
+// GEMMs take xhat and the dxn GEMM yields g = gamma * dxn directly; the weight gradient leaves the kernel
+// as dW' = sum dqkv^T xhat, and twh_dw_finalize turns it into dW = dW' diag(gamma) and
+// dgamma_c = sum_j W[j][c] dW'[j][c] (the LN gamma gradient sum_v dxn*xhat, regrouped).
+// ============================================================================================
+#ifndef TWH_FULL
+// measured at B = 8 (tools/tblock_time.py): PG 2 / FULL 0 / EARLY_WT 0 4.47 ms (no spills); PG 2 with both on
+// 5.35 ms (40 VGPRs spilled); PG 1 4.86 ms
+#define TWH_FULL 0      // twh_bwd: the head's 12 q/k/v weight fragments at once (1) or in two-tile batches (0)
+#endif
+#ifndef TWH_PG
+#define TWH_PG 2        // twh_bwd: pixels whose attention-core backward is interleaved phase by phase
+#endif
+#ifndef TWH_EARLY_WT
+#define TWH_EARLY_WT 0  // twh_bwd: W'^T fragments of the dxn GEMM issued before the dW GEMM (1)
+#endif
+constexpr int TH_XLD = 72;   // xhat / dy tile row stride (bf16, 144-B rows)
+constexpr int TH_NVMAX = 3;  // voxel tiles per group (4*F <= 48): the 8 slices then fit in LDS
+
+// lane (g, i) <- tile[r0 + 4g + e][c0 + i], e = 0..3 (hardware transpose read; EXEC all ones)
+__device__ __forceinline__ s16x4 tr4(const bf16* tile, int ld, int r0, int c0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tile + (r0 + 4 * g + q) * ld + c0 + 4 * p));
+}
+
+constexpr int TH_PLD = 68;  // fp32 row stride of a wave's partial dxn rows (written over its own slices)
+// an SGPR zero the compiler cannot see through: added to the weight-image pointers inside the group loop so
+// the (loop-invariant, per-head) fragment loads are not hoisted out of it and kept live across the loop
+__device__ __forceinline__ int opaque_zero() {
+  int z;
+  asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+  return z;
+}
+
+static size_t twh_smem(int F, int NV) {
+  (void)F;
+  const int R = NV * 16;
+  return (size_t)16 * RS * 4 + (size_t)8 * TWH_PG * 2 * 256 * 2 + (size_t)2 * R * TH_XLD * 2 +
+         (size_t)8 * 4 * R * HLD * 2 + 1024;  // + tail pad: masked k-slot gathers may read 4 rows past a slice
+}
+
+template <int NV>
+__global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ dy, const float* __restrict__ mr,
+    const float* __restrict__ lse, const bf16* __restrict__ wqkv, const bf16* __restrict__ wqkv_t,
+    const bf16* __restrict__ wout_t, const float* __restrict__ bias, const float* __restrict__ rotg,
+    bf16* __restrict__ dx, float* __restrict__ dw_slab, float* __restrict__ dbias_part, int B, int F, int HW,
+    float scale) {
+  constexpr int C = 64;
+  using T = TW<C, NV>;
+  constexpr int R = NV * 16;
+  static_assert(TH_PLD * 4 <= 4 * HLD * 2, "partial dxn rows fit over the wave's slices");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int FF = F * F;
+  float* rot = smem;                                 // [16][RS]
+  float* trbuf = rot + 16 * RS;                      // [8 waves][TWH_PG][2][16][16] bf16 P / dS tiles
+  bf16* xt = reinterpret_cast<bf16*>(trbuf) + 8 * TWH_PG * 2 * 256;  // [R][TH_XLD] xhat (bf16)
+  bf16* dyt = xt + R * TH_XLD;                       // [R][TH_XLD] dy
+  bf16* slices = dyt + R * TH_XLD;                   // 8 x [q|k|v|dO][R][HLD]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int h = wid;
+  bf16* sq = slices + wid * 4 * R * HLD;
+  bf16* sk = sq + R * HLD;
+  bf16* sv = sk + R * HLD;
+  bf16* sdo = sv + R * HLD;
+  for (int e = tid; e < F * 32; e += 512) rot[(e >> 5) * RS + (e & 31)] = rotg[e];
+  // this wave's (head's) bias entries, log2 units: transposed (i = lr, j = 4g + r) and row-major (i = 4g + r, j = lr)
+  float bt[4], brm[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int c = lg * 4 + r;
+    const bool ok = c < F && lr < F;
+    const int i0 = ok ? lr : 0, c0 = ok ? c : 0;
+    const float b0 = bias[(h * F + i0) * F + c0], b1 = bias[(h * F + c0) * F + i0];
+    bt[r] = ok ? b0 * LOG2E : 0.f;
+    brm[r] = ok ? b1 * LOG2E : 0.f;
+  }
+
+  const int VW = T::PW * F;
+  const int npg = (HW + T::PW - 1) / T::PW;
+  const int ngroups = B * npg;
+  // LN / LN-backward role of this thread: voxel vv of the group, channels 8cc..8cc+7
+  const int vv = tid >> 3, cc = tid & 7;
+  int fr[NV];
+#pragma unroll
+  for (int vt = 0; vt < NV; ++vt) fr[vt] = (vt * 16 + lr) % F;
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+
+  // the voxel row of (group gg, voxel v) or -1
+  auto vrow = [&](int gg, int v) -> int64_t {
+    const int b = gg / npg, pg = gg - b * npg;
+    if (v >= VW) return -1;
+    const int pp = v / F, f = v - pp * F, p = pg * T::PW + pp;
+    if (p >= HW) return -1;
+    return ((int64_t)b * F + f) * HW + p;
+  };
+  // prefetch registers: x, dy chunk and (mean, rstd) of this thread's voxel in the next group
+  bf16x8 xpf = zero8(), dpf = zero8();
+  float mpf = 0.f, rpf = 0.f;
+  bool okpf = false;
+  auto prefetch = [&](int gg) {
+    const int64_t row = gg < ngroups && vv < R ? vrow(gg, vv) : -1;
+    okpf = row >= 0;
+    const int64_t rr = okpf ? row : 0;  // unconditional loads, selected afterwards
+    xpf = ldnt16(x + rr * C + cc * 8);
+    dpf = ldnt16(dy + rr * C + cc * 8);
+    mpf = mr[rr * 2];
+    rpf = mr[rr * 2 + 1];
+  };
+
+  // weight-gradient accumulators dW'_h [q|k|v x 32 rows][64]: 6 row tiles x 4 column tiles
+  f32x4 dwacc[6][4];
+#pragma unroll
+  for (int m = 0; m < 6; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) dwacc[m][n] = z4;
+  float dbacc[4] = {0.f, 0.f, 0.f, 0.f};
+
+  prefetch(blockIdx.x);
+  TW_ST_DECL
+  for (int gg = blockIdx.x; gg < ngroups; gg += gridDim.x) {
+    const int b = gg / npg, p0 = (gg - b * npg) * T::PW;
+    // ---- LN of the group (this thread's voxel chunk) from the prefetch registers
+    float rstd_cur = 0.f;
+    if (vv < R) {
+      const bool ok = okpf;
+      bf16x8 xh, dv;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        xh[e] = (bf16)(ok ? ((float)xpf[e] - mpf) * rpf : 0.f);
+        dv[e] = ok ? dpf[e] : (bf16)0.f;
+      }
+      *reinterpret_cast<bf16x8*>(xt + vv * TH_XLD + cc * 8) = xh;
+      *reinterpret_cast<bf16x8*>(dyt + vv * TH_XLD + cc * 8) = dv;
+      rstd_cur = ok ? rpf : 0.f;
+    }
+    const bool ok_cur = okpf;
+    const int oz = opaque_zero();
+    const bf16* wq_g = wqkv + oz;
+    const bf16* wqt_g = wqkv_t + oz;
+    const bf16* wot_g = wout_t + oz;
+    __syncthreads();  // (A) tiles of this group ready; previous group's partials consumed
+    prefetch(gg + gridDim.x);  // next group's x / dy / stats: in flight during the head phase
+    TW_ST(0)
+
+    // ---- head phase: wave h
+    float Lp[T::PW];
+#pragma unroll
+    for (int pp = 0; pp < T::PW; ++pp) {
+      const bool ok = lr < F && p0 + pp < HW;
+      const float v = lse[(((int64_t)b * NH + h) * HW + (ok ? p0 + pp : 0)) * F + (ok ? lr : 0)];
+      Lp[pp] = ok ? v : 0.f;
+    }
+    {
+      bf16x8 xf[NV][T::KS];
+#pragma unroll
+      for (int vt = 0; vt < NV; ++vt)
+#pragma unroll
+        for (int ks = 0; ks < T::KS; ++ks) xf[vt][ks] = ld16(xt + (vt * 16 + lr) * TH_XLD + ks * 32 + lg * 8);
+      tw_qkv<C, NV, TWH_FULL != 0>(wq_g, xf, h, fr, scale, rot, sq, sk, sv, lr, lg);
+    }
+    TW_ST(1)
+    // dO_h^T = W_out[:, h]^T . dy^T
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      bf16x8 a[T::KS];
+#pragma unroll
+      for (int ks = 0; ks < T::KS; ++ks) a[ks] = ld_img(wot_g, h * 2 + dt, T::KS, ks, lane);
+#pragma unroll
+      for (int vt = 0; vt < NV; ++vt) {
+        f32x4 acc = z4;
+#pragma unroll
+        for (int ks = 0; ks < T::KS; ++ks)
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], ld16(dyt + (vt * 16 + lr) * TH_XLD + ks * 32 + lg * 8),
+                                                        acc, 0, 0, 0);
+        float o4[4] = {acc[0], acc[1], acc[2], acc[3]};
+        store4(sdo + (vt * 16 + lr) * HLD + dt * 16 + lg * 4, o4);
+      }
+    }
+    wave_lds_sync();
+    TW_ST(2)
+    // attention-core backward, TWH_PG pixels interleaved phase by phase; only the transposed orientation is
+    // computed (S^T, dP^T on MFMA, softmax rows per lane), P and dS reach the row-major orientation of the
+    // dK / dV products through a 16 x 16 bf16 LDS tile and the hardware transpose read
+    constexpr int PG = TWH_PG;
+    bf16* trt = reinterpret_cast<bf16*>(trbuf) + wid * PG * 2 * 256;  // [PG][P^T, dS^T][16][16]
+    for (int pp0 = 0; pp0 < T::PW; pp0 += PG) {
+      f32x4 st[PG], dpt[PG];
+#pragma unroll
+      for (int u = 0; u < PG; ++u) {
+        const int rb = (pp0 + u) * F;
+        const int rr = rb + (lr < F ? lr : 0);
+        const bf16x8 kr = sel8(lr < F, ld16(sk + rr * HLD + lg * 8));
+        const bf16x8 qr = sel8(lr < F, ld16(sq + rr * HLD + lg * 8));
+        const bf16x8 vr = sel8(lr < F, ld16(sv + rr * HLD + lg * 8));
+        const bf16x8 dor = sel8(lr < F, ld16(sdo + rr * HLD + lg * 8));
+        st[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kr, qr, z4, 0, 0, 0);    // S^T[j][i]
+        dpt[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vr, dor, z4, 0, 0, 0);  // dP^T[j][i]
+      }
+      bf16x8 dst_b[PG];
+#pragma unroll
+      for (int u = 0; u < PG; ++u) {
+        const bool pix = p0 + pp0 + u < HW;
+        float Li = Lp[0];
+#pragma unroll
+        for (int q = 1; q < T::PW; ++q) Li = pp0 + u == q ? Lp[q] : Li;
+        float pt[4], D = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool ok = pix && lg * 4 + r < F && lr < F;
+          pt[r] = ok ? __builtin_amdgcn_exp2f(fmaf(st[u][r], LOG2E, bt[r]) - Li) : 0.f;
+          D = fmaf(pt[r], dpt[u][r], D);
+        }
+        D = grp4_sum(D);
+        bf16x4 p4, d4;
+        dst_b[u] = zero8();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float ds = pt[r] * (dpt[u][r] - D);
+          dbacc[r] += ds;
+          dst_b[u][r] = (bf16)ds;
+          d4[r] = (bf16)ds;
+          p4[r] = (bf16)pt[r];
+        }
+        // tile[i = lr][j = 4g .. 4g+3]
+        *reinterpret_cast<bf16x4*>(trt + (u * 2 + 0) * 256 + lr * 16 + lg * 4) = p4;
+        *reinterpret_cast<bf16x4*>(trt + (u * 2 + 1) * 256 + lr * 16 + lg * 4) = d4;
+      }
+      f32x4 dqt[PG][2];
+#pragma unroll
+      for (int u = 0; u < PG; ++u)
+#pragma unroll
+        for (int half = 0; half < 2; ++half)
+          dqt[u][half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kslot_gather(sk, (pp0 + u) * F, half * 16, F, lane),
+                                                                 dst_b[u], z4, 0, 0, 0);  // dQ'^T[d][i]
+      wave_lds_sync();  // P / dS tiles visible
+      f32x4 dkt[PG][2], dvt[PG][2];
+#pragma unroll
+      for (int u = 0; u < PG; ++u) {
+        const bf16x8 p_b = kslot_gather_ld(trt + (u * 2 + 0) * 256, 16, 0, 0, F, lane);   // P[i = 4g+e][j = lr]
+        const bf16x8 ds_b = kslot_gather_ld(trt + (u * 2 + 1) * 256, 16, 0, 0, F, lane);  // dS[i = 4g+e][j = lr]
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const int rb = (pp0 + u) * F;
+          dkt[u][half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kslot_gather(sq, rb, half * 16, F, lane), ds_b, z4,
+                                                                 0, 0, 0);  // dK'^T[d][j]
+          dvt[u][half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kslot_gather(sdo, rb, half * 16, F, lane), p_b, z4,
+                                                                 0, 0, 0);  // dV^T[d][j]
+        }
+      }
+      wave_lds_sync();  // all reads of these pixels' rows (and the tiles) done before they are overwritten
+#pragma unroll
+      for (int u = 0; u < PG; ++u) {
+        const int rb = (pp0 + u) * F;
+        if (lr < F && p0 + pp0 + u < HW) {
+#pragma unroll
+          for (int half = 0; half < 2; ++half) {
+            const int d0 = half * 16 + lg * 4;
+            float q4[4] = {dqt[u][half][0], dqt[u][half][1], dqt[u][half][2], dqt[u][half][3]};
+            float k4[4] = {dkt[u][half][0], dkt[u][half][1], dkt[u][half][2], dkt[u][half][3]};
+            float v4[4] = {dvt[u][half][0], dvt[u][half][1], dvt[u][half][2], dvt[u][half][3]};
+            rope4(q4, rot, lr, d0, -1.f);
+            rope4(k4, rot, lr, d0, -1.f);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) q4[r] *= scale;
+            store4(sq + (rb + lr) * HLD + d0, q4);
+            store4(sk + (rb + lr) * HLD + d0, k4);
+            store4(sv + (rb + lr) * HLD + d0, v4);
+          }
+        }
+      }
+    }
+    wave_lds_sync();
+    TW_ST(3)
+    // this head's W'^T fragments for the dxn GEMM below, issued now so their latency hides behind the dW GEMM
+    bf16x8 wt[3][T::CT];
+    if constexpr (TWH_EARLY_WT != 0) {
+#pragma unroll
+      for (int kind = 0; kind < 3; ++kind)
+#pragma unroll
+        for (int ct = 0; ct < T::CT; ++ct) wt[kind][ct] = ld_img(wqt_g, ct, QKV / 32, kind * 8 + h, lane);
+    }
+    // dW'_h += dqkv_h^T . xhat over the group's voxels (K = voxels, 16 per step; padded rows are zero)
+#pragma unroll
+    for (int kk = 0; kk < NV; ++kk) {
+      s16x4 bx[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) bx[nt] = tr4(xt, TH_XLD, kk * 16, nt * 16, lane);
+#pragma unroll
+      for (int m = 0; m < 6; ++m) {
+        const bf16* src = (m >> 1) == 0 ? sq : ((m >> 1) == 1 ? sk : sv);
+        const s16x4 a = tr4(src, HLD, kk * 16, (m & 1) * 16, lane);
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          dwacc[m][nt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, bx[nt], dwacc[m][nt], 0, 0, 0);
+      }
+    }
+    TW_ST(4)
+    // dxn'_h^T = W'_qkv[h rows]^T . dqkv_h^T (this head's share; gamma folded: the sum over heads is
+    // g = gamma * dxn), kept in registers, then written as fp32 rows over the wave's own slices
+    f32x4 dxacc[T::CT][NV];
+#pragma unroll
+    for (int ct = 0; ct < T::CT; ++ct)
+#pragma unroll
+      for (int vt = 0; vt < NV; ++vt) dxacc[ct][vt] = z4;
+#pragma unroll
+    for (int kind = 0; kind < 3; ++kind) {
+      const bf16* src = kind == 0 ? sq : (kind == 1 ? sk : sv);
+#pragma unroll
+      for (int ct = 0; ct < T::CT; ++ct) {
+        const bf16x8 a = TWH_EARLY_WT != 0 ? wt[kind][ct] : ld_img(wqt_g, ct, QKV / 32, kind * 8 + h, lane);
+#pragma unroll
+        for (int vt = 0; vt < NV; ++vt)
+          dxacc[ct][vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ld16(src + (vt * 16 + lr) * HLD + lg * 8),
+                                                                  dxacc[ct][vt], 0, 0, 0);
+      }
+    }
+    wave_lds_sync();  // every read of this wave's slices done: they now take its partial dxn rows
+    {
+      float* part = reinterpret_cast<float*>(sq);
+#pragma unroll
+      for (int ct = 0; ct < T::CT; ++ct)
+#pragma unroll
+        for (int vt = 0; vt < NV; ++vt)
+          *reinterpret_cast<f32x4*>(part + (vt * 16 + lr) * TH_PLD + ct * 16 + lg * 4) = dxacc[ct][vt];
+    }
+    TW_ST(5)
+    __syncthreads();  // (B) every head's partial written
+
+    // ---- LN backward of this thread's voxel chunk: dx = rstd (g - mean(g) - xhat mean(g xhat)) + dy
+    {
+      const int v = vv < R ? vv : 0;
+      float g[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        const float* pw = reinterpret_cast<const float*>(slices + w * 4 * R * HLD) + v * TH_PLD + cc * 8;
+        const f32x4 a0 = *reinterpret_cast<const f32x4*>(pw);
+        const f32x4 a1 = *reinterpret_cast<const f32x4*>(pw + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { g[e] += a0[e]; g[4 + e] += a1[e]; }
+      }
+      const bf16x8 xh = *reinterpret_cast<const bf16x8*>(xt + v * TH_XLD + cc * 8);
+      const bf16x8 dv = *reinterpret_cast<const bf16x8*>(dyt + v * TH_XLD + cc * 8);
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { s1 += g[e]; s2 = fmaf(g[e], (float)xh[e], s2); }
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
+      s1 *= 1.f / C;
+      s2 *= 1.f / C;
+      if (vv < R && ok_cur) {
+        bf16x8 o8;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o8[e] = (bf16)(rstd_cur * (g[e] - s1 - (float)xh[e] * s2) + (float)dv[e]);
+        stnt16(dx + vrow(gg, vv) * C + cc * 8, o8);
+      }
+    }
+    TW_ST(6)
+  }
+  TW_ST_FLUSH(blockIdx.x * 8 + wid)
+  // ---- per-block outputs: dW'_h rows of the slab, dbias partials (cesm_relpos_bwd layout, B = 1)
+  float* slab = dw_slab + (int64_t)blockIdx.x * QKV * C;
+#pragma unroll
+  for (int m = 0; m < 6; ++m) {
+    const int j0 = (m >> 1) * INNER + h * DH + (m & 1) * 16 + lg * 4;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) slab[(int64_t)(j0 + r) * C + nt * 16 + lr] = dwacc[m][nt][r];
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int j = lg * 4 + r;
+    if (lr < F && j < F) dbias_part[((int64_t)h * gridDim.x + blockIdx.x) * FF + lr * F + j] = dbacc[r];
+  }
+}
+
+// fp32 weight -> A-fragment image (frag_image layout) of A = W diag(gamma) (trans = 0: A[m][k] = W[m][k] g[k],
+// W row-major [M][K]) or of A = (W diag(gamma))^T (trans = 1: A[m][k] = W[k][m] g[m], W [K][M])
+__global__ void frag_image_f32_kernel(const float* __restrict__ W, const float* __restrict__ gamma,
+                                      bf16* __restrict__ img, int M, int K, int trans) {
+  const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= (int64_t)M * K / 8) return;
+  const int lane = (int)(v & 63);
+  const int64_t tile = v >> 6;
+  const int KT = K / 32;
+  const int kt = (int)(tile % KT), mt = (int)(tile / KT);
+  const int m = mt * 16 + (lane & 15), k0 = kt * 32 + (lane >> 4) * 8;
+  bf16x8 o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = k0 + e;
+    const float w = trans ? W[(int64_t)k * M + m] : W[(int64_t)m * K + k];
+    const float gm = gamma ? gamma[trans ? m : k] : 1.f;
+    o[e] = (bf16)(w * gm);
+  }
+  *reinterpret_cast<bf16x8*>(img + v * 8) = o;
+}
+
+// slab [nblk][J][C] (dW' partials) -> dW (+)= (sum_blk slab) diag(gamma); tmp[j][c] = W[j][c] * sum_blk slab
+__global__ void twh_dw_reduce_kernel(const float* __restrict__ slab, int nblk, const float* __restrict__ w,
+                                     const float* __restrict__ gamma, float* __restrict__ dw, float* __restrict__ tmp,
+                                     int J, int C, int accumulate) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)J * C) return;
+  float s = 0.f;
+  for (int k = 0; k < nblk; ++k) s += slab[(int64_t)k * J * C + e];
+  const int c = (int)(e % C);
+  if (dw) dw[e] = (accumulate ? dw[e] : 0.f) + s * gamma[c];
+  tmp[e] = s * w[e];
+}
+// dgamma[c] (+)= sum_j tmp[j][c]
+__global__ void twh_dgamma_kernel(const float* __restrict__ tmp, float* __restrict__ dgamma, int J, int C,
+                                  int accumulate) {
+  const int c = blockIdx.x;
+  float s = 0.f;
+  for (int j = threadIdx.x; j < J; j += 256) s += tmp[(int64_t)j * C + c];
+  s = wave_sum(s);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float t = red[0] + red[1] + red[2] + red[3];
+    dgamma[c] = accumulate ? dgamma[c] + t : t;
+  }
+}
 
 extern "C" {
 
@@ -1583,6 +2054,70 @@ int cesm_tblock_bwd(const void* x, const void* dy, const float* gamma, const flo
       return CESM_EUNSUPPORTED;
   }
   if (dgamma) tb_sum_rows_kernel<<<C, 64, 0, stream>>>(dgamma_part, dgamma, B * nblk, C, accumulate);
+  return cesm_launch_status();
+}
+
+// blocks of cesm_tblock_bwd_dw (one per CU, grid-stride over pixel groups); 0 = shape not supported
+int cesm_tblock_bwd_dw_nblk(int B, int F, int HW, int C) {
+  if (C != 64 || F < 1 || 4 * F > 16 * TH_NVMAX || B < 1 || HW < 1) return 0;
+  const int ngroups = B * (int)cdiv(HW, 4);
+  return std::min(ngroups, cesm_num_cus());
+}
+
+// Forward with gamma folded into the QKV weights (the forward of cesm_tblock_bwd_dw, C = 64): as
+// cesm_tblock_fwd, but wqkv_f32 is the fp32 master weight [768][C]; the LN output fed to the GEMMs is xhat.
+int cesm_tblock_fwd_fold(const void* x, const float* gamma, const float* wqkv_f32, const void* wout,
+                         const float* bias, const float* rot, void* y, float* mr, float* lse, void* o, void* wimg,
+                         int B, int F, int HW, int C, float scale, float eps, hipStream_t stream) {
+  if (C != 64 || F < 1 || F > 16) return CESM_EUNSUPPORTED;
+  bf16* iq = (bf16*)wimg;
+  bf16* io = iq + 768 * C;
+  frag_image_f32_kernel<<<(unsigned)cdiv((int64_t)768 * C / 8, 256), 256, 0, stream>>>(wqkv_f32, gamma, iq, 768, C, 0);
+  frag_image(wout, io, C, INNER, stream);
+  const int nv = (TW<64>::PW * F + 15) / 16;
+  switch (nv) {
+    case 1: tw_fwd_launch_nv<64, 1, true>(x, gamma, iq, io, bias, rot, y, mr, lse, o, B, F, HW, scale, eps, stream); break;
+    case 2: tw_fwd_launch_nv<64, 2, true>(x, gamma, iq, io, bias, rot, y, mr, lse, o, B, F, HW, scale, eps, stream); break;
+    case 3: tw_fwd_launch_nv<64, 3, true>(x, gamma, iq, io, bias, rot, y, mr, lse, o, B, F, HW, scale, eps, stream); break;
+    case 4: tw_fwd_launch_nv<64, 4, true>(x, gamma, iq, io, bias, rot, y, mr, lse, o, B, F, HW, scale, eps, stream); break;
+    default: return CESM_EUNSUPPORTED;
+  }
+  return cesm_launch_status();
+}
+
+// Head-parallel fused backward of the temporal-attention block with in-kernel weight gradients (C = 64,
+// 4F <= 48; the forward must be cesm_tblock_fwd_fold's).  dx [B*F*HW][C]; dwqkv (+)= dW_qkv [768][C] and
+// dgamma (+)= the LN gamma gradient (each nullable); dbias_part [8][nblk][F][F] (cesm_relpos_bwd with
+// B = 1).  Workspaces: slab nblk*768*C floats, tmp 768*C floats, wimg (2*768 + 256)*C bf16.
+int cesm_tblock_bwd_dw(const void* x, const void* dy, const float* mr, const float* lse, const float* wqkv_f32,
+                       const float* gamma, const void* wout_t, const float* bias, const float* rot, void* dx,
+                       float* dwqkv, float* dgamma, float* dbias_part, float* slab, float* tmp, void* wimg, int nblk,
+                       int B, int F, int HW, int C, float scale, int accumulate, hipStream_t stream) {
+  if (nblk < 1 || nblk != cesm_tblock_bwd_dw_nblk(B, F, HW, C)) return CESM_EUNSUPPORTED;
+  bf16* iq = (bf16*)wimg;
+  bf16* iqt = iq + 768 * C;
+  bf16* iot = iqt + 768 * C;
+  const unsigned gi = (unsigned)cdiv((int64_t)768 * C / 8, 256);
+  frag_image_f32_kernel<<<gi, 256, 0, stream>>>(wqkv_f32, gamma, iq, 768, C, 0);   // W diag(gamma)
+  frag_image_f32_kernel<<<gi, 256, 0, stream>>>(wqkv_f32, gamma, iqt, C, 768, 1);  // (W diag(gamma))^T
+  frag_image(wout_t, iot, INNER, C, stream);
+  const int nv = (4 * F + 15) / 16;
+  const size_t sm = twh_smem(F, nv);
+#define TWH_LAUNCH(NVv)                                                                                      \
+  allow_smem(twh_bwd_kernel<NVv>, sm);                                                                       \
+  twh_bwd_kernel<NVv><<<nblk, 512, sm, stream>>>((const bf16*)x, (const bf16*)dy, mr, lse, iq, iqt, iot, bias, \
+                                                 rot, (bf16*)dx, slab, dbias_part, B, F, HW, scale)
+  switch (nv) {
+    case 1: TWH_LAUNCH(1); break;
+    case 2: TWH_LAUNCH(2); break;
+    case 3: TWH_LAUNCH(3); break;
+    default: return CESM_EUNSUPPORTED;
+  }
+#undef TWH_LAUNCH
+  const int64_t nel = (int64_t)768 * C;
+  twh_dw_reduce_kernel<<<(unsigned)cdiv(nel, 256), 256, 0, stream>>>(slab, nblk, wqkv_f32, gamma, dwqkv, tmp, 768, C,
+                                                                    accumulate);
+  if (dgamma) twh_dgamma_kernel<<<C, 256, 0, stream>>>(tmp, dgamma, 768, C, accumulate);
   return cesm_launch_status();
 }
 

@@ -355,6 +355,62 @@ def tblock_bwd(x, dy, gamma, mr, lse, wqkv, wqkv_t, wout_t, bias, rot, dgamma, d
     return dx, dqkv, o, xn
 
 
+def tblock_bwd_dw_supported(B, F, HW, C):
+    """shapes the head-parallel fused backward with in-kernel weight gradients handles (C = 64, 4F <= 48)"""
+    return lib().cesm_tblock_bwd_dw_nblk(B, F, HW, C) > 0
+
+
+def tblock_fwd_fold(x, gamma, wqkv_f32, wout, bias, rot, B, F, scale, save=True, eps=1e-5, save_o=False):
+    """tblock_fwd with the LN gamma folded into the QKV weights (the forward of tblock_bwd_dw); wqkv_f32 is
+    the fp32 master to_qkv weight [768, C].  Returns (y, mr, lse, o) as tblock_fwd."""
+    Nb, H, W, C = x.shape
+    _chk(x, dtype=torch.bfloat16)
+    _chk(wqkv_f32, (768, C), torch.float32)
+    _chk(wout, (C, 256), torch.bfloat16)
+    _chk(gamma, (C,), torch.float32)
+    y = empty(x.shape, x.dtype, x.device)
+    mr = empty((Nb * H * W, 2), torch.float32, x.device) if save else None
+    lse = empty((B, 8, H * W, F), torch.float32, x.device) if save else None
+    o = empty((Nb, H, W, 256), x.dtype, x.device) if save_o else None
+    wimg = empty(((768 + 256) * C,), torch.bfloat16, x.device)
+    call("cesm_tblock_fwd_fold", P(x), P(gamma), P(wqkv_f32), P(wout), P(bias), P(rot), P(y), P(mr), P(lse), P(o),
+         P(wimg), B, F, H * W, C, float(scale), float(eps), S())
+    return y, mr, lse, o
+
+
+def tblock_bwd_dw(x, dy, mr, lse, wqkv_f32, gamma, wout_t, bias, rot, dwqkv, dgamma, dtable, B, F, scale,
+                  num_buckets=32, max_distance=32):
+    """head-parallel fused temporal-block backward with in-kernel weight gradients (C = 64, 4F <= 48):
+    returns dx; dwqkv (+)= the to_qkv weight gradient, dgamma (+)= the LN gamma gradient, dtable (+)= the
+    rel-pos table gradient (each nullable).  The forward must be tblock_fwd_fold's."""
+    Nb, H, W, C = x.shape
+    HW = H * W
+    _chk(x, dtype=torch.bfloat16)
+    _chk(dy, x.shape, torch.bfloat16)
+    _chk(wqkv_f32, (768, C), torch.float32)
+    _chk(gamma, (C,), torch.float32)
+    _chk(wout_t, (256, C), torch.bfloat16)
+    _chk(dwqkv, (768, C), torch.float32)
+    _chk(dgamma, (C,), torch.float32)
+    if Nb != B * F or mr.shape != (Nb * HW, 2) or lse.shape != (B, 8, HW, F):
+        raise ValueError("tblock_bwd_dw: saved statistics do not match x")
+    nblk = lib().cesm_tblock_bwd_dw_nblk(B, F, HW, C)
+    if nblk <= 0:
+        raise ValueError(f"tblock_bwd_dw: unsupported shape C={C} F={F}")
+    dev = x.device
+    dx = empty(x.shape, x.dtype, dev)
+    dbp = empty((8, nblk, F, F), torch.float32, dev)
+    slab = empty((nblk, 768, C), torch.float32, dev)
+    tmp = empty((768, C), torch.float32, dev)
+    wimg = empty(((2 * 768 + 256) * C,), torch.bfloat16, dev)
+    call("cesm_tblock_bwd_dw", P(x), P(dy), P(mr), P(lse), P(wqkv_f32), P(gamma), P(wout_t), P(bias), P(rot), P(dx),
+         P(dwqkv), P(dgamma), P(dbp), P(slab), P(tmp), P(wimg), nblk, B, F, HW, C, float(scale), 1, S())
+    if dtable is not None:
+        ws = empty((8, F, F), torch.float32, dev)
+        call("cesm_relpos_bwd", P(dbp), nblk, 1, P(dtable), P(ws), F, 8, num_buckets, max_distance, 1, S())
+    return dx
+
+
 # fused SLA at C = 64 and 128 (measured +0.8 % step throughput for C = 128 with the parallel context
 # combine); CESM_SLAF_C64_ONLY=1 restores the unfused path at C = 128
 SLAF_C = (64,) if os.environ.get("CESM_SLAF_C64_ONLY") else (64, 128)

@@ -109,6 +109,12 @@ def gbuf(p):
     return p.grad
 
 
+def _gflat(p):
+    """flat view of p's gradient buffer (LayerNorm gamma [1, C, 1, 1, 1] -> [C]) or None"""
+    g = gbuf(p)
+    return None if g is None else g.view(-1)
+
+
 # ============================================================================ conv helpers
 class ConvSpec:
     """Geometry of one conv-like layer in GEMM terms (see csrc/conv.hip)."""
@@ -360,6 +366,15 @@ def _tblock_fused(rc, C):
             and C <= FUSED_TBLOCK_MAXC)
 
 
+# head-parallel backward with in-kernel weight gradients (C = 64, F <= 12): no 768-channel dqkv round trip
+TBLOCK_DW = os.environ.get("CESM_NO_TBLOCK_DW", "0") != "1"
+
+
+def _tblock_dw(rc, x):
+    Nb, H, W, C = x.shape
+    return TBLOCK_DW and _tblock_fused(rc, C) and K.tblock_bwd_dw_supported(rc.B, rc.F, H * W, C)
+
+
 def tattn_fwd(rc, res_mod, x):
     """Residual(PreNorm(EinopsToAndFrom(Attention))) over frames (video_net.py:368-454).
     bf16: one fused kernel (csrc/tblock.hip); fp32 parity mode: LN -> to_qkv -> core -> to_out."""
@@ -376,6 +391,14 @@ def tattn_fwd(rc, res_mod, x):
         v = K.conv_fwd(n, None, wv, None, (H, W, 256, 1, 1, 1, 0, 1))
         wo = rc.packed(attn.to_out.weight, C, 256, 1, 1, 0, 0)
         return K.conv_fwd(v, None, wo, None, (H, W, C, 1, 1, 1, 0, 1), res=x), None
+    if _tblock_dw(rc, x):
+        # gamma folded into the QKV weights (images built from the fp32 master weight); the backward computes
+        # the to_qkv and gamma gradients in-kernel.  O is always saved for the to_out weight gradient.
+        wo = rc.packed(attn.to_out.weight, C, 256, 1, 1, 0, 0)
+        y, mr, lse, o = K.tblock_fwd_fold(x, _flat(pre.norm.gamma), attn.to_qkv.weight, wo, rc.bias, rc.rot, rc.B,
+                                          rc.F, attn.scale, save=rc.save, eps=pre.norm.eps, save_o=rc.save)
+        st = SimpleNamespace(fused=True, fold=True, x=x, mr=mr, lse=lse, o=o) if rc.save else None
+        return y, st
     if _tblock_fused(rc, C):
         wq = rc.packed(attn.to_qkv.weight, 768, C, 1, 1, 0, 0)
         wo = rc.packed(attn.to_out.weight, C, 256, 1, 1, 0, 0)
@@ -383,7 +406,7 @@ def tattn_fwd(rc, res_mod, x):
         save_o = rc.save and C <= 256 and TW_FWD_O
         y, mr, lse, o = K.tblock_fwd(x, _flat(pre.norm.gamma), wq, wo, rc.bias, rc.rot, rc.B, rc.F, attn.scale,
                                      save=rc.save, eps=pre.norm.eps, save_o=save_o)
-        st = SimpleNamespace(fused=True, x=x, mr=mr, lse=lse, o=o) if rc.save else None
+        st = SimpleNamespace(fused=True, fold=False, x=x, mr=mr, lse=lse, o=o) if rc.save else None
         return y, st
     n, mr = K.ln_fwd(x, _flat(pre.norm.gamma), save=rc.save, eps=pre.norm.eps)
     qspec, ospec = ConvSpec(attn.to_qkv), ConvSpec(attn.to_out)
@@ -398,6 +421,15 @@ def tattn_bwd(rc, res_mod, st, dy):
     pre = res_mod.fn
     attn = pre.fn.fn
     Nb, H, W, C = st.x.shape
+    if st.fused and st.fold:
+        wo_t = rc.packed(attn.to_out.weight, 256, C, 1, 1, 1, 1)
+        dwo = gbuf(attn.to_out.weight)
+        dx = K.tblock_bwd_dw(st.x, dy, st.mr, st.lse, attn.to_qkv.weight, _flat(pre.norm.gamma), wo_t, rc.bias, rc.rot,
+                             gbuf(attn.to_qkv.weight), _gflat(pre.norm.gamma), rc.dtable, rc.B, rc.F, attn.scale)
+        if dwo is not None:
+            with rc.side(st.o, dy, attn=True):
+                K.conv_wgrad(st.o, None, dy, None, dwo, (H, W, C, 1, 1, 1, 0, 1), 0, 0)
+        return dx
     if st.fused:
         wq = rc.packed(attn.to_qkv.weight, 768, C, 1, 1, 0, 0)
         wq_t = rc.packed(attn.to_qkv.weight, C, 768, 1, 1, 1, 1)

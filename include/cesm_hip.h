@@ -126,6 +126,22 @@ int cesm_tblock_bwd(const void* x, const void* dy, const float* gamma, const flo
                     const void* wqkv, const void* wqkv_t, const void* wout_t, const float* bias, const float* rot,
                     void* dx, void* dqkv, void* o, void* xn, float* dbias_part, float* dgamma, float* dgamma_part, void* wimg,
                     int nblk, int B, int F, int HW, int C, float scale, int accumulate, hipStream_t stream);
+/* Fused temporal-attention block with in-kernel weight gradients (C = 64, 4F <= 48; csrc/tblock.hip):
+ * cesm_tblock_fwd_fold is cesm_tblock_fwd with LN gamma folded into the QKV weights (wqkv_f32: the fp32
+ * master weight [768][C]; wimg (768 + 256) * C bf16); cesm_tblock_bwd_dw is its backward: dx, and
+ * dwqkv (+)= dW_qkv, dgamma (+)= the LN gamma gradient (nullable) without the 768-channel dqkv / xn
+ * intermediates; dbias_part [8][nblk][F][F] (cesm_relpos_bwd, B = 1); slab nblk*768*C and tmp 768*C
+ * floats, wimg (2*768 + 256) * C bf16; nblk from cesm_tblock_bwd_dw_nblk (0 = unsupported shape).
+ * Replaces video_net.py:368-454 (Attention) + :90-98 (PreNorm LN) + :69-75 (Residual) and the
+ * to_qkv weight gradient of its backward. */
+int cesm_tblock_bwd_dw_nblk(int B, int F, int HW, int C);
+int cesm_tblock_fwd_fold(const void* x, const float* gamma, const float* wqkv_f32, const void* wout,
+                         const float* bias, const float* rot, void* y, float* mr, float* lse, void* o, void* wimg,
+                         int B, int F, int HW, int C, float scale, float eps, hipStream_t stream);
+int cesm_tblock_bwd_dw(const void* x, const void* dy, const float* mr, const float* lse, const float* wqkv_f32,
+                       const float* gamma, const void* wout_t, const float* bias, const float* rot, void* dx,
+                       float* dwqkv, float* dgamma, float* dbias_part, float* slab, float* tmp, void* wimg, int nblk,
+                       int B, int F, int HW, int C, float scale, int accumulate, hipStream_t stream);
 /* spatial linear attention core (video_net.py:335-345 between to_qkv and to_out) */
 int cesm_sla_nchunk(int HW);
 int cesm_sla_fwd(int dtype, const void* qkv, void* out, float* ctx, float* ml, float* ws, int Nf, int HW, float scale,

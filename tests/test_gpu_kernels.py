@@ -667,3 +667,61 @@ def test_fused_sla_backward(dev, H, W, C, save_o):
     print(f"fused sla bwd HxW={H}x{W}: " + " ".join(f"{k} {v:.2e}" for k, v in errs.items()))
     for k, v in errs.items():
         assert v < 3e-2, (k, v)
+
+
+@pytest.mark.parametrize("Fr", [1, 5, 12])
+@pytest.mark.parametrize("B,H,W", [(2, 5, 7), (1, 12, 16), (3, 9, 13)])
+def test_tblock_fold_forward_and_dw_backward(dev, Fr, B, H, W):
+    """cesm_tblock_fwd_fold + cesm_tblock_bwd_dw (head-parallel backward with in-kernel dW_qkv / dgamma, no
+    dqkv / xn intermediates; the level-0 training path at C = 64) vs float64 autograd through the
+    reference block (video_net.py:368-454 under Residual(PreNorm)); pixel counts that leave partial
+    4-pixel groups, groups spanning samples"""
+    C = 64
+    torch.manual_seed(21)
+    rot_mod = VN.RotaryEmbedding(32)
+    res_mod = VN.Residual(VN.PreNorm(C, VN.EinopsToAndFrom(VN.Attention(C, 8, 32, rot_mod)))).to(dev)
+    with torch.no_grad():
+        res_mod.fn.norm.gamma.uniform_(0.5, 1.5)
+    attn = res_mod.fn.fn.fn
+    assert K.tblock_bwd_dw_supported(B, Fr, H * W, C)
+    x = q(torch.randn(B, C, Fr, H, W), torch.bfloat16)
+    g = q(torch.randn(B, C, Fr, H, W), torch.bfloat16)
+    table = torch.randn(32, 8)
+    rc = make_rc(B, Fr, torch.bfloat16)
+    rc.bias = K.relpos_fwd(table.to(dev), Fr)
+    rc.rot = K.rope_table(rot_mod.freqs.to(dev), Fr)
+    xd = to_cl(x).to(dev, torch.bfloat16)
+    gd = to_cl(g).to(dev, torch.bfloat16)
+    wqkv = attn.to_qkv.weight.detach().contiguous()
+    wout = attn.to_out.weight.detach()
+    wo = K.conv_pack(wout, torch.bfloat16, C, 256, 1, 1, 0, 0)
+    wo_t = K.conv_pack(wout, torch.bfloat16, 256, C, 1, 1, 1, 1)
+    gamma = res_mod.fn.norm.gamma.detach().reshape(-1).contiguous()
+    y, mr, lse, o = K.tblock_fwd_fold(xd, gamma, wqkv, wo, rc.bias, rc.rot, B, Fr, attn.scale, save_o=True)
+    dgamma = torch.full((C,), 0.25, device=dev)   # accumulates (+=)
+    dtable = torch.zeros(32, 8, device=dev)
+    dwq = torch.full((768, C), 0.5, device=dev)   # accumulates (+=)
+    dx = K.tblock_bwd_dw(xd, gd, mr, lse, wqkv, gamma, wo_t, rc.bias, rc.rot, dwq, dgamma, dtable, B, Fr, attn.scale)
+    torch.cuda.synchronize()
+    dwo = gd.reshape(-1, C).double().t() @ o.reshape(-1, 256).double()
+    from oracle import ref_cpu as R
+    ref = R.Residual(R.PreNorm(C, R.EinopsToAndFrom(R.Attention(C, 8, 32, R.RotaryEmbedding(32))))).double()
+    ref.fn.norm.gamma.data.copy_(gamma.cpu().double().view_as(ref.fn.norm.gamma))
+    ref.fn.fn.fn.to_qkv.weight.data.copy_(wqkv.cpu().double())
+    ref.fn.fn.fn.to_out.weight.data.copy_(wout.cpu().to(torch.bfloat16).double())
+    rp = R.RelativePositionBias(8, 32, 32).double()
+    rp.relative_attention_bias.weight.data.copy_(table.double())
+    xr = x.double().requires_grad_(True)
+    yr = ref(xr, pos_bias=rp(Fr))
+    (yr * g.double()).sum().backward()
+    errs = {
+        "y": rel(from_cl(y, B), yr.detach()),
+        "dx": rel(from_cl(dx, B), xr.grad),
+        "dgamma": rel(dgamma.double() - 0.25, ref.fn.norm.gamma.grad.reshape(-1)),
+        "dtable": rel(dtable.double(), rp.relative_attention_bias.weight.grad),
+        "dWqkv": rel(dwq.double() - 0.5, ref.fn.fn.fn.to_qkv.weight.grad),
+        "dWout": rel(dwo, ref.fn.fn.fn.to_out.weight.grad),
+    }
+    print(f"tblock fold/dw C=64 F={Fr} B={B} {H}x{W}: " + " ".join(f"{k} {v:.2e}" for k, v in errs.items()))
+    for k, v in errs.items():
+        assert v < 3e-2, (k, v)

@@ -24,7 +24,7 @@ def timed(fn, reps):
 def main():
     C = int(sys.argv[1]) if len(sys.argv) > 1 else 64
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
-    B, F = 4, 12
+    B, F = (int(sys.argv[3]) if len(sys.argv) > 3 else 8), 12
     H, W = {64: (192, 288), 128: (96, 144)}[C]
     dev = torch.device("cuda")
     torch.manual_seed(0)
@@ -51,9 +51,28 @@ def main():
 
     def bwd():
         K.tblock_bwd(x, dy, gamma, mr, lse, wq, wq_t, wo_t, bias, rot, dgamma, dtable, B, F, 32 ** -0.5,
-                     want_wgrad_inputs=True, emit_o=False)
+                     want_wgrad_inputs=os.environ.get("TW_NOEMIT", "0") == "0", emit_o=False)
 
     tb = timed(bwd, reps)
+    # the old path's to_qkv weight gradient from the emitted dqkv / xn (what the dw kernel replaces)
+    st["b"] = K.tblock_bwd(x, dy, gamma, mr, lse, wq, wq_t, wo_t, bias, rot, dgamma, dtable, B, F, 32 ** -0.5,
+                           want_wgrad_inputs=True, emit_o=False)
+    dwq = torch.zeros(768, C, device=dev)
+
+    def qwgrad():
+        _, dqkv, _, xn = st["b"]
+        K.conv_wgrad(xn, None, dqkv, None, dwq, (H, W, 768, 1, 1, 1, 0, 1), 0, 0)
+
+    tqw = timed(qwgrad, reps)
+    tdw = float("nan")
+    if C == 64 and K.tblock_bwd_dw_supported(B, F, H * W, C):
+        wo_pack = K.conv_pack(wout, torch.bfloat16, C, 256, 1, 1, 0, 0)
+        yf, mrf, lsef, of = K.tblock_fwd_fold(x, gamma, wqkv, wo_pack, bias, rot, B, F, 32 ** -0.5, save_o=True)
+
+        def bwd_dw():
+            K.tblock_bwd_dw(x, dy, mrf, lsef, wqkv, gamma, wo_t, bias, rot, dwq, dgamma, dtable, B, F, 32 ** -0.5)
+
+        tdw = timed(bwd_dw, reps)
     bout = torch.randn(C, device=dev) * 0.1
 
     def sfwd():
@@ -63,11 +82,13 @@ def main():
     ys, sst = st["s"]
 
     def sbwd():
-        K.slaf_bwd(x, dy, gamma, wq, wq_t, wo_t, sst, dgamma, 32 ** -0.5, want_wgrad_inputs=True)
+        K.slaf_bwd(x, dy, gamma, wq, wq_t, wo_t, sst, dgamma, 32 ** -0.5,
+                   want_wgrad_inputs=os.environ.get("TW_NOEMIT", "0") == "0")
 
     sb = timed(sbwd, reps)
-    lib = os.environ.get("CESM_HIP_LIB", "default")
-    print(f"{lib}: C={C} tw_fwd {tf:.1f} us  tw_bwd {tb:.1f} us  sla_fwd {sf:.1f} us  sla_bwd {sb:.1f} us  "
+    lib = os.environ.get("CESM_HIP_LIB", "default") + (" noemit" if os.environ.get("TW_NOEMIT", "0") != "0" else "")
+    print(f"{lib}: C={C} tw_fwd {tf:.1f} us  tw_bwd {tb:.1f} us (+ qkv wgrad {tqw:.1f} us)  tw_bwd_dw {tdw:.1f} us  "
+          f"sla_fwd {sf:.1f} us  sla_bwd {sb:.1f} us  "
           f"y {float(y.float().abs().mean()):.6f} ys {float(ys.float().abs().mean()):.6f}")
 
 
