@@ -172,6 +172,71 @@ __device__ __forceinline__ bf16x8 ld_img(const bf16* img, int mt, int KT, int kt
 static inline void frag_image(const void* A, void* img, int M, int K, hipStream_t stream) {
   frag_image_kernel<<<(unsigned)cdiv((int64_t)M * K / 8, 256), 256, 0, stream>>>((const bf16*)A, (bf16*)img, M, K);
 }
+
+// lane (g, i) <- tile[r0 + 4g + e][c0 + i], e = 0..3 (hardware transpose read; EXEC all ones)
+__device__ __forceinline__ s16x4 tr4(const bf16* tile, int ld, int r0, int c0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tile + (r0 + 4 * g + q) * ld + c0 + 4 * p));
+}
+
+constexpr int TH_PLD = 68;  // fp32 row stride of a wave's partial dxn rows (written over its own slices)
+// an SGPR zero the compiler cannot see through: added to the weight-image pointers inside the group loop so
+// the (loop-invariant, per-head) fragment loads are not hoisted out of it and kept live across the loop
+__device__ __forceinline__ int opaque_zero() {
+  int z;
+  asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+  return z;
+}
+
+// fp32 weight -> A-fragment image (frag_image layout) of A = W diag(gamma) (trans = 0: A[m][k] = W[m][k] g[k],
+// W row-major [M][K]) or of A = (W diag(gamma))^T (trans = 1: A[m][k] = W[k][m] g[m], W [K][M])
+__global__ void frag_image_f32_kernel(const float* __restrict__ W, const float* __restrict__ gamma,
+                                      bf16* __restrict__ img, int M, int K, int trans) {
+  const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= (int64_t)M * K / 8) return;
+  const int lane = (int)(v & 63);
+  const int64_t tile = v >> 6;
+  const int KT = K / 32;
+  const int kt = (int)(tile % KT), mt = (int)(tile / KT);
+  const int m = mt * 16 + (lane & 15), k0 = kt * 32 + (lane >> 4) * 8;
+  bf16x8 o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = k0 + e;
+    const float w = trans ? W[(int64_t)k * M + m] : W[(int64_t)m * K + k];
+    const float gm = gamma ? gamma[trans ? m : k] : 1.f;
+    o[e] = (bf16)(w * gm);
+  }
+  *reinterpret_cast<bf16x8*>(img + v * 8) = o;
+}
+
+// slab [nblk][J][C] (dW' partials) -> dW (+)= (sum_blk slab) diag(gamma); tmp[j][c] = W[j][c] * sum_blk slab
+__global__ void twh_dw_reduce_kernel(const float* __restrict__ slab, int nblk, const float* __restrict__ w,
+                                     const float* __restrict__ gamma, float* __restrict__ dw, float* __restrict__ tmp,
+                                     int J, int C, int accumulate) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)J * C) return;
+  float s = 0.f;
+  for (int k = 0; k < nblk; ++k) s += slab[(int64_t)k * J * C + e];
+  const int c = (int)(e % C);
+  if (dw) dw[e] = (accumulate ? dw[e] : 0.f) + s * gamma[c];
+  tmp[e] = s * w[e];
+}
+// dgamma[c] (+)= sum_j tmp[j][c]
+__global__ void twh_dgamma_kernel(const float* __restrict__ tmp, float* __restrict__ dgamma, int J, int C,
+                                  int accumulate) {
+  const int c = blockIdx.x;
+  float s = 0.f;
+  for (int j = threadIdx.x; j < J; j += 256) s += tmp[(int64_t)j * C + c];
+  s = wave_sum(s);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float t = red[0] + red[1] + red[2] + red[3];
+    dgamma[c] = accumulate ? dgamma[c] + t : t;
+  }
+}
 }  // namespace
 
 // host-side switch for A/B runs of kernel variants (read once per process)

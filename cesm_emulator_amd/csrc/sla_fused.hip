@@ -933,6 +933,323 @@ __global__ __launch_bounds__(256) void slaf_sum_rows_kernel(const float* __restr
   }
 }
 
+__device__ __forceinline__ void wave_lds_sync_s() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ===================================================================================================
+// Head-parallel SLA backward with in-kernel weight gradients (C = 64; the forward ran with LN gamma
+// folded into the QKV weights, W' = W diag(gamma), and unit LN gamma).  A block of 8 waves (wave = head)
+// takes 48 pixels of one frame at a time: LN (xhat and dy tiles in LDS, block-cooperative) -> per wave:
+// raw q|k|v|do of its head (GEMMs) -> per-pixel softmax backward (as slab_dx) -> dq|dk|dv in its LDS slice
+// -> dW'_h += dqkv_h^T xhat (register accumulators for the whole kernel) and dxn'_h (this head's share) ->
+// the 8 shares summed through LDS -> LN backward -> dx.  No per-voxel intermediate reaches HBM (slab_dx
+// emitted the 768-channel dqkv and xn for a separate weight-gradient GEMM).
+// ===================================================================================================
+constexpr int SH_XLD = 72;   // xhat / dy tile row stride (bf16)
+constexpr int SH_SLD = 136;  // slice row stride (bf16): raw q|k|v|do (128 cols), then dq|dk|dv; fp32 partials over it
+constexpr int SH_PLD = 68;   // fp32 partial dxn row stride
+
+static size_t slah_smem(int NV) {
+  const int R = 16 * NV;
+  return (size_t)2 * R * SH_XLD * 2 + (size_t)8 * R * SH_SLD * 2;
+}
+
+template <int NV>
+__global__ __launch_bounds__(512, 1) void slah_dx_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ dy, const bf16* __restrict__ wqkv,
+    const bf16* __restrict__ wqkv_t, const bf16* __restrict__ wout_t, const float* __restrict__ kimg,
+    const bf16* __restrict__ actT, const bf16* __restrict__ actx, const bf16* __restrict__ adc,
+    const bf16* __restrict__ adcT, bf16* __restrict__ dx, float* __restrict__ dw_slab, int Nf, int HW, float scale,
+    float eps) {
+  constexpr int C = 64, KS = C / 32, CT = C / 16, R = 16 * NV;
+  static_assert(SH_PLD * 4 <= SH_SLD * 2, "partial dxn rows fit over the slice rows");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  bf16* xt = reinterpret_cast<bf16*>(smem);  // [R][SH_XLD] xhat
+  bf16* dyt = xt + R * SH_XLD;                // [R][SH_XLD] dy
+  bf16* slices = dyt + R * SH_XLD;            // 8 x [R][SH_SLD]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int h = wid;
+  bf16* sl = slices + wid * R * SH_SLD;
+  const int npg = (HW + R - 1) / R;
+  const int ngroups = Nf * npg;
+  const int vv = tid >> 3, cc = tid & 7;  // LN role: pixel vv of the group, channels 8cc..8cc+7
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+
+  auto prow = [&](int gg) -> int64_t {  // row of this thread's pixel in group gg, or -1
+    if (gg >= ngroups || vv >= R) return -1;
+    const int n = gg / npg, p = (gg - n * npg) * R + vv;
+    return p < HW ? (int64_t)n * HW + p : -1;
+  };
+  bf16x8 xpf = zero8(), dpf = zero8();
+  bool okpf = false;
+  auto prefetch = [&](int gg) {
+    const int64_t row = prow(gg);
+    okpf = row >= 0;
+    const int64_t rr = okpf ? row : 0;
+    xpf = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(x + rr * C + cc * 8));
+    dpf = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(dy + rr * C + cc * 8));
+  };
+
+  f32x4 dwacc[6][4];
+#pragma unroll
+  for (int m = 0; m < 6; ++m)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) dwacc[m][nt] = z4;
+
+  prefetch(blockIdx.x);
+  for (int gg = blockIdx.x; gg < ngroups; gg += gridDim.x) {
+    const int n = gg / npg, p0 = (gg - n * npg) * R;
+    // ---- LN of this thread's pixel chunk (statistics over its 8 lanes)
+    const bool ok_cur = okpf;
+    float rstd_cur;
+    {
+      float a[8], s = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { a[e] = ok_cur ? (float)xpf[e] : 0.f; s += a[e]; }
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) s += __shfl_xor(s, o, 64);
+      const float mean = s * (1.f / C);
+      float q = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { const float d = a[e] - mean; q = fmaf(d, d, q); }
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) q += __shfl_xor(q, o, 64);
+      const float rstd = 1.f / sqrtf(q * (1.f / C) + eps);
+      rstd_cur = ok_cur ? rstd : 0.f;
+      if (vv < R) {
+        bf16x8 xh, dv;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          xh[e] = (bf16)(ok_cur ? (a[e] - mean) * rstd : 0.f);
+          dv[e] = ok_cur ? dpf[e] : (bf16)0.f;
+        }
+        *reinterpret_cast<bf16x8*>(xt + vv * SH_XLD + cc * 8) = xh;
+        *reinterpret_cast<bf16x8*>(dyt + vv * SH_XLD + cc * 8) = dv;
+      }
+    }
+    const int oz = opaque_zero();
+    const bf16* wq_g = wqkv + oz;
+    const bf16* wqt_g = wqkv_t + oz;
+    const bf16* wot_g = wout_t + oz;
+    __syncthreads();  // (A)
+    prefetch(gg + gridDim.x);
+
+    // ---- phase A: raw q | k | v | do of head h, rows = pixels, cols kind*32 + d
+#pragma unroll
+    for (int kind = 0; kind < 4; ++kind) {
+      bf16x8 a[2][KS];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+          a[t][ks] = kind < 3 ? ld_img(wq_g, kind * 16 + h * 2 + t, KS, ks, lane) : ld_img(wot_g, h * 2 + t, KS, ks, lane);
+      const bf16* src = kind < 3 ? xt : dyt;
+#pragma unroll
+      for (int vt = 0; vt < NV; ++vt) {
+        bf16x8 b[KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) b[ks] = ld16(src + (vt * 16 + lr) * SH_XLD + ks * 32 + lg * 8);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          f32x4 acc = z4;
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[t][ks], b[ks], acc, 0, 0, 0);
+          float o4[4] = {acc[0], acc[1], acc[2], acc[3]};
+          store4(sl + (vt * 16 + lr) * SH_SLD + kind * 32 + t * 16 + lg * 4, o4);
+        }
+      }
+    }
+    wave_lds_sync_s();
+    // ---- phase B: per-pixel softmax backward (slab_dx's math); dq | dk | dv over cols 0..95
+    {
+      const int64_t fo = ((int64_t)(n * NH + h) * 2) * 64 * 8;
+      bf16x8 aT[2], ax[2], ad[2], adT[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        aT[t] = ld16(actT + fo + (t * 64 + lane) * 8);
+        ax[t] = ld16(actx + fo + (t * 64 + lane) * 8);
+        ad[t] = ld16(adc + fo + (t * 64 + lane) * 8);
+        adT[t] = ld16(adcT + fo + (t * 64 + lane) * 8);
+      }
+      float Kofs[2][4], Gd[2][4];
+      {
+        const f32x4* ki = reinterpret_cast<const f32x4*>(kimg + ((int64_t)(n * NH + h) * 64 + lane) * 16);
+        const f32x4 k0 = ki[0], k1 = ki[1], g0 = ki[2], g1 = ki[3];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { Kofs[0][r] = k0[r]; Kofs[1][r] = k1[r]; Gd[0][r] = g0[r]; Gd[1][r] = g1[r]; }
+      }
+#pragma unroll
+      for (int vt = 0; vt < NV; ++vt) {
+        const bool ok = p0 + vt * 16 + lr < HW;
+        bf16* row = sl + (vt * 16 + lr) * SH_SLD;
+        float qv[2][4], kv[2][4], vv4[2][4], dov[2][4];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          load4(row + 0 * 32 + t * 16 + lg * 4, qv[t]);
+          load4(row + 1 * 32 + t * 16 + lg * 4, kv[t]);
+          load4(row + 2 * 32 + t * 16 + lg * 4, vv4[t]);
+          load4(row + 3 * 32 + t * 16 + lg * 4, dov[t]);
+        }
+        float mx = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mx = fmaxf(mx, qv[t][r]);
+        mx = grp4_max(mx);
+        float ssum = 0.f;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            qv[t][r] = __builtin_amdgcn_exp2f((qv[t][r] - mx) * LOG2E);
+            ssum += qv[t][r];
+          }
+        const float inv = __builtin_amdgcn_rcpf(grp4_sum(ssum));
+        float qs[2][4], kt[2][4];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            qv[t][r] *= inv;
+            qs[t][r] = qv[t][r] * scale;
+            kt[t][r] = __builtin_amdgcn_exp2f(fmaf(kv[t][r], LOG2E, -Kofs[t][r]));
+          }
+        const bf16x8 qb = pack_kslot(qs[0], qs[1]);
+        const bf16x8 kb = pack_kslot(kt[0], kt[1]);
+        const bf16x8 vb = pack_kslot(vv4[0], vv4[1]);
+        const bf16x8 dob = pack_kslot(dov[0], dov[1]);
+        float dq[2][4], dk[2][4], dvv[2][4];
+        float sdq = 0.f;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const f32x4 dqt = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[t], dob, z4, 0, 0, 0);
+          const f32x4 dkt = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ad[t], vb, z4, 0, 0, 0);
+          const f32x4 dvt = __builtin_amdgcn_mfma_f32_16x16x32_bf16(adT[t], kb, z4, 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            dq[t][r] = dqt[r];
+            sdq = fmaf(qv[t][r], dqt[r], sdq);
+            dk[t][r] = kt[t][r] * (dkt[r] - Gd[t][r]);
+            dvv[t][r] = dvt[r];
+          }
+        }
+        (void)qb;
+        sdq = grp4_sum(sdq);
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            dq[t][r] = ok ? scale * qv[t][r] * (dq[t][r] - sdq) : 0.f;
+            dk[t][r] = ok ? dk[t][r] : 0.f;
+            dvv[t][r] = ok ? dvv[t][r] : 0.f;
+          }
+        // each lane overwrites exactly the q / k / v entries it read itself: no sync needed
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          store4(row + t * 16 + lg * 4, dq[t]);
+          store4(row + 32 + t * 16 + lg * 4, dk[t]);
+          store4(row + 64 + t * 16 + lg * 4, dvv[t]);
+        }
+      }
+    }
+    wave_lds_sync_s();
+    // ---- dW'_h += dqkv_h^T . xhat (K = pixels, 16 per step)
+#pragma unroll
+    for (int kk = 0; kk < NV; ++kk) {
+      s16x4 bx[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) bx[nt] = tr4(xt, SH_XLD, kk * 16, nt * 16, lane);
+#pragma unroll
+      for (int m = 0; m < 6; ++m) {
+        const s16x4 a = tr4(sl, SH_SLD, kk * 16, (m >> 1) * 32 + (m & 1) * 16, lane);
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          dwacc[m][nt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, bx[nt], dwacc[m][nt], 0, 0, 0);
+      }
+    }
+    // ---- dxn'_h (this head's share of g = gamma * dxn)
+    f32x4 dxacc[CT][NV];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+      for (int vt = 0; vt < NV; ++vt) dxacc[ct][vt] = z4;
+#pragma unroll
+    for (int kind = 0; kind < 3; ++kind)
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        const bf16x8 a = ld_img(wqt_g, ct, QKV / 32, kind * 8 + h, lane);
+#pragma unroll
+        for (int vt = 0; vt < NV; ++vt)
+          dxacc[ct][vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ld16(sl + (vt * 16 + lr) * SH_SLD + kind * 32 + lg * 8),
+                                                                  dxacc[ct][vt], 0, 0, 0);
+      }
+    wave_lds_sync_s();
+    {
+      float* part = reinterpret_cast<float*>(sl);
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+        for (int vt = 0; vt < NV; ++vt)
+          *reinterpret_cast<f32x4*>(part + (vt * 16 + lr) * SH_PLD + ct * 16 + lg * 4) = dxacc[ct][vt];
+    }
+    __syncthreads();  // (B)
+    // ---- LN backward of this thread's pixel chunk
+    {
+      const int v = vv < R ? vv : 0;
+      float g[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        const float* pw = reinterpret_cast<const float*>(slices + w * R * SH_SLD) + v * SH_PLD + cc * 8;
+        const f32x4 a0 = *reinterpret_cast<const f32x4*>(pw);
+        const f32x4 a1 = *reinterpret_cast<const f32x4*>(pw + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { g[e] += a0[e]; g[4 + e] += a1[e]; }
+      }
+      const bf16x8 xh = *reinterpret_cast<const bf16x8*>(xt + v * SH_XLD + cc * 8);
+      const bf16x8 dv = *reinterpret_cast<const bf16x8*>(dyt + v * SH_XLD + cc * 8);
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { s1 += g[e]; s2 = fmaf(g[e], (float)xh[e], s2); }
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
+      s1 *= 1.f / C;
+      s2 *= 1.f / C;
+      if (vv < R && ok_cur) {
+        bf16x8 o8;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o8[e] = (bf16)(rstd_cur * (g[e] - s1 - (float)xh[e] * s2) + (float)dv[e]);
+        __builtin_nontemporal_store(o8, reinterpret_cast<bf16x8*>(dx + ((int64_t)n * HW + p0 + vv) * C + cc * 8));
+      }
+    }
+  }
+  float* slab = dw_slab + (int64_t)blockIdx.x * QKV * C;
+#pragma unroll
+  for (int m = 0; m < 6; ++m) {
+    const int j0 = (m >> 1) * INNER + h * DH + (m & 1) * 16 + lg * 4;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) slab[(int64_t)(j0 + r) * C + nt * 16 + lr] = dwacc[m][nt][r];
+  }
+}
+
+__global__ void pack_scaled_kernel(const float* __restrict__ w, const float* __restrict__ cs, bf16* __restrict__ out,
+                                   int M, int K, int trans) {
+  const int64_t n = (int64_t)M * K;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    const int m = (int)(e / K), k = (int)(e - (int64_t)m * K);
+    const bf16 v = (bf16)(w[e] * (cs ? cs[k] : 1.f));
+    if (trans) out[(int64_t)k * M + m] = v;
+    else out[e] = v;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -1019,5 +1336,59 @@ int cesm_slaf_bwd(const void* x, const void* dy, const float* gamma, const void*
 
 // grid blocks of cesm_slaf_bwd's dx kernel (rows of its dgamma partial)
 int cesm_slaf_bwd_nblk(int Nf, int HW, int C) { return (int)cdiv(HW, C == 64 ? 128 : 64) * Nf; }
+
+// blocks of cesm_slaf_bwd_dw's head-parallel dx kernel (one per CU); 0 = shape not supported
+int cesm_slaf_bwd_dw_nblk(int Nf, int HW, int C) {
+  if (C != 64 || Nf < 1 || HW < 1) return 0;
+  const int ngroups = Nf * (int)cdiv(HW, 48);
+  return std::min(ngroups, cesm_num_cus());
+}
+
+// Fused SLA block backward with in-kernel weight gradients (C = 64).  The forward (cesm_slaf_fwd) must have
+// run with gamma_one (unit LN gamma) and wq_fold = bf16 W diag(gamma) [768][C] (cesm_pack_scaled); the same
+// two go to the dctx pass here.  dx; dwqkv (+)= dW_qkv and dgamma (+)= the LN gamma gradient (nullable).
+// Workspaces as cesm_slaf_bwd for part / G / adc / adcT; slab nblk_dx*768*C and tmp 768*C floats;
+// wimg (2*768 + 256)*C bf16.
+int cesm_slaf_bwd_dw(const void* x, const void* dy, const float* gamma_one, const void* wq_fold, const float* wqkv_f32,
+                     const float* gamma, const void* wout_t, const float* mz, const float* ctx32, const void* actT,
+                     const void* actx, void* dx, float* dwqkv, float* dgamma, float* part, float* G, void* adc,
+                     void* adcT, float* slab, float* tmp, void* wimg, int nblk_dx, int Nf, int HW, int C, float scale,
+                     float eps, int accumulate, hipStream_t stream) {
+  if (nblk_dx < 1 || nblk_dx != cesm_slaf_bwd_dw_nblk(Nf, HW, C)) return CESM_EUNSUPPORTED;
+  bf16* img_q = (bf16*)wimg;
+  bf16* img_qt = img_q + 768 * C;
+  bf16* img_ot = img_qt + 768 * C;
+  frag_image(wq_fold, img_q, 768, C, stream);
+  frag_image_f32_kernel<<<(unsigned)cdiv((int64_t)768 * C / 8, 256), 256, 0, stream>>>(wqkv_f32, gamma, img_qt, C,
+                                                                                          768, 1);
+  frag_image(wout_t, img_ot, 256, C, stream);
+  const int nsc = (HW + 63) / 64;
+  const int nblk = cesm_slaf_nblk(Nf, HW);
+  const int spb = (nsc + nblk - 1) / nblk;
+  slab_dctx_kernel<64><<<dim3(nblk, Nf), 512, 0, stream>>>((const bf16*)x, (const bf16*)dy, gamma_one,
+                                                           (const bf16*)wq_fold, (const bf16*)wout_t, part, HW, spb,
+                                                           scale, eps);
+  slab_combine_kernel<<<Nf * NH, 256, 0, stream>>>(part, nblk, ctx32, mz, G, (bf16*)adc, (bf16*)adcT);
+  const size_t sm = slah_smem(3);
+  hipFuncSetAttribute((const void*)slah_dx_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+  slah_dx_kernel<3><<<nblk_dx, 512, sm, stream>>>((const bf16*)x, (const bf16*)dy, img_q, img_qt, img_ot, G,
+                                                  (const bf16*)actT, (const bf16*)actx, (const bf16*)adc,
+                                                  (const bf16*)adcT, (bf16*)dx, slab, Nf, HW, scale, eps);
+  const int64_t nel = (int64_t)768 * C;
+  twh_dw_reduce_kernel<<<(unsigned)cdiv(nel, 256), 256, 0, stream>>>(slab, nblk_dx, wqkv_f32, gamma, dwqkv, tmp, 768,
+                                                                    C, accumulate);
+  if (dgamma) twh_dgamma_kernel<<<C, 256, 0, stream>>>(tmp, dgamma, 768, C, accumulate);
+  return cesm_launch_status();
+}
+
+// out[m][k] = bf16(w[m][k] * colscale[k]), w fp32 row-major [M][K] (trans = 0); trans = 1: out [K][M] = its
+// transpose (the swap-packed layout)
+int cesm_pack_scaled(const float* w, const float* colscale, void* out, int M, int K, int trans, hipStream_t stream) {
+  if (M < 1 || K < 1) return CESM_EINVAL;
+  const int64_t n = (int64_t)M * K;
+  pack_scaled_kernel<<<(unsigned)std::min<int64_t>(cdiv(n, 256), 4096), 256, 0, stream>>>(w, colscale, (bf16*)out, M,
+                                                                                          K, trans);
+  return cesm_launch_status();
+}
 
 }  // extern "C"

@@ -472,6 +472,55 @@ def slaf_bwd(x, dy, gamma, wqkv, wqkv_t, wout_t, state, dgamma, scale, want_wgra
     return dx, dqkv, o, xn
 
 
+def pack_scaled(w, colscale, trans=False):
+    """bf16 copy of w diag(colscale) (w fp32 [M, K]); trans: the transposed [K, M] layout"""
+    M, K = w.shape
+    _chk(w, dtype=torch.float32)
+    _chk(colscale, (K,), torch.float32)
+    out = empty((K, M) if trans else (M, K), torch.bfloat16, w.device)
+    call("cesm_pack_scaled", P(w), P(colscale), P(out), M, K, int(trans), S())
+    return out
+
+
+def slaf_bwd_dw_supported(Nf, HW, C):
+    return lib().cesm_slaf_bwd_dw_nblk(Nf, HW, C) > 0
+
+
+def slaf_bwd_dw(x, dy, gamma_one, wq_fold, wqkv_f32, gamma, wout_t, state, dwqkv, dgamma, scale, eps=1e-5):
+    """fused SLA block backward with in-kernel weight gradients (C = 64); the forward must have been
+    slaf_fwd(x, gamma_one, wq_fold, ...) with wq_fold = pack_scaled(wqkv_f32, gamma).  Returns dx; dwqkv /
+    dgamma (+)= the to_qkv / LN gamma gradients (nullable)."""
+    Nf, H, W, C = x.shape
+    HW = H * W
+    mz, ctx32, actT, actx, _o = state
+    _chk(x, dtype=torch.bfloat16)
+    _chk(dy, x.shape, torch.bfloat16)
+    _chk(wq_fold, (768, C), torch.bfloat16)
+    _chk(wqkv_f32, (768, C), torch.float32)
+    _chk(gamma, (C,), torch.float32)
+    _chk(gamma_one, (C,), torch.float32)
+    _chk(wout_t, (256, C), torch.bfloat16)
+    _chk(dwqkv, (768, C), torch.float32)
+    _chk(dgamma, (C,), torch.float32)
+    nblk_dx = lib().cesm_slaf_bwd_dw_nblk(Nf, HW, C)
+    if nblk_dx <= 0:
+        raise ValueError(f"slaf_bwd_dw: unsupported shape C={C}")
+    dev = x.device
+    dx = empty(x.shape, x.dtype, dev)
+    nblk = lib().cesm_slaf_nblk(Nf, HW)
+    part = empty((nblk * Nf * 8 * 1024,), torch.float32, dev)
+    G = empty((Nf, 8, 64, 16), torch.float32, dev)
+    adc = empty((Nf, 8, 2, 64, 8), torch.bfloat16, dev)
+    adcT = empty((Nf, 8, 2, 64, 8), torch.bfloat16, dev)
+    slab = empty((nblk_dx, 768, C), torch.float32, dev)
+    tmp = empty((768, C), torch.float32, dev)
+    wimg = empty(((2 * 768 + 256) * C,), torch.bfloat16, dev)
+    call("cesm_slaf_bwd_dw", P(x), P(dy), P(gamma_one), P(wq_fold), P(wqkv_f32), P(gamma), P(wout_t), P(mz), P(ctx32),
+         P(actT), P(actx), P(dx), P(dwqkv), P(dgamma), P(part), P(G), P(adc), P(adcT), P(slab), P(tmp), P(wimg),
+         nblk_dx, Nf, HW, C, float(scale), float(eps), 1, S())
+    return dx
+
+
 def sla_fwd(qkv, Nf, HW, scale):
     nchunk = lib().cesm_sla_nchunk(HW)
     out = empty((qkv.shape[0], 256), qkv.dtype, qkv.device)

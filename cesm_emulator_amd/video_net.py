@@ -109,6 +109,12 @@ def gbuf(p):
     return p.grad
 
 
+def _wflat(p):
+    """gradient buffer of a 1x1 conv weight [O, I, 1, 1] viewed as [O, I] (or None)"""
+    g = gbuf(p)
+    return None if g is None else g.view(g.shape[0], g.shape[1])
+
+
 def _gflat(p):
     """flat view of p's gradient buffer (LayerNorm gamma [1, C, 1, 1, 1] -> [C]) or None"""
     g = gbuf(p)
@@ -462,19 +468,46 @@ def _sla_fused(rc, C):
     return FUSED_SLA and rc.cdt == torch.bfloat16 and C in K.SLAF_C
 
 
+# head-parallel SLA backward with in-kernel weight gradients (C = 64)
+SLA_DW = os.environ.get("CESM_NO_SLA_DW", "0") != "1"
+_ONES = {}
+
+
+def _ones(C, device):
+    t = _ONES.get((C, device))
+    if t is None:
+        t = _ONES[(C, device)] = torch.ones(C, device=device)
+    return t
+
+
+def _sla_dw(rc, x):
+    Nb, H, W, C = x.shape
+    return SLA_DW and _sla_fused(rc, C) and K.slaf_bwd_dw_supported(Nb, H * W, C)
+
+
 def sla_fwd(rc, res_mod, x):
     """Residual(PreNorm(SpatialLinearAttention)) per frame (video_net.py:313-347).
     bf16, C=64: fused kernels (csrc/sla_fused.hip); otherwise LN -> to_qkv -> core -> to_out."""
     pre = res_mod.fn
     sla = pre.fn
     Nb, H, W, C = x.shape
+    if _sla_dw(rc, x):
+        # LN gamma folded into the QKV weights (unit gamma in the kernels): the backward then produces the
+        # to_qkv and gamma gradients in-kernel.  O is always saved for the to_out weight gradient.
+        gamma = _flat(pre.norm.gamma)
+        wq_fold = K.pack_scaled(sla.to_qkv.weight.reshape(768, C), gamma)
+        wo = rc.packed(sla.to_out.weight, C, 256, 1, 1, 0, 0)
+        ones = _ones(C, x.device)
+        y, state = K.slaf_fwd(x, ones, wq_fold, wo, sla.to_out.bias, sla.scale, eps=pre.norm.eps, save_o=rc.save)
+        st = SimpleNamespace(fused=True, fold=True, x=x, state=state, wq_fold=wq_fold) if rc.save else None
+        return y, st
     if _sla_fused(rc, C):
         wq = rc.packed(sla.to_qkv.weight, 768, C, 1, 1, 0, 0)
         wo = rc.packed(sla.to_out.weight, C, 256, 1, 1, 0, 0)
         # training: the forward also writes O (to_out's input) so the backward does not emit it
         y, state = K.slaf_fwd(x, _flat(pre.norm.gamma), wq, wo, sla.to_out.bias, sla.scale, eps=pre.norm.eps,
                               save_o=rc.save and SLA_FWD_O)
-        st = SimpleNamespace(fused=True, x=x, state=state) if rc.save else None
+        st = SimpleNamespace(fused=True, fold=False, x=x, state=state) if rc.save else None
         return y, st
     n, mr = K.ln_fwd(x, _flat(pre.norm.gamma), save=rc.save, eps=pre.norm.eps)
     qkv, qst = conv_forward(rc, ConvSpec(sla.to_qkv), n)
@@ -488,6 +521,19 @@ def sla_bwd(rc, res_mod, st, dy):
     pre = res_mod.fn
     sla = pre.fn
     Nb, H, W, C = st.x.shape
+    if st.fused and st.fold:
+        wo_t = rc.packed(sla.to_out.weight, 256, C, 1, 1, 1, 1)
+        dwo, dbo = gbuf(sla.to_out.weight), gbuf(sla.to_out.bias)
+        dx = K.slaf_bwd_dw(st.x, dy, _ones(C, dy.device), st.wq_fold, sla.to_qkv.weight.reshape(768, C),
+                           _flat(pre.norm.gamma), wo_t, st.state, _wflat(sla.to_qkv.weight), _gflat(pre.norm.gamma),
+                           sla.scale, eps=pre.norm.eps)
+        o = st.state[4]
+        with rc.side(o, dy, attn=True):
+            if dwo is not None and K.conv_wgrad(o, None, dy, None, dwo, (H, W, C, 1, 1, 1, 0, 1), 0, 0, db=dbo):
+                dbo = None
+            if dbo is not None:
+                K.colsum(dy, dbo)
+        return dx
     if st.fused:
         wq = rc.packed(sla.to_qkv.weight, 768, C, 1, 1, 0, 0)
         wq_t = rc.packed(sla.to_qkv.weight, C, 768, 1, 1, 1, 1)

@@ -725,3 +725,52 @@ def test_tblock_fold_forward_and_dw_backward(dev, Fr, B, H, W):
     print(f"tblock fold/dw C=64 F={Fr} B={B} {H}x{W}: " + " ".join(f"{k} {v:.2e}" for k, v in errs.items()))
     for k, v in errs.items():
         assert v < 3e-2, (k, v)
+
+
+@pytest.mark.parametrize("H,W", [(8, 8), (12, 20), (37, 29), (48, 96)])
+def test_sla_fold_forward_and_dw_backward(dev, H, W):
+    """the level-0 SLA training path at C = 64: slaf_fwd with LN gamma folded into W_qkv (pack_scaled, unit
+    gamma) + cesm_slaf_bwd_dw (head-parallel backward, in-kernel dW_qkv / dgamma, no dqkv / xn
+    intermediates) vs float64 autograd through the reference block (video_net.py:313-347); pixel counts
+    that leave partial 48-pixel groups"""
+    C = 64
+    torch.manual_seed(15)
+    B, Fr = 2, 3
+    res = _sla_block(C, dev)
+    sla = res.fn.fn
+    x = q(torch.randn(B, C, Fr, H, W), torch.bfloat16)
+    g = q(torch.randn(B, C, Fr, H, W), torch.bfloat16)
+    xd = to_cl(x).to(dev, torch.bfloat16)
+    gd = to_cl(g).to(dev, torch.bfloat16)
+    wqkv = sla.to_qkv.weight.detach().reshape(768, C).contiguous()
+    wout = sla.to_out.weight.detach().reshape(C, 256)
+    wo = K.conv_pack(wout, torch.bfloat16, C, 256, 1, 1, 0, 0)
+    wo_t = K.conv_pack(wout, torch.bfloat16, 256, C, 1, 1, 1, 1)
+    gamma = res.fn.norm.gamma.detach().reshape(-1).contiguous()
+    ones = torch.ones(C, device=dev)
+    wq_fold = K.pack_scaled(wqkv, gamma)
+    assert torch.equal(wq_fold.float().cpu(), (wqkv * gamma).to(torch.bfloat16).float().cpu())
+    assert torch.equal(K.pack_scaled(wqkv, gamma, trans=True), wq_fold.t().contiguous())
+    y, st = K.slaf_fwd(xd, ones, wq_fold, wo, sla.to_out.bias.detach(), sla.scale, save_o=True)
+    dgamma = torch.full((C,), 0.25, device=dev)
+    dwq = torch.full((768, C), 0.5, device=dev)
+    assert K.slaf_bwd_dw_supported(B * Fr, H * W, C)
+    dx = K.slaf_bwd_dw(xd, gd, ones, wq_fold, wqkv, gamma, wo_t, st, dwq, dgamma, sla.scale)
+    torch.cuda.synchronize()
+    o = st[4]
+    dwo = gd.reshape(-1, C).double().t() @ o.reshape(-1, 256).double()
+    ref = _sla_block_ref(res, C)
+    ref.fn.fn.to_qkv.weight.data.copy_(sla.to_qkv.weight.detach().cpu().double())  # fp32 master (folded in bf16)
+    xr = x.double().requires_grad_(True)
+    yr = ref(xr)
+    (yr * g.double()).sum().backward()
+    errs = {
+        "y": rel(from_cl(y, B), yr.detach()),
+        "dx": rel(from_cl(dx, B), xr.grad),
+        "dgamma": rel(dgamma.double() - 0.25, ref.fn.norm.gamma.grad.reshape(-1)),
+        "dWqkv": rel(dwq.double() - 0.5, ref.fn.fn.to_qkv.weight.grad.reshape(768, C)),
+        "dWout": rel(dwo, ref.fn.fn.to_out.weight.grad.reshape(C, 256)),
+    }
+    print(f"sla fold/dw HxW={H}x{W}: " + " ".join(f"{k} {v:.2e}" for k, v in errs.items()))
+    for k, v in errs.items():
+        assert v < 3e-2, (k, v)

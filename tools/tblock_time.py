@@ -86,9 +86,27 @@ def main():
                    want_wgrad_inputs=os.environ.get("TW_NOEMIT", "0") == "0")
 
     sb = timed(sbwd, reps)
+    # the old SLA path's to_qkv weight gradient, and the in-kernel-dW backward (C = 64)
+    st["sb"] = K.slaf_bwd(x, dy, gamma, wq, wq_t, wo_t, sst, dgamma, 32 ** -0.5, want_wgrad_inputs=True)
+
+    def sqwgrad():
+        _, dqkv, _, xn = st["sb"]
+        K.conv_wgrad(xn, None, dqkv, None, dwq, (H, W, 768, 1, 1, 1, 0, 1), 0, 0)
+
+    tsq = timed(sqwgrad, reps)
+    tsdw = float("nan")
+    if K.slaf_bwd_dw_supported(B * F, H * W, C):
+        ones = torch.ones(C, device=dev)
+        wqf = K.pack_scaled(wqkv, gamma)
+        _, sstf = K.slaf_fwd(x, ones, wqf, wo, bout, 32 ** -0.5, save_o=True)
+
+        def sbwd_dw():
+            K.slaf_bwd_dw(x, dy, ones, wqf, wqkv, gamma, wo_t, sstf, dwq, dgamma, 32 ** -0.5)
+
+        tsdw = timed(sbwd_dw, reps)
     lib = os.environ.get("CESM_HIP_LIB", "default") + (" noemit" if os.environ.get("TW_NOEMIT", "0") != "0" else "")
     print(f"{lib}: C={C} tw_fwd {tf:.1f} us  tw_bwd {tb:.1f} us (+ qkv wgrad {tqw:.1f} us)  tw_bwd_dw {tdw:.1f} us  "
-          f"sla_fwd {sf:.1f} us  sla_bwd {sb:.1f} us  "
+          f"sla_fwd {sf:.1f} us  sla_bwd {sb:.1f} us (+ qkv wgrad {tsq:.1f} us)  sla_bwd_dw {tsdw:.1f} us  "
           f"y {float(y.float().abs().mean()):.6f} ys {float(ys.float().abs().mean()):.6f}")
 
 
