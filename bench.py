@@ -163,6 +163,20 @@ class KernelProbe:
             return (f"twh_bwd_kernel<{nv}> (+ dW / dgamma / dbias reductions)",
                     v * (tw_core_flop(C, F) + 2.0 * 768 * C), float(v * (3 * C * 2 + 40)))
 
+        def tattn_fwd(qkv, bias, rot, B, F, HW, scale, save=True):
+            v = B * F * HW
+            lab = (f"tflash_fwd_kernel<{(F + 15) // 16}>" if K._tflash(qkv, F) else "tattn_fwd_kernel")
+            # q.k and attn.v over the F frames of each pixel and head; bytes: qkv read, out (+ lse) written
+            return lab, 4.0 * F * 32 * 8 * v, float(v * (768 * 2 + 256 * 2 + (32 if save else 0)))
+
+        def tattn_bwd(qkv, o, dout, lse, bias, rot, dtable, B, F, HW, scale, num_buckets=32, max_distance=32):
+            v = B * F * HW
+            nt = (F + 15) // 16
+            lab = (f"tflash_bwd_q_kernel<{nt}> + tflash_bwd_kv_kernel<{nt}>" if K._tflash(qkv, F)
+                   else "tattn_bwd_kernel")
+            # dP, dQ, dK, dV products (2x the forward); bytes: qkv, o, dout, lse read, dqkv written
+            return lab, 8.0 * F * 32 * 8 * v, float(v * (768 * 2 * 2 + 256 * 2 * 2 + 32))
+
         def sla_flop(C):  # per voxel: to_qkv + to_out + context k v^T and context^T q (8 heads, 32 x 32)
             return 2.0 * 768 * C + 2.0 * 256 * C + 2.0 * 2 * 32 * 32 * 8
 
@@ -204,6 +218,7 @@ class KernelProbe:
 
         for name, fn in dict(conv_fwd=conv_fwd, conv_wgrad=conv_wgrad, tblock_fwd=tblock_fwd, tblock_bwd=tblock_bwd,
                              tblock_fwd_fold=tblock_fwd_fold, tblock_bwd_dw=tblock_bwd_dw,
+                             tattn_fwd=tattn_fwd, tattn_bwd=tattn_bwd,
                              slaf_fwd=slaf_fwd, slaf_bwd=slaf_bwd, gn_stats=gn_stats, gn_apply=gn_apply, gn_bwd=gn_bwd,
                              ln_fwd=ln_fwd, ln_bwd=ln_bwd, adamw=adamw, add=add).items():
             self._wrap(name, fn)

@@ -1,0 +1,539 @@
+// Temporal attention core on MFMA for the unfused path (bf16): long windows (F = 120, BASELINE config 4) and
+// the C >= 256 levels.  Same contract as tattn_fwd / tattn_bwd in attn.hip (video_net.py:403-454):
+//   per (sample b, pixel p, head h): q' = scale R_f q_f, k' = R_f k_f (RoPE, rotary_embedding.py:35-48),
+//   S[i][j] = q'_i . k'_j + bias[h][i][j], P = softmax_j S, O_i = sum_j P_ij v_j.
+// One wave owns one (pixel, head): F <= 128 frames = NT 16-frame tiles, every q.k product a 16x16x32 MFMA
+// (K = the 32 head dims).  The transposed orientation is used throughout: S^T tiles put a query column in
+// each lane group, so the softmax over keys is an in-lane loop + a 4-lane-group reduction, and two key
+// tiles of P^T in MFMA D layout are directly a B operand through the k-slot map (slot (g, j < 4) <-> key
+// 4g + j, (g, 4 + j) <-> 16 + 4g + j); the matching A operands (V^T, K'^T, Q'^T, dO^T) are gathered from
+// LDS-staged rows with the hardware transpose read.
+// The rel-pos bias depends on j - i only: it is read from a per-head table by offset (2F - 1 entries), and
+// its gradient is accumulated by offset in registers (the offset of every element a lane holds is fixed by
+// the lane, the register index and the (query tile, key tile) pair) and reduced to buckets afterwards.
+// Backward = two kernels: dq (query tiles outer; D_i = dO_i . O_i; dbias) and dk / dv (key tiles outer).
+#include "common.h"
+
+namespace {
+
+constexpr int NH = 8, DH = 32, INNER = 256, QKV = 768;
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr int TF_LD = 40;     // staged-row stride (bf16): 80-B rows
+constexpr int TF_MAXT = 8;    // 16-frame tiles: F <= 128
+
+__device__ __forceinline__ bf16x8 zero8() {
+  bf16x8 z;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) z[i] = (bf16)0.f;
+  return z;
+}
+__device__ __forceinline__ bf16x8 ld16(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+__device__ __forceinline__ float grp4_sum(float v) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float grp4_max(float v) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ bf16x8 pack_kslot(const float* t0, const float* t1) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    r[j] = (bf16)t0[j];
+    r[4 + j] = (bf16)t1[j];
+  }
+  return r;
+}
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// 8 head dims 8g..8g+7 of one frame row (16-B load), RoPE-rotated by frame f when rot != null, times `scale`
+__device__ __forceinline__ bf16x8 row_frag(const bf16* p, const float* __restrict__ rot, int f, int g, float scale,
+                                           bool ok) {
+  const bf16x8 v = ld16(p);
+  bf16x8 o = zero8();
+  if (rot) {
+    const f32x4 c0 = *reinterpret_cast<const f32x4*>(rot + (f * 16 + 4 * g) * 2);      // pairs 4g, 4g+1
+    const f32x4 c1 = *reinterpret_cast<const f32x4*>(rot + (f * 16 + 4 * g + 2) * 2);  // pairs 4g+2, 4g+3
+    const float cs[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float c = cs[2 * u], s = cs[2 * u + 1];
+      const float a = (float)v[2 * u], b = (float)v[2 * u + 1];
+      o[2 * u] = (bf16)(ok ? (a * c - b * s) * scale : 0.f);
+      o[2 * u + 1] = (bf16)(ok ? (b * c + a * s) * scale : 0.f);
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = ok ? v[e] : (bf16)0.f;
+  }
+  return o;
+}
+
+// A operand with rows = 16 head dims (c0 .. c0+15) and k-slots = the 32 frames of pair s of a staged
+// [frames][TF_LD] tile: lane (g, i) <- tile[32s + kslot(g, j)][c0 + i]
+__device__ __forceinline__ bf16x8 tr_pair(const bf16* tile, int s, int c0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tile + (32 * s + 4 * g + q) * TF_LD + c0 + 4 * p));
+  const s16x4 b =
+      __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tile + (32 * s + 16 + 4 * g + q) * TF_LD + c0 + 4 * p));
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    r[j] = __builtin_bit_cast(bf16, (short)a[j]);
+    r[4 + j] = __builtin_bit_cast(bf16, (short)b[j]);
+  }
+  return r;
+}
+
+// R^T (inverse rotation) of dims d0 .. d0+3 (two pairs) of frame f, times `scale`
+__device__ __forceinline__ void rope4_inv(float* v, const float* __restrict__ rot, int f, int d0, float scale) {
+  const f32x4 cs = *reinterpret_cast<const f32x4*>(rot + (f * 16 + d0 / 2) * 2);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const float c = cs[2 * u], s = cs[2 * u + 1];
+    const float a = v[2 * u], b = v[2 * u + 1];
+    v[2 * u] = (a * c + b * s) * scale;
+    v[2 * u + 1] = (b * c - a * s) * scale;
+  }
+}
+
+__device__ __forceinline__ void store4b(bf16* p, const float* v) {
+  bf16x4 a = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+  *reinterpret_cast<bf16x4*>(p) = a;
+}
+
+// bias by offset n = j - i (index n + F - 1), log2 units, for head h
+__device__ __forceinline__ void load_boff(const float* __restrict__ bias, float* boff, int h, int F, int tid, int nthr) {
+  for (int e = tid; e < 2 * F - 1; e += nthr) {
+    const int n = e - (F - 1);
+    const int i = n < 0 ? -n : 0, j = i + n;
+    boff[e] = bias[((int64_t)h * F + i) * F + j] * LOG2E;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ forward
+// grid (cdiv(HW, 4), B * 8), 256 threads: wave = one pixel of one (sample, head)
+template <int NT>
+__global__ __launch_bounds__(256) void tflash_fwd_kernel(const bf16* __restrict__ qkv, const float* __restrict__ bias,
+                                                         const float* __restrict__ rot, bf16* __restrict__ out,
+                                                         float* __restrict__ lse, int F, int HW, float scale) {
+  constexpr int NP = (NT + 1) / 2, NR = 32 * NP;  // key-tile pairs, staged rows
+  __shared__ float boff[2 * 16 * TF_MAXT];
+  __shared__ __attribute__((aligned(16))) bf16 vst[4][NR * TF_LD];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, lr = lane & 15, g = lane >> 4;
+  const int b = blockIdx.y >> 3, h = blockIdx.y & 7;
+  load_boff(bias, boff, h, F, tid, 256);
+  __syncthreads();
+  const int p = blockIdx.x * 4 + wid;
+  if (p >= HW) return;
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  const int64_t row0 = (int64_t)b * F * HW + p;  // voxel of frame f: row0 + f * HW
+  bf16* vs = vst[wid];
+  for (int e = lane; e < NR * 4; e += 64) {  // V rows (zero past F)
+    const int f = e >> 2, c = e & 3;
+    const bf16x8 v = ld16(qkv + (row0 + (int64_t)(f < F ? f : 0) * HW) * QKV + 2 * INNER + h * DH + c * 8);
+    *reinterpret_cast<bf16x8*>(vs + f * TF_LD + c * 8) = f < F ? v : zero8();
+  }
+  bf16x8 kf[NT];
+#pragma unroll
+  for (int kt = 0; kt < NT; ++kt) {
+    const int f = kt * 16 + lr;
+    const bool ok = f < F;
+    kf[kt] = row_frag(qkv + (row0 + (int64_t)(ok ? f : 0) * HW) * QKV + INNER + h * DH + g * 8, rot, ok ? f : 0, g, 1.f, ok);
+  }
+  wsync();
+  bf16x8 vf[NP][2];
+#pragma unroll
+  for (int s = 0; s < NP; ++s)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) vf[s][t] = tr_pair(vs, s, t * 16, lane);
+
+  for (int qt = 0; qt < NT; ++qt) {
+    const int fq = qt * 16 + lr;
+    const bool okq = fq < F;
+    const bf16x8 qf = row_frag(qkv + (row0 + (int64_t)(okq ? fq : 0) * HW) * QKV + h * DH + g * 8, rot, okq ? fq : 0, g,
+                               scale, okq);
+    float sc[2 * NP][4];
+    float m = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 2 * NP; ++kt) {
+      const f32x4 st = kt < NT ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt < NT ? kt : 0], qf, z4, 0, 0, 0) : z4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kt * 16 + 4 * g + r;
+        const bool ok = okq && key < F;
+        const float bo = boff[ok ? key - fq + F - 1 : 0];
+        sc[kt][r] = ok ? fmaf(st[r], LOG2E, bo) : -INFINITY;
+        m = fmaxf(m, sc[kt][r]);
+      }
+    }
+    m = grp4_max(m);
+    const float mm = m == -INFINITY ? 0.f : m;
+    float l = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 2 * NP; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        sc[kt][r] = __builtin_amdgcn_exp2f(sc[kt][r] - mm);  // exp2(-inf) = 0
+        l += sc[kt][r];
+      }
+    l = grp4_sum(l);
+    f32x4 ot[2] = {z4, z4};
+#pragma unroll
+    for (int s = 0; s < NP; ++s) {
+      const bf16x8 pb = pack_kslot(sc[2 * s], sc[2 * s + 1]);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) ot[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[s][t], pb, ot[t], 0, 0, 0);
+    }
+    if (okq) {
+      const float inv = __builtin_amdgcn_rcpf(l);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        float o4[4] = {ot[t][0] * inv, ot[t][1] * inv, ot[t][2] * inv, ot[t][3] * inv};
+        store4b(out + (row0 + (int64_t)fq * HW) * INNER + h * DH + t * 16 + 4 * g, o4);
+      }
+      if (lse && g == 0) lse[(((int64_t)b * NH + h) * HW + p) * F + fq] = mm + log2f(l);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ backward, dq
+// grid (nblk, B * 8), 64*NT threads: wave w = query tile w of the block's current pixel (grid-stride over pixels),
+// the pixel's K' and V rows staged once in LDS for all waves.  Writes dq into dqkv, D_i = dO_i . O_i into dbuf
+// [B][8][HW][F], and per-block dbias-by-offset partials part[(b*8 + h)][blk][2F - 1].  With the query tile
+// fixed per wave, the dbias accumulator of (r, kt) holds one diagonal kt - qt for every pixel: static registers.
+template <int NT>
+__global__ __launch_bounds__(64 * NT) void tflash_bwd_q_kernel(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
+    const float* __restrict__ lse, const float* __restrict__ bias, const float* __restrict__ rot,
+    bf16* __restrict__ dqkv, float* __restrict__ dbuf, float* __restrict__ part, int F, int HW, float scale) {
+  constexpr int NP = (NT + 1) / 2, NR = 32 * NP, NTH = 64 * NT;
+  __shared__ float boff[2 * 16 * TF_MAXT];
+  __shared__ float dacc[2 * 16 * TF_MAXT];
+  __shared__ __attribute__((aligned(16))) bf16 ks[NR * TF_LD];
+  __shared__ __attribute__((aligned(16))) bf16 vs[NR * TF_LD];
+  const int tid = threadIdx.x, lane = tid & 63, qt = tid >> 6, lr = lane & 15, g = lane >> 4;
+  const int b = blockIdx.y >> 3, h = blockIdx.y & 7;
+  load_boff(bias, boff, h, F, tid, NTH);
+  for (int e = tid; e < 2 * 16 * TF_MAXT; e += NTH) dacc[e] = 0.f;
+  for (int e = tid; e < (NR - 16 * NT) * 4; e += NTH) {  // rows past the last key tile stay zero
+    const int f = 16 * NT + (e >> 2), c = e & 3;
+    *reinterpret_cast<bf16x8*>(ks + f * TF_LD + c * 8) = zero8();
+  }
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  float dba[4][NT];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int kt = 0; kt < NT; ++kt) dba[r][kt] = 0.f;
+  const int fq = qt * 16 + lr;
+  const bool okq = fq < F;
+
+  for (int p = blockIdx.x; p < HW; p += gridDim.x) {
+    const int64_t row0 = (int64_t)b * F * HW + p;
+    __syncthreads();  // previous pixel's rows consumed
+    for (int e = tid; e < 16 * NT * 4; e += NTH) {  // rotated K' rows and V rows, 16-B chunks
+      const int f = e >> 2, c = e & 3;
+      const bool ok = f < F;
+      const int64_t rr = (row0 + (int64_t)(ok ? f : 0) * HW) * QKV;
+      *reinterpret_cast<bf16x8*>(ks + f * TF_LD + c * 8) = row_frag(qkv + rr + INNER + h * DH + c * 8, rot, ok ? f : 0, c, 1.f, ok);
+      *reinterpret_cast<bf16x8*>(vs + f * TF_LD + c * 8) = row_frag(qkv + rr + 2 * INNER + h * DH + c * 8, nullptr, 0, c, 1.f, ok);
+    }
+    const int64_t vq = row0 + (int64_t)(okq ? fq : 0) * HW;
+    const bf16x8 qf = row_frag(qkv + vq * QKV + h * DH + g * 8, rot, okq ? fq : 0, g, scale, okq);
+    const bf16x8 dof = row_frag(dout + vq * INNER + h * DH + g * 8, nullptr, 0, g, 1.f, okq);
+    const float Li = okq ? lse[(((int64_t)b * NH + h) * HW + p) * F + fq] : 0.f;
+    __syncthreads();  // rows staged
+    // pass 1: P^T and dP^T of every key tile, D_i = sum_j P_ij dP_ij (exact: at F = 1 the bias gradient is 0)
+    float pt[NT][4], dpt[NT][4];
+    float D = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NT; ++kt) {
+      const bf16x8 kf = ld16(ks + (kt * 16 + lr) * TF_LD + g * 8);
+      const bf16x8 vf = ld16(vs + (kt * 16 + lr) * TF_LD + g * 8);
+      const f32x4 st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf, z4, 0, 0, 0);   // S'^T
+      const f32x4 dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, dof, z4, 0, 0, 0);  // dP^T
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kt * 16 + 4 * g + r;
+        const bool ok = okq && key < F;
+        const float bo = boff[ok ? key - fq + F - 1 : 0];
+        pt[kt][r] = ok ? __builtin_amdgcn_exp2f(fmaf(st[r], LOG2E, bo) - Li) : 0.f;
+        dpt[kt][r] = dp[r];
+        D = fmaf(pt[kt][r], dp[r], D);
+      }
+    }
+    D = grp4_sum(D);
+    if (okq && g == 0) dbuf[(((int64_t)b * NH + h) * HW + p) * F + fq] = D;
+    // pass 2: dS^T = P^T (dP^T - D) -> dbias, dQ'^T = K'^T dS^T
+    f32x4 dqt[2] = {z4, z4};
+#pragma unroll
+    for (int s = 0; s < NP; ++s) {
+      float dsv[2][4];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int kt = 2 * s + u;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float ds = kt < NT ? pt[kt < NT ? kt : 0][r] * (dpt[kt < NT ? kt : 0][r] - D) : 0.f;
+          dsv[u][r] = ds;
+          if (kt < NT) dba[r][kt < NT ? kt : 0] += ds;
+        }
+      }
+      const bf16x8 db = pack_kslot(dsv[0], dsv[1]);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        dqt[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_pair(ks, s, t * 16, lane), db, dqt[t], 0, 0, 0);
+    }
+    if (okq) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int d0 = t * 16 + 4 * g;
+        float v4[4] = {dqt[t][0], dqt[t][1], dqt[t][2], dqt[t][3]};
+        rope4_inv(v4, rot, fq, d0, scale);  // dq = scale R^T dQ'
+        store4b(dqkv + (row0 + (int64_t)fq * HW) * QKV + h * DH + d0, v4);
+      }
+    }
+  }
+  // dbias partials by offset n = 16 (kt - qt) + 4g + r - lr: once per wave (LDS atomics), then the block's row
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int kt = 0; kt < NT; ++kt) {
+      const int n = 16 * (kt - qt) + 4 * g + r - lr;
+      if (n > -F && n < F && dba[r][kt] != 0.f) atomicAdd(&dacc[n + F - 1], dba[r][kt]);
+    }
+  __syncthreads();
+  for (int e = tid; e < 2 * F - 1; e += NTH)
+    part[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * (2 * F - 1) + e] = dacc[e];
+}
+
+// ------------------------------------------------------------------------------------------------ backward, dk dv
+// grid (cdiv(HW, 4), B * 8), 256 threads: wave = one pixel; key tiles outer, query-tile pairs inner
+template <int NT>
+__global__ __launch_bounds__(256, 2) void tflash_bwd_kv_kernel(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ dbuf, const float* __restrict__ bias, const float* __restrict__ rot,
+    bf16* __restrict__ dqkv, int F, int HW, float scale) {
+  constexpr int NP = (NT + 1) / 2, NR = 32 * NP;
+  __shared__ float boff[2 * 16 * TF_MAXT];
+  __shared__ __attribute__((aligned(16))) bf16 stg[4][NR * TF_LD];
+  __shared__ float lds_l[4][NR], lds_d[4][NR];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, lr = lane & 15, g = lane >> 4;
+  const int b = blockIdx.y >> 3, h = blockIdx.y & 7;
+  load_boff(bias, boff, h, F, tid, 256);
+  __syncthreads();
+  const int p = blockIdx.x * 4 + wid;
+  if (p >= HW) return;
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  const int64_t row0 = (int64_t)b * F * HW + p;
+  bf16* st = stg[wid];
+  float* Ls = lds_l[wid];
+  float* Ds = lds_d[wid];
+  for (int e = lane; e < NR; e += 64) {
+    const bool ok = e < F;
+    const int64_t si = (((int64_t)b * NH + h) * HW + p) * F + (ok ? e : 0);
+    Ls[e] = ok ? lse[si] : 0.f;
+    Ds[e] = ok ? dbuf[si] : 0.f;
+  }
+  for (int e = lane; e < (NR - 16 * NT) * 4; e += 64) {
+    const int f = 16 * NT + (e >> 2), c = e & 3;
+    *reinterpret_cast<bf16x8*>(st + f * TF_LD + c * 8) = zero8();
+  }
+  // query-row operands: Q' (rotated, scaled) and dO as A fragments, and their k-slot transposes
+  bf16x8 qa[NT], da[NT], qtf[NP][2], dtf[NP][2];
+#pragma unroll
+  for (int qt = 0; qt < NT; ++qt) {
+    const int f = qt * 16 + lr;
+    const bool ok = f < F;
+    const int64_t vq = row0 + (int64_t)(ok ? f : 0) * HW;
+    qa[qt] = row_frag(qkv + vq * QKV + h * DH + g * 8, rot, ok ? f : 0, g, scale, ok);
+    da[qt] = row_frag(dout + vq * INNER + h * DH + g * 8, nullptr, 0, g, 1.f, ok);
+    *reinterpret_cast<bf16x8*>(st + f * TF_LD + g * 8) = qa[qt];
+  }
+  wsync();
+#pragma unroll
+  for (int s = 0; s < NP; ++s)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) qtf[s][t] = tr_pair(st, s, t * 16, lane);
+  wsync();
+#pragma unroll
+  for (int qt = 0; qt < NT; ++qt) *reinterpret_cast<bf16x8*>(st + (qt * 16 + lr) * TF_LD + g * 8) = da[qt];
+  wsync();
+#pragma unroll
+  for (int s = 0; s < NP; ++s)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) dtf[s][t] = tr_pair(st, s, t * 16, lane);
+
+  for (int kt = 0; kt < NT; ++kt) {
+    const int fk = kt * 16 + lr;
+    const bool okk = fk < F;
+    const int64_t rk = (row0 + (int64_t)(okk ? fk : 0) * HW) * QKV;
+    const bf16x8 kb = row_frag(qkv + rk + INNER + h * DH + g * 8, rot, okk ? fk : 0, g, 1.f, okk);  // K'^T col
+    const bf16x8 vb = row_frag(qkv + rk + 2 * INNER + h * DH + g * 8, nullptr, 0, g, 1.f, okk);     // V^T col
+    f32x4 dk[2] = {z4, z4}, dv[2] = {z4, z4};
+#pragma unroll
+    for (int s = 0; s < NP; ++s) {
+      float pv[2][4], dsv[2][4];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int qt = 2 * s + u;
+        if (qt < NT) {
+          const f32x4 sq = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[qt], kb, z4, 0, 0, 0);  // S'[q][key]
+          const f32x4 dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da[qt], vb, z4, 0, 0, 0);  // dP[q][key]
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int q = qt * 16 + 4 * g + r;
+            const bool ok = okk && q < F;
+            const float bo = boff[ok ? fk - q + F - 1 : 0];
+            const float pp = ok ? __builtin_amdgcn_exp2f(fmaf(sq[r], LOG2E, bo) - Ls[q]) : 0.f;
+            pv[u][r] = pp;
+            dsv[u][r] = pp * (dp[r] - Ds[q]);
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) pv[u][r] = dsv[u][r] = 0.f;
+        }
+      }
+      const bf16x8 pb = pack_kslot(pv[0], pv[1]);
+      const bf16x8 db = pack_kslot(dsv[0], dsv[1]);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        dv[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dtf[s][t], pb, dv[t], 0, 0, 0);  // dV^T[d][key]
+        dk[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qtf[s][t], db, dk[t], 0, 0, 0);  // dK'^T[d][key]
+      }
+    }
+    if (okk) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int d0 = t * 16 + 4 * g;
+        float k4[4] = {dk[t][0], dk[t][1], dk[t][2], dk[t][3]};
+        float v4[4] = {dv[t][0], dv[t][1], dv[t][2], dv[t][3]};
+        rope4_inv(k4, rot, fk, d0, 1.f);  // dk = R^T dK'
+        bf16* dst = dqkv + (row0 + (int64_t)fk * HW) * QKV + h * DH + d0;
+        store4b(dst + INNER, k4);
+        store4b(dst + 2 * INNER, v4);
+      }
+    }
+  }
+}
+
+// dtable[bucket][h] (+)= sum over partials and offsets n with bucket(n) of part[(b*8 + h)][blk][n + F - 1]
+__device__ int tf_bucket(int rel, int num_buckets, int max_distance) {  // relpos_bucket of attn.hip
+  int n = -rel;
+  const int nb = num_buckets / 2;
+  int ret = n < 0 ? nb : 0;
+  n = n < 0 ? -n : n;
+  const int max_exact = nb / 2;
+  if (n < max_exact) return ret + n;
+  const float lg = logf((float)n / (float)max_exact) / logf((float)max_distance / (float)max_exact) *
+                   (float)(nb - max_exact);
+  int large = max_exact + (int)lg;
+  if (large > nb - 1) large = nb - 1;
+  return ret + large;
+}
+// stage 1: off[h][n] = sum over samples and blocks (block per (h, n), fixed order)
+__global__ void tf_dbias_off_kernel(const float* __restrict__ part, float* __restrict__ off, int nblk, int B, int F) {
+  const int h = blockIdx.y, e = blockIdx.x;
+  const int NO = 2 * F - 1;
+  float s = 0.f;
+  for (int k = threadIdx.x; k < B * nblk; k += 256) {
+    const int bb = k / nblk, kk = k - bb * nblk;
+    s += part[((int64_t)(bb * NH + h) * nblk + kk) * NO + e];
+  }
+  s = wave_sum(s);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) off[h * NO + e] = red[0] + red[1] + red[2] + red[3];
+}
+// stage 2: dtable[bucket][h] (+)= sum of off[h][n] over the offsets of that bucket
+__global__ void tf_dtable_kernel(const float* __restrict__ off, float* __restrict__ dtable, int F, int num_buckets,
+                                 int max_distance, int accumulate) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= num_buckets * NH) return;
+  const int bk = t / NH, h = t % NH;
+  float s = 0.f;
+  for (int n = -(F - 1); n < F; ++n)
+    if (tf_bucket(n, num_buckets, max_distance) == bk) s += off[h * (2 * F - 1) + n + F - 1];
+  dtable[t] = accumulate ? dtable[t] + s : s;
+}
+
+}  // namespace
+
+extern "C" {
+
+// supported windows of the MFMA temporal-attention core (bf16)
+int cesm_tflash_supported(int F) { return F >= 1 && F <= 16 * TF_MAXT; }
+
+// blocks per (sample, head) of cesm_tflash_bwd's dq kernel (its dbias partial rows)
+int cesm_tflash_nblk(int HW) { return std::max(1, std::min(HW, 128)); }
+
+// forward: qkv [B*F*HW][768] bf16 -> out [B*F*HW][256] bf16, lse [B][8][HW][F] (log2 units, nullable);
+// bias [8][F][F] (expanded rel-pos bias), rot [F][16][2]
+int cesm_tflash_fwd(const void* qkv, const float* bias, const float* rot, void* out, float* lse, int B, int F, int HW,
+                    float scale, hipStream_t stream) {
+  if (!cesm_tflash_supported(F) || B < 1 || HW < 1) return CESM_EUNSUPPORTED;
+  dim3 grid((unsigned)cdiv(HW, 4), B * NH);
+  const int nt = (F + 15) / 16;
+#define TFF(N) tflash_fwd_kernel<N><<<grid, 256, 0, stream>>>((const bf16*)qkv, bias, rot, (bf16*)out, lse, F, HW, scale)
+  switch (nt) {
+    case 1: TFF(1); break;
+    case 2: TFF(2); break;
+    case 3: TFF(3); break;
+    case 4: TFF(4); break;
+    case 5: TFF(5); break;
+    case 6: TFF(6); break;
+    case 7: TFF(7); break;
+    case 8: TFF(8); break;
+    default: return CESM_EUNSUPPORTED;
+  }
+#undef TFF
+  return cesm_launch_status();
+}
+
+// backward: dqkv [B*F*HW][768] (every channel written), from qkv, the forward's o and lse, and dout [..][256];
+// dtable (+)= the rel-pos table gradient (nullable).  Workspaces: dbuf B*8*HW*F floats, part
+// B*8*nblk*(2F-1) floats (nblk = cesm_tflash_nblk(HW)), off 8*(2F-1) floats.
+int cesm_tflash_bwd(const void* qkv, const void* o, const void* dout, const float* lse, const float* bias,
+                    const float* rot, void* dqkv, float* dtable, float* dbuf, float* part, float* off, int B, int F,
+                    int HW, float scale, int num_buckets, int max_distance, int accumulate, hipStream_t stream) {
+  if (!cesm_tflash_supported(F) || B < 1 || HW < 1) return CESM_EUNSUPPORTED;
+  const int nt = (F + 15) / 16;
+  const int nblk = cesm_tflash_nblk(HW);
+  dim3 gq(nblk, B * NH), gk((unsigned)cdiv(HW, 4), B * NH);
+#define TFB(N)                                                                                                         \
+  tflash_bwd_q_kernel<N><<<gq, 64 * N, 0, stream>>>((const bf16*)qkv, (const bf16*)o, (const bf16*)dout, lse, bias, rot, \
+                                                 (bf16*)dqkv, dbuf, part, F, HW, scale);                               \
+  tflash_bwd_kv_kernel<N><<<gk, 256, 0, stream>>>((const bf16*)qkv, (const bf16*)dout, lse, dbuf, bias, rot,           \
+                                                  (bf16*)dqkv, F, HW, scale)
+  switch (nt) {
+    case 1: TFB(1); break;
+    case 2: TFB(2); break;
+    case 3: TFB(3); break;
+    case 4: TFB(4); break;
+    case 5: TFB(5); break;
+    case 6: TFB(6); break;
+    case 7: TFB(7); break;
+    case 8: TFB(8); break;
+    default: return CESM_EUNSUPPORTED;
+  }
+#undef TFB
+  if (dtable) {
+    tf_dbias_off_kernel<<<dim3(2 * F - 1, NH), 256, 0, stream>>>(part, off, nblk, B, F);
+    tf_dtable_kernel<<<(unsigned)cdiv(num_buckets * NH, 64), 64, 0, stream>>>(off, dtable, F, num_buckets,
+                                                                               max_distance, accumulate);
+  }
+  return cesm_launch_status();
+}
+
+}  // extern "C"

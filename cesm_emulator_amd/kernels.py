@@ -281,16 +281,39 @@ def relpos_fwd(table, F, num_buckets=32, max_distance=32):
     return bias
 
 
+# bf16 temporal-attention core on MFMA (csrc/tflash.hip) for F <= 128; CESM_NO_TFLASH=1: the VALU kernels
+TFLASH = os.environ.get("CESM_NO_TFLASH", "0") != "1"
+
+
+def _tflash(qkv, F):
+    return TFLASH and qkv.dtype == torch.bfloat16 and lib().cesm_tflash_supported(F) == 1
+
+
 def tattn_fwd(qkv, bias, rot, B, F, HW, scale, save=True):
     V = qkv.shape[0]
+    _chk(qkv, (B * F * HW, 768))
     out = empty((V, 256), qkv.dtype, qkv.device)
     lse = empty((B, 8, HW, F), torch.float32, qkv.device) if save else None
+    if _tflash(qkv, F):
+        call("cesm_tflash_fwd", P(qkv), P(bias), P(rot), P(out), P(lse), B, F, HW, float(scale), S())
+        return out, lse
     call("cesm_tattn_fwd", dtcode(qkv), P(qkv), P(bias), P(rot), P(out), P(lse), B, F, HW, float(scale), S())
     return out, lse
 
 
 def tattn_bwd(qkv, o, dout, lse, bias, rot, dtable, B, F, HW, scale, num_buckets=32, max_distance=32):
     dqkv = empty(qkv.shape, qkv.dtype, qkv.device)
+    if _tflash(qkv, F):
+        _chk(o, (qkv.shape[0], 256), qkv.dtype)
+        _chk(dout, (qkv.shape[0], 256), qkv.dtype)
+        dev = qkv.device
+        nblk = lib().cesm_tflash_nblk(HW)
+        dbuf = empty((B, 8, HW, F), torch.float32, dev)
+        part = empty((B * 8 * nblk * (2 * F - 1),), torch.float32, dev)
+        off = empty((8 * (2 * F - 1),), torch.float32, dev)
+        call("cesm_tflash_bwd", P(qkv), P(o), P(dout), P(lse), P(bias), P(rot), P(dqkv), P(dtable), P(dbuf), P(part),
+             P(off), B, F, HW, float(scale), num_buckets, max_distance, 1, S())
+        return dqkv
     nblk = lib().cesm_tattn_nblk(F, HW)
     part = empty((B * 8 * nblk, F, F), torch.float32, qkv.device)
     call("cesm_tattn_bwd", dtcode(qkv), P(qkv), P(o), P(dout), P(lse), P(bias), P(rot), P(dqkv), P(part), B, F, HW,

@@ -107,6 +107,18 @@ int cesm_tattn_fwd(int dtype, const void* qkv, const float* bias, const float* r
 int cesm_tattn_bwd(int dtype, const void* qkv, const void* o, const void* dout, const float* lse, const float* bias,
                    const float* rot, void* dqkv, float* dbias_part, int B, int F, int HW, float scale,
                    hipStream_t stream);
+/* Temporal-attention core on MFMA (bf16, csrc/tflash.hip; F <= 128): same contract as cesm_tattn_fwd /
+ * cesm_tattn_bwd (video_net.py:403-454) for the unfused path (long windows, C >= 256 levels).  fwd: qkv
+ * [B*F*HW][768] -> out [..][256], lse [B][8][HW][F] (log2 units, nullable); bias [8][F][F], rot [F][16][2].
+ * bwd: dqkv [..][768] from qkv, o (the forward's out), lse, dout [..][256]; dtable (+)= the rel-pos table
+ * gradient (nullable).  Workspaces: dbuf B*8*HW*F, part B*8*cesm_tflash_nblk(HW)*(2F-1), off 8*(2F-1) floats. */
+int cesm_tflash_supported(int F);
+int cesm_tflash_nblk(int HW);
+int cesm_tflash_fwd(const void* qkv, const float* bias, const float* rot, void* out, float* lse, int B, int F, int HW,
+                    float scale, hipStream_t stream);
+int cesm_tflash_bwd(const void* qkv, const void* o, const void* dout, const float* lse, const float* bias,
+                    const float* rot, void* dqkv, float* dtable, float* dbuf, float* part, float* off, int B, int F,
+                    int HW, float scale, int num_buckets, int max_distance, int accumulate, hipStream_t stream);
 /* Fused temporal-attention block forward, bf16 (csrc/tblock.hip): y = x + Residual(PreNorm(Attention))
  * (video_net.py:69-98, :350-454) with LN, QKV GEMM, RoPE, MFMA core, out-proj in one kernel; x,y
  * [B*F*HW][C], wqkv [768][C], wout [C][256] packed bf16; saves mr [B*F*HW][2] and lse [B][8][HW][F].
