@@ -667,12 +667,16 @@ __global__ __launch_bounds__(256, 2) void slab_dx_kernel(
     float* __restrict__ dgamma_part, int HW, float scale, float eps) {
   constexpr int KS = C / 32, CT = C / 16;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* sg = smem;      // [C] dgamma accumulator
-  float* sgm = smem + C;  // [C] LN gamma (LDS reads do not queue behind the emission stores)
+  // per-wave dgamma accumulators [4][C] (each written by one wave, lanes on distinct channels, summed in a
+  // fixed order at the end: the block's partial is the same on every run — LDS float atomics across waves
+  // were not)
+  float* sgm = smem;  // [C] LN gamma (LDS reads do not queue behind the emission stores)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
-  bf16* sq = reinterpret_cast<bf16*>(smem + 2 * C) + wid * 16 * NV * DQLD;
-  for (int e = tid; e < C; e += 256) { sg[e] = 0.f; sgm[e] = gamma[e]; }
+  float* sg = smem + C + wid * C;
+  bf16* sq = reinterpret_cast<bf16*>(smem + 5 * C) + wid * 16 * NV * DQLD;
+  for (int e = tid; e < 4 * C; e += 256) smem[C + e] = 0.f;
+  for (int e = tid; e < C; e += 256) sgm[e] = gamma[e];
   __syncthreads();
   const int n = blockIdx.y;
   const int p0 = (blockIdx.x * 4 + wid) * 16 * NV;
@@ -900,7 +904,7 @@ __global__ __launch_bounds__(256, 2) void slab_dx_kernel(
         }
         if (lr == 0) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) atomicAdd(&sg[co + r], d4[r]);
+          for (int r = 0; r < 4; ++r) sg[co + r] += d4[r];
         }
         float dv4[4];
         load4(dy + (rb + (ok ? p : 0)) * C + co, dv4);
@@ -915,7 +919,8 @@ __global__ __launch_bounds__(256, 2) void slab_dx_kernel(
   }
   __syncthreads();
   for (int e = tid; e < C; e += 256)
-    dgamma_part[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * C + e] = sg[e];
+    dgamma_part[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * C + e] =
+        ((smem[C + e] + smem[2 * C + e]) + smem[3 * C + e]) + smem[4 * C + e];
 }
 
 __global__ __launch_bounds__(256) void slaf_sum_rows_kernel(const float* __restrict__ part, float* __restrict__ dst,
@@ -1319,7 +1324,7 @@ int cesm_slaf_bwd(const void* x, const void* dy, const float* gamma, const void*
   // NV = 16-pixel tiles per wave: 2 at C = 64, 1 at C = 128 (registers); dgp rows = grid blocks
   const int NVr = C == 64 ? 2 : 1;
   dim3 grid((unsigned)cdiv(HW, 64 * NVr), Nf);
-  const size_t sm = (size_t)C * 8 + (size_t)4 * 16 * NVr * DQLD * 2;
+  const size_t sm = (size_t)C * 20 + (size_t)4 * 16 * NVr * DQLD * 2;
   if (C == 64)
     slab_dx_kernel<64, 2><<<grid, 256, sm, stream>>>(
         (const bf16*)x, (const bf16*)dy, gamma, img_q, img_qt, img_ot, G,

@@ -1061,12 +1061,16 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
   constexpr bool DG_REG = false;  // dgamma partials flushed per pixel group (LDS atomics)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int FF = F * F;
-  float* sb = smem;                  // [8][F][F]
-  float* sdb = sb + NH * FF;         // [8][F][F] block dbias accumulator
-  float* sg = sdb + NH * FF;         // [C] block dgamma accumulator
-  float* sgm = sg + C;               // [C] LN gamma (LDS reads do not queue behind the emission stores)
-  float* rot = sgm + C;              // [16][RS]
+  // dbias / dgamma accumulators per wave ([4][8][F][F], [4][C]; one writer each, summed in a fixed order at the
+  // end, so the block partials repeat exactly — LDS float atomics across the waves did not)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  float* sb = smem;                      // [8][F][F]
+  float* sdb0 = sb + NH * FF;            // [4][8][F][F]
+  float* sg0 = sdb0 + 4 * NH * FF;       // [4][C]
+  float* sgm = sg0 + 4 * C;              // [C] LN gamma (LDS reads do not queue behind the emission stores)
+  float* rot = sgm + C;                  // [16][RS]
+  float* sdb = sdb0 + wid * NH * FF;
+  float* sg = sg0 + wid * C;
   const int lr = lane & 15, lg = lane >> 4;
   const int b = blockIdx.y;
   const int VW = T::PW * F;
@@ -1077,8 +1081,10 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
   bf16* sv = sk + R * HLD;
   bf16* sdo = sv + R * HLD;
   float* sld = reinterpret_cast<float*>(reinterpret_cast<bf16*>(rot + 16 * RS) + 4 * 4 * R * HLD) + wid * 32;
-  for (int e = tid; e < NH * FF; e += 256) { sb[e] = bias[e] * LOG2E; sdb[e] = 0.f; }
-  for (int e = tid; e < C; e += 256) { sg[e] = 0.f; sgm[e] = gamma[e]; }
+  for (int e = tid; e < NH * FF; e += 256) sb[e] = bias[e] * LOG2E;
+  for (int e = tid; e < 4 * NH * FF; e += 256) sdb0[e] = 0.f;
+  for (int e = tid; e < 4 * C; e += 256) sg0[e] = 0.f;
+  for (int e = tid; e < C; e += 256) sgm[e] = gamma[e];
   for (int e = tid; e < F * 32; e += 256) rot[(e >> 5) * RS + (e & 31)] = rotg[e];
   __syncthreads();
 
@@ -1280,7 +1286,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        if (lr < F && lg * 4 + r < F) atomicAdd(&sdb[(h * F + lr) * F + lg * 4 + r], dbr[r]);
+        if (lr < F && lg * 4 + r < F) sdb[(h * F + lr) * F + lg * 4 + r] += dbr[r];
       wave_lds_sync();
       TW_ST(3)
       // dxn^T += W_qkv[h rows]^T . [dq|dk|dv]_h^T ; emit dqkv_h
@@ -1381,7 +1387,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
           }
           if (lr == 0) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) atomicAdd(&sg[co + r], d4[r]);
+            for (int r = 0; r < 4; ++r) sg[co + r] += d4[r];
           }
         }
         float dv[4];
@@ -1405,15 +1411,18 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
         float v = dgam[ct][r];
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
-        if (lr == 0) atomicAdd(&sg[ct * 16 + lg * 4 + r], v);
+        if (lr == 0) sg[ct * 16 + lg * 4 + r] += v;
       }
   }
   __syncthreads();
-  for (int e = tid; e < NH * FF; e += 256) {
+  const int S = NH * FF;
+  for (int e = tid; e < S; e += 256) {
     const int h = e / FF, r = e - h * FF;
-    dbias_part[(((int64_t)b * NH + h) * gridDim.x + blockIdx.x) * FF + r] = sdb[e];
+    dbias_part[(((int64_t)b * NH + h) * gridDim.x + blockIdx.x) * FF + r] =
+        ((sdb0[e] + sdb0[S + e]) + sdb0[2 * S + e]) + sdb0[3 * S + e];
   }
-  for (int e = tid; e < C; e += 256) dgamma_part[((int64_t)b * gridDim.x + blockIdx.x) * C + e] = sg[e];
+  for (int e = tid; e < C; e += 256)
+    dgamma_part[((int64_t)b * gridDim.x + blockIdx.x) * C + e] = ((sg0[e] + sg0[C + e]) + sg0[2 * C + e]) + sg0[3 * C + e];
 }
 
 __global__ void tb_sum_rows_kernel(const float* __restrict__ part, float* __restrict__ dst, int nrows, int C,
@@ -1433,7 +1442,7 @@ static size_t tw_fwd_smem(int F) {  // NOLINT
 template <int C>
 static size_t tw_bwd_smem(int F) {
   const int R = ((TW<C>::PW * F + 15) / 16) * 16;
-  return (size_t)(2 * NH * F * F + 2 * C + 16 * RS) * 4 + (size_t)4 * 4 * R * HLD * 2 + 4 * 32 * 4;
+  return (size_t)(5 * NH * F * F + 5 * C + 16 * RS) * 4 + (size_t)4 * 4 * R * HLD * 2 + 4 * 32 * 4;
 }
 template <typename K>
 static void allow_smem(K kernel, size_t bytes) {

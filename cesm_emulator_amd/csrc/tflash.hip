@@ -304,14 +304,29 @@ __global__ __launch_bounds__(64 * NT) void tflash_bwd_q_kernel(
       }
     }
   }
-  // dbias partials by offset n = 16 (kt - qt) + 4g + r - lr: once per wave (LDS atomics), then the block's row
+  // dbias partials by offset n = 16 (kt - qt) + 4g + r - lr: the lanes' accumulators are staged one key tile at a
+  // time and each offset sums its contributions in a fixed (kt, qt, g, r) order, so the block's row is the same on
+  // every run (LDS float atomics over lanes and waves were not)
+  __shared__ float dstage[TF_MAXT][4][64];
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
+  for (int kt = 0; kt < NT; ++kt) {
+    __syncthreads();
 #pragma unroll
-    for (int kt = 0; kt < NT; ++kt) {
-      const int n = 16 * (kt - qt) + 4 * g + r - lr;
-      if (n > -F && n < F && dba[r][kt] != 0.f) atomicAdd(&dacc[n + F - 1], dba[r][kt]);
+    for (int r = 0; r < 4; ++r) dstage[qt][r][lane] = dba[r][kt];
+    __syncthreads();
+    for (int e = tid; e < 2 * F - 1; e += NTH) {
+      const int n = e - (F - 1);
+      float a = dacc[e];
+      for (int q = 0; q < NT; ++q)
+        for (int gg = 0; gg < 4; ++gg)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int l = 16 * (kt - q) + 4 * gg + r - n;
+            if (l >= 0 && l < 16) a += dstage[q][r][gg * 16 + l];
+          }
+      dacc[e] = a;
     }
+  }
   __syncthreads();
   for (int e = tid; e < 2 * F - 1; e += NTH)
     part[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * (2 * F - 1) + e] = dacc[e];
