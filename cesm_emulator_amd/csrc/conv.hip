@@ -636,6 +636,194 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
   }
 }
 
+
+// ----------------------------------------------------------------------------------------
+// 4x4 / stride-2 / pad-1 convs (Downsample, video_net.py:61-62) and their transposes (Upsample, :65-66;
+// each is also the other's data gradient) as halo-tiled implicit GEMMs on the low-resolution grid.  Both
+// are 3x3 stride-1 neighbourhoods in which only a 2x2 subset of the taps is live per parity:
+//   DOWN  y[oy][ox] = sum_{ky,kx} W[ky*4+kx] . x[2oy-1+ky][2ox-1+kx]; split by the input parity (a, b)
+//         (x_ab[Y][X] = x[2Y+a][2X+b]) the live taps are ky = (1-a) + 2t (t = 0, 1), read at halo row
+//         offset (1-a) + t of the (TH+2) x (TW+2) halo of x_ab around the output tile;
+//   UP    the transposed conv in its gather form (S = 1, U = 2, P = 2, taps flipped by the packing):
+//         y[2Y+py][2X+px] = sum over ky = py + 2t, kx = px + 2u of W[ky*4+kx] . x[Y-1+py+t][X-1+px+u].
+// The tap base (1-a or py) is a template parameter of the per-stage MFMA loop, so every LDS address stays
+// compile-time + lane constant as in conv3x3_bf16_kernel (same 2 x 2 wave tiling, 64 co per block, two
+// blocks per CU).  DOWN runs 4 parity stages per 32-channel chunk (consecutive stages touch the same input
+// lines); UP gives each output parity its own blocks (blockIdx.z = parity * Cout/64 + co block).  The
+// generic implicit GEMM it replaces gathered every (pixel, tap) pair from global memory, 16 K-steps of 8
+// MFMAs per wave per chunk (190-260 TF/s on the bench shapes).
+// ----------------------------------------------------------------------------------------
+template <int TW, int BY, int BX>
+__device__ __forceinline__ void s2_taps(const bf16* sh, const bf16* sw, const int (&boff)[8][3], const int (&aoff)[2],
+                                        f32x4 (&acc)[2][8]) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int oy = BY + (t >> 1), ox = BX + (t & 1);
+    bf16x8 af[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) af[i] = *reinterpret_cast<const bf16x8*>(sw + aoff[i] + t * H3_BN * H3_LD);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(sh + boff[j][ox] + oy * H3_P * H3_LD);
+      acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bfr, acc[0][j], 0, 0, 0);
+      acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bfr, acc[1][j], 0, 0, 0);
+    }
+  }
+}
+
+template <int TW, bool UP>
+__global__ __launch_bounds__(256, 2) void convs2_bf16_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                             const float* __restrict__ bias, const bf16* __restrict__ res,
+                                                             bf16* __restrict__ y, ConvGeom g, int tiles_x, int TH,
+                                                             int Hl, int Wl) {
+  __shared__ __attribute__((aligned(16))) bf16 sh[H3_NROW * H3_LD];
+  __shared__ __attribute__((aligned(16))) bf16 sw[4 * H3_BN * H3_LD];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int n = blockIdx.y;
+  const int ty = blockIdx.x / tiles_x, tx = blockIdx.x - ty * tiles_x;
+  const int y0 = ty * TH, x0 = tx * TW;  // tile origin on the low-resolution grid
+  constexpr int HWd = TW + 2;
+  const int HP = (TH + 2) * HWd;
+  const int ncob = g.Cout / H3_BN;
+  const int par = UP ? (int)blockIdx.z / ncob : 0;
+  const int n0 = ((int)blockIdx.z - par * ncob) * H3_BN;
+  const int ppy = par >> 1, ppx = par & 1;
+  const int Cin = g.C1;
+  const int nchunk = Cin / 32;
+  constexpr int WPT = 4 * H3_BN * 4 / 256;  // weight vectors per thread (4 taps x 64 co x 4 vectors)
+
+  // stage s: halo of the (parity sub-)image and the 4 live taps' weights for one 32-channel chunk
+  auto stage = [&](int ch, int a, int b, int by, int bx) {
+    const int c0 = ch * 32;
+    bf16x8 hreg[H3_HPT], wreg[WPT];
+#pragma unroll
+    for (int k = 0; k < H3_HPT; ++k) {
+      const int e = tid + k * 256;
+      bf16x8 v = {};
+      if (e < HP * 4) {
+        const int hp = e >> 2, part = e & 3;
+        const int r = hp / HWd, c = hp - r * HWd;
+        const int Y = y0 - 1 + r, X = x0 - 1 + c;
+        const int iy = UP ? Y : 2 * Y + a, ix = UP ? X : 2 * X + b;
+        if ((unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi)
+          v = *reinterpret_cast<const bf16x8*>(x + (((int64_t)n * g.Hi + iy) * g.Wi + ix) * Cin + c0 + part * 8);
+      }
+      hreg[k] = v;
+    }
+#pragma unroll
+    for (int k = 0; k < WPT; ++k) {
+      const int e = tid + k * 256;
+      const int row = e >> 2, part = e & 3;  // row = t * 64 + co
+      const int t = row / H3_BN, co = row - t * H3_BN;
+      const int tap = (by + 2 * (t >> 1)) * 4 + bx + 2 * (t & 1);
+      wreg[k] = *reinterpret_cast<const bf16x8*>(w + ((int64_t)(n0 + co) * 16 + tap) * Cin + c0 + part * 8);
+    }
+#pragma unroll
+    for (int k = 0; k < H3_HPT; ++k) {
+      const int e = tid + k * 256;
+      if (e < HP * 4) {
+        const int hp = e >> 2, r = hp / HWd, c = hp - r * HWd;
+        *reinterpret_cast<bf16x8*>(sh + h3_off(r * H3_P + c, e & 3)) = hreg[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < WPT; ++k) {
+      const int e = tid + k * 256;
+      *reinterpret_cast<bf16x8*>(sw + h3_off(e >> 2, e & 3)) = wreg[k];
+    }
+  };
+
+  f32x4 acc[2][8];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int lr = lane & 15, lg = lane >> 4;
+  int hoff[8], pyx[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int p = wc * 128 + j * 16 + lr;
+    const int py = p / TW, px = p - py * TW;
+    const bool in = py < TH;
+    hoff[j] = in ? py * H3_P + px : 0;
+    pyx[j] = in ? (py << 16) | px : -1;
+  }
+  int boff[8][3], aoff[2];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) boff[j][kx] = h3_off(hoff[j] + kx, lg);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) aoff[i] = h3_off(wr * 32 + i * 16 + lr, lg);
+
+  if constexpr (UP) {
+    for (int ch = 0; ch < nchunk; ++ch) {
+      if (ch) __syncthreads();  // previous chunk fully consumed
+      stage(ch, 0, 0, ppy, ppx);
+      __syncthreads();
+      switch (par) {  // block-uniform
+        case 0: s2_taps<TW, 0, 0>(sh, sw, boff, aoff, acc); break;
+        case 1: s2_taps<TW, 0, 1>(sh, sw, boff, aoff, acc); break;
+        case 2: s2_taps<TW, 1, 0>(sh, sw, boff, aoff, acc); break;
+        default: s2_taps<TW, 1, 1>(sh, sw, boff, aoff, acc); break;
+      }
+    }
+  } else {
+    for (int ch = 0; ch < nchunk; ++ch) {
+#pragma unroll
+      for (int ab = 0; ab < 4; ++ab) {
+        const int a = ab >> 1, b = ab & 1;
+        if (ch || ab) __syncthreads();
+        stage(ch, a, b, 1 - a, 1 - b);
+        __syncthreads();
+        if (ab == 0) s2_taps<TW, 1, 1>(sh, sw, boff, aoff, acc);       // a = 0, b = 0
+        else if (ab == 1) s2_taps<TW, 1, 0>(sh, sw, boff, aoff, acc);  // a = 0, b = 1
+        else if (ab == 2) s2_taps<TW, 0, 1>(sh, sw, boff, aoff, acc);  // a = 1, b = 0
+        else s2_taps<TW, 0, 0>(sh, sw, boff, aoff, acc);                // a = 1, b = 1
+      }
+    }
+  }
+  // epilogue: lane holds co = n0 + wr*32 + i*16 + 4*lg + r of tile pixel (py, px)
+  float bv[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) epi_bias(bias, n0 + wr * 32 + i * 16 + lg * 4, bv[i]);
+  int64_t mj[8];
+  bool okj[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int Y = y0 + (pyx[j] >> 16), X = x0 + (pyx[j] & 0xffff);
+    okj[j] = pyx[j] >= 0 && Y < Hl && X < Wl;
+    const int oy = UP ? 2 * Y + ppy : Y, ox = UP ? 2 * X + ppx : X;
+    mj[j] = okj[j] ? ((int64_t)n * g.Ho + oy) * g.Wo + ox : 0;
+  }
+  bf16x4 rv[8][2];
+  if (res) {  // uniform
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) rv[j][i] = epi_res(res, nullptr, mj[j], n0 + wr * 32 + i * 16 + lg * 4, g.Cout, 0, okj[j]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) rv[j][i] = bf16x4{};
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (!okj[j]) continue;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int co = n0 + wr * 32 + i * 16 + lg * 4;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bv[i][r] + b2f(rv[j][i], r);
+      store4(y + mj[j] * g.Cout + co, v);
+    }
+  }
+}
+
 // ----------------------------------------------------------------------------------------
 // 3x3 / stride 1 / pad 1 conv (bf16), v3 "wide wave": block = TH x TW (<= 512) output pixels of one
 // image x 64 output channels; 4 waves, wave w owns tile pixels [128w, 128w + 128) (8 fragment groups
@@ -2695,7 +2883,7 @@ enum ConvFwdVariant {
   CFV_INVALID = -1,
   CFV_GEMM1X1_128 = 0, CFV_GEMM1X1_64, CFV_P36_RW, CFV_P36, CFV_P32_3STAGE, CFV_P32_RW, CFV_P32, CFV_W36, CFV_W32,
   CFV_V2, CFV_HALO36, CFV_HALO32, CFV_TCONV_PAR_128, CFV_TCONV_PAR_64, CFV_GEN_BF16_128, CFV_GEN_BF16_64,
-  CFV_GEN_F32_128, CFV_GEN_F32_64, CFV_COUNT
+  CFV_GEN_F32_128, CFV_GEN_F32_64, CFV_S2DOWN36, CFV_S2DOWN32, CFV_S2UP36, CFV_S2UP32, CFV_COUNT
 };
 static const char* const kConvFwdVariantName[CFV_COUNT] = {
     "gemm1x1_kernel<128>", "gemm1x1_kernel<64>", "conv3x3p_kernel<36,8,true>", "conv3x3p_kernel<36,8,false>",
@@ -2703,7 +2891,8 @@ static const char* const kConvFwdVariantName[CFV_COUNT] = {
     "conv3x3w_kernel<36>", "conv3x3w_kernel<32>", "conv3x3v2_kernel", "conv3x3_bf16_kernel<36>",
     "conv3x3_bf16_kernel<32>", "conv_fwd_bf16_kernel<128,true>", "conv_fwd_bf16_kernel<64,true>",
     "conv_fwd_bf16_kernel<128>", "conv_fwd_bf16_kernel<64>", "conv_fwd_kernel<float,128>",
-    "conv_fwd_kernel<float,64>"};
+    "conv_fwd_kernel<float,64>", "convs2_bf16_kernel<36,down>", "convs2_bf16_kernel<32,down>",
+    "convs2_bf16_kernel<36,up>", "convs2_bf16_kernel<32,up>"};
 
 struct ConvFwdPlan {
   ConvFwdVariant v = CFV_INVALID;
@@ -2755,6 +2944,16 @@ static ConvFwdPlan conv_fwd_plan(int dtype, int Nb, int Hi, int Wi, int C1, int 
     pl.TH = H3_TH; pl.TW = H3_TW;
     if (!getenv_flag("CESM_CONV3X3_FIXED_TILE")) c2_tile(Ho, Wo, pl.TH, pl.TW, true);
     pl.v = pl.TW == 36 ? CFV_HALO36 : CFV_HALO32;
+  } else if (dtype == CESM_DT_BF16 && KH == 4 && KW == 4 && C2 == 0 && Co1 == Cout && (Cout % H3_BN) == 0 &&
+             !getenv_flag("CESM_NO_S2HALO") &&
+             ((S == 2 && P == 1 && U == 1 && Hi == 2 * Ho && Wi == 2 * Wo) ||
+              (S == 1 && P == 2 && U == 2 && Ho == 2 * Hi && Wo == 2 * Wi))) {
+    // stride-2 4x4 conv / its transpose: halo kernel on the low-resolution grid
+    const bool up = U == 2;
+    const int Hl = up ? Hi : Ho, Wl = up ? Wi : Wo;
+    pl.TH = H3_TH; pl.TW = H3_TW;
+    c2_tile(Hl, Wl, pl.TH, pl.TW, true);
+    pl.v = up ? (pl.TW == 36 ? CFV_S2UP36 : CFV_S2UP32) : (pl.TW == 36 ? CFV_S2DOWN36 : CFV_S2DOWN32);
   } else if (dtype == CESM_DT_BF16 && U == 2 && S == 1 && KH % 2 == 0 && KW % 2 == 0 && Ho % 2 == 0 &&
              Wo % 2 == 0 && !getenv_flag("CESM_NO_PARITY_TCONV")) {
     pl.v = BN == 128 ? CFV_TCONV_PAR_128 : CFV_TCONV_PAR_64;
@@ -2865,6 +3064,24 @@ int cesm_conv_fwd(int dtype, const void* x1, const void* x2, const void* wp, con
         conv3x3_bf16_kernel<36><<<g3, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, TH);
       else
         conv3x3_bf16_kernel<32><<<g3, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, TH);
+      break;
+    }
+    case CFV_S2DOWN36:
+    case CFV_S2DOWN32:
+    case CFV_S2UP36:
+    case CFV_S2UP32: {
+      const bool up = pl.v == CFV_S2UP36 || pl.v == CFV_S2UP32;
+      const int Hl = up ? Hi : Ho, Wl = up ? Wi : Wo;
+      const int tx = (int)cdiv(Wl, TW), ty = (int)cdiv(Hl, TH);
+      dim3 g3(tx * ty, Nb, (Cout / H3_BN) * (up ? 4 : 1));
+      if (pl.v == CFV_S2DOWN36)
+        convs2_bf16_kernel<36, false><<<g3, 256, 0, stream>>>(bx1, bwp, bias, br, by1, g, tx, TH, Hl, Wl);
+      else if (pl.v == CFV_S2DOWN32)
+        convs2_bf16_kernel<32, false><<<g3, 256, 0, stream>>>(bx1, bwp, bias, br, by1, g, tx, TH, Hl, Wl);
+      else if (pl.v == CFV_S2UP36)
+        convs2_bf16_kernel<36, true><<<g3, 256, 0, stream>>>(bx1, bwp, bias, br, by1, g, tx, TH, Hl, Wl);
+      else
+        convs2_bf16_kernel<32, true><<<g3, 256, 0, stream>>>(bx1, bwp, bias, br, by1, g, tx, TH, Hl, Wl);
       break;
     }
     case CFV_TCONV_PAR_128:

@@ -107,6 +107,50 @@ def test_conv3x3p_level0_bf16(dev, H, W, with_res):
     assert e_fwd < 1e-2 and e_dx < 1e-2 and e_dw < 1e-2 and e_db < 1e-2
 
 
+# ------------------------------------------------------------------ Down / Upsample (A13)
+@pytest.mark.parametrize("kind", ["down", "up"])
+@pytest.mark.parametrize("C,H,W", [(64, 96, 144), (128, 26, 38), (256, 48, 72), (64, 18, 22)])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_stride2_conv_halo_bf16(dev, kind, C, H, W, with_res):
+    """convs2_bf16_kernel (4x4 / stride-2 / pad-1 conv and its transpose on the low-resolution grid, halo
+    tiled; each is the other's data gradient): forward, dgrad (with the fused skip-gradient residual the
+    Downsample backward uses, video_net.py:767) and the weight gradient vs float64 on bf16-rounded operands.
+    (H, W) is the high-resolution grid; widths that take 36- and 32-wide tiles and partial tiles."""
+    B, Fr = 1, 2
+    Hl, Wl = H // 2, W // 2
+    if kind == "down":
+        mod = nn.Conv3d(C, C, (1, 4, 4), (1, 2, 2), (0, 1, 1))
+        xin = torch.randn(B, C, Fr, H, W)
+        assert K.conv_fwd_variant(BF, B * Fr, H, W, C, 0, Hl, Wl, C, C, 4, 4, 2, 1, 1).startswith("convs2_bf16_kernel")
+    else:
+        mod = nn.ConvTranspose3d(C, C, (1, 4, 4), (1, 2, 2), (0, 1, 1))
+        xin = torch.randn(B, C, Fr, Hl, Wl)
+        assert K.conv_fwd_variant(BF, B * Fr, Hl, Wl, C, 0, H, W, C, C, 4, 4, 1, 2, 2).startswith("convs2_bf16_kernel")
+    torch.manual_seed(C + H)
+    md = type(mod)(C, C, (1, 4, 4), (1, 2, 2), (0, 1, 1)).to(dev)
+    md.load_state_dict(mod.state_dict())
+    rc = VN.RunCtx(_PackHost(), B, Fr, BF, True)
+    spec = VN.ConvSpec(md)
+    res = torch.randn(B, C, Fr, *((Hl, Wl) if kind == "down" else (H, W))) if with_res else None
+    y, st = VN.conv_forward(rc, spec, to_cl(xin).to(dev, BF), res=None if res is None else to_cl(res).to(dev, BF))
+    xr = q(xin).requires_grad_(True)
+    wr = mod.weight.detach().to(BF).double().requires_grad_(True)
+    br = mod.bias.detach().double().requires_grad_(True)
+    fn = F.conv3d if kind == "down" else F.conv_transpose3d
+    yr = fn(xr, wr, br, (1, 2, 2), (0, 1, 1))
+    e_fwd = rel(from_cl(y, B), yr + q(res) if with_res else yr)
+    g = torch.randn_like(yr)
+    yr.backward(q(g))
+    dres = torch.randn(*xin.shape) if with_res else None
+    dx = VN.conv_backward(rc, spec, st, to_cl(g.float()).to(dev, BF), True,
+                          None if dres is None else to_cl(dres).to(dev, BF))
+    torch.cuda.synchronize()
+    e_dx = rel(from_cl(dx, B), xr.grad + q(dres) if with_res else xr.grad)
+    e_dw, e_db = rel(md.weight.grad, wr.grad), rel(md.bias.grad, br.grad)
+    print(f"{kind} C={C} {H}x{W} res={with_res}: fwd {e_fwd:.2e} dx {e_dx:.2e} dw {e_dw:.2e} db {e_db:.2e}")
+    assert e_fwd < 1e-2 and e_dx < 1e-2 and e_dw < 1e-2 and e_db < 1e-2
+
+
 # ------------------------------------------------------------------ whole network, bf16 (A3, A9-A14)
 def _pair(mults, seed=1):
     torch.manual_seed(seed)

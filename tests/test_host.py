@@ -154,8 +154,11 @@ def test_bench_shape_dispatch_table():
     assert wv(192, 288, 256, 0, 192, 288, 64, 64, 1, 1, 1, 0, 1, with_bias=True) == "wgrad_wide_kernel<64,true>"
     # 1x1 res_conv / to_qkv GEMMs, down- and up-sampling
     assert fv(192, 288, 64, 0, 192, 288, 768, 768, 1, 1, 1, 0, 1) == "gemm1x1_kernel<128>"
-    assert fv(192, 288, 64, 0, 96, 144, 64, 64, 4, 4, 2, 1, 1) == "conv_fwd_bf16_kernel<64>"
-    assert fv(96, 144, 64, 0, 192, 288, 64, 64, 4, 4, 1, 2, 2) == "conv_fwd_bf16_kernel<64,true>"
+    # down / up (4x4 stride 2 and its transpose; tile width chosen on the low-resolution grid)
+    assert fv(192, 288, 64, 0, 96, 144, 64, 64, 4, 4, 2, 1, 1) == "convs2_bf16_kernel<32,down>"
+    assert fv(96, 144, 64, 0, 192, 288, 64, 64, 4, 4, 1, 2, 2) == "convs2_bf16_kernel<32,up>"
+    assert fv(96, 144, 128, 0, 48, 72, 128, 128, 4, 4, 2, 1, 1) == "convs2_bf16_kernel<36,down>"
+    assert fv(24, 36, 256, 0, 48, 72, 256, 256, 4, 4, 1, 2, 2) == "convs2_bf16_kernel<36,up>"
     # fp32 parity mode: the generic kernels
     assert K.conv_fwd_variant(torch.float32, N, 192, 288, 64, 0, 192, 288, 64, 64, 3, 3, 1, 1, 1) == \
         "conv_fwd_kernel<float,64>"
