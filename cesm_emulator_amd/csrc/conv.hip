@@ -2217,6 +2217,147 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_bf16_kernel(const bf16* __res
     }
 }
 
+// Weight gradient of the 4x4 / stride-2 / pad-1 conv (Downsample; the Upsample's weight gradient is the same
+// operation with dOut as the input and x as dY), halo-tiled like wgrad3x3_bf16_kernel on the low-resolution
+// dY grid.  Block = (64 co) x (32 ci chunk) x one input parity (a, b) = its 4 live taps ky = (1-a) + 2t,
+// kx = (1-b) + 2u, whose inputs are the (TH+2) x (TW+2) halo of x_ab[Y][X] = x[2Y+a][2X+b] at offsets
+// (1-a+t, 1-b+u) - the forward's parity split (convs2_bf16_kernel).  Replaces the wide-tile wgrad, which
+// gathered every (pixel, tap) pair (315 TF/s on the bench shapes).
+template <int BY, int BX>
+__device__ __forceinline__ void ws2_taps(const bf16* sdy, const bf16* shx, const int (&aoff)[2][2],
+                                         const int (&boff)[2][3], f32x4 (&acc)[2][4]) {
+#pragma unroll 1
+  for (int py = 0; py < W3_TH; ++py) {
+    bf16x8 af[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(sdy + aoff[i][half] + py * 32 * 64));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) af[i][half * 4 + e] = __builtin_bit_cast(bf16, (short)v[e]);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int oy = BY + (t >> 1), ox = BX + (t & 1);
+      bf16x8 bfr;
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const s16x4 v =
+            __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(shx + boff[half][ox] + (py + oy) * W3_P * 32));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bfr[half * 4 + e] = __builtin_bit_cast(bf16, (short)v[e]);
+      }
+      acc[0][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bfr, acc[0][t], 0, 0, 0);
+      acc[1][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bfr, acc[1][t], 0, 0, 0);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void wgrads2_bf16_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                              float* __restrict__ slab, ConvGeom g, int tiles_x,
+                                                              int ntiles) {
+  __shared__ __attribute__((aligned(16))) bf16 sdy[W3_TH * W3_TW * 64];        // 32 KB, 128-B rows
+  __shared__ __attribute__((aligned(16))) bf16 shx[(W3_TH + 2) * W3_P * 32];  // 30 KB, 64-B rows
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int cot0 = (wid >> 1) * 2, cit = wid & 1;
+  const int co0 = blockIdx.x * 64;
+  const int ab = (int)blockIdx.y & 3, a = ab >> 1, b = ab & 1;
+  const int ci0 = ((int)blockIdx.y >> 2) * 32;
+  const int Cin = g.C1;
+  const int tiles_per_img = tiles_x * ((g.Ho + W3_TH - 1) / W3_TH);
+
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int lr = lane & 15, lg = lane >> 4, q = lr >> 2, pp = lr & 3;
+  int aoff[2][2], boff[2][3];
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const int r = lg * 8 + half * 4 + q;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) aoff[i][half] = r * 64 + ((((cot0 + i) * 4 + pp) ^ w3_swz_dy(r)) * 4);
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) boff[half][kx] = (r + kx) * 32 + (((cit * 4 + pp) ^ w3_swz_x(r + kx)) * 4);
+  }
+  for (int tile = blockIdx.z; tile < ntiles; tile += gridDim.z) {
+    const int n = tile / tiles_per_img;
+    const int rem = tile - n * tiles_per_img;
+    const int ty = rem / tiles_x, tx = rem - ty * tiles_x;
+    const int y0 = ty * W3_TH, x0 = tx * W3_TW;
+    __syncthreads();
+    {
+      bf16x8 yv[8], hv[6];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {  // dY: 256 px x 8 vectors
+        const int e = tid + k * 256;
+        const int p = e >> 3, part = e & 7;
+        const int oy = y0 + (p >> 5), ox = x0 + (p & 31);
+        bf16x8 v = {};
+        if (oy < g.Ho && ox < g.Wo)
+          v = *reinterpret_cast<const bf16x8*>(dy + (((int64_t)n * g.Ho + oy) * g.Wo + ox) * g.Cout + co0 + part * 8);
+        yv[k] = v;
+      }
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {  // halo of x_ab: 340 px x 4 vectors
+        const int e = tid + k * 256;
+        bf16x8 v = {};
+        if (e < W3_NPIX * 4) {
+          const int hp = e >> 2, part = e & 3;
+          const int r = hp / W3_HW, c = hp - r * W3_HW;
+          const int iy = 2 * (y0 - 1 + r) + a, ix = 2 * (x0 - 1 + c) + b;
+          if ((unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi)
+            v = *reinterpret_cast<const bf16x8*>(x + (((int64_t)n * g.Hi + iy) * g.Wi + ix) * Cin + ci0 + part * 8);
+        }
+        hv[k] = v;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int e = tid + k * 256;
+        const int p = e >> 3, part = e & 7;
+        const int ch = (part * 2) ^ w3_swz_dy(p);
+        *reinterpret_cast<bf16x8*>(sdy + p * 64 + ch * 4) = yv[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const int e = tid + k * 256;
+        if (e < W3_NPIX * 4) {
+          const int hp = e >> 2, part = e & 3;
+          const int r = hp / W3_HW, row = r * W3_P + (hp - r * W3_HW);
+          const int ch = (part * 2) ^ w3_swz_x(row);
+          *reinterpret_cast<bf16x8*>(shx + row * 32 + ch * 4) = hv[k];
+        }
+      }
+    }
+    __syncthreads();
+    switch (ab) {  // block-uniform: tap bases 1-a, 1-b
+      case 0: ws2_taps<1, 1>(sdy, shx, aoff, boff, acc); break;
+      case 1: ws2_taps<1, 0>(sdy, shx, aoff, boff, acc); break;
+      case 2: ws2_taps<0, 1>(sdy, shx, aoff, boff, acc); break;
+      default: ws2_taps<0, 0>(sdy, shx, aoff, boff, acc); break;
+    }
+  }
+  // D[co][ci] per tap: lane col lr -> ci, rows 4lg+r -> co; tap = ky*4 + kx
+  const int K = 16 * Cin;
+  float* out = slab + (int64_t)blockIdx.z * g.Cout * K;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int tap = (1 - a + 2 * (t >> 1)) * 4 + (1 - b + 2 * (t & 1));
+      const int ci = ci0 + cit * 16 + lr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + (cot0 + i) * 16 + lg * 4 + r;
+        out[(int64_t)co * K + tap * Cin + ci] = acc[i][t][r];
+      }
+    }
+}
+
 // Same weight gradient on 8 x 36 pixel tiles (288 px = 9 K-chunks of 32 flat pixels): every U-Net
 // level's width (288/144/72/36) is a multiple of 36, so no tile column is wasted (the 8 x 32 tiles
 // above compute 36-px rows as two 32-px tiles: 56 % useful at 24 x 36).  A K-chunk may span two
@@ -3121,7 +3262,7 @@ int cesm_conv_fwd(int dtype, const void* x1, const void* x2, const void* wp, con
 
 namespace {
 // Kernel selection of cesm_conv_wgrad (host only)
-enum WgradVariant { WGV_W36 = 0, WGV_W32, WGV_WIDE, WGV_GEN };
+enum WgradVariant { WGV_W36 = 0, WGV_W32, WGV_WIDE, WGV_GEN, WGV_S2 };
 static int wgrad_plan(int dtype, int64_t M, int Hi, int Wi, int Ho, int Wo, int KH, int KW, int S, int P, int U) {
   const bool halo3 = dtype == CESM_DT_BF16 && KH == 3 && KW == 3 && S == 1 && P == 1 && U == 1 && Ho == Hi &&
                      Wo == Wi && !getenv_flag("CESM_NO_HALO");
@@ -3130,6 +3271,10 @@ static int wgrad_plan(int dtype, int64_t M, int Hi, int Wi, int Ho, int Wo, int 
   if (halo3 && (Wo % W36_TW) == 0 && 5 * Wo <= 4 * (int)cdiv(Wo, W3_TW) * W3_TW && !getenv_flag("CESM_NO_WGRAD36"))
     return WGV_W36;
   if (halo3) return WGV_W32;
+  // (32-wide pixel tiles: at Wo = 36 the second tile of a row is 8/9 empty and the wide kernel is faster)
+  if (dtype == CESM_DT_BF16 && KH == 4 && KW == 4 && S == 2 && P == 1 && U == 1 && Hi == 2 * Ho && Wi == 2 * Wo &&
+      Wo >= 64 && !getenv_flag("CESM_NO_S2HALO"))
+    return WGV_S2;
   if (dtype == CESM_DT_BF16 && M < (1ll << 31) && !getenv_flag("CESM_NO_WIDE_WGRAD")) return WGV_WIDE;
   return WGV_GEN;
 }
@@ -3140,9 +3285,12 @@ extern "C" {
 const char* cesm_conv_wgrad_variant(int dtype, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout,
                                     int Co1, int KH, int KW, int S, int P, int U, int with_bias) {
   const int64_t M = (int64_t)Nb * Ho * Wo;
-  switch (wgrad_plan(dtype, M, Hi, Wi, Ho, Wo, KH, KW, S, P, U)) {
+  int wv = wgrad_plan(dtype, M, Hi, Wi, Ho, Wo, KH, KW, S, P, U);
+  if (wv == WGV_S2 && (with_bias || C2 || Co1 != Cout)) wv = WGV_WIDE;  // (cesm_conv_wgrad's fallback)
+  switch (wv) {
     case WGV_W36: return "wgrad3x3w36_kernel";
     case WGV_W32: return "wgrad3x3_bf16_kernel";
+    case WGV_S2: return "wgrads2_bf16_kernel";
     case WGV_WIDE: {
       const int bm = (Cout % 256 == 0 && Co1 % 256 == 0) ? 256 : ((Cout % 128 == 0 && Co1 % 128 == 0) ? 128 : 64);
       static const char* const names[6] = {"wgrad_wide_kernel<64,false>", "wgrad_wide_kernel<64,true>",
@@ -3185,7 +3333,13 @@ int cesm_conv_wgrad(int dtype, const void* x1, const void* x2, const void* dy1, 
     wgrad3x3_bf16_kernel<<<g3, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
                                                  (const bf16*)dy2, slab, g, tx, ntiles);
     nsplit = (int)g3.z;
-  } else if (wv == WGV_WIDE) {
+  } else if (wv == WGV_S2 && C2 == 0 && Co1 == Cout && !db) {
+    const int tx = (int)cdiv(Wo, W3_TW);
+    const int ntiles = Nb * tx * (int)cdiv(Ho, W3_TH);
+    dim3 g3(Cout / 64, (Cin / 32) * 4, std::min(nsplit, ntiles));
+    wgrads2_bf16_kernel<<<g3, 256, 0, stream>>>((const bf16*)x1, (const bf16*)dy1, slab, g, tx, ntiles);
+    nsplit = (int)g3.z;
+  } else if (wv == WGV_WIDE || wv == WGV_S2) {
     // wide-tile kernel; nsplit from the caller sized the slab for 64-row tiles, keep it
     const int bm = (Cout % 256 == 0 && Co1 % 256 == 0) ? 256 : ((Cout % 128 == 0 && Co1 % 128 == 0) ? 128 : 64);
     dim3 gw(Cout / bm, K / 64, nsplit);

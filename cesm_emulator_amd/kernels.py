@@ -133,10 +133,15 @@ def conv_wgrad(x1, x2, dy1, dy2, dw, geom, swap, flip, accumulate=True, db=None)
     K = KH * KW * (C1 + C2)
     M = Nb * Ho * Wo
     halo3 = KH == 3 and KW == 3 and St == 1 and Pd == 1 and U == 1
-    if halo3 and x1.dtype == torch.bfloat16:
-        # wgrad3x3 kernel: blocks of 64 co x 32 ci (all 9 taps), split over pixel tiles
+    # 4x4 stride-2 (Downsample / the Upsample's weight gradient): wgrads2 kernel, blocks of 64 co x 32 ci x one
+    # input parity (4 taps); its bias gradient is the caller's column sum (same condition as cesm_conv_wgrad)
+    s2 = (KH == 4 and KW == 4 and St == 2 and Pd == 1 and U == 1 and Hi == 2 * Ho and Wi == 2 * Wo and Wo >= 64
+          and x2 is None
+          and dy2 is None and x1.dtype == torch.bfloat16 and os.environ.get("CESM_NO_S2HALO", "0") in ("", "0"))
+    if (halo3 or s2) and x1.dtype == torch.bfloat16:
+        # halo wgrad kernels: blocks of 64 co x 32 ci (all 9 taps / one parity's 4), split over pixel tiles
         nb = WGRAD_BLOCKS // 2
-        nsplit = max(1, min(nb // max(1, (Cout // 64) * ((C1 + C2) // 32)), max(1, M // 256)))
+        nsplit = max(1, min(nb // max(1, (Cout // 64) * ((C1 + C2) // 32) * (4 if s2 else 1)), max(1, M // 256)))
     else:
         bm = _wgrad_bm(x1, Cout, Co1)
         nsplit = _wgrad_nsplit(M, Cout, K, bm, WGRAD_BLOCKS // 2 if bm == 256 else WGRAD_BLOCKS)
@@ -144,7 +149,7 @@ def conv_wgrad(x1, x2, dy1, dy2, dw, geom, swap, flip, accumulate=True, db=None)
     if CONV_TRACE is not None:
         CONV_TRACE.append(("wgrad", Nb, Hi, Wi, C1 + C2, Ho, Wo, Cout, KH, KW, St, Pd, U))
     # the bias rides on the wide-tile kernel only (same dispatch condition as cesm_conv_wgrad)
-    wide = (x1.dtype == torch.bfloat16 and not halo3 and M < (1 << 31) and dy2 is None
+    wide = (x1.dtype == torch.bfloat16 and not halo3 and not s2 and M < (1 << 31) and dy2 is None
             and os.environ.get("CESM_NO_WIDE_WGRAD", "0") in ("", "0") and FUSED_BIAS_GRAD)
     if db is not None and wide:
         _chk(db, (Cout,), torch.float32)

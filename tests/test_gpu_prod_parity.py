@@ -109,7 +109,7 @@ def test_conv3x3p_level0_bf16(dev, H, W, with_res):
 
 # ------------------------------------------------------------------ Down / Upsample (A13)
 @pytest.mark.parametrize("kind", ["down", "up"])
-@pytest.mark.parametrize("C,H,W", [(64, 96, 144), (128, 26, 38), (256, 48, 72), (64, 18, 22)])
+@pytest.mark.parametrize("C,H,W", [(64, 96, 144), (128, 26, 38), (256, 48, 72), (64, 18, 22), (64, 130, 160)])
 @pytest.mark.parametrize("with_res", [False, True])
 def test_stride2_conv_halo_bf16(dev, kind, C, H, W, with_res):
     """convs2_bf16_kernel (4x4 / stride-2 / pad-1 conv and its transpose on the low-resolution grid, halo
@@ -126,6 +126,8 @@ def test_stride2_conv_halo_bf16(dev, kind, C, H, W, with_res):
         mod = nn.ConvTranspose3d(C, C, (1, 4, 4), (1, 2, 2), (0, 1, 1))
         xin = torch.randn(B, C, Fr, Hl, Wl)
         assert K.conv_fwd_variant(BF, B * Fr, Hl, Wl, C, 0, H, W, C, C, 4, 4, 1, 2, 2).startswith("convs2_bf16_kernel")
+    wv = K.conv_wgrad_variant(BF, B * Fr, H, W, C, 0, Hl, Wl, C, C, 4, 4, 2, 1, 1)
+    assert wv == ("wgrads2_bf16_kernel" if Wl >= 64 else "wgrad_wide_kernel<%d,false>" % min(C, 256))
     torch.manual_seed(C + H)
     md = type(mod)(C, C, (1, 4, 4), (1, 2, 2), (0, 1, 1)).to(dev)
     md.load_state_dict(mod.state_dict())

@@ -159,6 +159,9 @@ def test_bench_shape_dispatch_table():
     assert fv(96, 144, 64, 0, 192, 288, 64, 64, 4, 4, 1, 2, 2) == "convs2_bf16_kernel<32,up>"
     assert fv(96, 144, 128, 0, 48, 72, 128, 128, 4, 4, 2, 1, 1) == "convs2_bf16_kernel<36,down>"
     assert fv(24, 36, 256, 0, 48, 72, 256, 256, 4, 4, 1, 2, 2) == "convs2_bf16_kernel<36,up>"
+    assert wv(192, 288, 64, 0, 96, 144, 64, 64, 4, 4, 2, 1, 1) == "wgrads2_bf16_kernel"
+    assert wv(192, 288, 64, 0, 96, 144, 64, 64, 4, 4, 2, 1, 1, with_bias=True) == "wgrad_wide_kernel<64,true>"
+    assert wv(48, 72, 256, 0, 24, 36, 256, 256, 4, 4, 2, 1, 1) == "wgrad_wide_kernel<256,false>"
     # fp32 parity mode: the generic kernels
     assert K.conv_fwd_variant(torch.float32, N, 192, 288, 64, 0, 192, 288, 64, 64, 3, 3, 1, 1, 1) == \
         "conv_fwd_kernel<float,64>"

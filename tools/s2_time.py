@@ -35,11 +35,15 @@ def main():
         wu = K.conv_pack(w, torch.bfloat16, C, C, 4, 4, 1, 1)
         t_d = timed(lambda: K.conv_fwd(x, None, wd, None, (Hl, Wl, C, 4, 4, 2, 1, 1)))
         t_u = timed(lambda: K.conv_fwd(xl, None, wu, None, (H, W, C, 4, 4, 1, 2, 2)))
+        yl = torch.randn(N, Hl, Wl, C, device=dev).to(torch.bfloat16)
+        dw = torch.zeros(C, C, 1, 4, 4, device=dev)
+        t_w = timed(lambda: K.conv_wgrad(x, None, yl, None, dw, (Hl, Wl, C, 4, 4, 2, 1, 1), 0, 0))
         fl = 2 * 16 * C * C * N * Hl * Wl
-        tot += t_d + t_u
+        print(f"{tag} {H}x{W}x{C}: wgrad {t_w:.1f} us ({fl / t_w / 1e6:.0f} TF/s)", flush=True)
+        tot += t_d + t_u + t_w
         print(f"{tag} {H}x{W}x{C}: down {t_d:.1f} us ({fl / t_d / 1e6:.0f} TF/s), up {t_u:.1f} us "
               f"({fl / t_u / 1e6:.0f} TF/s)", flush=True)
-    print(f"{tag} total {tot:.1f} us (x2 per step: fwd + dgrad of each)")
+    print(f"{tag} total {tot:.1f} us (per step: x2 for down/up, x2 wgrad)")
 
 
 if __name__ == "__main__":
