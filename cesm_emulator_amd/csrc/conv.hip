@@ -2669,29 +2669,21 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(const float* __restrict__
 // Wave w owns tile rows 4w..4w+3 (4 fragment groups of 16 px) x 64 co; B fragments are gathered
 // straight from the LDS halo (8 taps per lane, converted to bf16), A fragments from the LDS weights.
 // Replaces one LDS read per FMA of the VALU kernel (6272 per pixel) with ~100 per pixel.
+// Persistent over tiles (round 2): the 64 x 98 weight is staged and converted to A fragments once per block
+// (it was once per 256-pixel tile, which dominated: 1.13 ms per level-0 launch), then the block loops over its
+// tiles (tile = blockIdx.x + k * gridDim.x) with the fragments in registers.
 __global__ __launch_bounds__(256) void stem_fwd_mfma_kernel(const float* __restrict__ xt, const float* __restrict__ cond,
                                                             const float* __restrict__ w, const float* __restrict__ bias,
                                                             bf16* __restrict__ y, int B, int F, int Fx, int Fc, int H,
-                                                            int W, int Co, int KS) {
+                                                            int W, int Co, int KS, int ntiles) {
   constexpr int TS = 16, TWM = 22;  // tile and max halo width (KS <= 7)
   __shared__ float tin[2][TWM * TWM];
   __shared__ float tw[64 * 128];    // W[co][k], k padded to 128 with zeros
   const int PAD = KS / 2, TW = TS + KS - 1, KK = KS * KS;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
-  const int n = blockIdx.z;
-  const int b = n / F, f = n - b * F;
-  const int ty0 = (blockIdx.x / ((W + TS - 1) / TS)) * TS;
-  const int tx0 = (blockIdx.x % ((W + TS - 1) / TS)) * TS;
   const int cog = blockIdx.y * 64;
-  const float* s0 = xt + ((int64_t)b * Fx + (Fx == 1 ? 0 : f)) * H * W;
-  const float* s1 = cond + ((int64_t)b * Fc + (Fc == 1 ? 0 : f)) * H * W;
-  for (int e = tid; e < TW * TW; e += 256) {
-    const int yy = ty0 - PAD + e / TW, xx = tx0 - PAD + e % TW;
-    const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
-    tin[0][(e / TW) * TWM + e % TW] = ok ? s0[(int64_t)yy * W + xx] : 0.f;
-    tin[1][(e / TW) * TWM + e % TW] = ok ? s1[(int64_t)yy * W + xx] : 0.f;
-  }
+  const int tiles_x = (W + TS - 1) / TS, tiles_img = tiles_x * ((H + TS - 1) / TS);
   for (int e = tid; e < 64 * 128; e += 256) {
     const int co = e >> 7, k = e & 127;
     tw[e] = k < 2 * KK ? w[(int64_t)(cog + co) * 2 * KK + k] : 0.f;
@@ -2713,40 +2705,81 @@ __global__ __launch_bounds__(256) void stem_fwd_mfma_kernel(const float* __restr
     for (int e = 0; e < 8; ++e) {
       const int k = ks * 32 + lg * 8 + e;
       const int ci = k / KK, r = k - ci * KK, ky = r / KS, kx = r - ky * KS;
-      toff[ks][e] = k < 2 * KK ? ci * TWM * TWM + ky * TWM + kx : -1;
+      // padding taps (k >= 2 KK) read tap 0: their weights are zero and the halo holds finite values
+      toff[ks][e] = k < 2 * KK ? ci * TWM * TWM + ky * TWM + kx : 0;
     }
-  const float* tbase = &tin[0][0];
-  f32x4 acc[4][4];
+  float bv[4][4];
 #pragma unroll
   for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[ct][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < 4; ++r) bv[ct][r] = bias[cog + ct * 16 + lg * 4 + r];
+  const float* tbase = &tin[0][0];
+  // the next tile's halo values (TW*TW <= 484 <= 2 x 256) are loaded into registers while this tile computes
+  float hv[2][2];
+  auto fetch = [&](int tile) {
+    const int n = tile / tiles_img, tr = tile - n * tiles_img;
+    const int b = n / F, f = n - b * F;
+    const int ty0 = (tr / tiles_x) * TS, tx0 = (tr - (tr / tiles_x) * tiles_x) * TS;
+    const float* s0 = xt + ((int64_t)b * Fx + (Fx == 1 ? 0 : f)) * H * W;
+    const float* s1 = cond + ((int64_t)b * Fc + (Fc == 1 ? 0 : f)) * H * W;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int py = wid * 4 + j, px = lr;  // group j = tile row py, pixel lr
-    const int pbase = py * TWM + px;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      bf16x8 bfr;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) bfr[e] = (bf16)(toff[ks][e] >= 0 ? tbase[pbase + toff[ks][e]] : 0.f);
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct) acc[ct][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ct][ks], bfr, acc[ct][j], 0, 0, 0);
+    for (int q = 0; q < 2; ++q) {
+      const int e = tid + q * 256;
+      const int yy = ty0 - PAD + e / TW, xx = tx0 - PAD + e % TW;
+      const bool ok = tile < ntiles && e < TW * TW && yy >= 0 && yy < H && xx >= 0 && xx < W;
+      const int64_t o = ok ? (int64_t)yy * W + xx : 0;
+      const float v0 = s0[o], v1 = s1[o];  // unpredicated loads, selected after
+      hv[q][0] = ok ? v0 : 0.f;
+      hv[q][1] = ok ? v1 : 0.f;
     }
-  }
-  // lane holds co = cog + ct*16 + lg*4 + r of pixel (wid*4 + j, lr)
+  };
+  if ((int)blockIdx.x < ntiles) fetch(blockIdx.x);
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int n = tile / tiles_img, tr = tile - n * tiles_img;
+    const int ty0 = (tr / tiles_x) * TS, tx0 = (tr - (tr / tiles_x) * tiles_x) * TS;
+    __syncthreads();  // previous tile's gathers done
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int oy = ty0 + wid * 4 + j, ox = tx0 + lr;
-    if (oy >= H || ox >= W) continue;
-    bf16* dst = y + (((int64_t)n * H + oy) * W + ox) * Co + cog;
+    for (int q = 0; q < 2; ++q) {
+      const int e = tid + q * 256;
+      if (e < TW * TW) {
+        tin[0][(e / TW) * TWM + e % TW] = hv[q][0];
+        tin[1][(e / TW) * TWM + e % TW] = hv[q][1];
+      }
+    }
+    __syncthreads();
+    fetch(tile + gridDim.x);
+    f32x4 acc[4][4];
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct) {
-      const int co = ct * 16 + lg * 4;
-      float v[4];
+    for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = acc[ct][j][r] + bias[cog + co + r];
-      store4(dst + co, v);
+      for (int j = 0; j < 4; ++j) acc[ct][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int py = wid * 4 + j, px = lr;  // group j = tile row py, pixel lr
+      const int pbase = py * TWM + px;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        bf16x8 bfr;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bfr[e] = (bf16)tbase[pbase + toff[ks][e]];
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) acc[ct][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ct][ks], bfr, acc[ct][j], 0, 0, 0);
+      }
+    }
+    // lane holds co = cog + ct*16 + lg*4 + r of pixel (wid*4 + j, lr)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int oy = ty0 + wid * 4 + j, ox = tx0 + lr;
+      if (oy >= H || ox >= W) continue;
+      bf16* dst = y + (((int64_t)n * H + oy) * W + ox) * Co + cog;
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        const int co = ct * 16 + lg * 4;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[ct][j][r] + bv[ct][r];
+        store4(dst + co, v);
+      }
     }
   }
 }
@@ -2928,12 +2961,24 @@ __global__ __launch_bounds__(256) void stem_wgrad_mfma_kernel(const float* __res
   }
 }
 
-__global__ void sum_partials_kernel(const float* __restrict__ part, float* __restrict__ dst, int nsplit, int64_t n,
-                                    int accumulate) {
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int k = 0; k < nsplit; ++k) s += part[(int64_t)k * n + e];
-    dst[e] = accumulate ? dst[e] + s : s;
+// dst[e] (+)= sum_k part[k][e]: block = 64 elements x 16 split groups (each thread sums every 16th split, the
+// 16 group sums are added in a fixed order), so a few thousand elements over hundreds of splits still fill the
+// chip (one thread per element ran 512 dependent loads: 120 us for the stem's 6272 x 512 partials)
+__global__ __launch_bounds__(1024) void sum_partials_kernel(const float* __restrict__ part, float* __restrict__ dst,
+                                                            int nsplit, int64_t n, int accumulate) {
+  __shared__ float red[16][65];
+  const int el = threadIdx.x & 63, kg = threadIdx.x >> 6;
+  const int64_t e = blockIdx.x * (int64_t)64 + el;
+  float s = 0.f;
+  if (e < n)
+    for (int k = kg; k < nsplit; k += 16) s += part[(int64_t)k * n + e];
+  red[kg][el] = s;
+  __syncthreads();
+  if (kg == 0 && e < n) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) t += red[q][el];
+    dst[e] = accumulate ? dst[e] + t : t;
   }
 }
 
@@ -2982,28 +3027,43 @@ __global__ void head_dgrad_kernel(const float* __restrict__ dout, const float* _
   }
 }
 
-// head weight/bias grads: part[blk][c] (c < C) and part[blk][C] = bias
+// head weight/bias grads: part[blk][c] (c < C) and part[blk][C] = bias.  Thread = (pixel lane pl, 8-channel chunk
+// sub): one coalesced pass over the mid frame (the per-channel strided loop it replaces read it C + 1 times:
+// 0.5 ms per step); per-block sums over the 32 pixel lanes in a fixed order
 template <typename T>
-__global__ void head_wgrad_kernel(const float* __restrict__ dout, const T* __restrict__ x, float* __restrict__ part,
-                                  int B, int F, int HW, int C, int64_t px_per_blk) {
-  __shared__ float red[256];
+__global__ __launch_bounds__(256) void head_wgrad_kernel(const float* __restrict__ dout, const T* __restrict__ x,
+                                                         float* __restrict__ part, int B, int F, int HW, int C,
+                                                         int64_t px_per_blk) {
+  __shared__ float red[32][65];
   const int64_t total = (int64_t)B * HW;
   const int64_t p0 = blockIdx.x * px_per_blk, p1 = min(total, p0 + px_per_blk);
-  for (int c = 0; c <= C; ++c) {
-    float s = 0.f;
-    for (int64_t q = p0 + threadIdx.x; q < p1; q += blockDim.x) {
+  const int sub = threadIdx.x & 7, pl = threadIdx.x >> 3;
+  for (int c0 = 0; c0 < C; c0 += 64) {
+    const bool live = c0 + sub * 8 < C;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, gs = 0.f;
+    for (int64_t q = p0 + pl; q < p1; q += 32) {
       const int b = (int)(q / HW);
       const int64_t p = q - (int64_t)b * HW;
       const float g = dout[q];
-      s += (c == C) ? g : g * to_f(x[(((int64_t)b * F + F / 2) * HW + p) * C + c]);
+      gs += g;
+      if (live) {
+        float v[8];
+        load8(x + (((int64_t)b * F + F / 2) * HW + p) * C + c0 + sub * 8, v);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] = fmaf(g, v[i], acc[i]);
+      }
     }
-    red[threadIdx.x] = s;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) red[pl][sub * 8 + i] = acc[i];
+    if (sub == 0) red[pl][64] = gs;
     __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-      if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-      __syncthreads();
+    if (threadIdx.x < 65) {
+      const int c = threadIdx.x;
+      float t = 0.f;
+      for (int q = 0; q < 32; ++q) t += red[q][c];
+      if (c < 64 && c0 + c < C) part[(int64_t)blockIdx.x * (C + 1) + c0 + c] = t;
+      if (c == 64 && c0 == 0) part[(int64_t)blockIdx.x * (C + 1) + C] = t;
     }
-    if (threadIdx.x == 0) part[(int64_t)blockIdx.x * (C + 1) + c] = red[0];
     __syncthreads();
   }
 }
@@ -3415,9 +3475,11 @@ int cesm_stem_fwd(int dtype, const float* xt, const float* cond, const float* w,
                   int F, int Fx, int Fc, int H, int W, int Co, int KS, hipStream_t stream) {
   if (KS > 7 || Co % 64) return CESM_EINVAL;
   dim3 grid((unsigned)(cdiv(H, 16) * cdiv(W, 16)), Co / 64, B * F);
-  if (dtype == CESM_DT_BF16 && 2 * KS * KS <= 128 && !getenv_flag("CESM_STEM_VALU"))
-    stem_fwd_mfma_kernel<<<grid, 256, 0, stream>>>(xt, cond, w, bias, (bf16*)y, B, F, Fx, Fc, H, W, Co, KS);
-  else if (dtype == CESM_DT_BF16)
+  if (dtype == CESM_DT_BF16 && 2 * KS * KS <= 128 && !getenv_flag("CESM_STEM_VALU")) {
+    const int ntiles = (int)(cdiv(H, 16) * cdiv(W, 16)) * B * F;
+    dim3 gp((unsigned)std::min(ntiles, 4 * cesm_num_cus()), Co / 64);
+    stem_fwd_mfma_kernel<<<gp, 256, 0, stream>>>(xt, cond, w, bias, (bf16*)y, B, F, Fx, Fc, H, W, Co, KS, ntiles);
+  } else if (dtype == CESM_DT_BF16)
     stem_fwd_kernel<bf16><<<grid, 256, 0, stream>>>(xt, cond, w, bias, (bf16*)y, B, F, Fx, Fc, H, W, Co, KS);
   else if (dtype == CESM_DT_F32)
     stem_fwd_kernel<float><<<grid, 256, 0, stream>>>(xt, cond, w, bias, (float*)y, B, F, Fx, Fc, H, W, Co, KS);
@@ -3440,7 +3502,7 @@ int cesm_stem_wgrad(int dtype, const float* xt, const float* cond, const void* d
   else
     return CESM_EINVAL;
   const int64_t n = (int64_t)Co * 2 * KS * KS;
-  sum_partials_kernel<<<(unsigned)cdiv(n, 256), 256, 0, stream>>>(part, dw, nblk, n, accumulate);
+  sum_partials_kernel<<<(unsigned)cdiv(n, 64), 1024, 0, stream>>>(part, dw, nblk, n, accumulate);
   return cesm_launch_status();
 }
 
