@@ -2716,7 +2716,9 @@ __global__ __launch_bounds__(256) void stem_fwd_mfma_kernel(const float* __restr
   const float* tbase = &tin[0][0];
   // the next tile's halo values (TW*TW <= 484 <= 2 x 256) are loaded into registers while this tile computes
   float hv[2][2];
-  auto fetch = [&](int tile) {
+  auto fetch = [&](int tile_in) {
+    // past the last tile: addresses of tile 0 (in bounds), values zeroed below
+    const int tile = tile_in < ntiles ? tile_in : 0;
     const int n = tile / tiles_img, tr = tile - n * tiles_img;
     const int b = n / F, f = n - b * F;
     const int ty0 = (tr / tiles_x) * TS, tx0 = (tr - (tr / tiles_x) * tiles_x) * TS;
@@ -2726,7 +2728,7 @@ __global__ __launch_bounds__(256) void stem_fwd_mfma_kernel(const float* __restr
     for (int q = 0; q < 2; ++q) {
       const int e = tid + q * 256;
       const int yy = ty0 - PAD + e / TW, xx = tx0 - PAD + e % TW;
-      const bool ok = tile < ntiles && e < TW * TW && yy >= 0 && yy < H && xx >= 0 && xx < W;
+      const bool ok = tile_in < ntiles && e < TW * TW && yy >= 0 && yy < H && xx >= 0 && xx < W;
       const int64_t o = ok ? (int64_t)yy * W + xx : 0;
       const float v0 = s0[o], v1 = s1[o];  // unpredicated loads, selected after
       hv[q][0] = ok ? v0 : 0.f;

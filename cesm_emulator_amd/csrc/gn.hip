@@ -15,6 +15,23 @@
 
 namespace {
 
+// streaming activation accesses are non-temporal (bf16): measured at the level-0 bench shape stats 122 -> 107 us,
+// apply (+ residual) 389 -> 370 us, backward 679 -> 631 us (tools/gn_time.py); -DGN_NO_NT restores plain accesses
+#ifndef GN_NO_NT
+__device__ __forceinline__ void gl8(const bf16* p, float* v) { ldnt4(p, v); ldnt4(p + 4, v + 4); }
+__device__ __forceinline__ void gl8(const float* p, float* v) { load8(p, v); }
+__device__ __forceinline__ void gs8(bf16* p, const float* v) {
+  bf16x8 a;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = (bf16)v[i];
+  stnt16(p, a);
+}
+__device__ __forceinline__ void gs8(float* p, const float* v) { store8(p, v); }
+#else
+template <typename T> __device__ __forceinline__ void gl8(const T* p, float* v) { load8(p, v); }
+template <typename T> __device__ __forceinline__ void gs8(T* p, const float* v) { store8(p, v); }
+#endif
+
 // row chunks per sample for the reduction kernels: >= ~8 row-iterations per thread, <= 256 chunks
 // (small levels still get ~1000 blocks in total)
 static int gn_nchunk(int64_t rows_b, int C) {
@@ -42,7 +59,7 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const T* __restrict__ y, 
 #pragma unroll 4
     for (int64_t r = r0 + rr; r < r1; r += rl) {
       float v[8];
-      load8(base + r * C + c8 * 8, v);
+      gl8(base + r * C + c8 * 8, v);
 #pragma unroll
       for (int i = 0; i < 8; ++i) { s += v[i]; ss = fmaf(v[i], v[i], ss); }
     }
@@ -140,14 +157,14 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ y, 
 #pragma unroll 4
   for (int64_t r = r0 + rr; r < r1; r += rl) {
     float v[8], rv[8];
-    load8(y + off + r * C, v);
-    if (res) load8(res + off + r * C, rv);
+    gl8(y + off + r * C, v);
+    if (res) gl8(res + off + r * C, rv);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const float a = silu_t<T>(fmaf(v[i], A1[i], A0[i]));
       v[i] = res ? a + rv[i] : a;
     }
-    store8(out + off + r * C, v);
+    gs8(out + off + r * C, v);
   }
 }
 
@@ -170,8 +187,8 @@ __global__ __launch_bounds__(256) void gn_bwd_reduce_kernel(const T* __restrict_
 #pragma unroll 4
     for (int64_t r = r0 + rr; r < r1; r += rl) {
       float v[8], d[8];
-      load8(y + off + r * C, v);
-      load8(dout + off + r * C, d);
+      gl8(y + off + r * C, v);
+      gl8(dout + off + r * C, d);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const float da = d[i] * dsilu_t<T>(fmaf(v[i], A1[i], A0[i]));
@@ -327,14 +344,14 @@ __global__ __launch_bounds__(256) void gn_bwd_apply_kernel(const T* __restrict__
 #pragma unroll 4
   for (int64_t r = r0 + rr; r < r1; r += rl) {
     float v[8], d[8];
-    load8(y + off + r * C, v);
-    load8(dout + off + r * C, d);
+    gl8(y + off + r * C, v);
+    gl8(dout + off + r * C, d);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const float da = d[i] * dsilu_t<T>(fmaf(v[i], A1[i], A0[i]));
       d[i] = fmaf(da, E1[i], fmaf(v[i], E2[i], E3[i]));
     }
-    store8(dy + off + r * C, d);
+    gs8(dy + off + r * C, d);
   }
 }
 
