@@ -109,6 +109,10 @@ class KernelProbe:
                 b += res.numel() * es_of(res) + (0 if res2 is None else res2.numel() * es_of(res2))
             return lab, f, b
 
+        def conv_fwd_gn(x1, x2, wp, bias, geom, B, nslot):
+            lab, f, b = conv_fwd(x1, x2, wp, bias, geom)
+            return lab, f, b + B * nslot * geom[2] * 2  # + the GroupNorm partials (float2 per channel quad)
+
         def conv_wgrad(x1, x2, dy1, dy2, dw, geom, swap, flip, accumulate=True, db=None):
             Ho, Wo, Cout, KH, KW, St, Pd, U = geom
             Nb, Hi, Wi, C1 = x1.shape
@@ -197,6 +201,9 @@ class KernelProbe:
         def gn_stats(y, B, G, eps=1e-5):
             return "gn_stats_kernel", 0.0, float(y.numel() * es_of(y))
 
+        def gn_stats_part(part, rows_b, G, eps=1e-5):
+            return "gn_part_finalize_kernel", 0.0, float(part.numel() * 4)
+
         def gn_apply(y, stats, gamma, beta, ss, res, B, G):
             return "gn_apply_kernel", 0.0, float(y.numel() * es_of(y) * (3 if res is not None else 2))
 
@@ -216,10 +223,10 @@ class KernelProbe:
         def add(a, b):
             return "add_kernel", 0.0, float(a.numel() * es_of(a) * 3)
 
-        for name, fn in dict(conv_fwd=conv_fwd, conv_wgrad=conv_wgrad, tblock_fwd=tblock_fwd, tblock_bwd=tblock_bwd,
+        for name, fn in dict(conv_fwd=conv_fwd, conv_fwd_gn=conv_fwd_gn, conv_wgrad=conv_wgrad, tblock_fwd=tblock_fwd, tblock_bwd=tblock_bwd,
                              tblock_fwd_fold=tblock_fwd_fold, tblock_bwd_dw=tblock_bwd_dw,
                              tattn_fwd=tattn_fwd, tattn_bwd=tattn_bwd,
-                             slaf_fwd=slaf_fwd, slaf_bwd=slaf_bwd, gn_stats=gn_stats, gn_apply=gn_apply, gn_bwd=gn_bwd,
+                             slaf_fwd=slaf_fwd, slaf_bwd=slaf_bwd, gn_stats=gn_stats, gn_stats_part=gn_stats_part, gn_apply=gn_apply, gn_bwd=gn_bwd,
                              ln_fwd=ln_fwd, ln_bwd=ln_bwd, adamw=adamw, add=add).items():
             self._wrap(name, fn)
 

@@ -21,12 +21,12 @@ _CTYPE = {"int": ctypes.c_int, "int64_t": ctypes.c_int64, "float": ctypes.c_floa
 
 
 def parse_header(path: Path = HEADER):
-    """Return {name: (restype, [argtypes])} for every `int cesm_*(...)` / `const char* cesm_*(...)`
-    declaration (the latter: host-only queries returning a static string)."""
+    """Return {name: (restype, [argtypes])} for every `int cesm_*(...)` / `int64_t cesm_*(...)` /
+    `const char* cesm_*(...)` declaration (the last two: host-only queries)."""
     text = path.read_text()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     decls = {}
-    for m in re.finditer(r"\b(int|const\s+char\s*\*)\s*(cesm_\w+)\s*\(([^)]*)\)\s*;", text, flags=re.S):
+    for m in re.finditer(r"\b(int|int64_t|const\s+char\s*\*)\s*(cesm_\w+)\s*\(([^)]*)\)\s*;", text, flags=re.S):
         ret, name, args = m.group(1), m.group(2), m.group(3)
         types = []
         for a in args.split(","):
@@ -38,7 +38,7 @@ def parse_header(path: Path = HEADER):
             else:
                 base = a.rsplit(" ", 1)[0]
                 types.append(_CTYPE[base])
-        decls[name] = (ctypes.c_int if ret == "int" else ctypes.c_char_p, types)
+        decls[name] = ({"int": ctypes.c_int, "int64_t": ctypes.c_int64}.get(ret, ctypes.c_char_p), types)
     return decls
 
 

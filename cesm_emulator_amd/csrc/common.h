@@ -142,6 +142,17 @@ __device__ __forceinline__ float wave_max(float v) {
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
 }
+// sum over each row of 16 lanes (lanes 16r..16r+15), every lane of the row gets the total; DPP adds in a
+// fixed order (quad swaps, half-row mirror, row mirror), so the result is bit-reproducible
+#define CESM_DPP_ADD(v, ctrl) \
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), ctrl, 0xF, 0xF, false))
+__device__ __forceinline__ float row16_sum(float v) {
+  CESM_DPP_ADD(v, 0xB1);   // quad_perm [1,0,3,2]
+  CESM_DPP_ADD(v, 0x4E);   // quad_perm [2,3,0,1]
+  CESM_DPP_ADD(v, 0x141);  // row_half_mirror
+  CESM_DPP_ADD(v, 0x140);  // row_mirror
+  return v;
+}
 // sum over aligned groups of `width` lanes (width power of two <= 64)
 __device__ __forceinline__ float group_sum(float v, int width) {
   for (int o = width >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

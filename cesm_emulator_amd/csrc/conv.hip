@@ -486,7 +486,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
                                                               const bf16* __restrict__ w, const float* __restrict__ bias,
                                                               const bf16* __restrict__ res, const bf16* __restrict__ res2,
                                                               bf16* __restrict__ y1, bf16* __restrict__ y2, ConvGeom g,
-                                                              int tiles_x, int TH) {
+                                                              int tiles_x, int TH, float* __restrict__ gnp = nullptr,
+                                                              int gn_fimg = 1) {
   __shared__ __attribute__((aligned(16))) bf16 sh[H3_NROW * H3_LD];
   __shared__ __attribute__((aligned(16))) bf16 sw[9 * H3_BN * H3_LD];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -620,6 +621,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
 #pragma unroll
       for (int i = 0; i < 2; ++i) rv[j][i] = bf16x4{};
   }
+  // GroupNorm statistics partials (gnp: the Block conv feeding a GroupNorm): per channel quad (i, lg) the sum
+  // and sum of squares of the output over this wave's valid pixels
+  float gsum[2] = {0.f, 0.f}, gsq[2] = {0.f, 0.f};
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     if (!okj[j]) continue;
@@ -632,6 +636,21 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
       for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bv[i][r] + b2f(rv[j][i], r);
       if (co < g.Co1) store4(y1 + m * g.Co1 + co, v);
       else store4(y2 + m * Co2 + (co - g.Co1), v);
+      if (gnp) {  // uniform
+        gsum[i] += (v[0] + v[1]) + (v[2] + v[3]);
+        gsq[i] += fmaf(v[3], v[3], fmaf(v[2], v[2], fmaf(v[1], v[1], v[0] * v[0])));
+      }
+    }
+  }
+  if (gnp) {
+    const int b = n / gn_fimg, f = n - b * gn_fimg;
+    const int64_t nslot = (int64_t)gn_fimg * gridDim.x * 2;
+    const int64_t slot = ((int64_t)f * gridDim.x + blockIdx.x) * 2 + wc;
+    float2* dst = reinterpret_cast<float2*>(gnp) + ((int64_t)b * nslot + slot) * (g.Cout / 4) + (n0 + wr * 32) / 4 + lg;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float a = row16_sum(gsum[i]), q = row16_sum(gsq[i]);
+      if (lr == 0) dst[i * 4] = make_float2(a, q);
     }
   }
 }
@@ -1091,7 +1110,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
                                                           const bf16* __restrict__ res, const bf16* __restrict__ res2,
                                                           bf16* __restrict__ y1, bf16* __restrict__ y2, ConvGeom g,
                                                           int tiles_x, int tiles_per_img, int TH, int ncob, int nitems,
-                                                          int dbg) {
+                                                          int dbg, float* __restrict__ gnp, int gn_fimg) {
   static_assert(TW + 2 <= CP_PITCH && NG <= 8 && HPW <= CW_HPW, "tile geometry");
   static_assert(NST == 2 || (NST == 3 && RW), "3 stages only with resident weights");
   // one LDS array (a second __shared__ object can make hipcc drain the DMA before ds_reads):
@@ -1227,8 +1246,14 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
         if (s >= 2 && s + 1 < nsteps && nchunk == 2) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       } else if (epi) {
-        if constexpr (NG == 8) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+        // younger than step s's DMA: the epilogue's 2*NG output stores (+ 4 GroupNorm partial stores)
+        if (gnp) {
+          if constexpr (NG == 8) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+        } else {
+          if constexpr (NG == 8) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+        }
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
@@ -1285,6 +1310,16 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
     const bf16* rsrc = first ? res : res2;
     const __amdgpu_buffer_rsrc_t rrs =
         __builtin_amdgcn_make_buffer_rsrc((void*)((rsrc ? rsrc : y1) + img), (short)0, img_bytes, 0x00020000);
+    // GroupNorm statistics partials of this wave's pixels (gnp: the Block conv feeding a GroupNorm):
+    // per channel quad (i, lg) the sum and sum of squares of (acc + bias) over the valid pixels
+    float gsum[4] = {0.f, 0.f, 0.f, 0.f}, gsq[4] = {0.f, 0.f, 0.f, 0.f};
+    float gm[NG];
+#pragma unroll
+    for (int j = 0; j < NG; ++j) {
+      const int p = wid * 16 * NG + j * 16 + lr;
+      const int oy = y0 + p / TW, ox = x0 + (p - (p / TW) * TW);
+      gm[j] = (p < TH * TW && oy < g.Ho && ox < g.Wo) ? 1.f : 0.f;
+    }
 #pragma unroll
     for (int r0 = 0; r0 < NG; r0 += RG) {
       const int nj = NG - r0 < RG ? NG - r0 : RG;
@@ -1298,6 +1333,12 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
             const int j = r0 + jj;
             float v[4] = {acc[i][j][0] + bv[0], acc[i][j][1] + bv[1], acc[i][j][2] + bv[2], acc[i][j][3] + bv[3]};
             store4(so + (jj * 16 + lr) * CP_ELD + co, v);
+            if (gnp) {  // uniform
+              const float sv = (v[0] + v[1]) + (v[2] + v[3]);
+              const float qv = fmaf(v[3], v[3], fmaf(v[2], v[2], fmaf(v[1], v[1], v[0] * v[0])));
+              gsum[i] = fmaf(gm[j], sv, gsum[i]);
+              gsq[i] = fmaf(gm[j], qv, gsq[i]);
+            }
           }
         }
       }
@@ -1351,6 +1392,17 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
       }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next round overwrites
+    }
+    if (gnp) {  // after the output stores: exactly 4 more stores (the next step's vmcnt counts them)
+      const int b = n / gn_fimg, f = n - b * gn_fimg;
+      const int64_t nslot = (int64_t)gn_fimg * tiles_per_img * 4;
+      const int64_t slot = ((int64_t)f * tiles_per_img + (y0 / TH) * tiles_x + x0 / TW) * 4 + wid;
+      float2* dst = reinterpret_cast<float2*>(gnp) + ((int64_t)b * nslot + slot) * (g.Cout / 4) + n0 / 4 + lg;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float a = row16_sum(gsum[i]), q = row16_sum(gsq[i]);
+        if (lr == 0) dst[i * 4] = make_float2(a, q);
+      }
     }
     epi = true;
   }
@@ -3181,12 +3233,26 @@ const char* cesm_conv_fwd_variant(int dtype, int Nb, int Hi, int Wi, int C1, int
   return pl.v == CFV_INVALID ? "invalid" : kConvFwdVariantName[pl.v];
 }
 
-// Generic implicit-GEMM conv / dgrad.  Shapes: x1 [Nb][Hi][Wi][C1], x2 [Nb][Hi][Wi][C2] (may be
-// null if C2 == 0), wp [Cout][KH*KW][C1+C2] packed, y1 [Nb][Ho][Wo][Co1], y2 [..][Cout-Co1].
-int cesm_conv_fwd(int dtype, const void* x1, const void* x2, const void* wp, const float* bias, const void* res,
-                  const void* res2, void* y1, void* y2, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout, int Co1,
-                  int KH, int KW, int S, int P, int U, hipStream_t stream) {
-  if (Nb <= 0 || Ho <= 0 || Wo <= 0) return CESM_OK;
+}  // extern "C"
+
+namespace {
+// GroupNorm statistics partial slots per sample that the halo conv of plan pl writes for Nb images in B samples:
+// conv3x3p: (frame, tile, wave), conv3x3_bf16: (frame, tile, pixel half); 0 = this plan has no partials
+int64_t conv_gn_nslot(const ConvFwdPlan& pl, int Nb, int Ho, int Wo, int B) {
+  if (B <= 0 || Nb % B) return 0;
+  const int64_t fimg = Nb / B;
+  const int64_t tiles = (pl.TW > 0 && pl.TH > 0) ? cdiv(Wo, pl.TW) * cdiv(Ho, pl.TH) : 0;
+  switch (pl.v) {
+    case CFV_P36_RW: case CFV_P36: case CFV_P32_RW: case CFV_P32: return fimg * tiles * 4;
+    case CFV_HALO36: case CFV_HALO32: return fimg * tiles * 2;
+    default: return 0;
+  }
+}
+
+int conv_fwd_launch(int dtype, const void* x1, const void* x2, const void* wp, const float* bias, const void* res,
+                    const void* res2, void* y1, void* y2, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo,
+                    int Cout, int Co1, int KH, int KW, int S, int P, int U, float* gnp, int gn_fimg,
+                    hipStream_t stream) {
   const ConvFwdPlan pl = conv_fwd_plan(dtype, Nb, Hi, Wi, C1, C2, Ho, Wo, Cout, Co1, KH, KW, S, P, U);
   if (pl.v == CFV_INVALID) return CESM_EINVAL;
   ConvGeom g{Nb, Hi, Wi, Ho, Wo, C1, C2, Cout, Co1, KH, KW, S, P, U};
@@ -3222,22 +3288,22 @@ int cesm_conv_fwd(int dtype, const void* x1, const void* x2, const void* wp, con
       const int nblk = std::min(nitems, cesm_num_cus());
       if (pl.v == CFV_P36_RW)
         conv3x3p_kernel<36, 8, true><<<nblk, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, tx * ty,
-                                                               TH, ncob, nitems, dbg);
+                                                               TH, ncob, nitems, dbg, gnp, gn_fimg);
       else if (pl.v == CFV_P36)
         conv3x3p_kernel<36, 8, false><<<nblk, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx,
-                                                                tx * ty, TH, ncob, nitems, dbg);
+                                                                tx * ty, TH, ncob, nitems, dbg, gnp, gn_fimg);
       else if (pl.v == CFV_P32_3STAGE)
         // experimental: 8 x 32 tiles, 3 LDS stages (two steps of DMA in flight) - measured slower than
         // 2 stages of 14 x 32 tiles (345 vs 315 us): the level-0 conv is HBM-bound (block-0 stamps: 2.2 GHz,
         // DMA-only 175 us vs MFMA-only 166 us per launch), deeper prefetch does not add overlap
         conv3x3p_kernel<32, 4, true, 3, 7><<<std::min(nitems, cesm_num_cus()), 256, 0, stream>>>(
-            bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, tx * ty, TH, 1, Nb * tx * ty, dbg);
+            bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, tx * ty, TH, 1, Nb * tx * ty, dbg, nullptr, 1);
       else if (pl.v == CFV_P32_RW)
         conv3x3p_kernel<32, 7, true><<<nblk, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, tx * ty,
-                                                               TH, ncob, nitems, dbg);
+                                                               TH, ncob, nitems, dbg, gnp, gn_fimg);
       else
         conv3x3p_kernel<32, 7, false><<<nblk, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx,
-                                                                tx * ty, TH, ncob, nitems, dbg);
+                                                                tx * ty, TH, ncob, nitems, dbg, gnp, gn_fimg);
       break;
     }
     case CFV_W36:
@@ -3264,9 +3330,11 @@ int cesm_conv_fwd(int dtype, const void* x1, const void* x2, const void* wp, con
       const int tx = (int)cdiv(Wo, TW), ty = (int)cdiv(Ho, TH);
       dim3 g3(tx * ty, Nb, Cout / H3_BN);
       if (pl.v == CFV_HALO36)
-        conv3x3_bf16_kernel<36><<<g3, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, TH);
+        conv3x3_bf16_kernel<36><<<g3, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, TH, gnp,
+                                                         gn_fimg);
       else
-        conv3x3_bf16_kernel<32><<<g3, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, TH);
+        conv3x3_bf16_kernel<32><<<g3, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, TH, gnp,
+                                                         gn_fimg);
       break;
     }
     case CFV_S2DOWN36:
@@ -3318,6 +3386,36 @@ int cesm_conv_fwd(int dtype, const void* x1, const void* x2, const void* wp, con
       return CESM_EINVAL;
   }
   return cesm_launch_status();
+}
+}  // namespace
+
+extern "C" {
+
+// Generic implicit-GEMM conv / dgrad.  Shapes: x1 [Nb][Hi][Wi][C1], x2 [Nb][Hi][Wi][C2] (may be
+// null if C2 == 0), wp [Cout][KH*KW][C1+C2] packed, y1 [Nb][Ho][Wo][Co1], y2 [..][Cout-Co1].
+int cesm_conv_fwd(int dtype, const void* x1, const void* x2, const void* wp, const float* bias, const void* res,
+                  const void* res2, void* y1, void* y2, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout, int Co1,
+                  int KH, int KW, int S, int P, int U, hipStream_t stream) {
+  if (Nb <= 0 || Ho <= 0 || Wo <= 0) return CESM_OK;
+  return conv_fwd_launch(dtype, x1, x2, wp, bias, res, res2, y1, y2, Nb, Hi, Wi, C1, C2, Ho, Wo, Cout, Co1, KH, KW, S, P,
+                         U, nullptr, 1, stream);
+}
+
+int64_t cesm_conv_gn_nslot(int dtype, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout, int KH, int KW,
+                           int S, int P, int U, int B) {
+  const ConvFwdPlan pl = conv_fwd_plan(dtype, Nb, Hi, Wi, C1, C2, Ho, Wo, Cout, Cout, KH, KW, S, P, U);
+  return conv_gn_nslot(pl, Nb, Ho, Wo, B);
+}
+
+int cesm_conv_fwd_gn(int dtype, const void* x1, const void* x2, const void* wp, const float* bias, void* y, float* gnpart,
+                     int B, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout, int KH, int KW, int S,
+                     int P, int U, hipStream_t stream) {
+  if (Nb <= 0 || Ho <= 0 || Wo <= 0) return CESM_OK;
+  const ConvFwdPlan pl = conv_fwd_plan(dtype, Nb, Hi, Wi, C1, C2, Ho, Wo, Cout, Cout, KH, KW, S, P, U);
+  if (pl.v == CFV_INVALID) return CESM_EINVAL;
+  if (!gnpart || conv_gn_nslot(pl, Nb, Ho, Wo, B) == 0) return CESM_EUNSUPPORTED;
+  return conv_fwd_launch(dtype, x1, x2, wp, bias, nullptr, nullptr, y, nullptr, Nb, Hi, Wi, C1, C2, Ho, Wo, Cout, Cout,
+                         KH, KW, S, P, U, gnpart, Nb / B, stream);
 }
 
 }  // extern "C"

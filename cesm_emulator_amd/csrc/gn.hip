@@ -100,6 +100,42 @@ __global__ __launch_bounds__(64) void gn_finalize_kernel(const double* __restric
   stats[i * 2 + 1] = (float)(1.0 / sqrt(var + (double)eps));
 }
 
+// stats[b][g] = (mean, rstd) from the producing conv's epilogue partials part[b][slot][C/4] (float2 per channel
+// quad: sum, sum of squares; cesm_conv_fwd_gn): one 256-thread block per (b, g), thread t takes the (slot, quad)
+// pairs t, t + 256, ... of the group in order and accumulates in double, then a fixed-order tree -> reproducible
+__global__ __launch_bounds__(256) void gn_part_finalize_kernel(const float2* __restrict__ part, float* __restrict__ stats,
+                                                               int G, int64_t nslot, int nq, double count, float eps) {
+  const int i = blockIdx.x;
+  const int b = i / G, g = i - b * G;
+  const int qpg = nq / G;
+  const int64_t n = nslot * qpg;
+  const float2* base = part + (int64_t)b * nslot * nq + g * qpg;
+  double a = 0.0, q = 0.0;
+  for (int64_t e = threadIdx.x; e < n; e += 256) {
+    const int64_t sl = e / qpg;
+    const float2 v = base[sl * nq + (e - sl * qpg)];
+    a += v.x;
+    q += v.y;
+  }
+  __shared__ double red[2][256];
+  red[0][threadIdx.x] = a;
+  red[1][threadIdx.x] = q;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + w];
+      red[1][threadIdx.x] += red[1][threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x) return;
+  const double mean = red[0][0] / count;
+  double var = red[1][0] / count - mean * mean;
+  if (var < 0) var = 0;
+  stats[i * 2] = (float)mean;
+  stats[i * 2 + 1] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
 // coefficients: A1[b][c], A0[b][c] with a = y*A1 + A0 (gn_coef8 below)
 __device__ __forceinline__ void load_coef8(const float* p, float* v) {
   const f32x4 a = *reinterpret_cast<const f32x4*>(p);
@@ -391,6 +427,14 @@ int cesm_gn_stats(int dtype, const void* y, float* stats, double* ws, int B, int
 }
 
 // ss: [B][2C] (scale | shift) or null; res: residual [B*rows_b][C] or null; ws: >= 2*B*C floats
+int cesm_gn_stats_part(const float* part, float* stats, int B, int64_t nslot, int C, int G, int64_t rows_b, float eps,
+                       hipStream_t stream) {
+  if (B <= 0 || G <= 0 || C % (4 * G) || nslot <= 0 || rows_b <= 0) return CESM_EINVAL;
+  gn_part_finalize_kernel<<<B * G, 256, 0, stream>>>(reinterpret_cast<const float2*>(part), stats, G, nslot, C / 4,
+                                                     (double)rows_b * (C / G), eps);
+  return cesm_launch_status();
+}
+
 int cesm_gn_apply(int dtype, const void* y, const float* stats, const float* gamma, const float* beta,
                   const float* ss, const void* res, void* out, float* ws, int B, int64_t rows_b, int C, int G,
                   hipStream_t stream) {

@@ -92,6 +92,35 @@ def conv_fwd(x1, x2, wp, bias, geom, res=None, res2=None, out_split=None):
     return y1 if y2 is None else (y1, y2)
 
 
+def conv_gn_nslot(x1, x2, geom, B):
+    """GroupNorm partial slots per sample cesm_conv_fwd_gn writes for this conv (0: the kernel has none)"""
+    Ho, Wo, Cout, KH, KW, St, Pd, U = geom
+    Nb, Hi, Wi, C1 = x1.shape
+    C2 = 0 if x2 is None else x2.shape[3]
+    return int(lib().cesm_conv_gn_nslot(dtcode(x1), Nb, Hi, Wi, C1, C2, Ho, Wo, Cout, KH, KW, St, Pd, U, B))
+
+
+def conv_fwd_gn(x1, x2, wp, bias, geom, B, nslot):
+    """conv_fwd of a Block conv (video_net.py:215) that also writes the GroupNorm statistics partials of its
+    output (per sample, slot and channel quad: sum, sum of squares); returns (y, part) for gn_stats_part"""
+    Ho, Wo, Cout, KH, KW, St, Pd, U = geom
+    Nb, Hi, Wi, C1 = x1.shape
+    C2 = 0 if x2 is None else x2.shape[3]
+    _chk(x1)
+    if x2 is not None:
+        _chk(x2, (Nb, Hi, Wi, C2), x1.dtype)
+    _chk(wp, (Cout, KH * KW * (C1 + C2)), x1.dtype)
+    if bias is not None:
+        _chk(bias, (Cout,), torch.float32)
+    y = empty((Nb, Ho, Wo, Cout), x1.dtype, x1.device)
+    part = empty((B, nslot, Cout // 4, 2), torch.float32, x1.device)
+    call("cesm_conv_fwd_gn", dtcode(x1), P(x1), P(x2), P(wp), P(bias), P(y), P(part), B, Nb, Hi, Wi, C1, C2, Ho, Wo,
+         Cout, KH, KW, St, Pd, U, S())
+    if CONV_TRACE is not None:
+        CONV_TRACE.append(("fwd", Nb, Hi, Wi, C1 + C2, Ho, Wo, Cout, KH, KW, St, Pd, U))
+    return y, part
+
+
 # shape log of conv launches (set CESM_TRACE_CONV=1; tools/conv_shapes.py prints it)
 CONV_TRACE = [] if os.environ.get("CESM_TRACE_CONV") else None
 
@@ -218,6 +247,14 @@ def gn_stats(y, B, G, eps=1e-5):
     stats = empty((B, G, 2), torch.float32, y.device)
     ws = empty((B * 256 * G * 2,), torch.float64, y.device)
     call("cesm_gn_stats", dtcode(y), P(y), P(stats), P(ws), B, rows_b, C, G, float(eps), S())
+    return stats
+
+
+def gn_stats_part(part, rows_b, G, eps=1e-5):
+    """GroupNorm (mean, rstd) [B][G][2] from conv_fwd_gn's partials (replaces gn_stats' pass over y)"""
+    B, nslot, nq, _ = part.shape
+    stats = empty((B, G, 2), torch.float32, part.device)
+    call("cesm_gn_stats_part", P(part), P(stats), B, nslot, nq * 4, G, rows_b, float(eps), S())
     return stats
 
 

@@ -308,12 +308,30 @@ def _flat(p):
     return p.reshape(-1)
 
 
+# GroupNorm statistics from partials written by the Block conv's epilogue (halo conv kernels) instead of a
+# separate pass over y; CESM_NO_GN_EPI=1 restores the pass
+GN_EPI_STATS = os.environ.get("CESM_NO_GN_EPI", "0") != "1"
+
+
 def block_fwd(rc, blk, x1, x2, ss, res):
     """Block (video_net.py:212-227): conv3x3 -> GroupNorm -> scale/shift -> SiLU (+res)."""
     spec = ConvSpec(blk.proj)
-    y, cst = conv_forward(rc, spec, x1, x2)
     G = blk.norm.num_groups
-    stats = K.gn_stats(y, rc.B, G, blk.norm.eps)
+    Nb, H, W, _ = x1.shape
+    geom_hw = spec.out_hw(H, W)
+    nslot = 0
+    if GN_EPI_STATS and x1.dtype == torch.bfloat16 and spec.cout % (4 * G) == 0:
+        St, Pd, U, swap, flip = spec.fwd_map()
+        geom = (geom_hw[0], geom_hw[1], spec.cout, spec.k, spec.k, St, Pd, U)
+        nslot = K.conv_gn_nslot(x1, x2, geom, rc.B)
+    if nslot > 0:
+        wp = rc.packed(spec.mod.weight, spec.cout, spec.cin, spec.k, spec.k, swap, flip)
+        y, part = K.conv_fwd_gn(x1, x2, wp, spec.mod.bias, geom, rc.B, nslot)
+        cst = SimpleNamespace(x1=x1, x2=x2, geom=geom, swap=swap, flip=flip) if rc.save else None
+        stats = K.gn_stats_part(part, y.numel() // (spec.cout * rc.B), G, blk.norm.eps)
+    else:
+        y, cst = conv_forward(rc, spec, x1, x2)
+        stats = K.gn_stats(y, rc.B, G, blk.norm.eps)
     out = K.gn_apply(y, stats, blk.norm.weight, blk.norm.bias, ss, res, rc.B, G)
     st = SimpleNamespace(spec=spec, cst=cst, y=y, stats=stats, ss=ss) if rc.save else None
     return out, st

@@ -36,6 +36,16 @@ extern "C" {
 int cesm_conv_fwd(int dtype, const void* x1, const void* x2, const void* wp, const float* bias, const void* res,
                   const void* res2, void* y1, void* y2, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout, int Co1,
                   int KH, int KW, int S, int P, int U, hipStream_t stream);
+/* cesm_conv_fwd (Co1 = Cout, no residual) that also writes the GroupNorm statistics partials of its output
+ * y (the Block conv feeding GroupNorm, video_net.py:215-217): gnpart [B][nslot][Cout/4] float2 (sum, sum of
+ * squares per channel quad over the pixels of one partial slot), every entry written once, no atomics;
+ * nslot from cesm_conv_gn_nslot (0: the kernel for this shape has no partials -> CESM_EUNSUPPORTED here,
+ * use cesm_gn_stats).  Nb = B * frames. */
+int64_t cesm_conv_gn_nslot(int dtype, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout, int KH, int KW,
+                           int S, int P, int U, int B);
+int cesm_conv_fwd_gn(int dtype, const void* x1, const void* x2, const void* wp, const float* bias, void* y, float* gnpart,
+                     int B, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout, int KH, int KW, int S,
+                     int P, int U, hipStream_t stream);
 /* name of the kernel cesm_conv_fwd launches for these arguments (host-only query, no GPU work; the
  * launcher itself selects through the same function).  "invalid" if cesm_conv_fwd would return EINVAL. */
 const char* cesm_conv_fwd_variant(int dtype, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout,
@@ -77,6 +87,10 @@ int cesm_head_bwd(int dtype, const float* dout, const void* x, const float* w, v
  * GroupNorm(G,C) eps, affine, then x*(scale+1)+shift, SiLU, + residual: video_net.py:216-227, :265. */
 int cesm_gn_stats(int dtype, const void* y, float* stats, double* ws, int B, int64_t rows_b, int C, int G, float eps,
                   hipStream_t stream);
+/* stats [B][G] (mean, rstd) from cesm_conv_fwd_gn's partials (replaces cesm_gn_stats' pass over y):
+ * fixed-order double reduction, rows_b = voxels per sample */
+int cesm_gn_stats_part(const float* part, float* stats, int B, int64_t nslot, int C, int G, int64_t rows_b, float eps,
+                       hipStream_t stream);
 int cesm_gn_apply(int dtype, const void* y, const float* stats, const float* gamma, const float* beta,
                   const float* ss, const void* res, void* out, float* ws, int B, int64_t rows_b, int C, int G,
                   hipStream_t stream);

@@ -107,6 +107,51 @@ def test_conv3x3p_level0_bf16(dev, H, W, with_res):
     assert e_fwd < 1e-2 and e_dx < 1e-2 and e_dw < 1e-2 and e_db < 1e-2
 
 
+# ------------------------------------------------------------------ GroupNorm statistics from the conv epilogue
+@pytest.mark.parametrize("C1,C2,Cout,H,W,B,Fr,kern", [
+    (64, 0, 64, 20, 96, 2, 3, "conv3x3p_kernel<32,7,true>"),     # level 0, partial 14-row tile
+    (64, 0, 64, 30, 288, 1, 2, "conv3x3p_kernel<32,7,true>"),    # full bench width
+    (64, 0, 64, 18, 72, 2, 2, "conv3x3_bf16_kernel<36>"),        # 8 channels per group, 36-wide tiles
+    (64, 64, 64, 20, 96, 2, 2, "conv3x3_bf16_kernel<32>"),       # decoder concat input
+    (128, 0, 128, 24, 144, 2, 2, "conv3x3_bf16_kernel<32>"),     # level 1 (16 channels per group)
+    (256, 128, 128, 12, 72, 1, 3, "conv3x3_bf16_kernel<36>"),    # concat, Cin != Cout
+    (256, 0, 256, 12, 72, 2, 2, "conv3x3_bf16_kernel<36>"),      # level 2 (32 per group)
+    (512, 0, 512, 6, 36, 2, 2, "conv3x3_bf16_kernel<36>"),       # level 3 (64 per group: both co halves)
+])
+def test_gn_epilogue_stats_bf16(dev, C1, C2, Cout, H, W, B, Fr, kern):
+    """The Block conv writes GroupNorm (sum, sum of squares) partials per channel quad from its epilogue
+    (cesm_conv_fwd_gn); cesm_gn_stats_part reduces them.  y must be bit-identical to the plain conv launch,
+    and (mean, rstd) must match the separate statistics pass over the stored y (gn_stats) to the bf16
+    rounding of y (the partials see the fp32 values before rounding: |d mean| / std and d rstd / rstd ~ 1e-5)."""
+    G = 8
+    Nb = B * Fr
+    assert K.conv_fwd_variant(BF, Nb, H, W, C1, C2, H, W, Cout, Cout, 3, 3, 1, 1, 1) == kern
+    torch.manual_seed(C1 + C2 + H + W)
+    x1 = (torch.randn(Nb, H, W, C1, device=dev) + 0.3).to(BF)
+    x2 = torch.randn(Nb, H, W, C2, device=dev).to(BF) if C2 else None
+    w = torch.randn(Cout, C1 + C2, 1, 3, 3, device=dev) * (C1 + C2) ** -0.5 / 3
+    bias = torch.randn(Cout, device=dev) * 0.5
+    wp = K.conv_pack(w, BF, Cout, C1 + C2, 3, 3, 0, 0)
+    geom = (H, W, Cout, 3, 3, 1, 1, 1)
+    nslot = K.conv_gn_nslot(x1, x2, geom, B)
+    assert nslot > 0
+    y, part = K.conv_fwd_gn(x1, x2, wp, bias, geom, B, nslot)
+    y0 = K.conv_fwd(x1, x2, wp, bias, geom)
+    st = K.gn_stats_part(part, y.numel() // (Cout * B), G)
+    st0 = K.gn_stats(y0, B, G)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y0)
+    m, r = st[..., 0].double().cpu(), st[..., 1].double().cpu()
+    m0, r0 = st0[..., 0].double().cpu(), st0[..., 1].double().cpu()
+    dm = ((m - m0).abs() * r0).max().item()
+    dr = ((r - r0).abs() / r0).max().item()
+    print(f"{kern} {C1}+{C2}->{Cout} {H}x{W}: |d mean|/std {dm:.2e}  d rstd/rstd {dr:.2e}  nslot {nslot}")
+    assert dm < 2e-4 and dr < 2e-4
+    # run-to-run reproducible
+    _, part2 = K.conv_fwd_gn(x1, x2, wp, bias, geom, B, nslot)
+    assert torch.equal(part, part2)
+
+
 # ------------------------------------------------------------------ Down / Upsample (A13)
 @pytest.mark.parametrize("kind", ["down", "up"])
 @pytest.mark.parametrize("C,H,W", [(64, 96, 144), (128, 26, 38), (256, 48, 72), (64, 18, 22), (64, 130, 160)])

@@ -26,7 +26,7 @@ def main():
     N = 96
     tag = " ".join(f"{k}={v}" for k, v in os.environ.items() if k.startswith("CESM_CONV3X3")) or "default"
     out = []
-    for (H, W, C, C2) in [(96, 144, 128, 0), (48, 72, 256, 0), (24, 36, 512, 0), (192, 288, 64, 64), (96, 144, 128, 128)]:
+    for (H, W, C, C2) in [(192, 288, 64, 0), (96, 144, 128, 0), (48, 72, 256, 0), (24, 36, 512, 0), (192, 288, 64, 64), (96, 144, 128, 128)]:
         x = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
         x2 = torch.randn(N, H, W, C2, device=dev).to(torch.bfloat16) if C2 else None
         Co = C if not C2 else C

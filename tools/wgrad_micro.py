@@ -13,7 +13,7 @@ def main():
     levels = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0, 3]
     dev = torch.device("cuda")
     for lvl in levels:
-        Nb, H, W, C = 48, 192 >> lvl, 288 >> lvl, 64 << lvl
+        Nb, H, W, C = 96, 192 >> lvl, 288 >> lvl, 64 << lvl
         torch.manual_seed(0)
         x = torch.randn(Nb, H, W, C, device=dev).to(torch.bfloat16)
         dy = torch.randn(Nb, H, W, C, device=dev).to(torch.bfloat16)
@@ -30,7 +30,9 @@ def main():
         torch.cuda.synchronize()
         us = s.elapsed_time(e) * 1e3 / reps
         flop = 2.0 * Nb * H * W * C * C * 9
-        print(f"wgrad3x3 level {lvl} {C}->{C}: {us:.1f} us {flop / us / 1e6:.1f} TFLOP/s", flush=True)
+        v = K.conv_wgrad_variant(torch.bfloat16, Nb, H, W, C, 0, H, W, C, C, 3, 3, 1, 1, 1, False) \
+            if hasattr(K, "conv_wgrad_variant") else "?"
+        print(f"wgrad3x3 level {lvl} {C}->{C} {v}: {us:.1f} us {flop / us / 1e6:.1f} TFLOP/s", flush=True)
 
 
 if __name__ == "__main__":
