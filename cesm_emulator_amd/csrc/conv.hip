@@ -2174,37 +2174,40 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_bf16_kernel(const bf16* __res
 #pragma unroll
     for (int kx = 0; kx < 3; ++kx) boff[half][kx] = (r + kx) * 32 + (((cit * 4 + pp) ^ w3_swz_x(r + kx)) * 4);
   }
-  for (int tile = blockIdx.z; tile < ntiles; tile += gridDim.z) {
+  // the next tile's dY / halo vectors are loaded into registers (unpredicated: clamped address + select)
+  // while the current tile is consumed, and written to LDS after the barrier that ends its reads
+  bf16x8 yv[8], hv[6];
+  auto gload = [&](int tile) {
     const int n = tile / tiles_per_img;
     const int rem = tile - n * tiles_per_img;
     const int ty = rem / tiles_x, tx = rem - ty * tiles_x;
     const int y0 = ty * W3_TH, x0 = tx * W3_TW;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {       // dY: 256 px x 8 vectors
+      const int e = tid + k * 256;
+      const int p = e >> 3, part = e & 7;
+      const int oy = y0 + (p >> 5), ox = x0 + (p & 31);
+      const bool ok = oy < g.Ho && ox < g.Wo;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(
+          ys + (ok ? (((int64_t)n * g.Ho + oy) * g.Wo + ox) * ycs : 0) + ycc + part * 8);
+      yv[k] = ok ? v : bf16x8{};
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {       // halo: 340 px x 4 vectors
+      const int e = tid + k * 256;
+      const int hp = e >> 2, part = e & 3;
+      const int r = hp / W3_HW, c = hp - r * W3_HW;
+      const int iy = y0 - 1 + r, ix = x0 - 1 + c;
+      const bool ok = e < W3_NPIX * 4 && (unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(
+          xs + (ok ? (((int64_t)n * g.Hi + iy) * g.Wi + ix) * xcs : 0) + xcc + part * 8);
+      hv[k] = ok ? v : bf16x8{};
+    }
+  };
+  if ((int)blockIdx.z < ntiles) gload(blockIdx.z);
+  for (int tile = blockIdx.z; tile < ntiles; tile += gridDim.z) {
     __syncthreads();
     {
-      bf16x8 yv[8], hv[6];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {       // dY: 256 px x 8 vectors
-        const int e = tid + k * 256;
-        const int p = e >> 3, part = e & 7;
-        const int oy = y0 + (p >> 5), ox = x0 + (p & 31);
-        bf16x8 v = {};
-        if (oy < g.Ho && ox < g.Wo)
-          v = *reinterpret_cast<const bf16x8*>(ys + (((int64_t)n * g.Ho + oy) * g.Wo + ox) * ycs + ycc + part * 8);
-        yv[k] = v;
-      }
-#pragma unroll
-      for (int k = 0; k < 6; ++k) {       // halo: 340 px x 4 vectors
-        const int e = tid + k * 256;
-        bf16x8 v = {};
-        if (e < W3_NPIX * 4) {
-          const int hp = e >> 2, part = e & 3;
-          const int r = hp / W3_HW, c = hp - r * W3_HW;
-          const int iy = y0 - 1 + r, ix = x0 - 1 + c;
-          if ((unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi)
-            v = *reinterpret_cast<const bf16x8*>(xs + (((int64_t)n * g.Hi + iy) * g.Wi + ix) * xcs + xcc + part * 8);
-        }
-        hv[k] = v;
-      }
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int e = tid + k * 256;
@@ -2224,6 +2227,7 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_bf16_kernel(const bf16* __res
       }
     }
     __syncthreads();
+    if (tile + (int)gridDim.z < ntiles) gload(tile + gridDim.z);
 #pragma unroll 1
     for (int py = 0; py < W3_TH; ++py) {
       // A = dY^T (rows co, K = 32 pixels of row py): tr reads, rows = pixel py*32 + k
@@ -2254,6 +2258,163 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_bf16_kernel(const bf16* __res
     }
   }
   // D[co][ci] per tap: lane col lr -> ci, rows 4lg+r -> co
+  const int K = 9 * Cin;
+  float* out = slab + (int64_t)blockIdx.z * g.Cout * K;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int ci = ci0 + cit * 16 + lr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + (cot0 + i) * 16 + lg * 4 + r;
+        out[(int64_t)co * K + tap * Cin + ci] = acc[i][tap][r];
+      }
+    }
+}
+
+// Same weight gradient with blocks of 64 co x 64 ci and 8 waves (one block per CU, two waves per SIMD; wave w:
+// co tiles {2*(w>>2), 2*(w>>2)+1} x ci tile w&3).  The wgrad is bound by the per-CU load rate (~7.6 B/cycle
+// with plain 16-B loads: 54 KB per 8 x 32 tile of a 64 x 32 block, the dY tile re-read by every ci block):
+// 64 ci per block loads each dY tile once per 64 input channels (75 KB per tile for twice the MACs).  The
+// input halo is kept as two 32-channel planes so the fragment reads are the 64-ci kernel's.
+constexpr int W3_PLANE = (W3_TH + 2) * W3_P * 32;  // halo plane (bf16 elements)
+
+__global__ __launch_bounds__(512, 1) void wgrad3x3c64_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
+                                                             const bf16* __restrict__ dy1, const bf16* __restrict__ dy2,
+                                                             float* __restrict__ slab, ConvGeom g, int tiles_x,
+                                                             int ntiles) {
+  __shared__ __attribute__((aligned(16))) bf16 sdy[W3_TH * W3_TW * 64];  // 32 KB, 128-B rows
+  __shared__ __attribute__((aligned(16))) bf16 shx[2 * W3_PLANE];        // 2 x 30 KB, 64-B rows
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int cot0 = (wid >> 2) * 2, cit = wid & 3;
+  const int co0 = blockIdx.x * 64, ci0 = blockIdx.y * 64;
+  const int Cin = g.C1 + g.C2;
+  const bf16* xs; int xcs, xcc;
+  if (ci0 < g.C1) { xs = x1; xcs = g.C1; xcc = ci0; } else { xs = x2; xcs = g.C2; xcc = ci0 - g.C1; }
+  const bf16* ys; int ycs, ycc;
+  const int Co2 = g.Cout - g.Co1;
+  if (co0 < g.Co1) { ys = dy1; ycs = g.Co1; ycc = co0; } else { ys = dy2; ycs = Co2; ycc = co0 - g.Co1; }
+  const int tiles_per_img = tiles_x * ((g.Ho + W3_TH - 1) / W3_TH);
+
+  f32x4 acc[2][9];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int lr = lane & 15, lg = lane >> 4, q = lr >> 2, pp = lr & 3;
+  const bf16* shp = shx + (cit >> 1) * W3_PLANE;
+  int aoff[2][2], boff[2][3];
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const int r = lg * 8 + half * 4 + q;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) aoff[i][half] = r * 64 + ((((cot0 + i) * 4 + pp) ^ w3_swz_dy(r)) * 4);
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) boff[half][kx] = (r + kx) * 32 + ((((cit & 1) * 4 + pp) ^ w3_swz_x(r + kx)) * 4);
+  }
+  // next tile's vectors in registers (unpredicated loads: clamped address + select), written to LDS after
+  // the barrier that ends the current tile's reads
+  bf16x8 yv[4], hv[6];
+  auto gload = [&](int tile) {
+    const int n = tile / tiles_per_img;
+    const int rem = tile - n * tiles_per_img;
+    const int ty = rem / tiles_x, tx = rem - ty * tiles_x;
+    const int y0 = ty * W3_TH, x0 = tx * W3_TW;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {       // dY: 256 px x 8 vectors
+      const int e = tid + k * 512;
+      const int p = e >> 3, part = e & 7;
+      const int oy = y0 + (p >> 5), ox = x0 + (p & 31);
+      const bool ok = oy < g.Ho && ox < g.Wo;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(
+          ys + (ok ? (((int64_t)n * g.Ho + oy) * g.Wo + ox) * ycs : 0) + ycc + part * 8);
+      yv[k] = ok ? v : bf16x8{};
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {       // halo: 340 px x 8 vectors (64 ci)
+      const int e = tid + k * 512;
+      const int hp = e >> 3, part = e & 7;
+      const int r = hp / W3_HW, c = hp - r * W3_HW;
+      const int iy = y0 - 1 + r, ix = x0 - 1 + c;
+      const bool ok = e < W3_NPIX * 8 && (unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(
+          xs + (ok ? (((int64_t)n * g.Hi + iy) * g.Wi + ix) * xcs : 0) + xcc + part * 8);
+      hv[k] = ok ? v : bf16x8{};
+    }
+  };
+  if ((int)blockIdx.z < ntiles) gload(blockIdx.z);
+  for (int tile = blockIdx.z; tile < ntiles; tile += gridDim.z) {
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int e = tid + k * 512;
+      const int p = e >> 3, part = e & 7;  // chunk pair (2part, 2part+1) of 8-B chunks
+      const int ch = (part * 2) ^ w3_swz_dy(p);
+      *reinterpret_cast<bf16x8*>(sdy + p * 64 + ch * 4) = yv[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const int e = tid + k * 512;
+      if (e < W3_NPIX * 8) {
+        const int hp = e >> 3, part = e & 7;
+        const int r = hp / W3_HW, row = r * W3_P + (hp - r * W3_HW);
+        const int ch = ((part & 3) * 2) ^ w3_swz_x(row);
+        *reinterpret_cast<bf16x8*>(shx + (part >> 2) * W3_PLANE + row * 32 + ch * 4) = hv[k];
+      }
+    }
+    __syncthreads();
+    if (tile + (int)gridDim.z < ntiles) gload(tile + gridDim.z);
+    // the 22 fragment reads of pixel row py+1 are issued between the 18 MFMAs of row py (two register
+    // sets; 1 read : 1 MFMA via sched_group_barrier), so no row waits for its LDS reads
+    bf16x8 fa[2][2], fb[2][9];
+    auto rd = [&](int py, int b) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(sdy + aoff[i][half] + py * 32 * 64));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) fa[b][i][half * 4 + e] = __builtin_bit_cast(bf16, (short)v[e]);
+        }
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int ky = tap / 3, kx = tap - ky * 3;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (LDS_PTR(s16x4))(shp + boff[half][kx] + (py + ky) * W3_P * 32));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) fb[b][tap][half * 4 + e] = __builtin_bit_cast(bf16, (short)v[e]);
+        }
+      }
+    };
+    auto mm = [&](int b) {
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        acc[0][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[b][0], fb[b][tap], acc[0][tap], 0, 0, 0);
+        acc[1][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[b][1], fb[b][tap], acc[1][tap], 0, 0, 0);
+      }
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int py = 0; py < W3_TH; ++py) {
+      const int b = py & 1;
+      __builtin_amdgcn_sched_barrier(0);
+      if (py + 1 < W3_TH) rd(py + 1, b ^ 1);
+      mm(b);
+      if (py + 1 < W3_TH) {
+#pragma unroll
+        for (int q2 = 0; q2 < 18; ++q2) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
   const int K = 9 * Cin;
   float* out = slab + (int64_t)blockIdx.z * g.Cout * K;
 #pragma unroll
@@ -2449,37 +2610,38 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3w36_kernel(const bf16* __restr
 #pragma unroll
     for (int i = 0; i < 2; ++i) aoff[i][half] = r * 64 + ((((cot0 + i) * 4 + pp) ^ w3_swz_dy(r)) * 4);
   }
-  for (int tile = blockIdx.z; tile < ntiles; tile += gridDim.z) {
+  bf16x8 yv[9], hv[6];  // next tile's vectors in registers (see wgrad3x3_bf16_kernel)
+  auto gload = [&](int tile) {
     const int n = tile / tiles_per_img;
     const int rem = tile - n * tiles_per_img;
     const int ty = rem / tiles_x, tx = rem - ty * tiles_x;
     const int y0 = ty * W36_TH, x0 = tx * W36_TW;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {       // dY: 288 px x 8 vectors
+      const int e = tid + k * 256;
+      const int p = e >> 3, part = e & 7;
+      const int oy = y0 + p / W36_TW, ox = x0 + (p - (p / W36_TW) * W36_TW);
+      const bool ok = oy < g.Ho && ox < g.Wo;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(
+          ys + (ok ? (((int64_t)n * g.Ho + oy) * g.Wo + ox) * ycs : 0) + ycc + part * 8);
+      yv[k] = ok ? v : bf16x8{};
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {       // halo: 380 px x 4 vectors
+      const int e = tid + k * 256;
+      const int hp = e >> 2, part = e & 3;
+      const int r = hp / W36_HW, c = hp - r * W36_HW;
+      const int iy = y0 - 1 + r, ix = x0 - 1 + c;
+      const bool ok = e < W36_NPIX * 4 && (unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(
+          xs + (ok ? (((int64_t)n * g.Hi + iy) * g.Wi + ix) * xcs : 0) + xcc + part * 8);
+      hv[k] = ok ? v : bf16x8{};
+    }
+  };
+  if ((int)blockIdx.z < ntiles) gload(blockIdx.z);
+  for (int tile = blockIdx.z; tile < ntiles; tile += gridDim.z) {
     __syncthreads();
     {
-      bf16x8 yv[9], hv[6];
-#pragma unroll
-      for (int k = 0; k < 9; ++k) {       // dY: 288 px x 8 vectors
-        const int e = tid + k * 256;
-        const int p = e >> 3, part = e & 7;
-        const int oy = y0 + p / W36_TW, ox = x0 + (p - (p / W36_TW) * W36_TW);
-        bf16x8 v = {};
-        if (oy < g.Ho && ox < g.Wo)
-          v = *reinterpret_cast<const bf16x8*>(ys + (((int64_t)n * g.Ho + oy) * g.Wo + ox) * ycs + ycc + part * 8);
-        yv[k] = v;
-      }
-#pragma unroll
-      for (int k = 0; k < 6; ++k) {       // halo: 380 px x 4 vectors
-        const int e = tid + k * 256;
-        bf16x8 v = {};
-        if (e < W36_NPIX * 4) {
-          const int hp = e >> 2, part = e & 3;
-          const int r = hp / W36_HW, c = hp - r * W36_HW;
-          const int iy = y0 - 1 + r, ix = x0 - 1 + c;
-          if ((unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi)
-            v = *reinterpret_cast<const bf16x8*>(xs + (((int64_t)n * g.Hi + iy) * g.Wi + ix) * xcs + xcc + part * 8);
-        }
-        hv[k] = v;
-      }
 #pragma unroll
       for (int k = 0; k < 9; ++k) {
         const int e = tid + k * 256;
@@ -2499,6 +2661,7 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3w36_kernel(const bf16* __restr
       }
     }
     __syncthreads();
+    if (tile + (int)gridDim.z < ntiles) gload(tile + gridDim.z);
     // flat pixel of this lane's two 4-pixel groups in K-chunk kc: P = kc*32 + r0[half]; (row, col) of
     // it in the 36-wide tile advance incrementally (32 < 36: at most one wrap per chunk)
     int prow[2], pcol[2];
@@ -2560,6 +2723,169 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3w36_kernel(const bf16* __restr
 // sum slabs over splits (fixed order) and scatter into the PyTorch weight layout
 // dst[((d0*D1 + d1)*KH + kyt)*KW + kxt], with (d0,d1) = swap ? (ci,co) : (co,ci) and
 // (kyt,kxt) = flip ? (KH-1-ky, KW-1-kx) : (ky,kx).
+// 8 x 36 tiles (levels 2-3) with the 64 co x 64 ci / 8-wave blocking and the K-chunk software pipeline of
+// wgrad3x3c64_kernel: each wave's 22 fragment reads of K-chunk kc+1 are issued between the 18 MFMAs of chunk kc
+__global__ __launch_bounds__(512, 1) void wgrad3x3w36c64_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
+                                                                const bf16* __restrict__ dy1, const bf16* __restrict__ dy2,
+                                                                float* __restrict__ slab, ConvGeom g, int tiles_x,
+                                                                int ntiles) {
+  __shared__ __attribute__((aligned(16))) bf16 sdy[W36_NP * 64];  // 36 KB, 128-B rows
+  __shared__ __attribute__((aligned(16))) bf16 shx[2 * W3_PLANE];  // 2 x 30 KB, 64-B rows
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int cot0 = (wid >> 2) * 2, cit = wid & 3;
+  const int co0 = blockIdx.x * 64, ci0 = blockIdx.y * 64;
+  const int Cin = g.C1 + g.C2;
+  const bf16* xs; int xcs, xcc;
+  if (ci0 < g.C1) { xs = x1; xcs = g.C1; xcc = ci0; } else { xs = x2; xcs = g.C2; xcc = ci0 - g.C1; }
+  const bf16* ys; int ycs, ycc;
+  const int Co2 = g.Cout - g.Co1;
+  if (co0 < g.Co1) { ys = dy1; ycs = g.Co1; ycc = co0; } else { ys = dy2; ycs = Co2; ycc = co0 - g.Co1; }
+  const int tiles_per_img = tiles_x * ((g.Ho + W36_TH - 1) / W36_TH);
+
+  f32x4 acc[2][9];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int lr = lane & 15, lg = lane >> 4, q = lr >> 2, pp = lr & 3;
+  const bf16* shp = shx + (cit >> 1) * W3_PLANE;
+  const int cx = (cit & 1) * 4 + pp;
+  int aoff[2][2];
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const int r = lg * 8 + half * 4 + q;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) aoff[i][half] = r * 64 + ((((cot0 + i) * 4 + pp) ^ w3_swz_dy(r)) * 4);
+  }
+  bf16x8 yv[5], hv[6];
+  auto gload = [&](int tile) {
+    const int n = tile / tiles_per_img;
+    const int rem = tile - n * tiles_per_img;
+    const int ty = rem / tiles_x, tx = rem - ty * tiles_x;
+    const int y0 = ty * W36_TH, x0 = tx * W36_TW;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {       // dY: 288 px x 8 vectors
+      const int e = tid + k * 512;
+      const int p = e >> 3, part = e & 7;
+      const int oy = y0 + p / W36_TW, ox = x0 + (p - (p / W36_TW) * W36_TW);
+      const bool ok = e < W36_NP * 8 && oy < g.Ho && ox < g.Wo;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(
+          ys + (ok ? (((int64_t)n * g.Ho + oy) * g.Wo + ox) * ycs : 0) + ycc + part * 8);
+      yv[k] = ok ? v : bf16x8{};
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {       // halo: 380 px x 8 vectors (64 ci)
+      const int e = tid + k * 512;
+      const int hp = e >> 3, part = e & 7;
+      const int r = hp / W36_HW, c = hp - r * W36_HW;
+      const int iy = y0 - 1 + r, ix = x0 - 1 + c;
+      const bool ok = e < W36_NPIX * 8 && (unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(
+          xs + (ok ? (((int64_t)n * g.Hi + iy) * g.Wi + ix) * xcs : 0) + xcc + part * 8);
+      hv[k] = ok ? v : bf16x8{};
+    }
+  };
+  if ((int)blockIdx.z < ntiles) gload(blockIdx.z);
+  for (int tile = blockIdx.z; tile < ntiles; tile += gridDim.z) {
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int e = tid + k * 512;
+      if (e < W36_NP * 8) {
+        const int p = e >> 3, part = e & 7;
+        const int ch = (part * 2) ^ w3_swz_dy(p);
+        *reinterpret_cast<bf16x8*>(sdy + p * 64 + ch * 4) = yv[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const int e = tid + k * 512;
+      if (e < W36_NPIX * 8) {
+        const int hp = e >> 3, part = e & 7;
+        const int r = hp / W36_HW, row = r * W3_P + (hp - r * W36_HW);
+        const int ch = ((part & 3) * 2) ^ w3_swz_x(row);
+        *reinterpret_cast<bf16x8*>(shx + (part >> 2) * W3_PLANE + row * 32 + ch * 4) = hv[k];
+      }
+    }
+    __syncthreads();
+    if (tile + (int)gridDim.z < ntiles) gload(tile + gridDim.z);
+    // flat pixel of this lane's two 4-pixel groups in K-chunk kc: P = kc*32 + r0[half] -> (row, col) of the
+    // 36-wide tile (32 < 36: at most one wrap per chunk)
+    int prow[2], pcol[2];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) { prow[half] = 0; pcol[half] = lg * 8 + half * 4 + q; }
+    bf16x8 fa[2][2], fb[2][9];
+    auto rd = [&](int kc, int b) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(sdy + aoff[i][half] + kc * 32 * 64));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) fa[b][i][half * 4 + e] = __builtin_bit_cast(bf16, (short)v[e]);
+        }
+      int bo[2][3];
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const int hb = prow[half] * W3_P + pcol[half];
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) bo[half][kx] = (hb + kx) * 32 + ((cx ^ w3_swz_x(hb + kx)) * 4);
+        pcol[half] += 32;
+        if (pcol[half] >= W36_TW) { pcol[half] -= W36_TW; ++prow[half]; }
+      }
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int ky = tap / 3, kx = tap - ky * 3;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(shp + bo[half][kx] + ky * W3_P * 32));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) fb[b][tap][half * 4 + e] = __builtin_bit_cast(bf16, (short)v[e]);
+        }
+      }
+    };
+    auto mm = [&](int b) {
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        acc[0][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[b][0], fb[b][tap], acc[0][tap], 0, 0, 0);
+        acc[1][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[b][1], fb[b][tap], acc[1][tap], 0, 0, 0);
+      }
+    };
+    constexpr int NKC = W36_NP / 32;
+    rd(0, 0);
+#pragma unroll
+    for (int kc = 0; kc < NKC; ++kc) {
+      const int b = kc & 1;
+      __builtin_amdgcn_sched_barrier(0);
+      if (kc + 1 < NKC) rd(kc + 1, b ^ 1);
+      mm(b);
+      if (kc + 1 < NKC) {
+#pragma unroll
+        for (int q2 = 0; q2 < 18; ++q2) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  const int K = 9 * Cin;
+  float* out = slab + (int64_t)blockIdx.z * g.Cout * K;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int ci = ci0 + cit * 16 + lr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + (cot0 + i) * 16 + lg * 4 + r;
+        out[(int64_t)co * K + tap * Cin + ci] = acc[i][tap][r];
+      }
+    }
+}
+
 // dst (+)= sum over the nsplit slabs, remapped to the PyTorch layout.  Block = 64 consecutive slab
 // elements x 4 split-groups (coalesced 256-B rows per split), fixed-order combine in LDS.
 __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ dst,
@@ -3422,15 +3748,15 @@ int cesm_conv_fwd_gn(int dtype, const void* x1, const void* x2, const void* wp, 
 
 namespace {
 // Kernel selection of cesm_conv_wgrad (host only)
-enum WgradVariant { WGV_W36 = 0, WGV_W32, WGV_WIDE, WGV_GEN, WGV_S2 };
+enum WgradVariant { WGV_W36 = 0, WGV_W32, WGV_WIDE, WGV_GEN, WGV_S2, WGV_W32C64, WGV_W36C64 };
 static int wgrad_plan(int dtype, int64_t M, int Hi, int Wi, int Ho, int Wo, int KH, int KW, int S, int P, int U) {
   const bool halo3 = dtype == CESM_DT_BF16 && KH == 3 && KW == 3 && S == 1 && P == 1 && U == 1 && Ho == Hi &&
                      Wo == Wi && !getenv_flag("CESM_NO_HALO");
   // 8 x 36 tiles only where 32-wide tiles waste >= 20 % of the columns (W = 36, 72); at W = 144 / 288
   // the 8 x 32 kernel's row-aligned K chunks are faster despite the partial last tile
   if (halo3 && (Wo % W36_TW) == 0 && 5 * Wo <= 4 * (int)cdiv(Wo, W3_TW) * W3_TW && !getenv_flag("CESM_NO_WGRAD36"))
-    return WGV_W36;
-  if (halo3) return WGV_W32;
+    return getenv_flag("CESM_WGRAD3X3_C32") ? WGV_W36 : WGV_W36C64;
+  if (halo3) return getenv_flag("CESM_WGRAD3X3_C32") ? WGV_W32 : WGV_W32C64;  // (C1 % 64 == 0: cesm_conv_wgrad)
   // (32-wide pixel tiles: at Wo = 36 the second tile of a row is 8/9 empty and the wide kernel is faster)
   if (dtype == CESM_DT_BF16 && KH == 4 && KW == 4 && S == 2 && P == 1 && U == 1 && Hi == 2 * Ho && Wi == 2 * Wo &&
       Wo >= 64 && !getenv_flag("CESM_NO_S2HALO"))
@@ -3450,6 +3776,8 @@ const char* cesm_conv_wgrad_variant(int dtype, int Nb, int Hi, int Wi, int C1, i
   switch (wv) {
     case WGV_W36: return "wgrad3x3w36_kernel";
     case WGV_W32: return "wgrad3x3_bf16_kernel";
+    case WGV_W32C64: return "wgrad3x3c64_kernel";
+    case WGV_W36C64: return "wgrad3x3w36c64_kernel";
     case WGV_S2: return "wgrads2_bf16_kernel";
     case WGV_WIDE: {
       const int bm = (Cout % 256 == 0 && Co1 % 256 == 0) ? 256 : ((Cout % 128 == 0 && Co1 % 128 == 0) ? 128 : 64);
@@ -3479,11 +3807,25 @@ int cesm_conv_wgrad(int dtype, const void* x1, const void* x2, const void* dy1, 
   const int K = KH * KW * Cin;
   dim3 grid(Cout / 64, K / 64, nsplit);
   const int wv = wgrad_plan(dtype, M, Hi, Wi, Ho, Wo, KH, KW, S, P, U);
-  if (wv == WGV_W36) {
+  if (wv == WGV_W36C64) {
+    const int tx = Wo / W36_TW;
+    const int ntiles = Nb * tx * (int)cdiv(Ho, W36_TH);
+    dim3 g3(Cout / 64, Cin / 64, std::min(nsplit, ntiles));
+    wgrad3x3w36c64_kernel<<<g3, 512, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
+                                                  (const bf16*)dy2, slab, g, tx, ntiles);
+    nsplit = (int)g3.z;
+  } else if (wv == WGV_W36) {
     const int tx = Wo / W36_TW;
     const int ntiles = Nb * tx * (int)cdiv(Ho, W36_TH);
     dim3 g3(Cout / 64, Cin / 32, std::min(nsplit, ntiles));
     wgrad3x3w36_kernel<<<g3, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
+                                               (const bf16*)dy2, slab, g, tx, ntiles);
+    nsplit = (int)g3.z;
+  } else if (wv == WGV_W32C64) {
+    const int tx = (int)cdiv(Wo, W3_TW);
+    const int ntiles = Nb * tx * (int)cdiv(Ho, W3_TH);
+    dim3 g3(Cout / 64, Cin / 64, std::min(nsplit, ntiles));
+    wgrad3x3c64_kernel<<<g3, 512, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
                                                (const bf16*)dy2, slab, g, tx, ntiles);
     nsplit = (int)g3.z;
   } else if (wv == WGV_W32) {

@@ -111,6 +111,7 @@ __global__ __launch_bounds__(256) void gn_part_finalize_kernel(const float2* __r
   const int64_t n = nslot * qpg;
   const float2* base = part + (int64_t)b * nslot * nq + g * qpg;
   double a = 0.0, q = 0.0;
+#pragma unroll 8
   for (int64_t e = threadIdx.x; e < n; e += 256) {
     const int64_t sl = e / qpg;
     const float2 v = base[sl * nq + (e - sl * qpg)];

@@ -125,7 +125,7 @@ def test_wgrad_fused_bias(dev, cin, cout, k, st):
     assert torch.equal(dw1, dw2)
 
 
-@pytest.mark.parametrize("H,W,cin,cout", [(12, 72, 64, 64), (8, 36, 128, 64), (6, 36, 64, 128)])
+@pytest.mark.parametrize("H,W,cin,cout", [(12, 72, 64, 64), (8, 36, 128, 64), (6, 36, 64, 128), (10, 36, 256, 512), (20, 64, 128, 64)])
 def test_conv3x3_tile_shapes_bf16(dev, H, W, cin, cout):
     """widths that are multiples of 36 take the 36-wide halo tiles (fwd/dgrad) and the 8 x 36 weight-
     gradient tiles; heights that are not tile multiples leave partial tile rows"""

@@ -158,7 +158,7 @@ def test_bench_shape_dispatch_table():
     wv = lambda *a, **k: K.conv_wgrad_variant(bf, N, *a, **k)  # noqa: E731
     # level 0, 64 -> 64 3x3 (fwd and dgrad): the persistent resident-weight kernel
     assert fv(192, 288, 64, 0, 192, 288, 64, 64, 3, 3, 1, 1, 1) == "conv3x3p_kernel<32,7,true>"
-    assert wv(192, 288, 64, 0, 192, 288, 64, 64, 3, 3, 1, 1, 1) == "wgrad3x3_bf16_kernel"
+    assert wv(192, 288, 64, 0, 192, 288, 64, 64, 3, 3, 1, 1, 1) == "wgrad3x3c64_kernel"
     # level-0 concat inputs (up path / out_conv: 64 + 64 -> 64)
     assert fv(192, 288, 64, 64, 192, 288, 64, 64, 3, 3, 1, 1, 1) == "conv3x3_bf16_kernel<32>"
     # levels 1-3 (144, 72, 36 wide)
