@@ -165,7 +165,7 @@ def test_bench_shape_dispatch_table():
     assert fv(96, 144, 128, 0, 96, 144, 128, 128, 3, 3, 1, 1, 1) == "conv3x3_bf16_kernel<32>"
     assert fv(48, 72, 256, 0, 48, 72, 256, 256, 3, 3, 1, 1, 1) == "conv3x3_bf16_kernel<36>"
     assert fv(24, 36, 512, 0, 24, 36, 512, 512, 3, 3, 1, 1, 1) == "conv3x3_bf16_kernel<36>"
-    assert wv(24, 36, 512, 0, 24, 36, 512, 512, 3, 3, 1, 1, 1) == "wgrad3x3w36_kernel"
+    assert wv(24, 36, 512, 0, 24, 36, 512, 512, 3, 3, 1, 1, 1) == "wgrad3x3w36c64_kernel"
     # 768-channel qkv weight gradient of the fused attention blocks; the SLA to_out with its bias
     assert wv(192, 288, 64, 0, 192, 288, 768, 768, 1, 1, 1, 0, 1) == "wgrad_wide_kernel<256,false>"
     assert wv(192, 288, 256, 0, 192, 288, 64, 64, 1, 1, 1, 0, 1, with_bias=True) == "wgrad_wide_kernel<64,true>"
