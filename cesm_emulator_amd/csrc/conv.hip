@@ -481,6 +481,9 @@ constexpr int H3_WPT = H3_WVEC / 256;
 // tap offsets ky * H3_P and tap * 64 stay immediate.
 __device__ __forceinline__ int h3_off(int row, int ch) { return row * H3_LD + ((ch ^ ((row >> 1) & 2)) << 3); }
 
+#ifndef H3_PIPE
+#define H3_PIPE 1  // conv3x3_bf16_kernel: software-pipelined tap fragments (0: the compiler's read -> MFMA order)
+#endif
 template <int TW>
 __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
                                                               const bf16* __restrict__ w, const float* __restrict__ bias,
@@ -581,6 +584,39 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
     if (ch) __syncthreads();  // previous chunk fully consumed
     stage(ch);
     __syncthreads();
+#if H3_PIPE
+    // the 10 fragment reads of tap t+1 are issued between the 16 MFMAs of tap t (two register sets), so no
+    // MFMA waits on a read issued just before it (the compiler's order was read -> wait -> 2 MFMAs)
+    bf16x8 fa[2][2], fb[2][8];
+    auto rd = [&](int tap, int b) {
+      const int ky = tap / 3, kx = tap - ky * 3;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[b][i] = *reinterpret_cast<const bf16x8*>(sw + aoff[i] + tap * H3_BN * H3_LD);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) fb[b][j] = *reinterpret_cast<const bf16x8*>(sh + boff[j][kx] + ky * H3_P * H3_LD);
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int b = tap & 1;
+      __builtin_amdgcn_sched_barrier(0);
+      if (tap + 1 < 9) rd(tap + 1, b ^ 1);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[b][0], fb[b][j], acc[0][j], 0, 0, 0);
+        acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[b][1], fb[b][j], acc[1][j], 0, 0, 0);
+      }
+      if (tap + 1 < 9) {
+#pragma unroll
+        for (int q2 = 0; q2 < 10; ++q2) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#else
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int ky = tap / 3, kx = tap - ky * 3;
@@ -595,6 +631,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
         acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bfr, acc[1][j], 0, 0, 0);
       }
     }
+#endif
   }
   // epilogue: lane holds co = n0 + wr*32 + i*16 + 4*lg + r of pixel (py, px)
   const int Co2 = g.Cout - g.Co1;
