@@ -1550,6 +1550,18 @@ extern "C" int cesm_diag_tw_stamps(unsigned long long* out, int n) {
 #ifndef TWH_PG
 #define TWH_PG 2        // twh_bwd: pixels whose attention-core backward is interleaved phase by phase
 #endif
+#ifndef TWH_QKV_PIPE
+#define TWH_QKV_PIPE 1  // twh_bwd: double-buffered q/k/v weight batches, the first issued before barrier A
+#endif
+#ifndef TWH_WPIPE
+#define TWH_WPIPE 1  // twh_bwd: the dxn GEMM's weight fragments in a TWH_RING-deep ring
+#endif
+#ifndef TWH_RING
+#define TWH_RING 2
+#endif
+#ifndef TWH_DO_PF
+#define TWH_DO_PF 1  // twh_bwd: the dO GEMM's weights issued during the last q/k/v batch (needs QKV_PIPE)
+#endif
 #ifndef TWH_EARLY_WT
 #define TWH_EARLY_WT 0  // twh_bwd: W'^T fragments of the dxn GEMM issued before the dW GEMM (1)
 #endif
@@ -1664,6 +1676,23 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
     const bf16* wq_g = wqkv + oz;
     const bf16* wqt_g = wqkv_t + oz;
     const bf16* wot_g = wout_t + oz;
+#if TWH_QKV_PIPE
+    // q/k/v weight fragments in two-tile batches, double-buffered: batch 0 issued before barrier A (its L2
+    // latency overlaps the barrier wait), batch c+1 issued before batch c's MFMAs
+    bf16x8 wqa[2][2][T::KS];
+#if TWH_DO_PF
+    bf16x8 wob[2][T::KS];
+#endif
+    auto ldq = [&](int c2, int buf) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int ct = c2 + u, mt = (ct >> 1) * 16 + h * 2 + (ct & 1);
+#pragma unroll
+        for (int ks = 0; ks < T::KS; ++ks) wqa[buf][u][ks] = ld_img(wq_g, mt, T::KS, ks, lane);
+      }
+    };
+    ldq(0, 0);
+#endif
     __syncthreads();  // (A) tiles of this group ready; previous group's partials consumed
     prefetch(gg + gridDim.x);  // next group's x / dy / stats: in flight during the head phase
     TW_ST(0)
@@ -1682,7 +1711,43 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
       for (int vt = 0; vt < NV; ++vt)
 #pragma unroll
         for (int ks = 0; ks < T::KS; ++ks) xf[vt][ks] = ld16(xt + (vt * 16 + lr) * TH_XLD + ks * 32 + lg * 8);
+#if TWH_QKV_PIPE
+#pragma unroll
+      for (int c2 = 0; c2 < 6; c2 += 2) {
+        const int buf = (c2 >> 1) & 1;
+        if (c2 + 2 < 6) ldq(c2 + 2, buf ^ 1);
+#if TWH_DO_PF
+        else {  // the dO GEMM's W_out^T fragments, in flight during the last q/k/v batch
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int ks = 0; ks < T::KS; ++ks) wob[dt][ks] = ld_img(wot_g, h * 2 + dt, T::KS, ks, lane);
+        }
+#endif
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int ct = c2 + u, kind = ct >> 1;
+          bf16* dst = kind == 0 ? sq : (kind == 1 ? sk : sv);
+          const int d0 = (ct & 1) * 16 + lg * 4;
+#pragma unroll
+          for (int vt = 0; vt < NV; ++vt) {
+            f32x4 acc = z4;
+#pragma unroll
+            for (int ks = 0; ks < T::KS; ++ks)
+              acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wqa[buf][u][ks], xf[vt][ks], acc, 0, 0, 0);
+            float o4[4] = {acc[0], acc[1], acc[2], acc[3]};
+            if (kind == 0) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) o4[r] *= scale;
+            }
+            if (kind < 2) rope4(o4, rot, fr[vt], d0, 1.f);
+            store4(dst + (vt * 16 + lr) * HLD + d0, o4);
+          }
+        }
+      }
+#else
       tw_qkv<C, NV, TWH_FULL != 0>(wq_g, xf, h, fr, scale, rot, sq, sk, sv, lr, lg);
+#endif
     }
     TW_ST(1)
     // dO_h^T = W_out[:, h]^T . dy^T
@@ -1690,7 +1755,13 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
     for (int dt = 0; dt < 2; ++dt) {
       bf16x8 a[T::KS];
 #pragma unroll
-      for (int ks = 0; ks < T::KS; ++ks) a[ks] = ld_img(wot_g, h * 2 + dt, T::KS, ks, lane);
+      for (int ks = 0; ks < T::KS; ++ks) {
+#if TWH_DO_PF
+        a[ks] = wob[dt][ks];
+#else
+        a[ks] = ld_img(wot_g, h * 2 + dt, T::KS, ks, lane);
+#endif
+      }
 #pragma unroll
       for (int vt = 0; vt < NV; ++vt) {
         f32x4 acc = z4;
@@ -1805,6 +1876,13 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
 #pragma unroll
         for (int ct = 0; ct < T::CT; ++ct) wt[kind][ct] = ld_img(wqt_g, ct, QKV / 32, kind * 8 + h, lane);
     }
+#if TWH_WPIPE
+    // the dxn GEMM's W'^T fragments (kind, ct) in a 3-deep ring: the first two in flight during the dW GEMM
+    bf16x8 wring[TWH_RING];
+    auto ldw = [&](int idx) { return ld_img(wqt_g, idx % T::CT, QKV / 32, (idx / T::CT) * 8 + h, lane); };
+#pragma unroll
+    for (int r = 0; r < TWH_RING - 1; ++r) wring[r] = ldw(r);
+#endif
     // dW'_h += dqkv_h^T . xhat over the group's voxels (K = voxels, 16 per step; padded rows are zero)
 #pragma unroll
     for (int kk = 0; kk < NV; ++kk) {
@@ -1833,7 +1911,13 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
       const bf16* src = kind == 0 ? sq : (kind == 1 ? sk : sv);
 #pragma unroll
       for (int ct = 0; ct < T::CT; ++ct) {
+#if TWH_WPIPE
+        const int idx = kind * T::CT + ct;
+        if (idx + TWH_RING - 1 < 3 * T::CT) wring[(idx + TWH_RING - 1) % TWH_RING] = ldw(idx + TWH_RING - 1);
+        const bf16x8 a = wring[idx % TWH_RING];
+#else
         const bf16x8 a = TWH_EARLY_WT != 0 ? wt[kind][ct] : ld_img(wqt_g, ct, QKV / 32, kind * 8 + h, lane);
+#endif
 #pragma unroll
         for (int vt = 0; vt < NV; ++vt)
           dxacc[ct][vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ld16(src + (vt * 16 + lr) * HLD + lg * 8),
