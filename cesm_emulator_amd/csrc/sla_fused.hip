@@ -953,6 +953,9 @@ __device__ __forceinline__ void wave_lds_sync_s() {
 // the 8 shares summed through LDS -> LN backward -> dx.  No per-voxel intermediate reaches HBM (slab_dx
 // emitted the 768-channel dqkv and xn for a separate weight-gradient GEMM).
 // ===================================================================================================
+#ifndef SLAH_WPIPE
+#define SLAH_WPIPE 1  // slah_dx: weight fragments issued one GEMM step ahead (first before barrier A / the dW GEMM)
+#endif
 constexpr int SH_XLD = 72;   // xhat / dy tile row stride (bf16)
 constexpr int SH_SLD = 136;  // slice row stride (bf16): raw q|k|v|do (128 cols), then dq|dk|dv; fp32 partials over it
 constexpr int SH_PLD = 68;   // fp32 partial dxn row stride
@@ -1040,18 +1043,36 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
     const bf16* wq_g = wqkv + oz;
     const bf16* wqt_g = wqkv_t + oz;
     const bf16* wot_g = wout_t + oz;
+#if SLAH_WPIPE
+    // phase A's weight fragments double-buffered per kind: kind 0 issued before barrier A (its L2 latency
+    // overlaps the barrier wait), kind k+1 before kind k's MFMAs
+    bf16x8 wa[2][2][KS];
+    auto lda = [&](int kind, int buf) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+          wa[buf][t][ks] = kind < 3 ? ld_img(wq_g, kind * 16 + h * 2 + t, KS, ks, lane) : ld_img(wot_g, h * 2 + t, KS, ks, lane);
+    };
+    lda(0, 0);
+#endif
     __syncthreads();  // (A)
     prefetch(gg + gridDim.x);
 
     // ---- phase A: raw q | k | v | do of head h, rows = pixels, cols kind*32 + d
 #pragma unroll
     for (int kind = 0; kind < 4; ++kind) {
+#if SLAH_WPIPE
+      if (kind + 1 < 4) lda(kind + 1, (kind + 1) & 1);
+      const auto& a = wa[kind & 1];
+#else
       bf16x8 a[2][KS];
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks)
           a[t][ks] = kind < 3 ? ld_img(wq_g, kind * 16 + h * 2 + t, KS, ks, lane) : ld_img(wot_g, h * 2 + t, KS, ks, lane);
+#endif
       const bf16* src = kind < 3 ? xt : dyt;
 #pragma unroll
       for (int vt = 0; vt < NV; ++vt) {
@@ -1162,6 +1183,12 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
       }
     }
     wave_lds_sync_s();
+#if SLAH_WPIPE
+    // the dxn GEMM's W'^T fragments one ahead: the first in flight during the dW GEMM
+    bf16x8 wring[2];
+    auto ldw = [&](int idx) { return ld_img(wqt_g, idx % CT, QKV / 32, (idx / CT) * 8 + h, lane); };
+    wring[0] = ldw(0);
+#endif
     // ---- dW'_h += dqkv_h^T . xhat (K = pixels, 16 per step)
 #pragma unroll
     for (int kk = 0; kk < NV; ++kk) {
@@ -1186,7 +1213,13 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
     for (int kind = 0; kind < 3; ++kind)
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
+#if SLAH_WPIPE
+        const int idx = kind * CT + ct;
+        if (idx + 1 < 3 * CT) wring[(idx + 1) & 1] = ldw(idx + 1);
+        const bf16x8 a = wring[idx & 1];
+#else
         const bf16x8 a = ld_img(wqt_g, ct, QKV / 32, kind * 8 + h, lane);
+#endif
 #pragma unroll
         for (int vt = 0; vt < NV; ++vt)
           dxacc[ct][vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ld16(sl + (vt * 16 + lr) * SH_SLD + kind * 32 + lg * 8),
