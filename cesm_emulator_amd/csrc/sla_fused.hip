@@ -84,23 +84,33 @@ __global__ __launch_bounds__(512) void slaf_stats_kernel(const bf16* __restrict_
 #pragma unroll
     for (int b = 0; b < 2; ++b) uT[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  // the next 64-pixel chunk's x vectors are loaded into registers while the current one is consumed
+  constexpr int NPASS = 64 / PPP;
+  const int sub = tid % L;
+  bf16x8 xr[NPASS];
+  auto gload = [&](int sc) {
+#pragma unroll
+    for (int k = 0; k < NPASS; ++k) {
+      const int p = sc * 64 + k * PPP + tid / L;
+      xr[k] = *reinterpret_cast<const bf16x8*>(xf + (int64_t)(p < HW ? p : 0) * C + sub * 8);  // row 0 past HW
+    }
+  };
+  if (sc0 < sc1) gload(sc0);
+  float gm8[8];
+  load8(gamma + sub * 8, gm8);
 
   for (int sc = sc0; sc < sc1; ++sc) {
     const int p0 = sc * 64;
     __syncthreads();
     // LN of 64 pixels into xs (rows beyond HW zero)
     {
-      const int sub = tid % L;
-      float gm8[8];
-      load8(gamma + sub * 8, gm8);
 #pragma unroll
       for (int pp0 = 0; pp0 < 64; pp0 += PPP) {
         const int pl = pp0 + tid / L;
         const int p = p0 + pl;
         float a[8];
-        load8(xf + (int64_t)(p < HW ? p : 0) * C + sub * 8, a);  // unpredicated (row 0 past HW), selected
 #pragma unroll
-        for (int i = 0; i < 8; ++i) a[i] = p < HW ? a[i] : 0.f;
+        for (int i = 0; i < 8; ++i) a[i] = p < HW ? (float)xr[pp0 / PPP][i] : 0.f;
         float sm = 0.f;
 #pragma unroll
         for (int i = 0; i < 8; ++i) sm += a[i];
@@ -117,6 +127,7 @@ __global__ __launch_bounds__(512) void slaf_stats_kernel(const bf16* __restrict_
       }
     }
     __syncthreads();
+    if (sc + 1 < sc1) gload(sc + 1);
     // k, v of this head for 64 pixels: D[px = vt*16 + 4g + r][ch = t*16 + i]
     f32x4 kk[4][2], vv[4][2];
 #pragma unroll
@@ -498,21 +509,33 @@ __global__ __launch_bounds__(512) void slab_dctx_kernel(const bf16* __restrict__
 #pragma unroll
     for (int b = 0; b < 2; ++b) dc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  // the next 64-pixel chunk's x / dy vectors are loaded into registers while the current one is consumed
+  constexpr int NPASS = 64 / PPP;
+  const int sub = tid % L;
+  bf16x8 xr[NPASS], dr[NPASS];
+  auto gload = [&](int sc) {
+#pragma unroll
+    for (int k = 0; k < NPASS; ++k) {
+      const int p = sc * 64 + k * PPP + tid / L;
+      const int64_t ps = p < HW ? p : 0;  // unpredicated loads (row 0 past HW), selected when staged
+      xr[k] = *reinterpret_cast<const bf16x8*>(xb + ps * C + sub * 8);
+      dr[k] = *reinterpret_cast<const bf16x8*>(db + ps * C + sub * 8);
+    }
+  };
+  if (sc0 < sc1) gload(sc0);
+  float gm8[8];
+  load8(gamma + sub * 8, gm8);
   for (int sc = sc0; sc < sc1; ++sc) {
     const int p0 = sc * 64;
     __syncthreads();
     {
-      const int sub = tid % L;
-      float gm8[8];
-      load8(gamma + sub * 8, gm8);
 #pragma unroll
       for (int pp0 = 0; pp0 < 64; pp0 += PPP) {
         const int pl = pp0 + tid / L;
         const int p = p0 + pl;
         float a[8], d8[8];
-        const int64_t ps = p < HW ? p : 0;  // unpredicated loads (row 0 past HW), then selected
-        load8(xb + ps * C + sub * 8, a);
-        load8(db + ps * C + sub * 8, d8);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { a[i] = (float)xr[pp0 / PPP][i]; d8[i] = (float)dr[pp0 / PPP][i]; }
 #pragma unroll
         for (int i = 0; i < 8; ++i) { a[i] = p < HW ? a[i] : 0.f; d8[i] = p < HW ? d8[i] : 0.f; }
         float sm = 0.f;
@@ -532,6 +555,7 @@ __global__ __launch_bounds__(512) void slab_dctx_kernel(const bf16* __restrict__
       }
     }
     __syncthreads();
+    if (sc + 1 < sc1) gload(sc + 1);
     float qt[4][2][4], dv[4][2][4];  // q~ [px tile][d tile][r], do [px tile][e tile][r]
 #pragma unroll
     for (int vt = 0; vt < 4; ++vt) {
