@@ -1385,6 +1385,13 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
       // the plain path keeps its own loop (uniform branch)
       constexpr int CP_RB = 4;
       if (!rsrc) {
+        // all rows of the round read from LDS first, then stored (one ds_read -> wait -> store chain per row
+        // exposed the LDS latency 14 times per item)
+        bf16x8 rows[2 * RG];
+#pragma unroll
+        for (int u = 0; u < 2 * RG; ++u)
+          if (u < 2 * nj) rows[u] = *reinterpret_cast<const bf16x8*>(so + (u * 8 + (lane >> 3)) * CP_ELD + (lane & 7) * 8);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int u = 0; u < 2 * RG; ++u) {
           if (u < 2 * nj) {
@@ -1393,8 +1400,8 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
             const int oy = y0 + p / TW, ox = x0 + (p - (p / TW) * TW);
             const bool ok = p < TH * TW && oy < g.Ho && ox < g.Wo;
             const int off = (ok ? oy * g.Wo + ox : 0) * cstride + cofs;
-            const bf16x8 v = *reinterpret_cast<const bf16x8*>(so + pl * CP_ELD + (lane & 7) * 8);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yrs, ok ? off * 2 : 0x7ffffff0, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, rows[u]), yrs,
+                                                   ok && !(dbg & 8) ? off * 2 : 0x7ffffff0, 0, 0);
           }
         }
       } else {
@@ -1414,12 +1421,15 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
           if (u < 2 * nj)
             rv[uu] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rrs, offs[uu] * 2, 0, 0));
         }
+        bf16x8 rows[CP_RB];
+#pragma unroll
+        for (int uu = 0; uu < CP_RB; ++uu)
+          if (u0 + uu < 2 * nj) rows[uu] = *reinterpret_cast<const bf16x8*>(so + ((u0 + uu) * 8 + (lane >> 3)) * CP_ELD + (lane & 7) * 8);
 #pragma unroll
         for (int uu = 0; uu < CP_RB; ++uu) {
           const int u = u0 + uu;
           if (u < 2 * nj) {
-            const int pl = u * 8 + (lane >> 3);
-            bf16x8 v = *reinterpret_cast<const bf16x8*>(so + pl * CP_ELD + (lane & 7) * 8);
+            bf16x8 v = rows[uu];
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = (bf16)((float)v[e] + (float)rv[uu][e]);
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yrs, oks[uu] ? offs[uu] * 2 : 0x7ffffff0,
@@ -3644,7 +3654,7 @@ int conv_fwd_launch(int dtype, const void* x1, const void* x2, const void* wp, c
     case CFV_P32_RW:
     case CFV_P32: {
       const int dbg = (getenv_flag("CESM_DBG_NODMA") ? 1 : 0) | (getenv_flag("CESM_DBG_NOMFMA") ? 2 : 0) |
-                      (getenv_flag("CESM_DBG_NOEPI") ? 4 : 0) | (getenv_flag("CESM_DBG_CLOCK") ? 16 : 0);
+                      (getenv_flag("CESM_DBG_NOEPI") ? 4 : 0) | (getenv_flag("CESM_DBG_NOSTORE") ? 8 : 0);
       const int tx = (int)cdiv(Wo, TW), ty = (int)cdiv(Ho, TH);
       const int ncob = Cout / 64;
       const int nitems = Nb * tx * ty * ncob;

@@ -36,6 +36,12 @@ def main():
         t = timed(lambda: K.conv_fwd(x, x2, wp, None, (H, W, Co, 3, 3, 1, 1, 1)))
         fl = 2 * 9 * (C + C2) * Co * N * H * W
         out.append(f"{H}x{W}x{C}+{C2}->{Co} {v}: {t:.1f} us ({fl / t / 1e6:.0f} TF/s)")
+    # level-0 conv with the fused residual (the ResnetBlock skip gradient in the dgrad)
+    x = torch.randn(N, 192, 288, 64, device=dev).to(torch.bfloat16)
+    r = torch.randn_like(x)
+    wp = K.conv_pack(torch.randn(64, 64, 1, 3, 3, device=dev) * 0.02, torch.bfloat16, 64, 64, 3, 3, 0, 0)
+    t = timed(lambda: K.conv_fwd(x, None, wp, None, (192, 288, 64, 3, 3, 1, 1, 1), res=r))
+    out.append(f"192x288x64 + residual: {t:.1f} us")
     print(f"[{tag}] " + " | ".join(out), flush=True)
 
 
