@@ -480,12 +480,19 @@ __device__ __forceinline__ float row16_sum(float v) {
 }
 
 // grid (nblk, Nf), 512 threads; partial per (n, b, h): dctx[32 d][32 e]
-template <int C>
+// DWO (C = 64, the in-kernel-dW backward): also the to_out weight / bias gradient inputs without the forward's
+// 256-channel O: O_h = ctx_h^T q~_h per pixel, so dW_out[:, h] = (sum_px dy q~_h^T) ctx_h — the per-block
+// M_h = sum_px dy q~_h^T (64 x 32, K = pixels on MFMA: dy^T by k-slot transposed reads from the staged tile, q~ the
+// packed fragment the dctx product already uses) goes to partm [n][blk][h][64][32], sum_px dy to partb [n][blk][C]
+template <int C, bool DWO = false>
 __global__ __launch_bounds__(512) void slab_dctx_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
                                                         const float* __restrict__ gamma, const bf16* __restrict__ wqkv,
                                                         const bf16* __restrict__ wout_t, float* __restrict__ part,
-                                                        int HW, int spb, float scale, float eps) {
+                                                        int HW, int spb, float scale, float eps,
+                                                        float* __restrict__ partm = nullptr,
+                                                        float* __restrict__ partb = nullptr) {
   constexpr int KS = C / 32, XLD = C + 8, L = C / 8, PPP = 512 / L;
+  static_assert(!DWO || C == 64, "to_out gradient inputs at C = 64 only");
   __shared__ __attribute__((aligned(16))) bf16 xs[64 * XLD];
   __shared__ __attribute__((aligned(16))) bf16 ds[64 * XLD];
   const int tid = threadIdx.x, lane = tid & 63, h = tid >> 6;
@@ -509,6 +516,12 @@ __global__ __launch_bounds__(512) void slab_dctx_kernel(const bf16* __restrict__
 #pragma unroll
     for (int b = 0; b < 2; ++b) dc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  f32x4 macc[4][2];  // DWO: M_h [c tile][d tile]
+  float bsum[8];     // DWO: this thread's sum of dy over its pixels, channels sub*8 ..
+#pragma unroll
+  for (int a = 0; a < 4; ++a) macc[a][0] = macc[a][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 8; ++i) bsum[i] = 0.f;
   // the next 64-pixel chunk's x / dy vectors are loaded into registers while the current one is consumed
   constexpr int NPASS = 64 / PPP;
   const int sub = tid % L;
@@ -550,6 +563,10 @@ __global__ __launch_bounds__(512) void slab_dctx_kernel(const bf16* __restrict__
         const float rstd = 1.f / sqrtf(q / C + eps);
 #pragma unroll
         for (int i = 0; i < 8; ++i) a[i] = p < HW ? (a[i] - mean) * rstd * gm8[i] : 0.f;
+        if constexpr (DWO) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) bsum[i] += d8[i];
+        }
         store8(xs + pl * XLD + sub * 8, a);
         store8(ds + pl * XLD + sub * 8, d8);
       }
@@ -600,6 +617,52 @@ __global__ __launch_bounds__(512) void slab_dctx_kernel(const bf16* __restrict__
       for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b) dc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Aq[a], Bd[b], dc[a][b], 0, 0, 0);
+      if constexpr (DWO) {
+        // dy^T as the A operand: lane (i = channel, g) element e = dy[px of k-slot (g, e)][ct*16 + i]
+        const int g = lane >> 4, qq = (lane >> 2) & 3, pq = lane & 3;
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) {
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (LDS_PTR(s16x4))(ds + (va * 16 + 4 * g + qq) * XLD + ct * 16 + 4 * pq));
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (LDS_PTR(s16x4))(ds + (vb * 16 + 4 * g + qq) * XLD + ct * 16 + 4 * pq));
+          bf16x8 ady;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            ady[e] = __builtin_bit_cast(bf16, (short)lo[e]);
+            ady[4 + e] = __builtin_bit_cast(bf16, (short)hi[e]);
+          }
+#pragma unroll
+          for (int t = 0; t < 2; ++t) macc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ady, Aq[t], macc[ct][t], 0, 0, 0);
+        }
+      }
+    }
+  }
+  if constexpr (DWO) {
+    float* om = partm + (((int64_t)n * gridDim.x + blockIdx.x) * NH + h) * 2048;  // [c][d]
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) om[(ct * 16 + lg * 4 + r) * 32 + t * 16 + lr] = macc[ct][t][r];
+    // bias: threads sharing sub (lanes l, l^8, l^16, ... and the 8 waves) summed in a fixed order
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int o = 8; o < 64; o <<= 1) bsum[i] += __shfl_xor(bsum[i], o, 64);
+    __syncthreads();
+    float* sb = reinterpret_cast<float*>(xs);  // [8 waves][64 channels]
+    if (lane < 8) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) sb[h * 64 + lane * 8 + i] = bsum[i];
+    }
+    __syncthreads();
+    if (tid < 64) {
+      float b = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) b += sb[w * 64 + tid];
+      partb[((int64_t)n * gridDim.x + blockIdx.x) * 64 + tid] = b;
     }
   }
   float* o = part + (((int64_t)n * gridDim.x + blockIdx.x) * NH + h) * 1024;
@@ -609,6 +672,41 @@ __global__ __launch_bounds__(512) void slab_dctx_kernel(const bf16* __restrict__
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int r = 0; r < 4; ++r) o[(a * 16 + lg * 4 + r) * 32 + b * 16 + lr] = dc[a][b][r];
+}
+
+// to_out weight gradient from slab_dctx<64, true>'s partials: per (frame n, head h) R[c][e] = sum_d
+// (sum_blk M[n][blk][h][c][d]) ctx32[n][h][d][e]  (grid Nf * 8, 256 threads; fixed-order sums)
+__global__ __launch_bounds__(256) void slab_dwout_frame_kernel(const float* __restrict__ partm, int nblk,
+                                                               const float* __restrict__ ctx32, float* __restrict__ R) {
+  __shared__ float sm[64][33];
+  __shared__ float sc[32][33];
+  const int nh = blockIdx.x, n = nh / NH, h = nh % NH, tid = threadIdx.x;
+  for (int i = tid; i < 1024; i += 256) sc[i >> 5][i & 31] = ctx32[(int64_t)nh * 1024 + i];
+  const float* pm = partm + ((int64_t)n * nblk * NH + h) * 2048;
+  for (int i = tid; i < 2048; i += 256) {
+    float m = 0.f;
+    for (int b = 0; b < nblk; ++b) m += pm[(int64_t)b * NH * 2048 + i];
+    sm[i >> 5][i & 31] = m;
+  }
+  __syncthreads();
+  for (int i = tid; i < 2048; i += 256) {
+    const int c = i >> 5, e = i & 31;
+    float r = 0.f;
+#pragma unroll 8
+    for (int d = 0; d < 32; ++d) r = fmaf(sm[c][d], sc[d][e], r);
+    R[(int64_t)nh * 2048 + i] = r;
+  }
+}
+
+// dwout [C = 64][256] (+)= sum over frames of R[n][h][c][e] at column h*32 + e (thread per output element)
+__global__ __launch_bounds__(256) void slab_dwout_sum_kernel(const float* __restrict__ R, int Nf, float* __restrict__ dwout,
+                                                             int accumulate) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;  // (c, h, e)
+  if (idx >= 64 * 256) return;
+  const int c = idx >> 8, k = idx & 255, h = k >> 5, e = k & 31;
+  float s = 0.f;
+  for (int n = 0; n < Nf; ++n) s += R[((int64_t)(n * NH + h) * 64 + c) * 32 + e];
+  dwout[idx] = accumulate ? dwout[idx] + s : s;
 }
 
 // grid (Nf * 8), 256 threads: dctx = sum of partials; G; A-fragment images adc (rows d / k = e) and
@@ -1413,10 +1511,12 @@ int cesm_slaf_bwd_dw_nblk(int Nf, int HW, int C) {
 // wimg (2*768 + 256)*C bf16.
 int cesm_slaf_bwd_dw(const void* x, const void* dy, const float* gamma_one, const void* wq_fold, const float* wqkv_f32,
                      const float* gamma, const void* wout_t, const float* mz, const float* ctx32, const void* actT,
-                     const void* actx, void* dx, float* dwqkv, float* dgamma, float* part, float* G, void* adc,
-                     void* adcT, float* slab, float* tmp, void* wimg, int nblk_dx, int Nf, int HW, int C, float scale,
-                     float eps, int accumulate, hipStream_t stream) {
+                     const void* actx, void* dx, float* dwqkv, float* dgamma, float* dwout, float* dbout, float* part,
+                     float* G, void* adc, void* adcT, float* slab, float* tmp, float* partm, float* partb, void* wimg,
+                     int nblk_dx, int Nf, int HW, int C, float scale, float eps, int accumulate, hipStream_t stream) {
   if (nblk_dx < 1 || nblk_dx != cesm_slaf_bwd_dw_nblk(Nf, HW, C)) return CESM_EUNSUPPORTED;
+  const bool dwo = dwout || dbout;
+  if (dwo && (!partm || !partb || !dwout || !dbout)) return CESM_EINVAL;
   bf16* img_q = (bf16*)wimg;
   bf16* img_qt = img_q + 768 * C;
   bf16* img_ot = img_qt + 768 * C;
@@ -1427,9 +1527,20 @@ int cesm_slaf_bwd_dw(const void* x, const void* dy, const float* gamma_one, cons
   const int nsc = (HW + 63) / 64;
   const int nblk = cesm_slaf_nblk(Nf, HW);
   const int spb = (nsc + nblk - 1) / nblk;
-  slab_dctx_kernel<64><<<dim3(nblk, Nf), 512, 0, stream>>>((const bf16*)x, (const bf16*)dy, gamma_one,
-                                                           (const bf16*)wq_fold, (const bf16*)wout_t, part, HW, spb,
-                                                           scale, eps);
+  if (dwo) {
+    slab_dctx_kernel<64, true><<<dim3(nblk, Nf), 512, 0, stream>>>((const bf16*)x, (const bf16*)dy, gamma_one,
+                                                                   (const bf16*)wq_fold, (const bf16*)wout_t, part, HW,
+                                                                   spb, scale, eps, partm, partb);
+    // partm is re-used for R once the per-frame products are formed (R: Nf*8*2048 floats <= partm)
+    float* R = partm + (int64_t)Nf * nblk * NH * 2048;
+    slab_dwout_frame_kernel<<<Nf * NH, 256, 0, stream>>>(partm, nblk, ctx32, R);
+    slab_dwout_sum_kernel<<<64, 256, 0, stream>>>(R, Nf, dwout, accumulate);
+    slaf_sum_rows_kernel<<<64, 256, 0, stream>>>(partb, dbout, Nf * nblk, 64, accumulate);
+  } else {
+    slab_dctx_kernel<64><<<dim3(nblk, Nf), 512, 0, stream>>>((const bf16*)x, (const bf16*)dy, gamma_one,
+                                                             (const bf16*)wq_fold, (const bf16*)wout_t, part, HW, spb,
+                                                             scale, eps);
+  }
   slab_combine_kernel<<<Nf * NH, 256, 0, stream>>>(part, nblk, ctx32, mz, G, (bf16*)adc, (bf16*)adcT);
   const size_t sm = slah_smem(3);
   hipFuncSetAttribute((const void*)slah_dx_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);

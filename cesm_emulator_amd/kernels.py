@@ -551,10 +551,12 @@ def slaf_bwd_dw_supported(Nf, HW, C):
     return lib().cesm_slaf_bwd_dw_nblk(Nf, HW, C) > 0
 
 
-def slaf_bwd_dw(x, dy, gamma_one, wq_fold, wqkv_f32, gamma, wout_t, state, dwqkv, dgamma, scale, eps=1e-5):
+def slaf_bwd_dw(x, dy, gamma_one, wq_fold, wqkv_f32, gamma, wout_t, state, dwqkv, dgamma, scale, eps=1e-5,
+                dwout=None, dbout=None):
     """fused SLA block backward with in-kernel weight gradients (C = 64); the forward must have been
     slaf_fwd(x, gamma_one, wq_fold, ...) with wq_fold = pack_scaled(wqkv_f32, gamma).  Returns dx; dwqkv /
-    dgamma (+)= the to_qkv / LN gamma gradients (nullable)."""
+    dgamma (+)= the to_qkv / LN gamma gradients, dwout [C, 256] / dbout [C] (+)= the to_out weight / bias
+    gradients (both or neither; computed from the recomputed q~ and the saved context: no O needed)."""
     Nf, H, W, C = x.shape
     HW = H * W
     mz, ctx32, actT, actx, _o = state
@@ -580,9 +582,17 @@ def slaf_bwd_dw(x, dy, gamma_one, wq_fold, wqkv_f32, gamma, wout_t, state, dwqkv
     slab = empty((nblk_dx, 768, C), torch.float32, dev)
     tmp = empty((768, C), torch.float32, dev)
     wimg = empty(((2 * 768 + 256) * C,), torch.bfloat16, dev)
+    if (dwout is None) != (dbout is None):
+        raise ValueError("slaf_bwd_dw: dwout and dbout go together")
+    partm = partb = None
+    if dwout is not None:
+        _chk(dwout, (C, 256), torch.float32)
+        _chk(dbout, (C,), torch.float32)
+        partm = empty(((nblk + 1) * Nf * 8 * 2048,), torch.float32, dev)
+        partb = empty((nblk * Nf * C,), torch.float32, dev)
     call("cesm_slaf_bwd_dw", P(x), P(dy), P(gamma_one), P(wq_fold), P(wqkv_f32), P(gamma), P(wout_t), P(mz), P(ctx32),
-         P(actT), P(actx), P(dx), P(dwqkv), P(dgamma), P(part), P(G), P(adc), P(adcT), P(slab), P(tmp), P(wimg),
-         nblk_dx, Nf, HW, C, float(scale), float(eps), 1, S())
+         P(actT), P(actx), P(dx), P(dwqkv), P(dgamma), P(dwout), P(dbout), P(part), P(G), P(adc), P(adcT), P(slab),
+         P(tmp), P(partm), P(partb), P(wimg), nblk_dx, Nf, HW, C, float(scale), float(eps), 1, S())
     return dx
 
 

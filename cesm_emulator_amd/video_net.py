@@ -498,6 +498,11 @@ def _ones(C, device):
     return t
 
 
+# to_out weight / bias gradients of the in-kernel-dW SLA backward from the recomputed q~ and the forward's
+# context (no 256-channel O written by the forward); CESM_SLA_DWOUT=0 restores O + the wide weight-gradient GEMM
+SLA_DWOUT = os.environ.get("CESM_SLA_DWOUT", "1") != "0"
+
+
 def _sla_dw(rc, x):
     Nb, H, W, C = x.shape
     return SLA_DW and _sla_fused(rc, C) and K.slaf_bwd_dw_supported(Nb, H * W, C)
@@ -511,12 +516,14 @@ def sla_fwd(rc, res_mod, x):
     Nb, H, W, C = x.shape
     if _sla_dw(rc, x):
         # LN gamma folded into the QKV weights (unit gamma in the kernels): the backward then produces the
-        # to_qkv and gamma gradients in-kernel.  O is always saved for the to_out weight gradient.
+        # to_qkv and gamma gradients in-kernel, and (SLA_DWOUT) the to_out gradients from the recomputed q~ and
+        # the saved context, so O is not written; otherwise O is saved for a to_out weight-gradient GEMM.
         gamma = _flat(pre.norm.gamma)
         wq_fold = K.pack_scaled(sla.to_qkv.weight.reshape(768, C), gamma)
         wo = rc.packed(sla.to_out.weight, C, 256, 1, 1, 0, 0)
         ones = _ones(C, x.device)
-        y, state = K.slaf_fwd(x, ones, wq_fold, wo, sla.to_out.bias, sla.scale, eps=pre.norm.eps, save_o=rc.save)
+        y, state = K.slaf_fwd(x, ones, wq_fold, wo, sla.to_out.bias, sla.scale, eps=pre.norm.eps,
+                              save_o=rc.save and not SLA_DWOUT)
         st = SimpleNamespace(fused=True, fold=True, x=x, state=state, wq_fold=wq_fold) if rc.save else None
         return y, st
     if _sla_fused(rc, C):
@@ -542,10 +549,18 @@ def sla_bwd(rc, res_mod, st, dy):
     if st.fused and st.fold:
         wo_t = rc.packed(sla.to_out.weight, 256, C, 1, 1, 1, 1)
         dwo, dbo = gbuf(sla.to_out.weight), gbuf(sla.to_out.bias)
+        o = st.state[4]
+        in_kernel = o is None  # the forward did not write O (SLA_DWOUT): to_out gradients from the dctx pass
+        if in_kernel and (dwo is None) != (dbo is None):  # one of the two frozen: a scratch destination
+            dwo = dwo if dwo is not None else torch.zeros_like(sla.to_out.weight)
+            dbo = dbo if dbo is not None else torch.zeros_like(sla.to_out.bias)
         dx = K.slaf_bwd_dw(st.x, dy, _ones(C, dy.device), st.wq_fold, sla.to_qkv.weight.reshape(768, C),
                            _flat(pre.norm.gamma), wo_t, st.state, _wflat(sla.to_qkv.weight), _gflat(pre.norm.gamma),
-                           sla.scale, eps=pre.norm.eps)
-        o = st.state[4]
+                           sla.scale, eps=pre.norm.eps,
+                           dwout=dwo.view(C, 256) if in_kernel and dwo is not None else None,
+                           dbout=dbo if in_kernel and dwo is not None else None)
+        if in_kernel:
+            return dx
         with rc.side(o, dy, attn=True):
             if dwo is not None and K.conv_wgrad(o, None, dy, None, dwo, (H, W, C, 1, 1, 1, 0, 1), 0, 0, db=dbo):
                 dbo = None

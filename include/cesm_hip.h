@@ -201,14 +201,17 @@ int cesm_slaf_bwd(const void* x, const void* dy, const float* gamma, const void*
  * gamma_one (unit LN gamma) and wq_fold = bf16 W_qkv diag(gamma) (cesm_pack_scaled); this backward returns
  * dx and accumulates dwqkv (+)= dW_qkv [768][C], dgamma (+)= the LN gamma gradient (nullable) without the
  * 768-channel dqkv / xn intermediates of cesm_slaf_bwd.  nblk_dx from cesm_slaf_bwd_dw_nblk (0 = unsupported);
- * slab nblk_dx*768*C, tmp 768*C floats; wimg (2*768 + 256)*C bf16.  Replaces video_net.py:313-347 (SLA) +
- * :90-98 + :69-75 and the to_qkv weight gradient of its backward. */
+ * slab nblk_dx*768*C, tmp 768*C floats; wimg (2*768 + 256)*C bf16.  dwout [C][256] / dbout [C] (+)= the to_out
+ * weight / bias gradients (both or neither; nullable) from the recomputed q~ and the forward's context, so the
+ * forward need not write O: partm (cesm_slaf_nblk + 1) * Nf * 8 * 2048 floats, partb cesm_slaf_nblk * Nf * C.
+ * Replaces video_net.py:313-347 (SLA) + :90-98 + :69-75 and the to_qkv / to_out weight gradients of its
+ * backward. */
 int cesm_slaf_bwd_dw_nblk(int Nf, int HW, int C);
 int cesm_slaf_bwd_dw(const void* x, const void* dy, const float* gamma_one, const void* wq_fold, const float* wqkv_f32,
                      const float* gamma, const void* wout_t, const float* mz, const float* ctx32, const void* actT,
-                     const void* actx, void* dx, float* dwqkv, float* dgamma, float* part, float* G, void* adc,
-                     void* adcT, float* slab, float* tmp, void* wimg, int nblk_dx, int Nf, int HW, int C, float scale,
-                     float eps, int accumulate, hipStream_t stream);
+                     const void* actx, void* dx, float* dwqkv, float* dgamma, float* dwout, float* dbout, float* part,
+                     float* G, void* adc, void* adcT, float* slab, float* tmp, float* partm, float* partb, void* wimg,
+                     int nblk_dx, int Nf, int HW, int C, float scale, float eps, int accumulate, hipStream_t stream);
 /* out = bf16(w diag(colscale)) for an fp32 row-major w [M][K] (trans = 1: written transposed, [K][M]) */
 int cesm_pack_scaled(const float* w, const float* colscale, void* out, int M, int K, int trans, hipStream_t stream);
 int cesm_slaf_bwd_nblk(int Nf, int HW, int C);

@@ -764,12 +764,24 @@ def test_sla_fold_forward_and_dw_backward(dev, H, W):
     xr = x.double().requires_grad_(True)
     yr = ref(xr)
     (yr * g.double()).sum().backward()
+    # the training path's to_out gradients: in the dctx pass from the recomputed q~ and the saved context
+    # (the forward then writes no O); accumulated onto 0.5 / 0.25
+    _, st_no = K.slaf_fwd(xd, ones, wq_fold, wo, sla.to_out.bias.detach(), sla.scale, save_o=False)
+    assert st_no[4] is None
+    dwo_k = torch.full((C, 256), 0.5, device=dev)
+    dbo_k = torch.full((C,), 0.25, device=dev)
+    dx2 = K.slaf_bwd_dw(xd, gd, ones, wq_fold, wqkv, gamma, wo_t, st_no, torch.zeros(768, C, device=dev),
+                        torch.zeros(C, device=dev), sla.scale, dwout=dwo_k, dbout=dbo_k)
+    torch.cuda.synchronize()
+    assert torch.equal(dx2, dx)
     errs = {
         "y": rel(from_cl(y, B), yr.detach()),
         "dx": rel(from_cl(dx, B), xr.grad),
         "dgamma": rel(dgamma.double() - 0.25, ref.fn.norm.gamma.grad.reshape(-1)),
         "dWqkv": rel(dwq.double() - 0.5, ref.fn.fn.to_qkv.weight.grad.reshape(768, C)),
         "dWout": rel(dwo, ref.fn.fn.to_out.weight.grad.reshape(C, 256)),
+        "dWout_inkernel": rel(dwo_k.double() - 0.5, ref.fn.fn.to_out.weight.grad.reshape(C, 256)),
+        "dbout_inkernel": rel(dbo_k.double() - 0.25, ref.fn.fn.to_out.bias.grad.reshape(-1)),
     }
     print(f"sla fold/dw HxW={H}x{W}: " + " ".join(f"{k} {v:.2e}" for k, v in errs.items()))
     for k, v in errs.items():
