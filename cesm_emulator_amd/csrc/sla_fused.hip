@@ -685,6 +685,7 @@ __global__ __launch_bounds__(256) void slab_dwout_frame_kernel(const float* __re
   const float* pm = partm + ((int64_t)n * nblk * NH + h) * 2048;
   for (int i = tid; i < 2048; i += 256) {
     float m = 0.f;
+#pragma unroll 4
     for (int b = 0; b < nblk; ++b) m += pm[(int64_t)b * NH * 2048 + i];
     sm[i >> 5][i & 31] = m;
   }
@@ -705,6 +706,7 @@ __global__ __launch_bounds__(256) void slab_dwout_sum_kernel(const float* __rest
   if (idx >= 64 * 256) return;
   const int c = idx >> 8, k = idx & 255, h = k >> 5, e = k & 31;
   float s = 0.f;
+#pragma unroll 8
   for (int n = 0; n < Nf; ++n) s += R[((int64_t)(n * NH + h) * 64 + c) * 32 + e];
   dwout[idx] = accumulate ? dwout[idx] + s : s;
 }

@@ -692,6 +692,7 @@ class UNetModel3D(nn.Module):
                 continue
             tab = self._pack_tables.get(cdt)
             if tab is None:
+                assert all(e.out.numel() < 2 ** 31 for e in ents)  # the batch kernel indexes in 32 bits
                 rows = [[e.w.data_ptr(), e.out.data_ptr(), *e.geo] for e in ents]
                 tab = torch.tensor(rows, dtype=torch.int64).to(ents[0].out.device)
                 self._pack_tables[cdt] = tab
