@@ -481,6 +481,9 @@ constexpr int H3_WPT = H3_WVEC / 256;
 // tap offsets ky * H3_P and tap * 64 stay immediate.
 __device__ __forceinline__ int h3_off(int row, int ch) { return row * H3_LD + ((ch ^ ((row >> 1) & 2)) << 3); }
 
+#ifndef H3_DMA
+#define H3_DMA 1  // conv3x3_bf16_kernel: chunk staging by buffer-LDS-DMA (0: global -> registers -> LDS)
+#endif
 #ifndef H3_PIPE
 #define H3_PIPE 1  // conv3x3_bf16_kernel: software-pipelined tap fragments (0: the compiler's read -> MFMA order)
 #endif
@@ -504,6 +507,48 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
   const int Cin = g.C1 + g.C2;
   const int nchunk = Cin / 32;
 
+#if H3_DMA
+  // stage one 32-channel chunk by buffer-LDS-DMA (no registers, no address VALU per element beyond one per
+  // 16-B piece): 1-KiB pieces of 16 LDS rows, each lane fetching the global chunk that the row swizzle puts in
+  // its slot (chunk = slot ^ ((row >> 1) & 2)); halo rows outside the tile / image read as zeros (out-of-range
+  // offset).  The second co-resident block computes while this one waits.
+  auto stage = [&](int ch) {
+    const int c0 = ch * 32;
+    const bf16* src;
+    int cs, cc;
+    if (c0 < g.C1) { src = x1; cs = g.C1; cc = c0; } else { src = x2; cs = g.C2; cc = c0 - g.C1; }
+    const int64_t img = (int64_t)g.Hi * g.Wi * cs;
+    const __amdgpu_buffer_rsrc_t xrs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(src + n * img + cc), (short)0, (int)(img * 2 - cc * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(w + (int64_t)n0 * 9 * Cin + c0), (short)0, H3_BN * 9 * Cin * 2 - c0 * 2, 0x00020000);
+    const int prow = lane >> 2, pslot = lane & 3;
+    constexpr int HPC = H3_NROW / 16;  // halo pieces (25)
+#pragma unroll
+    for (int k = 0; k < (HPC + 3) / 4; ++k) {
+      const int q = wid + 4 * k;
+      if (q < HPC) {  // wave-uniform
+        const int row = 16 * q + prow;
+        const int r = row / H3_P, col = row - r * H3_P;
+        const int iy = y0 - 1 + r, ix = x0 - 1 + col;
+        const bool in = r < TH + 2 && col < HWd && (unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi;
+        const int chunk = pslot ^ ((row >> 1) & 2);
+        const int vo = in ? ((iy * g.Wi + ix) * cs + chunk * 8) * 2 : 0x7ffffff0;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)(sh + q * 512), 16, vo, 0,
+                                                 0, 0);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {  // weights: 9 taps x 64 co rows = 36 pieces
+      const int q = wid + 4 * k, row = 16 * q + prow;  // row = tap * 64 + co
+      const int tap = row >> 6, co = row & 63;
+      const int chunk = pslot ^ ((row >> 1) & 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(sw + q * 512), 16,
+                                               ((co * 9 + tap) * Cin + chunk * 8) * 2, 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+#else
   // stage one 32-channel chunk: global -> registers -> LDS (transient registers; the second
   // co-resident block computes while this one loads)
   auto stage = [&](int ch) {
@@ -546,6 +591,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
       *reinterpret_cast<bf16x8*>(sw + h3_off(e >> 2, e & 3)) = wreg[k];
     }
   };
+#endif
 
   f32x4 acc[2][8];
 #pragma unroll
