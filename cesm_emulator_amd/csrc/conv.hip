@@ -795,6 +795,45 @@ __global__ __launch_bounds__(256, 2) void convs2_bf16_kernel(const bf16* __restr
   const int nchunk = Cin / 32;
   constexpr int WPT = 4 * H3_BN * 4 / 256;  // weight vectors per thread (4 taps x 64 co x 4 vectors)
 
+#if H3_DMA
+  // stage s by buffer-LDS-DMA (as conv3x3_bf16_kernel): halo of the (parity sub-)image and the 4 live taps'
+  // weights for one 32-channel chunk
+  (void)WPT;
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(x + (int64_t)n * g.Hi * g.Wi * Cin), (short)0, (int)((int64_t)g.Hi * g.Wi * Cin * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(w + (int64_t)n0 * 16 * Cin), (short)0, H3_BN * 16 * Cin * 2, 0x00020000);
+  auto stage = [&](int ch, int a, int b, int by, int bx) {
+    const int c0 = ch * 32;
+    const int prow = lane >> 2, pslot = lane & 3;
+    constexpr int HPC = H3_NROW / 16;
+#pragma unroll
+    for (int k = 0; k < (HPC + 3) / 4; ++k) {
+      const int q = wid + 4 * k;
+      if (q < HPC) {  // wave-uniform
+        const int row = 16 * q + prow;
+        const int r = row / H3_P, col = row - r * H3_P;
+        const int Y = y0 - 1 + r, X = x0 - 1 + col;
+        const int iy = UP ? Y : 2 * Y + a, ix = UP ? X : 2 * X + b;
+        const bool in = r < TH + 2 && col < HWd && (unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi;
+        const int chunk = pslot ^ ((row >> 1) & 2);
+        const int vo = in ? ((iy * g.Wi + ix) * Cin + c0 + chunk * 8) * 2 : 0x7ffffff0;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)(sh + q * 512), 16, vo, 0,
+                                                 0, 0);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // 4 taps x 64 co rows = 16 pieces
+      const int q = wid + 4 * k, row = 16 * q + prow;  // row = t * 64 + co
+      const int t = row >> 6, co = row & 63;
+      const int tap = (by + 2 * (t >> 1)) * 4 + bx + 2 * (t & 1);
+      const int chunk = pslot ^ ((row >> 1) & 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(sw + q * 512), 16,
+                                               ((co * 16 + tap) * Cin + c0 + chunk * 8) * 2, 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+#else
   // stage s: halo of the (parity sub-)image and the 4 live taps' weights for one 32-channel chunk
   auto stage = [&](int ch, int a, int b, int by, int bx) {
     const int c0 = ch * 32;
@@ -835,6 +874,7 @@ __global__ __launch_bounds__(256, 2) void convs2_bf16_kernel(const bf16* __restr
       *reinterpret_cast<bf16x8*>(sw + h3_off(e >> 2, e & 3)) = wreg[k];
     }
   };
+#endif
 
   f32x4 acc[2][8];
 #pragma unroll
