@@ -772,6 +772,40 @@ __device__ __forceinline__ void s2_taps(const bf16* sh, const bf16* sw, const in
     }
   }
 }
+template <int TW, int BY, int BX>
+__device__ __forceinline__ void s2_taps_pipe(const bf16* sh, const bf16* sw, const int (&boff)[8][3], const int (&aoff)[2],
+                                        f32x4 (&acc)[2][8]) {
+  // tap t+1's 10 fragment reads issued between tap t's 16 MFMAs (as conv3x3_bf16_kernel)
+  bf16x8 fa[2][2], fb[2][8];
+  auto rd = [&](int t, int b) {
+    const int oy = BY + (t >> 1), ox = BX + (t & 1);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) fa[b][i] = *reinterpret_cast<const bf16x8*>(sw + aoff[i] + t * H3_BN * H3_LD);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fb[b][j] = *reinterpret_cast<const bf16x8*>(sh + boff[j][ox] + oy * H3_P * H3_LD);
+  };
+  rd(0, 0);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int b = t & 1;
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 1 < 4) rd(t + 1, b ^ 1);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[b][0], fb[b][j], acc[0][j], 0, 0, 0);
+      acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[b][1], fb[b][j], acc[1][j], 0, 0, 0);
+    }
+    if (t + 1 < 4) {
+#pragma unroll
+      for (int q2 = 0; q2 < 10; ++q2) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
 
 template <int TW, bool UP>
 __global__ __launch_bounds__(256, 2) void convs2_bf16_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
@@ -920,10 +954,11 @@ __global__ __launch_bounds__(256, 2) void convs2_bf16_kernel(const bf16* __restr
         if (ch || ab) __syncthreads();
         stage(ch, a, b, 1 - a, 1 - b);
         __syncthreads();
-        if (ab == 0) s2_taps<TW, 1, 1>(sh, sw, boff, aoff, acc);       // a = 0, b = 0
-        else if (ab == 1) s2_taps<TW, 1, 0>(sh, sw, boff, aoff, acc);  // a = 0, b = 1
-        else if (ab == 2) s2_taps<TW, 0, 1>(sh, sw, boff, aoff, acc);  // a = 1, b = 0
-        else s2_taps<TW, 0, 0>(sh, sw, boff, aoff, acc);                // a = 1, b = 1
+        // (down: the software-pipelined taps; the up kernel keeps the plain loop, pipelined it spills)
+        if (ab == 0) s2_taps_pipe<TW, 1, 1>(sh, sw, boff, aoff, acc);       // a = 0, b = 0
+        else if (ab == 1) s2_taps_pipe<TW, 1, 0>(sh, sw, boff, aoff, acc);  // a = 0, b = 1
+        else if (ab == 2) s2_taps_pipe<TW, 0, 1>(sh, sw, boff, aoff, acc);  // a = 1, b = 0
+        else s2_taps_pipe<TW, 0, 0>(sh, sw, boff, aoff, acc);                // a = 1, b = 1
       }
     }
   }
