@@ -959,9 +959,11 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
 #pragma unroll
       for (int u = 0; u < PG; ++u) {
         const int rb = (pg + u) * F;
-        const int rr = rb + (lr < F ? lr : 0);  // unpredicated LDS reads, zeroed after
-        const bf16x8 ka = sel8(lr < F, ld16(sk + rr * HLD + lg * 8));
-        const bf16x8 qb = sel8(lr < F, ld16(sq + rr * HLD + lg * 8));
+        // rows past F read the pixel's row 0 (finite): key rows j >= F are masked by bt = -inf below and query
+        // columns i >= F are never stored, so no select is needed
+        const int rr = rb + (lr < F ? lr : 0);
+        const bf16x8 ka = ld16(sk + rr * HLD + lg * 8);
+        const bf16x8 qb = ld16(sq + rr * HLD + lg * 8);
         st[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qb, z4, 0, 0, 0);
       }
       bf16x8 va[PG][2];
