@@ -1198,11 +1198,11 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
           const float v = lse[(((int64_t)b * NH + h) * HW + p) * F + (lr < F ? lr : 0)];
           Li = lr < F ? v : 0.f;
         }
-        const int rr = rb + (lr < F ? lr : 0);  // LDS reads unpredicated: a row of this pixel, zeroed after
-        const bf16x8 kr = sel8(lr < F, ld16(sk + rr * HLD + lg * 8));
-        const bf16x8 qr = sel8(lr < F, ld16(sq + rr * HLD + lg * 8));
-        const bf16x8 vr = sel8(lr < F, ld16(sv + rr * HLD + lg * 8));
-        const bf16x8 dor = sel8(lr < F, ld16(sdo + rr * HLD + lg * 8));
+        const int rr = rb + (lr < F ? lr : 0);  // rows past F read the pixel's row 0 (finite); every product is masked by ok / pt = 0
+        const bf16x8 kr = ld16(sk + rr * HLD + lg * 8);
+        const bf16x8 qr = ld16(sq + rr * HLD + lg * 8);
+        const bf16x8 vr = ld16(sv + rr * HLD + lg * 8);
+        const bf16x8 dor = ld16(sdo + rr * HLD + lg * 8);
         // -- transposed orientation: lane (g, i): entries (j = 4g + r, i)
         float D = 0.f;
         bf16x8 dst_b = zero8(), pt_b = zero8();
@@ -1788,10 +1788,10 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
       for (int u = 0; u < PG; ++u) {
         const int rb = (pp0 + u) * F;
         const int rr = rb + (lr < F ? lr : 0);
-        const bf16x8 kr = sel8(lr < F, ld16(sk + rr * HLD + lg * 8));
-        const bf16x8 qr = sel8(lr < F, ld16(sq + rr * HLD + lg * 8));
-        const bf16x8 vr = sel8(lr < F, ld16(sv + rr * HLD + lg * 8));
-        const bf16x8 dor = sel8(lr < F, ld16(sdo + rr * HLD + lg * 8));
+        const bf16x8 kr = ld16(sk + rr * HLD + lg * 8);
+        const bf16x8 qr = ld16(sq + rr * HLD + lg * 8);
+        const bf16x8 vr = ld16(sv + rr * HLD + lg * 8);
+        const bf16x8 dor = ld16(sdo + rr * HLD + lg * 8);
         st[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kr, qr, z4, 0, 0, 0);    // S^T[j][i]
         dpt[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vr, dor, z4, 0, 0, 0);  // dP^T[j][i]
       }
