@@ -1550,7 +1550,7 @@ extern "C" int cesm_diag_tw_stamps(unsigned long long* out, int n) {
 #define TWH_FULL 0      // twh_bwd: the head's 12 q/k/v weight fragments at once (1) or in two-tile batches (0)
 #endif
 #ifndef TWH_PG
-#define TWH_PG 2        // twh_bwd: pixels whose attention-core backward is interleaved phase by phase
+#define TWH_PG 1        // twh_bwd: pixels whose attention-core backward is interleaved phase by phase
 #endif
 #ifndef TWH_QKV_PIPE
 #define TWH_QKV_PIPE 1  // twh_bwd: double-buffered q/k/v weight batches, the first issued before barrier A
