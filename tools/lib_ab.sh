@@ -13,12 +13,13 @@ lib() { if [ "$1" = default ]; then echo cesm_emulator_amd/libcesm_hip.so; else 
 for v in "$@"; do
   echo "== gn_time $v" >> $out
   CESM_HIP_LIB=$(lib $v) timeout -k 10 120 python3 tools/gn_time.py >> $out 2>&1
+  CESM_HIP_LIB=$(lib $v) timeout -k 10 120 python3 tools/wred_time.py >> $out 2>&1
 done
 for rep in 1 2; do
   for v in "$@"; do
     echo "== bench $v rep $rep" >> $out
     CESM_HIP_LIB=$(lib $v) timeout -k 10 180 python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-probe \
-      2>/dev/null | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$v', d['value'], d['ms_per_step'])" >> $out
+      2>/dev/null | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$v', d['value'], d['ms_per_step'], d.get('loss'))" >> $out
   done
 done
 cat $out
