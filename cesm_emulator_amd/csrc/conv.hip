@@ -3081,61 +3081,6 @@ __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __r
   dst[di] = accumulate ? dst[di] + s : s;
 }
 
-// Same reduction with more loads in flight (total % 4 == 0): block = 64 lanes x float4 (256 consecutive slab
-// elements) x 16 split groups (1024 threads), 4 independent float4 partial sums per thread, fixed-order combine.
-// The per-lane chain of dependent loads of the kernel above made it latency-bound (~16 us per ~38 MB slab).
-#ifndef WRED_V2
-#define WRED_V2 0
-#endif
-constexpr int WRED_G = 16;
-__global__ __launch_bounds__(1024) void conv_wgrad_reduce4_kernel(const float* __restrict__ slab, float* __restrict__ dst,
-                                                                 int nsplit, int Cout, int Cin, int KH, int KW, int swap,
-                                                                 int flip, int accumulate) {
-  const int64_t K = (int64_t)KH * KW * Cin;
-  const int64_t total = (int64_t)Cout * K;
-  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int64_t e = (blockIdx.x * 64ll + lane) * 4;
-  float4 s[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) s[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (e < total) {
-    int k = grp, j = 0;
-    for (; k + 3 * WRED_G < nsplit; k += 4 * WRED_G) {
-      float4 a[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const float4*>(slab + (int64_t)(k + u * WRED_G) * total + e);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) { s[u].x += a[u].x; s[u].y += a[u].y; s[u].z += a[u].z; s[u].w += a[u].w; }
-    }
-    for (; k < nsplit; k += WRED_G, j = (j + 1) & 3) {
-      const float4 a = *reinterpret_cast<const float4*>(slab + (int64_t)k * total + e);
-      s[j].x += a.x; s[j].y += a.y; s[j].z += a.z; s[j].w += a.w;
-    }
-  }
-  __shared__ float4 red[WRED_G][64];
-  red[grp][lane] = make_float4(((s[0].x + s[1].x) + s[2].x) + s[3].x, ((s[0].y + s[1].y) + s[2].y) + s[3].y,
-                               ((s[0].z + s[1].z) + s[2].z) + s[3].z, ((s[0].w + s[1].w) + s[2].w) + s[3].w);
-  __syncthreads();
-  if (grp >= 4 || e >= total) return;
-  // wave w finishes component w of every lane's float4 (fixed order over the groups)
-  const int comp = grp;
-  float t = 0.f;
-#pragma unroll
-  for (int g = 0; g < WRED_G; ++g) {
-    const float4 r = red[g][lane];
-    t += comp == 0 ? r.x : comp == 1 ? r.y : comp == 2 ? r.z : r.w;
-  }
-  const int64_t ee = e + comp;
-  const int co = (int)(ee / K);
-  const int kc = (int)(ee - (int64_t)co * K);
-  const int tap = kc / Cin, ci = kc - tap * Cin;
-  int ky = tap / KW, kx = tap - ky * KW;
-  if (flip) { ky = KH - 1 - ky; kx = KW - 1 - kx; }
-  const int d0 = swap ? ci : co, d1 = swap ? co : ci, D1 = swap ? Cout : Cin;
-  const int64_t di = (((int64_t)d0 * D1 + d1) * KH + ky) * KW + kx;
-  dst[di] = accumulate ? dst[di] + t : t;
-}
-
 // pack a PyTorch conv weight into the GEMM layout Wp[co][tap][ci] (cast to T)
 template <typename T>
 __global__ void conv_pack_kernel(const float* __restrict__ src, T* __restrict__ dst, int Cout, int Cin, int KH,
@@ -4095,12 +4040,8 @@ int cesm_conv_wgrad(int dtype, const void* x1, const void* x2, const void* dy1, 
   else
     return CESM_EINVAL;
   const int64_t total = (int64_t)Cout * K;
-  if (WRED_V2 && total % 4 == 0)
-    conv_wgrad_reduce4_kernel<<<(unsigned)cdiv(total, 256), 64 * WRED_G, 0, stream>>>(slab, dw, nsplit, Cout, Cin, KH,
-                                                                                        KW, swap, flip, accumulate);
-  else
-    conv_wgrad_reduce_kernel<<<(unsigned)cdiv(total, 64), 256, 0, stream>>>(slab, dw, nsplit, Cout, Cin, KH, KW, swap,
-                                                                            flip, accumulate);
+  conv_wgrad_reduce_kernel<<<(unsigned)cdiv(total, 64), 256, 0, stream>>>(slab, dw, nsplit, Cout, Cin, KH, KW, swap,
+                                                                          flip, accumulate);
   return cesm_launch_status();
 }
 

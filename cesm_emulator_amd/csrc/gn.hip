@@ -17,11 +17,6 @@ namespace {
 
 // streaming activation accesses are non-temporal (bf16): measured at the level-0 bench shape stats 122 -> 107 us,
 // apply (+ residual) 389 -> 370 us, backward 679 -> 631 us (tools/gn_time.py); -DGN_NO_NT restores plain accesses
-// GN_REV: the apply passes walk their rows last-to-first, so their first reads are the rows the producing pass
-// touched last (still in the memory-side cache) and their last writes are the rows the consuming conv reads first
-#ifndef GN_REV
-#define GN_REV 0
-#endif
 #ifndef GN_NO_NT
 __device__ __forceinline__ void gl8(const bf16* p, float* v) { ldnt4(p, v); ldnt4(p + 4, v + 4); }
 __device__ __forceinline__ void gl8(const float* p, float* v) { load8(p, v); }
@@ -187,8 +182,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ y, const GnAffine coef,
                                                        const T* __restrict__ res, T* __restrict__ out, int64_t rows_b,
                                                        int C, int nchunk) {
-  const int b = GN_REV ? (int)gridDim.y - 1 - (int)blockIdx.y : blockIdx.y;
-  const int chunk = GN_REV ? nchunk - 1 - (int)blockIdx.x : blockIdx.x;
+  const int b = blockIdx.y, chunk = blockIdx.x;
   const int cv = C / 8, rl = 256 / cv;
   const int c8 = threadIdx.x % cv, rr = threadIdx.x / cv;
   if (rr >= rl) return;
@@ -198,11 +192,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ y, 
   const int64_t r0 = chunk * rpc, r1 = min(rows_b, r0 + rpc);
   const int64_t off = (int64_t)b * rows_b * C + c8 * 8;
 #pragma unroll 4
-#if GN_REV
-  for (int64_t r = r1 - 1 - rr; r >= r0; r -= rl) {
-#else
   for (int64_t r = r0 + rr; r < r1; r += rl) {
-#endif
     float v[8], rv[8];
     gl8(y + off + r * C, v);
     if (res) gl8(res + off + r * C, rv);
@@ -389,11 +379,7 @@ __global__ __launch_bounds__(256) void gn_bwd_apply_kernel(const T* __restrict__
   const int64_t r0 = chunk * rpc, r1 = min(rows_b, r0 + rpc);
   const int64_t off = (int64_t)b * rows_b * C + c8 * 8;
 #pragma unroll 4
-#if GN_REV
-  for (int64_t r = r1 - 1 - rr; r >= r0; r -= rl) {  // the reduce's chunks, tails first
-#else
   for (int64_t r = r0 + rr; r < r1; r += rl) {
-#endif
     float v[8], d[8];
     gl8(y + off + r * C, v);
     gl8(dout + off + r * C, d);
@@ -479,7 +465,7 @@ int cesm_gn_bwd(int dtype, const void* dout, const void* y, const float* stats, 
   float* E = coef + (int64_t)B * C * 2;
   const double count = (double)rows_b * (C / G);
   const GnAffine aff{stats, gamma, beta, ss, G};
-  const int nch = GN_REV ? nchunk : gn_apply_chunks(rows_b, C);
+  const int nch = gn_apply_chunks(rows_b, C);
   int rc = dispatch_dt(dtype, [&](auto* tp) {
     using T = std::remove_pointer_t<decltype(tp)>;
     gn_bwd_reduce_kernel<T><<<dim3(nchunk, B), 256, 0, stream>>>((const T*)dout, (const T*)y, aff, part, rows_b, C,
