@@ -55,10 +55,26 @@ def parse():
     ap.add_argument("--data", default="resident", choices=["resident", "device", "pinned"],
                     help="resident: one synthetic batch in HBM; device/pinned: the training data path in the loop")
     ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the CPU leg (cpu_baseline, fwd_error)")
-    ap.add_argument("--cpu-full-configs", default="more_blocks",
+    ap.add_argument("--cpu-full-configs", default="baseline,more_blocks",
                     help="comma list of configs whose full-grid oracle step is timed (D5), '' for none")
     ap.add_argument("--no-probe", action="store_true", help="no per-kernel HIP events in the timed region")
+    ap.add_argument("--dist-backend", default=None, choices=[None, "nccl", "gloo"],
+                    help="torch.distributed backend for N>1 (default nccl = RCCL; gloo rehearses the multi-rank path "
+                         "with several ranks on one GPU)")
+    ap.add_argument("--other-configs", default="baseline_f12_b8,more_blocks_f120_b1,more_blocks_f12_b5",
+                    help="extra single-GPU legs after the headline, outside its timed region (BASELINE.json configs "
+                         "2, 4 and 5 per GPU; N=1 only); '' for none")
     return ap.parse_args()
+
+
+# extra legs: name -> (config, per-GPU batch, frames, warm-up steps, timed steps, BASELINE.json config it stands for)
+OTHER_CONFIGS = {
+    "baseline_f12_b8": ("baseline", 8, 12, 3, 10, "configs[1]: config/baseline, 192x288x12, bf16, 1 GPU"),
+    "more_blocks_f120_b1": ("more_blocks", 1, 120, 3, 5,
+                            "configs[3] per-GPU leg: config/more_blocks, 192x288x120, 1 sample per GPU (8 GPUs DDP)"),
+    "more_blocks_f12_b5": ("more_blocks", 5, 12, 3, 10,
+                           "configs[4] per-GPU leg: config/more_blocks, 40-member batch over 8 GPUs = 5 per GPU"),
+}
 
 
 def load_cfg(name):
@@ -428,13 +444,96 @@ def make_feed(kind, B, F, H, W, dev, rank, world, steps_total):
     return gen()
 
 
+# ------------------------------------------------------------------------------------------------ timing
+def roofline_obj(d, steps, elapsed, peak):
+    """the contract's roofline object from a KernelProbe.table row of the dominant kernel"""
+    return {"bound": d["bound"],
+            "achieved": d["gbs"] if d["bound"] == "hbm" else d["tflops"],
+            "peak": PEAK_HBM_GBS if d["bound"] == "hbm" else peak,
+            "unit": "GB/s" if d["bound"] == "hbm" else "TFLOP/s",
+            "frac": d["frac"], "traffic": d["traffic"],
+            "kernel": d["kernel"], "launches": int(round(d["launches_per_step"] * steps)),
+            "avg_us": d["avg_us"], "ms_per_step": d["ms_per_step"],
+            "share_of_step": round(d["ms_per_step"] / (elapsed / steps * 1e3), 4),
+            "flop_per_launch": d["flop_per_launch"], "bytes_per_launch": d["bytes_per_launch"],
+            "traffic_note": ("PMC FETCH_SIZE (x2, gfx950) + WRITE_SIZE bytes per launch at this batch, copy-calibrated "
+                             f"({os.path.relpath(TRAFFIC_FILE, ROOT)})") if d["traffic"] is not None else
+                            "no PMC pass at this batch/config"}
+
+
+def other_leg(name, dev, probe, log):
+    """One extra single-GPU leg (OTHER_CONFIGS): resident synthetic batch, W warm-up steps (the last two profile
+    every kernel, choosing the dominant one), K timed steps bracketed by synchronize, the dominant kernel timed
+    live (as the headline).  Returns samples/s, ms/step, the step's MFMA fraction and the dominant-kernel roofline."""
+    from cesm_emulator_amd.model import Diffusion
+    from cesm_emulator_amd.optim import FusedAdamW
+    from cesm_emulator_amd.train import build_model_from_config, train_step, rank_generator
+    from cesm_emulator_amd.flops import train_flops_per_sample
+    cfg_name, B, F, warm, steps, what = OTHER_CONFIGS[name]
+    H, W = 192, 288
+    torch.manual_seed(1)
+    unet = build_model_from_config(load_cfg(cfg_name)["unet"]).to(dev)
+    unet.compute_dtype = torch.bfloat16
+    diff = Diffusion(unet).to(dev)
+    diff.generator = rank_generator(dev, 2, 0)
+    opt = FusedAdamW(diff.parameters(), lr=2e-4, betas=(0.9, 0.999), weight_decay=1e-4, max_grad_norm=1.0)
+    g = torch.Generator(device=dev).manual_seed(1000)
+    x0 = torch.randn(B, 1, H, W, device=dev, generator=g)
+    cond = torch.randn(B, 1, F, H, W, device=dev, generator=g)
+    torch.cuda.reset_peak_memory_stats(dev)
+    top_rows = None
+    if probe is not None:
+        probe.only = None
+    for i in range(warm):
+        if probe is not None and i == warm - 2:
+            probe.reset()
+            probe.active = True
+        train_step(diff, opt, x0, cond, 1.0, None)
+    torch.cuda.synchronize()
+    if probe is not None:
+        probe.active = False
+        top_rows = probe.table(2, PEAK_BF16_TFLOPS, load_traffic(B, F, cfg_name))
+        probe.only = {top_rows[0]["kernel"]}
+        probe.reset()
+        probe.active = True
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = train_step(diff, opt, x0, cond, 1.0, None)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    res = {"config": f"config/{cfg_name}, F={F}, {H}x{W}, per-GPU batch {B}", "stands_for": what,
+           "steps": steps, "warmup": warm, "samples_per_s": round(B * steps / elapsed, 4),
+           "ms_per_step": round(elapsed / steps * 1e3, 3), "loss": float(loss.item()),
+           "peak_mem_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)}
+    tflop = train_flops_per_sample(unet.net, F, H, W) / 1e12
+    res["step_mfma"] = {"train_tflop_per_sample": round(tflop, 4), "achieved_tflops": round(B * steps / elapsed * tflop, 2),
+                        "frac_of_peak": round(B * steps / elapsed * tflop / PEAK_BF16_TFLOPS, 4)}
+    if probe is not None:
+        probe.active = False
+        rows = probe.table(steps, PEAK_BF16_TFLOPS, load_traffic(B, F, cfg_name))
+        res["roofline"] = roofline_obj(rows[0], steps, elapsed, PEAK_BF16_TFLOPS)
+        res["top_kernels"] = [{k: r[k] for k in ("kernel", "ms_per_step", "avg_us", "tflops", "gbs", "frac")}
+                              for r in top_rows[:5]]
+        probe.reset()
+        probe.only = None
+    log(f"{name}: {res['samples_per_s']:.3f} samples/s ({res['ms_per_step']:.1f} ms/step), "
+        f"step MFMA {res['step_mfma']['frac_of_peak']:.3f}")
+    del diff, opt, unet, x0, cond
+    torch.cuda.empty_cache()
+    return res
+
+
 # ------------------------------------------------------------------------------------------------ main
 def main():
     a = parse()
     from cesm_emulator_amd import distributed as D
-    rank, local, world = D.setup()
+    rank, local, world = D.setup(backend=a.dist_backend)
     if world != a.gpus:
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    ndev = torch.cuda.device_count()
+    if local >= ndev:  # more ranks than GPUs (a gloo rehearsal): ranks share the devices round-robin
+        print(f"[bench] rank {rank}: LOCAL_RANK {local} >= {ndev} devices, using cuda:{local % ndev}", file=sys.stderr)
+        local = local % ndev
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
 
@@ -528,19 +627,7 @@ def main():
     if probe is not None:
         rows = probe.table(a.steps, peak, load_traffic(B, F, a.config) if a.dtype == "bf16" else None)
         top = (top_rows or rows)[:5]
-        d = rows[0]
-        roof = {"bound": d["bound"],
-                "achieved": d["gbs"] if d["bound"] == "hbm" else d["tflops"],
-                "peak": PEAK_HBM_GBS if d["bound"] == "hbm" else peak,
-                "unit": "GB/s" if d["bound"] == "hbm" else "TFLOP/s",
-                "frac": d["frac"], "traffic": d["traffic"],
-                "kernel": d["kernel"], "launches": int(round(d["launches_per_step"] * a.steps)),
-                "avg_us": d["avg_us"], "ms_per_step": d["ms_per_step"],
-                "share_of_step": round(d["ms_per_step"] / (elapsed / a.steps * 1e3), 4),
-                "flop_per_launch": d["flop_per_launch"], "bytes_per_launch": d["bytes_per_launch"],
-                "traffic_note": ("PMC FETCH_SIZE (x2, gfx950) + WRITE_SIZE bytes per launch at this batch, copy-calibrated "
-                                 f"({os.path.relpath(TRAFFIC_FILE, ROOT)})") if d["traffic"] is not None else
-                                "no PMC pass at this batch/config"}
+        roof = roofline_obj(rows[0], a.steps, elapsed, peak)
     out = {
         "metric": "train samples/sec (192x288xT frames)",
         "value": round(value, 4), "unit": "samples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
@@ -558,6 +645,16 @@ def main():
         "top_kernels": top,
     }
     log(f"timed {a.steps} steps: {elapsed:.2f}s -> {value:.2f} samples/s")
+    if world == 1 and a.other_configs and a.dtype == "bf16":
+        # BASELINE.json configs 2, 4 (per-GPU leg) and 5 (per-GPU batch), after the headline and outside its timed
+        # region; the headline's model, optimizer state and batch are freed first
+        del diff, opt, unet, next_batch
+        if a.data == "resident":
+            del cond, x0
+        torch.cuda.empty_cache()
+        out["other_configs"] = {}
+        for name in [n for n in a.other_configs.split(",") if n]:
+            out["other_configs"][name] = other_leg(name, dev, probe, log)
     if not a.no_cpu_baseline and world == 1:
         log("CPU leg (oracle fp32: forward error, train steps on host cores) ...")
         out["cpu_baseline"], out["fwd_error"] = cpu_leg(dev, a.cpu_full_configs)

@@ -190,13 +190,54 @@ __device__ __forceinline__ s16x4 tr4(const bf16* tile, int ld, int r0, int c0, i
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tile + (r0 + 4 * g + q) * ld + c0 + 4 * p));
 }
 
-constexpr int TH_PLD = 68;  // fp32 row stride of a wave's partial dxn rows (written over its own slices)
+// ---- "region" LDS tiles of the fused attention kernels (round 3) ----
+// A bf16 tile of R rows x 16*G columns is stored as G regions of [R][16] (32-B rows, region stride rs, a multiple of
+// 16), and in every row the two 16-B chunks swap when bit 2 of the row is set (SW = 1) or bit 2 ^ bit 3 (SW = 2).
+// The access sites of these kernels -- 16-B fragment reads of 16 rows (ds_read_b128), 8-B transposed / k-slot
+// reads of 8 consecutive rows (ds_read_b64_tr_b16), 8-B per-row reads of 16 rows (ds_read_b64) and 8-B column
+// stores of 16 rows (ds_write_b64) -- are then bank-conflict free, except the stores, which are 2-way, the minimum
+// for one 8-B column of 16 rows (SW = 1 for rows read from multiple-of-4 bases, SW = 2 where 16-row 8-B reads
+// occur; tools/lds_banks.py enumerates every site).  Column constants (the head dim half, the q/k/v kind) only
+// select a region -- an immediate offset -- so every site needs one per-lane offset register, which the
+// register-bound backward kernels depend on (an XOR-swizzled 64-B row needs one per column constant).
+// Round 2's padded rows (80 / 144 / 272 B) were 2-way on the fragment and transposed reads: 42-49 % of the LDS
+// cycles of tw_fwd / twh_bwd / slah_dx were bank conflicts (profiles/r2_v14_pmc_sq.txt).
+template <int SW = 1>
+__device__ __forceinline__ int rg_off(int r, int c, int rs) {
+  const int sw = SW == 1 ? (r >> 2) : ((r >> 2) ^ (r >> 3));
+  return (c >> 4) * rs + r * 16 + ((((c >> 3) ^ sw) & 1) << 3) + (c & 7);
+}
+// rg_off<1>(rb + i, c, rs) for rb % 4 == 0: bit 2 of rb + i is bit 2 of rb XOR bit 2 of i, so the offset is the
+// per-lane rg_off<1>(i, c, rs) XOR a uniform term, plus the uniform row base
+__device__ __forceinline__ int rg_at(int rb, int lane_off) { return rb * 16 + (lane_off ^ ((rb & 4) << 1)); }
+// hardware-transpose read of a region tile: lane (g, i) <- tile[r0 + 4g + e][c0 + i], e = 0..3 (EXEC all ones)
+template <int SW = 1>
+__device__ __forceinline__ s16x4 tr4_rg(const bf16* tile, int r0, int c0, int rs, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tile + rg_off<SW>(r0 + 4 * g + q, c0 + 4 * p, rs)));
+}
+// xhat / dy tiles of the head-parallel backwards: 4 regions, region stride R*16 + 16 (the 32-B stagger keeps the
+// LN role's 8-lane row writes conflict-free)
+__host__ __device__ constexpr int xt_rs(int R) { return R * 16 + 16; }
+__host__ __device__ constexpr int xt_elems(int R) { return 4 * xt_rs(R); }
+// fp32 partial dxn rows (written over a wave's own slices): 256-B rows, 16-B unit u at u ^ (r & 7) (conflict-free)
+constexpr int TH_PLD = 64;
+__device__ __forceinline__ int pl_off(int r, int c) { return r * TH_PLD + (((c >> 2) ^ (r & 7)) << 2) + (c & 3); }
 // an SGPR zero the compiler cannot see through: added to the weight-image pointers inside the group loop so
 // the (loop-invariant, per-head) fragment loads are not hoisted out of it and kept live across the loop
 __device__ __forceinline__ int opaque_zero() {
   int z;
   asm volatile("s_mov_b32 %0, 0" : "=s"(z));
   return z;
+}
+
+// a VGPR copy the compiler cannot see through: a lane index re-derived from it inside a loop keeps the lane-
+// dependent LDS offsets of that loop from being hoisted out of it as loop-invariant registers (they are
+// recomputed per iteration at a few VALU each instead), for kernels at the 256-VGPR limit
+__device__ __forceinline__ int opaque_v(int v) {
+  int r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(v));
+  return r;
 }
 
 // fp32 weight -> A-fragment image (frag_image layout) of A = W diag(gamma) (trans = 0: A[m][k] = W[m][k] g[k],

@@ -705,7 +705,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
       for (int i = 0; i < 2; ++i) rv[j][i] = bf16x4{};
   }
   // GroupNorm statistics partials (gnp: the Block conv feeding a GroupNorm): per channel quad (i, lg) the sum
-  // and sum of squares of the output over this wave's valid pixels
+  // and sum of squares of the stored bf16 output over this wave's valid pixels
   float gsum[2] = {0.f, 0.f}, gsq[2] = {0.f, 0.f};
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -717,6 +717,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
       float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bv[i][r] + b2f(rv[j][i], r);
+      if (gnp) {  // uniform: the statistics of the stored (bf16-rounded) y, which GroupNorm then normalises
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (float)(bf16)v[r];
+      }
       if (co < g.Co1) store4(y1 + m * g.Co1 + co, v);
       else store4(y2 + m * Co2 + (co - g.Co1), v);
       if (gnp) {  // uniform
@@ -1469,7 +1473,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
     const __amdgpu_buffer_rsrc_t rrs =
         __builtin_amdgcn_make_buffer_rsrc((void*)((rsrc ? rsrc : y1) + img), (short)0, img_bytes, 0x00020000);
     // GroupNorm statistics partials of this wave's pixels (gnp: the Block conv feeding a GroupNorm):
-    // per channel quad (i, lg) the sum and sum of squares of (acc + bias) over the valid pixels
+    // per channel quad (i, lg) the sum and sum of squares of bf16(acc + bias) over the valid pixels
     float gsum[4] = {0.f, 0.f, 0.f, 0.f}, gsq[4] = {0.f, 0.f, 0.f, 0.f};
     float gm[NG];
 #pragma unroll
@@ -1491,7 +1495,9 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
             const int j = r0 + jj;
             float v[4] = {acc[i][j][0] + bv[0], acc[i][j][1] + bv[1], acc[i][j][2] + bv[2], acc[i][j][3] + bv[3]};
             store4(so + (jj * 16 + lr) * CP_ELD + co, v);
-            if (gnp) {  // uniform
+            if (gnp) {  // uniform; statistics of the stored (bf16-rounded) y, which GroupNorm then normalises
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] = (float)(bf16)v[r];
               const float sv = (v[0] + v[1]) + (v[2] + v[3]);
               const float qv = fmaf(v[3], v[3], fmaf(v[2], v[2], fmaf(v[1], v[1], v[0] * v[0])));
               gsum[i] = fmaf(gm[j], sv, gsum[i]);

@@ -1080,13 +1080,19 @@ __device__ __forceinline__ void wave_lds_sync_s() {
 #ifndef SLAH_WPIPE
 #define SLAH_WPIPE 1  // slah_dx: weight fragments issued one GEMM step ahead (first before barrier A / the dW GEMM)
 #endif
-constexpr int SH_XLD = 72;   // xhat / dy tile row stride (bf16)
-constexpr int SH_SLD = 136;  // slice row stride (bf16): raw q|k|v|do (128 cols), then dq|dk|dv; fp32 partials over it
-constexpr int SH_PLD = 68;   // fp32 partial dxn row stride
+// xhat / dy tiles: region tiles (common.h xt_rs); fp32 partial dxn rows: pl_off layout over the wave's slice
+constexpr int SH_SLD = 128;  // slice row stride (bf16): raw q|k|v|do (128 cols), then dq|dk|dv; fp32 partials over it
+// Slice layout (round 3): a region tile (common.h rg_off<2>) of eight [R][16] regions -- q, k, v, do, two head-dim
+// halves each -- with the two 16-B chunks of a row swapped when bit 2 ^ bit 3 of the row is set: the per-pixel 8-B
+// reads of phase B and the transposed dW reads are conflict-free, the dxn fragment reads 2-way, the column stores
+// 2-way (the minimum); each access site needs one per-lane offset register (tools/lds_banks.py).  Round 2's 272-B
+// rows were 2-way on the fragment and transposed reads (42 % of slah_dx's LDS cycles were conflicts).
+template <int R>
+__device__ __forceinline__ int sl_off(int r, int c) { return rg_off<2>(r, c, R * 16); }
 
 static size_t slah_smem(int NV) {
   const int R = 16 * NV;
-  return (size_t)2 * R * SH_XLD * 2 + (size_t)8 * R * SH_SLD * 2;
+  return (size_t)2 * xt_elems(R) * 2 + (size_t)8 * R * SH_SLD * 2;
 }
 
 template <int NV>
@@ -1097,11 +1103,11 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
     const bf16* __restrict__ adcT, bf16* __restrict__ dx, float* __restrict__ dw_slab, int Nf, int HW, float scale,
     float eps) {
   constexpr int C = 64, KS = C / 32, CT = C / 16, R = 16 * NV;
-  static_assert(SH_PLD * 4 <= SH_SLD * 2, "partial dxn rows fit over the slice rows");
+  static_assert(TH_PLD * 4 <= SH_SLD * 2, "partial dxn rows fit over the slice rows");
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  bf16* xt = reinterpret_cast<bf16*>(smem);  // [R][SH_XLD] xhat
-  bf16* dyt = xt + R * SH_XLD;                // [R][SH_XLD] dy
-  bf16* slices = dyt + R * SH_XLD;            // 8 x [R][SH_SLD]
+  bf16* xt = reinterpret_cast<bf16*>(smem);  // [R][64] xhat (region tile, xt_rs)
+  bf16* dyt = xt + xt_elems(R);               // [R][64] dy
+  bf16* slices = dyt + xt_elems(R);           // 8 x [R][SH_SLD] (sl_off layout)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const int h = wid;
@@ -1159,8 +1165,8 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
           xh[e] = (bf16)(ok_cur ? (a[e] - mean) * rstd : 0.f);
           dv[e] = ok_cur ? dpf[e] : (bf16)0.f;
         }
-        *reinterpret_cast<bf16x8*>(xt + vv * SH_XLD + cc * 8) = xh;
-        *reinterpret_cast<bf16x8*>(dyt + vv * SH_XLD + cc * 8) = dv;
+        *reinterpret_cast<bf16x8*>(xt + rg_off<1>(vv, cc * 8, xt_rs(R))) = xh;
+        *reinterpret_cast<bf16x8*>(dyt + rg_off<1>(vv, cc * 8, xt_rs(R))) = dv;
       }
     }
     const int oz = opaque_zero();
@@ -1202,14 +1208,14 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
       for (int vt = 0; vt < NV; ++vt) {
         bf16x8 b[KS];
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) b[ks] = ld16(src + (vt * 16 + lr) * SH_XLD + ks * 32 + lg * 8);
+        for (int ks = 0; ks < KS; ++ks) b[ks] = ld16(src + rg_off<1>(vt * 16 + lr, ks * 32 + lg * 8, xt_rs(R)));
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
           f32x4 acc = z4;
 #pragma unroll
           for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[t][ks], b[ks], acc, 0, 0, 0);
           float o4[4] = {acc[0], acc[1], acc[2], acc[3]};
-          store4(sl + (vt * 16 + lr) * SH_SLD + kind * 32 + t * 16 + lg * 4, o4);
+          store4(sl + sl_off<R>(vt * 16 + lr, kind * 32 + t * 16 + lg * 4), o4);
         }
       }
     }
@@ -1235,14 +1241,14 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
 #pragma unroll
       for (int vt = 0; vt < NV; ++vt) {
         const bool ok = p0 + vt * 16 + lr < HW;
-        bf16* row = sl + (vt * 16 + lr) * SH_SLD;
+        const int rw = vt * 16 + lr;
         float qv[2][4], kv[2][4], vv4[2][4], dov[2][4];
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          load4(row + 0 * 32 + t * 16 + lg * 4, qv[t]);
-          load4(row + 1 * 32 + t * 16 + lg * 4, kv[t]);
-          load4(row + 2 * 32 + t * 16 + lg * 4, vv4[t]);
-          load4(row + 3 * 32 + t * 16 + lg * 4, dov[t]);
+          load4(sl + sl_off<R>(rw, 0 * 32 + t * 16 + lg * 4), qv[t]);
+          load4(sl + sl_off<R>(rw, 1 * 32 + t * 16 + lg * 4), kv[t]);
+          load4(sl + sl_off<R>(rw, 2 * 32 + t * 16 + lg * 4), vv4[t]);
+          load4(sl + sl_off<R>(rw, 3 * 32 + t * 16 + lg * 4), dov[t]);
         }
         float mx = -INFINITY;
 #pragma unroll
@@ -1300,9 +1306,9 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
         // each lane overwrites exactly the q / k / v entries it read itself: no sync needed
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          store4(row + t * 16 + lg * 4, dq[t]);
-          store4(row + 32 + t * 16 + lg * 4, dk[t]);
-          store4(row + 64 + t * 16 + lg * 4, dvv[t]);
+          store4(sl + sl_off<R>(rw, t * 16 + lg * 4), dq[t]);
+          store4(sl + sl_off<R>(rw, 32 + t * 16 + lg * 4), dk[t]);
+          store4(sl + sl_off<R>(rw, 64 + t * 16 + lg * 4), dvv[t]);
         }
       }
     }
@@ -1318,10 +1324,10 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
     for (int kk = 0; kk < NV; ++kk) {
       s16x4 bx[4];
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) bx[nt] = tr4(xt, SH_XLD, kk * 16, nt * 16, lane);
+      for (int nt = 0; nt < 4; ++nt) bx[nt] = tr4_rg<1>(xt, kk * 16, nt * 16, xt_rs(R), lane);
 #pragma unroll
       for (int m = 0; m < 6; ++m) {
-        const s16x4 a = tr4(sl, SH_SLD, kk * 16, (m >> 1) * 32 + (m & 1) * 16, lane);
+        const s16x4 a = tr4_rg<2>(sl, kk * 16, (m >> 1) * 32 + (m & 1) * 16, R * 16, lane);
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt)
           dwacc[m][nt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, bx[nt], dwacc[m][nt], 0, 0, 0);
@@ -1346,7 +1352,7 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
 #endif
 #pragma unroll
         for (int vt = 0; vt < NV; ++vt)
-          dxacc[ct][vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ld16(sl + (vt * 16 + lr) * SH_SLD + kind * 32 + lg * 8),
+          dxacc[ct][vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ld16(sl + sl_off<R>(vt * 16 + lr, kind * 32 + lg * 8)),
                                                                   dxacc[ct][vt], 0, 0, 0);
       }
     wave_lds_sync_s();
@@ -1356,7 +1362,7 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
       for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
         for (int vt = 0; vt < NV; ++vt)
-          *reinterpret_cast<f32x4*>(part + (vt * 16 + lr) * SH_PLD + ct * 16 + lg * 4) = dxacc[ct][vt];
+          *reinterpret_cast<f32x4*>(part + pl_off(vt * 16 + lr, ct * 16 + lg * 4)) = dxacc[ct][vt];
     }
     __syncthreads();  // (B)
     // ---- LN backward of this thread's pixel chunk
@@ -1367,14 +1373,14 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
       for (int e = 0; e < 8; ++e) g[e] = 0.f;
 #pragma unroll
       for (int w = 0; w < 8; ++w) {
-        const float* pw = reinterpret_cast<const float*>(slices + w * R * SH_SLD) + v * SH_PLD + cc * 8;
-        const f32x4 a0 = *reinterpret_cast<const f32x4*>(pw);
-        const f32x4 a1 = *reinterpret_cast<const f32x4*>(pw + 4);
+        const float* pw = reinterpret_cast<const float*>(slices + w * R * SH_SLD);
+        const f32x4 a0 = *reinterpret_cast<const f32x4*>(pw + pl_off(v, cc * 8));
+        const f32x4 a1 = *reinterpret_cast<const f32x4*>(pw + pl_off(v, cc * 8 + 4));
 #pragma unroll
         for (int e = 0; e < 4; ++e) { g[e] += a0[e]; g[4 + e] += a1[e]; }
       }
-      const bf16x8 xh = *reinterpret_cast<const bf16x8*>(xt + v * SH_XLD + cc * 8);
-      const bf16x8 dv = *reinterpret_cast<const bf16x8*>(dyt + v * SH_XLD + cc * 8);
+      const bf16x8 xh = *reinterpret_cast<const bf16x8*>(xt + rg_off<1>(v, cc * 8, xt_rs(R)));
+      const bf16x8 dv = *reinterpret_cast<const bf16x8*>(dyt + rg_off<1>(v, cc * 8, xt_rs(R)));
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int e = 0; e < 8; ++e) { s1 += g[e]; s2 = fmaf(g[e], (float)xh[e], s2); }

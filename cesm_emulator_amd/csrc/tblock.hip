@@ -16,7 +16,17 @@
 namespace {
 
 constexpr int NH = 8, DH = 32, INNER = 256, QKV = 768;
-constexpr int HLD = 40;  // LDS row stride (bf16) of the per-head 32-wide tiles
+constexpr int HLD = 40;  // LDS row stride (bf16) of the per-head 32-wide tiles (tblock_*_kernel, C = 512)
+
+// Per-head q / k / v / dO slices of the wave-private and head-parallel kernels (round 3): region tiles (common.h
+// rg_off<1>) of two [R][16] regions -- head dims 0-15 and 16-31 -- with the two 16-B chunks of a row swapped when
+// bit 2 of the row is set.  Pixel rows start at multiples of 4 (frames padded to F4 = pad4(F) rows), so the
+// fragment reads of the attention core and the GEMMs, the k-slot gathers and the transposed dW reads are
+// bank-conflict free and the bf16x4 epilogue stores 2-way (the minimum).  The round-2 80-B rows (HLD) were
+// 2-way on the reads as well: 45-49 % of the LDS cycles of tw_fwd / twh_bwd were conflicts.
+constexpr int HS = 32;  // bf16 per slice row (both regions)
+template <int R>
+__device__ __forceinline__ int hs_off(int r, int c) { return rg_off<1>(r, c, R * 16); }
 
 __device__ __forceinline__ bf16x8 zero8() {
   bf16x8 z;
@@ -681,9 +691,11 @@ constexpr float LOG2E = 1.4426950408889634f;
 
 // k-slot gather with the hardware transpose read: lane (g, i) gets tile[rb + 4g + e][c0 + i] in
 // element e (e < 4; elements 4..7 and rows >= F are zero).  Must run with EXEC all ones.
+// (tile: a head slice of R rows, hs_off layout; rb % 4 == 0)
+template <int R>
 __device__ __forceinline__ bf16x8 kslot_gather(const bf16* tile, int rb, int c0, int F, int lane) {
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tile + (rb + 4 * g + q) * HLD + c0 + 4 * p));
+  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tile + rg_at(rb, hs_off<R>(4 * g + q, c0 + 4 * p))));
   bf16x8 r = zero8();
 #pragma unroll
   for (int e = 0; e < 4; ++e)
@@ -691,15 +703,23 @@ __device__ __forceinline__ bf16x8 kslot_gather(const bf16* tile, int rb, int c0,
   return r;
 }
 
-// kslot_gather for a tile of row stride ld (bf16 elements)
-__device__ __forceinline__ bf16x8 kslot_gather_ld(const bf16* tile, int ld, int rb, int c0, int F, int lane) {
+// 16 x 16 bf16 P / dS tiles of twh_bwd: 32-B rows, 8-B slot s of row r stored at s ^ ((r >> 2) & 3) (the
+// bf16x4 row writes of 16 lanes and the transposed reads are then both conflict-free; plain rows: 4-way writes)
+__device__ __forceinline__ int trt_off(int r, int c) { return r * 16 + (((c >> 2) ^ ((r >> 2) & 3)) << 2) + (c & 3); }
+// kslot_gather of a P / dS tile: lane (g, i) gets tile[4g + e][i] in element e (rows >= F zero)
+__device__ __forceinline__ bf16x8 kslot_gather_trt(const bf16* tile, int F, int lane) {
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tile + (rb + 4 * g + q) * ld + c0 + 4 * p));
+  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tile + trt_off(4 * g + q, 4 * p)));
   bf16x8 r = zero8();
 #pragma unroll
   for (int e = 0; e < 4; ++e)
     if (4 * g + e < F) r[e] = __builtin_bit_cast(bf16, (short)v[e]);
   return r;
+}
+// hardware-transpose read of a head slice: lane (g, i) <- tile[r0 + 4g + e][c0 + i]
+template <int R>
+__device__ __forceinline__ s16x4 tr4_hs(const bf16* tile, int r0, int c0, int lane) {
+  return tr4_rg<1>(tile, r0, c0, R * 16, lane);
 }
 
 // RoPE rotation of 4 consecutive head dims d0..d0+3 (two pairs) of frame f; sign=-1 applies R^T
@@ -717,10 +737,14 @@ __device__ __forceinline__ void rope4(float* o4, const float* rot, int f, int d0
 __device__ __forceinline__ bf16x8 sel8(bool ok, bf16x8 v) { return ok ? v : zero8(); }
 
 // rows of voxel v of the wave's pixel group
-__device__ __forceinline__ bool tw_row(int v, int VW, int F, int p0, int HW, int b, int64_t& row) {
+// (slice rows: pixel pp's frames at rows pp*F4 + f, F4 = F rounded up to a multiple of 4, VW = PW*F4; rows with
+// f >= F are padding.  Every pixel's rows then start on a multiple of 4, which the hs_off layout needs for its
+// conflict-free reads and which lets the address of row rb + i split into a per-lane part and a uniform XOR.)
+__device__ __forceinline__ int pad4(int F) { return (F + 3) & ~3; }
+__device__ __forceinline__ bool tw_row(int v, int VW, int F, int F4, int p0, int HW, int b, int64_t& row) {
   if (v >= VW) return false;
-  const int pp = v / F, f = v - pp * F, p = p0 + pp;
-  if (p >= HW) return false;
+  const int pp = v / F4, f = v - pp * F4, p = p0 + pp;
+  if (f >= F || p >= HW) return false;
   row = ((int64_t)b * F + f) * HW + p;
   return true;
 }
@@ -744,6 +768,7 @@ __device__ __forceinline__ void tw_qkv_pre(const bf16x8 (&a)[6][C / 32],
                                            const bf16x8 (&xf)[TW<C, NV>::NVTM][TW<C, NV>::KS], const int (&fr)[NV],
                                            float scale, const float* rot, bf16* sq, bf16* sk, bf16* sv, int lr, int lg) {
   using T = TW<C, NV>;
+  constexpr int R = NV * 16;  // slice rows
 #pragma unroll
   for (int ct = 0; ct < 6; ++ct) {
     const int kind = ct >> 1;
@@ -760,7 +785,7 @@ __device__ __forceinline__ void tw_qkv_pre(const bf16x8 (&a)[6][C / 32],
         for (int r = 0; r < 4; ++r) o4[r] *= scale;
       }
       if (kind < 2) rope4(o4, rot, fr[vt], d0, 1.f);
-      store4(dst + (vt * 16 + lr) * HLD + d0, o4);
+      store4(dst + hs_off<R>(vt * 16 + lr, d0), o4);
     }
   }
 }
@@ -769,6 +794,7 @@ template <int C, int NV, bool FULL = (C <= 64)>
 __device__ __forceinline__ void tw_qkv(const bf16* __restrict__ wqkv, const bf16x8 (&xf)[TW<C, NV>::NVTM][TW<C, NV>::KS],
                                        int h, const int (&fr)[NV], float scale, const float* rot, bf16* sq, bf16* sk,
                                        bf16* sv, int lr, int lg) {
+  constexpr int R = NV * 16;  // slice rows
   if constexpr (FULL) {
     bf16x8 a[6][C / 32];
     tw_load_wq<C, NV>(a, wqkv, h, lr, lg);
@@ -802,7 +828,7 @@ __device__ __forceinline__ void tw_qkv(const bf16* __restrict__ wqkv, const bf16
             for (int r = 0; r < 4; ++r) o4[r] *= scale;
           }
           if (kind < 2) rope4(o4, rot, fr[vt], d0, 1.f);
-          store4(dst + (vt * 16 + lr) * HLD + d0, o4);
+          store4(dst + hs_off<R>(vt * 16 + lr, d0), o4);
         }
       }
     }
@@ -814,7 +840,7 @@ __device__ __forceinline__ void tw_qkv(const bf16* __restrict__ wqkv, const bf16
 template <int C, int NV, bool GAM = true>
 __device__ __forceinline__ void tw_ln(const bf16* __restrict__ x, const float* __restrict__ gamma, float* mr_out,
                                       const float* __restrict__ mr_in, bf16x8 (&xf)[TW<C, NV>::NVTM][TW<C, NV>::KS], int NVT,
-                                      int VW, int F, int p0, int HW, int b, float eps, int lr, int lg) {
+                                      int VW, int F, int F4, int p0, int HW, int b, float eps, int lr, int lg) {
   using T = TW<C, NV>;
   // every load is unconditional (invalid voxels read row 0 and are zeroed by a select): a load under a
   // lane predicate becomes a branch with its own vmcnt(0), which serialised the 16 gamma and 2 x loads
@@ -833,7 +859,7 @@ __device__ __forceinline__ void tw_ln(const bf16* __restrict__ x, const float* _
 #pragma unroll
   for (int vt = 0; vt < T::NVTM; ++vt) {
     int64_t row = 0;
-    okv[vt] = vt < NVT && tw_row(vt * 16 + lr, VW, F, p0, HW, b, row);
+    okv[vt] = vt < NVT && tw_row(vt * 16 + lr, VW, F, F4, p0, HW, b, row);
     rows[vt] = okv[vt] ? row : 0;
 #pragma unroll
     for (int ks = 0; ks < T::KS; ++ks) raw[vt][ks] = ld16(x + rows[vt] * C + ks * 32 + lg * 8);
@@ -896,12 +922,12 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const int b = blockIdx.y;
-  const int VW = T::PW * F;
+  const int F4 = pad4(F), VW = T::PW * F4;
   constexpr int NVT = NV;
   const int R = NVT * 16;
-  bf16* sq = reinterpret_cast<bf16*>(rot + 16 * RS) + wid * 3 * R * HLD;
-  bf16* sk = sq + R * HLD;
-  bf16* sv = sk + R * HLD;
+  bf16* sq = reinterpret_cast<bf16*>(rot + 16 * RS) + wid * 3 * R * HS;
+  bf16* sk = sq + R * HS;
+  bf16* sv = sk + R * HS;
   for (int e = tid; e < NH * F * F; e += 256) sb[e] = bias[e] * LOG2E;
   for (int e = tid; e < F * 32; e += 256) rot[(e >> 5) * RS + (e & 31)] = rotg[e];
   __syncthreads();
@@ -909,12 +935,12 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
   if (p0 >= HW) return;
   int fr[NV];
 #pragma unroll
-  for (int vt = 0; vt < NV; ++vt) fr[vt] = (vt * 16 + lr) % F;
+  for (int vt = 0; vt < NV; ++vt) fr[vt] = (vt * 16 + lr) % F4 < F ? (vt * 16 + lr) % F4 : 0;
 
   bf16x8 xf[T::NVTM][T::KS];
   // FOLD: wqkv is the image of W diag(gamma) and the B fragments hold xhat (twh_bwd_kernel recomputes
   // q/k/v the same way, so forward and backward see identical bf16 operands)
-  tw_ln<C, NV, !FOLD>(x, gamma, mr, nullptr, xf, NVT, VW, F, p0, HW, b, eps, lr, lg);
+  tw_ln<C, NV, !FOLD>(x, gamma, mr, nullptr, xf, NVT, VW, F, F4, p0, HW, b, eps, lr, lg);
 
   f32x4 yacc[T::CT][T::NVTM];
 #pragma unroll
@@ -958,19 +984,19 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
       f32x4 st[PG];
 #pragma unroll
       for (int u = 0; u < PG; ++u) {
-        const int rb = (pg + u) * F;
+        const int rb = (pg + u) * F4;
         // rows past F read the pixel's row 0 (finite): key rows j >= F are masked by bt = -inf below and query
         // columns i >= F are never stored, so no select is needed
-        const int rr = rb + (lr < F ? lr : 0);
-        const bf16x8 ka = ld16(sk + rr * HLD + lg * 8);
-        const bf16x8 qb = ld16(sq + rr * HLD + lg * 8);
+        const int rr = rg_at(rb, hs_off<R>(lr < F ? lr : 0, lg * 8));
+        const bf16x8 ka = ld16(sk + rr);
+        const bf16x8 qb = ld16(sq + rr);
         st[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qb, z4, 0, 0, 0);
       }
       bf16x8 va[PG][2];
 #pragma unroll
       for (int u = 0; u < PG; ++u)
 #pragma unroll
-        for (int half = 0; half < 2; ++half) va[u][half] = kslot_gather(sv, (pg + u) * F, half * 16, F, lane);
+        for (int half = 0; half < 2; ++half) va[u][half] = kslot_gather<R>(sv, (pg + u) * F4, half * 16, F, lane);
       bf16x8 pb[PG];
 #pragma unroll
       for (int u = 0; u < PG; ++u) {
@@ -998,13 +1024,13 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
       }
 #pragma unroll
       for (int u = 0; u < PG; ++u) {
-        const int rb = (pg + u) * F;
+        const int rb = (pg + u) * F4;
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
           const f32x4 ot = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va[u][half], pb[u], z4, 0, 0, 0);
           if (lr < F) {
             float o4[4] = {ot[0], ot[1], ot[2], ot[3]};
-            store4(sq + (rb + lr) * HLD + half * 16 + lg * 4, o4);
+            store4(sq + rg_at(rb, hs_off<R>(lr, half * 16 + lg * 4)), o4);
           }
         }
       }
@@ -1017,12 +1043,12 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
     // y^T += W_out[:, h] . O_h^T
     bf16x8 ob[T::NVTM];
 #pragma unroll
-    for (int vt = 0; vt < T::NVTM; ++vt) ob[vt] = vt < NVT ? ld16(sq + (vt * 16 + lr) * HLD + lg * 8) : zero8();
+    for (int vt = 0; vt < T::NVTM; ++vt) ob[vt] = vt < NVT ? ld16(sq + hs_off<R>(vt * 16 + lr, lg * 8)) : zero8();
     if (o_out) {  // O_h for the to_out weight gradient (the backward then skips its emission)
 #pragma unroll
       for (int vt = 0; vt < T::NVTM; ++vt) {
         int64_t row = 0;
-        if (vt < NVT && tw_row(vt * 16 + lr, VW, F, p0, HW, b, row))
+        if (vt < NVT && tw_row(vt * 16 + lr, VW, F, F4, p0, HW, b, row))
           stnt16(o_out + row * INNER + h * DH + lg * 8, ob[vt]);
       }
     }
@@ -1039,7 +1065,7 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
   for (int vt = 0; vt < T::NVTM; ++vt) {
     if (vt >= NVT) break;
     int64_t row = 0;
-    if (!tw_row(vt * 16 + lr, VW, F, p0, HW, b, row)) continue;
+    if (!tw_row(vt * 16 + lr, VW, F, F4, p0, HW, b, row)) continue;
 #pragma unroll
     for (int ct = 0; ct < T::CT; ++ct) {
       const int co = ct * 16 + lg * 4;
@@ -1075,14 +1101,14 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
   float* sg = sg0 + wid * C;
   const int lr = lane & 15, lg = lane >> 4;
   const int b = blockIdx.y;
-  const int VW = T::PW * F;
+  const int F4 = pad4(F), VW = T::PW * F4;
   constexpr int NVT = NV;
   const int R = NVT * 16;
-  bf16* sq = reinterpret_cast<bf16*>(rot + 16 * RS) + wid * 4 * R * HLD;
-  bf16* sk = sq + R * HLD;
-  bf16* sv = sk + R * HLD;
-  bf16* sdo = sv + R * HLD;
-  float* sld = reinterpret_cast<float*>(reinterpret_cast<bf16*>(rot + 16 * RS) + 4 * 4 * R * HLD) + wid * 32;
+  bf16* sq = reinterpret_cast<bf16*>(rot + 16 * RS) + wid * 4 * R * HS;
+  bf16* sk = sq + R * HS;
+  bf16* sv = sk + R * HS;
+  bf16* sdo = sv + R * HS;
+  float* sld = reinterpret_cast<float*>(reinterpret_cast<bf16*>(rot + 16 * RS) + 4 * 4 * R * HS) + wid * 32;
   for (int e = tid; e < NH * FF; e += 256) sb[e] = bias[e] * LOG2E;
   for (int e = tid; e < 4 * NH * FF; e += 256) sdb0[e] = 0.f;
   for (int e = tid; e < 4 * C; e += 256) sg0[e] = 0.f;
@@ -1100,18 +1126,20 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
   int fr[NV];
 #pragma unroll
-  for (int vt = 0; vt < NV; ++vt) fr[vt] = (vt * 16 + lr) % F;
+  for (int vt = 0; vt < NV; ++vt) fr[vt] = (vt * 16 + lr) % F4 < F ? (vt * 16 + lr) % F4 : 0;
 
   TW_ST_DECL
   for (int pg = blockIdx.x * 4 + wid; pg < npg; pg += nw) {
     const int p0 = pg * T::PW;
+    // lane-derived LDS offsets recomputed per group from an opaque lane copy (not hoisted: register-bound kernel)
+    const int lane = opaque_v(threadIdx.x & 63), lr = lane & 15, lg = lane >> 4;
     bf16x8 xf[T::NVTM][T::KS];
-    tw_ln<C, NV>(x, sgm, nullptr, mr, xf, NVT, VW, F, p0, HW, b, 0.f, lr, lg);
+    tw_ln<C, NV>(x, sgm, nullptr, mr, xf, NVT, VW, F, F4, p0, HW, b, 0.f, lr, lg);
     int64_t vrow[T::NVTM];  // row of voxel (vt*16 + lane&15), -1 when outside the group
 #pragma unroll
     for (int vt = 0; vt < T::NVTM; ++vt) {
       int64_t row = 0;
-      vrow[vt] = tw_row(vt * 16 + lr, VW, F, p0, HW, b, row) ? row : -1;
+      vrow[vt] = tw_row(vt * 16 + lr, VW, F, F4, p0, HW, b, row) ? row : -1;
       if (vrow[vt] >= 0 && xn_out) {
 #pragma unroll
         for (int ks = 0; ks < T::KS; ++ks) stnt16(xn_out + row * C + ks * 32 + lg * 8, xf[vt][ks]);
@@ -1169,7 +1197,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
               acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], dyf, acc, 0, 0, 0);
             }
             float o4[4] = {acc[0], acc[1], acc[2], acc[3]};
-            store4(sdo + (vt * 16 + lr) * HLD + dt * 16 + lg * 4, o4);
+            store4(sdo + hs_off<R>(vt * 16 + lr, dt * 16 + lg * 4), o4);
           }
         }
       }
@@ -1189,7 +1217,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
       for (int pp = 0; pp < T::PW; ++pp) {
         const int p = p0 + pp;
         if (p >= HW) break;
-        const int rb = pp * F;
+        const int rb = pp * F4;
         float Li = Lp[0];
         if constexpr (LPF) {
 #pragma unroll
@@ -1198,11 +1226,11 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
           const float v = lse[(((int64_t)b * NH + h) * HW + p) * F + (lr < F ? lr : 0)];
           Li = lr < F ? v : 0.f;
         }
-        const int rr = rb + (lr < F ? lr : 0);  // rows past F read the pixel's row 0 (finite); every product is masked by ok / pt = 0
-        const bf16x8 kr = ld16(sk + rr * HLD + lg * 8);
-        const bf16x8 qr = ld16(sq + rr * HLD + lg * 8);
-        const bf16x8 vr = ld16(sv + rr * HLD + lg * 8);
-        const bf16x8 dor = ld16(sdo + rr * HLD + lg * 8);
+        const int rr = rg_at(rb, hs_off<R>(lr < F ? lr : 0, lg * 8));  // rows past F read the pixel's row 0 (finite); every product is masked by ok / pt = 0
+        const bf16x8 kr = ld16(sk + rr);
+        const bf16x8 qr = ld16(sq + rr);
+        const bf16x8 vr = ld16(sv + rr);
+        const bf16x8 dor = ld16(sdo + rr);
         // -- transposed orientation: lane (g, i): entries (j = 4g + r, i)
         float D = 0.f;
         bf16x8 dst_b = zero8(), pt_b = zero8();
@@ -1231,8 +1259,8 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
         f32x4 dqt[2];
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
-          const bf16x8 kg = kslot_gather(sk, rb, half * 16, F, lane);
-          const bf16x8 vg = kslot_gather(sv, rb, half * 16, F, lane);
+          const bf16x8 kg = kslot_gather<R>(sk, rb, half * 16, F, lane);
+          const bf16x8 vg = kslot_gather<R>(sv, rb, half * 16, F, lane);
           dqt[half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kg, dst_b, z4, 0, 0, 0);  // dQ'^T[d][i]
           if (!o_out) continue;  // O written by the forward (cesm_tblock_fwd o)
           const f32x4 ot = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vg, pt_b, z4, 0, 0, 0);  // O^T[d][i]
@@ -1262,8 +1290,8 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
         f32x4 dkt[2], dvt[2];
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
-          const bf16x8 qg = kslot_gather(sq, rb, half * 16, F, lane);
-          const bf16x8 dog = kslot_gather(sdo, rb, half * 16, F, lane);
+          const bf16x8 qg = kslot_gather<R>(sq, rb, half * 16, F, lane);
+          const bf16x8 dog = kslot_gather<R>(sdo, rb, half * 16, F, lane);
           dkt[half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qg, ds_b, z4, 0, 0, 0);   // dK'^T[d][j]
           dvt[half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dog, p_b, z4, 0, 0, 0);   // dV^T[d][j]
         }
@@ -1279,9 +1307,9 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
             rope4(k4, rot, lr, d0, -1.f);
 #pragma unroll
             for (int r = 0; r < 4; ++r) q4[r] *= scale;
-            store4(sq + (rb + lr) * HLD + d0, q4);
-            store4(sk + (rb + lr) * HLD + d0, k4);
-            store4(sv + (rb + lr) * HLD + d0, v4);
+            store4(sq + rg_at(rb, hs_off<R>(lr, d0)), q4);
+            store4(sk + rg_at(rb, hs_off<R>(lr, d0)), k4);
+            store4(sv + rg_at(rb, hs_off<R>(lr, d0)), v4);
           }
         }
         wave_lds_sync();
@@ -1297,7 +1325,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
         const bf16* src = kind == 0 ? sq : (kind == 1 ? sk : sv);
         bf16x8 bf[T::NVTM];
 #pragma unroll
-        for (int vt = 0; vt < T::NVTM; ++vt) bf[vt] = vt < NVT ? ld16(src + (vt * 16 + lr) * HLD + lg * 8) : zero8();
+        for (int vt = 0; vt < T::NVTM; ++vt) bf[vt] = vt < NVT ? ld16(src + hs_off<R>(vt * 16 + lr, lg * 8)) : zero8();
 #pragma unroll
         for (int ct = 0; ct < T::CT; ++ct) {
           const bf16x8 a = ld_img(wqkv_t, ct, QKV / 32, kind * 8 + h, lane);  // image of W_qkv^T [C][768]
@@ -1310,7 +1338,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
           for (int vt = 0; vt < T::NVTM; ++vt) {
             if (vt >= NVT) break;
             int64_t row = 0;
-            if (tw_row(vt * 16 + lr, VW, F, p0, HW, b, row))
+            if (tw_row(vt * 16 + lr, VW, F, F4, p0, HW, b, row))
               stnt16(dqkv_out + row * QKV + kind * INNER + h * DH + lg * 8, bf[vt]);
           }
         }
@@ -1325,8 +1353,8 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
           for (int vt = 0; vt < T::NVTM; ++vt) {
             if (vt >= NVT) break;
             int64_t row = 0;
-            if (tw_row(vt * 16 + lr, VW, F, p0, HW, b, row))
-              stnt16(dqkv_out + row * QKV + kind * INNER + h * DH + lg * 8, ld16(src + (vt * 16 + lr) * HLD + lg * 8));
+            if (tw_row(vt * 16 + lr, VW, F, F4, p0, HW, b, row))
+              stnt16(dqkv_out + row * QKV + kind * INNER + h * DH + lg * 8, ld16(src + hs_off<R>(vt * 16 + lr, lg * 8)));
           }
         }
       }
@@ -1339,7 +1367,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
 #pragma unroll
     for (int vt = 0; vt < T::NVTM; ++vt) {
       int64_t row = 0;
-      if (vt < NVT && tw_row(vt * 16 + lr, VW, F, p0, HW, b, row))
+      if (vt < NVT && tw_row(vt * 16 + lr, VW, F, F4, p0, HW, b, row))
 #pragma unroll
         for (int ct = 0; ct < T::CT; ++ct) {
           float o4[4] = {dxacc[ct][vt][0], dxacc[ct][vt][1], dxacc[ct][vt][2], dxacc[ct][vt][3]};
@@ -1352,7 +1380,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
     for (int vt = 0; vt < T::NVTM; ++vt) {
       if (vt >= NVT) break;
       int64_t row = 0;
-      const bool ok = tw_row(vt * 16 + lr, VW, F, p0, HW, b, row);
+      const bool ok = tw_row(vt * 16 + lr, VW, F, F4, p0, HW, b, row);
       row = ok ? row : 0;  // loads unpredicated (row 0 outside the group), results selected
       const float m0 = mr[row * 2], r0 = mr[row * 2 + 1];
       const float mean = ok ? m0 : 0.f, rstd = ok ? r0 : 0.f;
@@ -1439,12 +1467,12 @@ __global__ void tb_sum_rows_kernel(const float* __restrict__ part, float* __rest
 template <int C>
 static size_t tw_fwd_smem(int F) {  // NOLINT
   const int R = ((TW<C>::PW * F + 15) / 16) * 16;
-  return (size_t)(((NH * F * F + 3) & ~3) + 16 * RS) * 4 + (size_t)4 * 3 * R * HLD * 2;
+  return (size_t)(((NH * F * F + 3) & ~3) + 16 * RS) * 4 + (size_t)4 * 3 * R * HS * 2 + 512;  // + tail pad: k-slot gathers may read 4 rows past the last slice
 }
 template <int C>
 static size_t tw_bwd_smem(int F) {
   const int R = ((TW<C>::PW * F + 15) / 16) * 16;
-  return (size_t)(5 * NH * F * F + 5 * C + 16 * RS) * 4 + (size_t)4 * 4 * R * HLD * 2 + 4 * 32 * 4;
+  return (size_t)(5 * NH * F * F + 5 * C + 16 * RS) * 4 + (size_t)4 * 4 * R * HS * 2 + 4 * 32 * 4;
 }
 template <typename K>
 static void allow_smem(K kernel, size_t bytes) {
@@ -1567,14 +1595,13 @@ extern "C" int cesm_diag_tw_stamps(unsigned long long* out, int n) {
 #ifndef TWH_EARLY_WT
 #define TWH_EARLY_WT 0  // twh_bwd: W'^T fragments of the dxn GEMM issued before the dW GEMM (1)
 #endif
-constexpr int TH_XLD = 72;   // xhat / dy tile row stride (bf16, 144-B rows)
 constexpr int TH_NVMAX = 3;  // voxel tiles per group (4*F <= 48): the 8 slices then fit in LDS
 
 static size_t twh_smem(int F, int NV) {
   (void)F;
   const int R = NV * 16;
-  return (size_t)16 * RS * 4 + (size_t)8 * TWH_PG * 2 * 256 * 2 + (size_t)2 * R * TH_XLD * 2 +
-         (size_t)8 * 4 * R * HLD * 2 + 1024;  // + tail pad: masked k-slot gathers may read 4 rows past a slice
+  return (size_t)16 * RS * 4 + (size_t)8 * TWH_PG * 2 * 256 * 2 + (size_t)2 * xt_elems(R) * 2 +
+         (size_t)8 * 4 * R * HS * 2 + 1024;  // + tail pad: masked k-slot gathers may read 4 rows past a slice
 }
 
 template <int NV>
@@ -1587,21 +1614,21 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
   constexpr int C = 64;
   using T = TW<C, NV>;
   constexpr int R = NV * 16;
-  static_assert(TH_PLD * 4 <= 4 * HLD * 2, "partial dxn rows fit over the wave's slices");
+  static_assert(TH_PLD * 4 <= 4 * HS * 2, "partial dxn rows fit over the wave's slices");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int FF = F * F;
   float* rot = smem;                                 // [16][RS]
   float* trbuf = rot + 16 * RS;                      // [8 waves][TWH_PG][2][16][16] bf16 P / dS tiles
-  bf16* xt = reinterpret_cast<bf16*>(trbuf) + 8 * TWH_PG * 2 * 256;  // [R][TH_XLD] xhat (bf16)
-  bf16* dyt = xt + R * TH_XLD;                       // [R][TH_XLD] dy
-  bf16* slices = dyt + R * TH_XLD;                   // 8 x [q|k|v|dO][R][HLD]
+  bf16* xt = reinterpret_cast<bf16*>(trbuf) + 8 * TWH_PG * 2 * 256;  // [R][64] xhat (bf16, region tile, xt_rs)
+  bf16* dyt = xt + xt_elems(R);                      // [R][64] dy
+  bf16* slices = dyt + xt_elems(R);                  // 8 x [q|k|v|dO][R][HS] (hs_off layout)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const int h = wid;
-  bf16* sq = slices + wid * 4 * R * HLD;
-  bf16* sk = sq + R * HLD;
-  bf16* sv = sk + R * HLD;
-  bf16* sdo = sv + R * HLD;
+  bf16* sq = slices + wid * 4 * R * HS;
+  bf16* sk = sq + R * HS;
+  bf16* sv = sk + R * HS;
+  bf16* sdo = sv + R * HS;
   for (int e = tid; e < F * 32; e += 512) rot[(e >> 5) * RS + (e & 31)] = rotg[e];
   // this wave's (head's) bias entries, log2 units: transposed (i = lr, j = 4g + r) and row-major (i = 4g + r, j = lr)
   float bt[4], brm[4];
@@ -1615,22 +1642,22 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
     brm[r] = ok ? b1 * LOG2E : 0.f;
   }
 
-  const int VW = T::PW * F;
+  const int F4 = pad4(F), VW = T::PW * F4;
   const int npg = (HW + T::PW - 1) / T::PW;
   const int ngroups = B * npg;
   // LN / LN-backward role of this thread: voxel vv of the group, channels 8cc..8cc+7
   const int vv = tid >> 3, cc = tid & 7;
   int fr[NV];
 #pragma unroll
-  for (int vt = 0; vt < NV; ++vt) fr[vt] = (vt * 16 + lr) % F;
+  for (int vt = 0; vt < NV; ++vt) fr[vt] = (vt * 16 + lr) % F4 < F ? (vt * 16 + lr) % F4 : 0;
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
 
   // the voxel row of (group gg, voxel v) or -1
   auto vrow = [&](int gg, int v) -> int64_t {
     const int b = gg / npg, pg = gg - b * npg;
     if (v >= VW) return -1;
-    const int pp = v / F, f = v - pp * F, p = pg * T::PW + pp;
-    if (p >= HW) return -1;
+    const int pp = v / F4, f = v - pp * F4, p = pg * T::PW + pp;
+    if (f >= F || p >= HW) return -1;
     return ((int64_t)b * F + f) * HW + p;
   };
   // prefetch registers: x, dy chunk and (mean, rstd) of this thread's voxel in the next group
@@ -1659,6 +1686,8 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
   TW_ST_DECL
   for (int gg = blockIdx.x; gg < ngroups; gg += gridDim.x) {
     const int b = gg / npg, p0 = (gg - b * npg) * T::PW;
+    // lane-derived LDS offsets recomputed per group from an opaque lane copy (not hoisted: register-bound kernel)
+    const int lane = opaque_v(threadIdx.x & 63), lr = lane & 15, lg = lane >> 4;
     // ---- LN of the group (this thread's voxel chunk) from the prefetch registers
     float rstd_cur = 0.f;
     if (vv < R) {
@@ -1669,8 +1698,8 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
         xh[e] = (bf16)(ok ? ((float)xpf[e] - mpf) * rpf : 0.f);
         dv[e] = ok ? dpf[e] : (bf16)0.f;
       }
-      *reinterpret_cast<bf16x8*>(xt + vv * TH_XLD + cc * 8) = xh;
-      *reinterpret_cast<bf16x8*>(dyt + vv * TH_XLD + cc * 8) = dv;
+      *reinterpret_cast<bf16x8*>(xt + rg_off<1>(vv, cc * 8, xt_rs(R))) = xh;
+      *reinterpret_cast<bf16x8*>(dyt + rg_off<1>(vv, cc * 8, xt_rs(R))) = dv;
       rstd_cur = ok ? rpf : 0.f;
     }
     const bool ok_cur = okpf;
@@ -1712,7 +1741,7 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
 #pragma unroll
       for (int vt = 0; vt < NV; ++vt)
 #pragma unroll
-        for (int ks = 0; ks < T::KS; ++ks) xf[vt][ks] = ld16(xt + (vt * 16 + lr) * TH_XLD + ks * 32 + lg * 8);
+        for (int ks = 0; ks < T::KS; ++ks) xf[vt][ks] = ld16(xt + rg_off<1>(vt * 16 + lr, ks * 32 + lg * 8, xt_rs(R)));
 #if TWH_QKV_PIPE
 #pragma unroll
       for (int c2 = 0; c2 < 6; c2 += 2) {
@@ -1743,7 +1772,7 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
               for (int r = 0; r < 4; ++r) o4[r] *= scale;
             }
             if (kind < 2) rope4(o4, rot, fr[vt], d0, 1.f);
-            store4(dst + (vt * 16 + lr) * HLD + d0, o4);
+            store4(dst + hs_off<R>(vt * 16 + lr, d0), o4);
           }
         }
       }
@@ -1769,10 +1798,10 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
         f32x4 acc = z4;
 #pragma unroll
         for (int ks = 0; ks < T::KS; ++ks)
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], ld16(dyt + (vt * 16 + lr) * TH_XLD + ks * 32 + lg * 8),
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], ld16(dyt + rg_off<1>(vt * 16 + lr, ks * 32 + lg * 8, xt_rs(R))),
                                                         acc, 0, 0, 0);
         float o4[4] = {acc[0], acc[1], acc[2], acc[3]};
-        store4(sdo + (vt * 16 + lr) * HLD + dt * 16 + lg * 4, o4);
+        store4(sdo + hs_off<R>(vt * 16 + lr, dt * 16 + lg * 4), o4);
       }
     }
     wave_lds_sync();
@@ -1786,12 +1815,12 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
       f32x4 st[PG], dpt[PG];
 #pragma unroll
       for (int u = 0; u < PG; ++u) {
-        const int rb = (pp0 + u) * F;
-        const int rr = rb + (lr < F ? lr : 0);
-        const bf16x8 kr = ld16(sk + rr * HLD + lg * 8);
-        const bf16x8 qr = ld16(sq + rr * HLD + lg * 8);
-        const bf16x8 vr = ld16(sv + rr * HLD + lg * 8);
-        const bf16x8 dor = ld16(sdo + rr * HLD + lg * 8);
+        const int rb = (pp0 + u) * F4;
+        const int rr = rg_at(rb, hs_off<R>(lr < F ? lr : 0, lg * 8));
+        const bf16x8 kr = ld16(sk + rr);
+        const bf16x8 qr = ld16(sq + rr);
+        const bf16x8 vr = ld16(sv + rr);
+        const bf16x8 dor = ld16(sdo + rr);
         st[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kr, qr, z4, 0, 0, 0);    // S^T[j][i]
         dpt[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vr, dor, z4, 0, 0, 0);  // dP^T[j][i]
       }
@@ -1821,35 +1850,35 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
           p4[r] = (bf16)pt[r];
         }
         // tile[i = lr][j = 4g .. 4g+3]
-        *reinterpret_cast<bf16x4*>(trt + (u * 2 + 0) * 256 + lr * 16 + lg * 4) = p4;
-        *reinterpret_cast<bf16x4*>(trt + (u * 2 + 1) * 256 + lr * 16 + lg * 4) = d4;
+        *reinterpret_cast<bf16x4*>(trt + (u * 2 + 0) * 256 + trt_off(lr, lg * 4)) = p4;
+        *reinterpret_cast<bf16x4*>(trt + (u * 2 + 1) * 256 + trt_off(lr, lg * 4)) = d4;
       }
       f32x4 dqt[PG][2];
 #pragma unroll
       for (int u = 0; u < PG; ++u)
 #pragma unroll
         for (int half = 0; half < 2; ++half)
-          dqt[u][half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kslot_gather(sk, (pp0 + u) * F, half * 16, F, lane),
+          dqt[u][half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kslot_gather<R>(sk, (pp0 + u) * F4, half * 16, F, lane),
                                                                  dst_b[u], z4, 0, 0, 0);  // dQ'^T[d][i]
       wave_lds_sync();  // P / dS tiles visible
       f32x4 dkt[PG][2], dvt[PG][2];
 #pragma unroll
       for (int u = 0; u < PG; ++u) {
-        const bf16x8 p_b = kslot_gather_ld(trt + (u * 2 + 0) * 256, 16, 0, 0, F, lane);   // P[i = 4g+e][j = lr]
-        const bf16x8 ds_b = kslot_gather_ld(trt + (u * 2 + 1) * 256, 16, 0, 0, F, lane);  // dS[i = 4g+e][j = lr]
+        const bf16x8 p_b = kslot_gather_trt(trt + (u * 2 + 0) * 256, F, lane);   // P[i = 4g+e][j = lr]
+        const bf16x8 ds_b = kslot_gather_trt(trt + (u * 2 + 1) * 256, F, lane);  // dS[i = 4g+e][j = lr]
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
-          const int rb = (pp0 + u) * F;
-          dkt[u][half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kslot_gather(sq, rb, half * 16, F, lane), ds_b, z4,
+          const int rb = (pp0 + u) * F4;
+          dkt[u][half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kslot_gather<R>(sq, rb, half * 16, F, lane), ds_b, z4,
                                                                  0, 0, 0);  // dK'^T[d][j]
-          dvt[u][half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kslot_gather(sdo, rb, half * 16, F, lane), p_b, z4,
+          dvt[u][half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kslot_gather<R>(sdo, rb, half * 16, F, lane), p_b, z4,
                                                                  0, 0, 0);  // dV^T[d][j]
         }
       }
       wave_lds_sync();  // all reads of these pixels' rows (and the tiles) done before they are overwritten
 #pragma unroll
       for (int u = 0; u < PG; ++u) {
-        const int rb = (pp0 + u) * F;
+        const int rb = (pp0 + u) * F4;
         if (lr < F && p0 + pp0 + u < HW) {
 #pragma unroll
           for (int half = 0; half < 2; ++half) {
@@ -1861,9 +1890,9 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
             rope4(k4, rot, lr, d0, -1.f);
 #pragma unroll
             for (int r = 0; r < 4; ++r) q4[r] *= scale;
-            store4(sq + (rb + lr) * HLD + d0, q4);
-            store4(sk + (rb + lr) * HLD + d0, k4);
-            store4(sv + (rb + lr) * HLD + d0, v4);
+            store4(sq + rg_at(rb, hs_off<R>(lr, d0)), q4);
+            store4(sk + rg_at(rb, hs_off<R>(lr, d0)), k4);
+            store4(sv + rg_at(rb, hs_off<R>(lr, d0)), v4);
           }
         }
       }
@@ -1890,11 +1919,11 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
     for (int kk = 0; kk < NV; ++kk) {
       s16x4 bx[4];
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) bx[nt] = tr4(xt, TH_XLD, kk * 16, nt * 16, lane);
+      for (int nt = 0; nt < 4; ++nt) bx[nt] = tr4_rg<1>(xt, kk * 16, nt * 16, xt_rs(R), lane);
 #pragma unroll
       for (int m = 0; m < 6; ++m) {
         const bf16* src = (m >> 1) == 0 ? sq : ((m >> 1) == 1 ? sk : sv);
-        const s16x4 a = tr4(src, HLD, kk * 16, (m & 1) * 16, lane);
+        const s16x4 a = tr4_hs<R>(src, kk * 16, (m & 1) * 16, lane);
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt)
           dwacc[m][nt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, bx[nt], dwacc[m][nt], 0, 0, 0);
@@ -1922,7 +1951,7 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
 #endif
 #pragma unroll
         for (int vt = 0; vt < NV; ++vt)
-          dxacc[ct][vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ld16(src + (vt * 16 + lr) * HLD + lg * 8),
+          dxacc[ct][vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ld16(src + hs_off<R>(vt * 16 + lr, lg * 8)),
                                                                   dxacc[ct][vt], 0, 0, 0);
       }
     }
@@ -1933,7 +1962,7 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
       for (int ct = 0; ct < T::CT; ++ct)
 #pragma unroll
         for (int vt = 0; vt < NV; ++vt)
-          *reinterpret_cast<f32x4*>(part + (vt * 16 + lr) * TH_PLD + ct * 16 + lg * 4) = dxacc[ct][vt];
+          *reinterpret_cast<f32x4*>(part + pl_off(vt * 16 + lr, ct * 16 + lg * 4)) = dxacc[ct][vt];
     }
     TW_ST(5)
     __syncthreads();  // (B) every head's partial written
@@ -1946,14 +1975,14 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
       for (int e = 0; e < 8; ++e) g[e] = 0.f;
 #pragma unroll
       for (int w = 0; w < 8; ++w) {
-        const float* pw = reinterpret_cast<const float*>(slices + w * 4 * R * HLD) + v * TH_PLD + cc * 8;
-        const f32x4 a0 = *reinterpret_cast<const f32x4*>(pw);
-        const f32x4 a1 = *reinterpret_cast<const f32x4*>(pw + 4);
+        const float* pw = reinterpret_cast<const float*>(slices + w * 4 * R * HS);
+        const f32x4 a0 = *reinterpret_cast<const f32x4*>(pw + pl_off(v, cc * 8));
+        const f32x4 a1 = *reinterpret_cast<const f32x4*>(pw + pl_off(v, cc * 8 + 4));
 #pragma unroll
         for (int e = 0; e < 4; ++e) { g[e] += a0[e]; g[4 + e] += a1[e]; }
       }
-      const bf16x8 xh = *reinterpret_cast<const bf16x8*>(xt + v * TH_XLD + cc * 8);
-      const bf16x8 dv = *reinterpret_cast<const bf16x8*>(dyt + v * TH_XLD + cc * 8);
+      const bf16x8 xh = *reinterpret_cast<const bf16x8*>(xt + rg_off<1>(v, cc * 8, xt_rs(R)));
+      const bf16x8 dv = *reinterpret_cast<const bf16x8*>(dyt + rg_off<1>(v, cc * 8, xt_rs(R)));
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int e = 0; e < 8; ++e) { s1 += g[e]; s2 = fmaf(g[e], (float)xh[e], s2); }

@@ -54,6 +54,7 @@ class GradAllReducer:
 
     def __init__(self, bucket_bytes=32 << 20, use_side_stream=True):
         self.world = dist.get_world_size() if is_dist() else 1
+        self.rank = dist.get_rank() if is_dist() else 0
         self.bucket_elems = max(1, bucket_bytes // 4)
         self.side = use_side_stream
         self._stream = None

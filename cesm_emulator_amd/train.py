@@ -35,6 +35,20 @@ def rank_generator(device, seed=2, rank=0):
     return g
 
 
+def dp_generator(device, dp, seed=None):
+    """the per-rank t / eps stream of a data-parallel run: base seed `seed` (e.g. the training config's), or
+    one drawn on rank 0 from the default generator and broadcast, so every rank agrees on it whatever its
+    default generator state; the rank is the all-reducer's own (dp.rank), not a global lookup"""
+    if seed is None:
+        s = torch.randint(0, 2**31 - 1, (1,), dtype=torch.int64)
+        if getattr(dp, "world", 1) > 1 and torch.distributed.is_initialized():
+            dev = device if torch.distributed.get_backend() == "nccl" else torch.device("cpu")
+            s = s.to(dev)
+            torch.distributed.broadcast(s, src=0)
+        seed = int(s.item())
+    return rank_generator(device, seed, getattr(dp, "rank", 0))
+
+
 def make_optimizer(diffusion, train_cfg):
     """train.py:1077-1083 (+ the clip of :865 folded into the fused step)."""
     opt = train_cfg.get("optimizer", {})
@@ -60,12 +74,13 @@ def train_step(diffusion, optimizer, x0, cond, max_grad_norm=1.0, dp=None, t=Non
     return loss.detach()
 
 
-def train_one_epoch(diffusion, dl, optimizer, device, max_grad_norm=1.0, use_amp=True, epoch=1, dp=None):
-    """train.py:808-911; returns the epoch's mean loss."""
+def train_one_epoch(diffusion, dl, optimizer, device, max_grad_norm=1.0, use_amp=True, epoch=1, dp=None, seed=None):
+    """train.py:808-911; returns the epoch's mean loss.  With dp (world > 1) and no generator set yet, each rank
+    draws t / eps from its own stream (dp_generator: base `seed`, or one broadcast from rank 0)."""
     diffusion.train()
     diffusion.model.compute_dtype = torch.bfloat16 if use_amp else torch.float32
     if dp is not None and getattr(dp, "world", 1) > 1 and diffusion.generator is None:
-        diffusion.generator = rank_generator(device, 2, torch.distributed.get_rank())
+        diffusion.generator = dp_generator(device, dp, seed)
     total, steps = 0.0, 0
     for step, (cond, x0) in enumerate(dl, start=1):
         cond = cond.to(device, non_blocking=True)

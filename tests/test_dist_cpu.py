@@ -141,3 +141,34 @@ def test_overlapped_allreduce_matches_average(tmp_path):
     lo = r0["issued"].tolist()
     # buckets went out before finish(): after the last group only the shared param's bucket is left
     assert lo[0] < o and lo[-1] <= 64 and lo == sorted(lo, reverse=True), lo
+
+
+def _seed_worker(rank, world, port, out_path):
+    """train_one_epoch's data-parallel branch on CPU (gloo): each rank gets its own t / eps stream from a base
+    seed broadcast by rank 0 (the ranks' default generators deliberately differ here) and dp.rank"""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from types import SimpleNamespace
+    from cesm_emulator_amd import distributed as D
+    from cesm_emulator_amd.train import train_one_epoch
+    D.setup(backend="gloo")
+    torch.manual_seed(50 + rank)  # diverged default generators: the broadcast base seed must still agree
+    red = D.GradAllReducer()
+    diff = SimpleNamespace(train=lambda: None, model=SimpleNamespace(), generator=None)
+    train_one_epoch(diff, [], None, torch.device("cpu"), dp=red)  # empty loader: only the set-up runs
+    t = torch.randint(0, 1000, (16,), generator=diff.generator)
+    eps = torch.randn(16, generator=diff.generator)
+    torch.save({"t": t, "eps": eps, "seed": diff.generator.initial_seed(), "rank": red.rank}, out_path + f".{rank}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_train_one_epoch_rank_streams(tmp_path):
+    out = str(tmp_path / "seed.pt")
+    mp.spawn(_seed_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    r0 = torch.load(out + ".0", weights_only=True)
+    r1 = torch.load(out + ".1", weights_only=True)
+    assert (r0["rank"], r1["rank"]) == (0, 1)
+    assert r1["seed"] == r0["seed"] + 1  # one broadcast base seed, offset by the all-reducer's rank
+    assert not torch.equal(r0["t"], r1["t"]) and not torch.equal(r0["eps"], r1["eps"])

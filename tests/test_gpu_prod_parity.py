@@ -121,8 +121,9 @@ def test_conv3x3p_level0_bf16(dev, H, W, with_res):
 def test_gn_epilogue_stats_bf16(dev, C1, C2, Cout, H, W, B, Fr, kern):
     """The Block conv writes GroupNorm (sum, sum of squares) partials per channel quad from its epilogue
     (cesm_conv_fwd_gn); cesm_gn_stats_part reduces them.  y must be bit-identical to the plain conv launch,
-    and (mean, rstd) must match the separate statistics pass over the stored y (gn_stats) to the bf16
-    rounding of y (the partials see the fp32 values before rounding: |d mean| / std and d rstd / rstd ~ 1e-5)."""
+    and (mean, rstd) must match the separate statistics pass over the stored y (gn_stats) up to summation order:
+    the partials sum the bf16-rounded values the kernel stores (round 2 summed the fp32 values before rounding,
+    1e-5-level differences)."""
     G = 8
     Nb = B * Fr
     assert K.conv_fwd_variant(BF, Nb, H, W, C1, C2, H, W, Cout, Cout, 3, 3, 1, 1, 1) == kern
@@ -146,7 +147,7 @@ def test_gn_epilogue_stats_bf16(dev, C1, C2, Cout, H, W, B, Fr, kern):
     dm = ((m - m0).abs() * r0).max().item()
     dr = ((r - r0).abs() / r0).max().item()
     print(f"{kern} {C1}+{C2}->{Cout} {H}x{W}: |d mean|/std {dm:.2e}  d rstd/rstd {dr:.2e}  nslot {nslot}")
-    assert dm < 2e-4 and dr < 2e-4
+    assert dm < 1e-5 and dr < 1e-5
     # run-to-run reproducible
     _, part2 = K.conv_fwd_gn(x1, x2, wp, bias, geom, B, nslot)
     assert torch.equal(part, part2)

@@ -5,8 +5,11 @@ through the product's train_step + GradAllReducer (2 ranks, gloo, one GPU).
 Reference: dataset_single_member.py:168-196 (item), train.py:1005-1012 / 830-831 (DataLoader, pin,
 H2D), train.py:849-880 (step), model.py:205-206 (t / eps draws), SURVEY.md §8(e) E1.
 """
+import json
 import os
 import socket
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -61,8 +64,8 @@ def test_loader_batches_bit_equal_to_dataset(dev, kind, center, crop, p):
 
 def test_loaders_feed_training_identically(dev):
     """train_one_epoch fed by the pinned (host gather + side-stream H2D) and the device (HBM gather) loader
-    gives identical epoch losses and parameters (same numpy / t-eps seeds): bit-identical in fp32 mode,
-    to float-summation order in bf16"""
+    gives identical epoch losses and parameters (same numpy / t-eps seeds), bit-identical in fp32 and in bf16
+    mode (every reduction on the bf16 path has a fixed order, tests/test_gpu_determinism.py)"""
     cond, tgt = _fields(T=8, M=2, H=32, W=48, seed=1)
     Kw = 3
     out = {}
@@ -83,10 +86,7 @@ def test_loaders_feed_training_identically(dev):
         ldv, pd = out[(dt, "device")]
         print(f"{dt}: epoch loss pinned {lp:.6f} device {ldv:.6f}, params rel {rel(pp, pd):.2e}")
         assert np.isfinite(lp)
-        if dt == "fp32":
-            assert lp == ldv and torch.equal(pp, pd)
-        else:  # the fused bf16 backwards sum LayerNorm-gamma partials with LDS float atomics (order varies)
-            assert abs(lp - ldv) <= 1e-4 * abs(lp) and rel(pp, pd) < 1e-5
+        assert lp == ldv and torch.equal(pp, pd)
 
 
 # ------------------------------------------------------------------ optimizer / autograd / RNG plumbing
@@ -188,16 +188,16 @@ def _batch():
     return x0, cond, t, noise
 
 
-def _make(dev):
+def _make(dev, dtype=torch.float32):
     torch.manual_seed(1)
     net = UNet(ch_mults=(1, 2)).to(dev)
-    net.compute_dtype = torch.float32
+    net.compute_dtype = dtype
     d = Diffusion(net).to(dev)
     opt = FusedAdamW(d.parameters(), lr=1e-3, betas=(0.9, 0.999), weight_decay=1e-4, max_grad_norm=1.0)
     return d, opt
 
 
-def _dp_worker(rank, world, port, out_path):
+def _dp_worker(rank, world, port, out_path, dtype=torch.float32):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0")
     import torch.distributed as dist
@@ -205,7 +205,7 @@ def _dp_worker(rank, world, port, out_path):
     torch.cuda.set_device(0)
     D.setup(backend="gloo")
     dev = torch.device("cuda:0")
-    d, opt = _make(dev)
+    d, opt = _make(dev, dtype)
     red = D.GradAllReducer(bucket_bytes=256 << 10)
     if rank == 1:  # a perturbed replica is re-synchronised by the initial broadcast
         opt.flat.data.add_(1.0)
@@ -220,19 +220,21 @@ def _dp_worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-def test_dp_step_equals_full_batch_step(dev, tmp_path):
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["fp32", "bf16"])
+def test_dp_step_equals_full_batch_step(dev, tmp_path, dtype):
     """2 ranks (gloo on one GPU) through train_step + GradAllReducer.arm/finish (overlapped buckets) with
-    explicit t / eps: after two steps both replicas equal the 1-rank run on the concatenated batch"""
+    explicit t / eps: after two steps both replicas equal the 1-rank run on the concatenated batch, in the fp32
+    kernel mode and on the bf16 production kernels"""
     port = _free_port()
     out = str(tmp_path / "dp")
     ctx = mp.get_context("spawn")
-    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, out)) for r in range(2)]
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, out, dtype)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(timeout=240)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-    d, opt = _make(dev)
+    d, opt = _make(dev, dtype)
     x0, cond, t, noise = _batch()
     for _ in range(2):
         train_step(d, opt, x0.to(dev), cond.to(dev), 1.0, None, t=t.to(dev), noise=noise.to(dev))
@@ -240,8 +242,31 @@ def test_dp_step_equals_full_batch_step(dev, tmp_path):
     p0, p1 = torch.load(f"{out}.0", weights_only=True), torch.load(f"{out}.1", weights_only=True)
     assert torch.equal(p0, p1)
     moved = (full - p0).abs()
-    print(f"dp vs full batch: rel {rel(p0, full):.2e}, max abs {moved.max().item():.2e}")
-    # Adam moves each element ~lr*sign(g) in the first steps; fp32 reduction-order noise can only flip the
+    print(f"dp vs full batch ({dtype}): rel {rel(p0, full):.2e}, max abs {moved.max().item():.2e}")
+    # Adam moves each element ~lr*sign(g) in the first steps; reduction-order noise (fp32 accumulators in both
+    # modes: the bf16 path rounds the same per-sample activations, only the batch sums regroup) can only flip the
     # sign where |g| is at noise level, so compare element-wise against the step scale
     assert (moved > 0.05 * 1e-3).double().mean().item() < 1e-3
     assert rel(p0, full) < 1e-5
+
+
+def test_bench_multirank_gloo_rehearsal():
+    """bench.py's N > 1 path -- D.setup, the barrier, the MAX all-reduce of the elapsed time, the rank-0-only
+    JSON line and destroy_process_group (reference: train.py:207-221, 1075-1076) -- run as the driver runs it
+    (torch.distributed.run, one process per rank), 2 ranks sharing the one GPU over gloo"""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+           "--dist-backend", "gloo", "--steps", "2", "--warmup", "2", "--no-cpu-baseline", "--other-configs", "",
+           "--batch", "1", "--height", "64", "--width", "96"]
+    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 only
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["value"] > 0 and np.isfinite(out["loss"]) and out["steps"] == 2
