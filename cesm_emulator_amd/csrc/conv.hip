@@ -1266,6 +1266,15 @@ __device__ __forceinline__ void cp_taps(const char* sh, const char* sw, const in
 // bf16 in the stage just consumed and writes full 128-B pixel rows (+ residual) with exactly 2*NG
 // buffer stores per wave, so the next step waits for its DMA with vmcnt(2*NG), not for the stores.
 // ----------------------------------------------------------------------------------------
+// Dynamic item queue of conv3x3p (round 3): [0] next dynamic item - gridDim.x, [1] blocks finished.  Each block
+// takes item blockIdx.x first, then claims the next item one item ahead (thread 0, agent-scope atomic issued at the
+// item's first step, published through LDS at its second step's barrier), so a block slowed down by co-running
+// kernels (weight gradients on a second stream, RCCL all-reduces overlapped with the backward) takes fewer items
+// instead of leaving a static-split tail.  The last block to finish resets both counters for the next launch
+// (launches of this kernel are stream-ordered).  Outputs do not depend on the assignment (every item writes its own
+// pixels and GroupNorm slots).
+__device__ int g_cp_queue[2];
+
 template <int TW, int NG, bool RW, int NST = 2, int HPW = CW_HPW>
 __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
                                                           const bf16* __restrict__ w, const float* __restrict__ bias,
@@ -1284,9 +1293,10 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
   constexpr int STG = RW ? HPW * 4 * 1024 : CP_STAGE;
   constexpr int WRES = RW ? 2 * CW_WROWS * 64 : 0;
   constexpr int BIASB = RW ? 256 : 4096;
-  __shared__ __attribute__((aligned(1024))) char lds[NST * STG + WRES + BIASB];
+  __shared__ __attribute__((aligned(1024))) char lds[NST * STG + WRES + BIASB + 16];
   char* wres = lds + NST * STG;
   float* sbias = reinterpret_cast<float*>(lds + NST * STG + WRES);
+  int* s_next = reinterpret_cast<int*>(lds + NST * STG + WRES + BIASB);  // the claimed next item
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const int HP = (TH + 2) * CP_PITCH;
@@ -1297,6 +1307,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
   const int prow = lane >> 2, pslot = lane & 3;
   const int nmine = nitems > (int)blockIdx.x ? (nitems - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
   const int nsteps = nmine * nchunk;
+  const bool dynq = NST == 2 && nchunk >= 2 && !(dbg & 16);  // dynamic item queue (static split: dbg bit 16)
 
   // per-lane halo row -> tile-relative (hy, hx) of piece k (item independent); -1: zero row
   int hrel[HPW];
@@ -1331,8 +1342,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
   __amdgpu_buffer_rsrc_t dxrs, dwrs;
   int dcs = 0, dy0 = 0, dx0 = 0;
   char* dsh = lds;
-  auto step_src = [&](int s) {
-    const int it = (int)blockIdx.x + (s / nchunk) * (int)gridDim.x, ch = s % nchunk;
+  auto step_src = [&](int s, int it, int ch) {
     int n, cob;
     item_geo(it, n, dy0, dx0, cob);
     const int c0 = ch * 32;
@@ -1368,8 +1378,8 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
     }
   };
   constexpr int NPIECE = RW ? HPW : HPW + CW_WPW;  // per wave per step
-  auto issue = [&](int s) {
-    step_src(s);
+  auto issue = [&](int s, int it, int ch) {
+    step_src(s, it, ch);
 #pragma unroll
     for (int k = 0; k < NPIECE; ++k) issue_piece(k);
   };
@@ -1390,10 +1400,13 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
 
 #pragma unroll
   for (int q = 0; q < NST - 1; ++q)
-    if (q < nsteps) issue(q);
+    if (q < nsteps) issue(q, (int)blockIdx.x + (q / nchunk) * (int)gridDim.x, q % nchunk);
   int s = 0;
   bool epi = false;
-  for (int k = 0; k < nmine; ++k) {
+  int claim = 0;  // thread 0: the atomically claimed next item (dynq)
+  int it = (int)blockIdx.x;
+  for (int k = 0; it < nitems; ++k) {
+    int nxt = it + (int)gridDim.x;  // static split; dynq: replaced at the item's second step
     f32x4 acc[4][NG];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -1420,18 +1433,28 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       epi = false;
+      if (dynq && ch == 1) {  // publish the claimed next item (its atomic is older than this step's DMA: landed)
+        if (tid == 0) *s_next = claim;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
       __builtin_amdgcn_s_barrier();                     // ... for every wave; step s-1's reads are done
+      if (dynq && ch == 1) nxt = *s_next;
+      if (dynq && ch == 0 && tid == 0)  // claim the item after this one (returns long before step 1 needs it)
+        claim = (int)gridDim.x + __hip_atomic_fetch_add(&g_cp_queue[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const char* sh = lds + (s % NST) * STG;
       const char* sw = RW ? wres + ch * CW_WROWS * 64 : sh + CW_HROWS * 64;
       const int sp = s + NST - 1;  // step prefetched now, into the stage step s-1 used
-      const bool pf = sp < nsteps && !(dbg & 1);
+      // its item / chunk: NST = 2: the next chunk of this item, or the next item's first chunk
+      const int sp_it = NST == 2 ? (ch + 1 < nchunk ? it : nxt) : (int)blockIdx.x + (sp / nchunk) * (int)gridDim.x;
+      const int sp_ch = NST == 2 ? (ch + 1 < nchunk ? ch + 1 : 0) : sp % nchunk;
+      const bool pf = (NST == 2 ? sp_it < nitems : sp < nsteps) && !(dbg & 1);
       if ((dbg & 2) || !RW) {  // spreading the 19-piece (!RW) DMA over the taps spills at NG = 8
-        if (pf) issue(sp);
+        if (pf) issue(sp, sp_it, sp_ch);
         if (!(dbg & 2)) cp_taps<NG>(sh, sw, bad, a_lane, acc);
       } else if (pf) {
         // the prefetch DMA spread over this step's taps (issuing all of it up front stalls the wave on
         // the vector-memory queue before its first MFMA)
-        step_src(sp);
+        step_src(sp, sp_it, sp_ch);
         auto hook = [&](int tap) {
 #pragma unroll
           for (int k = 0; k < NPIECE; ++k)
@@ -1443,8 +1466,9 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
       }
     }
     int n, y0, x0, cob;
-    item_geo((int)blockIdx.x + k * (int)gridDim.x, n, y0, x0, cob);
+    item_geo(it, n, y0, x0, cob);
     const int n0 = cob * 64;
+    it = nxt;
     if (dbg & 4) {  // debug: no epilogue (keep the accumulators live)
       float sacc = 0.f;
 #pragma unroll
@@ -1579,6 +1603,12 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
       }
     }
     epi = true;
+  }
+  if (dynq && tid == 0) {  // the last block out resets the queue for the next launch
+    if (__hip_atomic_fetch_add(&g_cp_queue[1], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
+      __hip_atomic_store(&g_cp_queue[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&g_cp_queue[1], 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -3785,7 +3815,8 @@ int conv_fwd_launch(int dtype, const void* x1, const void* x2, const void* wp, c
     case CFV_P32_RW:
     case CFV_P32: {
       const int dbg = (getenv_flag("CESM_DBG_NODMA") ? 1 : 0) | (getenv_flag("CESM_DBG_NOMFMA") ? 2 : 0) |
-                      (getenv_flag("CESM_DBG_NOEPI") ? 4 : 0) | (getenv_flag("CESM_DBG_NOSTORE") ? 8 : 0);
+                      (getenv_flag("CESM_DBG_NOEPI") ? 4 : 0) | (getenv_flag("CESM_DBG_NOSTORE") ? 8 : 0) |
+                      (getenv_flag("CESM_CONV_STATIC") ? 16 : 0);  // static item split instead of the queue
       const int tx = (int)cdiv(Wo, TW), ty = (int)cdiv(Ho, TH);
       const int ncob = Cout / 64;
       const int nitems = Nb * tx * ty * ncob;

@@ -703,19 +703,6 @@ __device__ __forceinline__ bf16x8 kslot_gather(const bf16* tile, int rb, int c0,
   return r;
 }
 
-// 16 x 16 bf16 P / dS tiles of twh_bwd: 32-B rows, 8-B slot s of row r stored at s ^ ((r >> 2) & 3) (the
-// bf16x4 row writes of 16 lanes and the transposed reads are then both conflict-free; plain rows: 4-way writes)
-__device__ __forceinline__ int trt_off(int r, int c) { return r * 16 + (((c >> 2) ^ ((r >> 2) & 3)) << 2) + (c & 3); }
-// kslot_gather of a P / dS tile: lane (g, i) gets tile[4g + e][i] in element e (rows >= F zero)
-__device__ __forceinline__ bf16x8 kslot_gather_trt(const bf16* tile, int F, int lane) {
-  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tile + trt_off(4 * g + q, 4 * p)));
-  bf16x8 r = zero8();
-#pragma unroll
-  for (int e = 0; e < 4; ++e)
-    if (4 * g + e < F) r[e] = __builtin_bit_cast(bf16, (short)v[e]);
-  return r;
-}
 // hardware-transpose read of a head slice: lane (g, i) <- tile[r0 + 4g + e][c0 + i]
 template <int R>
 __device__ __forceinline__ s16x4 tr4_hs(const bf16* tile, int r0, int c0, int lane) {
@@ -1131,8 +1118,6 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
   TW_ST_DECL
   for (int pg = blockIdx.x * 4 + wid; pg < npg; pg += nw) {
     const int p0 = pg * T::PW;
-    // lane-derived LDS offsets recomputed per group from an opaque lane copy (not hoisted: register-bound kernel)
-    const int lane = opaque_v(threadIdx.x & 63), lr = lane & 15, lg = lane >> 4;
     bf16x8 xf[T::NVTM][T::KS];
     tw_ln<C, NV>(x, sgm, nullptr, mr, xf, NVT, VW, F, F4, p0, HW, b, 0.f, lr, lg);
     int64_t vrow[T::NVTM];  // row of voxel (vt*16 + lane&15), -1 when outside the group
@@ -1572,6 +1557,26 @@ extern "C" int cesm_diag_tw_stamps(unsigned long long* out, int n) {
 // as dW' = sum dqkv^T xhat, and twh_dw_finalize turns it into dW = dW' diag(gamma) and
 // dgamma_c = sum_j W[j][c] dW'[j][c] (the LN gamma gradient sum_v dxn*xhat, regrouped).
 // ============================================================================================
+// round-2 helpers of twh_bwd (80-B slice rows, see the TWH section)
+__device__ __forceinline__ bf16x8 kslot_gather_hld(const bf16* tile, int rb, int c0, int F, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tile + (rb + 4 * g + q) * HLD + c0 + 4 * p));
+  bf16x8 r = zero8();
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    if (4 * g + e < F) r[e] = __builtin_bit_cast(bf16, (short)v[e]);
+  return r;
+}
+__device__ __forceinline__ bf16x8 kslot_gather_ld(const bf16* tile, int ld, int rb, int c0, int F, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tile + (rb + 4 * g + q) * ld + c0 + 4 * p));
+  bf16x8 r = zero8();
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    if (4 * g + e < F) r[e] = __builtin_bit_cast(bf16, (short)v[e]);
+  return r;
+}
+
 #ifndef TWH_FULL
 // measured at B = 8 (tools/tblock_time.py): PG 2 / FULL 0 / EARLY_WT 0 4.47 ms (no spills); PG 2 with both on
 // 5.35 ms (40 VGPRs spilled); PG 1 4.86 ms
@@ -1595,13 +1600,19 @@ extern "C" int cesm_diag_tw_stamps(unsigned long long* out, int n) {
 #ifndef TWH_EARLY_WT
 #define TWH_EARLY_WT 0  // twh_bwd: W'^T fragments of the dxn GEMM issued before the dW GEMM (1)
 #endif
+constexpr int TH_XLD = 72;   // xhat / dy tile row stride (bf16, 144-B rows)
 constexpr int TH_NVMAX = 3;  // voxel tiles per group (4*F <= 48): the 8 slices then fit in LDS
+// twh_bwd keeps round 2's padded tiles (80-B slice rows, 144-B xhat / dy rows, 68-float partial rows): the region
+// layouts of the other fused kernels remove its LDS bank conflicts too, but their per-site lane offsets push this
+// 256-VGPR kernel into spills or, recomputed per group, into +7 % VALU -- 4.27-4.50 vs 4.06-4.08 ms per call at the
+// level-0 size (profiles/r3_lds_layout_ab.txt); its limiter is VALU issue, not LDS
+constexpr int TWH_PLD = 68;  // fp32 row stride of a wave's partial dxn rows (written over its own slices)
 
 static size_t twh_smem(int F, int NV) {
   (void)F;
   const int R = NV * 16;
-  return (size_t)16 * RS * 4 + (size_t)8 * TWH_PG * 2 * 256 * 2 + (size_t)2 * xt_elems(R) * 2 +
-         (size_t)8 * 4 * R * HS * 2 + 1024;  // + tail pad: masked k-slot gathers may read 4 rows past a slice
+  return (size_t)16 * RS * 4 + (size_t)8 * TWH_PG * 2 * 256 * 2 + (size_t)2 * R * TH_XLD * 2 +
+         (size_t)8 * 4 * R * HLD * 2 + 1024;  // + tail pad: masked k-slot gathers may read 4 rows past a slice
 }
 
 template <int NV>
@@ -1614,21 +1625,21 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
   constexpr int C = 64;
   using T = TW<C, NV>;
   constexpr int R = NV * 16;
-  static_assert(TH_PLD * 4 <= 4 * HS * 2, "partial dxn rows fit over the wave's slices");
+  static_assert(TWH_PLD * 4 <= 4 * HLD * 2, "partial dxn rows fit over the wave's slices");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int FF = F * F;
   float* rot = smem;                                 // [16][RS]
   float* trbuf = rot + 16 * RS;                      // [8 waves][TWH_PG][2][16][16] bf16 P / dS tiles
-  bf16* xt = reinterpret_cast<bf16*>(trbuf) + 8 * TWH_PG * 2 * 256;  // [R][64] xhat (bf16, region tile, xt_rs)
-  bf16* dyt = xt + xt_elems(R);                      // [R][64] dy
-  bf16* slices = dyt + xt_elems(R);                  // 8 x [q|k|v|dO][R][HS] (hs_off layout)
+  bf16* xt = reinterpret_cast<bf16*>(trbuf) + 8 * TWH_PG * 2 * 256;  // [R][TH_XLD] xhat (bf16)
+  bf16* dyt = xt + R * TH_XLD;                       // [R][TH_XLD] dy
+  bf16* slices = dyt + R * TH_XLD;                   // 8 x [q|k|v|dO][R][HLD]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const int h = wid;
-  bf16* sq = slices + wid * 4 * R * HS;
-  bf16* sk = sq + R * HS;
-  bf16* sv = sk + R * HS;
-  bf16* sdo = sv + R * HS;
+  bf16* sq = slices + wid * 4 * R * HLD;
+  bf16* sk = sq + R * HLD;
+  bf16* sv = sk + R * HLD;
+  bf16* sdo = sv + R * HLD;
   for (int e = tid; e < F * 32; e += 512) rot[(e >> 5) * RS + (e & 31)] = rotg[e];
   // this wave's (head's) bias entries, log2 units: transposed (i = lr, j = 4g + r) and row-major (i = 4g + r, j = lr)
   float bt[4], brm[4];
@@ -1642,22 +1653,22 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
     brm[r] = ok ? b1 * LOG2E : 0.f;
   }
 
-  const int F4 = pad4(F), VW = T::PW * F4;
+  const int VW = T::PW * F;
   const int npg = (HW + T::PW - 1) / T::PW;
   const int ngroups = B * npg;
   // LN / LN-backward role of this thread: voxel vv of the group, channels 8cc..8cc+7
   const int vv = tid >> 3, cc = tid & 7;
   int fr[NV];
 #pragma unroll
-  for (int vt = 0; vt < NV; ++vt) fr[vt] = (vt * 16 + lr) % F4 < F ? (vt * 16 + lr) % F4 : 0;
+  for (int vt = 0; vt < NV; ++vt) fr[vt] = (vt * 16 + lr) % F;
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
 
   // the voxel row of (group gg, voxel v) or -1
   auto vrow = [&](int gg, int v) -> int64_t {
     const int b = gg / npg, pg = gg - b * npg;
     if (v >= VW) return -1;
-    const int pp = v / F4, f = v - pp * F4, p = pg * T::PW + pp;
-    if (f >= F || p >= HW) return -1;
+    const int pp = v / F, f = v - pp * F, p = pg * T::PW + pp;
+    if (p >= HW) return -1;
     return ((int64_t)b * F + f) * HW + p;
   };
   // prefetch registers: x, dy chunk and (mean, rstd) of this thread's voxel in the next group
@@ -1686,8 +1697,6 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
   TW_ST_DECL
   for (int gg = blockIdx.x; gg < ngroups; gg += gridDim.x) {
     const int b = gg / npg, p0 = (gg - b * npg) * T::PW;
-    // lane-derived LDS offsets recomputed per group from an opaque lane copy (not hoisted: register-bound kernel)
-    const int lane = opaque_v(threadIdx.x & 63), lr = lane & 15, lg = lane >> 4;
     // ---- LN of the group (this thread's voxel chunk) from the prefetch registers
     float rstd_cur = 0.f;
     if (vv < R) {
@@ -1698,8 +1707,8 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
         xh[e] = (bf16)(ok ? ((float)xpf[e] - mpf) * rpf : 0.f);
         dv[e] = ok ? dpf[e] : (bf16)0.f;
       }
-      *reinterpret_cast<bf16x8*>(xt + rg_off<1>(vv, cc * 8, xt_rs(R))) = xh;
-      *reinterpret_cast<bf16x8*>(dyt + rg_off<1>(vv, cc * 8, xt_rs(R))) = dv;
+      *reinterpret_cast<bf16x8*>(xt + vv * TH_XLD + cc * 8) = xh;
+      *reinterpret_cast<bf16x8*>(dyt + vv * TH_XLD + cc * 8) = dv;
       rstd_cur = ok ? rpf : 0.f;
     }
     const bool ok_cur = okpf;
@@ -1741,7 +1750,7 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
 #pragma unroll
       for (int vt = 0; vt < NV; ++vt)
 #pragma unroll
-        for (int ks = 0; ks < T::KS; ++ks) xf[vt][ks] = ld16(xt + rg_off<1>(vt * 16 + lr, ks * 32 + lg * 8, xt_rs(R)));
+        for (int ks = 0; ks < T::KS; ++ks) xf[vt][ks] = ld16(xt + (vt * 16 + lr) * TH_XLD + ks * 32 + lg * 8);
 #if TWH_QKV_PIPE
 #pragma unroll
       for (int c2 = 0; c2 < 6; c2 += 2) {
@@ -1772,12 +1781,12 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
               for (int r = 0; r < 4; ++r) o4[r] *= scale;
             }
             if (kind < 2) rope4(o4, rot, fr[vt], d0, 1.f);
-            store4(dst + hs_off<R>(vt * 16 + lr, d0), o4);
+            store4(dst + (vt * 16 + lr) * HLD + d0, o4);
           }
         }
       }
 #else
-      tw_qkv<C, NV, TWH_FULL != 0>(wq_g, xf, h, fr, scale, rot, sq, sk, sv, lr, lg);
+#error "TWH_QKV_PIPE=0: tw_qkv writes the region layout, twh_bwd reads 80-B rows"
 #endif
     }
     TW_ST(1)
@@ -1798,10 +1807,10 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
         f32x4 acc = z4;
 #pragma unroll
         for (int ks = 0; ks < T::KS; ++ks)
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], ld16(dyt + rg_off<1>(vt * 16 + lr, ks * 32 + lg * 8, xt_rs(R))),
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], ld16(dyt + (vt * 16 + lr) * TH_XLD + ks * 32 + lg * 8),
                                                         acc, 0, 0, 0);
         float o4[4] = {acc[0], acc[1], acc[2], acc[3]};
-        store4(sdo + hs_off<R>(vt * 16 + lr, dt * 16 + lg * 4), o4);
+        store4(sdo + (vt * 16 + lr) * HLD + dt * 16 + lg * 4, o4);
       }
     }
     wave_lds_sync();
@@ -1815,12 +1824,12 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
       f32x4 st[PG], dpt[PG];
 #pragma unroll
       for (int u = 0; u < PG; ++u) {
-        const int rb = (pp0 + u) * F4;
-        const int rr = rg_at(rb, hs_off<R>(lr < F ? lr : 0, lg * 8));
-        const bf16x8 kr = ld16(sk + rr);
-        const bf16x8 qr = ld16(sq + rr);
-        const bf16x8 vr = ld16(sv + rr);
-        const bf16x8 dor = ld16(sdo + rr);
+        const int rb = (pp0 + u) * F;
+        const int rr = rb + (lr < F ? lr : 0);
+        const bf16x8 kr = ld16(sk + rr * HLD + lg * 8);
+        const bf16x8 qr = ld16(sq + rr * HLD + lg * 8);
+        const bf16x8 vr = ld16(sv + rr * HLD + lg * 8);
+        const bf16x8 dor = ld16(sdo + rr * HLD + lg * 8);
         st[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kr, qr, z4, 0, 0, 0);    // S^T[j][i]
         dpt[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vr, dor, z4, 0, 0, 0);  // dP^T[j][i]
       }
@@ -1850,35 +1859,35 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
           p4[r] = (bf16)pt[r];
         }
         // tile[i = lr][j = 4g .. 4g+3]
-        *reinterpret_cast<bf16x4*>(trt + (u * 2 + 0) * 256 + trt_off(lr, lg * 4)) = p4;
-        *reinterpret_cast<bf16x4*>(trt + (u * 2 + 1) * 256 + trt_off(lr, lg * 4)) = d4;
+        *reinterpret_cast<bf16x4*>(trt + (u * 2 + 0) * 256 + lr * 16 + lg * 4) = p4;
+        *reinterpret_cast<bf16x4*>(trt + (u * 2 + 1) * 256 + lr * 16 + lg * 4) = d4;
       }
       f32x4 dqt[PG][2];
 #pragma unroll
       for (int u = 0; u < PG; ++u)
 #pragma unroll
         for (int half = 0; half < 2; ++half)
-          dqt[u][half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kslot_gather<R>(sk, (pp0 + u) * F4, half * 16, F, lane),
+          dqt[u][half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kslot_gather_hld(sk, (pp0 + u) * F, half * 16, F, lane),
                                                                  dst_b[u], z4, 0, 0, 0);  // dQ'^T[d][i]
       wave_lds_sync();  // P / dS tiles visible
       f32x4 dkt[PG][2], dvt[PG][2];
 #pragma unroll
       for (int u = 0; u < PG; ++u) {
-        const bf16x8 p_b = kslot_gather_trt(trt + (u * 2 + 0) * 256, F, lane);   // P[i = 4g+e][j = lr]
-        const bf16x8 ds_b = kslot_gather_trt(trt + (u * 2 + 1) * 256, F, lane);  // dS[i = 4g+e][j = lr]
+        const bf16x8 p_b = kslot_gather_ld(trt + (u * 2 + 0) * 256, 16, 0, 0, F, lane);   // P[i = 4g+e][j = lr]
+        const bf16x8 ds_b = kslot_gather_ld(trt + (u * 2 + 1) * 256, 16, 0, 0, F, lane);  // dS[i = 4g+e][j = lr]
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
-          const int rb = (pp0 + u) * F4;
-          dkt[u][half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kslot_gather<R>(sq, rb, half * 16, F, lane), ds_b, z4,
+          const int rb = (pp0 + u) * F;
+          dkt[u][half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kslot_gather_hld(sq, rb, half * 16, F, lane), ds_b, z4,
                                                                  0, 0, 0);  // dK'^T[d][j]
-          dvt[u][half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kslot_gather<R>(sdo, rb, half * 16, F, lane), p_b, z4,
+          dvt[u][half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kslot_gather_hld(sdo, rb, half * 16, F, lane), p_b, z4,
                                                                  0, 0, 0);  // dV^T[d][j]
         }
       }
       wave_lds_sync();  // all reads of these pixels' rows (and the tiles) done before they are overwritten
 #pragma unroll
       for (int u = 0; u < PG; ++u) {
-        const int rb = (pp0 + u) * F4;
+        const int rb = (pp0 + u) * F;
         if (lr < F && p0 + pp0 + u < HW) {
 #pragma unroll
           for (int half = 0; half < 2; ++half) {
@@ -1890,9 +1899,9 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
             rope4(k4, rot, lr, d0, -1.f);
 #pragma unroll
             for (int r = 0; r < 4; ++r) q4[r] *= scale;
-            store4(sq + rg_at(rb, hs_off<R>(lr, d0)), q4);
-            store4(sk + rg_at(rb, hs_off<R>(lr, d0)), k4);
-            store4(sv + rg_at(rb, hs_off<R>(lr, d0)), v4);
+            store4(sq + (rb + lr) * HLD + d0, q4);
+            store4(sk + (rb + lr) * HLD + d0, k4);
+            store4(sv + (rb + lr) * HLD + d0, v4);
           }
         }
       }
@@ -1919,11 +1928,11 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
     for (int kk = 0; kk < NV; ++kk) {
       s16x4 bx[4];
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) bx[nt] = tr4_rg<1>(xt, kk * 16, nt * 16, xt_rs(R), lane);
+      for (int nt = 0; nt < 4; ++nt) bx[nt] = tr4(xt, TH_XLD, kk * 16, nt * 16, lane);
 #pragma unroll
       for (int m = 0; m < 6; ++m) {
         const bf16* src = (m >> 1) == 0 ? sq : ((m >> 1) == 1 ? sk : sv);
-        const s16x4 a = tr4_hs<R>(src, kk * 16, (m & 1) * 16, lane);
+        const s16x4 a = tr4(src, HLD, kk * 16, (m & 1) * 16, lane);
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt)
           dwacc[m][nt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, bx[nt], dwacc[m][nt], 0, 0, 0);
@@ -1951,7 +1960,7 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
 #endif
 #pragma unroll
         for (int vt = 0; vt < NV; ++vt)
-          dxacc[ct][vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ld16(src + hs_off<R>(vt * 16 + lr, lg * 8)),
+          dxacc[ct][vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ld16(src + (vt * 16 + lr) * HLD + lg * 8),
                                                                   dxacc[ct][vt], 0, 0, 0);
       }
     }
@@ -1962,7 +1971,7 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
       for (int ct = 0; ct < T::CT; ++ct)
 #pragma unroll
         for (int vt = 0; vt < NV; ++vt)
-          *reinterpret_cast<f32x4*>(part + pl_off(vt * 16 + lr, ct * 16 + lg * 4)) = dxacc[ct][vt];
+          *reinterpret_cast<f32x4*>(part + (vt * 16 + lr) * TWH_PLD + ct * 16 + lg * 4) = dxacc[ct][vt];
     }
     TW_ST(5)
     __syncthreads();  // (B) every head's partial written
@@ -1975,14 +1984,14 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
       for (int e = 0; e < 8; ++e) g[e] = 0.f;
 #pragma unroll
       for (int w = 0; w < 8; ++w) {
-        const float* pw = reinterpret_cast<const float*>(slices + w * 4 * R * HS);
-        const f32x4 a0 = *reinterpret_cast<const f32x4*>(pw + pl_off(v, cc * 8));
-        const f32x4 a1 = *reinterpret_cast<const f32x4*>(pw + pl_off(v, cc * 8 + 4));
+        const float* pw = reinterpret_cast<const float*>(slices + w * 4 * R * HLD) + v * TWH_PLD + cc * 8;
+        const f32x4 a0 = *reinterpret_cast<const f32x4*>(pw);
+        const f32x4 a1 = *reinterpret_cast<const f32x4*>(pw + 4);
 #pragma unroll
         for (int e = 0; e < 4; ++e) { g[e] += a0[e]; g[4 + e] += a1[e]; }
       }
-      const bf16x8 xh = *reinterpret_cast<const bf16x8*>(xt + rg_off<1>(v, cc * 8, xt_rs(R)));
-      const bf16x8 dv = *reinterpret_cast<const bf16x8*>(dyt + rg_off<1>(v, cc * 8, xt_rs(R)));
+      const bf16x8 xh = *reinterpret_cast<const bf16x8*>(xt + v * TH_XLD + cc * 8);
+      const bf16x8 dv = *reinterpret_cast<const bf16x8*>(dyt + v * TH_XLD + cc * 8);
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int e = 0; e < 8; ++e) { s1 += g[e]; s2 = fmaf(g[e], (float)xh[e], s2); }

@@ -247,7 +247,9 @@ def test_dp_step_equals_full_batch_step(dev, tmp_path, dtype):
     # modes: the bf16 path rounds the same per-sample activations, only the batch sums regroup) can only flip the
     # sign where |g| is at noise level, so compare element-wise against the step scale
     assert (moved > 0.05 * 1e-3).double().mean().item() < 1e-3
-    assert rel(p0, full) < 1e-5
+    # whole-vector gate: fp32 1e-5; bf16 2e-4 (measured 8.3e-5: the bf16 gradients' noise floor is higher, and the
+    # few entries whose gradient sits at it move by up to +-lr in either run -- the element gate above bounds them)
+    assert rel(p0, full) < (1e-5 if dtype == torch.float32 else 2e-4)
 
 
 def test_bench_multirank_gloo_rehearsal():
