@@ -225,18 +225,12 @@ BF16_GRAD_MEDIAN_GATE = 4e-2
 BF16_GRAD_COS_GATE = 0.99
 
 
-@pytest.mark.parametrize("mults", [(1, 2, 4), (1, 2, 4, 8)])
-def test_whole_net_bf16_forward_backward(dev, mults):
-    """bf16 training path at a level-0 width that is a multiple of 32 (64 x 96, F = 12): the fused
-    temporal / spatial attention blocks (C = 64, 128), conv3x3p at level 0, halo convs, wgrad_wide and
-    gemm1x1 — eps_pred, loss and every parameter gradient vs the fp32 oracle (video_net.py:766-871,
-    model.py:203-208)."""
+def _bf16_fwd_bwd(dev, mults, B, Fr, H, W, seed, tag):
+    """eps_pred, loss and every parameter gradient of the bf16 training path vs the fp32 oracle; returns the rows"""
     ref, prod = _pair(mults)
     prod = prod.to(dev)
     prod.compute_dtype = BF
-    B, Fr, H, W = 1, 12, 64, 96
-    assert K.conv_fwd_variant(BF, B * Fr, H, W, 64, 0, H, W, 64, 64, 3, 3, 1, 1, 1) == "conv3x3p_kernel<32,7,true>"
-    x0, cond, t, noise = _inputs(B, Fr, H, W, seed=31)
+    x0, cond, t, noise = _inputs(B, Fr, H, W, seed=seed)
     dref, dprod = R.Diffusion(ref), Diffusion(prod).to(dev)
     # eps_pred on the same x_t
     xt, _ = dref.q_sample(x0, t, noise)
@@ -261,7 +255,7 @@ def test_whole_net_bf16_forward_backward(dev, mults):
     rows.sort(reverse=True)
     rels = sorted(r[0] for r in rows)
     median = rels[len(rels) // 2]
-    print(f"bf16 mults={mults}: eps_pred rel {e_eps:.3e}, loss rel {e_loss:.3e}, grads: median rel {median:.3e}, "
+    print(f"bf16 {tag}: eps_pred rel {e_eps:.3e}, loss rel {e_loss:.3e}, grads: median rel {median:.3e}, "
           f"worst rel {rows[0][0]:.3e} ({rows[0][2]}), worst cos {min(r[1] for r in rows):.5f}")
     for r in rows[:8]:
         print(f"   {r[0]:.3e}  cos {r[1]:.5f}  {r[2]}")
@@ -269,6 +263,17 @@ def test_whole_net_bf16_forward_backward(dev, mults):
     assert median < BF16_GRAD_MEDIAN_GATE
     for e, c, name in rows:
         assert e < BF16_GRAD_REL_GATE and c > BF16_GRAD_COS_GATE, (name, e, c)
+    return rows
+
+
+@pytest.mark.parametrize("mults", [(1, 2, 4), (1, 2, 4, 8)])
+def test_whole_net_bf16_forward_backward(dev, mults):
+    """bf16 training path at a level-0 width that is a multiple of 32 (64 x 96, F = 12): the fused
+    temporal / spatial attention blocks (C = 64, 128), conv3x3p at level 0, halo convs, wgrad_wide and
+    gemm1x1 — eps_pred, loss and every parameter gradient vs the fp32 oracle (video_net.py:766-871,
+    model.py:203-208)."""
+    assert K.conv_fwd_variant(BF, 12, 64, 96, 64, 0, 64, 96, 64, 64, 3, 3, 1, 1, 1) == "conv3x3p_kernel<32,7,true>"
+    _bf16_fwd_bwd(dev, mults, 1, 12, 64, 96, 31, f"mults={mults}")
 
 
 # ------------------------------------------------------------------ full-size configs 2 and 3 (D2)
@@ -379,3 +384,12 @@ def test_more_blocks_decadal_window_bf16_forward(dev):
     e = rel(y, y_ref)
     print(f"more_blocks F=120 bf16 fwd rel {e:.3e}")
     assert e < BF16_FWD_GATE
+
+
+def test_more_blocks_decadal_window_bf16_forward_backward(dev):
+    """config 4's training path in bf16 (more_blocks at F = 120, 32 x 64 grid: conv3x3p at level 0, the unfused
+    long-window temporal path -- gemm1x1 projections + the MFMA flash cores tflash_fwd / tflash_bwd_q / kv at
+    every level, the fused SLA blocks): eps_pred, loss and every parameter gradient vs the fp32 oracle, same gates
+    as the F = 12 whole-net test (video_net.py:403-454 at F = 120)"""
+    assert K.conv_fwd_variant(BF, 120, 32, 64, 64, 0, 32, 64, 64, 64, 3, 3, 1, 1, 1) == "conv3x3p_kernel<32,7,true>"
+    _bf16_fwd_bwd(dev, (1, 2, 4, 8), 1, 120, 32, 64, 53, "more_blocks F=120")

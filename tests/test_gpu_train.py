@@ -246,10 +246,13 @@ def test_dp_step_equals_full_batch_step(dev, tmp_path, dtype):
     # Adam moves each element ~lr*sign(g) in the first steps; reduction-order noise (fp32 accumulators in both
     # modes: the bf16 path rounds the same per-sample activations, only the batch sums regroup) can only flip the
     # sign where |g| is at noise level, so compare element-wise against the step scale
-    assert (moved > 0.05 * 1e-3).double().mean().item() < 1e-3
-    # whole-vector gate: fp32 1e-5; bf16 2e-4 (measured 8.3e-5: the bf16 gradients' noise floor is higher, and the
-    # few entries whose gradient sits at it move by up to +-lr in either run -- the element gate above bounds them)
-    assert rel(p0, full) < (1e-5 if dtype == torch.float32 else 2e-4)
+    # fp32: < 0.1 % of the entries off by > 0.05 lr, whole vector rel < 1e-5.  bf16: the gradients' noise floor is
+    # higher (every stored activation is bf16-rounded, so a regrouped batch sum flips downstream roundings), and the
+    # entries whose gradient sits at it move by up to +-lr in either run: measured 0.08-0.11 % of the entries and
+    # rel 0.8-1.1e-4 over two runs -> gates 0.5 % and 3e-4 (a wrong reduction moves O(1) of the entries)
+    frac_gate, rel_gate = (1e-3, 1e-5) if dtype == torch.float32 else (5e-3, 3e-4)
+    assert (moved > 0.05 * 1e-3).double().mean().item() < frac_gate
+    assert rel(p0, full) < rel_gate
 
 
 def test_bench_multirank_gloo_rehearsal():
