@@ -1111,6 +1111,10 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const int h = wid;
+#ifndef SLAH_PRIO
+#define SLAH_PRIO 0
+#endif
+  if (SLAH_PRIO && wid >= 4) __builtin_amdgcn_s_setprio(1);  // second-dispatched half (MI355X_MICROARCH §Two waves per SIMD, item 4)
   bf16* sl = slices + wid * R * SH_SLD;
   const int npg = (HW + R - 1) / R;
   const int ngroups = Nf * npg;

@@ -703,6 +703,20 @@ __device__ __forceinline__ bf16x8 kslot_gather(const bf16* tile, int rb, int c0,
   return r;
 }
 
+// kslot_gather<R> without the per-element frame mask (see kslot_raw): for operands whose partner is zero at every
+// k-slot of a frame >= F
+__device__ __forceinline__ bf16x8 kslot_raw(const s16x4 v) {
+  bf16x8 r = zero8();
+#pragma unroll
+  for (int e = 0; e < 4; ++e) r[e] = __builtin_bit_cast(bf16, (short)v[e]);
+  return r;
+}
+template <int R>
+__device__ __forceinline__ bf16x8 kslot_gather_raw(const bf16* tile, int rb, int c0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  return kslot_raw(__builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tile + rg_at(rb, hs_off<R>(4 * g + q, c0 + 4 * p)))));
+}
+
 // hardware-transpose read of a head slice: lane (g, i) <- tile[r0 + 4g + e][c0 + i]
 template <int R>
 __device__ __forceinline__ s16x4 tr4_hs(const bf16* tile, int r0, int c0, int lane) {
@@ -917,6 +931,8 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
   bf16* sv = sk + R * HS;
   for (int e = tid; e < NH * F * F; e += 256) sb[e] = bias[e] * LOG2E;
   for (int e = tid; e < F * 32; e += 256) rot[(e >> 5) * RS + (e & 31)] = rotg[e];
+  // tail pad past the last wave's slices: its last pixel's unmasked V gathers read up to 16 - F4 <= 12 rows into it
+  for (int e = tid; e < 256; e += 256) reinterpret_cast<float*>(reinterpret_cast<bf16*>(rot + 16 * RS) + 4 * 3 * R * HS)[e] = 0.f;
   __syncthreads();
   const int p0 = (blockIdx.x * 4 + wid) * T::PW;
   if (p0 >= HW) return;
@@ -983,7 +999,7 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
 #pragma unroll
       for (int u = 0; u < PG; ++u)
 #pragma unroll
-        for (int half = 0; half < 2; ++half) va[u][half] = kslot_gather<R>(sv, (pg + u) * F4, half * 16, F, lane);
+        for (int half = 0; half < 2; ++half) va[u][half] = kslot_gather_raw<R>(sv, (pg + u) * F4, half * 16, lane);  // P^T is 0 at keys >= F
       bf16x8 pb[PG];
 #pragma unroll
       for (int u = 0; u < PG; ++u) {
@@ -1095,12 +1111,16 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
   bf16* sk = sq + R * HS;
   bf16* sv = sk + R * HS;
   bf16* sdo = sv + R * HS;
-  float* sld = reinterpret_cast<float*>(reinterpret_cast<bf16*>(rot + 16 * RS) + 4 * 4 * R * HS) + wid * 32;
+  // 16 zero rows past the last wave's slices (its last pixel's unmasked k-slot gathers read up to 12 rows into
+  // them), then Li / D
+  float* spad = reinterpret_cast<float*>(reinterpret_cast<bf16*>(rot + 16 * RS) + 4 * 4 * R * HS);
+  float* sld = spad + 8 * HS + wid * 32;
   for (int e = tid; e < NH * FF; e += 256) sb[e] = bias[e] * LOG2E;
   for (int e = tid; e < 4 * NH * FF; e += 256) sdb0[e] = 0.f;
   for (int e = tid; e < 4 * C; e += 256) sg0[e] = 0.f;
   for (int e = tid; e < C; e += 256) sgm[e] = gamma[e];
   for (int e = tid; e < F * 32; e += 256) rot[(e >> 5) * RS + (e & 31)] = rotg[e];
+  for (int e = tid; e < 8 * HS; e += 256) spad[e] = 0.f;
   __syncthreads();
 
   const int npg = (HW + T::PW - 1) / T::PW;
@@ -1244,8 +1264,8 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
         f32x4 dqt[2];
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
-          const bf16x8 kg = kslot_gather<R>(sk, rb, half * 16, F, lane);
-          const bf16x8 vg = kslot_gather<R>(sv, rb, half * 16, F, lane);
+          const bf16x8 kg = kslot_gather_raw<R>(sk, rb, half * 16, lane);  // dS^T / P^T are 0 at frames >= F
+          const bf16x8 vg = kslot_gather_raw<R>(sv, rb, half * 16, lane);
           dqt[half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kg, dst_b, z4, 0, 0, 0);  // dQ'^T[d][i]
           if (!o_out) continue;  // O written by the forward (cesm_tblock_fwd o)
           const f32x4 ot = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vg, pt_b, z4, 0, 0, 0);  // O^T[d][i]
@@ -1275,8 +1295,8 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
         f32x4 dkt[2], dvt[2];
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
-          const bf16x8 qg = kslot_gather<R>(sq, rb, half * 16, F, lane);
-          const bf16x8 dog = kslot_gather<R>(sdo, rb, half * 16, F, lane);
+          const bf16x8 qg = kslot_gather_raw<R>(sq, rb, half * 16, lane);
+          const bf16x8 dog = kslot_gather_raw<R>(sdo, rb, half * 16, lane);
           dkt[half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qg, ds_b, z4, 0, 0, 0);   // dK'^T[d][j]
           dvt[half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dog, p_b, z4, 0, 0, 0);   // dV^T[d][j]
         }
@@ -1452,12 +1472,12 @@ __global__ void tb_sum_rows_kernel(const float* __restrict__ part, float* __rest
 template <int C>
 static size_t tw_fwd_smem(int F) {  // NOLINT
   const int R = ((TW<C>::PW * F + 15) / 16) * 16;
-  return (size_t)(((NH * F * F + 3) & ~3) + 16 * RS) * 4 + (size_t)4 * 3 * R * HS * 2 + 512;  // + tail pad: k-slot gathers may read 4 rows past the last slice
+  return (size_t)(((NH * F * F + 3) & ~3) + 16 * RS) * 4 + (size_t)4 * 3 * R * HS * 2 + 1024;  // + 16-row tail pad: k-slot gathers read up to 12 rows past the last slice
 }
 template <int C>
 static size_t tw_bwd_smem(int F) {
   const int R = ((TW<C>::PW * F + 15) / 16) * 16;
-  return (size_t)(5 * NH * F * F + 5 * C + 16 * RS) * 4 + (size_t)4 * 4 * R * HS * 2 + 4 * 32 * 4;
+  return (size_t)(5 * NH * F * F + 5 * C + 16 * RS) * 4 + (size_t)4 * 4 * R * HS * 2 + 8 * HS * 4 + 4 * 32 * 4;
 }
 template <typename K>
 static void allow_smem(K kernel, size_t bytes) {
@@ -1576,6 +1596,18 @@ __device__ __forceinline__ bf16x8 kslot_gather_ld(const bf16* tile, int ld, int 
     if (4 * g + e < F) r[e] = __builtin_bit_cast(bf16, (short)v[e]);
   return r;
 }
+// Unmasked k-slot gathers (round 3): where the other MFMA operand is exactly zero at every k-slot of a frame >= F
+// (P, dS and their transposes are 0 there), the rows read past the pixel's F frames -- the next pixel's finite
+// rows, or the zero-initialised tail pad past the last slice -- contribute 0, so the 4 per-element selects
+// (v_cndmask + repacking, ~15 % of twh_bwd's VALU) are not needed
+__device__ __forceinline__ bf16x8 kslot_gather_hld_raw(const bf16* tile, int rb, int c0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  return kslot_raw(__builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tile + (rb + 4 * g + q) * HLD + c0 + 4 * p)));
+}
+__device__ __forceinline__ bf16x8 kslot_gather_ld_raw(const bf16* tile, int ld, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  return kslot_raw(__builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tile + (4 * g + q) * ld + 4 * p)));
+}
 
 #ifndef TWH_FULL
 // measured at B = 8 (tools/tblock_time.py): PG 2 / FULL 0 / EARLY_WT 0 4.47 ms (no spills); PG 2 with both on
@@ -1608,11 +1640,15 @@ constexpr int TH_NVMAX = 3;  // voxel tiles per group (4*F <= 48): the 8 slices 
 // level-0 size (profiles/r3_lds_layout_ab.txt); its limiter is VALU issue, not LDS
 constexpr int TWH_PLD = 68;  // fp32 row stride of a wave's partial dxn rows (written over its own slices)
 
+// per-wave slice region: q | k | v | dO [R][HLD] + a 16-row zero pad: the unmasked k-slot gathers of the wave's last
+// pixel read up to (PW-1)F + 16 - R <= 12 rows past dO (F = 4), which must be finite (the next wave's region may
+// still hold fp32 partial rows)
+#define TWH_WSTRIDE(R) (4 * (R) * HLD + 16 * HLD)
 static size_t twh_smem(int F, int NV) {
   (void)F;
   const int R = NV * 16;
   return (size_t)16 * RS * 4 + (size_t)8 * TWH_PG * 2 * 256 * 2 + (size_t)2 * R * TH_XLD * 2 +
-         (size_t)8 * 4 * R * HLD * 2 + 1024;  // + tail pad: masked k-slot gathers may read 4 rows past a slice
+         (size_t)8 * TWH_WSTRIDE(R) * 2;
 }
 
 template <int NV>
@@ -1636,11 +1672,17 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const int h = wid;
-  bf16* sq = slices + wid * 4 * R * HLD;
+#ifndef TWH_PRIO
+#define TWH_PRIO 0
+#endif
+  if (TWH_PRIO && wid >= 4) __builtin_amdgcn_s_setprio(1);  // second-dispatched half (MI355X_MICROARCH §Two waves per SIMD, item 4)
+  bf16* sq = slices + wid * TWH_WSTRIDE(R);
   bf16* sk = sq + R * HLD;
   bf16* sv = sk + R * HLD;
   bf16* sdo = sv + R * HLD;
   for (int e = tid; e < F * 32; e += 512) rot[(e >> 5) * RS + (e & 31)] = rotg[e];
+  // the wave's 16-row pad past dO (never written afterwards: the partial rows fit over the slices)
+  for (int e = lane; e < 8 * HLD; e += 64) reinterpret_cast<float*>(sq + 4 * R * HLD)[e] = 0.f;
   // this wave's (head's) bias entries, log2 units: transposed (i = lr, j = 4g + r) and row-major (i = 4g + r, j = lr)
   float bt[4], brm[4];
 #pragma unroll
@@ -1867,20 +1909,20 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
       for (int u = 0; u < PG; ++u)
 #pragma unroll
         for (int half = 0; half < 2; ++half)
-          dqt[u][half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kslot_gather_hld(sk, (pp0 + u) * F, half * 16, F, lane),
+          dqt[u][half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kslot_gather_hld_raw(sk, (pp0 + u) * F, half * 16, lane),
                                                                  dst_b[u], z4, 0, 0, 0);  // dQ'^T[d][i]
       wave_lds_sync();  // P / dS tiles visible
       f32x4 dkt[PG][2], dvt[PG][2];
 #pragma unroll
       for (int u = 0; u < PG; ++u) {
-        const bf16x8 p_b = kslot_gather_ld(trt + (u * 2 + 0) * 256, 16, 0, 0, F, lane);   // P[i = 4g+e][j = lr]
-        const bf16x8 ds_b = kslot_gather_ld(trt + (u * 2 + 1) * 256, 16, 0, 0, F, lane);  // dS[i = 4g+e][j = lr]
+        const bf16x8 p_b = kslot_gather_ld_raw(trt + (u * 2 + 0) * 256, 16, lane);   // P[i = 4g+e][j = lr]
+        const bf16x8 ds_b = kslot_gather_ld_raw(trt + (u * 2 + 1) * 256, 16, lane);  // dS[i = 4g+e][j = lr]
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
           const int rb = (pp0 + u) * F;
-          dkt[u][half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kslot_gather_hld(sq, rb, half * 16, F, lane), ds_b, z4,
+          dkt[u][half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kslot_gather_hld_raw(sq, rb, half * 16, lane), ds_b, z4,
                                                                  0, 0, 0);  // dK'^T[d][j]
-          dvt[u][half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kslot_gather_hld(sdo, rb, half * 16, F, lane), p_b, z4,
+          dvt[u][half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kslot_gather_hld_raw(sdo, rb, half * 16, lane), p_b, z4,
                                                                  0, 0, 0);  // dV^T[d][j]
         }
       }
@@ -1984,7 +2026,7 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
       for (int e = 0; e < 8; ++e) g[e] = 0.f;
 #pragma unroll
       for (int w = 0; w < 8; ++w) {
-        const float* pw = reinterpret_cast<const float*>(slices + w * 4 * R * HLD) + v * TWH_PLD + cc * 8;
+        const float* pw = reinterpret_cast<const float*>(slices + w * TWH_WSTRIDE(R)) + v * TWH_PLD + cc * 8;
         const f32x4 a0 = *reinterpret_cast<const f32x4*>(pw);
         const f32x4 a1 = *reinterpret_cast<const f32x4*>(pw + 4);
 #pragma unroll
