@@ -974,7 +974,9 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int j = lg * 4 + r;
-      bt[r] = (j < F && lr < F) ? sb[(h * F + lr) * F + j] : -INFINITY;
+      // query lanes lr >= F take row 0's biases: their max is finite, so no lane needs a -inf guard below (their
+      // O columns and lse are never stored)
+      bt[r] = j < F ? sb[(h * F + (lr < F ? lr : 0)) * F + j] : -INFINITY;
     }
     wave_lds_sync();
     // attention core, base-2 softmax; O overwrites the pixel's own q rows.  Pixels go in groups of PG
@@ -1015,12 +1017,12 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
         float pr[4], l = 0.f;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          pr[r] = sc[r] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(sc[r] - m);
+          pr[r] = __builtin_amdgcn_exp2f(sc[r] - m);  // exp2(-inf) = 0 past F (m is finite: key 0 < F)
           l += pr[r];
         }
         l = grp4_sum(l);
         if (lse && lg == 0 && lr < F && p < HW) lse[(((int64_t)b * NH + h) * HW + p) * F + lr] = m + log2f(l);  // log2 units
-        const float inv = lr < F ? __builtin_amdgcn_rcpf(l) : 0.f;
+        const float inv = __builtin_amdgcn_rcpf(l);
         pb[u] = zero8();
 #pragma unroll
         for (int r = 0; r < 4; ++r) pb[u][r] = (bf16)(pr[r] * inv);
