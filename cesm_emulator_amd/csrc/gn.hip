@@ -32,13 +32,19 @@ template <typename T> __device__ __forceinline__ void gl8(const T* p, float* v) 
 template <typename T> __device__ __forceinline__ void gs8(T* p, const float* v) { store8(p, v); }
 #endif
 
-// row chunks per sample for the reduction kernels: >= ~8 row-iterations per thread, <= 256 chunks
-// (small levels still get ~1000 blocks in total)
-static int gn_nchunk(int64_t rows_b, int C) {
+// row chunks per sample for the reduction kernels: >= ~8 row-iterations per thread, at most
+// max(256, 1024 / B) chunks, so a B = 1 long window (F = 120: ~1M rows per sample) still launches 1024
+// blocks = 4 per CU instead of 256 (measured: the 1-block-per-CU grid ran the bwd reduction at ~40 % of
+// the apply kernel's bandwidth).  Workspaces hold max(B * 256, 1024) chunk partials (gn_ws_chunks).
+#ifndef GN_SMALLB_CHUNKS
+#define GN_SMALLB_CHUNKS 1024  // A/B knob (256 = the round-2 fixed cap)
+#endif
+static int gn_nchunk(int64_t rows_b, int C, int B) {
   const int rl = 256 / (C / 8);
+  const int cap = B >= GN_SMALLB_CHUNKS / 256 ? 256 : GN_SMALLB_CHUNKS / B;
   int64_t n = rows_b / (rl * 8);
   if (n < 1) n = 1;
-  if (n > 256) n = 256;
+  if (n > cap) n = cap;
   return (int)n;
 }
 
@@ -412,11 +418,11 @@ static int gn_apply_chunks(int64_t rows_b, int C) {
 
 extern "C" {
 
-// y: [B][rows_b][C] (rows_b = F*H*W); writes stats[B][G][2] = (mean, rstd); ws >= B*256*G*2 doubles
+// y: [B][rows_b][C] (rows_b = F*H*W); writes stats[B][G][2] = (mean, rstd); ws >= max(B*256, 1024)*G*2 doubles
 int cesm_gn_stats(int dtype, const void* y, float* stats, double* ws, int B, int64_t rows_b, int C, int G, float eps,
                   hipStream_t stream) {
   if (C % 8 || C / 8 > 256 || C % G || (C / G) % 8) return CESM_EINVAL;
-  const int nchunk = gn_nchunk(rows_b, C);
+  const int nchunk = gn_nchunk(rows_b, C, B);
   dim3 grid(nchunk, B);
   int rc = dispatch_dt(dtype, [&](auto* tp) {
     using T = std::remove_pointer_t<decltype(tp)>;
@@ -453,12 +459,12 @@ int cesm_gn_apply(int dtype, const void* y, const float* stats, const float* gam
 
 // Backward of out = silu(GN(y)*(1+scale)+shift) (+res).  Writes dy, dss [B][2C] (if non-null),
 // dgamma/dbeta and the producing conv's bias gradient dbias = sum dy (each nullable; accumulate flag).
-// ws: float workspace >= B*256*C*3 + B*C*3 + B*C*5 floats.
+// ws: float workspace >= max(B*256, 1024)*C*3 + B*C*3 + B*C*5 floats.
 int cesm_gn_bwd(int dtype, const void* dout, const void* y, const float* stats, const float* gamma,
                 const float* beta, const float* ss, void* dy, float* dss, float* dgamma, float* dbeta, float* dbias,
                 float* ws, int B, int64_t rows_b, int C, int G, int accumulate, hipStream_t stream) {
   if (C % 8 || C / 8 > 128 || C % G || C / G > 64 || 64 % (C / G) || G > 64) return CESM_EINVAL;
-  const int nchunk = gn_nchunk(rows_b, C);
+  const int nchunk = gn_nchunk(rows_b, C, B);
   float* part = ws;
   float* pb = part + (int64_t)B * nchunk * C * 3;
   float* coef = pb + (int64_t)B * C * 3;

@@ -1555,7 +1555,7 @@ int cesm_slaf_bwd_dw(const void* x, const void* dy, const float* gamma_one, cons
   }
   slab_combine_kernel<<<Nf * NH, 256, 0, stream>>>(part, nblk, ctx32, mz, G, (bf16*)adc, (bf16*)adcT);
   const size_t sm = slah_smem(3);
-  hipFuncSetAttribute((const void*)slah_dx_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+  (void)hipFuncSetAttribute((const void*)slah_dx_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
   slah_dx_kernel<3><<<nblk_dx, 512, sm, stream>>>((const bf16*)x, (const bf16*)dy, img_q, img_qt, img_ot, G,
                                                   (const bf16*)actT, (const bf16*)actx, (const bf16*)adc,
                                                   (const bf16*)adcT, (bf16*)dx, slab, Nf, HW, scale, eps);

@@ -1483,7 +1483,7 @@ static size_t tw_bwd_smem(int F) {
 }
 template <typename K>
 static void allow_smem(K kernel, size_t bytes) {
-  if (bytes > 65536) hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (bytes > 65536) (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
 template <int C, int NV, bool FOLD = false>

@@ -12,6 +12,9 @@
 // its gradient is accumulated by offset in registers (the offset of every element a lane holds is fixed by
 // the lane, the register index and the (query tile, key tile) pair) and reduced to buckets afterwards.
 // Backward = two kernels: dq (query tiles outer; D_i = dO_i . O_i; dbias) and dk / dv (key tiles outer).
+// Every kernel here is capped at 256 registers (>= 2 waves per SIMD): with a 512-register budget the compiler
+// selects the AGPR form of the MFMAs, and the score tiles -- consumed by VALU right away -- then cost 4
+// v_accvgpr_read each and share one accumulator quad, serialising the MFMAs behind s_nop waits.
 #include "common.h"
 
 namespace {
@@ -53,6 +56,29 @@ __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// RoPE (cos, sin) of the 4 dim pairs 4g..4g+3 of frame f
+__device__ __forceinline__ void rot8_load(const float* __restrict__ rot, int f, int g, float* cs) {
+  const f32x4 c0 = *reinterpret_cast<const f32x4*>(rot + (f * 16 + 4 * g) * 2);
+  const f32x4 c1 = *reinterpret_cast<const f32x4*>(rot + (f * 16 + 4 * g + 2) * 2);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    cs[i] = c0[i];
+    cs[4 + i] = c1[i];
+  }
+}
+// the 8 dims of a raw row chunk rotated with rot8_load's coefficients, times `scale`
+__device__ __forceinline__ bf16x8 rope8(const bf16x8 v, const float* cs, float scale) {
+  bf16x8 o;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const float c = cs[2 * u], s = cs[2 * u + 1];
+    const float a = (float)v[2 * u], b = (float)v[2 * u + 1];
+    o[2 * u] = (bf16)((a * c - b * s) * scale);
+    o[2 * u + 1] = (bf16)((b * c + a * s) * scale);
+  }
+  return o;
 }
 
 // 8 head dims 8g..8g+7 of one frame row (16-B load), RoPE-rotated by frame f when rot != null, times `scale`
@@ -111,29 +137,75 @@ __device__ __forceinline__ void store4b(bf16* p, const float* v) {
   *reinterpret_cast<bf16x4*>(p) = a;
 }
 
-// bias by offset n = j - i (index n + F - 1), log2 units, for head h
-__device__ __forceinline__ void load_boff(const float* __restrict__ bias, float* boff, int h, int F, int tid, int nthr) {
-  for (int e = tid; e < 2 * F - 1; e += nthr) {
-    const int n = e - (F - 1);
-    const int i = n < 0 ? -n : 0, j = i + n;
-    boff[e] = bias[((int64_t)h * F + i) * F + j] * LOG2E;
+// Score-tile bias table: tab[c][k] = bias(n) for n = sign * (k + c - 16 NT) (log2 units, 0 for |n| >= F), four
+// copies shifted by c = 0..3.  An MFMA D fragment's four consecutive offsets (register r of lane (g, lr) in the
+// (row tile a, column tile b) block: n = 16 (b - a) + 4g - lr + r) are then ONE aligned 16-B read at
+// btab_lane(..) + 16 (b - a): lane-constant base, immediate offset per tile pair -- instead of an index
+// computation, clamp and 4-B read per element.  Every offset a padded row / column can form is in range.
+template <int NT>
+__device__ __forceinline__ void load_btab(const float* __restrict__ bias, float* tab, int h, int F, int sign, int tid,
+                                          int nthr) {
+  constexpr int TL = 32 * NT;
+  for (int e = tid; e < 4 * TL; e += nthr) {
+    const int c = e / TL, k = e - c * TL;
+    const int n = sign * (k + c - 16 * NT);
+    float v = 0.f;
+    if (n > -F && n < F) {
+      const int i = n < 0 ? -n : 0, j = i + n;
+      v = bias[((int64_t)h * F + i) * F + j] * LOG2E;
+    }
+    tab[e] = v;
   }
 }
+template <int NT>
+__device__ __forceinline__ const float* btab_lane(const float* tab, int lr, int g) {
+  const int e0 = 4 * g - lr + 16 * NT, c = e0 & 3;  // e0 - c >= 0 and e0 + 16 (NT - 1) + 3 < 32 NT
+  return tab + c * 32 * NT + (e0 - c);
+}
+// Block -> (4-pixel group, head) of the per-pixel kernels (fwd, bwd_kv): grid (8 * 8 * cdiv(groups, 8), B).
+// A head's q / k / v are 64 B of the voxel's 1536-B qkv row, half a 128-B line.  Workgroups are dealt to the
+// 8 XCDs round-robin (linear id mod 8), so the 8 blocks an XCD receives back to back (ids L, L + 8, ...) are
+// the 8 heads of one pixel group: every line is fetched once into that XCD's L2 and used whole.  (One head per
+// grid row instead fetched each line twice from HBM: the head-pair partner ran 1/8 of the grid later.)
+#ifndef TF_QPRE
+#define TF_QPRE 0  // forward Q' fragments all loaded in the prologue (1: measured 1.7x slower at F = 120)
+#endif
+#ifndef TF_FWD_WPE
+#define TF_FWD_WPE 2  // forward waves per SIMD the register allocation targets (>= 2: VGPR-form MFMAs)
+#endif
+#ifndef TF_KV_PF
+#define TF_KV_PF 1  // A/B knob: dk / dv key-tile rows prefetched a tile ahead
+#endif
+#ifndef TF_XCD_MAP
+#define TF_XCD_MAP 1  // A/B knob: 0 = head-major grid (round 2)
+#endif
+__device__ __forceinline__ void tf_block(int& grp, int& h) {
+  const int L = blockIdx.x, j = L >> 3;
+  h = TF_XCD_MAP ? j & 7 : L / (gridDim.x / 8);
+  grp = TF_XCD_MAP ? (j >> 3) * 8 + (L & 7) : L % (gridDim.x / 8);
+}
+static unsigned tf_grid_x(int HW) { return (unsigned)(64 * cdiv(cdiv(HW, 4), 8)); }
+
+// padded query rows: their lse makes every P entry exactly 0 (exp2(x - 1e30) = 0 for any finite x)
+constexpr float TF_LSE_PAD = 1e30f;
 
 // ------------------------------------------------------------------------------------------------ forward
-// grid (cdiv(HW, 4), B * 8), 256 threads: wave = one pixel of one (sample, head)
+// grid (tf_grid_x(HW), B), 256 threads: wave = one pixel of one (sample, head) (tf_block)
 template <int NT>
-__global__ __launch_bounds__(256) void tflash_fwd_kernel(const bf16* __restrict__ qkv, const float* __restrict__ bias,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE))) void tflash_fwd_kernel(const bf16* __restrict__ qkv, const float* __restrict__ bias,
                                                          const float* __restrict__ rot, bf16* __restrict__ out,
                                                          float* __restrict__ lse, int F, int HW, float scale) {
   constexpr int NP = (NT + 1) / 2, NR = 32 * NP;  // key-tile pairs, staged rows
-  __shared__ float boff[2 * 16 * TF_MAXT];
+  __shared__ __attribute__((aligned(16))) float btab[4 * 32 * NT];
   __shared__ __attribute__((aligned(16))) bf16 vst[4][NR * TF_LD];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, lr = lane & 15, g = lane >> 4;
-  const int b = blockIdx.y >> 3, h = blockIdx.y & 7;
-  load_boff(bias, boff, h, F, tid, 256);
+  int grp, h;
+  tf_block(grp, h);
+  const int b = blockIdx.y;
+  if (grp * 4 >= HW) return;  // whole block (padded groups)
+  load_btab<NT>(bias, btab, h, F, 1, tid, 256);
   __syncthreads();
-  const int p = blockIdx.x * 4 + wid;
+  const int p = grp * 4 + wid;
   if (p >= HW) return;
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
   const int64_t row0 = (int64_t)b * F * HW + p;  // voxel of frame f: row0 + f * HW
@@ -143,12 +215,15 @@ __global__ __launch_bounds__(256) void tflash_fwd_kernel(const bf16* __restrict_
     const bf16x8 v = ld16(qkv + (row0 + (int64_t)(f < F ? f : 0) * HW) * QKV + 2 * INNER + h * DH + c * 8);
     *reinterpret_cast<bf16x8*>(vs + f * TF_LD + c * 8) = f < F ? v : zero8();
   }
-  bf16x8 kf[NT];
+  // every K' and Q' fragment up front (TF_QPRE): one exposed load latency per wave instead of one per query tile
+  bf16x8 kf[NT], qfa[TF_QPRE ? NT : 1];
 #pragma unroll
   for (int kt = 0; kt < NT; ++kt) {
     const int f = kt * 16 + lr;
     const bool ok = f < F;
-    kf[kt] = row_frag(qkv + (row0 + (int64_t)(ok ? f : 0) * HW) * QKV + INNER + h * DH + g * 8, rot, ok ? f : 0, g, 1.f, ok);
+    const int64_t rr = (row0 + (int64_t)(ok ? f : 0) * HW) * QKV + h * DH + g * 8;
+    kf[kt] = row_frag(qkv + rr + INNER, rot, ok ? f : 0, g, 1.f, true);
+    if (TF_QPRE) qfa[TF_QPRE ? kt : 0] = row_frag(qkv + rr, rot, ok ? f : 0, g, scale, true);
   }
   wsync();
   bf16x8 vf[NP][2];
@@ -157,27 +232,40 @@ __global__ __launch_bounds__(256) void tflash_fwd_kernel(const bf16* __restrict_
 #pragma unroll
     for (int t = 0; t < 2; ++t) vf[s][t] = tr_pair(vs, s, t * 16, lane);
 
+  // Padded rows are never zeroed in registers: their loads are clamped to frame 0 (finite data).  Keys past F
+  // exist only in the last key tile and get an additive -inf there; padded query columns compute a finite
+  // softmax that is not stored.
+  const float* bl = btab_lane<NT>(btab, lr, g);
+  float kmask[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) kmask[r] = 16 * (NT - 1) + 4 * g + r < F ? 0.f : -INFINITY;
+
   for (int qt = 0; qt < NT; ++qt) {
     const int fq = qt * 16 + lr;
     const bool okq = fq < F;
-    const bf16x8 qf = row_frag(qkv + (row0 + (int64_t)(okq ? fq : 0) * HW) * QKV + h * DH + g * 8, rot, okq ? fq : 0, g,
-                               scale, okq);
+    const bf16x8 qf = TF_QPRE ? qfa[TF_QPRE ? qt : 0]
+                              : row_frag(qkv + (row0 + (int64_t)(okq ? fq : 0) * HW) * QKV + h * DH + g * 8, rot,
+                                         okq ? fq : 0, g, scale, true);
+    const float* bq = bl - 16 * qt;
     float sc[2 * NP][4];
     float m = -INFINITY;
 #pragma unroll
     for (int kt = 0; kt < 2 * NP; ++kt) {
-      const f32x4 st = kt < NT ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt < NT ? kt : 0], qf, z4, 0, 0, 0) : z4;
+      if (kt < NT) {
+        const f32x4 st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt < NT ? kt : 0], qf, z4, 0, 0, 0);
+        const f32x4 bo = *reinterpret_cast<const f32x4*>(bq + 16 * kt);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = kt * 16 + 4 * g + r;
-        const bool ok = okq && key < F;
-        const float bo = boff[ok ? key - fq + F - 1 : 0];
-        sc[kt][r] = ok ? fmaf(st[r], LOG2E, bo) : -INFINITY;
-        m = fmaxf(m, sc[kt][r]);
+        for (int r = 0; r < 4; ++r) {
+          sc[kt][r] = fmaf(st[r], LOG2E, bo[r]);
+          if (kt == NT - 1) sc[kt][r] += kmask[r];
+          m = fmaxf(m, sc[kt][r]);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sc[kt][r] = -INFINITY;
       }
     }
-    m = grp4_max(m);
-    const float mm = m == -INFINITY ? 0.f : m;
+    const float mm = grp4_max(m);  // finite: key 0 is valid for every query row
     float l = 0.f;
 #pragma unroll
     for (int kt = 0; kt < 2 * NP; ++kt)
@@ -212,18 +300,18 @@ __global__ __launch_bounds__(256) void tflash_fwd_kernel(const bf16* __restrict_
 // [B][8][HW][F], and per-block dbias-by-offset partials part[(b*8 + h)][blk][2F - 1].  With the query tile
 // fixed per wave, the dbias accumulator of (r, kt) holds one diagonal kt - qt for every pixel: static registers.
 template <int NT>
-__global__ __launch_bounds__(64 * NT) void tflash_bwd_q_kernel(
+__global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(2))) void tflash_bwd_q_kernel(
     const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
     const float* __restrict__ lse, const float* __restrict__ bias, const float* __restrict__ rot,
     bf16* __restrict__ dqkv, float* __restrict__ dbuf, float* __restrict__ part, int F, int HW, float scale) {
   constexpr int NP = (NT + 1) / 2, NR = 32 * NP, NTH = 64 * NT;
-  __shared__ float boff[2 * 16 * TF_MAXT];
+  __shared__ __attribute__((aligned(16))) float btab[4 * 32 * NT];
   __shared__ float dacc[2 * 16 * TF_MAXT];
   __shared__ __attribute__((aligned(16))) bf16 ks[NR * TF_LD];
   __shared__ __attribute__((aligned(16))) bf16 vs[NR * TF_LD];
   const int tid = threadIdx.x, lane = tid & 63, qt = tid >> 6, lr = lane & 15, g = lane >> 4;
   const int b = blockIdx.y >> 3, h = blockIdx.y & 7;
-  load_boff(bias, boff, h, F, tid, NTH);
+  load_btab<NT>(bias, btab, h, F, 1, tid, NTH);
   for (int e = tid; e < 2 * 16 * TF_MAXT; e += NTH) dacc[e] = 0.f;
   for (int e = tid; e < (NR - 16 * NT) * 4; e += NTH) {  // rows past the last key tile stay zero
     const int f = 16 * NT + (e >> 2), c = e & 3;
@@ -237,21 +325,45 @@ __global__ __launch_bounds__(64 * NT) void tflash_bwd_q_kernel(
     for (int kt = 0; kt < NT; ++kt) dba[r][kt] = 0.f;
   const int fq = qt * 16 + lr;
   const bool okq = fq < F;
+  const float* bq = btab_lane<NT>(btab, lr, g) - 16 * qt;
+  bool kok[4];  // keys of the last key tile below F
+#pragma unroll
+  for (int r = 0; r < 4; ++r) kok[r] = 16 * (NT - 1) + 4 * g + r < F;
+
+  // Software pipeline over the block's pixels: the next pixel's raw rows are loaded into registers while the
+  // current one is computed (one block per CU at 2 waves per SIMD: a load issued at the top of an iteration
+  // was fully exposed).  Each thread stages exactly one 16-B chunk of K' and of V per pixel (16 NT frames x 4
+  // chunks = NTH); its frame, and so its RoPE coefficients, are the same for every pixel, as are the query's.
+  const int sf = tid >> 2, sc = tid & 3;
+  const bool sok = sf < F;
+  const int sfc = sok ? sf : 0, fqc = okq ? fq : 0;
+  float kcs[8], qcs[8];
+  rot8_load(rot, sfc, sc, kcs);
+  rot8_load(rot, fqc, g, qcs);
+  bf16x8 kraw = zero8(), vraw = zero8(), qraw = zero8(), draw = zero8();
+  float lraw = 0.f;
+  auto fetch = [&](int pp) {
+    const int64_t r0 = (int64_t)b * F * HW + pp;
+    const int64_t rs = (r0 + (int64_t)sfc * HW) * QKV + h * DH + sc * 8;
+    kraw = ld16(qkv + rs + INNER);
+    vraw = ld16(qkv + rs + 2 * INNER);
+    const int64_t vq = r0 + (int64_t)fqc * HW;
+    qraw = ld16(qkv + vq * QKV + h * DH + g * 8);
+    draw = ld16(dout + vq * INNER + h * DH + g * 8);
+    lraw = lse[(((int64_t)b * NH + h) * HW + pp) * F + fqc];
+  };
+  if ((int)blockIdx.x < HW) fetch(blockIdx.x);
 
   for (int p = blockIdx.x; p < HW; p += gridDim.x) {
     const int64_t row0 = (int64_t)b * F * HW + p;
     __syncthreads();  // previous pixel's rows consumed
-    for (int e = tid; e < 16 * NT * 4; e += NTH) {  // rotated K' rows and V rows, 16-B chunks
-      const int f = e >> 2, c = e & 3;
-      const bool ok = f < F;
-      const int64_t rr = (row0 + (int64_t)(ok ? f : 0) * HW) * QKV;
-      *reinterpret_cast<bf16x8*>(ks + f * TF_LD + c * 8) = row_frag(qkv + rr + INNER + h * DH + c * 8, rot, ok ? f : 0, c, 1.f, ok);
-      *reinterpret_cast<bf16x8*>(vs + f * TF_LD + c * 8) = row_frag(qkv + rr + 2 * INNER + h * DH + c * 8, nullptr, 0, c, 1.f, ok);
-    }
-    const int64_t vq = row0 + (int64_t)(okq ? fq : 0) * HW;
-    const bf16x8 qf = row_frag(qkv + vq * QKV + h * DH + g * 8, rot, okq ? fq : 0, g, scale, okq);
-    const bf16x8 dof = row_frag(dout + vq * INNER + h * DH + g * 8, nullptr, 0, g, 1.f, okq);
-    const float Li = okq ? lse[(((int64_t)b * NH + h) * HW + p) * F + fq] : 0.f;
+    *reinterpret_cast<bf16x8*>(ks + sf * TF_LD + sc * 8) = sok ? rope8(kraw, kcs, 1.f) : zero8();
+    *reinterpret_cast<bf16x8*>(vs + sf * TF_LD + sc * 8) = sok ? vraw : zero8();
+    // padded query rows: finite clamped data, P = 0 through Li (so D = dS = 0 there)
+    const bf16x8 qf = rope8(qraw, qcs, scale);
+    const bf16x8 dof = draw;
+    const float Li = okq ? lraw : TF_LSE_PAD;
+    if (p + (int)gridDim.x < HW) fetch(p + gridDim.x);
     __syncthreads();  // rows staged
     // pass 1: P^T and dP^T of every key tile, D_i = sum_j P_ij dP_ij (exact: at F = 1 the bias gradient is 0)
     float pt[NT][4], dpt[NT][4];
@@ -262,12 +374,11 @@ __global__ __launch_bounds__(64 * NT) void tflash_bwd_q_kernel(
       const bf16x8 vf = ld16(vs + (kt * 16 + lr) * TF_LD + g * 8);
       const f32x4 st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf, z4, 0, 0, 0);   // S'^T
       const f32x4 dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, dof, z4, 0, 0, 0);  // dP^T
+      const f32x4 bo = *reinterpret_cast<const f32x4*>(bq + 16 * kt);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int key = kt * 16 + 4 * g + r;
-        const bool ok = okq && key < F;
-        const float bo = boff[ok ? key - fq + F - 1 : 0];
-        pt[kt][r] = ok ? __builtin_amdgcn_exp2f(fmaf(st[r], LOG2E, bo) - Li) : 0.f;
+        pt[kt][r] = __builtin_amdgcn_exp2f(fmaf(st[r], LOG2E, bo[r]) - Li);
+        if (kt == NT - 1) pt[kt][r] = kok[r] ? pt[kt][r] : 0.f;
         dpt[kt][r] = dp[r];
         D = fmaf(pt[kt][r], dp[r], D);
       }
@@ -333,21 +444,24 @@ __global__ __launch_bounds__(64 * NT) void tflash_bwd_q_kernel(
 }
 
 // ------------------------------------------------------------------------------------------------ backward, dk dv
-// grid (cdiv(HW, 4), B * 8), 256 threads: wave = one pixel; key tiles outer, query-tile pairs inner
+// grid (tf_grid_x(HW), B), 256 threads: wave = one pixel (tf_block); key tiles outer, query-tile pairs inner
 template <int NT>
 __global__ __launch_bounds__(256, 2) void tflash_bwd_kv_kernel(
     const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ dbuf, const float* __restrict__ bias, const float* __restrict__ rot,
     bf16* __restrict__ dqkv, int F, int HW, float scale) {
   constexpr int NP = (NT + 1) / 2, NR = 32 * NP;
-  __shared__ float boff[2 * 16 * TF_MAXT];
+  __shared__ __attribute__((aligned(16))) float btab[4 * 32 * NT];
   __shared__ __attribute__((aligned(16))) bf16 stg[4][NR * TF_LD];
-  __shared__ float lds_l[4][NR], lds_d[4][NR];
+  __shared__ __attribute__((aligned(16))) float lds_l[4][NR], lds_d[4][NR];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, lr = lane & 15, g = lane >> 4;
-  const int b = blockIdx.y >> 3, h = blockIdx.y & 7;
-  load_boff(bias, boff, h, F, tid, 256);
+  int grp, h;
+  tf_block(grp, h);
+  const int b = blockIdx.y;
+  if (grp * 4 >= HW) return;  // whole block (padded groups)
+  load_btab<NT>(bias, btab, h, F, -1, tid, 256);  // rows = queries here: offsets key - query = -(q - key)
   __syncthreads();
-  const int p = blockIdx.x * 4 + wid;
+  const int p = grp * 4 + wid;
   if (p >= HW) return;
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
   const int64_t row0 = (int64_t)b * F * HW + p;
@@ -357,7 +471,7 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_kv_kernel(
   for (int e = lane; e < NR; e += 64) {
     const bool ok = e < F;
     const int64_t si = (((int64_t)b * NH + h) * HW + p) * F + (ok ? e : 0);
-    Ls[e] = ok ? lse[si] : 0.f;
+    Ls[e] = ok ? lse[si] : TF_LSE_PAD;  // padded query rows: P = dS = 0, no mask in the loop
     Ds[e] = ok ? dbuf[si] : 0.f;
   }
   for (int e = lane; e < (NR - 16 * NT) * 4; e += 64) {
@@ -371,8 +485,8 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_kv_kernel(
     const int f = qt * 16 + lr;
     const bool ok = f < F;
     const int64_t vq = row0 + (int64_t)(ok ? f : 0) * HW;
-    qa[qt] = row_frag(qkv + vq * QKV + h * DH + g * 8, rot, ok ? f : 0, g, scale, ok);
-    da[qt] = row_frag(dout + vq * INNER + h * DH + g * 8, nullptr, 0, g, 1.f, ok);
+    qa[qt] = row_frag(qkv + vq * QKV + h * DH + g * 8, rot, ok ? f : 0, g, scale, true);  // padded: P = dS = 0
+    da[qt] = row_frag(dout + vq * INNER + h * DH + g * 8, nullptr, 0, g, 1.f, true);
     *reinterpret_cast<bf16x8*>(st + f * TF_LD + g * 8) = qa[qt];
   }
   wsync();
@@ -389,12 +503,26 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_kv_kernel(
 #pragma unroll
     for (int t = 0; t < 2; ++t) dtf[s][t] = tr_pair(st, s, t * 16, lane);
 
+  const float* bl = btab_lane<NT>(btab, lr, g);
+  // key tile kt + 1's raw K / V rows and RoPE coefficients are loaded while tile kt is computed (TF_KV_PF)
+  bf16x8 kraw, vraw;
+  float kcs[8];
+  auto fetch = [&](int t) {
+    const int fk = t * 16 + lr, fkc = fk < F ? fk : 0;
+    const int64_t rk = (row0 + (int64_t)fkc * HW) * QKV + h * DH + g * 8;
+    kraw = ld16(qkv + rk + INNER);
+    vraw = ld16(qkv + rk + 2 * INNER);
+    rot8_load(rot, fkc, g, kcs);
+  };
+  if (TF_KV_PF) fetch(0);
   for (int kt = 0; kt < NT; ++kt) {
     const int fk = kt * 16 + lr;
-    const bool okk = fk < F;
-    const int64_t rk = (row0 + (int64_t)(okk ? fk : 0) * HW) * QKV;
-    const bf16x8 kb = row_frag(qkv + rk + INNER + h * DH + g * 8, rot, okk ? fk : 0, g, 1.f, okk);  // K'^T col
-    const bf16x8 vb = row_frag(qkv + rk + 2 * INNER + h * DH + g * 8, nullptr, 0, g, 1.f, okk);     // V^T col
+    const bool okk = fk < F;  // padded key columns: finite garbage, not stored
+    const float* bk = bl - 16 * kt;
+    if (!TF_KV_PF) fetch(kt);
+    const bf16x8 kb = rope8(kraw, kcs, 1.f);  // K'^T col
+    const bf16x8 vb = vraw;                   // V^T col
+    if (TF_KV_PF && kt + 1 < NT) fetch(kt + 1);
     f32x4 dk[2] = {z4, z4}, dv[2] = {z4, z4};
 #pragma unroll
     for (int s = 0; s < NP; ++s) {
@@ -405,14 +533,14 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_kv_kernel(
         if (qt < NT) {
           const f32x4 sq = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[qt], kb, z4, 0, 0, 0);  // S'[q][key]
           const f32x4 dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da[qt], vb, z4, 0, 0, 0);  // dP[q][key]
+          const f32x4 bo = *reinterpret_cast<const f32x4*>(bk + 16 * qt);
+          const f32x4 lq = *reinterpret_cast<const f32x4*>(Ls + qt * 16 + 4 * g);
+          const f32x4 dq = *reinterpret_cast<const f32x4*>(Ds + qt * 16 + 4 * g);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int q = qt * 16 + 4 * g + r;
-            const bool ok = okk && q < F;
-            const float bo = boff[ok ? fk - q + F - 1 : 0];
-            const float pp = ok ? __builtin_amdgcn_exp2f(fmaf(sq[r], LOG2E, bo) - Ls[q]) : 0.f;
+            const float pp = __builtin_amdgcn_exp2f(fmaf(sq[r], LOG2E, bo[r]) - lq[r]);
             pv[u][r] = pp;
-            dsv[u][r] = pp * (dp[r] - Ds[q]);
+            dsv[u][r] = pp * (dp[r] - dq[r]);
           }
         } else {
 #pragma unroll
@@ -498,7 +626,7 @@ int cesm_tflash_nblk(int HW) { return std::max(1, std::min(HW, 128)); }
 int cesm_tflash_fwd(const void* qkv, const float* bias, const float* rot, void* out, float* lse, int B, int F, int HW,
                     float scale, hipStream_t stream) {
   if (!cesm_tflash_supported(F) || B < 1 || HW < 1) return CESM_EUNSUPPORTED;
-  dim3 grid((unsigned)cdiv(HW, 4), B * NH);
+  dim3 grid(tf_grid_x(HW), B);
   const int nt = (F + 15) / 16;
 #define TFF(N) tflash_fwd_kernel<N><<<grid, 256, 0, stream>>>((const bf16*)qkv, bias, rot, (bf16*)out, lse, F, HW, scale)
   switch (nt) {
@@ -525,7 +653,7 @@ int cesm_tflash_bwd(const void* qkv, const void* o, const void* dout, const floa
   if (!cesm_tflash_supported(F) || B < 1 || HW < 1) return CESM_EUNSUPPORTED;
   const int nt = (F + 15) / 16;
   const int nblk = cesm_tflash_nblk(HW);
-  dim3 gq(nblk, B * NH), gk((unsigned)cdiv(HW, 4), B * NH);
+  dim3 gq(nblk, B * NH), gk(tf_grid_x(HW), B);
 #define TFB(N)                                                                                                         \
   tflash_bwd_q_kernel<N><<<gq, 64 * N, 0, stream>>>((const bf16*)qkv, (const bf16*)o, (const bf16*)dout, lse, bias, rot, \
                                                  (bf16*)dqkv, dbuf, part, F, HW, scale);                               \

@@ -245,7 +245,7 @@ def gn_stats(y, B, G, eps=1e-5):
     C = y.shape[-1]
     rows_b = y.numel() // (C * B)
     stats = empty((B, G, 2), torch.float32, y.device)
-    ws = empty((B * 256 * G * 2,), torch.float64, y.device)
+    ws = empty((max(B * 256, 1024) * G * 2,), torch.float64, y.device)
     call("cesm_gn_stats", dtcode(y), P(y), P(stats), P(ws), B, rows_b, C, G, float(eps), S())
     return stats
 
@@ -275,7 +275,7 @@ def gn_bwd(dout, y, stats, gamma, beta, ss, dgamma, dbeta, B, G, want_dss, dbias
     rows_b = y.numel() // (C * B)
     dy = empty(y.shape, y.dtype, y.device)
     dss = empty((B, 2 * C), torch.float32, y.device) if want_dss else None
-    ws = empty((B * 256 * C * 3 + B * C * 3 + B * C * 5,), torch.float32, y.device)
+    ws = empty((max(B * 256, 1024) * C * 3 + B * C * 3 + B * C * 5,), torch.float32, y.device)
     call("cesm_gn_bwd", dtcode(y), P(dout), P(y), P(stats), P(gamma), P(beta), P(ss), P(dy), P(dss), P(dgamma),
          P(dbeta), P(dbias), P(ws), B, rows_b, C, G, 1, S())
     return dy, dss

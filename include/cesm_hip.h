@@ -85,6 +85,7 @@ int cesm_head_bwd(int dtype, const float* dout, const void* x, const float* w, v
 
 /* ---- normalisation (csrc/norm.hip) -------------------------------------------------------
  * GroupNorm(G,C) eps, affine, then x*(scale+1)+shift, SiLU, + residual: video_net.py:216-227, :265. */
+/* ws >= max(B*256, 1024)*G*2 doubles */
 int cesm_gn_stats(int dtype, const void* y, float* stats, double* ws, int B, int64_t rows_b, int C, int G, float eps,
                   hipStream_t stream);
 /* stats [B][G] (mean, rstd) from cesm_conv_fwd_gn's partials (replaces cesm_gn_stats' pass over y):
@@ -95,7 +96,7 @@ int cesm_gn_apply(int dtype, const void* y, const float* stats, const float* gam
                   const float* ss, const void* res, void* out, float* ws, int B, int64_t rows_b, int C, int G,
                   hipStream_t stream);
 /* backward; also writes the producing conv's bias gradient dbias (+)= sum dy (nullable) without another
- * pass over dy.  ws >= B*256*C*3 + B*C*3 + B*C*5 floats. */
+ * pass over dy.  ws >= max(B*256, 1024)*C*3 + B*C*3 + B*C*5 floats. */
 int cesm_gn_bwd(int dtype, const void* dout, const void* y, const float* stats, const float* gamma,
                 const float* beta, const float* ss, void* dy, float* dss, float* dgamma, float* dbeta, float* dbias,
                 float* ws, int B, int64_t rows_b, int C, int G, int accumulate, hipStream_t stream);

@@ -1,5 +1,6 @@
 """HIP-event timing of the GroupNorm passes at the level-0 bench shape (B = 8, F = 12, 192x288, C = 64) and
-level 1 (96x144, C = 128): stats, apply (with / without residual), backward (reduce + apply); effective GB/s."""
+level 1 (96x144, C = 128): stats, apply (with / without residual), backward (reduce + apply); effective GB/s.
+GN_SHAPES=f120: the long-window leg instead (B = 1, F = 120, levels 0 and 1)."""
 import os
 import sys
 
@@ -24,7 +25,9 @@ def timed(fn, reps=10):
 def main():
     dev = torch.device("cuda")
     B, F, G = 8, 12, 8
-    tag = os.environ.get("CESM_HIP_LIB", "default")
+    if os.environ.get("GN_SHAPES") == "f120":
+        B, F = 1, 120
+    tag = os.environ.get("CESM_HIP_LIB", "default") + f" B={B} F={F}"
     for (H, W, C) in [(192, 288, 64), (96, 144, 128)]:
         y = torch.randn(B * F, H, W, C, device=dev).to(torch.bfloat16)
         res = torch.randn_like(y)
