@@ -311,7 +311,10 @@ __global__ __launch_bounds__(256) void slaf_combine_kernel(const float* __restri
 // slaf_out: wave = 16*NV pixels of one frame, all heads; grid (cdiv(HW, 64*NV), Nf), 256 threads.
 // ---------------------------------------------------------------------------------------------------
 template <int C, int NV>
-__global__ __launch_bounds__(256) void slaf_out_kernel(const bf16* __restrict__ x, const float* __restrict__ gamma,
+#ifndef SLAF_WPE
+#define SLAF_WPE 2  // slaf_out capped at 256 registers (VGPR-form MFMAs, no AGPR stash); 1 = round-2 allocation
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLAF_WPE))) void slaf_out_kernel(const bf16* __restrict__ x, const float* __restrict__ gamma,
                                                        const bf16* __restrict__ wqkv, const bf16* __restrict__ wout,
                                                        const float* __restrict__ bout, const bf16* __restrict__ actT,
                                                        bf16* __restrict__ y, bf16* __restrict__ o_out, int HW, float scale, float eps) {

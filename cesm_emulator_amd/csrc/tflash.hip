@@ -176,6 +176,9 @@ __device__ __forceinline__ const float* btab_lane(const float* tab, int lr, int 
 #ifndef TF_KV_PF
 #define TF_KV_PF 1  // A/B knob: dk / dv key-tile rows prefetched a tile ahead
 #endif
+#ifndef TF_VH
+#define TF_VH 2  // forward V staging: key-tile pairs per part (4 = all at F = 128)
+#endif
 #ifndef TF_XCD_MAP
 #define TF_XCD_MAP 1  // A/B knob: 0 = head-major grid (round 2)
 #endif
@@ -196,8 +199,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE)
                                                          const float* __restrict__ rot, bf16* __restrict__ out,
                                                          float* __restrict__ lse, int F, int HW, float scale) {
   constexpr int NP = (NT + 1) / 2, NR = 32 * NP;  // key-tile pairs, staged rows
+  // V rows are staged TF_VH key-tile pairs at a time: the V^T fragments live in registers afterwards, so the
+  // wave's staging slice only has to hold part of them -- less LDS per block, one more block per CU
+  constexpr int VH = NP < TF_VH ? NP : TF_VH, NVR = 32 * VH;
   __shared__ __attribute__((aligned(16))) float btab[4 * 32 * NT];
-  __shared__ __attribute__((aligned(16))) bf16 vst[4][NR * TF_LD];
+  __shared__ __attribute__((aligned(16))) bf16 vst[4][NVR * TF_LD];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, lr = lane & 15, g = lane >> 4;
   int grp, h;
   tf_block(grp, h);
@@ -210,11 +216,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE)
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
   const int64_t row0 = (int64_t)b * F * HW + p;  // voxel of frame f: row0 + f * HW
   bf16* vs = vst[wid];
-  for (int e = lane; e < NR * 4; e += 64) {  // V rows (zero past F)
-    const int f = e >> 2, c = e & 3;
-    const bf16x8 v = ld16(qkv + (row0 + (int64_t)(f < F ? f : 0) * HW) * QKV + 2 * INNER + h * DH + c * 8);
-    *reinterpret_cast<bf16x8*>(vs + f * TF_LD + c * 8) = f < F ? v : zero8();
-  }
   // every K' and Q' fragment up front (TF_QPRE): one exposed load latency per wave instead of one per query tile
   bf16x8 kf[NT], qfa[TF_QPRE ? NT : 1];
 #pragma unroll
@@ -225,12 +226,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE)
     kf[kt] = row_frag(qkv + rr + INNER, rot, ok ? f : 0, g, 1.f, true);
     if (TF_QPRE) qfa[TF_QPRE ? kt : 0] = row_frag(qkv + rr, rot, ok ? f : 0, g, scale, true);
   }
-  wsync();
   bf16x8 vf[NP][2];
 #pragma unroll
-  for (int s = 0; s < NP; ++s)
+  for (int s0 = 0; s0 < NP; s0 += VH) {
+    if (s0) wsync();  // previous part's transposed reads done
+    for (int e = lane; e < NVR * 4; e += 64) {  // V rows 32 s0 .. (zero past F)
+      const int fl = e >> 2, c = e & 3, f = 32 * s0 + fl;
+      const bf16x8 v = ld16(qkv + (row0 + (int64_t)(f < F ? f : 0) * HW) * QKV + 2 * INNER + h * DH + c * 8);
+      *reinterpret_cast<bf16x8*>(vs + fl * TF_LD + c * 8) = f < F ? v : zero8();
+    }
+    wsync();
 #pragma unroll
-    for (int t = 0; t < 2; ++t) vf[s][t] = tr_pair(vs, s, t * 16, lane);
+    for (int s = s0; s < s0 + VH && s < NP; ++s)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) vf[s][t] = tr_pair(vs, s - s0, t * 16, lane);
+  }
 
   // Padded rows are never zeroed in registers: their loads are clamped to frame 0 (finite data).  Keys past F
   // exist only in the last key tile and get an additive -inf there; padded query columns compute a finite
