@@ -1615,18 +1615,30 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
 // ----------------------------------------------------------------------------------------
 // 1x1 conv (bf16) as a GEMM: Y[m][co] = bias[co] + res[m][co] + sum_k X[m][k] W[co][k], X = [x1 | x2]
 // concatenated on channels, Y = [y1 | y2] split at Co1.  Block = 128 pixels x BN output channels
-// (grid.x = co blocks, fast, so a pixel tile's co blocks share its X rows in L2); K in steps of 64
+// (the co blocks of a pixel tile run back to back on one XCD, sharing its X rows in L2); K in steps of 64
 // through two LDS stages filled by buffer-LDS-DMA (128-B rows, 16-B chunk index XORed with row & 7,
 // out-of-range rows -> zeros); 4 waves = 2 (co halves) x 2 (64-pixel halves).  The epilogue stages
 // (acc + bias) as bf16 pixel rows in LDS and writes them (+ residual) with coalesced 16-B accesses.
 // Replaces the generic implicit-GEMM path for every 1x1 conv: attention projections at levels with
-// C >= 128, res_conv, and their data gradients.
+// C >= 128, res_conv, and their data gradients.  NS = 1 (K = 64: one LDS stage, 35 KB) runs 4 blocks per
+// CU instead of 2: the K = 64 projections (to_qkv 64 -> 768 of the long-window level 0) are output-store
+// streams whose per-block load -> MFMA -> store phases need the extra blocks to overlap.  The X buffer
+// resource covers the block's own 128 rows only, so M * K is not limited to 2^31 bytes.
 // ----------------------------------------------------------------------------------------
 constexpr int G1_BM = 128;
+#ifndef G1_NS1
+#define G1_NS1 1   // A/B knob: single-stage K = 64 variant (0 = always two stages)
+#endif
+#ifndef G1_XCD
+#define G1_XCD 1   // A/B knob: XCD-grouped co blocks (0 = co-block-fastest linear order)
+#endif
+#ifndef G1_BIGM
+#define G1_BIGM 1  // A/B knob: gemm1x1 for M * K >= 2^31 bytes too (0 = generic conv there, round 2)
+#endif
 __device__ __forceinline__ int g1_off(int row, int chunk) { return (row << 7) + ((chunk ^ (row & 7)) << 4); }
 
-template <int BN>
-__global__ __launch_bounds__(256, 2) void gemm1x1_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
+template <int BN, int NS>
+__global__ __launch_bounds__(256, NS == 1 ? 4 : 2) void gemm1x1_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
                                                          const bf16* __restrict__ w, const float* __restrict__ bias,
                                                          const bf16* __restrict__ res, const bf16* __restrict__ res2,
                                                          bf16* __restrict__ y1, bf16* __restrict__ y2, int M, int C1,
@@ -1634,13 +1646,19 @@ __global__ __launch_bounds__(256, 2) void gemm1x1_kernel(const bf16* __restrict_
   constexpr int STAGE = (G1_BM + BN) * 128;  // bytes
   constexpr int TM = BN / 32;                // 16-co fragments per wave
   constexpr int ELD = BN + 8;                // epilogue row (bf16)
-  static_assert(G1_BM * ELD * 2 <= 2 * STAGE, "epilogue tile fits the stages");
-  __shared__ __attribute__((aligned(1024))) char lds[2 * STAGE];
+  constexpr int LDSB = NS * STAGE > G1_BM * ELD * 2 ? NS * STAGE : G1_BM * ELD * 2;
+  __shared__ __attribute__((aligned(1024))) char lds[LDSB];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
   const int lr = lane & 15, lg = lane >> 4;
   const int K = C1 + C2, nk = K / 64;
-  const int m0 = blockIdx.y * G1_BM, n0 = blockIdx.x * BN;
+  // 1-D grid: the ncb co blocks of a pixel tile are dealt to ONE XCD back to back (linear id mod 8 = XCD), so
+  // the tile's X rows are fetched into that XCD's L2 once instead of into up to ncb different L2s
+  const int ncb = Cout / BN, L = blockIdx.x, jx = L >> 3;
+  const int cb = G1_XCD ? jx % ncb : L % ncb;
+  const int tile = G1_XCD ? (jx / ncb) * 8 + (L & 7) : L / ncb;
+  if (tile * G1_BM >= M) return;  // padded tiles (whole block)
+  const int m0 = tile * G1_BM, n0 = cb * BN;
   const int prow = lane >> 3, pslot = lane & 7;
 
   auto issue = [&](int ks) {
@@ -1648,11 +1666,12 @@ __global__ __launch_bounds__(256, 2) void gemm1x1_kernel(const bf16* __restrict_
     const bf16* src;
     int cs, cc;
     if (c0 < C1) { src = x1; cs = C1; cc = c0; } else { src = x2; cs = C2; cc = c0 - C1; }
+    const int rows = M - m0 < G1_BM ? M - m0 : G1_BM;
     const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(src + (int64_t)m0 * cs + cc), (short)0, (int)((int64_t)(M - m0) * cs * 2 - cc * 2), 0x00020000);
+        (void*)(src + (int64_t)m0 * cs + cc), (short)0, rows * cs * 2 - cc * 2, 0x00020000);
     const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(w + (int64_t)n0 * K + c0), (short)0, BN * K * 2 - c0 * 2, 0x00020000);
-    char* sx = lds + (ks & 1) * STAGE;
+    char* sx = lds + (NS == 2 ? (ks & 1) * STAGE : 0);
     char* sw = sx + G1_BM * 128;
 #pragma unroll
     for (int k = 0; k < G1_BM / 32; ++k) {  // 8-row pieces, 4 per wave
@@ -1681,8 +1700,8 @@ __global__ __launch_bounds__(256, 2) void gemm1x1_kernel(const bf16* __restrict_
   for (int ks = 0; ks < nk; ++ks) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // stage ks landed for all waves; stage ks+1's previous reads (step ks-1) are done
-    if (ks + 1 < nk) issue(ks + 1);
-    const char* sx = lds + (ks & 1) * STAGE;
+    if (NS == 2 && ks + 1 < nk) issue(ks + 1);
+    const char* sx = lds + (NS == 2 ? (ks & 1) * STAGE : 0);
     const char* sw = sx + G1_BM * 128;
 #pragma unroll
     for (int k32 = 0; k32 < 2; ++k32) {
@@ -3699,7 +3718,7 @@ static ConvFwdPlan conv_fwd_plan(int dtype, int Nb, int Hi, int Wi, int C1, int 
                      Wo == Wi && (Co1 % H3_BN) == 0 && !getenv_flag("CESM_NO_HALO");
   const bool g1x1 = dtype == CESM_DT_BF16 && KH == 1 && KW == 1 && S == 1 && P == 0 && U == 1 && Ho == Hi &&
                     Wo == Wi && (C1 % 64) == 0 && (C2 % 64) == 0 && (Co1 % 8) == 0 && M < (1ll << 31) &&
-                    M * (C1 > C2 ? C1 : C2) * 2 < (1ll << 31) && !getenv_flag("CESM_NO_GEMM1X1");
+                    (G1_BIGM || M * (C1 > C2 ? C1 : C2) * 2 < (1ll << 31)) && !getenv_flag("CESM_NO_GEMM1X1");
   if (g1x1) {
     pl.v = (Cout % 128 == 0) ? CFV_GEMM1X1_128 : CFV_GEMM1X1_64;
   } else if (halo3 && Cout <= 1024 && !getenv_flag("CESM_CONV3X3_V1") &&
@@ -3800,13 +3819,16 @@ int conv_fwd_launch(int dtype, const void* x1, const void* x2, const void* wp, c
   switch (pl.v) {
     case CFV_GEMM1X1_128:
     case CFV_GEMM1X1_64: {
+      const bool one = C1 + C2 == 64 && G1_NS1;
+#define G1L(BNv, NSv)                                                                                               \
+  gemm1x1_kernel<BNv, NSv><<<dim3((unsigned)(Cout / BNv * 8 * cdiv(cdiv(M, G1_BM), 8))), 256, 0, stream>>>(      \
+      bx1, bx2, bwp, bias, br, br2, by1, by2, (int)M, C1, C2, Cout, Co1)
       if (pl.v == CFV_GEMM1X1_128) {
-        dim3 gg(Cout / 128, (unsigned)cdiv(M, G1_BM));
-        gemm1x1_kernel<128><<<gg, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, (int)M, C1, C2, Cout, Co1);
+        if (one) G1L(128, 1); else G1L(128, 2);
       } else {
-        dim3 gg(Cout / 64, (unsigned)cdiv(M, G1_BM));
-        gemm1x1_kernel<64><<<gg, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, (int)M, C1, C2, Cout, Co1);
+        if (one) G1L(64, 1); else G1L(64, 2);
       }
+#undef G1L
       break;
     }
     case CFV_P36_RW:

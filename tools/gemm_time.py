@@ -1,6 +1,9 @@
 """HIP-event timing of the 1x1 convs (gemm1x1_kernel) at bench shapes (more_blocks, B*F = 96): the unfused
 attention projections of levels 2-3 and their data gradients, and level-0/1 res_convs.
-usage: [CESM_HIP_LIB=...] python tools/gemm_time.py"""
+usage: [CESM_HIP_LIB=...] [G1_SHAPES=f120] python tools/gemm_time.py
+G1_SHAPES=f120: the long-window leg (B = 1, F = 120): each level's unfused temporal-block projections
+(to_qkv C -> 768, to_out 256 -> C) and their data gradients (768 -> C, C -> 256)."""
+import os
 import sys
 
 import torch
@@ -25,9 +28,14 @@ def main():
     dev = torch.device("cuda")
     N = 96
     out, tot = [], 0.0
-    for (H, W, C1, C2, Cout) in [(48, 72, 256, 0, 768), (48, 72, 768, 0, 256), (48, 72, 256, 0, 256),
+    shapes = [(48, 72, 256, 0, 768), (48, 72, 768, 0, 256), (48, 72, 256, 0, 256),
                                  (24, 36, 512, 0, 768), (24, 36, 768, 0, 512), (24, 36, 256, 0, 512),
-                                 (192, 288, 64, 64, 64), (96, 144, 128, 128, 128)]:
+                                 (192, 288, 64, 64, 64), (96, 144, 128, 128, 128)]
+    if os.environ.get("G1_SHAPES") == "f120":
+        N = 120
+        shapes = [(H, W, a, 0, b) for (H, W, C) in [(192, 288, 64), (96, 144, 128), (48, 72, 256), (24, 36, 512)]
+                  for (a, b) in [(C, 768), (256, C), (768, C), (C, 256)]]
+    for (H, W, C1, C2, Cout) in shapes:
         x1 = torch.randn(N, H, W, C1, device=dev).to(torch.bfloat16)
         x2 = torch.randn(N, H, W, C2, device=dev).to(torch.bfloat16) if C2 else None
         w = torch.randn(Cout, C1 + C2, 1, 1, 1, device=dev) * 0.05
