@@ -487,6 +487,9 @@ __device__ __forceinline__ int h3_off(int row, int ch) { return row * H3_LD + ((
 #ifndef H3_PIPE
 #define H3_PIPE 1  // conv3x3_bf16_kernel: software-pipelined tap fragments (0: the compiler's read -> MFMA order)
 #endif
+#ifndef H3_XCD
+#define H3_XCD 1  // A/B knob: XCD-grouped co blocks of a halo tile (0 = co-block-slowest order)
+#endif
 template <int TW>
 __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
                                                               const bf16* __restrict__ w, const float* __restrict__ bias,
@@ -498,12 +501,19 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
   __shared__ __attribute__((aligned(16))) bf16 sw[9 * H3_BN * H3_LD];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
-  const int n = blockIdx.y;
-  const int ty = blockIdx.x / tiles_x, tx = blockIdx.x - ty * tiles_x;
+  // 1-D grid (h3_grid): the ncob co blocks of a (image, tile) run back to back on ONE XCD (linear id mod 8), so
+  // its input halo is fetched into that XCD's L2 once (co-block-slowest order re-read every halo ncob times)
+  const int ntile = tiles_x * ((g.Ho + TH - 1) / TH), ncob = g.Cout / H3_BN;
+  const int L = blockIdx.x, jx = L >> 3;
+  const int cb = H3_XCD ? jx % ncob : L / (gridDim.x / ncob);
+  const int tflat = H3_XCD ? (jx / ncob) * 8 + (L & 7) : L % (gridDim.x / ncob);
+  if (tflat >= g.Nb * ntile) return;  // padded items (whole block)
+  const int n = tflat / ntile, tt = tflat - n * ntile;
+  const int ty = tt / tiles_x, tx = tt - ty * tiles_x;
   const int y0 = ty * TH, x0 = tx * TW;
   constexpr int HWd = TW + 2;
   const int HP = (TH + 2) * HWd;
-  const int n0 = blockIdx.z * H3_BN;
+  const int n0 = cb * H3_BN;
   const int Cin = g.C1 + g.C2;
   const int nchunk = Cin / 32;
 
@@ -731,8 +741,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
   }
   if (gnp) {
     const int b = n / gn_fimg, f = n - b * gn_fimg;
-    const int64_t nslot = (int64_t)gn_fimg * gridDim.x * 2;
-    const int64_t slot = ((int64_t)f * gridDim.x + blockIdx.x) * 2 + wc;
+    const int64_t nslot = (int64_t)gn_fimg * ntile * 2;
+    const int64_t slot = ((int64_t)f * ntile + tt) * 2 + wc;
     float2* dst = reinterpret_cast<float2*>(gnp) + ((int64_t)b * nslot + slot) * (g.Cout / 4) + (n0 + wr * 32) / 4 + lg;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -3885,7 +3895,7 @@ int conv_fwd_launch(int dtype, const void* x1, const void* x2, const void* wp, c
     case CFV_HALO36:
     case CFV_HALO32: {
       const int tx = (int)cdiv(Wo, TW), ty = (int)cdiv(Ho, TH);
-      dim3 g3(tx * ty, Nb, Cout / H3_BN);
+      const unsigned g3 = (unsigned)(Cout / H3_BN) * 8u * (unsigned)cdiv((int64_t)tx * ty * Nb, 8);
       if (pl.v == CFV_HALO36)
         conv3x3_bf16_kernel<36><<<g3, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, TH, gnp,
                                                          gn_fimg);

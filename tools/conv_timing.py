@@ -34,7 +34,7 @@ def key_fwd(x1, x2, wp, bias, geom, **k):
     return d, 2.0 * x1.shape[0] * Ho * Wo * Cout * cin * taps
 
 
-def key_wg(x1, x2, dy1, dy2, dw, geom, swap, flip, accumulate=True):
+def key_wg(x1, x2, dy1, dy2, dw, geom, swap, flip, accumulate=True, **k):
     Ho, Wo, Cout, KH, KW, St, Pd, U = geom
     cin = x1.shape[3] + (0 if x2 is None else x2.shape[3])
     taps = KH * KW if U == 1 else KH * KW // (U * U)
@@ -42,10 +42,15 @@ def key_wg(x1, x2, dy1, dy2, dw, geom, swap, flip, accumulate=True):
     return d, 2.0 * x1.shape[0] * Ho * Wo * Cout * cin * taps
 
 
+def key_fwd_gn(x1, x2, wp, bias, geom, B, nslot, **k):
+    return key_fwd(x1, x2, wp, bias, geom)
+
+
 def main():
     K.conv_fwd = wrap("fwd", K.conv_fwd, key_fwd)
+    K.conv_fwd_gn = wrap("fwdgn", K.conv_fwd_gn, key_fwd_gn)
     K.conv_wgrad = wrap("wgrad", K.conv_wgrad, key_wg)
-    sys.argv = ["bench.py", "--steps", "1", "--warmup", "2", "--no-cpu-baseline"] + sys.argv[1:]
+    sys.argv = ["bench.py", "--steps", "1", "--warmup", "2", "--no-cpu-baseline", "--other-configs", ""] + sys.argv[1:]
     import cesm_emulator_amd.train as T
     ts = T.train_step
     calls = [0]
