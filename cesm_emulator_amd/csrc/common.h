@@ -195,9 +195,11 @@ __device__ __forceinline__ s16x4 tr4(const bf16* tile, int ld, int r0, int c0, i
 // 16), and in every row the two 16-B chunks swap when bit 2 of the row is set (SW = 1) or bit 2 ^ bit 3 (SW = 2).
 // The access sites of these kernels -- 16-B fragment reads of 16 rows (ds_read_b128), 8-B transposed / k-slot
 // reads of 8 consecutive rows (ds_read_b64_tr_b16), 8-B per-row reads of 16 rows (ds_read_b64) and 8-B column
-// stores of 16 rows (ds_write_b64) -- are then bank-conflict free, except the stores, which are 2-way, the minimum
-// for one 8-B column of 16 rows (SW = 1 for rows read from multiple-of-4 bases, SW = 2 where 16-row 8-B reads
-// occur; tools/lds_banks.py enumerates every site).  Column constants (the head dim half, the q/k/v kind) only
+// stores of 16 rows (ds_write_b64) -- are then bank-conflict free, except the stores, which are 2-way (SW = 1 for
+// rows read from multiple-of-4 bases, SW = 2 where 16-row 8-B reads occur; tools/lds_banks.py enumerates every
+// site, tools/lds_probe.hip measures them: SQ_LDS_BANK_CONFLICT 0 on the reads, 50 % of the store cycles).  A
+// conflict-free store needs the 8-B slot XORed with (r >> 2) & 3, which splits the 16-B read pairs of odd row
+// groups and is not XOR-separable for reads at 4-aligned row bases: measured free stores, not adopted (§6b).  Column constants (the head dim half, the q/k/v kind) only
 // select a region -- an immediate offset -- so every site needs one per-lane offset register, which the
 // register-bound backward kernels depend on (an XOR-swizzled 64-B row needs one per column constant).
 // Round 2's padded rows (80 / 144 / 272 B) were 2-way on the fragment and transposed reads: 42-49 % of the LDS
