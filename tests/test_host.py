@@ -133,16 +133,16 @@ def test_flop_count_reconciles_with_survey():
 # ------------------------------------------------------------------ kernel dispatch (host-only queries)
 def test_gn_epilogue_slot_counts():
     """GroupNorm partial slots the Block convs write from their epilogue (cesm_conv_gn_nslot, host only):
-    conv3x3p per (frame, 14x32 tile, wave), the halo conv per (frame, tile, pixel half); 0 where the kernel
+    conv3x3p per (frame, 14x32 tile, wave), the halo conv per (frame, tile, wave = 64-pixel quarter); 0 where the kernel
     has no partials (fp32 generic conv, 1x1, B not dividing the batch) -> the separate statistics pass"""
     from cesm_emulator_amd import kernels as K
     bf = torch.bfloat16
     g3 = lambda H, W, C: (H, W, C, 3, 3, 1, 1, 1)  # noqa: E731
     x = torch.empty(96, 192, 288, 64, dtype=bf)
     assert K.conv_gn_nslot(x, None, g3(192, 288, 64), 8) == 12 * (14 * 9) * 4
-    assert K.conv_gn_nslot(x, x, g3(192, 288, 64), 8) == 12 * (24 * 9) * 2
+    assert K.conv_gn_nslot(x, x, g3(192, 288, 64), 8) == 12 * (24 * 9) * 4
     x1 = torch.empty(96, 96, 144, 128, dtype=bf)
-    assert K.conv_gn_nslot(x1, None, g3(96, 144, 128), 8) == 12 * (12 * 5) * 2
+    assert K.conv_gn_nslot(x1, None, g3(96, 144, 128), 8) == 12 * (12 * 5) * 4
     assert K.conv_gn_nslot(x1, None, g3(96, 144, 128), 7) == 0
     assert K.conv_gn_nslot(x1.float(), None, g3(96, 144, 128), 8) == 0
     assert K.conv_gn_nslot(x1, None, (96, 144, 128, 1, 1, 1, 0, 1), 8) == 0
