@@ -487,6 +487,9 @@ __device__ __forceinline__ int h3_off(int row, int ch) { return row * H3_LD + ((
 #ifndef H3_PIPE
 #define H3_PIPE 1  // conv3x3_bf16_kernel: software-pipelined tap fragments (0: the compiler's read -> MFMA order)
 #endif
+#ifndef H3_SQ
+#define H3_SQ 1  // A/B knob: 64 co x 64 px wave tiles (0 = 32 co x 128 px, round 2)
+#endif
 #ifndef H3_XCD
 #define H3_XCD 1  // A/B knob: XCD-grouped co blocks of a halo tile (0 = co-block-slowest order)
 #endif
@@ -500,7 +503,11 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
   __shared__ __attribute__((aligned(16))) bf16 sh[H3_NROW * H3_LD];
   __shared__ __attribute__((aligned(16))) bf16 sw[9 * H3_BN * H3_LD];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 1, wc = wid & 1;
+  // wave tile: H3_SQ (round 3) 64 co x 64 px = 4 x 4 MFMA tiles per wave (8 fragment reads per 16 MFMAs per tap);
+  // else 32 co x 128 px = 2 x 8 (10 reads per 16 MFMAs: the 4 waves' reads exceeded the LDS array's 256 B/clk)
+  constexpr int NI = H3_SQ ? 4 : 2, NJ = H3_SQ ? 4 : 8;
+  const int wr = H3_SQ ? 0 : wid >> 1, wc = H3_SQ ? wid : wid & 1;
+  constexpr int PXW = 16 * NJ;  // pixels per wave
   // 1-D grid (h3_grid): the ncob co blocks of a (image, tile) run back to back on ONE XCD (linear id mod 8), so
   // its input halo is fetched into that XCD's L2 once (co-block-slowest order re-read every halo ncob times)
   const int ntile = tiles_x * ((g.Ho + TH - 1) / TH), ncob = g.Cout / H3_BN;
@@ -603,23 +610,23 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
   };
 #endif
 
-  f32x4 acc[2][8];
+  f32x4 acc[NI][NJ];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < NI; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int lr = lane & 15, lg = lane >> 4;
-  // pixel group j of this wave: tile pixel p = wc*128 + j*16 + lr -> halo row of tap (0,0)
-  int hoff[8], pyx[8];
+  // pixel group j of this wave: tile pixel p = wc*PXW + j*16 + lr -> halo row of tap (0,0)
+  int hoff[NJ], pyx[NJ];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
+  for (int j = 0; j < NJ; ++j) {
     int py, px;
     if constexpr (TW == 32) {  // rows of two 16-pixel groups: compile-time offsets per j
-      py = wc * 4 + (j >> 1);
+      py = wc * (NJ / 2) + (j >> 1);
       px = (j & 1) * 16 + lr;
     } else {
-      const int p = wc * 128 + j * 16 + lr;
+      const int p = wc * PXW + j * 16 + lr;
       py = p / TW;
       px = p - py * TW;
     }
@@ -629,13 +636,13 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
     pyx[j] = in ? (py << 16) | px : -1;
   }
   // fragment addresses for ky = 0 / tap = 0; the other taps add immediates (swizzle-preserving steps)
-  int boff[8][3], aoff[2];
+  int boff[NJ][3], aoff[NI];
 #pragma unroll
-  for (int j = 0; j < 8; ++j)
+  for (int j = 0; j < NJ; ++j)
 #pragma unroll
     for (int kx = 0; kx < 3; ++kx) boff[j][kx] = h3_off(hoff[j] + kx, lg);
 #pragma unroll
-  for (int i = 0; i < 2; ++i) aoff[i] = h3_off(wr * 32 + i * 16 + lr, lg);
+  for (int i = 0; i < NI; ++i) aoff[i] = h3_off(wr * 32 + i * 16 + lr, lg);
   for (int ch = 0; ch < nchunk; ++ch) {
     if (ch) __syncthreads();  // previous chunk fully consumed
     stage(ch);
@@ -643,13 +650,13 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
 #if H3_PIPE
     // the 10 fragment reads of tap t+1 are issued between the 16 MFMAs of tap t (two register sets), so no
     // MFMA waits on a read issued just before it (the compiler's order was read -> wait -> 2 MFMAs)
-    bf16x8 fa[2][2], fb[2][8];
+    bf16x8 fa[2][NI], fb[2][NJ];
     auto rd = [&](int tap, int b) {
       const int ky = tap / 3, kx = tap - ky * 3;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) fa[b][i] = *reinterpret_cast<const bf16x8*>(sw + aoff[i] + tap * H3_BN * H3_LD);
+      for (int i = 0; i < NI; ++i) fa[b][i] = *reinterpret_cast<const bf16x8*>(sw + aoff[i] + tap * H3_BN * H3_LD);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) fb[b][j] = *reinterpret_cast<const bf16x8*>(sh + boff[j][kx] + ky * H3_P * H3_LD);
+      for (int j = 0; j < NJ; ++j) fb[b][j] = *reinterpret_cast<const bf16x8*>(sh + boff[j][kx] + ky * H3_P * H3_LD);
     };
     rd(0, 0);
 #pragma unroll
@@ -658,17 +665,17 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
       __builtin_amdgcn_sched_barrier(0);
       if (tap + 1 < 9) rd(tap + 1, b ^ 1);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[b][0], fb[b][j], acc[0][j], 0, 0, 0);
-        acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[b][1], fb[b][j], acc[1][j], 0, 0, 0);
-      }
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[b][i], fb[b][j], acc[i][j], 0, 0, 0);
       if (tap + 1 < 9) {
 #pragma unroll
-        for (int q2 = 0; q2 < 10; ++q2) {
+        for (int q2 = 0; q2 < NI + NJ; ++q2) {
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
         }
-        __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, NI * NJ - (NI + NJ), 0);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -676,53 +683,55 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int ky = tap / 3, kx = tap - ky * 3;
-      bf16x8 af[2];
+      bf16x8 af[NI];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < NI; ++i)
         af[i] = *reinterpret_cast<const bf16x8*>(sw + aoff[i] + tap * H3_BN * H3_LD);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(sh + boff[j][kx] + ky * H3_P * H3_LD);
-        acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bfr, acc[0][j], 0, 0, 0);
-        acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bfr, acc[1][j], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < NI; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][j], 0, 0, 0);
       }
     }
 #endif
   }
   // epilogue: lane holds co = n0 + wr*32 + i*16 + 4*lg + r of pixel (py, px)
   const int Co2 = g.Cout - g.Co1;
-  float bv[2][4];
+  float bv[NI][4];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) epi_bias(bias, n0 + wr * 32 + i * 16 + lg * 4, bv[i]);
-  int64_t mj[8];
-  bool okj[8];
+  for (int i = 0; i < NI; ++i) epi_bias(bias, n0 + wr * 32 + i * 16 + lg * 4, bv[i]);
+  int64_t mj[NJ];
+  bool okj[NJ];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
+  for (int j = 0; j < NJ; ++j) {
     const int oy = y0 + (pyx[j] >> 16), ox = x0 + (pyx[j] & 0xffff);
     okj[j] = pyx[j] >= 0 && oy < g.Ho && ox < g.Wo;
     mj[j] = okj[j] ? ((int64_t)n * g.Ho + oy) * g.Wo + ox : 0;
   }
-  bf16x4 rv[8][2];
+  bf16x4 rv[NJ][NI];
   if (res || res2) {  // uniform
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
-      for (int i = 0; i < 2; ++i) rv[j][i] = epi_res(res, res2, mj[j], n0 + wr * 32 + i * 16 + lg * 4, g.Co1, Co2, okj[j]);
+      for (int i = 0; i < NI; ++i) rv[j][i] = epi_res(res, res2, mj[j], n0 + wr * 32 + i * 16 + lg * 4, g.Co1, Co2, okj[j]);
   } else {
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
-      for (int i = 0; i < 2; ++i) rv[j][i] = bf16x4{};
+      for (int i = 0; i < NI; ++i) rv[j][i] = bf16x4{};
   }
   // GroupNorm statistics partials (gnp: the Block conv feeding a GroupNorm): per channel quad (i, lg) the sum
   // and sum of squares of the stored bf16 output over this wave's valid pixels
-  float gsum[2] = {0.f, 0.f}, gsq[2] = {0.f, 0.f};
+  float gsum[NI], gsq[NI];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
+  for (int i = 0; i < NI; ++i) gsum[i] = gsq[i] = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
     if (!okj[j]) continue;
     const int64_t m = mj[j];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NI; ++i) {
       const int co = n0 + wr * 32 + i * 16 + lg * 4;
       float v[4];
 #pragma unroll
@@ -741,11 +750,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
   }
   if (gnp) {
     const int b = n / gn_fimg, f = n - b * gn_fimg;
-    const int64_t nslot = (int64_t)gn_fimg * ntile * 2;
-    const int64_t slot = ((int64_t)f * ntile + tt) * 2 + wc;
+    constexpr int SPT = 4 / (H3_SQ ? 1 : 2);  // GroupNorm slots per tile (= pixel ranges): h3_gn_slots
+    const int64_t nslot = (int64_t)gn_fimg * ntile * SPT;
+    const int64_t slot = ((int64_t)f * ntile + tt) * SPT + wc;
     float2* dst = reinterpret_cast<float2*>(gnp) + ((int64_t)b * nslot + slot) * (g.Cout / 4) + (n0 + wr * 32) / 4 + lg;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NI; ++i) {
       const float a = row16_sum(gsum[i]), q = row16_sum(gsq[i]);
       if (lr == 0) dst[i * 4] = make_float2(a, q);
     }
@@ -3807,7 +3817,7 @@ int64_t conv_gn_nslot(const ConvFwdPlan& pl, int Nb, int Ho, int Wo, int B) {
   const int64_t tiles = (pl.TW > 0 && pl.TH > 0) ? cdiv(Wo, pl.TW) * cdiv(Ho, pl.TH) : 0;
   switch (pl.v) {
     case CFV_P36_RW: case CFV_P36: case CFV_P32_RW: case CFV_P32: return fimg * tiles * 4;
-    case CFV_HALO36: case CFV_HALO32: return fimg * tiles * 2;
+    case CFV_HALO36: case CFV_HALO32: return fimg * tiles * (H3_SQ ? 4 : 2);
     default: return 0;
   }
 }
