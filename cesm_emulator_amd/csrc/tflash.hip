@@ -81,6 +81,33 @@ __device__ __forceinline__ bf16x8 rope8(const bf16x8 v, const float* cs, float s
   return o;
 }
 
+// Buffer-resource addressing of a 16-frame tile (TF_BUF): the tile's base is wave-uniform (SGPRs), a lane's
+// frame row is a 32-bit byte offset lr * HW * rowbytes (< 2^31: checked on the host), and the resource ends
+// after the tile's last valid frame, so loads of frames >= F return zeros and stores to them are dropped --
+// no 64-bit lane address math and no predicate branch per tile (the 64-bit math was ~60 of the forward's
+// ~320 VALU per query tile).
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, int nvalid, int64_t fstride_b, int rowb) {
+  const int64_t n = nvalid > 0 ? (int64_t)(nvalid - 1) * fstride_b + rowb : 0;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)n, 0x00020000);
+}
+__device__ __forceinline__ bf16x8 buf_ld16(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ void buf_rot8(__amdgpu_buffer_rsrc_t r, int off, float* cs) {
+  const f32x4 c0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+  const f32x4 c1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off + 16, 0, 0));
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    cs[i] = c0[i];
+    cs[4 + i] = c1[i];
+  }
+}
+__device__ __forceinline__ void buf_st4b(__amdgpu_buffer_rsrc_t r, int off, const float* v) {
+  bf16x4 a = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, a), r, off, 0, 0);
+}
+
 // 8 head dims 8g..8g+7 of one frame row (16-B load), RoPE-rotated by frame f when rot != null, times `scale`
 __device__ __forceinline__ bf16x8 row_frag(const bf16* p, const float* __restrict__ rot, int f, int g, float scale,
                                            bool ok) {
@@ -179,6 +206,9 @@ __device__ __forceinline__ const float* btab_lane(const float* tab, int lr, int 
 #ifndef TF_VH
 #define TF_VH 2  // forward V staging: key-tile pairs per part (4 = all at F = 128)
 #endif
+#ifndef TF_BUF
+#define TF_BUF 1  // A/B knob: buffer-resource tile addressing in the per-query-tile loop (0 = 64-bit lane math)
+#endif
 #ifndef TF_XCD_MAP
 #define TF_XCD_MAP 1  // A/B knob: 0 = head-major grid (round 2)
 #endif
@@ -211,11 +241,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE)
   if (grp * 4 >= HW) return;  // whole block (padded groups)
   load_btab<NT>(bias, btab, h, F, 1, tid, 256);
   __syncthreads();
-  const int p = grp * 4 + wid;
+  const int p = grp * 4 + __builtin_amdgcn_readfirstlane(wid);  // wave-uniform (buffer bases in SGPRs)
   if (p >= HW) return;
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
   const int64_t row0 = (int64_t)b * F * HW + p;  // voxel of frame f: row0 + f * HW
   bf16* vs = vst[wid];
+  // TF_BUF lane offsets: frame lr of a 16-frame tile
+  const int q_off = (lr * HW * QKV + g * 8) * 2, o_off = (lr * HW * INNER + 4 * g) * 2;
+  const __amdgpu_buffer_rsrc_t rot_rs = tile_rsrc(rot, F, 16 * 2 * 4, 16 * 2 * 4);
+  const int rot_off = (lr * 16 + 4 * g) * 2 * 4;
   // every K' and Q' fragment up front (TF_QPRE): one exposed load latency per wave instead of one per query tile
   bf16x8 kf[NT], qfa[TF_QPRE ? NT : 1];
 #pragma unroll
@@ -253,9 +287,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE)
   for (int qt = 0; qt < NT; ++qt) {
     const int fq = qt * 16 + lr;
     const bool okq = fq < F;
-    const bf16x8 qf = TF_QPRE ? qfa[TF_QPRE ? qt : 0]
-                              : row_frag(qkv + (row0 + (int64_t)(okq ? fq : 0) * HW) * QKV + h * DH + g * 8, rot,
-                                         okq ? fq : 0, g, scale, true);
+    const int nq = F - qt * 16;  // valid frames of this query tile (wave-uniform)
+    bf16x8 qf;
+    if (TF_QPRE) {
+      qf = qfa[TF_QPRE ? qt : 0];
+    } else if (TF_BUF) {
+      const __amdgpu_buffer_rsrc_t qrs =
+          tile_rsrc(qkv + (row0 + (int64_t)qt * 16 * HW) * QKV + h * DH, nq, (int64_t)HW * QKV * 2, DH * 2);
+      float cs[8];
+      buf_rot8(rot_rs, rot_off + qt * 16 * 16 * 2 * 4, cs);
+      qf = rope8(buf_ld16(qrs, q_off), cs, scale);  // frames >= F: zeros
+    } else {
+      qf = row_frag(qkv + (row0 + (int64_t)(okq ? fq : 0) * HW) * QKV + h * DH + g * 8, rot, okq ? fq : 0, g, scale,
+                    true);
+    }
     const float* bq = bl - 16 * qt;
     float sc[2 * NP][4];
     float m = -INFINITY;
@@ -292,7 +337,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE)
 #pragma unroll
       for (int t = 0; t < 2; ++t) ot[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[s][t], pb, ot[t], 0, 0, 0);
     }
-    if (okq) {
+    if (TF_BUF) {  // stores of frames >= F fall outside the resources and are dropped
+      const float inv = __builtin_amdgcn_rcpf(l);
+      const __amdgpu_buffer_rsrc_t ors =
+          tile_rsrc(out + (row0 + (int64_t)qt * 16 * HW) * INNER + h * DH, nq, (int64_t)HW * INNER * 2, DH * 2);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        float o4[4] = {ot[t][0] * inv, ot[t][1] * inv, ot[t][2] * inv, ot[t][3] * inv};
+        buf_st4b(ors, o_off + t * 32, o4);
+      }
+      if (lse) {
+        const __amdgpu_buffer_rsrc_t lrs =
+            tile_rsrc(lse + (((int64_t)b * NH + h) * HW + p) * F + qt * 16, nq, 4, 4);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, mm + log2f(l)), lrs,
+                                              g == 0 ? lr * 4 : 0x7ffffff0, 0, 0);
+      }
+    } else if (okq) {
       const float inv = __builtin_amdgcn_rcpf(l);
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -636,6 +696,7 @@ int cesm_tflash_nblk(int HW) { return std::max(1, std::min(HW, 128)); }
 int cesm_tflash_fwd(const void* qkv, const float* bias, const float* rot, void* out, float* lse, int B, int F, int HW,
                     float scale, hipStream_t stream) {
   if (!cesm_tflash_supported(F) || B < 1 || HW < 1) return CESM_EUNSUPPORTED;
+  if ((int64_t)16 * HW * QKV * 2 >= (1ll << 31)) return CESM_EUNSUPPORTED;  // TF_BUF 32-bit lane offsets
   dim3 grid(tf_grid_x(HW), B);
   const int nt = (F + 15) / 16;
 #define TFF(N) tflash_fwd_kernel<N><<<grid, 256, 0, stream>>>((const bf16*)qkv, bias, rot, (bf16*)out, lse, F, HW, scale)
