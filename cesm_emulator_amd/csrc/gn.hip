@@ -107,28 +107,40 @@ __global__ __launch_bounds__(64) void gn_finalize_kernel(const double* __restric
 }
 
 // stats[b][g] = (mean, rstd) from the producing conv's epilogue partials part[b][slot][C/4] (float2 per channel
-// quad: sum, sum of squares; cesm_conv_fwd_gn): one 256-thread block per (b, g), thread t takes the (slot, quad)
-// pairs t, t + 256, ... of the group in order and accumulates in double, then a fixed-order tree -> reproducible
-__global__ __launch_bounds__(256) void gn_part_finalize_kernel(const float2* __restrict__ part, float* __restrict__ stats,
-                                                               int G, int64_t nslot, int nq, double count, float eps) {
+// quad: sum, sum of squares; cesm_conv_fwd_gn): one GNP_T-thread block per (b, g), thread t takes the (slot, quad)
+// pairs t, t + GNP_T, ... of the group in order and accumulates in double, then a fixed-order tree -> reproducible.
+constexpr int GNP_T = 256;
+__global__ __launch_bounds__(GNP_T) void gn_part_finalize_kernel(const float2* __restrict__ part, float* __restrict__ stats,
+                                                                 int G, int64_t nslot, int nq, double count, float eps) {
   const int i = blockIdx.x;
   const int b = i / G, g = i - b * G;
   const int qpg = nq / G;
   const int64_t n = nslot * qpg;
   const float2* base = part + (int64_t)b * nslot * nq + g * qpg;
   double a = 0.0, q = 0.0;
+  if ((qpg & (qpg - 1)) == 0 && n < (1ll << 31)) {  // uniform: power-of-two quads per group (C / 4G), 32-bit index
+    const int sh = __ffs(qpg) - 1, nn = (int)n;
 #pragma unroll 8
-  for (int64_t e = threadIdx.x; e < n; e += 256) {
-    const int64_t sl = e / qpg;
-    const float2 v = base[sl * nq + (e - sl * qpg)];
-    a += v.x;
-    q += v.y;
+    for (int e = threadIdx.x; e < nn; e += GNP_T) {
+      const int sl = e >> sh;
+      const float2 v = base[(int64_t)sl * nq + (e & (qpg - 1))];
+      a += v.x;
+      q += v.y;
+    }
+  } else {
+#pragma unroll 8
+    for (int64_t e = threadIdx.x; e < n; e += GNP_T) {
+      const int64_t sl = e / qpg;
+      const float2 v = base[sl * nq + (e - sl * qpg)];
+      a += v.x;
+      q += v.y;
+    }
   }
-  __shared__ double red[2][256];
+  __shared__ double red[2][GNP_T];
   red[0][threadIdx.x] = a;
   red[1][threadIdx.x] = q;
   __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
+  for (int w = GNP_T / 2; w > 0; w >>= 1) {
     if ((int)threadIdx.x < w) {
       red[0][threadIdx.x] += red[0][threadIdx.x + w];
       red[1][threadIdx.x] += red[1][threadIdx.x + w];
@@ -138,6 +150,59 @@ __global__ __launch_bounds__(256) void gn_part_finalize_kernel(const float2* __r
   if (threadIdx.x) return;
   const double mean = red[0][0] / count;
   double var = red[1][0] / count - mean * mean;
+  if (var < 0) var = 0;
+  stats[i * 2] = (float)mean;
+  stats[i * 2 + 1] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+// Large sample (F = 120: ~60 k slots) in two stages, because G = 8 blocks per sample each striding over every
+// 128-B slot row for their 16 B left the chip idle (38 us per call): stage 1, grid (S = nslot / 64, B): block j
+// reduces slots [64 j, 64 j + 64) (the last block also the remainder) for ALL channel quads (coalesced rows),
+// fixed-order tree over its row lanes, and writes (sum, sumsq) as doubles over its own first two slot rows (read
+// by nobody else; the partials are scratch); stage 2: per (b, g) the S block sums in order.
+constexpr int GNP_PER = 64;
+__global__ __launch_bounds__(256) void gn_part_stage1_kernel(float2* __restrict__ part, int64_t nslot, int C4, int S) {
+  const int b = blockIdx.y, j = blockIdx.x, tid = threadIdx.x;
+  const int64_t s0 = (int64_t)j * GNP_PER, s1 = j == S - 1 ? nslot : s0 + GNP_PER;
+  const int R = 256 / C4, qd = tid % C4, sr = tid / C4;
+  float2* base = part + (int64_t)b * nslot * C4;
+  double a = 0.0, q = 0.0;
+  for (int64_t sl = s0 + sr; sl < s1; sl += R) {
+    const float2 v = base[sl * C4 + qd];
+    a += v.x;
+    q += v.y;
+  }
+  __shared__ double red[2][256];
+  red[0][tid] = a;
+  red[1][tid] = q;
+  __syncthreads();  // every read of this block's slots is done: its first two rows may be overwritten below
+  for (int w = R >> 1; w > 0; w >>= 1) {
+    if (sr < w) {
+      red[0][tid] += red[0][tid + w * C4];
+      red[1][tid] += red[1][tid + w * C4];
+    }
+    __syncthreads();
+  }
+  if (sr == 0) reinterpret_cast<double2*>(base + s0 * C4)[qd] = make_double2(red[0][tid], red[1][tid]);
+}
+__global__ __launch_bounds__(64) void gn_part_stage2_kernel(const float2* __restrict__ part, float* __restrict__ stats,
+                                                             int G, int64_t nslot, int C4, int S, double count,
+                                                             float eps) {
+  const int i = blockIdx.x, b = i / G, g = i - b * G, qpg = C4 / G;
+  const float2* base = part + (int64_t)b * nslot * C4;
+  double a = 0.0, q = 0.0;
+  for (int j = threadIdx.x; j < S; j += 64) {
+    const double2* r = reinterpret_cast<const double2*>(base + (int64_t)j * GNP_PER * C4) + g * qpg;
+    for (int k = 0; k < qpg; ++k) {
+      a += r[k].x;
+      q += r[k].y;
+    }
+  }
+  a = wave_sum_d(a);
+  q = wave_sum_d(q);
+  if (threadIdx.x) return;
+  const double mean = a / count;
+  double var = q / count - mean * mean;
   if (var < 0) var = 0;
   stats[i * 2] = (float)mean;
   stats[i * 2 + 1] = (float)(1.0 / sqrt(var + (double)eps));
@@ -437,7 +502,16 @@ int cesm_gn_stats(int dtype, const void* y, float* stats, double* ws, int B, int
 int cesm_gn_stats_part(const float* part, float* stats, int B, int64_t nslot, int C, int G, int64_t rows_b, float eps,
                        hipStream_t stream) {
   if (B <= 0 || G <= 0 || C % (4 * G) || nslot <= 0 || rows_b <= 0) return CESM_EINVAL;
-  gn_part_finalize_kernel<<<B * G, 256, 0, stream>>>(reinterpret_cast<const float2*>(part), stats, G, nslot, C / 4,
+  const int C4 = C / 4;
+  if (nslot >= 8192 && C4 <= 256 && 256 % C4 == 0) {
+    const int S = (int)(nslot / GNP_PER);  // >= 64 slots (>= 2 rows) per stage-1 block
+    gn_part_stage1_kernel<<<dim3(S, B), 256, 0, stream>>>(const_cast<float2*>(reinterpret_cast<const float2*>(part)),
+                                                          nslot, C4, S);
+    gn_part_stage2_kernel<<<B * G, 64, 0, stream>>>(reinterpret_cast<const float2*>(part), stats, G, nslot, C4, S,
+                                                    (double)rows_b * (C / G), eps);
+    return cesm_launch_status();
+  }
+  gn_part_finalize_kernel<<<B * G, GNP_T, 0, stream>>>(reinterpret_cast<const float2*>(part), stats, G, nslot, C4,
                                                      (double)rows_b * (C / G), eps);
   return cesm_launch_status();
 }

@@ -108,6 +108,28 @@ def test_conv3x3p_level0_bf16(dev, H, W, with_res):
 
 
 # ------------------------------------------------------------------ GroupNorm statistics from the conv epilogue
+@pytest.mark.parametrize("nslot, C", [(9000, 64), (28805, 128), (6048, 64)])
+def test_gn_stats_part_two_stage(dev, nslot, C):
+    """GroupNorm (mean, rstd) from conv-epilogue partials at the long-window slot counts: nslot >= 8192 takes the
+    two-stage reduction (64-slot blocks over all channel quads, then per group), smaller counts the one-stage
+    kernel; both against float64 sums of the same partials"""
+    torch.manual_seed(11)
+    B, G = 2, 8
+    rows_b = nslot * 7
+    part = torch.randn(B, nslot, C // 4, 2, device=dev) * 3
+    part[..., 1] = part[..., 1].abs() * 40 + 1
+    p64 = part.double().view(B, nslot, G, C // 4 // G, 2)
+    s = p64[..., 0].sum((1, 3))
+    q = p64[..., 1].sum((1, 3))
+    cnt = rows_b * (C // G)
+    mean = s / cnt
+    rstd = 1.0 / torch.sqrt((q / cnt - mean * mean).clamp_min(0) + 1e-5)
+    st = K.gn_stats_part(part.clone(), rows_b, G)
+    assert torch.allclose(st[..., 0].double(), mean, rtol=1e-6, atol=1e-9)
+    assert torch.allclose(st[..., 1].double(), rstd, rtol=1e-6, atol=1e-9)
+    assert torch.equal(st, K.gn_stats_part(part.clone(), rows_b, G))  # fixed order: repeatable
+
+
 @pytest.mark.parametrize("C1,C2,Cout,H,W,B,Fr,kern", [
     (64, 0, 64, 20, 96, 2, 3, "conv3x3p_kernel<32,7,true>"),     # level 0, partial 14-row tile
     (64, 0, 64, 30, 288, 1, 2, "conv3x3p_kernel<32,7,true>"),    # full bench width
