@@ -369,12 +369,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE)
 // the pixel's K' and V rows staged once in LDS for all waves.  Writes dq into dqkv, D_i = dO_i . O_i into dbuf
 // [B][8][HW][F], and per-block dbias-by-offset partials part[(b*8 + h)][blk][2F - 1].  With the query tile
 // fixed per wave, the dbias accumulator of (r, kt) holds one diagonal kt - qt for every pixel: static registers.
-template <int NT>
-__global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(2))) void tflash_bwd_q_kernel(
+// TF_DO (round 3): D_i = dO_i . O_i from the forward's (bf16) output instead of sum_j P_ij dP_ij, so one pass over
+// the key tiles does S, dP -> P, dS -> dbias, dQ with no P / dP arrays in registers (64 VGPRs at NT = 8): the
+// kernel fits 128 VGPRs, i.e. 2 blocks of 8 waves per CU instead of 1 (the pass-1 / pass-2 form was latency
+// bound at 2 waves per SIMD in barrier lockstep).  Only for F > 16 (NT >= 2): with D from O the F = 1 rel-pos
+// bias gradient would be the rounding difference of two 32-term dot products instead of exactly 0.  Measured at
+// F = 120 (tools/tf_ab.sh): 192x288 13.5 -> 14.3 ms (slower: the lost register prefetch), 96x144 +1 %, 48x72 -5 %,
+// 24x36 -17 % -> used below TF_DO_MAXHW pixels.
+#ifndef TF_DO
+#define TF_DO 1
+#endif
+#ifndef TF_DO_MAXHW
+#define TF_DO_MAXHW 8192
+#endif
+template <int NT, bool DOV>
+__global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(DOV ? 4 : 2))) void tflash_bwd_q_kernel(
     const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
     const float* __restrict__ lse, const float* __restrict__ bias, const float* __restrict__ rot,
     bf16* __restrict__ dqkv, float* __restrict__ dbuf, float* __restrict__ part, int F, int HW, float scale) {
   constexpr int NP = (NT + 1) / 2, NR = 32 * NP, NTH = 64 * NT;
+  constexpr bool DO_ = DOV;
   __shared__ __attribute__((aligned(16))) float btab[4 * 32 * NT];
   __shared__ float dacc[2 * 16 * TF_MAXT];
   __shared__ __attribute__((aligned(16))) bf16 ks[NR * TF_LD];
@@ -407,9 +421,14 @@ __global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(2))) vo
   const int sf = tid >> 2, sc = tid & 3;
   const bool sok = sf < F;
   const int sfc = sok ? sf : 0, fqc = okq ? fq : 0;
-  float kcs[8], qcs[8];
-  rot8_load(rot, sfc, sc, kcs);
-  rot8_load(rot, fqc, g, qcs);
+  // TF_DO (two blocks per CU, <= 128 VGPRs): no register prefetch (the co-resident block hides this one's loads,
+  // all issued before the staging barrier), and the RoPE coefficients are re-read per pixel (L1 / L2-resident
+  // table) instead of living in 16 registers
+  float kcs[DO_ ? 1 : 8], qcs[DO_ ? 1 : 8];
+  if (!DO_) {
+    rot8_load(rot, sfc, sc, kcs);
+    rot8_load(rot, fqc, g, qcs);
+  }
   bf16x8 kraw = zero8(), vraw = zero8(), qraw = zero8(), draw = zero8();
   float lraw = 0.f;
   auto fetch = [&](int pp) {
@@ -417,24 +436,92 @@ __global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(2))) vo
     const int64_t rs = (r0 + (int64_t)sfc * HW) * QKV + h * DH + sc * 8;
     kraw = ld16(qkv + rs + INNER);
     vraw = ld16(qkv + rs + 2 * INNER);
-    const int64_t vq = r0 + (int64_t)fqc * HW;
-    qraw = ld16(qkv + vq * QKV + h * DH + g * 8);
-    draw = ld16(dout + vq * INNER + h * DH + g * 8);
-    lraw = lse[(((int64_t)b * NH + h) * HW + pp) * F + fqc];
+    if (!DO_) {
+      const int64_t vq = r0 + (int64_t)fqc * HW;
+      qraw = ld16(qkv + vq * QKV + h * DH + g * 8);
+      draw = ld16(dout + vq * INNER + h * DH + g * 8);
+      lraw = lse[(((int64_t)b * NH + h) * HW + pp) * F + fqc];
+    }
   };
-  if ((int)blockIdx.x < HW) fetch(blockIdx.x);
+  if (!DO_ && (int)blockIdx.x < HW) fetch(blockIdx.x);
 
   for (int p = blockIdx.x; p < HW; p += gridDim.x) {
     const int64_t row0 = (int64_t)b * F * HW + p;
     __syncthreads();  // previous pixel's rows consumed
-    *reinterpret_cast<bf16x8*>(ks + sf * TF_LD + sc * 8) = sok ? rope8(kraw, kcs, 1.f) : zero8();
-    *reinterpret_cast<bf16x8*>(vs + sf * TF_LD + sc * 8) = sok ? vraw : zero8();
-    // padded query rows: finite clamped data, P = 0 through Li (so D = dS = 0 there)
-    const bf16x8 qf = rope8(qraw, qcs, scale);
-    const bf16x8 dof = draw;
-    const float Li = okq ? lraw : TF_LSE_PAD;
-    if (p + (int)gridDim.x < HW) fetch(p + gridDim.x);
+    bf16x8 qf, dof;
+    float Li, Do = 0.f;
+    if (DO_) {
+      fetch(p);  // K / V rows of this pixel (the co-resident block hides the latency)
+      float cs[8];
+      rot8_load(rot, sfc, sc, cs);
+      *reinterpret_cast<bf16x8*>(ks + sf * TF_LD + sc * 8) = sok ? rope8(kraw, cs, 1.f) : zero8();
+      *reinterpret_cast<bf16x8*>(vs + sf * TF_LD + sc * 8) = sok ? vraw : zero8();
+      const int64_t vq = row0 + (int64_t)fqc * HW;
+      const bf16x8 qr = ld16(qkv + vq * QKV + h * DH + g * 8);
+      dof = ld16(dout + vq * INNER + h * DH + g * 8);
+      const bf16x8 orw = ld16(o + vq * INNER + h * DH + g * 8);
+      const float lr_ = lse[(((int64_t)b * NH + h) * HW + p) * F + fqc];
+      rot8_load(rot, fqc, g, cs);
+      qf = rope8(qr, cs, scale);
+      Li = okq ? lr_ : TF_LSE_PAD;  // padded query rows: P = 0 (so dS = 0 there)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) Do = fmaf((float)dof[e], (float)orw[e], Do);
+    } else {
+      *reinterpret_cast<bf16x8*>(ks + sf * TF_LD + sc * 8) = sok ? rope8(kraw, kcs, 1.f) : zero8();
+      *reinterpret_cast<bf16x8*>(vs + sf * TF_LD + sc * 8) = sok ? vraw : zero8();
+      // padded query rows: finite clamped data, P = 0 through Li (so D = dS = 0 there)
+      qf = rope8(qraw, qcs, scale);
+      dof = draw;
+      Li = okq ? lraw : TF_LSE_PAD;
+    }
+    if (!DO_ && p + (int)gridDim.x < HW) fetch(p + gridDim.x);
     __syncthreads();  // rows staged
+    if (DO_) {
+      const float D = grp4_sum(Do);
+      if (okq && g == 0) dbuf[(((int64_t)b * NH + h) * HW + p) * F + fq] = D;
+      // one pass: S'^T, dP^T -> P^T, dS^T = P^T (dP^T - D) -> dbias, dQ'^T = K'^T dS^T
+      f32x4 dqt[2] = {z4, z4};
+#pragma unroll
+      for (int s = 0; s < NP; ++s) {
+        float dsv[2][4];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int kt = 2 * s + u;
+          if (kt < NT) {
+            const bf16x8 kf = ld16(ks + (kt * 16 + lr) * TF_LD + g * 8);
+            const bf16x8 vf = ld16(vs + (kt * 16 + lr) * TF_LD + g * 8);
+            const f32x4 st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf, z4, 0, 0, 0);   // S'^T
+            const f32x4 dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, dof, z4, 0, 0, 0);  // dP^T
+            const f32x4 bo = *reinterpret_cast<const f32x4*>(bq + 16 * kt);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float pp = __builtin_amdgcn_exp2f(fmaf(st[r], LOG2E, bo[r]) - Li);
+              if (kt == NT - 1) pp = kok[r] ? pp : 0.f;
+              const float ds = pp * (dp[r] - D);
+              dsv[u][r] = ds;
+              dba[r][kt < NT ? kt : 0] += ds;
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dsv[u][r] = 0.f;
+          }
+        }
+        const bf16x8 db = pack_kslot(dsv[0], dsv[1]);
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          dqt[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_pair(ks, s, t * 16, lane), db, dqt[t], 0, 0, 0);
+      }
+      if (okq) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int d0 = t * 16 + 4 * g;
+          float v4[4] = {dqt[t][0], dqt[t][1], dqt[t][2], dqt[t][3]};
+          rope4_inv(v4, rot, fq, d0, scale);  // dq = scale R^T dQ'
+          store4b(dqkv + (row0 + (int64_t)fq * HW) * QKV + h * DH + d0, v4);
+        }
+      }
+      continue;
+    }
     // pass 1: P^T and dP^T of every key tile, D_i = sum_j P_ij dP_ij (exact: at F = 1 the bias gradient is 0)
     float pt[NT][4], dpt[NT][4];
     float D = 0.f;
@@ -725,9 +812,14 @@ int cesm_tflash_bwd(const void* qkv, const void* o, const void* dout, const floa
   const int nt = (F + 15) / 16;
   const int nblk = cesm_tflash_nblk(HW);
   dim3 gq(nblk, B * NH), gk(tf_grid_x(HW), B);
+  const bool dov = TF_DO && nt >= 2 && HW < TF_DO_MAXHW;
 #define TFB(N)                                                                                                         \
-  tflash_bwd_q_kernel<N><<<gq, 64 * N, 0, stream>>>((const bf16*)qkv, (const bf16*)o, (const bf16*)dout, lse, bias, rot, \
-                                                 (bf16*)dqkv, dbuf, part, F, HW, scale);                               \
+  if (dov && N >= 2)                                                                                                   \
+    tflash_bwd_q_kernel<N, (N >= 2)><<<gq, 64 * N, 0, stream>>>((const bf16*)qkv, (const bf16*)o, (const bf16*)dout,   \
+                                                                lse, bias, rot, (bf16*)dqkv, dbuf, part, F, HW, scale); \
+  else                                                                                                                 \
+    tflash_bwd_q_kernel<N, false><<<gq, 64 * N, 0, stream>>>((const bf16*)qkv, (const bf16*)o, (const bf16*)dout, lse, \
+                                                             bias, rot, (bf16*)dqkv, dbuf, part, F, HW, scale);       \
   tflash_bwd_kv_kernel<N><<<gk, 256, 0, stream>>>((const bf16*)qkv, (const bf16*)dout, lse, dbuf, bias, rot,           \
                                                   (bf16*)dqkv, F, HW, scale)
   switch (nt) {
