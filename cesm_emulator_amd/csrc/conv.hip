@@ -493,19 +493,28 @@ __device__ __forceinline__ int h3_off(int row, int ch) { return row * H3_LD + ((
 #ifndef H3_XCD
 #define H3_XCD 1  // A/B knob: XCD-grouped co blocks of a halo tile (0 = co-block-slowest order)
 #endif
-template <int TW>
+#ifndef H3_BIG
+#define H3_BIG 1  // A/B knob: 448-pixel tiles with 64 co x 112 px wave tiles (0 = 256-pixel tiles, 64 x 64)
+#endif
+template <int TW, int NJv = 4>
 __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
                                                               const bf16* __restrict__ w, const float* __restrict__ bias,
                                                               const bf16* __restrict__ res, const bf16* __restrict__ res2,
                                                               bf16* __restrict__ y1, bf16* __restrict__ y2, ConvGeom g,
                                                               int tiles_x, int TH, float* __restrict__ gnp = nullptr,
                                                               int gn_fimg = 1) {
-  __shared__ __attribute__((aligned(16))) bf16 sh[H3_NROW * H3_LD];
+  // NJv = 7 (H3_BIG): tiles of up to 448 pixels ((TH+2) <= 16 halo rows of H3_P), 64 co x 112 px per wave: 11
+  // fragment reads per 28 MFMAs per tap (0.39 per MFMA instead of 0.5) and the 36-KiB weight chunk staged once
+  // per 448 instead of 256 pixels; 77 KiB of LDS, still 2 blocks per CU
+  static_assert(NJv == 4 || (NJv == 7 && H3_SQ && H3_DMA), "big tiles need square wave tiles and DMA staging");
+  constexpr int NROWS = (NJv == 7 ? 16 : 10) * H3_P;
+  __shared__ __attribute__((aligned(16))) bf16 sh[NROWS * H3_LD];
   __shared__ __attribute__((aligned(16))) bf16 sw[9 * H3_BN * H3_LD];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  // wave tile: H3_SQ (round 3) 64 co x 64 px = 4 x 4 MFMA tiles per wave (8 fragment reads per 16 MFMAs per tap);
-  // else 32 co x 128 px = 2 x 8 (10 reads per 16 MFMAs: the 4 waves' reads exceeded the LDS array's 256 B/clk)
-  constexpr int NI = H3_SQ ? 4 : 2, NJ = H3_SQ ? 4 : 8;
+  // wave tile: H3_SQ (round 3) 64 co x 16 NJv px = 4 x NJv MFMA tiles per wave (8 fragment reads per 16 MFMAs per
+  // tap at NJv = 4); else 32 co x 128 px = 2 x 8 (10 reads per 16 MFMAs: the 4 waves' reads exceeded the LDS
+  // array's 256 B/clk)
+  constexpr int NI = H3_SQ ? 4 : 2, NJ = H3_SQ ? NJv : 8;
   const int wr = H3_SQ ? 0 : wid >> 1, wc = H3_SQ ? wid : wid & 1;
   constexpr int PXW = 16 * NJ;  // pixels per wave
   // 1-D grid (h3_grid): the ncob co blocks of a (image, tile) run back to back on ONE XCD (linear id mod 8), so
@@ -540,11 +549,14 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
     const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(w + (int64_t)n0 * 9 * Cin + c0), (short)0, H3_BN * 9 * Cin * 2 - c0 * 2, 0x00020000);
     const int prow = lane >> 2, pslot = lane & 3;
-    constexpr int HPC = H3_NROW / 16;  // halo pieces (25)
+    constexpr int HPC = NROWS / 16;  // halo pieces (25 / 40)
+    // NJv = 7: only the pieces the tile's halo rows span (pixels past the tile read row 0);
+    // NJv = 4 at TW = 32 reads rows up to 9 for pixels past a short tile (discarded), so all 25 are staged
+    const int hpc = NJv == 4 ? HPC : ((TH + 2) * H3_P + 15) >> 4;
 #pragma unroll
     for (int k = 0; k < (HPC + 3) / 4; ++k) {
       const int q = wid + 4 * k;
-      if (q < HPC) {  // wave-uniform
+      if (q < hpc) {  // wave-uniform
         const int row = 16 * q + prow;
         const int r = row / H3_P, col = row - r * H3_P;
         const int iy = y0 - 1 + r, ix = x0 - 1 + col;
@@ -622,7 +634,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     int py, px;
-    if constexpr (TW == 32) {  // rows of two 16-pixel groups: compile-time offsets per j
+    if constexpr (TW == 32 && NJ % 2 == 0) {  // rows of two 16-pixel groups: compile-time offsets per j
       py = wc * (NJ / 2) + (j >> 1);
       px = (j & 1) * 16 + lr;
     } else {
@@ -632,7 +644,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
     }
     const bool in = py < TH;
     // TW == 32: rows past TH stay inside the LDS halo buffer (results discarded), no select needed
-    hoff[j] = (TW == 32 || in) ? py * H3_P + px : 0;
+    hoff[j] = ((TW == 32 && NJ % 2 == 0) || in) ? py * H3_P + px : 0;
     pyx[j] = in ? (py << 16) | px : -1;
   }
   // fragment addresses for ky = 0 / tap = 0; the other taps add immediates (swizzle-preserving steps)
@@ -1649,6 +1661,9 @@ constexpr int G1_BM = 128;
 #ifndef G1_NS1
 #define G1_NS1 1   // A/B knob: single-stage K = 64 variant (0 = always two stages)
 #endif
+#ifndef G1_NT
+#define G1_NT 0    // A/B knob: non-temporal output stores
+#endif
 #ifndef G1_XCD
 #define G1_XCD 1   // A/B knob: XCD-grouped co blocks (0 = co-block-fastest linear order)
 #endif
@@ -1788,7 +1803,8 @@ __global__ __launch_bounds__(256, NS == 1 ? 4 : 2) void gemm1x1_kernel(const bf1
 #pragma unroll
       for (int q = 0; q < 8; ++q) v[q] = (bf16)((float)v[q] + (float)rv[it][q]);
     }
-    *reinterpret_cast<bf16x8*>(dst) = v;
+    if (G1_NT) stnt16(dst, v);
+    else *reinterpret_cast<bf16x8*>(dst) = v;
   }
 }
 
@@ -1998,6 +2014,21 @@ static void c2_tile(int Ho, int Wo, int& TH, int& TW, bool only_32_36 = false) {
       const double util = (double)Ho * Wo / ((double)ntile * 256);
       // a non-32 width must buy > 10 % utilisation (32-wide tiles align with the fragment rows)
       const double u = tw == 32 ? util + 0.10 : util;
+      if (u > best + 1e-9 || (u > best - 1e-9 && ntile < bt)) { best = u; bt = ntile; TH = th; TW = tw; }
+    }
+  }
+}
+
+// halo-conv tile for the 448-pixel blocks (conv3x3_bf16_kernel<TW, 7>): TW in {32, 36}, TH*TW <= 448,
+// TH + 2 <= 16 halo rows; the most useful / computed pixels, a 32-wide tile needs > 5 % better utilisation
+static void h3_big_tile(int Ho, int Wo, int& TH, int& TW) {
+  double best = -1.0;
+  int bt = 1 << 30;
+  for (int tw : {36, 32}) {
+    for (int th = 1; th * tw <= 448 && th + 2 <= 16; ++th) {
+      const int ntile = (int)(cdiv(Ho, th) * cdiv(Wo, tw));
+      const double util = (double)Ho * Wo / ((double)ntile * 448);
+      const double u = tw == 32 ? util - 0.05 : util;
       if (u > best + 1e-9 || (u > best - 1e-9 && ntile < bt)) { best = u; bt = ntile; TH = th; TW = tw; }
     }
   }
@@ -3770,7 +3801,10 @@ static ConvFwdPlan conv_fwd_plan(int dtype, int Nb, int Hi, int Wi, int C1, int 
     pl.v = CFV_V2;
   } else if (halo3) {
     pl.TH = H3_TH; pl.TW = H3_TW;
-    if (!getenv_flag("CESM_CONV3X3_FIXED_TILE")) c2_tile(Ho, Wo, pl.TH, pl.TW, true);
+    if (!getenv_flag("CESM_CONV3X3_FIXED_TILE")) {
+      if (H3_BIG && H3_SQ && H3_DMA) h3_big_tile(Ho, Wo, pl.TH, pl.TW);
+      else c2_tile(Ho, Wo, pl.TH, pl.TW, true);
+    }
     pl.v = pl.TW == 36 ? CFV_HALO36 : CFV_HALO32;
   } else if (dtype == CESM_DT_BF16 && KH == 4 && KW == 4 && C2 == 0 && Co1 == Cout && (Cout % H3_BN) == 0 &&
              !getenv_flag("CESM_NO_S2HALO") &&
@@ -3906,12 +3940,12 @@ int conv_fwd_launch(int dtype, const void* x1, const void* x2, const void* wp, c
     case CFV_HALO32: {
       const int tx = (int)cdiv(Wo, TW), ty = (int)cdiv(Ho, TH);
       const unsigned g3 = (unsigned)(Cout / H3_BN) * 8u * (unsigned)cdiv((int64_t)tx * ty * Nb, 8);
-      if (pl.v == CFV_HALO36)
-        conv3x3_bf16_kernel<36><<<g3, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, TH, gnp,
-                                                         gn_fimg);
-      else
-        conv3x3_bf16_kernel<32><<<g3, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, TH, gnp,
-                                                         gn_fimg);
+      const bool big = TH * TW > 256;  // h3_tile chose a 448-pixel tile (H3_BIG)
+#define H3L(TWv, NJv)                                                                                                \
+  conv3x3_bf16_kernel<TWv, NJv><<<g3, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, TH, gnp, gn_fimg)
+      if (pl.v == CFV_HALO36) { if (big) H3L(36, 7); else H3L(36, 4); }
+      else { if (big) H3L(32, 7); else H3L(32, 4); }
+#undef H3L
       break;
     }
     case CFV_S2DOWN36:

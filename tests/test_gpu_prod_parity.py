@@ -134,8 +134,9 @@ def test_gn_stats_part_two_stage(dev, nslot, C):
     (64, 0, 64, 20, 96, 2, 3, "conv3x3p_kernel<32,7,true>"),     # level 0, partial 14-row tile
     (64, 0, 64, 30, 288, 1, 2, "conv3x3p_kernel<32,7,true>"),    # full bench width
     (64, 0, 64, 18, 72, 2, 2, "conv3x3_bf16_kernel<36>"),        # 8 channels per group, 36-wide tiles
-    (64, 64, 64, 20, 96, 2, 2, "conv3x3_bf16_kernel<32>"),       # decoder concat input
-    (128, 0, 128, 24, 144, 2, 2, "conv3x3_bf16_kernel<32>"),     # level 1 (16 channels per group)
+    (64, 64, 64, 28, 64, 2, 2, "conv3x3_bf16_kernel<32>"),       # decoder concat input, 32-wide 14-row tiles
+    (128, 0, 128, 24, 144, 2, 2, "conv3x3_bf16_kernel<36>"),     # level 1 (16 channels per group)
+    (64, 64, 64, 20, 96, 2, 2, "conv3x3_bf16_kernel<36>"),       # concat, partial tiles in both directions
     (256, 128, 128, 12, 72, 1, 3, "conv3x3_bf16_kernel<36>"),    # concat, Cin != Cout
     (256, 0, 256, 12, 72, 2, 2, "conv3x3_bf16_kernel<36>"),      # level 2 (32 per group)
     (512, 0, 512, 6, 36, 2, 2, "conv3x3_bf16_kernel<36>"),       # level 3 (64 per group: both co halves)

@@ -140,9 +140,9 @@ def test_gn_epilogue_slot_counts():
     g3 = lambda H, W, C: (H, W, C, 3, 3, 1, 1, 1)  # noqa: E731
     x = torch.empty(96, 192, 288, 64, dtype=bf)
     assert K.conv_gn_nslot(x, None, g3(192, 288, 64), 8) == 12 * (14 * 9) * 4
-    assert K.conv_gn_nslot(x, x, g3(192, 288, 64), 8) == 12 * (24 * 9) * 4
+    assert K.conv_gn_nslot(x, x, g3(192, 288, 64), 8) == 12 * (16 * 8) * 4  # 12 x 36 tiles (448-px blocks)
     x1 = torch.empty(96, 96, 144, 128, dtype=bf)
-    assert K.conv_gn_nslot(x1, None, g3(96, 144, 128), 8) == 12 * (12 * 5) * 4
+    assert K.conv_gn_nslot(x1, None, g3(96, 144, 128), 8) == 12 * (8 * 4) * 4
     assert K.conv_gn_nslot(x1, None, g3(96, 144, 128), 7) == 0
     assert K.conv_gn_nslot(x1.float(), None, g3(96, 144, 128), 8) == 0
     assert K.conv_gn_nslot(x1, None, (96, 144, 128, 1, 1, 1, 0, 1), 8) == 0
@@ -160,9 +160,9 @@ def test_bench_shape_dispatch_table():
     assert fv(192, 288, 64, 0, 192, 288, 64, 64, 3, 3, 1, 1, 1) == "conv3x3p_kernel<32,7,true>"
     assert wv(192, 288, 64, 0, 192, 288, 64, 64, 3, 3, 1, 1, 1) == "wgrad3x3c64_kernel"
     # level-0 concat inputs (up path / out_conv: 64 + 64 -> 64)
-    assert fv(192, 288, 64, 64, 192, 288, 64, 64, 3, 3, 1, 1, 1) == "conv3x3_bf16_kernel<32>"
+    assert fv(192, 288, 64, 64, 192, 288, 64, 64, 3, 3, 1, 1, 1) == "conv3x3_bf16_kernel<36>"
     # levels 1-3 (144, 72, 36 wide)
-    assert fv(96, 144, 128, 0, 96, 144, 128, 128, 3, 3, 1, 1, 1) == "conv3x3_bf16_kernel<32>"
+    assert fv(96, 144, 128, 0, 96, 144, 128, 128, 3, 3, 1, 1, 1) == "conv3x3_bf16_kernel<36>"
     assert fv(48, 72, 256, 0, 48, 72, 256, 256, 3, 3, 1, 1, 1) == "conv3x3_bf16_kernel<36>"
     assert fv(24, 36, 512, 0, 24, 36, 512, 512, 3, 3, 1, 1, 1) == "conv3x3_bf16_kernel<36>"
     assert wv(24, 36, 512, 0, 24, 36, 512, 512, 3, 3, 1, 1, 1) == "wgrad3x3w36c64_kernel"

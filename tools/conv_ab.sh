@@ -7,8 +7,9 @@ root=${GRAFT_REPO_ROOT:-$(pwd)}
 cd /tmp && export TMPDIR=/tmp
 cd "$root"
 mkdir -p gpurun_out
-timeout -k 10 300 python3 -u -m pytest tests -m gpu -x -q -k "conv or gemm or gn" --timeout 120 --timeout-method thread > gpurun_out/${tag}_conv_pytest.log 2>&1
-tail -2 gpurun_out/${tag}_conv_pytest.log
+[ -z "$SKIP_TESTS" ] && timeout -k 10 300 python3 -u -m pytest tests -m gpu -x -q -k "conv or gemm or gn" --timeout 120 --timeout-method thread > gpurun_out/${tag}_conv_pytest.log 2>&1
+true
+tail -2 gpurun_out/${tag}_conv_pytest.log 2>/dev/null || true
 out=gpurun_out/${tag}_conv.txt
 : > $out
 for rep in 1 2; do
