@@ -2554,14 +2554,22 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_bf16_kernel(const bf16* __res
 // input halo is kept as two 32-channel planes so the fragment reads are the 64-ci kernel's.
 constexpr int W3_PLANE = (W3_TH + 2) * W3_P * 32;  // halo plane (bf16 elements)
 
-__global__ __launch_bounds__(512, 1) void wgrad3x3c64_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
+// WG4 (round 3): 4 waves (one per SIMD, 512 registers), wave = one 16-channel ci tile x ALL four co tiles x 9
+// taps (144 accumulators): 26 transposed fragment reads per 36 MFMAs per pixel row instead of 22 per 18 (the
+// 8-wave form read 0.61 KiB of LDS per MFMA, past what the LDS array serves at the MFMA rate)
+#ifndef WG4
+#define WG4 0  // measured neutral (63.69 vs 63.58 ms conv total): the wgrads lose latency hiding at 1 wave/SIMD
+#endif
+constexpr int WG_NT = WG4 ? 256 : 512;  // threads per block
+constexpr int WG_NI = WG4 ? 4 : 2;      // co tiles per wave
+__global__ __launch_bounds__(WG_NT, 1) void wgrad3x3c64_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
                                                              const bf16* __restrict__ dy1, const bf16* __restrict__ dy2,
                                                              float* __restrict__ slab, ConvGeom g, int tiles_x,
                                                              int ntiles) {
   __shared__ __attribute__((aligned(16))) bf16 sdy[W3_TH * W3_TW * 64];  // 32 KB, 128-B rows
   __shared__ __attribute__((aligned(16))) bf16 shx[2 * W3_PLANE];        // 2 x 30 KB, 64-B rows
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int cot0 = (wid >> 2) * 2, cit = wid & 3;
+  const int cot0 = WG4 ? 0 : (wid >> 2) * 2, cit = wid & 3;
   const int co0 = blockIdx.x * 64, ci0 = blockIdx.y * 64;
   const int Cin = g.C1 + g.C2;
   const bf16* xs; int xcs, xcc;
@@ -2571,34 +2579,35 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3c64_kernel(const bf16* __restr
   if (co0 < g.Co1) { ys = dy1; ycs = g.Co1; ycc = co0; } else { ys = dy2; ycs = Co2; ycc = co0 - g.Co1; }
   const int tiles_per_img = tiles_x * ((g.Ho + W3_TH - 1) / W3_TH);
 
-  f32x4 acc[2][9];
+  f32x4 acc[WG_NI][9];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < WG_NI; ++i)
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int lr = lane & 15, lg = lane >> 4, q = lr >> 2, pp = lr & 3;
   const bf16* shp = shx + (cit >> 1) * W3_PLANE;
-  int aoff[2][2], boff[2][3];
+  int aoff[WG_NI][2], boff[2][3];
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     const int r = lg * 8 + half * 4 + q;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) aoff[i][half] = r * 64 + ((((cot0 + i) * 4 + pp) ^ w3_swz_dy(r)) * 4);
+    for (int i = 0; i < WG_NI; ++i) aoff[i][half] = r * 64 + ((((cot0 + i) * 4 + pp) ^ w3_swz_dy(r)) * 4);
 #pragma unroll
     for (int kx = 0; kx < 3; ++kx) boff[half][kx] = (r + kx) * 32 + ((((cit & 1) * 4 + pp) ^ w3_swz_x(r + kx)) * 4);
   }
   // next tile's vectors in registers (unpredicated loads: clamped address + select), written to LDS after
   // the barrier that ends the current tile's reads
-  bf16x8 yv[4], hv[6];
+  constexpr int YV = 2048 / WG_NT, HV = (W3_NPIX * 8 + WG_NT - 1) / WG_NT;
+  bf16x8 yv[YV], hv[HV];
   auto gload = [&](int tile) {
     const int n = tile / tiles_per_img;
     const int rem = tile - n * tiles_per_img;
     const int ty = rem / tiles_x, tx = rem - ty * tiles_x;
     const int y0 = ty * W3_TH, x0 = tx * W3_TW;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {       // dY: 256 px x 8 vectors
-      const int e = tid + k * 512;
+    for (int k = 0; k < YV; ++k) {      // dY: 256 px x 8 vectors
+      const int e = tid + k * WG_NT;
       const int p = e >> 3, part = e & 7;
       const int oy = y0 + (p >> 5), ox = x0 + (p & 31);
       const bool ok = oy < g.Ho && ox < g.Wo;
@@ -2607,8 +2616,8 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3c64_kernel(const bf16* __restr
       yv[k] = ok ? v : bf16x8{};
     }
 #pragma unroll
-    for (int k = 0; k < 6; ++k) {       // halo: 340 px x 8 vectors (64 ci)
-      const int e = tid + k * 512;
+    for (int k = 0; k < HV; ++k) {      // halo: 340 px x 8 vectors (64 ci)
+      const int e = tid + k * WG_NT;
       const int hp = e >> 3, part = e & 7;
       const int r = hp / W3_HW, c = hp - r * W3_HW;
       const int iy = y0 - 1 + r, ix = x0 - 1 + c;
@@ -2622,15 +2631,15 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3c64_kernel(const bf16* __restr
   for (int tile = blockIdx.z; tile < ntiles; tile += gridDim.z) {
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int e = tid + k * 512;
+    for (int k = 0; k < YV; ++k) {
+      const int e = tid + k * WG_NT;
       const int p = e >> 3, part = e & 7;  // chunk pair (2part, 2part+1) of 8-B chunks
       const int ch = (part * 2) ^ w3_swz_dy(p);
       *reinterpret_cast<bf16x8*>(sdy + p * 64 + ch * 4) = yv[k];
     }
 #pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      const int e = tid + k * 512;
+    for (int k = 0; k < HV; ++k) {
+      const int e = tid + k * WG_NT;
       if (e < W3_NPIX * 8) {
         const int hp = e >> 3, part = e & 7;
         const int r = hp / W3_HW, row = r * W3_P + (hp - r * W3_HW);
@@ -2640,12 +2649,12 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3c64_kernel(const bf16* __restr
     }
     __syncthreads();
     if (tile + (int)gridDim.z < ntiles) gload(tile + gridDim.z);
-    // the 22 fragment reads of pixel row py+1 are issued between the 18 MFMAs of row py (two register
+    // the fragment reads of pixel row py+1 (2 NI + 18) are issued between the 9 NI MFMAs of row py (two register
     // sets; 1 read : 1 MFMA via sched_group_barrier), so no row waits for its LDS reads
-    bf16x8 fa[2][2], fb[2][9];
+    bf16x8 fa[2][WG_NI], fb[2][9];
     auto rd = [&](int py, int b) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < WG_NI; ++i)
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
           const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(sdy + aoff[i][half] + py * 32 * 64));
@@ -2666,10 +2675,10 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3c64_kernel(const bf16* __restr
     };
     auto mm = [&](int b) {
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        acc[0][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[b][0], fb[b][tap], acc[0][tap], 0, 0, 0);
-        acc[1][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[b][1], fb[b][tap], acc[1][tap], 0, 0, 0);
-      }
+      for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+        for (int i = 0; i < WG_NI; ++i)
+          acc[i][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[b][i], fb[b][tap], acc[i][tap], 0, 0, 0);
     };
     rd(0, 0);
 #pragma unroll
@@ -2679,12 +2688,15 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3c64_kernel(const bf16* __restr
       if (py + 1 < W3_TH) rd(py + 1, b ^ 1);
       mm(b);
       if (py + 1 < W3_TH) {
+        constexpr int NRD = 2 * WG_NI + 18, NMF = 9 * WG_NI;
+        constexpr int NPAIR = NRD < NMF ? NRD : NMF;
 #pragma unroll
-        for (int q2 = 0; q2 < 18; ++q2) {
+        for (int q2 = 0; q2 < NPAIR; ++q2) {
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
         }
-        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+        if (NRD > NPAIR) __builtin_amdgcn_sched_group_barrier(0x100, NRD - NPAIR, 0);
+        if (NMF > NPAIR) __builtin_amdgcn_sched_group_barrier(0x008, NMF - NPAIR, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -2692,7 +2704,7 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3c64_kernel(const bf16* __restr
   const int K = 9 * Cin;
   float* out = slab + (int64_t)blockIdx.z * g.Cout * K;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < WG_NI; ++i)
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int ci = ci0 + cit * 16 + lr;
@@ -2999,14 +3011,14 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3w36_kernel(const bf16* __restr
 // (kyt,kxt) = flip ? (KH-1-ky, KW-1-kx) : (ky,kx).
 // 8 x 36 tiles (levels 2-3) with the 64 co x 64 ci / 8-wave blocking and the K-chunk software pipeline of
 // wgrad3x3c64_kernel: each wave's 22 fragment reads of K-chunk kc+1 are issued between the 18 MFMAs of chunk kc
-__global__ __launch_bounds__(512, 1) void wgrad3x3w36c64_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
+__global__ __launch_bounds__(WG_NT, 1) void wgrad3x3w36c64_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
                                                                 const bf16* __restrict__ dy1, const bf16* __restrict__ dy2,
                                                                 float* __restrict__ slab, ConvGeom g, int tiles_x,
                                                                 int ntiles) {
   __shared__ __attribute__((aligned(16))) bf16 sdy[W36_NP * 64];  // 36 KB, 128-B rows
   __shared__ __attribute__((aligned(16))) bf16 shx[2 * W3_PLANE];  // 2 x 30 KB, 64-B rows
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int cot0 = (wid >> 2) * 2, cit = wid & 3;
+  const int cot0 = WG4 ? 0 : (wid >> 2) * 2, cit = wid & 3;
   const int co0 = blockIdx.x * 64, ci0 = blockIdx.y * 64;
   const int Cin = g.C1 + g.C2;
   const bf16* xs; int xcs, xcc;
@@ -3016,31 +3028,32 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3w36c64_kernel(const bf16* __re
   if (co0 < g.Co1) { ys = dy1; ycs = g.Co1; ycc = co0; } else { ys = dy2; ycs = Co2; ycc = co0 - g.Co1; }
   const int tiles_per_img = tiles_x * ((g.Ho + W36_TH - 1) / W36_TH);
 
-  f32x4 acc[2][9];
+  f32x4 acc[WG_NI][9];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < WG_NI; ++i)
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int lr = lane & 15, lg = lane >> 4, q = lr >> 2, pp = lr & 3;
   const bf16* shp = shx + (cit >> 1) * W3_PLANE;
   const int cx = (cit & 1) * 4 + pp;
-  int aoff[2][2];
+  int aoff[WG_NI][2];
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     const int r = lg * 8 + half * 4 + q;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) aoff[i][half] = r * 64 + ((((cot0 + i) * 4 + pp) ^ w3_swz_dy(r)) * 4);
+    for (int i = 0; i < WG_NI; ++i) aoff[i][half] = r * 64 + ((((cot0 + i) * 4 + pp) ^ w3_swz_dy(r)) * 4);
   }
-  bf16x8 yv[5], hv[6];
+  constexpr int YV = (W36_NP * 8 + WG_NT - 1) / WG_NT, HV = (W36_NPIX * 8 + WG_NT - 1) / WG_NT;
+  bf16x8 yv[YV], hv[HV];
   auto gload = [&](int tile) {
     const int n = tile / tiles_per_img;
     const int rem = tile - n * tiles_per_img;
     const int ty = rem / tiles_x, tx = rem - ty * tiles_x;
     const int y0 = ty * W36_TH, x0 = tx * W36_TW;
 #pragma unroll
-    for (int k = 0; k < 5; ++k) {       // dY: 288 px x 8 vectors
-      const int e = tid + k * 512;
+    for (int k = 0; k < YV; ++k) {       // dY: 288 px x 8 vectors
+      const int e = tid + k * WG_NT;
       const int p = e >> 3, part = e & 7;
       const int oy = y0 + p / W36_TW, ox = x0 + (p - (p / W36_TW) * W36_TW);
       const bool ok = e < W36_NP * 8 && oy < g.Ho && ox < g.Wo;
@@ -3049,8 +3062,8 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3w36c64_kernel(const bf16* __re
       yv[k] = ok ? v : bf16x8{};
     }
 #pragma unroll
-    for (int k = 0; k < 6; ++k) {       // halo: 380 px x 8 vectors (64 ci)
-      const int e = tid + k * 512;
+    for (int k = 0; k < HV; ++k) {       // halo: 380 px x 8 vectors (64 ci)
+      const int e = tid + k * WG_NT;
       const int hp = e >> 3, part = e & 7;
       const int r = hp / W36_HW, c = hp - r * W36_HW;
       const int iy = y0 - 1 + r, ix = x0 - 1 + c;
@@ -3064,8 +3077,8 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3w36c64_kernel(const bf16* __re
   for (int tile = blockIdx.z; tile < ntiles; tile += gridDim.z) {
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      const int e = tid + k * 512;
+    for (int k = 0; k < YV; ++k) {
+      const int e = tid + k * WG_NT;
       if (e < W36_NP * 8) {
         const int p = e >> 3, part = e & 7;
         const int ch = (part * 2) ^ w3_swz_dy(p);
@@ -3073,8 +3086,8 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3w36c64_kernel(const bf16* __re
       }
     }
 #pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      const int e = tid + k * 512;
+    for (int k = 0; k < HV; ++k) {
+      const int e = tid + k * WG_NT;
       if (e < W36_NPIX * 8) {
         const int hp = e >> 3, part = e & 7;
         const int r = hp / W36_HW, row = r * W3_P + (hp - r * W36_HW);
@@ -3089,10 +3102,10 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3w36c64_kernel(const bf16* __re
     int prow[2], pcol[2];
 #pragma unroll
     for (int half = 0; half < 2; ++half) { prow[half] = 0; pcol[half] = lg * 8 + half * 4 + q; }
-    bf16x8 fa[2][2], fb[2][9];
+    bf16x8 fa[2][WG_NI], fb[2][9];
     auto rd = [&](int kc, int b) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < WG_NI; ++i)
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
           const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(sdy + aoff[i][half] + kc * 32 * 64));
@@ -3122,8 +3135,9 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3w36c64_kernel(const bf16* __re
     auto mm = [&](int b) {
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
-        acc[0][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[b][0], fb[b][tap], acc[0][tap], 0, 0, 0);
-        acc[1][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[b][1], fb[b][tap], acc[1][tap], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < WG_NI; ++i)
+          acc[i][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[b][i], fb[b][tap], acc[i][tap], 0, 0, 0);
       }
     };
     constexpr int NKC = W36_NP / 32;
@@ -3135,12 +3149,15 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3w36c64_kernel(const bf16* __re
       if (kc + 1 < NKC) rd(kc + 1, b ^ 1);
       mm(b);
       if (kc + 1 < NKC) {
+        constexpr int NRD = 2 * WG_NI + 18, NMF = 9 * WG_NI;
+        constexpr int NPAIR = NRD < NMF ? NRD : NMF;
 #pragma unroll
-        for (int q2 = 0; q2 < 18; ++q2) {
+        for (int q2 = 0; q2 < NPAIR; ++q2) {
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
         }
-        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+        if (NRD > NPAIR) __builtin_amdgcn_sched_group_barrier(0x100, NRD - NPAIR, 0);
+        if (NMF > NPAIR) __builtin_amdgcn_sched_group_barrier(0x008, NMF - NPAIR, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -3148,7 +3165,7 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3w36c64_kernel(const bf16* __re
   const int K = 9 * Cin;
   float* out = slab + (int64_t)blockIdx.z * g.Cout * K;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < WG_NI; ++i)
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int ci = ci0 + cit * 16 + lr;
@@ -4096,7 +4113,7 @@ int cesm_conv_wgrad(int dtype, const void* x1, const void* x2, const void* dy1, 
     const int tx = Wo / W36_TW;
     const int ntiles = Nb * tx * (int)cdiv(Ho, W36_TH);
     dim3 g3(Cout / 64, Cin / 64, std::min(nsplit, ntiles));
-    wgrad3x3w36c64_kernel<<<g3, 512, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
+    wgrad3x3w36c64_kernel<<<g3, WG_NT, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
                                                   (const bf16*)dy2, slab, g, tx, ntiles);
     nsplit = (int)g3.z;
   } else if (wv == WGV_W36) {
@@ -4110,7 +4127,7 @@ int cesm_conv_wgrad(int dtype, const void* x1, const void* x2, const void* dy1, 
     const int tx = (int)cdiv(Wo, W3_TW);
     const int ntiles = Nb * tx * (int)cdiv(Ho, W3_TH);
     dim3 g3(Cout / 64, Cin / 64, std::min(nsplit, ntiles));
-    wgrad3x3c64_kernel<<<g3, 512, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
+    wgrad3x3c64_kernel<<<g3, WG_NT, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
                                                (const bf16*)dy2, slab, g, tx, ntiles);
     nsplit = (int)g3.z;
   } else if (wv == WGV_W32) {
