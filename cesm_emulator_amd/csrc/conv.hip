@@ -496,6 +496,11 @@ __device__ __forceinline__ int h3_off(int row, int ch) { return row * H3_LD + ((
 #ifndef H3_BIG
 #define H3_BIG 1  // A/B knob: 448-pixel tiles with 64 co x 112 px wave tiles (0 = 256-pixel tiles, 64 x 64)
 #endif
+#ifndef H3_DB
+#define H3_DB 0  // A/B knob: double-buffered chunks in the big-tile kernel (one block per CU): measured slower, conv
+                 // total per step 64.0 -> 68.2 ms (levels 1-3 -20..-28 %; the second co-resident block hides the
+                 // staging better than the in-block prefetch at one wave per SIMD; profiles/r3_h3db_conv_ab.txt)
+#endif
 template <int TW, int NJv = 4>
 __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
                                                               const bf16* __restrict__ w, const float* __restrict__ bias,
@@ -508,8 +513,13 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
   // per 448 instead of 256 pixels; 77 KiB of LDS, still 2 blocks per CU
   static_assert(NJv == 4 || (NJv == 7 && H3_SQ && H3_DMA), "big tiles need square wave tiles and DMA staging");
   constexpr int NROWS = (NJv == 7 ? 16 : 10) * H3_P;
-  __shared__ __attribute__((aligned(16))) bf16 sh[NROWS * H3_LD];
-  __shared__ __attribute__((aligned(16))) bf16 sw[9 * H3_BN * H3_LD];
+  // H3_DB (big tiles): two chunk buffers (152 KiB, one block per CU): chunk ch+1's DMA is issued before chunk ch's
+  // MFMAs instead of the second co-resident block covering the wait
+  constexpr int NBUF = (H3_DB && NJv == 7) ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) bf16 shm[NBUF][NROWS * H3_LD];
+  __shared__ __attribute__((aligned(16))) bf16 swm[NBUF][9 * H3_BN * H3_LD];
+  bf16* sh = shm[0];
+  bf16* sw = swm[0];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   // wave tile: H3_SQ (round 3) 64 co x 16 NJv px = 4 x NJv MFMA tiles per wave (8 fragment reads per 16 MFMAs per
   // tap at NJv = 4); else 32 co x 128 px = 2 x 8 (10 reads per 16 MFMAs: the 4 waves' reads exceeded the LDS
@@ -538,7 +548,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
   // 16-B piece): 1-KiB pieces of 16 LDS rows, each lane fetching the global chunk that the row swizzle puts in
   // its slot (chunk = slot ^ ((row >> 1) & 2)); halo rows outside the tile / image read as zeros (out-of-range
   // offset).  The second co-resident block computes while this one waits.
-  auto stage = [&](int ch) {
+  auto stage = [&](int ch, int buf) {
+    bf16* const sh = shm[buf];
+    bf16* const sw = swm[buf];
     const int c0 = ch * 32;
     const bf16* src;
     int cs, cc;
@@ -575,12 +587,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
       __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(sw + q * 512), 16,
                                                ((co * 9 + tap) * Cin + chunk * 8) * 2, 0, 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (NBUF == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
 #else
   // stage one 32-channel chunk: global -> registers -> LDS (transient registers; the second
   // co-resident block computes while this one loads)
-  auto stage = [&](int ch) {
+  auto stage = [&](int ch, int) {
     const int c0 = ch * 32;
     const bf16* src;
     int cs, cc;
@@ -655,10 +667,20 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
     for (int kx = 0; kx < 3; ++kx) boff[j][kx] = h3_off(hoff[j] + kx, lg);
 #pragma unroll
   for (int i = 0; i < NI; ++i) aoff[i] = h3_off(wr * 32 + i * 16 + lr, lg);
+  if (NBUF == 2) stage(0, 0);
   for (int ch = 0; ch < nchunk; ++ch) {
-    if (ch) __syncthreads();  // previous chunk fully consumed
-    stage(ch);
-    __syncthreads();
+    if (NBUF == 2) {
+      // chunk ch has landed (this wave's DMA) and every wave is past chunk ch-1, whose buffer the next DMA reuses
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (ch + 1 < nchunk) stage(ch + 1, (ch + 1) & 1);
+      sh = shm[ch & 1];
+      sw = swm[ch & 1];
+    } else {
+      if (ch) __syncthreads();  // previous chunk fully consumed
+      stage(ch, 0);
+      __syncthreads();
+    }
 #if H3_PIPE
     // the 10 fragment reads of tap t+1 are issued between the 16 MFMAs of tap t (two register sets), so no
     // MFMA waits on a read issued just before it (the compiler's order was read -> wait -> 2 MFMAs)

@@ -248,12 +248,31 @@ __device__ __forceinline__ void gn_coef8(const GnAffine& q, int b, int c0, int C
   }
 }
 
+// The backward per sample (cesm_gn_bwd): reduce + finalize + apply of one sample back to back while its
+// (dout, y) pair fits this budget, so gn_bwd_apply could re-read them from the Infinity Cache instead of HBM.
+// Measured off: the whole bench step 132.0 -> 138.0 ms with it (the 3 launches per sample and the one-block
+// finalize per sample cost more than the on-die re-read saves; non-temporal reduction loads 139.6 ms); the
+// reversed sample order in gn_apply (GN_FWD_REV) was neutral (138.0 vs 138.1); profiles/r3_gn_per_sample_ab.txt
+#ifndef GN_PER_SAMPLE
+#define GN_PER_SAMPLE 0
+#endif
+#ifndef GN_MALL_BYTES
+#define GN_MALL_BYTES (176ll << 20)
+#endif
+#ifndef GN_PS_NT
+#define GN_PS_NT false  // the per-sample reduction's loads: default policy (false) or non-temporal (true)
+#endif
+// gn_apply: samples in reverse order (the producing conv wrote the last ones last; they may still be on-die)
+#ifndef GN_FWD_REV
+#define GN_FWD_REV 0
+#endif
+
 // grid (nchunk, B): thread = (8-channel group c8, row lane rr), rows strided by 256/(C/8)
 template <typename T>
 __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ y, const GnAffine coef,
                                                        const T* __restrict__ res, T* __restrict__ out, int64_t rows_b,
                                                        int C, int nchunk) {
-  const int b = blockIdx.y, chunk = blockIdx.x;
+  const int b = GN_FWD_REV ? gridDim.y - 1 - blockIdx.y : blockIdx.y, chunk = blockIdx.x;
   const int cv = C / 8, rl = 256 / cv;
   const int c8 = threadIdx.x % cv, rr = threadIdx.x / cv;
   if (rr >= rl) return;
@@ -277,11 +296,11 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ y, 
 }
 
 // part[b][chunk][c] = (S1 = sum da, S3 = sum da*y, Sy = sum y)
-template <typename T>
+template <typename T, bool NT = true>
 __global__ __launch_bounds__(256) void gn_bwd_reduce_kernel(const T* __restrict__ dout, const T* __restrict__ y,
                                                             const GnAffine coef, float* __restrict__ part,
-                                                            int64_t rows_b, int C, int nchunk) {
-  const int b = blockIdx.y, chunk = blockIdx.x;
+                                                            int64_t rows_b, int C, int nchunk, int b0) {
+  const int bl = blockIdx.y, b = bl + b0, chunk = blockIdx.x;
   const int cv = C / 8, rl = 256 / cv;
   const int tid = threadIdx.x;
   const int c8 = tid % cv, rr = tid / cv;
@@ -295,8 +314,13 @@ __global__ __launch_bounds__(256) void gn_bwd_reduce_kernel(const T* __restrict_
 #pragma unroll 4
     for (int64_t r = r0 + rr; r < r1; r += rl) {
       float v[8], d[8];
-      gl8(y + off + r * C, v);
-      gl8(dout + off + r * C, d);
+      if (NT) {
+        gl8(y + off + r * C, v);
+        gl8(dout + off + r * C, d);
+      } else {  // default policy: the lines stay in the Infinity Cache for gn_bwd_apply's re-read
+        load8(y + off + r * C, v);
+        load8(dout + off + r * C, d);
+      }
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const float da = d[i] * dsilu_t<T>(fmaf(v[i], A1[i], A0[i]));
@@ -332,7 +356,7 @@ __global__ __launch_bounds__(256) void gn_bwd_reduce_kernel(const T* __restrict_
     }
     __syncthreads();
   }
-  float* o = part + ((int64_t)b * nchunk + chunk) * C * 3;
+  float* o = part + ((int64_t)bl * nchunk + chunk) * C * 3;
   for (int c = tid; c < C; c += 256) {
     o[c * 3] = red[0][c];
     o[c * 3 + 1] = red[1][c];
@@ -351,8 +375,8 @@ __global__ __launch_bounds__(1024) void gn_bwd_finalize_kernel(const float* __re
                                                               const float* __restrict__ beta,
                                                               const float* __restrict__ ss, float* __restrict__ dss,
                                                               float* __restrict__ pb, float* __restrict__ E, int C,
-                                                              int G, int nchunk, double count, float rows_b) {
-  const int b = blockIdx.x;
+                                                              int G, int nchunk, double count, float rows_b, int b0) {
+  const int bl = blockIdx.x, b = bl + b0;
   const int cl = threadIdx.x & 63, kg = threadIdx.x >> 6;
   const int c = blockIdx.y * 64 + cl;
   __shared__ float red[GNF_KG][3][64];
@@ -362,7 +386,7 @@ __global__ __launch_bounds__(1024) void gn_bwd_finalize_kernel(const float* __re
   float s1 = 0.f, s3 = 0.f, sy = 0.f;
   if (c < C)
     for (int k = kg; k < nchunk; k += GNF_KG) {
-      const float* p = part + (((int64_t)b * nchunk + k) * C + c) * 3;
+      const float* p = part + (((int64_t)bl * nchunk + k) * C + c) * 3;
       s1 += p[0];
       s3 += p[1];
       sy += p[2];
@@ -436,8 +460,9 @@ __global__ void gn_param_grad_kernel(const float* __restrict__ pb, float* __rest
 template <typename T>
 __global__ __launch_bounds__(256) void gn_bwd_apply_kernel(const T* __restrict__ dout, const T* __restrict__ y,
                                                            const GnAffine coef, const float* __restrict__ E,
-                                                           T* __restrict__ dy, int64_t rows_b, int C, int nchunk) {
-  const int b = blockIdx.y, chunk = blockIdx.x;
+                                                           T* __restrict__ dy, int64_t rows_b, int C, int nchunk,
+                                                           int b0) {
+  const int b = blockIdx.y + b0, chunk = blockIdx.x;
   const int cv = C / 8, rl = 256 / cv;
   const int c8 = threadIdx.x % cv, rr = threadIdx.x / cv;
   if (rr >= rl) return;
@@ -538,22 +563,46 @@ int cesm_gn_bwd(int dtype, const void* dout, const void* y, const float* stats, 
                 const float* beta, const float* ss, void* dy, float* dss, float* dgamma, float* dbeta, float* dbias,
                 float* ws, int B, int64_t rows_b, int C, int G, int accumulate, hipStream_t stream) {
   if (C % 8 || C / 8 > 128 || C % G || C / G > 64 || 64 % (C / G) || G > 64) return CESM_EINVAL;
-  const int nchunk = gn_nchunk(rows_b, C, B);
-  float* part = ws;
-  float* pb = part + (int64_t)B * nchunk * C * 3;
-  float* coef = pb + (int64_t)B * C * 3;
-  float* E = coef + (int64_t)B * C * 2;
   const double count = (double)rows_b * (C / G);
   const GnAffine aff{stats, gamma, beta, ss, G};
   const int nch = gn_apply_chunks(rows_b, C);
-  int rc = dispatch_dt(dtype, [&](auto* tp) {
+  const int64_t esz = dtype == CESM_DT_BF16 ? 2 : 4;
+  float* part = ws;
+  int rc;
+  if (GN_PER_SAMPLE && B > 1 && 2 * rows_b * C * esz <= (int64_t)GN_MALL_BYTES) {
+    // one sample at a time, last sample first: the reduction's reads of (dout, y) of a sample (<= GN_MALL_BYTES)
+    // are still in the 256-MiB Infinity Cache when gn_bwd_apply re-reads them, and the last sample's dout is the
+    // part of it the producing kernel wrote last.  The chunk partials of one sample reuse one region.
+    const int nc1 = gn_nchunk(rows_b, C, 1);  // <= 1024 <= max(B * 256, 1024)
+    float* pb = part + (int64_t)nc1 * C * 3;
+    float* E = pb + (int64_t)B * C * 3 + (int64_t)B * C * 2;
+    rc = dispatch_dt(dtype, [&](auto* tp) {
+      using T = std::remove_pointer_t<decltype(tp)>;
+      for (int b = B - 1; b >= 0; --b) {
+        gn_bwd_reduce_kernel<T, GN_PS_NT><<<dim3(nc1, 1), 256, 0, stream>>>((const T*)dout, (const T*)y, aff, part,
+                                                                           rows_b, C, nc1, b);
+        gn_bwd_finalize_kernel<<<dim3(1, (unsigned)cdiv(C, 64)), 64 * GNF_KG, 0, stream>>>(
+            part, stats, gamma, beta, ss, dss, pb, E, C, G, nc1, count, (float)rows_b, b);
+        gn_bwd_apply_kernel<T><<<dim3(nch, 1), 256, 0, stream>>>((const T*)dout, (const T*)y, aff, E, (T*)dy, rows_b,
+                                                                 C, nch, b);
+      }
+    });
+    if (rc) return rc;
+    gn_param_grad_kernel<<<(unsigned)cdiv(C, 256), 256, 0, stream>>>(pb, dgamma, dbeta, dbias, B, C, accumulate);
+    return cesm_launch_status();
+  }
+  const int nchunk = gn_nchunk(rows_b, C, B);
+  float* pb = part + (int64_t)B * nchunk * C * 3;
+  float* coef = pb + (int64_t)B * C * 3;
+  float* E = coef + (int64_t)B * C * 2;
+  rc = dispatch_dt(dtype, [&](auto* tp) {
     using T = std::remove_pointer_t<decltype(tp)>;
     gn_bwd_reduce_kernel<T><<<dim3(nchunk, B), 256, 0, stream>>>((const T*)dout, (const T*)y, aff, part, rows_b, C,
-                                                                 nchunk);
+                                                                 nchunk, 0);
     gn_bwd_finalize_kernel<<<dim3(B, (unsigned)cdiv(C, 64)), 64 * GNF_KG, 0, stream>>>(part, stats, gamma, beta, ss, dss, pb,
-                                                                               E, C, G, nchunk, count, (float)rows_b);
+                                                                               E, C, G, nchunk, count, (float)rows_b, 0);
     gn_bwd_apply_kernel<T><<<dim3(nch, B), 256, 0, stream>>>((const T*)dout, (const T*)y, aff, E, (T*)dy, rows_b, C,
-                                                             nch);
+                                                             nch, 0);
   });
   if (rc) return rc;
   gn_param_grad_kernel<<<(unsigned)cdiv(C, 256), 256, 0, stream>>>(pb, dgamma, dbeta, dbias, B, C, accumulate);
