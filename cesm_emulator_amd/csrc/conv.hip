@@ -2247,11 +2247,17 @@ __device__ __forceinline__ int wgb_swz(int r) {  // XOR on 4-element chunk index
 // over dY, which re-read the whole tensor).
 // (BIAS: compile-time, so the plain instantiation keeps its register count — the bias accumulators
 // pushed the BM = 256 kernel past 128 VGPRs, a wave per SIMD fewer and 43 % slower.)
+// WW_XCD: 1-D grid, the (co block, K column block) tiles of one pixel split on ONE XCD back to back (linear id mod 8
+// = XCD), so the split's dY / x rows are fetched into that XCD's L2 once and re-read there by the split's other tiles
+// (the 3-D grid deals a split's tiles to consecutive ids = different XCDs)
+#ifndef WW_XCD
+#define WW_XCD 0  // measured slower: whole step 130.4 -> 131.5 ms (profiles/r3_gn_iters_ab.txt, wwxcd rows)
+#endif
 template <int BM, bool BIAS = false>
 __global__ __launch_bounds__(256) void wgrad_wide_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
                                                          const bf16* __restrict__ dy1, const bf16* __restrict__ dy2,
                                                          float* __restrict__ slab, float* __restrict__ bslab, ConvGeom g,
-                                                         int M, int px_per_split) {
+                                                         int M, int px_per_split, int gx = 0, int gy = 0, int nsplit = 0) {
   constexpr int VPRY = BM / 8, RPPY = 256 / VPRY, NPY = WG_BP / RPPY;
   constexpr int MT = BM / 64;  // 16-row co tiles per wave
   __shared__ __attribute__((aligned(16))) bf16 tY[2][WG_BP * BM];
@@ -2259,12 +2265,21 @@ __global__ __launch_bounds__(256) void wgrad_wide_kernel(const bf16* __restrict_
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const int Cin = g.C1 + g.C2;
-  const int co0 = blockIdx.x * BM;
-  const int kcol0 = blockIdx.y * 64;
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (gx > 0) {  // WW_XCD mapping (uniform)
+    const int L = blockIdx.x, j = L >> 3, nt = gx * gy;
+    const int t = j % nt;
+    bz = (j / nt) * 8 + (L & 7);
+    if (bz >= nsplit) return;  // padded ids (whole block)
+    bx = t % gx;
+    by = t / gx;
+  }
+  const int co0 = bx * BM;
+  const int kcol0 = by * 64;
   const int tap = kcol0 / Cin;
   const int ci0 = kcol0 - tap * Cin;
   const int ky = tap / g.KW, kx = tap - ky * g.KW;
-  const int pbeg = blockIdx.z * px_per_split;
+  const int pbeg = bz * px_per_split;
   const int pend = min(M, pbeg + px_per_split);
   const bf16* xs; int xcs, xcc;
   if (ci0 < g.C1) { xs = x1; xcs = g.C1; xcc = ci0; } else { xs = x2; xcs = g.C2; xcc = ci0 - g.C1; }
@@ -2334,7 +2349,7 @@ __global__ __launch_bounds__(256) void wgrad_wide_kernel(const bf16* __restrict_
   for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bool bias_blk = BIAS && blockIdx.y == 0;  // uniform
+  const bool bias_blk = BIAS && by == 0;  // uniform
   f32x4 bacc[BIAS ? MT : 1];
 #pragma unroll
   for (int i = 0; i < (BIAS ? MT : 1); ++i) bacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -2400,10 +2415,10 @@ __global__ __launch_bounds__(256) void wgrad_wide_kernel(const bf16* __restrict_
 #pragma unroll
     for (int i = 0; i < (BIAS ? MT : 1); ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) bslab[(int64_t)blockIdx.z * g.Cout + co0 + wid * (BM / 4) + i * 16 + lg * 4 + r] = bacc[i][r];
+      for (int r = 0; r < 4; ++r) bslab[(int64_t)bz * g.Cout + co0 + wid * (BM / 4) + i * 16 + lg * 4 + r] = bacc[i][r];
   }
   const int K = g.KH * g.KW * Cin;
-  float* out = slab + (int64_t)blockIdx.z * g.Cout * K;
+  float* out = slab + (int64_t)bz * g.Cout * K;
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -4168,12 +4183,15 @@ int cesm_conv_wgrad(int dtype, const void* x1, const void* x2, const void* dy1, 
   } else if (wv == WGV_WIDE || wv == WGV_S2) {
     // wide-tile kernel; nsplit from the caller sized the slab for 64-row tiles, keep it
     const int bm = (Cout % 256 == 0 && Co1 % 256 == 0) ? 256 : ((Cout % 128 == 0 && Co1 % 128 == 0) ? 128 : 64);
-    dim3 gw(Cout / bm, K / 64, nsplit);
+    const int gx = Cout / bm, gy = (int)(K / 64);
+    dim3 gw(gx, gy, nsplit);
+    if (WW_XCD) gw = dim3((unsigned)(cdiv(nsplit, 8) * 8 * gx * gy));
     auto launch = [&](auto bmc, auto biasc) {
       constexpr int BMv = decltype(bmc)::value;
       constexpr bool Bv = decltype(biasc)::value;
       wgrad_wide_kernel<BMv, Bv><<<gw, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
-                                                         (const bf16*)dy2, slab, bslab, g, (int)M, (int)pps);
+                                                         (const bf16*)dy2, slab, bslab, g, (int)M, (int)pps,
+                                                         WW_XCD ? gx : 0, gy, nsplit);
     };
     using T0 = std::false_type;
     using T1 = std::true_type;

@@ -495,10 +495,13 @@ static int dispatch_dt(int dtype, F&& f) {
   return CESM_EINVAL;
 }
 
+#ifndef GN_APPLY_ITERS
+#define GN_APPLY_ITERS 8  // row-iterations per thread of the streaming apply kernels: whole step 16 -> 8: -0.5 ms
+                          // (two calls, profiles/r3_gn_iters_ab.txt); 4 the same as 8, 32 +0.5 ms
+#endif
 static int gn_apply_chunks(int64_t rows_b, int C) {
-  // ~16 row-iterations per thread
   const int rl = 256 / (C / 8);
-  int64_t n = rows_b / (rl * 16);
+  int64_t n = rows_b / (rl * GN_APPLY_ITERS);
   if (n < 1) n = 1;
   if (n > 4096) n = 4096;
   return (int)n;

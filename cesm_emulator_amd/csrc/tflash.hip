@@ -209,6 +209,10 @@ __device__ __forceinline__ const float* btab_lane(const float* tab, int lr, int 
 #ifndef TF_BUF
 #define TF_BUF 1  // A/B knob: buffer-resource tile addressing in the per-query-tile loop (0 = 64-bit lane math)
 #endif
+#ifndef TF_QPF
+#define TF_QPF 0  // A/B knob: forward query-tile rows prefetched a tile ahead (measured neutral at F = 120: 192x288
+                  // 4616 -> 4547 us, 96x144 +1 %, 48x72 -2 %, 24x36 +0..8 %; profiles/r3_tf_qpf_ab.txt)
+#endif
 #ifndef TF_XCD_MAP
 #define TF_XCD_MAP 1  // A/B knob: 0 = head-major grid (round 2)
 #endif
@@ -284,6 +288,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE)
 #pragma unroll
   for (int r = 0; r < 4; ++r) kmask[r] = 16 * (NT - 1) + 4 * g + r < F ? 0.f : -INFINITY;
 
+  // TF_QPF: the next query tile's raw q rows and RoPE coefficients are loaded while the current tile computes (one
+  // exposed load latency per wave instead of one per query tile; 12 more VGPRs, unlike TF_QPRE's 32 + RoPE)
+  bf16x8 qraw_n = zero8();
+  float cs_n[8];
+  auto qload = [&](int qt, bf16x8& raw, float* cs) {
+    const __amdgpu_buffer_rsrc_t qrs =
+        tile_rsrc(qkv + (row0 + (int64_t)qt * 16 * HW) * QKV + h * DH, F - qt * 16, (int64_t)HW * QKV * 2, DH * 2);
+    buf_rot8(rot_rs, rot_off + qt * 16 * 16 * 2 * 4, cs);
+    raw = buf_ld16(qrs, q_off);
+  };
+  if (TF_QPF && TF_BUF && !TF_QPRE) qload(0, qraw_n, cs_n);
   for (int qt = 0; qt < NT; ++qt) {
     const int fq = qt * 16 + lr;
     const bool okq = fq < F;
@@ -291,6 +306,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE)
     bf16x8 qf;
     if (TF_QPRE) {
       qf = qfa[TF_QPRE ? qt : 0];
+    } else if (TF_QPF && TF_BUF) {
+      const bf16x8 raw = qraw_n;
+      float cs[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) cs[i] = cs_n[i];
+      if (qt + 1 < NT) qload(qt + 1, qraw_n, cs_n);  // frames >= F: zeros
+      qf = rope8(raw, cs, scale);
     } else if (TF_BUF) {
       const __amdgpu_buffer_rsrc_t qrs =
           tile_rsrc(qkv + (row0 + (int64_t)qt * 16 * HW) * QKV + h * DH, nq, (int64_t)HW * QKV * 2, DH * 2);

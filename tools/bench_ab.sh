@@ -15,7 +15,7 @@ out=gpurun_out/${tag}_bench_ab.txt
 for rep in 1 2; do
   for v in default "$@"; do
     if [ "$v" == default ]; then lib=""; else lib=cesm_emulator_amd/libcesm_hip_$v.so; fi
-    CESM_HIP_LIB=$lib timeout -k 10 300 python3 bench.py --no-cpu-baseline --other-configs "" $args 2>/dev/null | \
+    CESM_HIP_LIB=$lib timeout -k 10 300 python3 bench.py --no-cpu-baseline --other-configs "" $args 2>>gpurun_out/${tag}_bench_ab.err | \
       python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$v', d['value'], d['ms_per_step'])" >> $out
   done
 done
