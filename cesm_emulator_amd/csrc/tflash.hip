@@ -401,11 +401,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE)
 #ifndef TF_DO
 #define TF_DO 1
 #endif
+#ifndef TF_DO_PF
+#define TF_DO_PF 0  // A/B knob: register prefetch of the next pixel's rows in the single-pass (D from O) dq kernel, at
+                    // 159 VGPRs (one block per CU; at 128 it spills 31): F = 120 bwd 192x288 13.2 -> 15.1 ms, 96x144
+                    // 3.50 -> 3.96, 24x36 371 -> 467 us -- the second co-resident block hides the loads better
+                    // (profiles/r3_tf_dopf_ab.txt; single-pass without prefetch everywhere: 13.2 -> 13.8 ms)
+#endif
 #ifndef TF_DO_MAXHW
 #define TF_DO_MAXHW 8192
 #endif
 template <int NT, bool DOV>
-__global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(DOV ? 4 : 2))) void tflash_bwd_q_kernel(
+__global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(DOV && !TF_DO_PF ? 4 : 2))) void tflash_bwd_q_kernel(
     const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
     const float* __restrict__ lse, const float* __restrict__ bias, const float* __restrict__ rot,
     bf16* __restrict__ dqkv, float* __restrict__ dbuf, float* __restrict__ part, int F, int HW, float scale) {
@@ -451,21 +457,24 @@ __global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(DOV ? 4
     rot8_load(rot, sfc, sc, kcs);
     rot8_load(rot, fqc, g, qcs);
   }
-  bf16x8 kraw = zero8(), vraw = zero8(), qraw = zero8(), draw = zero8();
+  bf16x8 kraw = zero8(), vraw = zero8(), qraw = zero8(), draw = zero8(), oraw = zero8();
   float lraw = 0.f;
+  // TF_DO_PF: the single-pass kernel prefetches the next pixel's rows too (K, V, q, dO, O, lse: 21 registers)
+  constexpr bool PF = !DO_ || TF_DO_PF;
   auto fetch = [&](int pp) {
     const int64_t r0 = (int64_t)b * F * HW + pp;
     const int64_t rs = (r0 + (int64_t)sfc * HW) * QKV + h * DH + sc * 8;
     kraw = ld16(qkv + rs + INNER);
     vraw = ld16(qkv + rs + 2 * INNER);
-    if (!DO_) {
+    if (PF) {
       const int64_t vq = r0 + (int64_t)fqc * HW;
       qraw = ld16(qkv + vq * QKV + h * DH + g * 8);
       draw = ld16(dout + vq * INNER + h * DH + g * 8);
+      if (DO_) oraw = ld16(o + vq * INNER + h * DH + g * 8);
       lraw = lse[(((int64_t)b * NH + h) * HW + pp) * F + fqc];
     }
   };
-  if (!DO_ && (int)blockIdx.x < HW) fetch(blockIdx.x);
+  if (PF && (int)blockIdx.x < HW) fetch(blockIdx.x);
 
   for (int p = blockIdx.x; p < HW; p += gridDim.x) {
     const int64_t row0 = (int64_t)b * F * HW + p;
@@ -473,16 +482,17 @@ __global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(DOV ? 4
     bf16x8 qf, dof;
     float Li, Do = 0.f;
     if (DO_) {
-      fetch(p);  // K / V rows of this pixel (the co-resident block hides the latency)
+      if (!PF) fetch(p);  // K / V rows of this pixel (the co-resident block hides the latency)
       float cs[8];
       rot8_load(rot, sfc, sc, cs);
       *reinterpret_cast<bf16x8*>(ks + sf * TF_LD + sc * 8) = sok ? rope8(kraw, cs, 1.f) : zero8();
       *reinterpret_cast<bf16x8*>(vs + sf * TF_LD + sc * 8) = sok ? vraw : zero8();
       const int64_t vq = row0 + (int64_t)fqc * HW;
-      const bf16x8 qr = ld16(qkv + vq * QKV + h * DH + g * 8);
-      dof = ld16(dout + vq * INNER + h * DH + g * 8);
-      const bf16x8 orw = ld16(o + vq * INNER + h * DH + g * 8);
-      const float lr_ = lse[(((int64_t)b * NH + h) * HW + p) * F + fqc];
+      const bf16x8 qr = PF ? qraw : ld16(qkv + vq * QKV + h * DH + g * 8);
+      dof = PF ? draw : ld16(dout + vq * INNER + h * DH + g * 8);
+      const bf16x8 orw = PF ? oraw : ld16(o + vq * INNER + h * DH + g * 8);
+      const float lr_ = PF ? lraw : lse[(((int64_t)b * NH + h) * HW + p) * F + fqc];
+      if (PF && p + (int)gridDim.x < HW) fetch(p + gridDim.x);
       rot8_load(rot, fqc, g, cs);
       qf = rope8(qr, cs, scale);
       Li = okq ? lr_ : TF_LSE_PAD;  // padded query rows: P = 0 (so dS = 0 there)
