@@ -39,9 +39,12 @@ template <typename T> __device__ __forceinline__ void gs8(T* p, const float* v) 
 #ifndef GN_SMALLB_CHUNKS
 #define GN_SMALLB_CHUNKS 1024  // A/B knob (256 = the round-2 fixed cap)
 #endif
+#ifndef GN_BIGB_CAP
+#define GN_BIGB_CAP 256  // A/B knob: chunks per sample at B >= 4 (<= 1024: the workspace holds B * 1024 partials)
+#endif
 static int gn_nchunk(int64_t rows_b, int C, int B) {
   const int rl = 256 / (C / 8);
-  const int cap = B >= GN_SMALLB_CHUNKS / 256 ? 256 : GN_SMALLB_CHUNKS / B;
+  const int cap = B >= GN_SMALLB_CHUNKS / 256 ? GN_BIGB_CAP : GN_SMALLB_CHUNKS / B;
   int64_t n = rows_b / (rl * 8);
   if (n < 1) n = 1;
   if (n > cap) n = cap;
@@ -561,7 +564,7 @@ int cesm_gn_apply(int dtype, const void* y, const float* stats, const float* gam
 
 // Backward of out = silu(GN(y)*(1+scale)+shift) (+res).  Writes dy, dss [B][2C] (if non-null),
 // dgamma/dbeta and the producing conv's bias gradient dbias = sum dy (each nullable; accumulate flag).
-// ws: float workspace >= max(B*256, 1024)*C*3 + B*C*3 + B*C*5 floats.
+// ws: float workspace >= B*1024*C*3 + B*C*3 + B*C*5 floats.
 int cesm_gn_bwd(int dtype, const void* dout, const void* y, const float* stats, const float* gamma,
                 const float* beta, const float* ss, void* dy, float* dss, float* dgamma, float* dbeta, float* dbias,
                 float* ws, int B, int64_t rows_b, int C, int G, int accumulate, hipStream_t stream) {

@@ -275,7 +275,7 @@ def gn_bwd(dout, y, stats, gamma, beta, ss, dgamma, dbeta, B, G, want_dss, dbias
     rows_b = y.numel() // (C * B)
     dy = empty(y.shape, y.dtype, y.device)
     dss = empty((B, 2 * C), torch.float32, y.device) if want_dss else None
-    ws = empty((max(B * 256, 1024) * C * 3 + B * C * 3 + B * C * 5,), torch.float32, y.device)
+    ws = empty((max(B * 1024, 1024) * C * 3 + B * C * 3 + B * C * 5,), torch.float32, y.device)  # <= 1024 chunks/sample
     call("cesm_gn_bwd", dtcode(y), P(dout), P(y), P(stats), P(gamma), P(beta), P(ss), P(dy), P(dss), P(dgamma),
          P(dbeta), P(dbias), P(ws), B, rows_b, C, G, 1, S())
     return dy, dss

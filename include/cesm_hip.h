@@ -97,7 +97,8 @@ int cesm_gn_apply(int dtype, const void* y, const float* stats, const float* gam
                   const float* ss, const void* res, void* out, float* ws, int B, int64_t rows_b, int C, int G,
                   hipStream_t stream);
 /* backward; also writes the producing conv's bias gradient dbias (+)= sum dy (nullable) without another
- * pass over dy.  ws >= max(B*256, 1024)*C*3 + B*C*3 + B*C*5 floats. */
+ * pass over dy.  ws >= max(B*1024, 1024)*C*3 + B*C*3 + B*C*5 floats (max(B*256, 1024) suffices in the default
+ * build; builds with -DGN_BIGB_CAP=512/1024 or -DGN_PER_SAMPLE=1 use up to 1024 chunk partials per sample). */
 int cesm_gn_bwd(int dtype, const void* dout, const void* y, const float* stats, const float* gamma,
                 const float* beta, const float* ss, void* dy, float* dss, float* dgamma, float* dbeta, float* dbias,
                 float* ws, int B, int64_t rows_b, int C, int G, int accumulate, hipStream_t stream);
