@@ -40,7 +40,8 @@ template <typename T> __device__ __forceinline__ void gs8(T* p, const float* v) 
 #define GN_SMALLB_CHUNKS 1024  // A/B knob (256 = the round-2 fixed cap)
 #endif
 #ifndef GN_BIGB_CAP
-#define GN_BIGB_CAP 256  // A/B knob: chunks per sample at B >= 4 (<= 1024: the workspace holds B * 1024 partials)
+#define GN_BIGB_CAP 256  // A/B knob: chunks per sample at B >= 4 (<= 1024: the workspace holds B * 1024 partials);
+                         // whole step 256 -> 512 / 1024: +0.2 / +0.5 ms (profiles/r3_gn_cap_ab.txt)
 #endif
 static int gn_nchunk(int64_t rows_b, int C, int B) {
   const int rl = 256 / (C / 8);
