@@ -3997,8 +3997,15 @@ int conv_fwd_launch(int dtype, const void* x1, const void* x2, const void* wp, c
       const bool big = TH * TW > 256;  // h3_tile chose a 448-pixel tile (H3_BIG)
 #define H3L(TWv, NJv)                                                                                                \
   conv3x3_bf16_kernel<TWv, NJv><<<g3, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, TH, gnp, gn_fimg)
+      // the 448-pixel instantiations exist only in builds with square wave tiles and DMA staging (the A/B knobs
+      // H3_SQ = 0 / H3_DMA = 0 keep compiling; conv_fwd_plan then never picks a big tile)
+#if H3_BIG && H3_SQ && H3_DMA
       if (pl.v == CFV_HALO36) { if (big) H3L(36, 7); else H3L(36, 4); }
       else { if (big) H3L(32, 7); else H3L(32, 4); }
+#else
+      (void)big;
+      if (pl.v == CFV_HALO36) H3L(36, 4); else H3L(32, 4);
+#endif
 #undef H3L
       break;
     }

@@ -531,13 +531,14 @@ int cesm_gn_stats(int dtype, const void* y, float* stats, double* ws, int B, int
 }
 
 // ss: [B][2C] (scale | shift) or null; res: residual [B*rows_b][C] or null; ws: >= 2*B*C floats
-int cesm_gn_stats_part(const float* part, float* stats, int B, int64_t nslot, int C, int G, int64_t rows_b, float eps,
+// part is consumed: at nslot >= 8192 the two-stage reduction writes its stage-1 block sums over the partials
+int cesm_gn_stats_part(float* part, float* stats, int B, int64_t nslot, int C, int G, int64_t rows_b, float eps,
                        hipStream_t stream) {
   if (B <= 0 || G <= 0 || C % (4 * G) || nslot <= 0 || rows_b <= 0) return CESM_EINVAL;
   const int C4 = C / 4;
   if (nslot >= 8192 && C4 <= 256 && 256 % C4 == 0) {
     const int S = (int)(nslot / GNP_PER);  // >= 64 slots (>= 2 rows) per stage-1 block
-    gn_part_stage1_kernel<<<dim3(S, B), 256, 0, stream>>>(const_cast<float2*>(reinterpret_cast<const float2*>(part)),
+    gn_part_stage1_kernel<<<dim3(S, B), 256, 0, stream>>>(reinterpret_cast<float2*>(part),
                                                           nslot, C4, S);
     gn_part_stage2_kernel<<<B * G, 64, 0, stream>>>(reinterpret_cast<const float2*>(part), stats, G, nslot, C4, S,
                                                     (double)rows_b * (C / G), eps);

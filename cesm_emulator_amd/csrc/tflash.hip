@@ -87,7 +87,12 @@ __device__ __forceinline__ bf16x8 rope8(const bf16x8 v, const float* cs, float s
 // no 64-bit lane address math and no predicate branch per tile (the 64-bit math was ~60 of the forward's
 // ~320 VALU per query tile).
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, int nvalid, int64_t fstride_b, int rowb) {
+// `nvalid` counts the valid frames from the tile's first one; the resource covers at most `maxrows` of them (16 for a
+// query / output tile: a 120-frame window at 192x288 would otherwise span 119 * HW * 1536 B, past the 32-bit
+// num_records, which then wrapped and dropped rows of the tile).  The host bounds maxrows * fstride_b < 2^31.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, int nvalid, int64_t fstride_b, int rowb,
+                                                            int maxrows = 16) {
+  nvalid = nvalid < maxrows ? nvalid : maxrows;
   const int64_t n = nvalid > 0 ? (int64_t)(nvalid - 1) * fstride_b + rowb : 0;
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)n, 0x00020000);
 }
@@ -252,7 +257,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE)
   bf16* vs = vst[wid];
   // TF_BUF lane offsets: frame lr of a 16-frame tile
   const int q_off = (lr * HW * QKV + g * 8) * 2, o_off = (lr * HW * INNER + 4 * g) * 2;
-  const __amdgpu_buffer_rsrc_t rot_rs = tile_rsrc(rot, F, 16 * 2 * 4, 16 * 2 * 4);
+  const __amdgpu_buffer_rsrc_t rot_rs = tile_rsrc(rot, F, 16 * 2 * 4, 16 * 2 * 4, TF_MAXT * 16);
   const int rot_off = (lr * 16 + 4 * g) * 2 * 4;
   // every K' and Q' fragment up front (TF_QPRE): one exposed load latency per wave instead of one per query tile
   bf16x8 kf[NT], qfa[TF_QPRE ? NT : 1];

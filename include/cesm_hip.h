@@ -91,7 +91,7 @@ int cesm_gn_stats(int dtype, const void* y, float* stats, double* ws, int B, int
 /* stats [B][G] (mean, rstd) from cesm_conv_fwd_gn's partials (replaces cesm_gn_stats' pass over y):
  * fixed-order double reduction, rows_b = voxels per sample.  part is scratch: for large nslot (>= 8192) the
  * two-stage reduction overwrites it with its block sums */
-int cesm_gn_stats_part(const float* part, float* stats, int B, int64_t nslot, int C, int G, int64_t rows_b, float eps,
+int cesm_gn_stats_part(float* part, float* stats, int B, int64_t nslot, int C, int G, int64_t rows_b, float eps,
                        hipStream_t stream);
 int cesm_gn_apply(int dtype, const void* y, const float* stats, const float* gamma, const float* beta,
                   const float* ss, const void* res, void* out, float* ws, int B, int64_t rows_b, int C, int G,

@@ -314,6 +314,40 @@ def test_temporal_attention_core(dev, cdt, Fr):
     assert rel(dtable, rp2.relative_attention_bias.weight.grad) < tol
 
 
+def test_tflash_long_window_full_grid(dev):
+    """the MFMA flash core at config 4's level-0 size (F = 120, 192x288, B = 1): the query / output tiles of the
+    late frames sit > 2^32 B past the tile base, so a tile resource spanning every remaining frame wrapped its
+    32-bit num_records and dropped rows.  Attention is per pixel, so the float64 reference (and the
+    dq / dk / dv it implies) is evaluated on a sample of pixels only (video_net.py:403-454)."""
+    torch.manual_seed(7)
+    B, Fr, HW = 1, 120, 192 * 288
+    scale = 32 ** -0.5
+    freqs = 1.0 / (10000 ** (torch.arange(0, 32, 2).float() / 32))
+    table = torch.randn(32, 8)
+    bias = K.relpos_fwd(table.to(dev), Fr)
+    rot = K.rope_table(freqs.to(dev), Fr)
+    qd = torch.randn(B * Fr * HW, 768, device=dev, dtype=torch.bfloat16)
+    out, lse = K.tattn_fwd(qd, bias, rot, B, Fr, HW, scale)
+    g = torch.randn(B * Fr * HW, 256, device=dev, dtype=torch.bfloat16)
+    dqkv = K.tattn_bwd(qd, out, g, lse, bias, rot, None, B, Fr, HW, scale)
+    torch.cuda.synchronize()
+    pix = torch.cat([torch.tensor([0, 1, HW // 2, HW - 1]), torch.randint(0, HW, (60,))]).to(dev)
+    npx = pix.numel()
+
+    def take(t):  # [B*F*HW, c] -> float64 CPU [B*F*npx, c] (the sampled pixels as a small grid)
+        return t.view(B, Fr, HW, -1)[:, :, pix].reshape(B * Fr * npx, -1).double().cpu()
+
+    qr = take(qd).requires_grad_(True)
+    o = _tattn_ref(qr, bias.double().cpu(), freqs, B, Fr, npx, scale)
+    assert torch.isfinite(out).all()
+    assert rel(take(out), o) < 2e-2
+    o.backward(take(g))
+    assert rel(take(dqkv), qr.grad) < 3e-2
+    # every frame of the late query tiles carries signal (the wrapped resource returned zero rows there)
+    per_frame = take(out).view(Fr, npx, 256).abs().sum((1, 2))
+    assert (per_frame > 0).all()
+
+
 def _sla_ref(qkv, Nf, HW, scale):
     x = qkv.view(Nf, HW, 3, 8, 32).permute(2, 0, 3, 4, 1)  # 3, Nf, h, d, n
     qq = x[0].softmax(dim=-2) * scale

@@ -416,3 +416,87 @@ def test_more_blocks_decadal_window_bf16_forward_backward(dev):
     as the F = 12 whole-net test (video_net.py:403-454 at F = 120)"""
     assert K.conv_fwd_variant(BF, 120, 32, 64, 64, 0, 32, 64, 64, 64, 3, 3, 1, 1, 1) == "conv3x3p_kernel<32,7,true>"
     _bf16_fwd_bwd(dev, (1, 2, 4, 8), 1, 120, 32, 64, 53, "more_blocks F=120")
+
+
+# ------------------------------------------------------------------ per-GPU legs of configs 4 and 5 at full size
+def _full_grid_net(dev, seed=1):
+    cfg = _cfg("more_blocks")
+    torch.manual_seed(seed)
+    prod = UNet(ch_mults=tuple(cfg["unet"]["ch_mults"])).to(dev)
+    prod.compute_dtype = BF
+    return Diffusion(prod).to(dev)
+
+
+def _full_inputs(dev, B, Fr, seed):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    H, W = 192, 288
+    x0 = torch.randn(B, 1, H, W, device=dev, generator=g)
+    cond = torch.randn(B, 1, Fr, H, W, device=dev, generator=g)
+    noise = torch.randn(B, 1, H, W, device=dev, generator=g)
+    t = torch.randint(0, 1000, (B,), device=dev, generator=g)
+    return x0, cond, t, noise
+
+
+def _loss_grads(d, x0, cond, t, noise):
+    for p in d.parameters():
+        p.grad = None
+    loss = d.loss(x0, cond, t=t, noise=noise)
+    loss.backward()
+    torch.cuda.synchronize()
+    return loss.detach().clone(), {n: p.grad.detach().float().clone() for n, p in d.named_parameters()
+                                   if p.grad is not None}
+
+
+def test_decadal_window_full_grid_bf16_step_repeatable(dev, monkeypatch):
+    """config 4's per-GPU leg at its real size: more_blocks, F = 120, 192 x 288, B = 1, bf16 (video_net.py:403-454,
+    train.py:1002).  The long window runs the unfused temporal path (gemm1x1 projections + the tflash MFMA cores,
+    asserted through the calls the step makes); every reduction on that path has a fixed order, so two steps on
+    identical inputs must give the same bits -- loss and every parameter gradient, all finite.  (The oracle cannot
+    run this size in test time; its F = 120 parity is test_more_blocks_decadal_window_*.)"""
+    assert K.conv_fwd_variant(BF, 120, 192, 288, 64, 0, 192, 288, 768, 768, 1, 1, 1, 0, 1) == "gemm1x1_kernel<128>"
+    assert K.conv_fwd_variant(BF, 120, 192, 288, 64, 0, 192, 288, 64, 64, 3, 3, 1, 1, 1) == "conv3x3p_kernel<32,7,true>"
+    seen = set()
+    real_call = K.call
+
+    def rec(name, *a):
+        seen.add(name)
+        return real_call(name, *a)
+
+    monkeypatch.setattr(K, "call", rec)
+    d = _full_grid_net(dev)
+    x0, cond, t, noise = _full_inputs(dev, 1, 120, seed=9)
+    l1, g1 = _loss_grads(d, x0, cond, t, noise)
+    assert {"cesm_tflash_fwd", "cesm_tflash_bwd"} <= seen, sorted(seen)
+    assert not any(n.startswith("cesm_tblock") for n in seen)  # the fused F <= 16 block must not be reached
+    l2, g2 = _loss_grads(d, x0, cond, t, noise)
+    print(f"F=120 full grid: loss {l1.item():.6f} / {l2.item():.6f}, {len(g1)} gradients, "
+          f"peak {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB")
+    assert torch.isfinite(l1) and torch.equal(l1, l2)
+    assert len(g1) == sum(1 for p in d.parameters() if p.requires_grad)
+    for n in g1:
+        assert torch.isfinite(g1[n]).all(), n
+        assert torch.equal(g1[n], g2[n]), n
+
+
+def test_full_grid_bf16_batch5_split(dev):
+    """config 5's per-GPU batch at its real size (more_blocks, 192 x 288 x 12, B = 5: the 40-member batch over 8
+    GPUs, train.py:1002): loss and every gradient equal the sample-weighted mean of a 2 + 3 split -- batch offsets
+    past 4 samples, odd batch sizes in every kernel's grid, the GroupNorm chunking at B = 5.  Gates as
+    test_full_grid_bf16_batch_halves (reduction orders depend on the batch; see there)."""
+    d = _full_grid_net(dev)
+    x0, cond, t, noise = _full_inputs(dev, 5, 12, seed=11)
+
+    def run(sl):
+        return _loss_grads(d, x0[sl], cond[sl], t[sl], noise[sl])
+
+    lf, gf = run(slice(0, 5))
+    la, ga = run(slice(0, 2))
+    lb, gb = run(slice(2, 5))
+    lm = (2 * la.item() + 3 * lb.item()) / 5
+    errs = sorted(((rel(gf[n], (2 * ga[n] + 3 * gb[n]) / 5), n) for n in gf), reverse=True)
+    median = errs[len(errs) // 2][0]
+    print(f"B=5 vs 2+3: loss {lf.item():.6f} vs {lm:.6f}; grad rel median {median:.2e}, "
+          f"worst {errs[0][0]:.2e} ({errs[0][1]})")
+    assert all(torch.isfinite(g).all() for g in gf.values())
+    assert abs(lf.item() - lm) / abs(lm) < 1e-3
+    assert median < BF16_GRAD_MEDIAN_GATE and errs[0][0] < BF16_GRAD_REL_GATE
