@@ -393,7 +393,14 @@ def cpu_leg(dev, full_configs):
     for _ in range(n1):
         R.train_step(d, opt, x0, cond)
     c1 = time.perf_counter() - t0
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    # cores = the intra-op threads the oracle actually ran with; the machine's logical CPUs and this process's
+    # affinity mask are recorded beside it (the GPU box caps OMP_NUM_THREADS at 16 on a many-core host)
     out = {"unit": "samples/s", "cores": torch.get_num_threads(), "kind": "port", "cpu_model": _cpu_model_name(),
+           "os_cpu_count": os.cpu_count(), "sched_affinity_cpus": affinity,
            "config1_samples_per_s": round(2 * n1 / c1, 4),
            "config1_sample": f"config/baseline F=8 32x48 B=2: 3 warm-up + {n1} timed steps, {c1:.2f}s"}
     full = {}

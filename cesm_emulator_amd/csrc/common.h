@@ -243,9 +243,12 @@ __device__ __forceinline__ int opaque_v(int v) {
 }
 
 // fp32 weight -> A-fragment image (frag_image layout) of A = W diag(gamma) (trans = 0: A[m][k] = W[m][k] g[k],
-// W row-major [M][K]) or of A = (W diag(gamma))^T (trans = 1: A[m][k] = W[k][m] g[m], W [K][M])
+// W row-major [M][K]) or of A = (W diag(gamma))^T (trans = 1: A[m][k] = W[k][m] g[m], W [K][M]).  The first nq rows
+// of W (the to_qkv query rows) are multiplied by qscale too: the attention scale folded into the weights, so the
+// kernels' q epilogue has no multiply (its gradient is restored in twh_dw_reduce_kernel).
 __global__ void frag_image_f32_kernel(const float* __restrict__ W, const float* __restrict__ gamma,
-                                      bf16* __restrict__ img, int M, int K, int trans) {
+                                      bf16* __restrict__ img, int M, int K, int trans, int nq = 0,
+                                      float qscale = 1.f) {
   const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (v >= (int64_t)M * K / 8) return;
   const int lane = (int)(v & 63);
@@ -259,19 +262,22 @@ __global__ void frag_image_f32_kernel(const float* __restrict__ W, const float* 
     const int k = k0 + e;
     const float w = trans ? W[(int64_t)k * M + m] : W[(int64_t)m * K + k];
     const float gm = gamma ? gamma[trans ? m : k] : 1.f;
-    o[e] = (bf16)(w * gm);
+    const float qs = (trans ? k : m) < nq ? qscale : 1.f;
+    o[e] = (bf16)(w * gm * qs);
   }
   *reinterpret_cast<bf16x8*>(img + v * 8) = o;
 }
 
-// slab [nblk][J][C] (dW' partials) -> dW (+)= (sum_blk slab) diag(gamma); tmp[j][c] = W[j][c] * sum_blk slab
+// slab [nblk][J][C] (dW' partials) -> dW (+)= (sum_blk slab) diag(gamma); tmp[j][c] = W[j][c] * sum_blk slab.
+// Rows j < nq were computed against weights carrying qscale (frag_image_f32_kernel): their sums are scaled back.
 __global__ void twh_dw_reduce_kernel(const float* __restrict__ slab, int nblk, const float* __restrict__ w,
                                      const float* __restrict__ gamma, float* __restrict__ dw, float* __restrict__ tmp,
-                                     int J, int C, int accumulate) {
+                                     int J, int C, int accumulate, int nq = 0, float qscale = 1.f) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= (int64_t)J * C) return;
   float s = 0.f;
   for (int k = 0; k < nblk; ++k) s += slab[(int64_t)k * J * C + e];
+  if (e / C < nq) s *= qscale;
   const int c = (int)(e % C);
   if (dw) dw[e] = (accumulate ? dw[e] : 0.f) + s * gamma[c];
   tmp[e] = s * w[e];

@@ -496,11 +496,8 @@ __device__ __forceinline__ int h3_off(int row, int ch) { return row * H3_LD + ((
 #ifndef H3_BIG
 #define H3_BIG 1  // A/B knob: 448-pixel tiles with 64 co x 112 px wave tiles (0 = 256-pixel tiles, 64 x 64)
 #endif
-#ifndef H3_DB
-#define H3_DB 0  // A/B knob: double-buffered chunks in the big-tile kernel (one block per CU): measured slower, conv
-                 // total per step 64.0 -> 68.2 ms (levels 1-3 -20..-28 %; the second co-resident block hides the
-                 // staging better than the in-block prefetch at one wave per SIMD; profiles/r3_h3db_conv_ab.txt)
-#endif
+// (Round 3: double-buffered chunks at one block per CU measured slower, conv total 64.0 -> 68.2 ms per step: the
+// second co-resident block hides the staging better than an in-block prefetch.  Removed.)
 template <int TW, int NJv = 4>
 __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
                                                               const bf16* __restrict__ w, const float* __restrict__ bias,
@@ -513,13 +510,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
   // per 448 instead of 256 pixels; 77 KiB of LDS, still 2 blocks per CU
   static_assert(NJv == 4 || (NJv == 7 && H3_SQ && H3_DMA), "big tiles need square wave tiles and DMA staging");
   constexpr int NROWS = (NJv == 7 ? 16 : 10) * H3_P;
-  // H3_DB (big tiles): two chunk buffers (152 KiB, one block per CU): chunk ch+1's DMA is issued before chunk ch's
-  // MFMAs instead of the second co-resident block covering the wait
-  constexpr int NBUF = (H3_DB && NJv == 7) ? 2 : 1;
-  __shared__ __attribute__((aligned(16))) bf16 shm[NBUF][NROWS * H3_LD];
-  __shared__ __attribute__((aligned(16))) bf16 swm[NBUF][9 * H3_BN * H3_LD];
-  bf16* sh = shm[0];
-  bf16* sw = swm[0];
+  __shared__ __attribute__((aligned(16))) bf16 sh[NROWS * H3_LD];
+  __shared__ __attribute__((aligned(16))) bf16 sw[9 * H3_BN * H3_LD];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   // wave tile: H3_SQ (round 3) 64 co x 16 NJv px = 4 x NJv MFMA tiles per wave (8 fragment reads per 16 MFMAs per
   // tap at NJv = 4); else 32 co x 128 px = 2 x 8 (10 reads per 16 MFMAs: the 4 waves' reads exceeded the LDS
@@ -548,9 +540,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
   // 16-B piece): 1-KiB pieces of 16 LDS rows, each lane fetching the global chunk that the row swizzle puts in
   // its slot (chunk = slot ^ ((row >> 1) & 2)); halo rows outside the tile / image read as zeros (out-of-range
   // offset).  The second co-resident block computes while this one waits.
-  auto stage = [&](int ch, int buf) {
-    bf16* const sh = shm[buf];
-    bf16* const sw = swm[buf];
+  auto stage = [&](int ch) {
     const int c0 = ch * 32;
     const bf16* src;
     int cs, cc;
@@ -587,12 +577,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
       __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(sw + q * 512), 16,
                                                ((co * 9 + tap) * Cin + chunk * 8) * 2, 0, 0, 0);
     }
-    if (NBUF == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
 #else
   // stage one 32-channel chunk: global -> registers -> LDS (transient registers; the second
   // co-resident block computes while this one loads)
-  auto stage = [&](int ch, int) {
+  auto stage = [&](int ch) {
     const int c0 = ch * 32;
     const bf16* src;
     int cs, cc;
@@ -667,20 +657,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
     for (int kx = 0; kx < 3; ++kx) boff[j][kx] = h3_off(hoff[j] + kx, lg);
 #pragma unroll
   for (int i = 0; i < NI; ++i) aoff[i] = h3_off(wr * 32 + i * 16 + lr, lg);
-  if (NBUF == 2) stage(0, 0);
   for (int ch = 0; ch < nchunk; ++ch) {
-    if (NBUF == 2) {
-      // chunk ch has landed (this wave's DMA) and every wave is past chunk ch-1, whose buffer the next DMA reuses
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (ch + 1 < nchunk) stage(ch + 1, (ch + 1) & 1);
-      sh = shm[ch & 1];
-      sw = swm[ch & 1];
-    } else {
-      if (ch) __syncthreads();  // previous chunk fully consumed
-      stage(ch, 0);
-      __syncthreads();
-    }
+    if (ch) __syncthreads();  // previous chunk fully consumed
+    stage(ch);
+    __syncthreads();
 #if H3_PIPE
     // the 10 fragment reads of tap t+1 are issued between the 16 MFMAs of tap t (two register sets), so no
     // MFMA waits on a read issued just before it (the compiler's order was read -> wait -> 2 MFMAs)
@@ -1320,14 +1300,9 @@ __device__ __forceinline__ void cp_taps(const char* sh, const char* sw, const in
 // bf16 in the stage just consumed and writes full 128-B pixel rows (+ residual) with exactly 2*NG
 // buffer stores per wave, so the next step waits for its DMA with vmcnt(2*NG), not for the stores.
 // ----------------------------------------------------------------------------------------
-// Dynamic item queue of conv3x3p (round 3): [0] next dynamic item - gridDim.x, [1] blocks finished.  Each block
-// takes item blockIdx.x first, then claims the next item one item ahead (thread 0, agent-scope atomic issued at the
-// item's first step, published through LDS at its second step's barrier), so a block slowed down by co-running
-// kernels (weight gradients on a second stream, RCCL all-reduces overlapped with the backward) takes fewer items
-// instead of leaving a static-split tail.  The last block to finish resets both counters for the next launch
-// (launches of this kernel are stream-ordered).  Outputs do not depend on the assignment (every item writes its own
-// pixels and GroupNorm slots).
-__device__ int g_cp_queue[2];
+// Items are split statically (item it = blockIdx.x + k * gridDim.x): the kernel keeps no state between launches,
+// so concurrent launches (two streams, graph branches, two model instances) are independent.  (Round 3 claimed
+// items from a process-global atomic counter instead: 596.6 vs 599.1 us per launch, not worth the hidden state.)
 
 template <int TW, int NG, bool RW, int NST = 2, int HPW = CW_HPW>
 __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
@@ -1335,7 +1310,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
                                                           const bf16* __restrict__ res, const bf16* __restrict__ res2,
                                                           bf16* __restrict__ y1, bf16* __restrict__ y2, ConvGeom g,
                                                           int tiles_x, int tiles_per_img, int TH, int ncob, int nitems,
-                                                          int dbg, float* __restrict__ gnp, int gn_fimg) {
+                                                          float* __restrict__ gnp, int gn_fimg) {
   static_assert(TW + 2 <= CP_PITCH && NG <= 8 && HPW <= CW_HPW, "tile geometry");
   static_assert(NST == 2 || (NST == 3 && RW), "3 stages only with resident weights");
   // one LDS array (a second __shared__ object can make hipcc drain the DMA before ds_reads):
@@ -1350,7 +1325,6 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
   __shared__ __attribute__((aligned(1024))) char lds[NST * STG + WRES + BIASB + 16];
   char* wres = lds + NST * STG;
   float* sbias = reinterpret_cast<float*>(lds + NST * STG + WRES);
-  int* s_next = reinterpret_cast<int*>(lds + NST * STG + WRES + BIASB);  // the claimed next item
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const int HP = (TH + 2) * CP_PITCH;
@@ -1361,7 +1335,6 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
   const int prow = lane >> 2, pslot = lane & 3;
   const int nmine = nitems > (int)blockIdx.x ? (nitems - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
   const int nsteps = nmine * nchunk;
-  const bool dynq = NST == 2 && nchunk >= 2 && !(dbg & 16);  // dynamic item queue (static split: dbg bit 16)
 
   // per-lane halo row -> tile-relative (hy, hx) of piece k (item independent); -1: zero row
   int hrel[HPW];
@@ -1457,10 +1430,9 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
     if (q < nsteps) issue(q, (int)blockIdx.x + (q / nchunk) * (int)gridDim.x, q % nchunk);
   int s = 0;
   bool epi = false;
-  int claim = 0;  // thread 0: the atomically claimed next item (dynq)
   int it = (int)blockIdx.x;
   for (int k = 0; it < nitems; ++k) {
-    int nxt = it + (int)gridDim.x;  // static split; dynq: replaced at the item's second step
+    const int nxt = it + (int)gridDim.x;
     f32x4 acc[4][NG];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -1487,51 +1459,38 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       epi = false;
-      if (dynq && ch == 1) {  // publish the claimed next item (its atomic is older than this step's DMA: landed)
-        if (tid == 0) *s_next = claim;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      }
       __builtin_amdgcn_s_barrier();                     // ... for every wave; step s-1's reads are done
-      if (dynq && ch == 1) nxt = *s_next;
-      if (dynq && ch == 0 && tid == 0)  // claim the item after this one (returns long before step 1 needs it)
-        claim = (int)gridDim.x + __hip_atomic_fetch_add(&g_cp_queue[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const char* sh = lds + (s % NST) * STG;
       const char* sw = RW ? wres + ch * CW_WROWS * 64 : sh + CW_HROWS * 64;
       const int sp = s + NST - 1;  // step prefetched now, into the stage step s-1 used
       // its item / chunk: NST = 2: the next chunk of this item, or the next item's first chunk
       const int sp_it = NST == 2 ? (ch + 1 < nchunk ? it : nxt) : (int)blockIdx.x + (sp / nchunk) * (int)gridDim.x;
       const int sp_ch = NST == 2 ? (ch + 1 < nchunk ? ch + 1 : 0) : sp % nchunk;
-      const bool pf = (NST == 2 ? sp_it < nitems : sp < nsteps) && !(dbg & 1);
-      if ((dbg & 2) || !RW) {  // spreading the 19-piece (!RW) DMA over the taps spills at NG = 8
+      const bool pf = NST == 2 ? sp_it < nitems : sp < nsteps;
+      if constexpr (!RW) {  // spreading the 19-piece (!RW) DMA over the taps spills at NG = 8
         if (pf) issue(sp, sp_it, sp_ch);
-        if (!(dbg & 2)) cp_taps<NG>(sh, sw, bad, a_lane, acc);
-      } else if (pf) {
-        // the prefetch DMA spread over this step's taps (issuing all of it up front stalls the wave on
-        // the vector-memory queue before its first MFMA)
-        step_src(sp, sp_it, sp_ch);
+        cp_taps<NG>(sh, sw, bad, a_lane, acc);
+      } else {
+        // the prefetch DMA spread over this step's taps (issuing all of it up front stalls the wave on the
+        // vector-memory queue before its first MFMA).  ONE tap loop for both cases (pf is a uniform branch inside
+        // the hook): with a second, hook-less copy of the loop the compiler gave the two copies different
+        // accumulator registers and copied all 112 of them AGPR -> VGPR -> AGPR at every step (224 v_accvgpr
+        // moves per 252 MFMAs)
+        if (pf) step_src(sp, sp_it, sp_ch);
         auto hook = [&](int tap) {
+          if (pf) {
 #pragma unroll
-          for (int k = 0; k < NPIECE; ++k)
-            if (k * 9 / NPIECE == tap) issue_piece(k);
+            for (int k = 0; k < NPIECE; ++k)
+              if (k * 9 / NPIECE == tap) issue_piece(k);
+          }
         };
         cp_taps<NG>(sh, sw, bad, a_lane, acc, hook);
-      } else {
-        cp_taps<NG>(sh, sw, bad, a_lane, acc);
       }
     }
     int n, y0, x0, cob;
     item_geo(it, n, y0, x0, cob);
     const int n0 = cob * 64;
     it = nxt;
-    if (dbg & 4) {  // debug: no epilogue (keep the accumulators live)
-      float sacc = 0.f;
-#pragma unroll
-      for (int j = 0; j < NG; ++j)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) sacc += acc[i][j][0];
-      if (sacc == 12345.f) y1[0] = (bf16)sacc;
-      continue;
-    }
     // epilogue through LDS, wave-private, in rounds of up to 4 fragment groups (64 px): (acc + bias)
     // -> bf16 rows [64 px][CP_ELD] in this wave's slice of the stage just consumed (barrier: every wave
     // is past its taps), then 8 lanes per pixel write full 128-B rows with 16-B buffer stores (+
@@ -1606,7 +1565,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
             const bool ok = p < TH * TW && oy < g.Ho && ox < g.Wo;
             const int off = (ok ? oy * g.Wo + ox : 0) * cstride + cofs;
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, rows[u]), yrs,
-                                                   ok && !(dbg & 8) ? off * 2 : 0x7ffffff0, 0, 0);
+                                                   ok ? off * 2 : 0x7ffffff0, 0, 0);
           }
         }
       } else {
@@ -1657,12 +1616,6 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
       }
     }
     epi = true;
-  }
-  if (dynq && tid == 0) {  // the last block out resets the queue for the next launch
-    if (__hip_atomic_fetch_add(&g_cp_queue[1], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
-      __hip_atomic_store(&g_cp_queue[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&g_cp_queue[1], 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
   }
 }
 
@@ -2247,17 +2200,12 @@ __device__ __forceinline__ int wgb_swz(int r) {  // XOR on 4-element chunk index
 // over dY, which re-read the whole tensor).
 // (BIAS: compile-time, so the plain instantiation keeps its register count — the bias accumulators
 // pushed the BM = 256 kernel past 128 VGPRs, a wave per SIMD fewer and 43 % slower.)
-// WW_XCD: 1-D grid, the (co block, K column block) tiles of one pixel split on ONE XCD back to back (linear id mod 8
-// = XCD), so the split's dY / x rows are fetched into that XCD's L2 once and re-read there by the split's other tiles
-// (the 3-D grid deals a split's tiles to consecutive ids = different XCDs)
-#ifndef WW_XCD
-#define WW_XCD 0  // measured slower: whole step 130.4 -> 131.5 ms (profiles/r3_gn_iters_ab.txt, wwxcd rows)
-#endif
+// (Round 3 measured an XCD-grouped 1-D grid for a pixel split's tiles: whole step 130.4 -> 131.5 ms; removed.)
 template <int BM, bool BIAS = false>
 __global__ __launch_bounds__(256) void wgrad_wide_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
                                                          const bf16* __restrict__ dy1, const bf16* __restrict__ dy2,
                                                          float* __restrict__ slab, float* __restrict__ bslab, ConvGeom g,
-                                                         int M, int px_per_split, int gx = 0, int gy = 0, int nsplit = 0) {
+                                                         int M, int px_per_split) {
   constexpr int VPRY = BM / 8, RPPY = 256 / VPRY, NPY = WG_BP / RPPY;
   constexpr int MT = BM / 64;  // 16-row co tiles per wave
   __shared__ __attribute__((aligned(16))) bf16 tY[2][WG_BP * BM];
@@ -2265,15 +2213,7 @@ __global__ __launch_bounds__(256) void wgrad_wide_kernel(const bf16* __restrict_
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const int Cin = g.C1 + g.C2;
-  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-  if (gx > 0) {  // WW_XCD mapping (uniform)
-    const int L = blockIdx.x, j = L >> 3, nt = gx * gy;
-    const int t = j % nt;
-    bz = (j / nt) * 8 + (L & 7);
-    if (bz >= nsplit) return;  // padded ids (whole block)
-    bx = t % gx;
-    by = t / gx;
-  }
+  const int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
   const int co0 = bx * BM;
   const int kcol0 = by * 64;
   const int tap = kcol0 / Cin;
@@ -2591,14 +2531,10 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_bf16_kernel(const bf16* __res
 // input halo is kept as two 32-channel planes so the fragment reads are the 64-ci kernel's.
 constexpr int W3_PLANE = (W3_TH + 2) * W3_P * 32;  // halo plane (bf16 elements)
 
-// WG4 (round 3): 4 waves (one per SIMD, 512 registers), wave = one 16-channel ci tile x ALL four co tiles x 9
-// taps (144 accumulators): 26 transposed fragment reads per 36 MFMAs per pixel row instead of 22 per 18 (the
-// 8-wave form read 0.61 KiB of LDS per MFMA, past what the LDS array serves at the MFMA rate)
-#ifndef WG4
-#define WG4 0  // measured neutral (63.69 vs 63.58 ms conv total): the wgrads lose latency hiding at 1 wave/SIMD
-#endif
-constexpr int WG_NT = WG4 ? 256 : 512;  // threads per block
-constexpr int WG_NI = WG4 ? 4 : 2;      // co tiles per wave
+// (Round 3 measured a 4-wave form -- one wave per SIMD, 144 accumulators, all four co tiles per wave -- as neutral,
+// 63.69 vs 63.58 ms conv total per step: fewer LDS reads per MFMA, less latency hiding.  Removed.)
+constexpr int WG_NT = 512;  // threads per block
+constexpr int WG_NI = 2;    // co tiles per wave
 __global__ __launch_bounds__(WG_NT, 1) void wgrad3x3c64_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
                                                              const bf16* __restrict__ dy1, const bf16* __restrict__ dy2,
                                                              float* __restrict__ slab, ConvGeom g, int tiles_x,
@@ -2606,7 +2542,7 @@ __global__ __launch_bounds__(WG_NT, 1) void wgrad3x3c64_kernel(const bf16* __res
   __shared__ __attribute__((aligned(16))) bf16 sdy[W3_TH * W3_TW * 64];  // 32 KB, 128-B rows
   __shared__ __attribute__((aligned(16))) bf16 shx[2 * W3_PLANE];        // 2 x 30 KB, 64-B rows
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int cot0 = WG4 ? 0 : (wid >> 2) * 2, cit = wid & 3;
+  const int cot0 = (wid >> 2) * 2, cit = wid & 3;
   const int co0 = blockIdx.x * 64, ci0 = blockIdx.y * 64;
   const int Cin = g.C1 + g.C2;
   const bf16* xs; int xcs, xcc;
@@ -3055,7 +2991,7 @@ __global__ __launch_bounds__(WG_NT, 1) void wgrad3x3w36c64_kernel(const bf16* __
   __shared__ __attribute__((aligned(16))) bf16 sdy[W36_NP * 64];  // 36 KB, 128-B rows
   __shared__ __attribute__((aligned(16))) bf16 shx[2 * W3_PLANE];  // 2 x 30 KB, 64-B rows
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int cot0 = WG4 ? 0 : (wid >> 2) * 2, cit = wid & 3;
+  const int cot0 = (wid >> 2) * 2, cit = wid & 3;
   const int co0 = blockIdx.x * 64, ci0 = blockIdx.y * 64;
   const int Cin = g.C1 + g.C2;
   const bf16* xs; int xcs, xcc;
@@ -3944,31 +3880,28 @@ int conv_fwd_launch(int dtype, const void* x1, const void* x2, const void* wp, c
     case CFV_P32_3STAGE:
     case CFV_P32_RW:
     case CFV_P32: {
-      const int dbg = (getenv_flag("CESM_DBG_NODMA") ? 1 : 0) | (getenv_flag("CESM_DBG_NOMFMA") ? 2 : 0) |
-                      (getenv_flag("CESM_DBG_NOEPI") ? 4 : 0) | (getenv_flag("CESM_DBG_NOSTORE") ? 8 : 0) |
-                      (getenv_flag("CESM_CONV_STATIC") ? 16 : 0);  // static item split instead of the queue
       const int tx = (int)cdiv(Wo, TW), ty = (int)cdiv(Ho, TH);
       const int ncob = Cout / 64;
       const int nitems = Nb * tx * ty * ncob;
       const int nblk = std::min(nitems, cesm_num_cus());
       if (pl.v == CFV_P36_RW)
         conv3x3p_kernel<36, 8, true><<<nblk, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, tx * ty,
-                                                               TH, ncob, nitems, dbg, gnp, gn_fimg);
+                                                               TH, ncob, nitems, gnp, gn_fimg);
       else if (pl.v == CFV_P36)
         conv3x3p_kernel<36, 8, false><<<nblk, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx,
-                                                                tx * ty, TH, ncob, nitems, dbg, gnp, gn_fimg);
+                                                                tx * ty, TH, ncob, nitems, gnp, gn_fimg);
       else if (pl.v == CFV_P32_3STAGE)
         // experimental: 8 x 32 tiles, 3 LDS stages (two steps of DMA in flight) - measured slower than
         // 2 stages of 14 x 32 tiles (345 vs 315 us): the level-0 conv is HBM-bound (block-0 stamps: 2.2 GHz,
         // DMA-only 175 us vs MFMA-only 166 us per launch), deeper prefetch does not add overlap
         conv3x3p_kernel<32, 4, true, 3, 7><<<std::min(nitems, cesm_num_cus()), 256, 0, stream>>>(
-            bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, tx * ty, TH, 1, Nb * tx * ty, dbg, nullptr, 1);
+            bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, tx * ty, TH, 1, Nb * tx * ty, nullptr, 1);
       else if (pl.v == CFV_P32_RW)
         conv3x3p_kernel<32, 7, true><<<nblk, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, tx * ty,
-                                                               TH, ncob, nitems, dbg, gnp, gn_fimg);
+                                                               TH, ncob, nitems, gnp, gn_fimg);
       else
         conv3x3p_kernel<32, 7, false><<<nblk, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx,
-                                                                tx * ty, TH, ncob, nitems, dbg, gnp, gn_fimg);
+                                                                tx * ty, TH, ncob, nitems, gnp, gn_fimg);
       break;
     }
     case CFV_W36:
@@ -4191,14 +4124,12 @@ int cesm_conv_wgrad(int dtype, const void* x1, const void* x2, const void* dy1, 
     // wide-tile kernel; nsplit from the caller sized the slab for 64-row tiles, keep it
     const int bm = (Cout % 256 == 0 && Co1 % 256 == 0) ? 256 : ((Cout % 128 == 0 && Co1 % 128 == 0) ? 128 : 64);
     const int gx = Cout / bm, gy = (int)(K / 64);
-    dim3 gw(gx, gy, nsplit);
-    if (WW_XCD) gw = dim3((unsigned)(cdiv(nsplit, 8) * 8 * gx * gy));
+    const dim3 gw(gx, gy, nsplit);
     auto launch = [&](auto bmc, auto biasc) {
       constexpr int BMv = decltype(bmc)::value;
       constexpr bool Bv = decltype(biasc)::value;
       wgrad_wide_kernel<BMv, Bv><<<gw, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
-                                                         (const bf16*)dy2, slab, bslab, g, (int)M, (int)pps,
-                                                         WW_XCD ? gx : 0, gy, nsplit);
+                                                         (const bf16*)dy2, slab, bslab, g, (int)M, (int)pps);
     };
     using T0 = std::false_type;
     using T1 = std::true_type;

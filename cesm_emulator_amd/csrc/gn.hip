@@ -252,31 +252,15 @@ __device__ __forceinline__ void gn_coef8(const GnAffine& q, int b, int c0, int C
   }
 }
 
-// The backward per sample (cesm_gn_bwd): reduce + finalize + apply of one sample back to back while its
-// (dout, y) pair fits this budget, so gn_bwd_apply could re-read them from the Infinity Cache instead of HBM.
-// Measured off: the whole bench step 132.0 -> 138.0 ms with it (the 3 launches per sample and the one-block
-// finalize per sample cost more than the on-die re-read saves; non-temporal reduction loads 139.6 ms); the
-// reversed sample order in gn_apply (GN_FWD_REV) was neutral (138.0 vs 138.1); profiles/r3_gn_per_sample_ab.txt
-#ifndef GN_PER_SAMPLE
-#define GN_PER_SAMPLE 0
-#endif
-#ifndef GN_MALL_BYTES
-#define GN_MALL_BYTES (176ll << 20)
-#endif
-#ifndef GN_PS_NT
-#define GN_PS_NT false  // the per-sample reduction's loads: default policy (false) or non-temporal (true)
-#endif
-// gn_apply: samples in reverse order (the producing conv wrote the last ones last; they may still be on-die)
-#ifndef GN_FWD_REV
-#define GN_FWD_REV 0
-#endif
+// (Round 3 measured two Infinity-Cache orders and removed them: the backward one sample at a time so gn_bwd_apply
+// re-reads (dout, y) on-die -- whole step 132.0 -> 138.0 ms; gn_apply in reversed sample order -- neutral.)
 
 // grid (nchunk, B): thread = (8-channel group c8, row lane rr), rows strided by 256/(C/8)
 template <typename T>
 __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ y, const GnAffine coef,
                                                        const T* __restrict__ res, T* __restrict__ out, int64_t rows_b,
                                                        int C, int nchunk) {
-  const int b = GN_FWD_REV ? gridDim.y - 1 - blockIdx.y : blockIdx.y, chunk = blockIdx.x;
+  const int b = blockIdx.y, chunk = blockIdx.x;
   const int cv = C / 8, rl = 256 / cv;
   const int c8 = threadIdx.x % cv, rr = threadIdx.x / cv;
   if (rr >= rl) return;
@@ -574,31 +558,8 @@ int cesm_gn_bwd(int dtype, const void* dout, const void* y, const float* stats, 
   const double count = (double)rows_b * (C / G);
   const GnAffine aff{stats, gamma, beta, ss, G};
   const int nch = gn_apply_chunks(rows_b, C);
-  const int64_t esz = dtype == CESM_DT_BF16 ? 2 : 4;
   float* part = ws;
   int rc;
-  if (GN_PER_SAMPLE && B > 1 && 2 * rows_b * C * esz <= (int64_t)GN_MALL_BYTES) {
-    // one sample at a time, last sample first: the reduction's reads of (dout, y) of a sample (<= GN_MALL_BYTES)
-    // are still in the 256-MiB Infinity Cache when gn_bwd_apply re-reads them, and the last sample's dout is the
-    // part of it the producing kernel wrote last.  The chunk partials of one sample reuse one region.
-    const int nc1 = gn_nchunk(rows_b, C, 1);  // <= 1024 <= max(B * 256, 1024)
-    float* pb = part + (int64_t)nc1 * C * 3;
-    float* E = pb + (int64_t)B * C * 3 + (int64_t)B * C * 2;
-    rc = dispatch_dt(dtype, [&](auto* tp) {
-      using T = std::remove_pointer_t<decltype(tp)>;
-      for (int b = B - 1; b >= 0; --b) {
-        gn_bwd_reduce_kernel<T, GN_PS_NT><<<dim3(nc1, 1), 256, 0, stream>>>((const T*)dout, (const T*)y, aff, part,
-                                                                           rows_b, C, nc1, b);
-        gn_bwd_finalize_kernel<<<dim3(1, (unsigned)cdiv(C, 64)), 64 * GNF_KG, 0, stream>>>(
-            part, stats, gamma, beta, ss, dss, pb, E, C, G, nc1, count, (float)rows_b, b);
-        gn_bwd_apply_kernel<T><<<dim3(nch, 1), 256, 0, stream>>>((const T*)dout, (const T*)y, aff, E, (T*)dy, rows_b,
-                                                                 C, nch, b);
-      }
-    });
-    if (rc) return rc;
-    gn_param_grad_kernel<<<(unsigned)cdiv(C, 256), 256, 0, stream>>>(pb, dgamma, dbeta, dbias, B, C, accumulate);
-    return cesm_launch_status();
-  }
   const int nchunk = gn_nchunk(rows_b, C, B);
   float* pb = part + (int64_t)B * nchunk * C * 3;
   float* coef = pb + (int64_t)B * C * 3;

@@ -717,6 +717,23 @@ __device__ __forceinline__ bf16x8 kslot_gather_raw(const bf16* tile, int rb, int
   return kslot_raw(__builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tile + rg_at(rb, hs_off<R>(4 * g + q, c0 + 4 * p)))));
 }
 
+// The attention-core products over frames (P V, dS K, dS^T Q, P^T dO) have K = 16 frames: they run as
+// v_mfma_f32_16x16x16_bf16 on 4-element operands -- the k-slot gather's hardware-transpose result as it comes, P /
+// dS packed from the lane's 4 score entries -- half the MFMA cycles of the 16x16x32 form with slots 4..7 zeroed,
+// and no zero fill moves.  Slot (g, e) pairs the same entries in both forms.
+__device__ __forceinline__ f32x4 mfma_k16(const s16x4 a, const s16x4 b, const f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ s16x4 bf16x4_bits(float a, float b, float c, float d) {
+  const bf16x4 v = {(bf16)a, (bf16)b, (bf16)c, (bf16)d};
+  return __builtin_bit_cast(s16x4, v);
+}
+template <int R>
+__device__ __forceinline__ s16x4 kslot4(const bf16* tile, int rb, int c0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tile + rg_at(rb, hs_off<R>(4 * g + q, c0 + 4 * p))));
+}
+
 // hardware-transpose read of a head slice: lane (g, i) <- tile[r0 + 4g + e][c0 + i]
 template <int R>
 __device__ __forceinline__ s16x4 tr4_hs(const bf16* tile, int r0, int c0, int lane) {
@@ -832,6 +849,66 @@ __device__ __forceinline__ void tw_qkv(const bf16* __restrict__ wqkv, const bf16
           store4(dst + hs_off<R>(vt * 16 + lr, d0), o4);
         }
       }
+    }
+  }
+}
+
+#ifndef TW_QKV_B
+#define TW_QKV_B 1  // tw_fwd: batched q / k / v phase (tw_qkv_b); 0 = round 3's per-tile MFMA -> epilogue chains
+#endif
+// RoPE of dims d0..d0+3 (two pairs) with preloaded coefficients cs = (c0, s0, c1, s1)
+__device__ __forceinline__ void rope4c(float* o4, const f32x4 cs) {
+#pragma unroll
+  for (int pr = 0; pr < 2; ++pr) {
+    const float c = cs[2 * pr], sn = cs[2 * pr + 1];
+    const float a0 = o4[2 * pr], a1 = o4[2 * pr + 1];
+    o4[2 * pr] = a0 * c - a1 * sn;
+    o4[2 * pr + 1] = a1 * c + a0 * sn;
+  }
+}
+// q'|k'|v tiles of one head, batched per kind (round 4): the kind's 2 x NV tiles (independent accumulators) are
+// issued back to back, the next kind's weight fragments are in flight meanwhile (double buffer), and the RoPE
+// coefficients are read from LDS before the MFMAs, so the epilogue waits on nothing.  (Round 3 ran each tile as
+// load-wait -> 2 MFMAs -> s_nop -> LDS read -> wait -> VALU -> store, one chain at a time.)
+template <int C, int NV, bool QSCALE = true>
+__device__ __forceinline__ void tw_qkv_b(const bf16* __restrict__ wqkv, const bf16x8 (&xf)[NV][C / 32], int h,
+                                         const int (&fr)[NV], float scale, const float* rot, bf16* sq, bf16* sk,
+                                         bf16* sv, int lr, int lg) {
+  using T = TW<C, NV>;
+  constexpr int R = NV * 16;
+  // 6 (kind, half) column tiles; the next tile's weight fragments in flight while this one computes
+  bf16x8 a[2][T::KS];
+  auto ld = [&](int ct, int buf) {
+#pragma unroll
+    for (int ks = 0; ks < T::KS; ++ks) a[buf][ks] = ld_img(wqkv, (ct >> 1) * 16 + h * 2 + (ct & 1), T::KS, ks, lg * 16 + lr);
+  };
+  ld(0, 0);
+#pragma unroll
+  for (int ct = 0; ct < 6; ++ct) {
+    const int buf = ct & 1, kind = ct >> 1, u = ct & 1;
+    if (ct + 1 < 6) ld(ct + 1, buf ^ 1);
+    f32x4 cs[NV];
+    if (kind < 2) {
+#pragma unroll
+      for (int vt = 0; vt < NV; ++vt) cs[vt] = *reinterpret_cast<const f32x4*>(rot + fr[vt] * RS + u * 16 + lg * 4);
+    }
+    f32x4 acc[NV];
+#pragma unroll
+    for (int vt = 0; vt < NV; ++vt) {
+      acc[vt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < T::KS; ++ks) acc[vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[buf][ks], xf[vt][ks], acc[vt], 0, 0, 0);
+    }
+    bf16* dst = kind == 0 ? sq : (kind == 1 ? sk : sv);
+#pragma unroll
+    for (int vt = 0; vt < NV; ++vt) {
+      float o4[4] = {acc[vt][0], acc[vt][1], acc[vt][2], acc[vt][3]};
+      if (QSCALE && kind == 0) {  // (folded weights: the scale is in the q rows)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o4[r] *= scale;
+      }
+      if (kind < 2) rope4c(o4, cs[vt]);
+      store4(dst + hs_off<R>(vt * 16 + lr, u * 16 + lg * 4), o4);
     }
   }
 }
@@ -964,10 +1041,11 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
       for (int ct = 0; ct < T::CT; ++ct) wo[ct] = ld_img(wout, ct, INNER / 32, h, lane);  // image of W_out [C][256]
     }
     if constexpr (PREF) {
-      tw_qkv_pre<C, NV>(wq, xf, fr, scale, rot, sq, sk, sv, lr, lg);
+      tw_qkv_pre<C, NV>(wq, xf, fr, FOLD ? 1.f : scale, rot, sq, sk, sv, lr, lg);  // FOLD: scale in the weights
       if (h + 1 < NH) tw_load_wq<C, NV>(wq, wqkv, h + 1, lr, lg);  // in flight during the core
     } else {
-      tw_qkv<C, NV, false>(wqkv, xf, h, fr, scale, rot, sq, sk, sv, lr, lg);  // two-tile weight batches
+      if constexpr (TW_QKV_B && C == 64) tw_qkv_b<C, NV, !FOLD>(wqkv, xf, h, fr, scale, rot, sq, sk, sv, lr, lg);
+      else tw_qkv<C, NV, false>(wqkv, xf, h, fr, FOLD ? 1.f : scale, rot, sq, sk, sv, lr, lg);  // two-tile batches
     }
     // bias (log2 units) of this lane's 4 entries (i = lr, j = 4g + r); -inf masks padding frames
     float bt[4];
@@ -997,12 +1075,12 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
         const bf16x8 qb = ld16(sq + rr);
         st[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qb, z4, 0, 0, 0);
       }
-      bf16x8 va[PG][2];
+      s16x4 va[PG][2];
 #pragma unroll
       for (int u = 0; u < PG; ++u)
 #pragma unroll
-        for (int half = 0; half < 2; ++half) va[u][half] = kslot_gather_raw<R>(sv, (pg + u) * F4, half * 16, lane);  // P^T is 0 at keys >= F
-      bf16x8 pb[PG];
+        for (int half = 0; half < 2; ++half) va[u][half] = kslot4<R>(sv, (pg + u) * F4, half * 16, lane);  // P^T is 0 at keys >= F
+      s16x4 pb[PG];
 #pragma unroll
       for (int u = 0; u < PG; ++u) {
         const int p = p0 + pg + u;
@@ -1023,16 +1101,14 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
         l = grp4_sum(l);
         if (lse && lg == 0 && lr < F && p < HW) lse[(((int64_t)b * NH + h) * HW + p) * F + lr] = m + log2f(l);  // log2 units
         const float inv = __builtin_amdgcn_rcpf(l);
-        pb[u] = zero8();
-#pragma unroll
-        for (int r = 0; r < 4; ++r) pb[u][r] = (bf16)(pr[r] * inv);
+        pb[u] = bf16x4_bits(pr[0] * inv, pr[1] * inv, pr[2] * inv, pr[3] * inv);
       }
 #pragma unroll
       for (int u = 0; u < PG; ++u) {
         const int rb = (pg + u) * F4;
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
-          const f32x4 ot = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va[u][half], pb[u], z4, 0, 0, 0);
+          const f32x4 ot = mfma_k16(va[u][half], pb[u], z4);
           if (lr < F) {
             float o4[4] = {ot[0], ot[1], ot[2], ot[3]};
             store4(sq + rg_at(rb, hs_off<R>(lr, half * 16 + lg * 4)), o4);
@@ -1240,7 +1316,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
         const bf16x8 dor = ld16(sdo + rr);
         // -- transposed orientation: lane (g, i): entries (j = 4g + r, i)
         float D = 0.f;
-        bf16x8 dst_b = zero8(), pt_b = zero8();
+        s16x4 dst_b, pt_b;
         {
           const f32x4 st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kr, qr, z4, 0, 0, 0);    // S^T[j][i]
           const f32x4 dpt = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vr, dor, z4, 0, 0, 0);  // dP^T[j][i]
@@ -1254,53 +1330,53 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
           }
           D = grp4_sum(D);
           if (lg == 0) { sld[lr] = Li; sld[16 + lr] = D; }
+          float dsv[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float ds = pt[r] * (dpt[r] - D);
-            dbr[r] += ds;
-            dst_b[r] = (bf16)ds;
-            pt_b[r] = (bf16)pt[r];
+            dsv[r] = pt[r] * (dpt[r] - D);
+            dbr[r] += dsv[r];
           }
+          dst_b = bf16x4_bits(dsv[0], dsv[1], dsv[2], dsv[3]);
+          pt_b = bf16x4_bits(pt[0], pt[1], pt[2], pt[3]);
         }
         // k-slot gathers: slot (g, e<4) <-> frame 4g+e, column d = half*16 + (lane & 15)
         f32x4 dqt[2];
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
-          const bf16x8 kg = kslot_gather_raw<R>(sk, rb, half * 16, lane);  // dS^T / P^T are 0 at frames >= F
-          const bf16x8 vg = kslot_gather_raw<R>(sv, rb, half * 16, lane);
-          dqt[half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kg, dst_b, z4, 0, 0, 0);  // dQ'^T[d][i]
+          const s16x4 kg = kslot4<R>(sk, rb, half * 16, lane);  // dS^T / P^T are 0 at frames >= F
+          dqt[half] = mfma_k16(kg, dst_b, z4);  // dQ'^T[d][i]
           if (!o_out) continue;  // O written by the forward (cesm_tblock_fwd o)
-          const f32x4 ot = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vg, pt_b, z4, 0, 0, 0);  // O^T[d][i]
+          const f32x4 ot = mfma_k16(kslot4<R>(sv, rb, half * 16, lane), pt_b, z4);  // O^T[d][i]
           if (lr < F) {
             float oo[4] = {ot[0], ot[1], ot[2], ot[3]};
             stnt4(o_out + (((int64_t)b * F + lr) * HW + p) * INNER + h * DH + half * 16 + lg * 4, oo);
           }
         }
         // -- row-major orientation: lane (g, j): entries (i = 4g + r, j); L_i, D_i from lane i
-        bf16x8 ds_b = zero8(), p_b = zero8();
+        s16x4 ds_b, p_b;
         {
           const f32x4 s_ = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qr, kr, z4, 0, 0, 0);    // S[i][j]
           const f32x4 dp_ = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dor, vr, z4, 0, 0, 0);  // dP[i][j]
           wave_lds_sync();
           const f32x4 L4 = *reinterpret_cast<const f32x4*>(sld + lg * 4);
           const f32x4 D4 = *reinterpret_cast<const f32x4*>(sld + 16 + lg * 4);
+          float pv[4], dv_[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int i = lg * 4 + r;
             const float Lr = L4[r], Dr = D4[r];
             const bool ok = i < F && lr < F;
-            const float pv = ok ? __builtin_amdgcn_exp2f(fmaf(s_[r], LOG2E, brm[r]) - Lr) : 0.f;
-            p_b[r] = (bf16)pv;
-            ds_b[r] = (bf16)(ok ? pv * (dp_[r] - Dr) : 0.f);
+            pv[r] = ok ? __builtin_amdgcn_exp2f(fmaf(s_[r], LOG2E, brm[r]) - Lr) : 0.f;
+            dv_[r] = ok ? pv[r] * (dp_[r] - Dr) : 0.f;
           }
+          p_b = bf16x4_bits(pv[0], pv[1], pv[2], pv[3]);
+          ds_b = bf16x4_bits(dv_[0], dv_[1], dv_[2], dv_[3]);
         }
         f32x4 dkt[2], dvt[2];
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
-          const bf16x8 qg = kslot_gather_raw<R>(sq, rb, half * 16, lane);
-          const bf16x8 dog = kslot_gather_raw<R>(sdo, rb, half * 16, lane);
-          dkt[half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qg, ds_b, z4, 0, 0, 0);   // dK'^T[d][j]
-          dvt[half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dog, p_b, z4, 0, 0, 0);   // dV^T[d][j]
+          dkt[half] = mfma_k16(kslot4<R>(sq, rb, half * 16, lane), ds_b, z4);   // dK'^T[d][j]
+          dvt[half] = mfma_k16(kslot4<R>(sdo, rb, half * 16, lane), p_b, z4);   // dV^T[d][j]
         }
         wave_lds_sync();  // all reads of this pixel's rows done before they are overwritten
         if (lr < F) {
@@ -1602,13 +1678,13 @@ __device__ __forceinline__ bf16x8 kslot_gather_ld(const bf16* tile, int ld, int 
 // (P, dS and their transposes are 0 there), the rows read past the pixel's F frames -- the next pixel's finite
 // rows, or the zero-initialised tail pad past the last slice -- contribute 0, so the 4 per-element selects
 // (v_cndmask + repacking, ~15 % of twh_bwd's VALU) are not needed
-__device__ __forceinline__ bf16x8 kslot_gather_hld_raw(const bf16* tile, int rb, int c0, int lane) {
+__device__ __forceinline__ s16x4 kslot4_hld(const bf16* tile, int rb, int c0, int lane) {
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  return kslot_raw(__builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tile + (rb + 4 * g + q) * HLD + c0 + 4 * p)));
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tile + (rb + 4 * g + q) * HLD + c0 + 4 * p));
 }
-__device__ __forceinline__ bf16x8 kslot_gather_ld_raw(const bf16* tile, int ld, int lane) {
+__device__ __forceinline__ s16x4 kslot4_ld(const bf16* tile, int ld, int lane) {
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  return kslot_raw(__builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tile + (4 * g + q) * ld + 4 * p)));
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tile + (4 * g + q) * ld + 4 * p));
 }
 
 #ifndef TWH_FULL
@@ -1616,9 +1692,9 @@ __device__ __forceinline__ bf16x8 kslot_gather_ld_raw(const bf16* tile, int ld, 
 // 5.35 ms (40 VGPRs spilled); PG 1 4.86 ms
 #define TWH_FULL 0      // twh_bwd: the head's 12 q/k/v weight fragments at once (1) or in two-tile batches (0)
 #endif
-#ifndef TWH_PG
-#define TWH_PG 1        // twh_bwd: pixels whose attention-core backward is interleaved phase by phase
-#endif
+// twh_bwd: pixels whose attention-core backward is interleaved phase by phase.  Fixed at 1 (round 2: 3375 vs
+// 3460 us with 2, 2 spills vs 10); 2 no longer fits the LDS next to the round-3 tiles, so it is not a knob.
+constexpr int TWH_PG = 1;
 #ifndef TWH_QKV_PIPE
 #define TWH_QKV_PIPE 1  // twh_bwd: double-buffered q/k/v weight batches, the first issued before barrier A
 #endif
@@ -1630,6 +1706,9 @@ __device__ __forceinline__ bf16x8 kslot_gather_ld_raw(const bf16* tile, int ld, 
 #endif
 #ifndef TWH_DO_PF
 #define TWH_DO_PF 1  // twh_bwd: the dO GEMM's weights issued during the last q/k/v batch (needs QKV_PIPE)
+#endif
+#ifndef TWH_QKV_B
+#define TWH_QKV_B 1  // twh_bwd: batched q / k / v recompute (see there); 0 = round 3's per-tile chains
 #endif
 #ifndef TWH_EARLY_WT
 #define TWH_EARLY_WT 0  // twh_bwd: W'^T fragments of the dxn GEMM issued before the dW GEMM (1)
@@ -1808,26 +1887,50 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
             for (int ks = 0; ks < T::KS; ++ks) wob[dt][ks] = ld_img(wot_g, h * 2 + dt, T::KS, ks, lane);
         }
 #endif
+        const int kind = c2 >> 1;  // the pair (c2, c2 + 1) = both 16-dim halves of one kind
+        bf16* dst = kind == 0 ? sq : (kind == 1 ? sk : sv);
+#if TWH_QKV_B
+        // batched (round 4), one 16-dim half at a time: the half's RoPE coefficients read first, its NV tiles issued
+        // back to back, then their epilogues (round 3: one MFMA -> s_nop -> LDS read -> wait -> VALU -> store chain
+        // per tile; both halves at once spill at 256 VGPRs)
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-          const int ct = c2 + u, kind = ct >> 1;
-          bf16* dst = kind == 0 ? sq : (kind == 1 ? sk : sv);
-          const int d0 = (ct & 1) * 16 + lg * 4;
+          f32x4 cs[NV];
+          if (kind < 2) {
+#pragma unroll
+            for (int vt = 0; vt < NV; ++vt) cs[vt] = *reinterpret_cast<const f32x4*>(rot + fr[vt] * RS + u * 16 + lg * 4);
+          }
+          f32x4 qacc[NV];
+#pragma unroll
+          for (int vt = 0; vt < NV; ++vt) {
+            qacc[vt] = z4;
+#pragma unroll
+            for (int ks = 0; ks < T::KS; ++ks)
+              qacc[vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wqa[buf][u][ks], xf[vt][ks], qacc[vt], 0, 0, 0);
+          }
+#pragma unroll
+          for (int vt = 0; vt < NV; ++vt) {
+            float o4[4] = {qacc[vt][0], qacc[vt][1], qacc[vt][2], qacc[vt][3]};  // q: scale in the weights
+            if (kind < 2) rope4c(o4, cs[vt]);
+            store4(dst + (vt * 16 + lr) * HLD + u * 16 + lg * 4, o4);
+          }
+        }
+#else
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int d0 = u * 16 + lg * 4;
 #pragma unroll
           for (int vt = 0; vt < NV; ++vt) {
             f32x4 acc = z4;
 #pragma unroll
             for (int ks = 0; ks < T::KS; ++ks)
               acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wqa[buf][u][ks], xf[vt][ks], acc, 0, 0, 0);
-            float o4[4] = {acc[0], acc[1], acc[2], acc[3]};
-            if (kind == 0) {
-#pragma unroll
-              for (int r = 0; r < 4; ++r) o4[r] *= scale;
-            }
+            float o4[4] = {acc[0], acc[1], acc[2], acc[3]};  // q: scale in the weights
             if (kind < 2) rope4(o4, rot, fr[vt], d0, 1.f);
             store4(dst + (vt * 16 + lr) * HLD + d0, o4);
           }
         }
+#endif
       }
 #else
 #error "TWH_QKV_PIPE=0: tw_qkv writes the region layout, twh_bwd reads 80-B rows"
@@ -1877,7 +1980,7 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
         st[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kr, qr, z4, 0, 0, 0);    // S^T[j][i]
         dpt[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vr, dor, z4, 0, 0, 0);  // dP^T[j][i]
       }
-      bf16x8 dst_b[PG];
+      s16x4 dst_b[PG];
 #pragma unroll
       for (int u = 0; u < PG; ++u) {
         const bool pix = p0 + pp0 + u < HW;
@@ -1893,15 +1996,14 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
         }
         D = grp4_sum(D);
         bf16x4 p4, d4;
-        dst_b[u] = zero8();
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float ds = pt[r] * (dpt[u][r] - D);
           dbacc[r] += ds;
-          dst_b[u][r] = (bf16)ds;
           d4[r] = (bf16)ds;
           p4[r] = (bf16)pt[r];
         }
+        dst_b[u] = __builtin_bit_cast(s16x4, d4);
         // tile[i = lr][j = 4g .. 4g+3]
         *reinterpret_cast<bf16x4*>(trt + (u * 2 + 0) * 256 + lr * 16 + lg * 4) = p4;
         *reinterpret_cast<bf16x4*>(trt + (u * 2 + 1) * 256 + lr * 16 + lg * 4) = d4;
@@ -1911,21 +2013,18 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
       for (int u = 0; u < PG; ++u)
 #pragma unroll
         for (int half = 0; half < 2; ++half)
-          dqt[u][half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kslot_gather_hld_raw(sk, (pp0 + u) * F, half * 16, lane),
-                                                                 dst_b[u], z4, 0, 0, 0);  // dQ'^T[d][i]
+          dqt[u][half] = mfma_k16(kslot4_hld(sk, (pp0 + u) * F, half * 16, lane), dst_b[u], z4);  // dQ'^T[d][i]
       wave_lds_sync();  // P / dS tiles visible
       f32x4 dkt[PG][2], dvt[PG][2];
 #pragma unroll
       for (int u = 0; u < PG; ++u) {
-        const bf16x8 p_b = kslot_gather_ld_raw(trt + (u * 2 + 0) * 256, 16, lane);   // P[i = 4g+e][j = lr]
-        const bf16x8 ds_b = kslot_gather_ld_raw(trt + (u * 2 + 1) * 256, 16, lane);  // dS[i = 4g+e][j = lr]
+        const s16x4 p_b = kslot4_ld(trt + (u * 2 + 0) * 256, 16, lane);   // P[i = 4g+e][j = lr]
+        const s16x4 ds_b = kslot4_ld(trt + (u * 2 + 1) * 256, 16, lane);  // dS[i = 4g+e][j = lr]
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
           const int rb = (pp0 + u) * F;
-          dkt[u][half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kslot_gather_hld_raw(sq, rb, half * 16, lane), ds_b, z4,
-                                                                 0, 0, 0);  // dK'^T[d][j]
-          dvt[u][half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kslot_gather_hld_raw(sdo, rb, half * 16, lane), p_b, z4,
-                                                                 0, 0, 0);  // dV^T[d][j]
+          dkt[u][half] = mfma_k16(kslot4_hld(sq, rb, half * 16, lane), ds_b, z4);   // dK'^T[d][j]
+          dvt[u][half] = mfma_k16(kslot4_hld(sdo, rb, half * 16, lane), p_b, z4);   // dV^T[d][j]
         }
       }
       wave_lds_sync();  // all reads of these pixels' rows (and the tiles) done before they are overwritten
@@ -1939,10 +2038,10 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
             float q4[4] = {dqt[u][half][0], dqt[u][half][1], dqt[u][half][2], dqt[u][half][3]};
             float k4[4] = {dkt[u][half][0], dkt[u][half][1], dkt[u][half][2], dkt[u][half][3]};
             float v4[4] = {dvt[u][half][0], dvt[u][half][1], dvt[u][half][2], dvt[u][half][3]};
+            // dq~ = R^T dQ' (the gradient w.r.t. the scaled q rows the images hold: twh_dw_reduce applies the
+            // scale to their weight gradient), dk = R^T dK'
             rope4(q4, rot, lr, d0, -1.f);
             rope4(k4, rot, lr, d0, -1.f);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) q4[r] *= scale;
             store4(sq + (rb + lr) * HLD + d0, q4);
             store4(sk + (rb + lr) * HLD + d0, k4);
             store4(sv + (rb + lr) * HLD + d0, v4);
@@ -2185,7 +2284,8 @@ int cesm_tblock_fwd_fold(const void* x, const float* gamma, const float* wqkv_f3
   if (C != 64 || F < 1 || F > 16) return CESM_EUNSUPPORTED;
   bf16* iq = (bf16*)wimg;
   bf16* io = iq + 768 * C;
-  frag_image_f32_kernel<<<(unsigned)cdiv((int64_t)768 * C / 8, 256), 256, 0, stream>>>(wqkv_f32, gamma, iq, 768, C, 0);
+  frag_image_f32_kernel<<<(unsigned)cdiv((int64_t)768 * C / 8, 256), 256, 0, stream>>>(wqkv_f32, gamma, iq, 768, C, 0,
+                                                                                      INNER, scale);  // q rows x scale
   frag_image(wout, io, C, INNER, stream);
   const int nv = (TW<64>::PW * F + 15) / 16;
   switch (nv) {
@@ -2211,8 +2311,9 @@ int cesm_tblock_bwd_dw(const void* x, const void* dy, const float* mr, const flo
   bf16* iqt = iq + 768 * C;
   bf16* iot = iqt + 768 * C;
   const unsigned gi = (unsigned)cdiv((int64_t)768 * C / 8, 256);
-  frag_image_f32_kernel<<<gi, 256, 0, stream>>>(wqkv_f32, gamma, iq, 768, C, 0);   // W diag(gamma)
-  frag_image_f32_kernel<<<gi, 256, 0, stream>>>(wqkv_f32, gamma, iqt, C, 768, 1);  // (W diag(gamma))^T
+  // W diag(gamma) and its transpose, the q rows times the attention scale (the kernel's q epilogues skip it)
+  frag_image_f32_kernel<<<gi, 256, 0, stream>>>(wqkv_f32, gamma, iq, 768, C, 0, INNER, scale);
+  frag_image_f32_kernel<<<gi, 256, 0, stream>>>(wqkv_f32, gamma, iqt, C, 768, 1, INNER, scale);
   frag_image(wout_t, iot, INNER, C, stream);
   const int nv = (4 * F + 15) / 16;
   const size_t sm = twh_smem(F, nv);
@@ -2229,7 +2330,7 @@ int cesm_tblock_bwd_dw(const void* x, const void* dy, const float* mr, const flo
 #undef TWH_LAUNCH
   const int64_t nel = (int64_t)768 * C;
   twh_dw_reduce_kernel<<<(unsigned)cdiv(nel, 256), 256, 0, stream>>>(slab, nblk, wqkv_f32, gamma, dwqkv, tmp, 768, C,
-                                                                    accumulate);
+                                                                    accumulate, INNER, scale);
   if (dgamma) twh_dgamma_kernel<<<C, 256, 0, stream>>>(tmp, dgamma, 768, C, accumulate);
   return cesm_launch_status();
 }

@@ -199,9 +199,6 @@ __device__ __forceinline__ const float* btab_lane(const float* tab, int lr, int 
 // 8 XCDs round-robin (linear id mod 8), so the 8 blocks an XCD receives back to back (ids L, L + 8, ...) are
 // the 8 heads of one pixel group: every line is fetched once into that XCD's L2 and used whole.  (One head per
 // grid row instead fetched each line twice from HBM: the head-pair partner ran 1/8 of the grid later.)
-#ifndef TF_QPRE
-#define TF_QPRE 0  // forward Q' fragments all loaded in the prologue (1: measured 1.7x slower at F = 120)
-#endif
 #ifndef TF_FWD_WPE
 #define TF_FWD_WPE 2  // forward waves per SIMD the register allocation targets (>= 2: VGPR-form MFMAs)
 #endif
@@ -213,10 +210,6 @@ __device__ __forceinline__ const float* btab_lane(const float* tab, int lr, int 
 #endif
 #ifndef TF_BUF
 #define TF_BUF 1  // A/B knob: buffer-resource tile addressing in the per-query-tile loop (0 = 64-bit lane math)
-#endif
-#ifndef TF_QPF
-#define TF_QPF 0  // A/B knob: forward query-tile rows prefetched a tile ahead (measured neutral at F = 120: 192x288
-                  // 4616 -> 4547 us, 96x144 +1 %, 48x72 -2 %, 24x36 +0..8 %; profiles/r3_tf_qpf_ab.txt)
 #endif
 #ifndef TF_XCD_MAP
 #define TF_XCD_MAP 1  // A/B knob: 0 = head-major grid (round 2)
@@ -259,15 +252,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE)
   const int q_off = (lr * HW * QKV + g * 8) * 2, o_off = (lr * HW * INNER + 4 * g) * 2;
   const __amdgpu_buffer_rsrc_t rot_rs = tile_rsrc(rot, F, 16 * 2 * 4, 16 * 2 * 4, TF_MAXT * 16);
   const int rot_off = (lr * 16 + 4 * g) * 2 * 4;
-  // every K' and Q' fragment up front (TF_QPRE): one exposed load latency per wave instead of one per query tile
-  bf16x8 kf[NT], qfa[TF_QPRE ? NT : 1];
+  // every K' fragment up front (all Q' fragments up front as well measured 1.7x slower at F = 120; the next query
+  // tile's rows prefetched a tile ahead, neutral: 192x288 4616 -> 4547 us, 48x72 -2 %, 24x36 +0..8 %)
+  bf16x8 kf[NT];
 #pragma unroll
   for (int kt = 0; kt < NT; ++kt) {
     const int f = kt * 16 + lr;
     const bool ok = f < F;
     const int64_t rr = (row0 + (int64_t)(ok ? f : 0) * HW) * QKV + h * DH + g * 8;
     kf[kt] = row_frag(qkv + rr + INNER, rot, ok ? f : 0, g, 1.f, true);
-    if (TF_QPRE) qfa[TF_QPRE ? kt : 0] = row_frag(qkv + rr, rot, ok ? f : 0, g, scale, true);
   }
   bf16x8 vf[NP][2];
 #pragma unroll
@@ -293,32 +286,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE)
 #pragma unroll
   for (int r = 0; r < 4; ++r) kmask[r] = 16 * (NT - 1) + 4 * g + r < F ? 0.f : -INFINITY;
 
-  // TF_QPF: the next query tile's raw q rows and RoPE coefficients are loaded while the current tile computes (one
-  // exposed load latency per wave instead of one per query tile; 12 more VGPRs, unlike TF_QPRE's 32 + RoPE)
-  bf16x8 qraw_n = zero8();
-  float cs_n[8];
-  auto qload = [&](int qt, bf16x8& raw, float* cs) {
-    const __amdgpu_buffer_rsrc_t qrs =
-        tile_rsrc(qkv + (row0 + (int64_t)qt * 16 * HW) * QKV + h * DH, F - qt * 16, (int64_t)HW * QKV * 2, DH * 2);
-    buf_rot8(rot_rs, rot_off + qt * 16 * 16 * 2 * 4, cs);
-    raw = buf_ld16(qrs, q_off);
-  };
-  if (TF_QPF && TF_BUF && !TF_QPRE) qload(0, qraw_n, cs_n);
   for (int qt = 0; qt < NT; ++qt) {
     const int fq = qt * 16 + lr;
     const bool okq = fq < F;
     const int nq = F - qt * 16;  // valid frames of this query tile (wave-uniform)
     bf16x8 qf;
-    if (TF_QPRE) {
-      qf = qfa[TF_QPRE ? qt : 0];
-    } else if (TF_QPF && TF_BUF) {
-      const bf16x8 raw = qraw_n;
-      float cs[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) cs[i] = cs_n[i];
-      if (qt + 1 < NT) qload(qt + 1, qraw_n, cs_n);  // frames >= F: zeros
-      qf = rope8(raw, cs, scale);
-    } else if (TF_BUF) {
+    if (TF_BUF) {
       const __amdgpu_buffer_rsrc_t qrs =
           tile_rsrc(qkv + (row0 + (int64_t)qt * 16 * HW) * QKV + h * DH, nq, (int64_t)HW * QKV * 2, DH * 2);
       float cs[8];

@@ -107,6 +107,33 @@ def test_conv3x3p_level0_bf16(dev, H, W, with_res):
     assert e_fwd < 1e-2 and e_dx < 1e-2 and e_dw < 1e-2 and e_db < 1e-2
 
 
+def test_conv3x3p_concurrent_streams(dev):
+    """conv3x3p launches overlapping on two HIP streams give the bits of the same launches in sequence: the
+    persistent kernel keeps no state between launches (its items are split statically; round 3's process-global
+    item counter made overlapping launches skip or repeat items).  C-ABI contract SURVEY §8(b) B3: caller-owned
+    buffers, enqueue-safe calls."""
+    Nb, H, W, C = 24, 96, 288, 64
+    geom = (H, W, C, 3, 3, 1, 1, 1)
+    assert K.conv_fwd_variant(BF, Nb, H, W, C, 0, H, W, C, C, 3, 3, 1, 1, 1) == "conv3x3p_kernel<32,7,true>"
+    torch.manual_seed(21)
+    xs = [torch.randn(Nb, H, W, C, device=dev).to(BF) for _ in range(4)]
+    ws = [K.conv_pack(torch.randn(C, C, 3, 3, device=dev) * 0.05, BF, C, C, 3, 3, False, False) for _ in range(4)]
+    bs = [torch.randn(C, device=dev) for _ in range(4)]
+    ref = [K.conv_fwd(xs[i], None, ws[i], bs[i], geom) for i in range(4)]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(device=dev) for _ in range(2)]
+    for rep in range(3):
+        outs = [None] * 4
+        for s in streams:
+            s.wait_stream(torch.cuda.current_stream())
+        for i in range(4):  # launches 0, 2 on one stream and 1, 3 on the other: pairs overlap on the device
+            with torch.cuda.stream(streams[i % 2]):
+                outs[i] = K.conv_fwd(xs[i], None, ws[i], bs[i], geom)
+        torch.cuda.synchronize()
+        for i in range(4):
+            assert torch.equal(outs[i], ref[i]), (rep, i)
+
+
 # ------------------------------------------------------------------ GroupNorm statistics from the conv epilogue
 @pytest.mark.parametrize("nslot, C", [(9000, 64), (28805, 128), (6048, 64)])
 def test_gn_stats_part_two_stage(dev, nslot, C):
