@@ -23,10 +23,15 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-I", str(ROOT /
 # repeatable; the other sources keep the packed forms (their epilogues measured faster with them: conv -7 %,
 # fused SLA forward -18 %) and are covered by the same bit-exact repeat tests (tests/test_gpu_determinism.py).
 NO_SLP = {"tblock.hip", "tflash.hip", "attn.hip"}
+# Attention sources: no NaN semantics, so fmaxf after a lane permute (the softmax row maxima) needs no canonicalising
+# v_max per operand (round 4, same-call A/B: SLA backward 4.92 -> 4.68 ms, forward 2.59 -> 2.51 ms at level 0).  Not
+# misc.hip: its gradient-norm check relies on isfinite.
+NO_NANS = {"tblock.hip", "tflash.hip", "attn.hip", "sla_fused.hip"}
 
 
 def _flags(src: Path):
-    return FLAGS + (["-fno-slp-vectorize"] if src.name in NO_SLP else [])
+    return (FLAGS + (["-fno-slp-vectorize"] if src.name in NO_SLP else []) +
+            (["-fno-honor-nans"] if src.name in NO_NANS else []))
 
 
 def _compile(src: Path) -> Path:

@@ -853,9 +853,6 @@ __device__ __forceinline__ void tw_qkv(const bf16* __restrict__ wqkv, const bf16
   }
 }
 
-#ifndef TW_QKV_B
-#define TW_QKV_B 1  // tw_fwd: batched q / k / v phase (tw_qkv_b); 0 = round 3's per-tile MFMA -> epilogue chains
-#endif
 // RoPE of dims d0..d0+3 (two pairs) with preloaded coefficients cs = (c0, s0, c1, s1)
 __device__ __forceinline__ void rope4c(float* o4, const f32x4 cs) {
 #pragma unroll
@@ -1044,7 +1041,7 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
       tw_qkv_pre<C, NV>(wq, xf, fr, FOLD ? 1.f : scale, rot, sq, sk, sv, lr, lg);  // FOLD: scale in the weights
       if (h + 1 < NH) tw_load_wq<C, NV>(wq, wqkv, h + 1, lr, lg);  // in flight during the core
     } else {
-      if constexpr (TW_QKV_B && C == 64) tw_qkv_b<C, NV, !FOLD>(wqkv, xf, h, fr, scale, rot, sq, sk, sv, lr, lg);
+      if constexpr (C == 64) tw_qkv_b<C, NV, !FOLD>(wqkv, xf, h, fr, scale, rot, sq, sk, sv, lr, lg);
       else tw_qkv<C, NV, false>(wqkv, xf, h, fr, FOLD ? 1.f : scale, rot, sq, sk, sv, lr, lg);  // two-tile batches
     }
     // bias (log2 units) of this lane's 4 entries (i = lr, j = 4g + r); -inf masks padding frames
@@ -1316,7 +1313,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
         const bf16x8 dor = ld16(sdo + rr);
         // -- transposed orientation: lane (g, i): entries (j = 4g + r, i)
         float D = 0.f;
-        s16x4 dst_b, pt_b;
+        bf16x8 dst_b = zero8(), pt_b = zero8();
         {
           const f32x4 st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kr, qr, z4, 0, 0, 0);    // S^T[j][i]
           const f32x4 dpt = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vr, dor, z4, 0, 0, 0);  // dP^T[j][i]
@@ -1330,53 +1327,54 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
           }
           D = grp4_sum(D);
           if (lg == 0) { sld[lr] = Li; sld[16 + lr] = D; }
-          float dsv[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            dsv[r] = pt[r] * (dpt[r] - D);
-            dbr[r] += dsv[r];
+            const float ds = pt[r] * (dpt[r] - D);
+            dbr[r] += ds;
+            dst_b[r] = (bf16)ds;
+            pt_b[r] = (bf16)pt[r];
           }
-          dst_b = bf16x4_bits(dsv[0], dsv[1], dsv[2], dsv[3]);
-          pt_b = bf16x4_bits(pt[0], pt[1], pt[2], pt[3]);
         }
         // k-slot gathers: slot (g, e<4) <-> frame 4g+e, column d = half*16 + (lane & 15)
         f32x4 dqt[2];
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
-          const s16x4 kg = kslot4<R>(sk, rb, half * 16, lane);  // dS^T / P^T are 0 at frames >= F
-          dqt[half] = mfma_k16(kg, dst_b, z4);  // dQ'^T[d][i]
+          // (the 16x16x16 form used in tw_fwd / twh_bwd measured 4-6 % slower in this kernel: kept at K = 32)
+          const bf16x8 kg = kslot_gather_raw<R>(sk, rb, half * 16, lane);  // dS^T / P^T are 0 at frames >= F
+          const bf16x8 vg = kslot_gather_raw<R>(sv, rb, half * 16, lane);
+          dqt[half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kg, dst_b, z4, 0, 0, 0);  // dQ'^T[d][i]
           if (!o_out) continue;  // O written by the forward (cesm_tblock_fwd o)
-          const f32x4 ot = mfma_k16(kslot4<R>(sv, rb, half * 16, lane), pt_b, z4);  // O^T[d][i]
+          const f32x4 ot = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vg, pt_b, z4, 0, 0, 0);  // O^T[d][i]
           if (lr < F) {
             float oo[4] = {ot[0], ot[1], ot[2], ot[3]};
             stnt4(o_out + (((int64_t)b * F + lr) * HW + p) * INNER + h * DH + half * 16 + lg * 4, oo);
           }
         }
         // -- row-major orientation: lane (g, j): entries (i = 4g + r, j); L_i, D_i from lane i
-        s16x4 ds_b, p_b;
+        bf16x8 ds_b = zero8(), p_b = zero8();
         {
           const f32x4 s_ = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qr, kr, z4, 0, 0, 0);    // S[i][j]
           const f32x4 dp_ = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dor, vr, z4, 0, 0, 0);  // dP[i][j]
           wave_lds_sync();
           const f32x4 L4 = *reinterpret_cast<const f32x4*>(sld + lg * 4);
           const f32x4 D4 = *reinterpret_cast<const f32x4*>(sld + 16 + lg * 4);
-          float pv[4], dv_[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int i = lg * 4 + r;
             const float Lr = L4[r], Dr = D4[r];
             const bool ok = i < F && lr < F;
-            pv[r] = ok ? __builtin_amdgcn_exp2f(fmaf(s_[r], LOG2E, brm[r]) - Lr) : 0.f;
-            dv_[r] = ok ? pv[r] * (dp_[r] - Dr) : 0.f;
+            const float pv = ok ? __builtin_amdgcn_exp2f(fmaf(s_[r], LOG2E, brm[r]) - Lr) : 0.f;
+            p_b[r] = (bf16)pv;
+            ds_b[r] = (bf16)(ok ? pv * (dp_[r] - Dr) : 0.f);
           }
-          p_b = bf16x4_bits(pv[0], pv[1], pv[2], pv[3]);
-          ds_b = bf16x4_bits(dv_[0], dv_[1], dv_[2], dv_[3]);
         }
         f32x4 dkt[2], dvt[2];
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
-          dkt[half] = mfma_k16(kslot4<R>(sq, rb, half * 16, lane), ds_b, z4);   // dK'^T[d][j]
-          dvt[half] = mfma_k16(kslot4<R>(sdo, rb, half * 16, lane), p_b, z4);   // dV^T[d][j]
+          const bf16x8 qg = kslot_gather_raw<R>(sq, rb, half * 16, lane);
+          const bf16x8 dog = kslot_gather_raw<R>(sdo, rb, half * 16, lane);
+          dkt[half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qg, ds_b, z4, 0, 0, 0);   // dK'^T[d][j]
+          dvt[half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dog, p_b, z4, 0, 0, 0);   // dV^T[d][j]
         }
         wave_lds_sync();  // all reads of this pixel's rows done before they are overwritten
         if (lr < F) {
@@ -1707,9 +1705,6 @@ constexpr int TWH_PG = 1;
 #ifndef TWH_DO_PF
 #define TWH_DO_PF 1  // twh_bwd: the dO GEMM's weights issued during the last q/k/v batch (needs QKV_PIPE)
 #endif
-#ifndef TWH_QKV_B
-#define TWH_QKV_B 1  // twh_bwd: batched q / k / v recompute (see there); 0 = round 3's per-tile chains
-#endif
 #ifndef TWH_EARLY_WT
 #define TWH_EARLY_WT 0  // twh_bwd: W'^T fragments of the dxn GEMM issued before the dW GEMM (1)
 #endif
@@ -1889,7 +1884,6 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
 #endif
         const int kind = c2 >> 1;  // the pair (c2, c2 + 1) = both 16-dim halves of one kind
         bf16* dst = kind == 0 ? sq : (kind == 1 ? sk : sv);
-#if TWH_QKV_B
         // batched (round 4), one 16-dim half at a time: the half's RoPE coefficients read first, its NV tiles issued
         // back to back, then their epilogues (round 3: one MFMA -> s_nop -> LDS read -> wait -> VALU -> store chain
         // per tile; both halves at once spill at 256 VGPRs)
@@ -1915,22 +1909,7 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
             store4(dst + (vt * 16 + lr) * HLD + u * 16 + lg * 4, o4);
           }
         }
-#else
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int d0 = u * 16 + lg * 4;
-#pragma unroll
-          for (int vt = 0; vt < NV; ++vt) {
-            f32x4 acc = z4;
-#pragma unroll
-            for (int ks = 0; ks < T::KS; ++ks)
-              acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wqa[buf][u][ks], xf[vt][ks], acc, 0, 0, 0);
-            float o4[4] = {acc[0], acc[1], acc[2], acc[3]};  // q: scale in the weights
-            if (kind < 2) rope4(o4, rot, fr[vt], d0, 1.f);
-            store4(dst + (vt * 16 + lr) * HLD + d0, o4);
-          }
-        }
-#endif
+
       }
 #else
 #error "TWH_QKV_PIPE=0: tw_qkv writes the region layout, twh_bwd reads 80-B rows"

@@ -37,8 +37,11 @@ def bump_param_epoch():
 # parameter-gradient GEMM (conv / 1x1 / qkv wgrads, bias column sums, stem wgrad) is enqueued on a second
 # HIP stream ordered after the kernel that produced its inputs.  The wgrads are HBM-bound (the level-0 qkv
 # wgrad streams 4.4 GB) while the dX kernels are MFMA/latency-bound, so the two co-run on the CUs.
-# "0": off, "attn": only the fused attention blocks' wgrads, "1": every wgrad
-WGRAD_STREAM = os.environ.get("CESM_WGRAD_STREAM", "0")
+# "0": off, "attn": only the fused attention blocks' wgrads, "1": every wgrad (default since round 4: whole step
+# 130.1 vs 131.8-132.2 ms, +1.3 % samples/s, same call, profiles/r4_wgrad_stream_ab.txt; round 3's 7-8x slowdown with
+# it on does not reproduce on the round-4 kernels: the per-step allocator counters are flat (no retries, no device
+# frees) and the trace shows the two streams co-running, profiles/r4_wgrad_stream_diag_*.txt)
+WGRAD_STREAM = os.environ.get("CESM_WGRAD_STREAM", "1")
 _WSTREAMS = {}
 
 

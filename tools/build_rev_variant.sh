@@ -10,7 +10,7 @@ cp cesm_emulator_amd/csrc/*.hip cesm_emulator_amd/csrc/*.h "$d"/
 git show "$rev:cesm_emulator_amd/csrc/$file" > "$d/$file"
 objs=""
 for f in "$d"/*.hip; do
-  case $(basename "$f") in tblock.hip|tflash.hip|attn.hip) noslp=-fno-slp-vectorize;; *) noslp=;; esac
+  case $(basename "$f") in tblock.hip|tflash.hip|attn.hip) noslp="-fno-slp-vectorize -fno-honor-nans";; sla_fused.hip) noslp=-fno-honor-nans;; *) noslp=;; esac
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I include $noslp -c "$f" -o "${f%.hip}.o" &
   objs="$objs ${f%.hip}.o"
 done

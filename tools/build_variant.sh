@@ -7,7 +7,7 @@ name=$1; flags=$2
 mkdir -p build/var_$name
 objs=""
 for f in cesm_emulator_amd/csrc/*.hip; do
-  case $(basename "$f") in tblock.hip|tflash.hip|attn.hip) noslp=-fno-slp-vectorize;; *) noslp=;; esac
+  case $(basename "$f") in tblock.hip|tflash.hip|attn.hip) noslp="-fno-slp-vectorize -fno-honor-nans";; sla_fused.hip) noslp=-fno-honor-nans;; *) noslp=;; esac
   o=build/var_$name/$(basename "$f" .hip).o
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I include $noslp $flags -c "$f" -o "$o" &
   objs="$objs $o"

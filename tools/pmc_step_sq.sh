@@ -16,7 +16,7 @@ for pmc in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_IN
   timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $pmc -d gpurun_out/${tag}_sq$i -o run -- \
     python3 tools/step_pmc.py 1 8 12 more_blocks > gpurun_out/${tag}_sq$i.log 2>&1
 done
-for k in twh_bwd slah_dx tw_fwd conv3x3p gn_bwd_apply; do
+for k in ${PMC_KERNELS:-twh_bwd slah_dx tw_fwd conv3x3p gn_bwd_apply}; do
   python3 tools/pmc.py gpurun_out/${tag}_sq1 gpurun_out/${tag}_sq2 gpurun_out/${tag}_sq3 --match=$k > gpurun_out/${tag}_sq_$k.txt
 done
 rm -rf gpurun_out/${tag}_sq1 gpurun_out/${tag}_sq2 gpurun_out/${tag}_sq3

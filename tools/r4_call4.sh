@@ -1,0 +1,19 @@
+#!/bin/bash
+# full GPU suite + contract bench + kernel summary + SQ counters of the conv kernels
+set -e
+tag=${1:-r4c4}
+root=${GRAFT_REPO_ROOT:-$(pwd)}
+cd /tmp && export TMPDIR=/tmp
+cd "$root"
+mkdir -p gpurun_out
+md5sum cesm_emulator_amd/*.so > gpurun_out/${tag}_md5.txt
+timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread > "gpurun_out/${tag}_pytest.log" 2>&1
+tail -2 "gpurun_out/${tag}_pytest.log"
+timeout -k 10 600 python3 bench.py > "gpurun_out/${tag}_bench.json" 2> "gpurun_out/${tag}_bench.err"
+python3 -c "import json; d=json.load(open('gpurun_out/${tag}_bench.json')); print(d['value'], d['ms_per_step'], d['roofline']['kernel'], d['roofline']['frac'], {k: v.get('ms_per_step') for k, v in d.get('other_configs', {}).items()})"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "gpurun_out/${tag}_prof" -o run -- \
+  python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --other-configs "" > "gpurun_out/${tag}_prof.json" 2> "gpurun_out/${tag}_prof.err"
+python3 tools/kstats.py "gpurun_out/${tag}_prof" 7 60 > "gpurun_out/${tag}_kernel_summary.txt"
+rm -rf "gpurun_out/${tag}_prof"
+head -12 "gpurun_out/${tag}_kernel_summary.txt"
+PMC_KERNELS="conv3x3_bf16_kernelILi36ELi7 conv3x3p wgrad3x3c64 twh_bwd tw_fwd slah_dx" bash tools/pmc_step_sq.sh ${tag}
