@@ -1620,6 +1620,308 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
 }
 
 // ----------------------------------------------------------------------------------------
+// 3x3 / stride 1 / pad 1 conv (bf16), warp-specialized persistent kernel (round 4).  One block of 8 waves per CU
+// (two per SIMD), static item split (item = (image, TH x TW tile of <= 256 px, 64-channel co block), the co blocks
+// of a tile on blocks of one XCD):
+//   waves 0-3 (compute): 64 co x 64 px each (4 x 4 MFMA tiles), the 9 taps of a 32-channel chunk from a halo +
+//     weight stage in LDS (cp_taps: tap t+1's 8 fragment reads between tap t's 16 MFMAs); at an item's last chunk
+//     they add the bias and write bf16 rows into a staging tile, and go straight on with the next item;
+//   waves 4-7 (load / store): the buffer-LDS-DMA of the next step's stage while the compute waves consume the
+//     current one, and the epilogue of the previous item from the staging tile -- residual (prefetched a step
+//     ahead), GroupNorm partials, 16-B row stores.
+// One s_barrier per step hands the stages over; the compute waves never wait on a load or a store, and the
+// epilogue (~40 % of conv3x3p's time at one wave per SIMD, where it could not overlap the MFMAs) runs beside the next
+// item's MFMAs.  Both roles pass exactly the same barriers.  LDS: 2 stages x 61 KiB + a 34 KiB staging tile.
+// ----------------------------------------------------------------------------------------
+constexpr int WS_PITCH = 40;                               // halo row pitch (pixels): ky steps keep the swizzle
+constexpr int WS_MAXTH = 8;                                // tile rows: (8 + 2) * 40 = 400 halo rows
+constexpr int WS_HROWS = (WS_MAXTH + 2) * WS_PITCH;        // 400
+constexpr int WS_WROWS = 9 * 64;                           // weight rows (tap * 64 + co)
+constexpr int WS_STAGE = (WS_HROWS + WS_WROWS) * 64;       // 62,464 B
+constexpr int WS_PIX = 256;                                // pixels per item (4 waves x 4 groups of 16)
+constexpr int WS_ELD = 68;                                 // staging row (bf16): 136 B, conflict-free 8-B writes
+constexpr int WS_LDS = 2 * WS_STAGE + WS_PIX * WS_ELD * 2;  // 159,744 B
+static_assert(WS_LDS <= 160 * 1024, "warp-specialized conv LDS");
+constexpr int WS_HPMAX = (WS_HROWS / 16 + 3) / 4;          // halo pieces per loader wave (<= 7)
+constexpr int WS_WP = WS_WROWS / 16 / 4;                   // weight pieces per loader wave (9)
+
+__device__ __forceinline__ void ws_decode(int it, int ncob, int ntile, int& tile, int& cb) {
+  // co blocks of a tile 8 ids apart: the blocks b, b + 8, ... that take them share an XCD (round-robin placement)
+  const int g = it / (8 * ncob), r = it - g * 8 * ncob;
+  cb = r >> 3;
+  tile = g * 8 + (r & 7);
+  (void)ntile;
+}
+
+template <int TW, bool GN>
+__global__ __launch_bounds__(512, 1) void conv3x3ws_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
+                                                           const bf16* __restrict__ w, const float* __restrict__ bias,
+                                                           const bf16* __restrict__ res, const bf16* __restrict__ res2,
+                                                           bf16* __restrict__ y1, bf16* __restrict__ y2, ConvGeom g,
+                                                           int TH, int tiles_x, int tiles_per_img, int ncob,
+                                                           int nitems_pad, float* __restrict__ gnp, int gn_fimg) {
+  __shared__ __attribute__((aligned(1024))) char lds[WS_LDS];
+  bf16* stg = reinterpret_cast<bf16*>(lds + 2 * WS_STAGE);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const bool loader = wid >= 4;  // wave-uniform role
+  const int wl = wid & 3;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int Cin = g.C1 + g.C2, nchunk = Cin / 32;
+  const int ntile = g.Nb * tiles_per_img;
+  const int G = (int)gridDim.x;
+  // the block's valid items: it = blockIdx.x + k * G (k < nk), tile < ntile; steps = valid items x chunks
+  auto next_valid = [&](int it) {
+    for (; it < nitems_pad; it += G) {
+      int tile, cb;
+      ws_decode(it, ncob, ntile, tile, cb);
+      if (tile < ntile) return it;
+    }
+    return nitems_pad;
+  };
+  auto geo = [&](int it, int& n, int& y0, int& x0, int& cb, int& tile) {
+    ws_decode(it, ncob, ntile, tile, cb);
+    n = tile / tiles_per_img;
+    const int r = tile - n * tiles_per_img, ty = r / tiles_x;
+    y0 = ty * TH;
+    x0 = (r - ty * tiles_x) * TW;
+  };
+
+  // ---------------- loader role state
+  const int prow = lane >> 2, pslot = lane & 3;
+  const int hpieces = ((TH + 2) * WS_PITCH + 15) >> 4;
+  int hrel[WS_HPMAX];  // halo piece k of this loader wave: lane row -> (hy << 16 | hx), -1 outside the halo
+#pragma unroll
+  for (int k = 0; k < WS_HPMAX; ++k) {
+    const int row = 16 * (wl + 4 * k) + prow;
+    const int hy = row / WS_PITCH, hx = row - hy * WS_PITCH;
+    hrel[k] = (hy < TH + 2 && hx < TW + 2) ? (hy << 16) | hx : -1;
+  }
+  auto issue_stage = [&](int it, int ch, int st) {  // loader waves: chunk ch of item it -> stage st
+    int n, y0, x0, cb, tile;
+    geo(it, n, y0, x0, cb, tile);
+    const int c0 = ch * 32;
+    const bf16* src;
+    int cs, cc;
+    if (c0 < g.C1) { src = x1; cs = g.C1; cc = c0; } else { src = x2; cs = g.C2; cc = c0 - g.C1; }
+    const int64_t img = (int64_t)g.Hi * g.Wi * cs;
+    const __amdgpu_buffer_rsrc_t xrs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(src + n * img + cc), (short)0, (int)(img * 2 - cc * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(w + (int64_t)cb * 64 * 9 * Cin + c0), (short)0, 64 * 9 * Cin * 2 - c0 * 2, 0x00020000);
+    char* dst = lds + st * WS_STAGE;
+#pragma unroll
+    for (int k = 0; k < WS_HPMAX; ++k) {
+      const int q = wl + 4 * k;
+      if (q < hpieces) {  // wave-uniform
+        const int chunk = pslot ^ cw_swz(16 * q + prow);
+        const int iy = y0 - 1 + (hrel[k] >> 16), ix = x0 - 1 + (hrel[k] & 0xffff);
+        const bool in = hrel[k] >= 0 && (unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi;
+        const int vo = in ? ((iy * g.Wi + ix) * cs + chunk * 8) * 2 : 0x7ffffff0;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)(dst + q * 1024), 16, vo,
+                                                 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < WS_WP; ++k) {
+      const int q = wl + 4 * k, row = 16 * q + prow;  // row = tap * 64 + co
+      const int chunk = pslot ^ cw_swz(row);
+      const int vo = (((row & 63) * 9 + (row >> 6)) * Cin + chunk * 8) * 2;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          wrs, (__attribute__((address_space(3))) void*)(dst + WS_HROWS * 64 + q * 1024), 16, vo, 0, 0, 0);
+    }
+  };
+  // epilogue rows of loader wave wl: pixels 64 wl + 8 u + (lane >> 3), u = 0..7, channels (lane & 7) * 8 .. + 7
+  bf16x8 resv[8];
+  auto out_px = [&](int y0, int x0, int u, int& oy, int& ox, bool& ok) {
+    const int p = 64 * wl + 8 * u + (lane >> 3);
+    const int py = p / TW, px = p - py * TW;
+    oy = y0 + py;
+    ox = x0 + px;
+    ok = py < TH && oy < g.Ho && ox < g.Wo;
+  };
+  auto out_rsrc = [&](int n, int cb, const bf16* a1, const bf16* a2, int& cofs, int& cstride) {
+    const int n0 = cb * 64;
+    const bool first = n0 < g.Co1;
+    cstride = first ? g.Co1 : g.Cout - g.Co1;
+    cofs = (first ? n0 : n0 - g.Co1) + (lane & 7) * 8;
+    const bf16* base = first ? a1 : a2;
+    const int64_t img = (int64_t)n * g.Ho * g.Wo * cstride;
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((base ? base : y1) + img), (short)0, g.Ho * g.Wo * cstride * 2,
+                                             0x00020000);
+  };
+  auto load_res = [&](int it) {  // residual rows of item it (issued a step before its epilogue)
+    int n, y0, x0, cb, tile;
+    geo(it, n, y0, x0, cb, tile);
+    int cofs, cstride;
+    const __amdgpu_buffer_rsrc_t rrs = out_rsrc(n, cb, res, res2, cofs, cstride);
+    const bool have = (cb * 64 < g.Co1 ? res : res2) != nullptr;  // this split's residual (none: loads return 0)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      int oy, ox;
+      bool ok;
+      out_px(y0, x0, u, oy, ox, ok);
+      const int off = have ? ((ok ? oy * g.Wo + ox : 0) * cstride + cofs) * 2 : 0x7ffffff0;
+      resv[u] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rrs, off, 0, 0));
+    }
+  };
+  const bool has_res = (res != nullptr) || (res2 != nullptr);
+  // epilogue of item it from the staging tile; returns after issuing its stores (8 rows + GN partial)
+  auto epilogue = [&](int it) {
+    int n, y0, x0, cb, tile;
+    geo(it, n, y0, x0, cb, tile);
+    bf16x8 rows[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      rows[u] = *reinterpret_cast<const bf16x8*>(stg + (64 * wl + 8 * u + (lane >> 3)) * WS_ELD + (lane & 7) * 8);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    int cofs, cstride;
+    const __amdgpu_buffer_rsrc_t yrs = out_rsrc(n, cb, y1, y2, cofs, cstride);
+    float gs[2] = {0.f, 0.f}, gq[2] = {0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      int oy, ox;
+      bool ok;
+      out_px(y0, x0, u, oy, ox, ok);
+      bf16x8 v = rows[u];
+      if (has_res) {  // uniform
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (bf16)((float)v[e] + (float)resv[u][e]);
+      }
+      if constexpr (GN) {  // statistics of the stored bf16 y (a GroupNorm conv has no residual)
+        const float m = ok ? 1.f : 0.f;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float a0 = (float)v[4 * h], a1 = (float)v[4 * h + 1], a2 = (float)v[4 * h + 2], a3 = (float)v[4 * h + 3];
+          gs[h] = fmaf(m, (a0 + a1) + (a2 + a3), gs[h]);
+          gq[h] = fmaf(m, fmaf(a3, a3, fmaf(a2, a2, fmaf(a1, a1, a0 * a0))), gq[h]);
+        }
+      }
+      const int off = ok ? ((oy * g.Wo + ox) * cstride + cofs) * 2 : 0x7ffffff0;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yrs, off, 0, 0);
+    }
+    if constexpr (GN) {
+      // lanes with equal (lane & 7) hold the same 8 channels: sum over lane bits 3..5 (fixed order)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int o = 8; o < 64; o <<= 1) {
+          gs[h] += __shfl_xor(gs[h], o, 64);
+          gq[h] += __shfl_xor(gq[h], o, 64);
+        }
+      }
+      const int b = n / gn_fimg, f = n - b * gn_fimg;
+      const int64_t nslot = (int64_t)gn_fimg * tiles_per_img * 4;
+      const int64_t slot = ((int64_t)f * tiles_per_img + (tile - n * tiles_per_img)) * 4 + wl;
+      // [B][nslot][C/4] float2: this wave's slot, the co block's 16 quads; lane c < 8 writes quads 2c, 2c + 1
+      float* dst = gnp + (((int64_t)b * nslot + slot) * (g.Cout / 4) + cb * 16) * 2;
+      const f32x4 v4 = {gs[0], gq[0], gs[1], gq[1]};
+      const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc((void*)dst, (short)0, 128, 0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v4), grs, lane < 8 ? lane * 16 : 0x7ffffff0, 0,
+                                             0);
+    }
+  };
+
+  // ---------------- compute role state
+  int bad[4][3];
+  {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int p = 64 * wl + 16 * j + lr;
+      const int py = p / TW, px = p - py * TW;
+      const int h0 = py < TH ? py * WS_PITCH + px : 0;
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) bad[j][kx] = cw_off(h0 + kx, lg);
+    }
+  }
+  const int a_lane = (lr << 6) + ((lg ^ cw_swz(lr)) << 4);
+  f32x4 bv4[4];  // the item's bias (co = i * 16 + 4 lg + r), loaded at its first chunk, used at its last
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // ---------------- the step loops: one per role, the same sequence of steps and barriers (a loop per role keeps
+  // the two roles' registers apart: one shared loop held the loader's residual rows live through the MFMAs)
+  int it0 = next_valid((int)blockIdx.x);
+  if (it0 >= nitems_pad) return;  // whole block, before any barrier
+  if (loader) {
+    issue_stage(it0, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int it = it0, ch = 0, s = 0, prev_it = -1;
+    while (true) {
+      __builtin_amdgcn_s_barrier();  // stage s landed; stage s - 1 consumed; staging of prev_it written (ch == 0)
+      const int nxt_ch = ch + 1 < nchunk ? ch + 1 : 0;
+      const int nxt_it = ch + 1 < nchunk ? it : next_valid(it + G);
+      const bool more = nxt_it < nitems_pad;
+      const bool epi = ch == 0 && prev_it >= 0;
+      if (epi) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // residual rows of prev_it
+      if (more) issue_stage(nxt_it, nxt_ch, (s + 1) & 1);
+      if (epi) epilogue(prev_it);
+      // the next step ends item nxt_it (nchunk >= 2): its residual rows now, in registers at its epilogue
+      const bool pre = more && has_res && nxt_ch == nchunk - 1;
+      if (pre) load_res(nxt_it);
+      // wait for this step's DMA only: the epilogue's stores (8 rows [+ 1 GN partial]) and the residual loads (8)
+      // issued after it may stay in flight
+      if (epi && pre) {
+        if constexpr (GN) asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      } else if (epi) {
+        if constexpr (GN) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else if (pre) {
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      if (ch == nchunk - 1) prev_it = it;
+      ch = nxt_ch;
+      it = nxt_it;
+      ++s;
+      if (!more) break;
+    }
+    __builtin_amdgcn_s_barrier();  // the last item's staging rows written
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    epilogue(prev_it);
+  } else {
+    int it = it0, ch = 0, s = 0;
+    while (true) {
+      __builtin_amdgcn_s_barrier();  // stage s landed; the staging tile free again (ch == 0)
+      const int nxt_ch = ch + 1 < nchunk ? ch + 1 : 0;
+      const int nxt_it = ch + 1 < nchunk ? it : next_valid(it + G);
+      if (ch == 0) {
+        int n, y0, x0, cb, tile;
+        geo(it, n, y0, x0, cb, tile);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          bv4[i] = bias ? *reinterpret_cast<const f32x4*>(bias + cb * 64 + i * 16 + lg * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      const char* sh = lds + (s & 1) * WS_STAGE;
+      cp_taps<4>(sh, sh + WS_HROWS * 64, bad, a_lane, acc);
+      if (ch == nchunk - 1) {  // item end: (acc + bias) as bf16 rows of the staging tile
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int co = i * 16 + lg * 4;
+          const f32x4 bv = bv4[i];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float v[4] = {acc[i][j][0] + bv[0], acc[i][j][1] + bv[1], acc[i][j][2] + bv[2], acc[i][j][3] + bv[3]};
+            store4(stg + (64 * wl + 16 * j + lr) * WS_ELD + co, v);
+            acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging rows visible at the barrier
+      ch = nxt_ch;
+      it = nxt_it;
+      ++s;
+      if (it >= nitems_pad) break;
+    }
+    __builtin_amdgcn_s_barrier();  // pairs with the loaders' last barrier
+  }
+}
+
+// ----------------------------------------------------------------------------------------
 // 1x1 conv (bf16) as a GEMM: Y[m][co] = bias[co] + res[m][co] + sum_k X[m][k] W[co][k], X = [x1 | x2]
 // concatenated on channels, Y = [y1 | y2] split at Co1.  Block = 128 pixels x BN output channels
 // (the co blocks of a pixel tile run back to back on one XCD, sharing its X rows in L2); K in steps of 64
@@ -1996,6 +2298,18 @@ static void c2_tile(int Ho, int Wo, int& TH, int& TW, bool only_32_36 = false) {
 
 // halo-conv tile for the 448-pixel blocks (conv3x3_bf16_kernel<TW, 7>): TW in {32, 36}, TH*TW <= 448,
 // TH + 2 <= 16 halo rows; the most useful / computed pixels, a 32-wide tile needs > 5 % better utilisation
+// warp-specialized conv tile: TW in {32, 36} (halo width <= WS_PITCH), TH * TW <= 256; returns the pixel utilisation
+static double ws_tile(int Ho, int Wo, int& TH, int& TW) {
+  double best = -1.0;
+  for (int tw : {32, 36}) {
+    for (int th = 1; th <= WS_MAXTH && th * tw <= WS_PIX; ++th) {
+      const double util = (double)Ho * Wo / ((double)cdiv(Ho, th) * cdiv(Wo, tw) * WS_PIX);
+      if (util > best + 1e-9) { best = util; TH = th; TW = tw; }
+    }
+  }
+  return best;
+}
+
 static void h3_big_tile(int Ho, int Wo, int& TH, int& TW) {
   double best = -1.0;
   int bt = 1 << 30;
@@ -3732,7 +4046,7 @@ enum ConvFwdVariant {
   CFV_INVALID = -1,
   CFV_GEMM1X1_128 = 0, CFV_GEMM1X1_64, CFV_P36_RW, CFV_P36, CFV_P32_3STAGE, CFV_P32_RW, CFV_P32, CFV_W36, CFV_W32,
   CFV_V2, CFV_HALO36, CFV_HALO32, CFV_TCONV_PAR_128, CFV_TCONV_PAR_64, CFV_GEN_BF16_128, CFV_GEN_BF16_64,
-  CFV_GEN_F32_128, CFV_GEN_F32_64, CFV_S2DOWN36, CFV_S2DOWN32, CFV_S2UP36, CFV_S2UP32, CFV_COUNT
+  CFV_GEN_F32_128, CFV_GEN_F32_64, CFV_S2DOWN36, CFV_S2DOWN32, CFV_S2UP36, CFV_S2UP32, CFV_WS32, CFV_WS36, CFV_COUNT
 };
 static const char* const kConvFwdVariantName[CFV_COUNT] = {
     "gemm1x1_kernel<128>", "gemm1x1_kernel<64>", "conv3x3p_kernel<36,8,true>", "conv3x3p_kernel<36,8,false>",
@@ -3741,7 +4055,7 @@ static const char* const kConvFwdVariantName[CFV_COUNT] = {
     "conv3x3_bf16_kernel<32>", "conv_fwd_bf16_kernel<128,true>", "conv_fwd_bf16_kernel<64,true>",
     "conv_fwd_bf16_kernel<128>", "conv_fwd_bf16_kernel<64>", "conv_fwd_kernel<float,128>",
     "conv_fwd_kernel<float,64>", "convs2_bf16_kernel<36,down>", "convs2_bf16_kernel<32,down>",
-    "convs2_bf16_kernel<36,up>", "convs2_bf16_kernel<32,up>"};
+    "convs2_bf16_kernel<36,up>", "convs2_bf16_kernel<32,up>", "conv3x3ws_kernel<32>", "conv3x3ws_kernel<36>"};
 
 struct ConvFwdPlan {
   ConvFwdVariant v = CFV_INVALID;
@@ -3760,8 +4074,15 @@ static ConvFwdPlan conv_fwd_plan(int dtype, int Nb, int Hi, int Wi, int C1, int 
   const bool g1x1 = dtype == CESM_DT_BF16 && KH == 1 && KW == 1 && S == 1 && P == 0 && U == 1 && Ho == Hi &&
                     Wo == Wi && (C1 % 64) == 0 && (C2 % 64) == 0 && (Co1 % 8) == 0 && M < (1ll << 31) &&
                     (G1_BIGM || M * (C1 > C2 ? C1 : C2) * 2 < (1ll << 31)) && !getenv_flag("CESM_NO_GEMM1X1");
+  int wth = 0, wtw = 0;
+  const double wutil = halo3 && (C1 + C2) >= 64 && getenv_flag("CESM_CONV_WS") ? ws_tile(Ho, Wo, wth, wtw) : 0.0;
   if (g1x1) {
     pl.v = (Cout % 128 == 0) ? CFV_GEMM1X1_128 : CFV_GEMM1X1_64;
+  } else if (wutil >= 0.9) {
+    // warp-specialized persistent conv (round 4) where its 256-pixel tiles cover the image to >= 90 %
+    pl.v = wtw == 36 ? CFV_WS36 : CFV_WS32;
+    pl.TH = wth;
+    pl.TW = wtw;
   } else if (halo3 && Cout <= 1024 && !getenv_flag("CESM_CONV3X3_V1") &&
              (getenv_flag("CESM_CONV3X3_V4") || ((C1 + C2) == 64 && Cout == 64 && (Wo % 32) == 0))) {
     // v4 (persistent, resident weights) for the level-0 64 -> 64 convs by default;
@@ -3842,6 +4163,7 @@ int64_t conv_gn_nslot(const ConvFwdPlan& pl, int Nb, int Ho, int Wo, int B) {
   switch (pl.v) {
     case CFV_P36_RW: case CFV_P36: case CFV_P32_RW: case CFV_P32: return fimg * tiles * 4;
     case CFV_HALO36: case CFV_HALO32: return fimg * tiles * (H3_SQ ? 4 : 2);
+    case CFV_WS32: case CFV_WS36: return fimg * tiles * 4;
     default: return 0;
   }
 }
@@ -3902,6 +4224,21 @@ int conv_fwd_launch(int dtype, const void* x1, const void* x2, const void* wp, c
       else
         conv3x3p_kernel<32, 7, false><<<nblk, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx,
                                                                 tx * ty, TH, ncob, nitems, gnp, gn_fimg);
+      break;
+    }
+    case CFV_WS32:
+    case CFV_WS36: {
+      const int tx = (int)cdiv(Wo, TW), ty = (int)cdiv(Ho, TH);
+      const int ncob = Cout / 64;
+      const int ntile = Nb * tx * ty;
+      const int nitems_pad = (int)cdiv(ntile, 8) * 8 * ncob;
+      const int nblk = std::min(nitems_pad, cesm_num_cus());
+#define WSL(TWv, GNv)                                                                                              \
+  conv3x3ws_kernel<TWv, GNv><<<nblk, 512, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, TH, tx, tx * ty, ncob, \
+                                                       nitems_pad, gnp, gn_fimg)
+      if (pl.v == CFV_WS36) { if (gnp) WSL(36, true); else WSL(36, false); }
+      else { if (gnp) WSL(32, true); else WSL(32, false); }
+#undef WSL
       break;
     }
     case CFV_W36:

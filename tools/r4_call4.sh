@@ -17,3 +17,5 @@ python3 tools/kstats.py "gpurun_out/${tag}_prof" 7 60 > "gpurun_out/${tag}_kerne
 rm -rf "gpurun_out/${tag}_prof"
 head -12 "gpurun_out/${tag}_kernel_summary.txt"
 PMC_KERNELS="conv3x3_bf16_kernelILi36ELi7 conv3x3p wgrad3x3c64 twh_bwd tw_fwd slah_dx" bash tools/pmc_step_sq.sh ${tag}
+timeout -k 10 300 python3 -u tools/ws_check.py > gpurun_out/${tag}_ws_check.txt 2>&1 || true
+tail -14 gpurun_out/${tag}_ws_check.txt
