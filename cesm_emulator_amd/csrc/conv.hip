@@ -2515,8 +2515,15 @@ __device__ __forceinline__ int wgb_swz(int r) {  // XOR on 4-element chunk index
 // (BIAS: compile-time, so the plain instantiation keeps its register count — the bias accumulators
 // pushed the BM = 256 kernel past 128 VGPRs, a wave per SIMD fewer and 43 % slower.)
 // (Round 3 measured an XCD-grouped 1-D grid for a pixel split's tiles: whole step 130.4 -> 131.5 ms; removed.)
+// wgrad_wide: register allocation for >= 2 waves per SIMD (256 registers).  With the unconstrained 512-register
+// budget the compiler kept the accumulators in VGPRs and copied each one into a[0:3] before its MFMA and back after
+// (AGPR-form MFMAs: 64 v_accvgpr_write + 64 v_accvgpr_read + s_nop per 16 MFMAs in the BM = 256 loop, 244 + 40
+// registers); capped: VGPR-form MFMAs, no copies, 178 / 122 / 68 registers at BM = 256 / 128 / 64.
+#ifndef WW_WPE
+#define WW_WPE 2
+#endif
 template <int BM, bool BIAS = false>
-__global__ __launch_bounds__(256) void wgrad_wide_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WW_WPE))) void wgrad_wide_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
                                                          const bf16* __restrict__ dy1, const bf16* __restrict__ dy2,
                                                          float* __restrict__ slab, float* __restrict__ bslab, ConvGeom g,
                                                          int M, int px_per_split) {
