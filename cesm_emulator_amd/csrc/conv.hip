@@ -2296,8 +2296,6 @@ static void c2_tile(int Ho, int Wo, int& TH, int& TW, bool only_32_36 = false) {
   }
 }
 
-// halo-conv tile for the 448-pixel blocks (conv3x3_bf16_kernel<TW, 7>): TW in {32, 36}, TH*TW <= 448,
-// TH + 2 <= 16 halo rows; the most useful / computed pixels, a 32-wide tile needs > 5 % better utilisation
 // warp-specialized conv tile: TW in {32, 36} (halo width <= WS_PITCH), TH * TW <= 256; returns the pixel utilisation
 static double ws_tile(int Ho, int Wo, int& TH, int& TW) {
   double best = -1.0;
@@ -2310,6 +2308,8 @@ static double ws_tile(int Ho, int Wo, int& TH, int& TW) {
   return best;
 }
 
+// halo-conv tile for the 448-pixel blocks (conv3x3_bf16_kernel<TW, 7>): TW in {32, 36}, TH*TW <= 448,
+// TH + 2 <= 16 halo rows; the most useful / computed pixels, a 32-wide tile needs > 5 % better utilisation
 static void h3_big_tile(int Ho, int Wo, int& TH, int& TW) {
   double best = -1.0;
   int bt = 1 << 30;
@@ -4082,7 +4082,12 @@ static ConvFwdPlan conv_fwd_plan(int dtype, int Nb, int Hi, int Wi, int C1, int 
                     Wo == Wi && (C1 % 64) == 0 && (C2 % 64) == 0 && (Co1 % 8) == 0 && M < (1ll << 31) &&
                     (G1_BIGM || M * (C1 > C2 ? C1 : C2) * 2 < (1ll << 31)) && !getenv_flag("CESM_NO_GEMM1X1");
   int wth = 0, wtw = 0;
-  const double wutil = halo3 && (C1 + C2) >= 64 && getenv_flag("CESM_CONV_WS") ? ws_tile(Ho, Wo, wth, wtw) : 0.0;
+  // warp-specialized conv: by default for the level-0 64 -> 64 shape only (the conv3x3p case: 579 -> 518 us at
+  // 96 x 192 x 288, profiles/r4c4_ws_check.txt); at 128 / 256 channels and for concat inputs it measured 0.85 - 1.01x
+  // of the halo conv, so there it is opt-in (CESM_CONV_WS=1); CESM_NO_CONV_WS=1 disables it
+  const bool ws = halo3 && (C1 + C2) >= 64 && !getenv_flag("CESM_NO_CONV_WS") &&
+                  (getenv_flag("CESM_CONV_WS") || (C1 == 64 && C2 == 0 && Cout == 64));
+  const double wutil = ws ? ws_tile(Ho, Wo, wth, wtw) : 0.0;
   if (g1x1) {
     pl.v = (Cout % 128 == 0) ? CFV_GEMM1X1_128 : CFV_GEMM1X1_64;
   } else if (wutil >= 0.9) {

@@ -610,6 +610,191 @@ __global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(DOV && 
     part[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * (2 * F - 1) + e] = dacc[e];
 }
 
+// ------------------------------------------------------------------------------------------- backward, dq (per wave)
+// Round 4 form of the dq pass for F > 16 (NT >= 2): one wave owns a (pixel, head) at a time -- all NT query
+// tiles -- and walks its pixels with no block barrier.  V fragments of every key tile live in registers for the
+// pixel, K' rows are staged in the wave's LDS rows (A fragments and k-slot transposes are read from there); both
+// the query-tile and the key-tile loops are unrolled, so the dbias accumulator of every (r, kt - qt) diagonal is
+// a static register (dba[4][2 NT - 1], 60 at NT = 8), summed over the wave's pixels.  D_i = dO_i . O_i (the
+// forward's bf16 output).  The block-per-pixel form (tflash_bwd_q_kernel: query tile = wave, two barriers per
+// pixel) ran in barrier lockstep on the staged rows.  Grid (nblk, B * 8) x 256 threads; the 4 waves' dbias rows
+// are reduced in a fixed order into the block's partial row, the same part[(b*8 + h)][blk][2F - 1] contract.
+// Every lane-derived quantity is recomputed per pixel from an opaque copy of the lane id: as loop invariants the
+// compiler hoisted them all (per-frame RoPE coefficients, bias-table reads, LDS and global addresses: > 200
+// VGPRs at NT = 8) out of the pixel loop and spilled.
+#ifndef TFQW_KREG
+#define TFQW_KREG 1  // K' A fragments of the pixel held in registers (0: re-read from the staged rows per query tile)
+#endif
+#ifndef TFQW_KTF
+#define TFQW_KTF 1  // K'^T k-slot fragments held in registers (0: transpose-read from LDS per query tile)
+#endif
+template <int NT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tflash_bwd_qw_kernel(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
+    const float* __restrict__ lse, const float* __restrict__ bias, const float* __restrict__ rot,
+    bf16* __restrict__ dqkv, float* __restrict__ dbuf, float* __restrict__ part, int F, int HW, float scale) {
+  constexpr int NP = (NT + 1) / 2, NR = 32 * NP, NC = 2 * NT - 1;
+  constexpr int CH = (NR * TF_LD * 2) / (4 * 64 * 4);  // diagonals staged per chunk in the wave's row buffer
+  static_assert(CH >= 1, "stage chunk");
+  __shared__ __attribute__((aligned(16))) float btab[4 * 32 * NT];
+  __shared__ __attribute__((aligned(16))) bf16 ksw[4][NR * TF_LD];
+  __shared__ float wsum[4][256];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: tile bases in SGPRs
+  const int b = blockIdx.y >> 3, h = blockIdx.y & 7;
+  load_btab<NT>(bias, btab, h, F, 1, tid, 256);
+  bf16* ks = ksw[wid];
+  for (int e = lane; e < (NR - 16 * NT) * 4; e += 64) {  // rows past the last key tile stay zero
+    const int f = 16 * NT + (e >> 2), c = e & 3;
+    *reinterpret_cast<bf16x8*>(ks + f * TF_LD + c * 8) = zero8();
+  }
+  __syncthreads();
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  float dba[4][NC];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < NC; ++c) dba[r][c] = 0.f;
+  // tile addressing as the forward's TF_BUF: wave-uniform tile base + one 32-bit lane offset for every tile, the
+  // resource ends at the tile's last valid frame (loads past F return 0, stores are dropped)
+  const int fs_qkv = HW * QKV * 2, fs_io = HW * INNER * 2;  // < 2^31 / 16: checked on the host
+
+  for (int p = blockIdx.x * 4 + wid; p < HW; p += 4 * (int)gridDim.x) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int lr = ln & 15, g = ln >> 4;
+    const int lo_qkv = lr * fs_qkv + h * DH * 2 + g * 16, lo_io = lr * fs_io + h * DH * 2 + g * 16;
+    const int64_t row0 = (int64_t)b * F * HW + p;
+    const float* lsep = lse + (((int64_t)b * NH + h) * HW + p) * F;
+    float* dbp = dbuf + (((int64_t)b * NH + h) * HW + p) * F;
+    bf16x8 vf[NT], kf[TFQW_KREG ? NT : 1], ktf[TFQW_KTF ? NP : 1][2];
+#pragma unroll
+    for (int kt = 0; kt < NT; ++kt) {
+      const auto rs = tile_rsrc(qkv + (row0 + (int64_t)kt * 16 * HW) * QKV, F - kt * 16, (int64_t)fs_qkv, QKV * 2);
+      const bf16x8 kr = buf_ld16(rs, lo_qkv + INNER * 2);
+      vf[kt] = buf_ld16(rs, lo_qkv + 2 * INNER * 2);
+      const int f = kt * 16 + lr;
+      float cs[8];
+      rot8_load(rot, f < F ? f : 0, g, cs);
+      if (kt == 0) wsync();  // previous pixel's reads of the rows done
+      const bf16x8 kv = rope8(kr, cs, 1.f);  // frames >= F: zeros
+      if (TFQW_KREG) kf[TFQW_KREG ? kt : 0] = kv;
+      *reinterpret_cast<bf16x8*>(ks + f * TF_LD + g * 8) = kv;
+    }
+    wsync();
+    if (TFQW_KTF)
+#pragma unroll
+      for (int s = 0; s < NP; ++s)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) ktf[TFQW_KTF ? s : 0][t] = tr_pair(ks, s, t * 16, ln);
+    const float* bl = btab_lane<NT>(btab, lr, g);
+
+#pragma unroll
+    for (int qt = 0; qt < NT; ++qt) {
+      const int fq = qt * 16 + lr;
+      const bool okq = fq < F;
+      const int fqc = okq ? fq : 0;
+      const auto rq = tile_rsrc(qkv + (row0 + (int64_t)qt * 16 * HW) * QKV, F - qt * 16, (int64_t)fs_qkv, QKV * 2);
+      const auto rd = tile_rsrc(dout + (row0 + (int64_t)qt * 16 * HW) * INNER, F - qt * 16, (int64_t)fs_io, INNER * 2);
+      const auto ro = tile_rsrc(o + (row0 + (int64_t)qt * 16 * HW) * INNER, F - qt * 16, (int64_t)fs_io, INNER * 2);
+      const bf16x8 qr = buf_ld16(rq, lo_qkv);
+      const bf16x8 dof = buf_ld16(rd, lo_io);
+      const bf16x8 orw = buf_ld16(ro, lo_io);
+      const float lq = lsep[fqc];
+      float cs[8];
+      rot8_load(rot, fqc, g, cs);
+      const bf16x8 qf = rope8(qr, cs, scale);
+      const float Li = okq ? lq : TF_LSE_PAD;  // padded query rows: P = 0 (so dS = 0 there)
+      float Do = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) Do = fmaf((float)dof[e], (float)orw[e], Do);
+      const float D = grp4_sum(Do);
+      if (okq && g == 0) dbp[fq] = D;
+      const float* bq = bl - 16 * qt;
+      f32x4 dqt[2] = {z4, z4};
+#pragma unroll
+      for (int s = 0; s < NP; ++s) {
+        float dsv[2][4];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int kt = 2 * s + u;
+          if (kt < NT) {
+            const bf16x8 ka = TFQW_KREG ? kf[TFQW_KREG ? kt : 0] : ld16(ks + (kt * 16 + lr) * TF_LD + g * 8);
+            const f32x4 st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf, z4, 0, 0, 0);        // S'^T
+            const f32x4 dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[kt], dof, z4, 0, 0, 0);  // dP^T
+            const f32x4 bo = *reinterpret_cast<const f32x4*>(bq + 16 * kt);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float pp = __builtin_amdgcn_exp2f(fmaf(st[r], LOG2E, bo[r]) - Li);
+              if (kt == NT - 1) pp = 16 * (NT - 1) + 4 * g + r < F ? pp : 0.f;  // keys of the last tile below F
+              const float ds = pp * (dp[r] - D);
+              dsv[u][r] = ds;
+              dba[r][kt - qt + NT - 1] += ds;
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dsv[u][r] = 0.f;
+          }
+        }
+        const bf16x8 db = pack_kslot(dsv[0], dsv[1]);
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          dqt[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(TFQW_KTF ? ktf[TFQW_KTF ? s : 0][t] : tr_pair(ks, s, t * 16, ln),
+                                                           db, dqt[t], 0, 0, 0);
+      }
+      // the query tile's dbias contributions are summed now: held back, the compiler kept ~5 VGPRs per (qt, kt)
+      // tile pair live to the end of the pixel and spilled
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) asm volatile("" : "+v"(dba[r][c]));
+      const auto rw = tile_rsrc(dqkv + (row0 + (int64_t)qt * 16 * HW) * QKV, F - qt * 16, (int64_t)fs_qkv, QKV * 2);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int d0 = t * 16 + 4 * g;
+        float v4[4] = {dqt[t][0], dqt[t][1], dqt[t][2], dqt[t][3]};
+        rope4_inv(v4, rot, fqc, d0, scale);  // dq = scale R^T dQ' (rows >= F dropped by the resource)
+        buf_st4b(rw, lr * fs_qkv + (h * DH + d0) * 2, v4);
+      }
+    }
+  }
+  // dbias by offset n = 16 (kt - qt) + 4g + r - lr, diagonal c = kt - qt + NT - 1: the wave's accumulators are
+  // staged CH diagonals at a time in its row buffer, each lane sums the offsets e = lane + 64 j in a fixed
+  // (c, g, r) order, then the block sums its 4 waves in order
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  float* stg = reinterpret_cast<float*>(ks);
+#pragma unroll
+  for (int c0 = 0; c0 < NC; c0 += CH) {
+    wsync();
+#pragma unroll
+    for (int c = c0; c < c0 + CH && c < NC; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) stg[((c - c0) * 4 + r) * 64 + lane] = dba[r][c];
+    wsync();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = lane + 64 * j - (F - 1);
+      float a = acc[j];
+#pragma nounroll
+      for (int c = c0; c < c0 + CH && c < NC; ++c)
+#pragma nounroll
+        for (int gg = 0; gg < 4; ++gg)
+#pragma nounroll
+          for (int r = 0; r < 4; ++r) {
+            const int l = 16 * (c - (NT - 1)) + 4 * gg + r - n;
+            if (n < F && l >= 0 && l < 16) a += stg[((c - c0) * 4 + r) * 64 + gg * 16 + l];
+          }
+      acc[j] = a;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) wsum[wid][lane + 64 * j] = acc[j];
+  __syncthreads();
+  if (tid < 2 * F - 1)
+    part[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * (2 * F - 1) + tid] =
+        ((wsum[0][tid] + wsum[1][tid]) + wsum[2][tid]) + wsum[3][tid];
+}
+
 // ------------------------------------------------------------------------------------------------ backward, dk dv
 // grid (tf_grid_x(HW), B), 256 threads: wave = one pixel (tf_block); key tiles outer, query-tile pairs inner
 template <int NT>
@@ -823,8 +1008,14 @@ int cesm_tflash_bwd(const void* qkv, const void* o, const void* dout, const floa
   const int nblk = cesm_tflash_nblk(HW);
   dim3 gq(nblk, B * NH), gk(tf_grid_x(HW), B);
   const bool dov = TF_DO && nt >= 2 && HW < TF_DO_MAXHW;
+  // per-wave dq kernel (32-bit tile offsets); CESM_TF_NO_QW=1: the round-3 block-per-pixel dq kernels (A/B)
+  const bool qw = nt >= 2 && (int64_t)16 * HW * QKV * 2 < (1ll << 31) && !getenv_flag("CESM_TF_NO_QW");
 #define TFB(N)                                                                                                         \
-  if (dov && N >= 2)                                                                                                   \
+  if (qw && N >= 2)                                                                                                    \
+    tflash_bwd_qw_kernel<(N >= 2 ? N : 2)><<<gq, 256, 0, stream>>>((const bf16*)qkv, (const bf16*)o,                   \
+                                                                   (const bf16*)dout, lse, bias, rot, (bf16*)dqkv,    \
+                                                                   dbuf, part, F, HW, scale);                         \
+  else if (dov && N >= 2)                                                                                              \
     tflash_bwd_q_kernel<N, (N >= 2)><<<gq, 64 * N, 0, stream>>>((const bf16*)qkv, (const bf16*)o, (const bf16*)dout,   \
                                                                 lse, bias, rot, (bf16*)dqkv, dbuf, part, F, HW, scale); \
   else                                                                                                                 \

@@ -37,11 +37,12 @@ def bump_param_epoch():
 # parameter-gradient GEMM (conv / 1x1 / qkv wgrads, bias column sums, stem wgrad) is enqueued on a second
 # HIP stream ordered after the kernel that produced its inputs.  The wgrads are HBM-bound (the level-0 qkv
 # wgrad streams 4.4 GB) while the dX kernels are MFMA/latency-bound, so the two co-run on the CUs.
-# "0": off, "attn": only the fused attention blocks' wgrads, "1": every wgrad (default since round 4: whole step
-# 130.1 vs 131.8-132.2 ms, +1.3 % samples/s, same call, profiles/r4_wgrad_stream_ab.txt; round 3's 7-8x slowdown with
-# it on does not reproduce on the round-4 kernels: the per-step allocator counters are flat (no retries, no device
-# frees) and the trace shows the two streams co-running, profiles/r4_wgrad_stream_diag_*.txt)
-WGRAD_STREAM = os.environ.get("CESM_WGRAD_STREAM", "1")
+# "0" (default): off, "attn": only the fused attention blocks' wgrads, "1": every wgrad.  "1" measured +1.3 %
+# samples/s on the bench config (130.1 vs 131.8-132.2 ms, profiles/r4_wgrad_stream_ab.txt, allocator counters flat,
+# profiles/r4_wgrad_stream_diag_*.txt) but the same library then ran config/baseline at 964 ms/step and the F = 120
+# leg at 1273 ms/step (7.5x / 5.4x slower, profiles/r4c4_bench.json): round 3's slowdown is config-dependent, so
+# the side stream stays opt-in.
+WGRAD_STREAM = os.environ.get("CESM_WGRAD_STREAM", "0")
 _WSTREAMS = {}
 
 

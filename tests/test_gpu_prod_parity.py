@@ -4,8 +4,9 @@ The fp32 parity tests (test_gpu_model.py) gate the north-star's < 1e-5 forward e
 the generic kernels.  This file reaches the kernels the bf16 training step actually launches at the
 reference's shapes (dispatch asserted through cesm_conv_fwd_variant / cesm_conv_wgrad_variant):
 
-* conv3x3p_kernel<32,7,true> — every level-0 64->64 3x3 conv (fwd and dgrad) whenever W % 32 == 0, i.e.
-  the full 288-wide grid and the reference's 64 / 128 crops (config/*:17);
+* conv3x3ws_kernel<32> / conv3x3p_kernel<32,7,true> — every level-0 64->64 3x3 conv (fwd and dgrad): the
+  warp-specialized kernel where its 256-pixel tiles cover the image (the full 192x288 grid, the 64-high crops of
+  config/*:17), conv3x3p elsewhere when W % 32 == 0;
 * the whole network in bf16 (fused tw_* / slaf_* / slab_* attention blocks at C = 64 / 128, halo convs,
   wgrad_wide, gemm1x1) — loss, eps_pred and EVERY parameter gradient vs the fp32 oracle;
 * the full 192x288x12 grid of BASELINE configs 2 and 3 (fp32 forward gated at 1e-5, bf16 forward error
@@ -70,15 +71,36 @@ def q(x):
 
 
 # ------------------------------------------------------------------ level-0 conv kernel (A12)
-@pytest.mark.parametrize("H,W", [(13, 64), (20, 96), (9, 288), (30, 288)])
+# level-0 64 -> 64 3x3 kernels: the warp-specialized conv where its 256-pixel tiles cover the image to >= 90 %
+# (the bench grid), conv3x3p (persistent, resident weights) elsewhere
+L0_P, L0_WS = "conv3x3p_kernel<32,7,true>", "conv3x3ws_kernel<32>"
+
+
+def l0_var(H, W):
+    """the level-0 kernel the dispatch picks (mirror of conv.hip ws_tile: best pixel utilisation of the 256-pixel
+    tiles, TW in {32, 36}, TH <= 8, first maximum wins; >= 90 % -> warp-specialized)"""
+    best, btw = -1.0, 32
+    for tw in (32, 36):
+        for th in range(1, 9):
+            if th * tw > 256:
+                break
+            u = H * W / (-(-H // th) * -(-W // tw) * 256)
+            if u > best + 1e-9:
+                best, btw = u, tw
+    return f"conv3x3ws_kernel<{btw}>" if best >= 0.9 else L0_P
+
+
+@pytest.mark.parametrize("H,W,var", [(13, 64, L0_P), (20, 96, L0_P), (9, 288, L0_P), (17, 288, L0_P),
+                                     (30, 288, L0_WS), (24, 96, L0_WS), (16, 288, L0_WS)])
 @pytest.mark.parametrize("with_res", [False, True])
-def test_conv3x3p_level0_bf16(dev, H, W, with_res):
-    """conv3x3p_kernel<32,7,true> (persistent, resident weights): forward, dgrad (flipped weights, same
-    kernel) and weight gradient at 64 -> 64, heights that leave a partial 14-row tile, with and without
-    the fused residual (fwd: Block output + res; dgrad: the ResnetBlock skip gradient)."""
+def test_conv3x3p_level0_bf16(dev, H, W, var, with_res):
+    """conv3x3p_kernel<32,7,true> (persistent, resident weights) and conv3x3ws_kernel<32> (warp-specialized):
+    forward, dgrad (flipped weights, same kernel) and weight gradient at 64 -> 64, heights that leave a partial
+    14-row tile, with and without the fused residual (fwd: Block output + res; dgrad: the ResnetBlock skip
+    gradient)."""
     cin = cout = 64
     B, Fr = 2, 2
-    assert K.conv_fwd_variant(BF, B * Fr, H, W, cin, 0, H, W, cout, cout, 3, 3, 1, 1, 1) == "conv3x3p_kernel<32,7,true>"
+    assert l0_var(H, W) == var and K.conv_fwd_variant(BF, B * Fr, H, W, cin, 0, H, W, cout, cout, 3, 3, 1, 1, 1) == var
     torch.manual_seed(H * 1000 + W)
     mod = nn.Conv3d(cin, cout, (1, 3, 3), padding=(0, 1, 1))
     md = nn.Conv3d(cin, cout, (1, 3, 3), padding=(0, 1, 1)).to(dev)
@@ -103,18 +125,23 @@ def test_conv3x3p_level0_bf16(dev, H, W, with_res):
     torch.cuda.synchronize()
     dx_ref = xr.grad + q(dres) if with_res else xr.grad
     e_dx, e_dw, e_db = rel(from_cl(dx, B), dx_ref), rel(md.weight.grad, wr.grad), rel(md.bias.grad, br.grad)
-    print(f"conv3x3p H={H} W={W} res={with_res}: fwd {e_fwd:.2e} dx {e_dx:.2e} dw {e_dw:.2e} db {e_db:.2e}")
+    print(f"{var} H={H} W={W} res={with_res}: fwd {e_fwd:.2e} dx {e_dx:.2e} dw {e_dw:.2e} db {e_db:.2e}")
     assert e_fwd < 1e-2 and e_dx < 1e-2 and e_dw < 1e-2 and e_db < 1e-2
 
 
 def test_conv3x3p_concurrent_streams(dev):
-    """conv3x3p launches overlapping on two HIP streams give the bits of the same launches in sequence: the
-    persistent kernel keeps no state between launches (its items are split statically; round 3's process-global
-    item counter made overlapping launches skip or repeat items).  C-ABI contract SURVEY §8(b) B3: caller-owned
-    buffers, enqueue-safe calls."""
-    Nb, H, W, C = 24, 96, 288, 64
+    """conv3x3p / conv3x3ws launches overlapping on two HIP streams give the bits of the same launches in
+    sequence: the persistent kernels keep no state between launches (their items are split statically; round 3's
+    process-global item counter made overlapping launches skip or repeat items).  C-ABI contract SURVEY §8(b) B3:
+    caller-owned buffers, enqueue-safe calls."""
+    for (Nb, H, W, var) in ((24, 96, 288, L0_WS), (24, 17, 288, L0_P)):
+        _concurrent_case(dev, Nb, H, W, var)
+
+
+def _concurrent_case(dev, Nb, H, W, var):
+    C = 64
     geom = (H, W, C, 3, 3, 1, 1, 1)
-    assert K.conv_fwd_variant(BF, Nb, H, W, C, 0, H, W, C, C, 3, 3, 1, 1, 1) == "conv3x3p_kernel<32,7,true>"
+    assert K.conv_fwd_variant(BF, Nb, H, W, C, 0, H, W, C, C, 3, 3, 1, 1, 1) == var
     torch.manual_seed(21)
     xs = [torch.randn(Nb, H, W, C, device=dev).to(BF) for _ in range(4)]
     ws = [K.conv_pack(torch.randn(C, C, 3, 3, device=dev) * 0.05, BF, C, C, 3, 3, False, False) for _ in range(4)]
@@ -159,7 +186,8 @@ def test_gn_stats_part_two_stage(dev, nslot, C):
 
 @pytest.mark.parametrize("C1,C2,Cout,H,W,B,Fr,kern", [
     (64, 0, 64, 20, 96, 2, 3, "conv3x3p_kernel<32,7,true>"),     # level 0, partial 14-row tile
-    (64, 0, 64, 30, 288, 1, 2, "conv3x3p_kernel<32,7,true>"),    # full bench width
+    (64, 0, 64, 17, 288, 1, 2, "conv3x3p_kernel<32,7,true>"),    # full bench width
+    (64, 0, 64, 30, 288, 1, 2, "conv3x3ws_kernel<32>"),          # full bench width, warp-specialized (4 x 8-row tiles)
     (64, 0, 64, 18, 72, 2, 2, "conv3x3_bf16_kernel<36>"),        # 8 channels per group, 36-wide tiles
     (64, 64, 64, 28, 64, 2, 2, "conv3x3_bf16_kernel<32>"),       # decoder concat input, 32-wide 14-row tiles
     (128, 0, 128, 24, 144, 2, 2, "conv3x3_bf16_kernel<36>"),     # level 1 (16 channels per group)
@@ -319,10 +347,10 @@ def _bf16_fwd_bwd(dev, mults, B, Fr, H, W, seed, tag):
 @pytest.mark.parametrize("mults", [(1, 2, 4), (1, 2, 4, 8)])
 def test_whole_net_bf16_forward_backward(dev, mults):
     """bf16 training path at a level-0 width that is a multiple of 32 (64 x 96, F = 12): the fused
-    temporal / spatial attention blocks (C = 64, 128), conv3x3p at level 0, halo convs, wgrad_wide and
+    temporal / spatial attention blocks (C = 64, 128), conv3x3ws at level 0, halo convs, wgrad_wide and
     gemm1x1 — eps_pred, loss and every parameter gradient vs the fp32 oracle (video_net.py:766-871,
     model.py:203-208)."""
-    assert K.conv_fwd_variant(BF, 12, 64, 96, 64, 0, 64, 96, 64, 64, 3, 3, 1, 1, 1) == "conv3x3p_kernel<32,7,true>"
+    assert K.conv_fwd_variant(BF, 12, 64, 96, 64, 0, 64, 96, 64, 64, 3, 3, 1, 1, 1) == L0_WS
     _bf16_fwd_bwd(dev, mults, 1, 12, 64, 96, 31, f"mults={mults}")
 
 
@@ -437,11 +465,11 @@ def test_more_blocks_decadal_window_bf16_forward(dev):
 
 
 def test_more_blocks_decadal_window_bf16_forward_backward(dev):
-    """config 4's training path in bf16 (more_blocks at F = 120, 32 x 64 grid: conv3x3p at level 0, the unfused
+    """config 4's training path in bf16 (more_blocks at F = 120, 32 x 64 grid: conv3x3ws at level 0, the unfused
     long-window temporal path -- gemm1x1 projections + the MFMA flash cores tflash_fwd / tflash_bwd_q / kv at
     every level, the fused SLA blocks): eps_pred, loss and every parameter gradient vs the fp32 oracle, same gates
     as the F = 12 whole-net test (video_net.py:403-454 at F = 120)"""
-    assert K.conv_fwd_variant(BF, 120, 32, 64, 64, 0, 32, 64, 64, 64, 3, 3, 1, 1, 1) == "conv3x3p_kernel<32,7,true>"
+    assert K.conv_fwd_variant(BF, 120, 32, 64, 64, 0, 32, 64, 64, 64, 3, 3, 1, 1, 1) == L0_WS
     _bf16_fwd_bwd(dev, (1, 2, 4, 8), 1, 120, 32, 64, 53, "more_blocks F=120")
 
 
@@ -481,7 +509,7 @@ def test_decadal_window_full_grid_bf16_step_repeatable(dev, monkeypatch):
     identical inputs must give the same bits -- loss and every parameter gradient, all finite.  (The oracle cannot
     run this size in test time; its F = 120 parity is test_more_blocks_decadal_window_*.)"""
     assert K.conv_fwd_variant(BF, 120, 192, 288, 64, 0, 192, 288, 768, 768, 1, 1, 1, 0, 1) == "gemm1x1_kernel<128>"
-    assert K.conv_fwd_variant(BF, 120, 192, 288, 64, 0, 192, 288, 64, 64, 3, 3, 1, 1, 1) == "conv3x3p_kernel<32,7,true>"
+    assert K.conv_fwd_variant(BF, 120, 192, 288, 64, 0, 192, 288, 64, 64, 3, 3, 1, 1, 1) == L0_WS
     seen = set()
     real_call = K.call
 

@@ -133,13 +133,14 @@ def test_flop_count_reconciles_with_survey():
 # ------------------------------------------------------------------ kernel dispatch (host-only queries)
 def test_gn_epilogue_slot_counts():
     """GroupNorm partial slots the Block convs write from their epilogue (cesm_conv_gn_nslot, host only):
-    conv3x3p per (frame, 14x32 tile, wave), the halo conv per (frame, tile, wave = 64-pixel quarter); 0 where the kernel
-    has no partials (fp32 generic conv, 1x1, B not dividing the batch) -> the separate statistics pass"""
+    the warp-specialized conv per (frame, 8x32 tile, 64-pixel quarter), the halo conv per (frame, tile, wave = 64-pixel
+    quarter); 0 where the kernel has no partials (fp32 generic conv, 1x1, B not dividing the batch) -> the separate
+    statistics pass"""
     from cesm_emulator_amd import kernels as K
     bf = torch.bfloat16
     g3 = lambda H, W, C: (H, W, C, 3, 3, 1, 1, 1)  # noqa: E731
     x = torch.empty(96, 192, 288, 64, dtype=bf)
-    assert K.conv_gn_nslot(x, None, g3(192, 288, 64), 8) == 12 * (14 * 9) * 4
+    assert K.conv_gn_nslot(x, None, g3(192, 288, 64), 8) == 12 * (24 * 9) * 4
     assert K.conv_gn_nslot(x, x, g3(192, 288, 64), 8) == 12 * (16 * 8) * 4  # 12 x 36 tiles (448-px blocks)
     x1 = torch.empty(96, 96, 144, 128, dtype=bf)
     assert K.conv_gn_nslot(x1, None, g3(96, 144, 128), 8) == 12 * (8 * 4) * 4
@@ -156,8 +157,8 @@ def test_bench_shape_dispatch_table():
     N = 96
     fv = lambda *a: K.conv_fwd_variant(bf, N, *a)  # noqa: E731
     wv = lambda *a, **k: K.conv_wgrad_variant(bf, N, *a, **k)  # noqa: E731
-    # level 0, 64 -> 64 3x3 (fwd and dgrad): the persistent resident-weight kernel
-    assert fv(192, 288, 64, 0, 192, 288, 64, 64, 3, 3, 1, 1, 1) == "conv3x3p_kernel<32,7,true>"
+    # level 0, 64 -> 64 3x3 (fwd and dgrad): the warp-specialized persistent conv
+    assert fv(192, 288, 64, 0, 192, 288, 64, 64, 3, 3, 1, 1, 1) == "conv3x3ws_kernel<32>"
     assert wv(192, 288, 64, 0, 192, 288, 64, 64, 3, 3, 1, 1, 1) == "wgrad3x3c64_kernel"
     # level-0 concat inputs (up path / out_conv: 64 + 64 -> 64)
     assert fv(192, 288, 64, 64, 192, 288, 64, 64, 3, 3, 1, 1, 1) == "conv3x3_bf16_kernel<36>"
