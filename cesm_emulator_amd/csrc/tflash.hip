@@ -622,6 +622,9 @@ __global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(DOV && 
 // Every lane-derived quantity is recomputed per pixel from an opaque copy of the lane id: as loop invariants the
 // compiler hoisted them all (per-frame RoPE coefficients, bias-table reads, LDS and global addresses: > 200
 // VGPRs at NT = 8) out of the pixel loop and spilled.
+#ifndef TF_QW_MINHW
+#define TF_QW_MINHW 32768
+#endif
 #ifndef TFQW_KREG
 #define TFQW_KREG 1  // K' A fragments of the pixel held in registers (0: re-read from the staged rows per query tile)
 #endif
@@ -1008,8 +1011,12 @@ int cesm_tflash_bwd(const void* qkv, const void* o, const void* dout, const floa
   const int nblk = cesm_tflash_nblk(HW);
   dim3 gq(nblk, B * NH), gk(tf_grid_x(HW), B);
   const bool dov = TF_DO && nt >= 2 && HW < TF_DO_MAXHW;
-  // per-wave dq kernel (32-bit tile offsets); CESM_TF_NO_QW=1: the round-3 block-per-pixel dq kernels (A/B)
-  const bool qw = nt >= 2 && (int64_t)16 * HW * QKV * 2 < (1ll << 31) && !getenv_flag("CESM_TF_NO_QW");
+  // per-wave dq kernel (32-bit tile offsets) from TF_QW_MINHW pixels: whole F = 120 backward 192x288 94.6 -> 14.0 ms
+  // (the block-per-pixel kernel's 432-pixel barrier-lockstep walk per block collapses there), 96x144 3.61 -> 3.72,
+  // 48x72 1.00 -> 1.10, 24x36 0.37 -> 0.41 (profiles/r4c5_qw_check.txt).  CESM_TF_QW=1 forces it for every F > 16,
+  // CESM_TF_NO_QW=1 disables it.
+  const bool qw = nt >= 2 && (int64_t)16 * HW * QKV * 2 < (1ll << 31) && !getenv_flag("CESM_TF_NO_QW") &&
+                  (HW >= TF_QW_MINHW || getenv_flag("CESM_TF_QW"));
 #define TFB(N)                                                                                                         \
   if (qw && N >= 2)                                                                                                    \
     tflash_bwd_qw_kernel<(N >= 2 ? N : 2)><<<gq, 256, 0, stream>>>((const bf16*)qkv, (const bf16*)o,                   \

@@ -2,7 +2,7 @@
 temporal-attention backward at the F = 120 level shapes and F = 12 / 24 / 40 windows, dqkv / rel-pos table
 gradient compared and timed.
 
-  python tools/tf_qw_check.py            (spawns itself twice: CESM_TF_NO_QW=1 and =0, then compares)
+  python tools/tf_qw_check.py            (spawns itself twice: CESM_TF_NO_QW=1 and CESM_TF_QW=1, then compares)
 """
 import os
 import subprocess
@@ -56,7 +56,7 @@ def main():
     outs = {}
     for v in ("1", "0"):
         path = f"/tmp/tf_qw_{v}.pt"
-        env = dict(os.environ, CESM_TF_NO_QW=v)
+        env = dict(os.environ, CESM_TF_NO_QW=v, CESM_TF_QW="0" if v == "1" else "1")
         r = subprocess.run([sys.executable, "-u", __file__, "--run", path], env=env, timeout=900)
         if r.returncode != 0:
             sys.exit(f"run CESM_TF_NO_QW={v} failed: {r.returncode}")
