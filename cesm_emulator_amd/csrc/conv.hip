@@ -493,6 +493,9 @@ __device__ __forceinline__ int h3_off(int row, int ch) { return row * H3_LD + ((
 #ifndef H3_XCD
 #define H3_XCD 1  // A/B knob: XCD-grouped co blocks of a halo tile (0 = co-block-slowest order)
 #endif
+#ifndef H3_TOUCH
+#define H3_TOUCH 0  // A/B knob: conv3x3_bf16_kernel L2 touch of the next input line two chunks ahead
+#endif
 #ifndef H3_BIG
 #define H3_BIG 1  // A/B knob: 448-pixel tiles with 64 co x 112 px wave tiles (0 = 256-pixel tiles, 64 x 64)
 #endif
@@ -536,6 +539,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
   const int nchunk = Cin / 32;
 
 #if H3_DMA
+  constexpr int H3_TPT = NJv == 7 ? 3 : 2;  // touch loads per thread: (TH + 2) x (TW + 2) <= 16 x 38 / 10 x 38 pixels
+  // the touch loads go LDS-direct into a never-read 256-B row per wave (no VGPRs held while they fly)
+  __shared__ __attribute__((aligned(16))) int tdump_s[H3_TOUCH ? 256 : 1];
+  int* tdump = tdump_s + (H3_TOUCH ? wid * 64 : 0);
   // stage one 32-channel chunk by buffer-LDS-DMA (no registers, no address VALU per element beyond one per
   // 16-B piece): 1-KiB pieces of 16 LDS rows, each lane fetching the global chunk that the row swizzle puts in
   // its slot (chunk = slot ^ ((row >> 1) & 2)); halo rows outside the tile / image read as zeros (out-of-range
@@ -577,7 +584,24 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
       __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(sw + q * 512), 16,
                                                ((co * 9 + tap) * Cin + chunk * 8) * 2, 0, 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // H3_TOUCH: at an even chunk of x1 whose pixel rows continue past this 128-B line, one 4-B load per halo pixel of
+    // the next line (chunks ch + 2, ch + 3) brings it into L2 while this chunk and the next compute; the wait below
+    // leaves those loads in flight (the next stage's vmcnt(0) retires them)
+    if (H3_TOUCH && (ch & 1) == 0 && c0 + 64 < g.C1) {
+#pragma unroll
+      for (int k = 0; k < H3_TPT; ++k) {
+        const int hp = tid + 256 * k;
+        const int r = hp / HWd, col = hp - r * HWd;
+        const int iy = y0 - 1 + r, ix = x0 - 1 + col;
+        const bool in = r < TH + 2 && (unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)tdump, 4,
+                                                 in ? ((iy * g.Wi + ix) * cs + 64) * 2 : 0x7ffffff0, 0, 0, 0);
+      }
+      if constexpr (H3_TPT == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   };
 #else
   // stage one 32-channel chunk: global -> registers -> LDS (transient registers; the second
@@ -1633,6 +1657,9 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
 // epilogue (~40 % of conv3x3p's time at one wave per SIMD, where it could not overlap the MFMAs) runs beside the next
 // item's MFMAs.  Both roles pass exactly the same barriers.  LDS: 2 stages x 61 KiB + a 34 KiB staging tile.
 // ----------------------------------------------------------------------------------------
+#ifndef WS_TOUCH
+#define WS_TOUCH 1  // L2 touch of the next item's halo lines a step ahead of its stage DMA
+#endif
 constexpr int WS_PITCH = 40;                               // halo row pitch (pixels): ky steps keep the swizzle
 constexpr int WS_MAXTH = 8;                                // tile rows: (8 + 2) * 40 = 400 halo rows
 constexpr int WS_HROWS = (WS_MAXTH + 2) * WS_PITCH;        // 400
@@ -1641,7 +1668,7 @@ constexpr int WS_STAGE = (WS_HROWS + WS_WROWS) * 64;       // 62,464 B
 constexpr int WS_PIX = 256;                                // pixels per item (4 waves x 4 groups of 16)
 constexpr int WS_ELD = 68;                                 // staging row (bf16): 136 B, conflict-free 8-B writes
 constexpr int WS_LDS = 2 * WS_STAGE + WS_PIX * WS_ELD * 2;  // 159,744 B
-static_assert(WS_LDS <= 160 * 1024, "warp-specialized conv LDS");
+static_assert(WS_LDS + 1024 <= 160 * 1024, "warp-specialized conv LDS");
 constexpr int WS_HPMAX = (WS_HROWS / 16 + 3) / 4;          // halo pieces per loader wave (<= 7)
 constexpr int WS_WP = WS_WROWS / 16 / 4;                   // weight pieces per loader wave (9)
 
@@ -1660,7 +1687,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3ws_kernel(const bf16* __restric
                                                            bf16* __restrict__ y1, bf16* __restrict__ y2, ConvGeom g,
                                                            int TH, int tiles_x, int tiles_per_img, int ncob,
                                                            int nitems_pad, float* __restrict__ gnp, int gn_fimg) {
-  __shared__ __attribute__((aligned(1024))) char lds[WS_LDS];
+  __shared__ __attribute__((aligned(1024))) char lds[WS_LDS + 1024];  // + the touch loads' never-read rows
   bf16* stg = reinterpret_cast<bf16*>(lds + 2 * WS_STAGE);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const bool loader = wid >= 4;  // wave-uniform role
@@ -1765,6 +1792,42 @@ __global__ __launch_bounds__(512, 1) void conv3x3ws_kernel(const bf16* __restric
     }
   };
   const bool has_res = (res != nullptr) || (res2 != nullptr);
+  // L2 touch of the next item's input halo (WS_TOUCH): one 4-B load per halo pixel line of x1, issued at an item's
+  // first step, so the stage DMA of that item -- a step later -- finds its lines in L2 instead of waiting out HBM
+  // latency with one stage in flight.  Covers every channel of a pixel when C1 * 2 <= 128 B (level 0).  The loads
+  // go LDS-direct into a never-read 256-B row per loader wave: no VGPRs held while they fly.
+  auto touch = [&](int it) {
+    int n, y0, x0, cb, tile;
+    geo(it, n, y0, x0, cb, tile);
+    const int64_t img = (int64_t)g.Hi * g.Wi * g.C1;
+    const __amdgpu_buffer_rsrc_t xrs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(x1 + n * img), (short)0, (int)(img * 2), 0x00020000);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int q = lane + 64 * (wl + 4 * k);
+      const int hy = q / (TW + 2), hx = q - hy * (TW + 2);
+      const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
+      const bool in = hy < TH + 2 && (unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)(lds + WS_LDS + wl * 256),
+                                               4, in ? (iy * g.Wi + ix) * g.C1 * 2 : 0x7ffffff0, 0, 0, 0);
+    }
+  };
+  // s_waitcnt vmcnt(n) for the counts the loader loop leaves in flight
+  auto vm_wait = [&](int n) {
+    switch (n) {
+      case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+      case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+      case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+      case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+      case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+      case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+      case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+      case 17: asm volatile("s_waitcnt vmcnt(17)" ::: "memory"); break;
+      case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+      case 19: asm volatile("s_waitcnt vmcnt(19)" ::: "memory"); break;
+      default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+  };
   // epilogue of item it from the staging tile; returns after issuing its stores (8 rows + GN partial)
   auto epilogue = [&](int it) {
     int n, y0, x0, cb, tile;
@@ -1849,6 +1912,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3ws_kernel(const bf16* __restric
     issue_stage(it0, 0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int it = it0, ch = 0, s = 0, prev_it = -1;
+    const bool do_touch = WS_TOUCH && g.C1 * 2 <= 128 && nchunk >= 2;
     while (true) {
       __builtin_amdgcn_s_barrier();  // stage s landed; stage s - 1 consumed; staging of prev_it written (ch == 0)
       const int nxt_ch = ch + 1 < nchunk ? ch + 1 : 0;
@@ -1861,19 +1925,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3ws_kernel(const bf16* __restric
       // the next step ends item nxt_it (nchunk >= 2): its residual rows now, in registers at its epilogue
       const bool pre = more && has_res && nxt_ch == nchunk - 1;
       if (pre) load_res(nxt_it);
-      // wait for this step's DMA only: the epilogue's stores (8 rows [+ 1 GN partial]) and the residual loads (8)
-      // issued after it may stay in flight
-      if (epi && pre) {
-        if constexpr (GN) asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      } else if (epi) {
-        if constexpr (GN) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      } else if (pre) {
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
+      // the item after next: its halo lines into L2 while this item's chunks run
+      int tit = nitems_pad;
+      if (do_touch && ch == 0) tit = next_valid(it + G);
+      const bool tch = tit < nitems_pad;
+      if (tch) touch(tit);
+      // wait for this step's DMA only: the epilogue's stores (8 rows [+ 1 GN partial]), the residual loads (8) and
+      // the touches (2) issued after it may stay in flight
+      vm_wait((epi ? (GN ? 9 : 8) : 0) + (pre ? 8 : 0) + (tch ? 2 : 0));
       if (ch == nchunk - 1) prev_it = it;
       ch = nxt_ch;
       it = nxt_it;
