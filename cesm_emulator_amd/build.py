@@ -55,10 +55,14 @@ def build(force: bool = False) -> Path:
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
         objs = list(ex.map(_compile, srcs))
     if force or not LIB.exists() or any(o.stat().st_mtime > LIB.stat().st_mtime for o in objs):
-        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-Wl,--no-undefined", *map(str, objs), "-o", str(LIB)]
+        # link next to the library and rename over it: a reader (a running process, a tree snapshot) sees the old
+        # or the new file, never a partly written one
+        tmp = LIB.with_name(LIB.name + ".tmp")
+        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-Wl,--no-undefined", *map(str, objs), "-o", str(tmp)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr}")
+        os.replace(tmp, LIB)
     return LIB
 
 

@@ -968,7 +968,35 @@ __global__ void tf_dtable_kernel(const float* __restrict__ off, float* __restric
 
 }  // namespace
 
+// which dq kernel cesm_tflash_bwd runs.  The per-wave kernel (32-bit tile offsets) from TF_QW_MINHW pixels: whole
+// F = 120 backward 192x288 94.6 -> 14.0 ms (the block-per-pixel kernel's 432-pixel barrier-lockstep walk per block
+// collapses there), 96x144 3.61 -> 3.72, 48x72 1.00 -> 1.10, 24x36 0.37 -> 0.41 (profiles/r4c5_qw_check.txt).
+// CESM_TF_QW=1 forces it for every F > 16, CESM_TF_NO_QW=1 disables it.
+enum TfDq { TF_DQ_BLOCK, TF_DQ_DOV, TF_DQ_WAVE };
+static TfDq tf_dq_kind(int nt, int HW) {
+  if (nt >= 2 && (int64_t)16 * HW * QKV * 2 < (1ll << 31) && !getenv_flag("CESM_TF_NO_QW") &&
+      (HW >= TF_QW_MINHW || getenv_flag("CESM_TF_QW")))
+    return TF_DQ_WAVE;
+  return TF_DO && nt >= 2 && HW < TF_DO_MAXHW ? TF_DQ_DOV : TF_DQ_BLOCK;
+}
+
 extern "C" {
+
+// name of the dq kernel cesm_tflash_bwd runs for (F, HW) (host-only query; "invalid" when F is unsupported)
+const char* cesm_tflash_bwd_variant(int F, int HW) {
+  static const char* names[3][9] = {
+      {"", "tflash_bwd_q_kernel<1,false>", "tflash_bwd_q_kernel<2,false>", "tflash_bwd_q_kernel<3,false>",
+       "tflash_bwd_q_kernel<4,false>", "tflash_bwd_q_kernel<5,false>", "tflash_bwd_q_kernel<6,false>",
+       "tflash_bwd_q_kernel<7,false>", "tflash_bwd_q_kernel<8,false>"},
+      {"", "", "tflash_bwd_q_kernel<2,true>", "tflash_bwd_q_kernel<3,true>", "tflash_bwd_q_kernel<4,true>",
+       "tflash_bwd_q_kernel<5,true>", "tflash_bwd_q_kernel<6,true>", "tflash_bwd_q_kernel<7,true>",
+       "tflash_bwd_q_kernel<8,true>"},
+      {"", "", "tflash_bwd_qw_kernel<2>", "tflash_bwd_qw_kernel<3>", "tflash_bwd_qw_kernel<4>",
+       "tflash_bwd_qw_kernel<5>", "tflash_bwd_qw_kernel<6>", "tflash_bwd_qw_kernel<7>", "tflash_bwd_qw_kernel<8>"}};
+  if (F < 1 || F > 16 * TF_MAXT || HW < 1) return "invalid";
+  const int nt = (F + 15) / 16;
+  return names[tf_dq_kind(nt, HW)][nt];
+}
 
 // supported windows of the MFMA temporal-attention core (bf16)
 int cesm_tflash_supported(int F) { return F >= 1 && F <= 16 * TF_MAXT; }
@@ -1010,13 +1038,8 @@ int cesm_tflash_bwd(const void* qkv, const void* o, const void* dout, const floa
   const int nt = (F + 15) / 16;
   const int nblk = cesm_tflash_nblk(HW);
   dim3 gq(nblk, B * NH), gk(tf_grid_x(HW), B);
-  const bool dov = TF_DO && nt >= 2 && HW < TF_DO_MAXHW;
-  // per-wave dq kernel (32-bit tile offsets) from TF_QW_MINHW pixels: whole F = 120 backward 192x288 94.6 -> 14.0 ms
-  // (the block-per-pixel kernel's 432-pixel barrier-lockstep walk per block collapses there), 96x144 3.61 -> 3.72,
-  // 48x72 1.00 -> 1.10, 24x36 0.37 -> 0.41 (profiles/r4c5_qw_check.txt).  CESM_TF_QW=1 forces it for every F > 16,
-  // CESM_TF_NO_QW=1 disables it.
-  const bool qw = nt >= 2 && (int64_t)16 * HW * QKV * 2 < (1ll << 31) && !getenv_flag("CESM_TF_NO_QW") &&
-                  (HW >= TF_QW_MINHW || getenv_flag("CESM_TF_QW"));
+  const TfDq kind = tf_dq_kind(nt, HW);
+  const bool qw = kind == TF_DQ_WAVE, dov = kind == TF_DQ_DOV;
 #define TFB(N)                                                                                                         \
   if (qw && N >= 2)                                                                                                    \
     tflash_bwd_qw_kernel<(N >= 2 ? N : 2)><<<gq, 256, 0, stream>>>((const bf16*)qkv, (const bf16*)o,                   \

@@ -703,6 +703,11 @@ def conv_fwd_variant(dtype, Nb, Hi, Wi, C1, C2, Ho, Wo, Cout, Co1, KH, KW, S, P,
     return lib().cesm_conv_fwd_variant(_DT[dtype], Nb, Hi, Wi, C1, C2, Ho, Wo, Cout, Co1, KH, KW, S, P, U).decode()
 
 
+def tflash_bwd_variant(F, HW):
+    """name of the dq kernel cesm_tflash_bwd selects (host-only query)"""
+    return lib().cesm_tflash_bwd_variant(F, HW).decode()
+
+
 def conv_wgrad_variant(dtype, Nb, Hi, Wi, C1, C2, Ho, Wo, Cout, Co1, KH, KW, S, P, U, with_bias=False):
     """name of the kernel cesm_conv_wgrad selects (host-only query)"""
     return lib().cesm_conv_wgrad_variant(_DT[dtype], Nb, Hi, Wi, C1, C2, Ho, Wo, Cout, Co1, KH, KW, S, P, U,

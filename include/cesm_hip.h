@@ -131,6 +131,8 @@ int cesm_tattn_bwd(int dtype, const void* qkv, const void* o, const void* dout, 
  * gradient (nullable).  Workspaces: dbuf B*8*HW*F, part B*8*cesm_tflash_nblk(HW)*(2F-1), off 8*(2F-1) floats. */
 int cesm_tflash_supported(int F);
 int cesm_tflash_nblk(int HW);
+/* name of the dq kernel cesm_tflash_bwd runs for (F, HW) (host-only query) */
+const char* cesm_tflash_bwd_variant(int F, int HW);
 int cesm_tflash_fwd(const void* qkv, const float* bias, const float* rot, void* out, float* lse, int B, int F, int HW,
                     float scale, hipStream_t stream);
 int cesm_tflash_bwd(const void* qkv, const void* o, const void* dout, const float* lse, const float* bias,

@@ -13,4 +13,5 @@ for f in cesm_emulator_amd/csrc/*.hip; do
   objs="$objs $o"
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -Wl,--no-undefined $objs -o cesm_emulator_amd/libcesm_hip_$name.so
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -Wl,--no-undefined $objs -o cesm_emulator_amd/libcesm_hip_$name.so.tmp
+mv -f cesm_emulator_amd/libcesm_hip_$name.so.tmp cesm_emulator_amd/libcesm_hip_$name.so
