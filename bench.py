@@ -15,7 +15,7 @@ Prints ONE JSON line (rank 0) with the contract fields plus
                 profiled ops in the last two warm-up steps, then timed live over the timed steps (events on the
                 stream it runs on, around its launches only, so the timed region stays uninstrumented otherwise):
                 algorithmic FLOP and bytes per launch, bound = the larger of the two floors, achieved / peak,
-                PMC traffic measured at the bench batch (profiles/r2_step_traffic.json);
+                PMC traffic measured at the bench batch (profiles/step_traffic.json);
   top_kernels   the five most expensive kernels by time per step (from the profiled warm-up steps), same fields;
   cpu_baseline  oracle fp32 train steps on the host cores (SURVEY.md §8(d) D5);
   fwd_error     forward error of the HIP path vs the CPU oracle (the metric's "fwd MSE vs ref").
@@ -38,7 +38,7 @@ sys.path.insert(0, ROOT)
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense BF16 MFMA (MI355X_MICROARCH.md, chip-level table)
 PEAK_F32_TFLOPS = 157.3     # f32 MFMA
 PEAK_HBM_GBS = 8000.0
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r2_step_traffic.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "step_traffic.json")
 
 
 def parse():

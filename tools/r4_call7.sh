@@ -20,7 +20,7 @@ tail -9 gpurun_out/${tag}_ws_h3touch.txt
 out=gpurun_out/${tag}_bench_ab.txt
 : > $out
 for rep in 1 2; do
-  for v in default wsT0 h3T; do
+  for v in default wsT0 h3T wgT; do
     lib=cesm_emulator_amd/libcesm_hip.so; [ $v != default ] && lib=cesm_emulator_amd/libcesm_hip_$v.so
     CESM_HIP_LIB=$lib timeout -k 10 240 python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --other-configs "" \
       > gpurun_out/${tag}_b.json 2>/dev/null
