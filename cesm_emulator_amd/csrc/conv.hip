@@ -2913,6 +2913,13 @@ constexpr int W3_PLANE = (W3_TH + 2) * W3_P * 32;  // halo plane (bf16 elements)
 
 // (Round 3 measured a 4-wave form -- one wave per SIMD, 144 accumulators, all four co tiles per wave -- as neutral,
 // 63.69 vs 63.58 ms conv total per step: fewer LDS reads per MFMA, less latency hiding.  Removed.)
+#ifndef W36_TOUCH
+#define W36_TOUCH 0
+#endif
+#ifndef WG_TOUCH
+#define WG_TOUCH 1  // 3x3 wgrad kernels: L2 touch of the tile after next (wgrad3x3c64 415 -> 389 us per launch in the step,
+                    // profiles/r4c7b_bench_ab.txt)
+#endif
 constexpr int WG_NT = 512;  // threads per block
 constexpr int WG_NI = 2;    // co tiles per wave
 __global__ __launch_bounds__(WG_NT, 1) void wgrad3x3c64_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
@@ -2980,6 +2987,34 @@ __global__ __launch_bounds__(WG_NT, 1) void wgrad3x3c64_kernel(const bf16* __res
       hv[k] = ok ? v : bf16x8{};
     }
   };
+  // WG_TOUCH (A/B knob): the dY and input-halo lines of the tile after next, LDS-direct into a never-read row per wave
+  // (4 B per 128-B pixel line), so the register prefetch of that tile a step later finds them in L2
+  __shared__ __attribute__((aligned(16))) int tdump[WG_TOUCH ? WG_NT : 1];
+  auto touch = [&](int tile) {
+    const int n = tile / tiles_per_img;
+    const int rem = tile - n * tiles_per_img;
+    const int ty = rem / tiles_x, tx = rem - ty * tiles_x;
+    const int y0 = ty * W3_TH, x0 = tx * W3_TW;
+    const int64_t yimg = (int64_t)g.Ho * g.Wo * ycs, ximg = (int64_t)g.Hi * g.Wi * xcs;
+    const __amdgpu_buffer_rsrc_t yrs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(ys + n * yimg + ycc), (short)0, (int)(yimg * 2 - ycc * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t xrs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(xs + n * ximg + xcc), (short)0, (int)(ximg * 2 - xcc * 2), 0x00020000);
+    auto* dst = (__attribute__((address_space(3))) void*)(tdump + (WG_TOUCH ? wid * 64 : 0));
+    {  // dY: 256 pixels
+      const int p = tid & 255;
+      const int oy = y0 + (p >> 5), ox = x0 + (p & 31);
+      const bool ok = tid < 256 && oy < g.Ho && ox < g.Wo;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(yrs, dst, 4, ok ? (oy * g.Wo + ox) * ycs * 2 : 0x7ffffff0, 0, 0, 0);
+    }
+    {  // halo: 340 pixels (threads 256..511 and 0..83)
+      const int hp = tid < 256 ? 256 + tid : tid - 256;
+      const int r = hp / W3_HW, c = hp - r * W3_HW;
+      const int iy = y0 - 1 + r, ix = x0 - 1 + c;
+      const bool ok = hp < W3_NPIX && (unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, dst, 4, ok ? (iy * g.Wi + ix) * xcs * 2 : 0x7ffffff0, 0, 0, 0);
+    }
+  };
   if ((int)blockIdx.z < ntiles) gload(blockIdx.z);
   for (int tile = blockIdx.z; tile < ntiles; tile += gridDim.z) {
     __syncthreads();
@@ -3002,6 +3037,7 @@ __global__ __launch_bounds__(WG_NT, 1) void wgrad3x3c64_kernel(const bf16* __res
     }
     __syncthreads();
     if (tile + (int)gridDim.z < ntiles) gload(tile + gridDim.z);
+    if (WG_TOUCH && tile + 2 * (int)gridDim.z < ntiles) touch(tile + 2 * gridDim.z);
     // the fragment reads of pixel row py+1 (2 NI + 18) are issued between the 9 NI MFMAs of row py (two register
     // sets; 1 read : 1 MFMA via sched_group_barrier), so no row waits for its LDS reads
     bf16x8 fa[2][WG_NI], fb[2][9];
@@ -3426,6 +3462,35 @@ __global__ __launch_bounds__(WG_NT, 1) void wgrad3x3w36c64_kernel(const bf16* __
       hv[k] = ok ? v : bf16x8{};
     }
   };
+  // W36_TOUCH (A/B knob, +8 spilled VGPRs): as wgrad3x3c64_kernel, the tile after next's dY / halo lines into L2
+  __shared__ __attribute__((aligned(16))) int tdump[W36_TOUCH ? WG_NT : 1];
+  auto touch = [&](int tile) {
+    const int n = tile / tiles_per_img;
+    const int rem = tile - n * tiles_per_img;
+    const int ty = rem / tiles_x, tx = rem - ty * tiles_x;
+    const int y0 = ty * W36_TH, x0 = tx * W36_TW;
+    const int64_t yimg = (int64_t)g.Ho * g.Wo * ycs, ximg = (int64_t)g.Hi * g.Wi * xcs;
+    const __amdgpu_buffer_rsrc_t yrs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(ys + n * yimg + ycc), (short)0, (int)(yimg * 2 - ycc * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t xrs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(xs + n * ximg + xcc), (short)0, (int)(ximg * 2 - xcc * 2), 0x00020000);
+    auto* dst = (__attribute__((address_space(3))) void*)(tdump + (W36_TOUCH ? wid * 64 : 0));
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {  // items 0..287: dY pixels, 288..667: halo pixels
+      const int e = tid + k * WG_NT;
+      if (e < W36_NP) {
+        const int oy = y0 + e / W36_TW, ox = x0 + e % W36_TW;
+        const bool ok = oy < g.Ho && ox < g.Wo;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(yrs, dst, 4, ok ? (oy * g.Wo + ox) * ycs * 2 : 0x7ffffff0, 0, 0, 0);
+      } else {
+        const int hp = e - W36_NP;
+        const int r = hp / W36_HW, c = hp - r * W36_HW;
+        const int iy = y0 - 1 + r, ix = x0 - 1 + c;
+        const bool ok = hp < W36_NPIX && (unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, dst, 4, ok ? (iy * g.Wi + ix) * xcs * 2 : 0x7ffffff0, 0, 0, 0);
+      }
+    }
+  };
   if ((int)blockIdx.z < ntiles) gload(blockIdx.z);
   for (int tile = blockIdx.z; tile < ntiles; tile += gridDim.z) {
     __syncthreads();
@@ -3450,6 +3515,7 @@ __global__ __launch_bounds__(WG_NT, 1) void wgrad3x3w36c64_kernel(const bf16* __
     }
     __syncthreads();
     if (tile + (int)gridDim.z < ntiles) gload(tile + gridDim.z);
+    if (W36_TOUCH && tile + 2 * (int)gridDim.z < ntiles) touch(tile + 2 * gridDim.z);
     // flat pixel of this lane's two 4-pixel groups in K-chunk kc: P = kc*32 + r0[half] -> (row, col) of the
     // 36-wide tile (32 < 36: at most one wrap per chunk)
     int prow[2], pcol[2];
