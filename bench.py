@@ -192,8 +192,9 @@ class KernelProbe:
         def tattn_bwd(qkv, o, dout, lse, bias, rot, dtable, B, F, HW, scale, num_buckets=32, max_distance=32):
             v = B * F * HW
             nt = (F + 15) // 16
-            lab = (f"tflash_bwd_q_kernel<{nt}> + tflash_bwd_kv_kernel<{nt}>" if K._tflash(qkv, F)
-                   else "tattn_bwd_kernel")
+            # the dq kernel by dispatch (per-wave from 32768 pixels, block-per-pixel below: cesm_tflash_bwd_variant)
+            lab = (f"{K.tflash_bwd_variant(F, HW).replace(',false>', '>').replace(',true>', '>')} + "
+                   f"tflash_bwd_kv_kernel<{nt}>" if K._tflash(qkv, F) else "tattn_bwd_kernel")
             # dP, dQ, dK, dV products (2x the forward); bytes: qkv, o, dout, lse read, dqkv written
             return lab, 8.0 * F * 32 * 8 * v, float(v * (768 * 2 * 2 + 256 * 2 * 2 + 32))
 
