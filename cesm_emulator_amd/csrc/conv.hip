@@ -1660,6 +1660,9 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
 #ifndef WS_TOUCH
 #define WS_TOUCH 1  // L2 touch of the next item's halo lines a step ahead of its stage DMA
 #endif
+#ifndef WS_RW
+#define WS_RW 1  // resident weights when Cin = 64 and one co block (the level-0 64 -> 64 conv)
+#endif
 constexpr int WS_PITCH = 40;                               // halo row pitch (pixels): ky steps keep the swizzle
 constexpr int WS_MAXTH = 8;                                // tile rows: (8 + 2) * 40 = 400 halo rows
 constexpr int WS_HROWS = (WS_MAXTH + 2) * WS_PITCH;        // 400
@@ -1669,6 +1672,7 @@ constexpr int WS_PIX = 256;                                // pixels per item (4
 constexpr int WS_ELD = 68;                                 // staging row (bf16): 136 B, conflict-free 8-B writes
 constexpr int WS_LDS = 2 * WS_STAGE + WS_PIX * WS_ELD * 2;  // 159,744 B
 static_assert(WS_LDS + 1024 <= 160 * 1024, "warp-specialized conv LDS");
+static_assert(2 * WS_WROWS * 64 + 2 * WS_HROWS * 64 == 2 * WS_STAGE, "resident-weight layout = the two stages");
 constexpr int WS_HPMAX = (WS_HROWS / 16 + 3) / 4;          // halo pieces per loader wave (<= 7)
 constexpr int WS_WP = WS_WROWS / 16 / 4;                   // weight pieces per loader wave (9)
 
@@ -1723,6 +1727,26 @@ __global__ __launch_bounds__(512, 1) void conv3x3ws_kernel(const bf16* __restric
     const int hy = row / WS_PITCH, hx = row - hy * WS_PITCH;
     hrel[k] = (hy < TH + 2 && hx < TW + 2) ? (hy << 16) | hx : -1;
   }
+  // RW (resident weights, WS_RW): with 64 input channels and one co block the two weight chunks never change, so
+  // they are staged once and the per-step DMA carries only the halo chunk (25 KB instead of 61 KB: the LDS-DMA
+  // fill rate per CU, not HBM, bounded the step).  The layout is the same 156 KB rearranged: weight chunks 0 / 1 at
+  // [0, 73728), halo stages at 73728 + st * 25600 (else stage st = halo + weights at st * WS_STAGE).
+  const bool rw = WS_RW && Cin == 64 && ncob == 1;
+  auto hbase = [&](int st) { return lds + (rw ? 2 * WS_WROWS * 64 + st * WS_HROWS * 64 : st * WS_STAGE); };
+  auto wbase = [&](int st, int ch) { return rw ? lds + ch * WS_WROWS * 64 : lds + st * WS_STAGE + WS_HROWS * 64; };
+  auto issue_w = [&](int cb, int ch, char* dst) {  // the weight chunk ch of co block cb
+    const int c0 = ch * 32;
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(w + (int64_t)cb * 64 * 9 * Cin + c0), (short)0, 64 * 9 * Cin * 2 - c0 * 2, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < WS_WP; ++k) {
+      const int q = wl + 4 * k, row = 16 * q + prow;  // row = tap * 64 + co
+      const int chunk = pslot ^ cw_swz(row);
+      const int vo = (((row & 63) * 9 + (row >> 6)) * Cin + chunk * 8) * 2;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(dst + q * 1024), 16, vo,
+                                               0, 0, 0);
+    }
+  };
   auto issue_stage = [&](int it, int ch, int st) {  // loader waves: chunk ch of item it -> stage st
     int n, y0, x0, cb, tile;
     geo(it, n, y0, x0, cb, tile);
@@ -1733,9 +1757,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3ws_kernel(const bf16* __restric
     const int64_t img = (int64_t)g.Hi * g.Wi * cs;
     const __amdgpu_buffer_rsrc_t xrs =
         __builtin_amdgcn_make_buffer_rsrc((void*)(src + n * img + cc), (short)0, (int)(img * 2 - cc * 2), 0x00020000);
-    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(w + (int64_t)cb * 64 * 9 * Cin + c0), (short)0, 64 * 9 * Cin * 2 - c0 * 2, 0x00020000);
-    char* dst = lds + st * WS_STAGE;
+    char* dst = hbase(st);
 #pragma unroll
     for (int k = 0; k < WS_HPMAX; ++k) {
       const int q = wl + 4 * k;
@@ -1748,14 +1770,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3ws_kernel(const bf16* __restric
                                                  0, 0, 0);
       }
     }
-#pragma unroll
-    for (int k = 0; k < WS_WP; ++k) {
-      const int q = wl + 4 * k, row = 16 * q + prow;  // row = tap * 64 + co
-      const int chunk = pslot ^ cw_swz(row);
-      const int vo = (((row & 63) * 9 + (row >> 6)) * Cin + chunk * 8) * 2;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          wrs, (__attribute__((address_space(3))) void*)(dst + WS_HROWS * 64 + q * 1024), 16, vo, 0, 0, 0);
-    }
+    if (!rw) issue_w(cb, ch, wbase(st, ch));
   };
   // epilogue rows of loader wave wl: pixels 64 wl + 8 u + (lane >> 3), u = 0..7, channels (lane & 7) * 8 .. + 7
   bf16x8 resv[8];
@@ -1909,6 +1924,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3ws_kernel(const bf16* __restric
   int it0 = next_valid((int)blockIdx.x);
   if (it0 >= nitems_pad) return;  // whole block, before any barrier
   if (loader) {
+    if (rw) {
+      issue_w(0, 0, wbase(0, 0));
+      issue_w(0, 1, wbase(0, 1));
+    }
     issue_stage(it0, 0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int it = it0, ch = 0, s = 0, prev_it = -1;
@@ -1955,8 +1974,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3ws_kernel(const bf16* __restric
         for (int i = 0; i < 4; ++i)
           bv4[i] = bias ? *reinterpret_cast<const f32x4*>(bias + cb * 64 + i * 16 + lg * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
       }
-      const char* sh = lds + (s & 1) * WS_STAGE;
-      cp_taps<4>(sh, sh + WS_HROWS * 64, bad, a_lane, acc);
+      cp_taps<4>(hbase(s & 1), wbase(s & 1, ch), bad, a_lane, acc);
       if (ch == nchunk - 1) {  // item end: (acc + bias) as bf16 rows of the staging tile
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
