@@ -493,6 +493,9 @@ __device__ __forceinline__ int h3_off(int row, int ch) { return row * H3_LD + ((
 #ifndef H3_XCD
 #define H3_XCD 1  // A/B knob: XCD-grouped co blocks of a halo tile (0 = co-block-slowest order)
 #endif
+#ifndef H3_WREG
+#define H3_WREG 0  // A/B knob: conv3x3_bf16_kernel weight chunk through registers instead of LDS-DMA
+#endif
 #ifndef H3_TOUCH
 #define H3_TOUCH 0  // A/B knob: conv3x3_bf16_kernel L2 touch of the next input line two chunks ahead
 #endif
@@ -576,13 +579,27 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
                                                  0, 0);
       }
     }
+    // H3_WREG (A/B knob): the weight chunk through registers (16-B global loads, then LDS stores after the wait)
+    // instead of LDS-DMA, so the per-chunk DMA volume is the halo only
+    bf16x8 wreg[H3_WREG ? H3_WPT : 1];
+    if (H3_WREG) {
 #pragma unroll
-    for (int k = 0; k < 9; ++k) {  // weights: 9 taps x 64 co rows = 36 pieces
-      const int q = wid + 4 * k, row = 16 * q + prow;  // row = tap * 64 + co
-      const int tap = row >> 6, co = row & 63;
-      const int chunk = pslot ^ ((row >> 1) & 2);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(sw + q * 512), 16,
-                                               ((co * 9 + tap) * Cin + chunk * 8) * 2, 0, 0, 0);
+      for (int k = 0; k < H3_WPT; ++k) {
+        const int e = tid + k * 256;
+        const int row = e >> 2, part = e & 3;  // row = tap * 64 + co
+        const int tap = row / H3_BN, co = row - tap * H3_BN;
+        wreg[k] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                 wrs, ((co * 9 + tap) * Cin + part * 8) * 2, 0, 0));
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {  // weights: 9 taps x 64 co rows = 36 pieces
+        const int q = wid + 4 * k, row = 16 * q + prow;  // row = tap * 64 + co
+        const int tap = row >> 6, co = row & 63;
+        const int chunk = pslot ^ ((row >> 1) & 2);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(sw + q * 512), 16,
+                                                 ((co * 9 + tap) * Cin + chunk * 8) * 2, 0, 0, 0);
+      }
     }
     // H3_TOUCH: at an even chunk of x1 whose pixel rows continue past this 128-B line, one 4-B load per halo pixel of
     // the next line (chunks ch + 2, ch + 3) brings it into L2 while this chunk and the next compute; the wait below
@@ -601,6 +618,13 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
       else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (H3_WREG) {
+#pragma unroll
+      for (int k = 0; k < H3_WPT; ++k) {
+        const int e = tid + k * 256;
+        *reinterpret_cast<bf16x8*>(sw + h3_off(e >> 2, e & 3)) = wreg[k];
+      }
     }
   };
 #else
