@@ -493,12 +493,6 @@ __device__ __forceinline__ int h3_off(int row, int ch) { return row * H3_LD + ((
 #ifndef H3_XCD
 #define H3_XCD 1  // A/B knob: XCD-grouped co blocks of a halo tile (0 = co-block-slowest order)
 #endif
-#ifndef H3_WREG
-#define H3_WREG 0  // A/B knob: conv3x3_bf16_kernel weight chunk through registers instead of LDS-DMA
-#endif
-#ifndef H3_TOUCH
-#define H3_TOUCH 0  // A/B knob: conv3x3_bf16_kernel L2 touch of the next input line two chunks ahead
-#endif
 #ifndef H3_BIG
 #define H3_BIG 1  // A/B knob: 448-pixel tiles with 64 co x 112 px wave tiles (0 = 256-pixel tiles, 64 x 64)
 #endif
@@ -542,10 +536,6 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
   const int nchunk = Cin / 32;
 
 #if H3_DMA
-  constexpr int H3_TPT = NJv == 7 ? 3 : 2;  // touch loads per thread: (TH + 2) x (TW + 2) <= 16 x 38 / 10 x 38 pixels
-  // the touch loads go LDS-direct into a never-read 256-B row per wave (no VGPRs held while they fly)
-  __shared__ __attribute__((aligned(16))) int tdump_s[H3_TOUCH ? 256 : 1];
-  int* tdump = tdump_s + (H3_TOUCH ? wid * 64 : 0);
   // stage one 32-channel chunk by buffer-LDS-DMA (no registers, no address VALU per element beyond one per
   // 16-B piece): 1-KiB pieces of 16 LDS rows, each lane fetching the global chunk that the row swizzle puts in
   // its slot (chunk = slot ^ ((row >> 1) & 2)); halo rows outside the tile / image read as zeros (out-of-range
@@ -579,53 +569,15 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
                                                  0, 0);
       }
     }
-    // H3_WREG (A/B knob): the weight chunk through registers (16-B global loads, then LDS stores after the wait)
-    // instead of LDS-DMA, so the per-chunk DMA volume is the halo only
-    bf16x8 wreg[H3_WREG ? H3_WPT : 1];
-    if (H3_WREG) {
 #pragma unroll
-      for (int k = 0; k < H3_WPT; ++k) {
-        const int e = tid + k * 256;
-        const int row = e >> 2, part = e & 3;  // row = tap * 64 + co
-        const int tap = row / H3_BN, co = row - tap * H3_BN;
-        wreg[k] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
-                                                 wrs, ((co * 9 + tap) * Cin + part * 8) * 2, 0, 0));
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < 9; ++k) {  // weights: 9 taps x 64 co rows = 36 pieces
-        const int q = wid + 4 * k, row = 16 * q + prow;  // row = tap * 64 + co
-        const int tap = row >> 6, co = row & 63;
-        const int chunk = pslot ^ ((row >> 1) & 2);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(sw + q * 512), 16,
-                                                 ((co * 9 + tap) * Cin + chunk * 8) * 2, 0, 0, 0);
-      }
+    for (int k = 0; k < 9; ++k) {  // weights: 9 taps x 64 co rows = 36 pieces
+      const int q = wid + 4 * k, row = 16 * q + prow;  // row = tap * 64 + co
+      const int tap = row >> 6, co = row & 63;
+      const int chunk = pslot ^ ((row >> 1) & 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(sw + q * 512), 16,
+                                               ((co * 9 + tap) * Cin + chunk * 8) * 2, 0, 0, 0);
     }
-    // H3_TOUCH: at an even chunk of x1 whose pixel rows continue past this 128-B line, one 4-B load per halo pixel of
-    // the next line (chunks ch + 2, ch + 3) brings it into L2 while this chunk and the next compute; the wait below
-    // leaves those loads in flight (the next stage's vmcnt(0) retires them)
-    if (H3_TOUCH && (ch & 1) == 0 && c0 + 64 < g.C1) {
-#pragma unroll
-      for (int k = 0; k < H3_TPT; ++k) {
-        const int hp = tid + 256 * k;
-        const int r = hp / HWd, col = hp - r * HWd;
-        const int iy = y0 - 1 + r, ix = x0 - 1 + col;
-        const bool in = r < TH + 2 && (unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)tdump, 4,
-                                                 in ? ((iy * g.Wi + ix) * cs + 64) * 2 : 0x7ffffff0, 0, 0, 0);
-      }
-      if constexpr (H3_TPT == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    if (H3_WREG) {
-#pragma unroll
-      for (int k = 0; k < H3_WPT; ++k) {
-        const int e = tid + k * 256;
-        *reinterpret_cast<bf16x8*>(sw + h3_off(e >> 2, e & 3)) = wreg[k];
-      }
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
 #else
   // stage one 32-channel chunk: global -> registers -> LDS (transient registers; the second
@@ -2955,9 +2907,6 @@ constexpr int W3_PLANE = (W3_TH + 2) * W3_P * 32;  // halo plane (bf16 elements)
 
 // (Round 3 measured a 4-wave form -- one wave per SIMD, 144 accumulators, all four co tiles per wave -- as neutral,
 // 63.69 vs 63.58 ms conv total per step: fewer LDS reads per MFMA, less latency hiding.  Removed.)
-#ifndef W36_TOUCH
-#define W36_TOUCH 0
-#endif
 #ifndef WG_TOUCH
 #define WG_TOUCH 1  // 3x3 wgrad kernels: L2 touch of the tile after next (wgrad3x3c64 415 -> 389 us per launch in the step,
                     // profiles/r4c7b_bench_ab.txt)
@@ -3504,35 +3453,6 @@ __global__ __launch_bounds__(WG_NT, 1) void wgrad3x3w36c64_kernel(const bf16* __
       hv[k] = ok ? v : bf16x8{};
     }
   };
-  // W36_TOUCH (A/B knob, +8 spilled VGPRs): as wgrad3x3c64_kernel, the tile after next's dY / halo lines into L2
-  __shared__ __attribute__((aligned(16))) int tdump[W36_TOUCH ? WG_NT : 1];
-  auto touch = [&](int tile) {
-    const int n = tile / tiles_per_img;
-    const int rem = tile - n * tiles_per_img;
-    const int ty = rem / tiles_x, tx = rem - ty * tiles_x;
-    const int y0 = ty * W36_TH, x0 = tx * W36_TW;
-    const int64_t yimg = (int64_t)g.Ho * g.Wo * ycs, ximg = (int64_t)g.Hi * g.Wi * xcs;
-    const __amdgpu_buffer_rsrc_t yrs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(ys + n * yimg + ycc), (short)0, (int)(yimg * 2 - ycc * 2), 0x00020000);
-    const __amdgpu_buffer_rsrc_t xrs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(xs + n * ximg + xcc), (short)0, (int)(ximg * 2 - xcc * 2), 0x00020000);
-    auto* dst = (__attribute__((address_space(3))) void*)(tdump + (W36_TOUCH ? wid * 64 : 0));
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {  // items 0..287: dY pixels, 288..667: halo pixels
-      const int e = tid + k * WG_NT;
-      if (e < W36_NP) {
-        const int oy = y0 + e / W36_TW, ox = x0 + e % W36_TW;
-        const bool ok = oy < g.Ho && ox < g.Wo;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(yrs, dst, 4, ok ? (oy * g.Wo + ox) * ycs * 2 : 0x7ffffff0, 0, 0, 0);
-      } else {
-        const int hp = e - W36_NP;
-        const int r = hp / W36_HW, c = hp - r * W36_HW;
-        const int iy = y0 - 1 + r, ix = x0 - 1 + c;
-        const bool ok = hp < W36_NPIX && (unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, dst, 4, ok ? (iy * g.Wi + ix) * xcs * 2 : 0x7ffffff0, 0, 0, 0);
-      }
-    }
-  };
   if ((int)blockIdx.z < ntiles) gload(blockIdx.z);
   for (int tile = blockIdx.z; tile < ntiles; tile += gridDim.z) {
     __syncthreads();
@@ -3557,7 +3477,6 @@ __global__ __launch_bounds__(WG_NT, 1) void wgrad3x3w36c64_kernel(const bf16* __
     }
     __syncthreads();
     if (tile + (int)gridDim.z < ntiles) gload(tile + gridDim.z);
-    if (W36_TOUCH && tile + 2 * (int)gridDim.z < ntiles) touch(tile + 2 * gridDim.z);
     // flat pixel of this lane's two 4-pixel groups in K-chunk kc: P = kc*32 + r0[half] -> (row, col) of the
     // 36-wide tile (32 < 36: at most one wrap per chunk)
     int prow[2], pcol[2];
