@@ -183,17 +183,19 @@ class KernelProbe:
             return (f"twh_bwd_kernel<{nv}> (+ dW / dgamma / dbias reductions)",
                     v * (tw_core_flop(C, F) + 2.0 * 768 * C), float(v * (3 * C * 2 + 40)))
 
-        def tattn_fwd(qkv, bias, rot, B, F, HW, scale, save=True):
+        def tattn_fwd(qkv, bias, rot, B, F, HW, scale, save=True, pixel_major=False):
             v = B * F * HW
             lab = (f"tflash_fwd_kernel<{(F + 15) // 16}>" if K._tflash(qkv, F) else "tattn_fwd_kernel")
             # q.k and attn.v over the F frames of each pixel and head; bytes: qkv read, out (+ lse) written
             return lab, 4.0 * F * 32 * 8 * v, float(v * (768 * 2 + 256 * 2 + (32 if save else 0)))
 
-        def tattn_bwd(qkv, o, dout, lse, bias, rot, dtable, B, F, HW, scale, num_buckets=32, max_distance=32):
+        def tattn_bwd(qkv, o, dout, lse, bias, rot, dtable, B, F, HW, scale, num_buckets=32, max_distance=32,
+                      pixel_major=False):
             v = B * F * HW
             nt = (F + 15) // 16
             # the dq kernel by dispatch (per-wave from 32768 pixels, block-per-pixel below: cesm_tflash_bwd_variant)
-            lab = (f"{K.tflash_bwd_variant(F, HW).replace(',false>', '>').replace(',true>', '>')} + "
+            dq = f"tflash_bwd_qw_kernel<{nt}>" if pixel_major else K.tflash_bwd_variant(F, HW)
+            lab = (f"{dq.replace(',false>', '>').replace(',true>', '>')} + "
                    f"tflash_bwd_kv_kernel<{nt}>" if K._tflash(qkv, F) else "tattn_bwd_kernel")
             # dP, dQ, dK, dV products (2x the forward); bytes: qkv, o, dout, lse read, dqkv written
             return lab, 8.0 * F * 32 * 8 * v, float(v * (768 * 2 * 2 + 256 * 2 * 2 + 32))
@@ -228,10 +230,10 @@ class KernelProbe:
             # reduce pass reads dout, y; apply pass reads dout, y and writes dy
             return "gn_bwd_reduce_kernel + gn_bwd_apply_kernel", 0.0, float(y.numel() * es_of(y) * 5)
 
-        def ln_fwd(x, gamma, save=True, eps=1e-5):
+        def ln_fwd(x, gamma, save=True, eps=1e-5, perm=None):
             return "ln_fwd_kernel", 0.0, float(x.numel() * es_of(x) * 2)
 
-        def ln_bwd(dy, x, mr, gamma, dgamma, dres=None):
+        def ln_bwd(dy, x, mr, gamma, dgamma, dres=None, perm=None):
             return "ln_bwd_kernel", 0.0, float(x.numel() * es_of(x) * (4 if dres is not None else 3))
 
         def adamw(p, g, m, v, info, lr, b1, b2, eps, wd, step_dev, use_clip):

@@ -11,11 +11,19 @@
 namespace {
 
 // ---------------------------------------------------------------- LayerNorm
+// pixel-major row of voxel v = (b*F + f)*HW + p: (b*HW + p)*F + f (pf = 0: identity)
+__device__ __forceinline__ int64_t ln_perm(int64_t v, int pf, int phw) {
+  if (!pf) return v;
+  const int64_t fhw = (int64_t)pf * phw;
+  const int64_t b = v / fhw, r = v - b * fhw;
+  const int f = (int)(r / phw), p = (int)(r - (int64_t)f * phw);
+  return (b * phw + p) * pf + f;
+}
 // lanes per voxel L = C/8 (8..64, power of two); each lane 8 channels
 template <typename T>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, const float* __restrict__ gamma,
                                                      T* __restrict__ out, float* __restrict__ mr, int64_t V, int C,
-                                                     float eps) {
+                                                     float eps, int pf, int phw) {
   const int L = C / 8;
   const int64_t gt = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t v = gt / L;
@@ -37,7 +45,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
   if (!ok) return;
 #pragma unroll
   for (int i = 0; i < 8; ++i) a[i] = (a[i] - mean) * rstd * gamma[sub * 8 + i];
-  store8(out + v * C + sub * 8, a);
+  store8(out + ln_perm(v, pf, phw) * C + sub * 8, a);
   if (sub == 0 && mr) { mr[v * 2] = mean; mr[v * 2 + 1] = rstd; }
 }
 
@@ -46,7 +54,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                      const float* __restrict__ mr, const float* __restrict__ gamma,
                                                      const T* __restrict__ dres, T* __restrict__ dx,
-                                                     float* __restrict__ part, int64_t V, int C) {
+                                                     float* __restrict__ part, int64_t V, int C, int pf, int phw) {
   const int L = C / 8;
   const int vpb = 256 / L;  // voxels per block-iteration
   const int sub = threadIdx.x % L, vl = threadIdx.x / L;
@@ -61,7 +69,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
     float mean = 0.f, rstd = 0.f;
     if (ok) {
       load8(x + v * C + sub * 8, a);
-      load8(dy + v * C + sub * 8, d);
+      load8(dy + ln_perm(v, pf, phw) * C + sub * 8, d);
       mean = mr[v * 2];
       rstd = mr[v * 2 + 1];
     } else {
@@ -125,27 +133,32 @@ static int dispatch_dt(int dtype, F&& f) {
 
 extern "C" {
 
-// x,out: [V][C]; mr: [V][2] (mean, rstd) saved for backward (may be null)
+// x,out: [V][C]; mr: [V][2] (mean, rstd) saved for backward (may be null).  perm_f > 0: V = B * perm_f * perm_hw
+// voxels in [B][F][HW] order, out rows written pixel-major ([B][HW][F]); mr in x's order
 int cesm_ln_fwd(int dtype, const void* x, const float* gamma, void* out, float* mr, int64_t V, int C, float eps,
-                hipStream_t stream) {
+                int perm_f, int perm_hw, hipStream_t stream) {
   if (C % 8 || C / 8 > 64 || ((C / 8) & (C / 8 - 1))) return CESM_EINVAL;
+  if (perm_f < 0 || (perm_f && (perm_hw < 1 || V % ((int64_t)perm_f * perm_hw)))) return CESM_EINVAL;
   const int64_t threads = V * (C / 8);
   const unsigned grid = (unsigned)cdiv(threads, 256);
   int rc = dispatch_dt(dtype, [&](auto* tp) {
     using T = std::remove_pointer_t<decltype(tp)>;
-    ln_fwd_kernel<T><<<grid, 256, 0, stream>>>((const T*)x, gamma, (T*)out, mr, V, C, eps);
+    ln_fwd_kernel<T><<<grid, 256, 0, stream>>>((const T*)x, gamma, (T*)out, mr, V, C, eps, perm_f, perm_hw);
   });
   if (rc) return rc;
   return cesm_launch_status();
 }
 
-// part: nblk*C floats
+// part: nblk*C floats; perm_f > 0: dy rows pixel-major (as cesm_ln_fwd's permuted out), x / dres / dx not
 int cesm_ln_bwd(int dtype, const void* dy, const void* x, const float* mr, const float* gamma, const void* dres,
-                void* dx, float* dgamma, float* part, int nblk, int64_t V, int C, int accumulate, hipStream_t stream) {
+                void* dx, float* dgamma, float* part, int nblk, int64_t V, int C, int accumulate, int perm_f, int perm_hw,
+                hipStream_t stream) {
   if (C % 8 || C / 8 > 64 || ((C / 8) & (C / 8 - 1)) || nblk <= 0) return CESM_EINVAL;
+  if (perm_f < 0 || (perm_f && (perm_hw < 1 || V % ((int64_t)perm_f * perm_hw)))) return CESM_EINVAL;
   int rc = dispatch_dt(dtype, [&](auto* tp) {
     using T = std::remove_pointer_t<decltype(tp)>;
-    ln_bwd_kernel<T><<<nblk, 256, 0, stream>>>((const T*)dy, (const T*)x, mr, gamma, (const T*)dres, (T*)dx, part, V, C);
+    ln_bwd_kernel<T><<<nblk, 256, 0, stream>>>((const T*)dy, (const T*)x, mr, gamma, (const T*)dres, (T*)dx, part, V, C,
+                                               perm_f, perm_hw);
   });
   if (rc) return rc;
   if (dgamma) sum_rows_kernel<<<C, 64, 0, stream>>>(part, dgamma, nblk, C, accumulate);

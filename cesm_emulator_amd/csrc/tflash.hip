@@ -229,7 +229,7 @@ constexpr float TF_LSE_PAD = 1e30f;
 template <int NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE))) void tflash_fwd_kernel(const bf16* __restrict__ qkv, const float* __restrict__ bias,
                                                          const float* __restrict__ rot, bf16* __restrict__ out,
-                                                         float* __restrict__ lse, int F, int HW, float scale) {
+                                                         float* __restrict__ lse, int F, int HW, float scale, int pm) {
   constexpr int NP = (NT + 1) / 2, NR = 32 * NP;  // key-tile pairs, staged rows
   // V rows are staged TF_VH key-tile pairs at a time: the V^T fragments live in registers afterwards, so the
   // wave's staging slice only has to hold part of them -- less LDS per block, one more block per CU
@@ -247,9 +247,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE)
   if (p >= HW) return;
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
   const int64_t row0 = (int64_t)b * F * HW + p;  // voxel of frame f: row0 + f * HW
+  // qkv rows: frame-major [B][F][HW] (pm = 0) or pixel-major [B][HW][F] (pm = 1: a pixel's frames contiguous)
+  const int64_t qrow0 = pm ? ((int64_t)b * HW + p) * F : row0;
+  const int qfs = pm ? 1 : HW;
   bf16* vs = vst[wid];
   // TF_BUF lane offsets: frame lr of a 16-frame tile
-  const int q_off = (lr * HW * QKV + g * 8) * 2, o_off = (lr * HW * INNER + 4 * g) * 2;
+  const int q_off = (lr * qfs * QKV + g * 8) * 2, o_off = (lr * HW * INNER + 4 * g) * 2;
   const __amdgpu_buffer_rsrc_t rot_rs = tile_rsrc(rot, F, 16 * 2 * 4, 16 * 2 * 4, TF_MAXT * 16);
   const int rot_off = (lr * 16 + 4 * g) * 2 * 4;
   // every K' fragment up front (all Q' fragments up front as well measured 1.7x slower at F = 120; the next query
@@ -259,7 +262,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE)
   for (int kt = 0; kt < NT; ++kt) {
     const int f = kt * 16 + lr;
     const bool ok = f < F;
-    const int64_t rr = (row0 + (int64_t)(ok ? f : 0) * HW) * QKV + h * DH + g * 8;
+    const int64_t rr = (qrow0 + (int64_t)(ok ? f : 0) * qfs) * QKV + h * DH + g * 8;
     kf[kt] = row_frag(qkv + rr + INNER, rot, ok ? f : 0, g, 1.f, true);
   }
   bf16x8 vf[NP][2];
@@ -268,7 +271,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE)
     if (s0) wsync();  // previous part's transposed reads done
     for (int e = lane; e < NVR * 4; e += 64) {  // V rows 32 s0 .. (zero past F)
       const int fl = e >> 2, c = e & 3, f = 32 * s0 + fl;
-      const bf16x8 v = ld16(qkv + (row0 + (int64_t)(f < F ? f : 0) * HW) * QKV + 2 * INNER + h * DH + c * 8);
+      const bf16x8 v = ld16(qkv + (qrow0 + (int64_t)(f < F ? f : 0) * qfs) * QKV + 2 * INNER + h * DH + c * 8);
       *reinterpret_cast<bf16x8*>(vs + fl * TF_LD + c * 8) = f < F ? v : zero8();
     }
     wsync();
@@ -293,12 +296,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE)
     bf16x8 qf;
     if (TF_BUF) {
       const __amdgpu_buffer_rsrc_t qrs =
-          tile_rsrc(qkv + (row0 + (int64_t)qt * 16 * HW) * QKV + h * DH, nq, (int64_t)HW * QKV * 2, DH * 2);
+          tile_rsrc(qkv + (qrow0 + (int64_t)qt * 16 * qfs) * QKV + h * DH, nq, (int64_t)qfs * QKV * 2, DH * 2);
       float cs[8];
       buf_rot8(rot_rs, rot_off + qt * 16 * 16 * 2 * 4, cs);
       qf = rope8(buf_ld16(qrs, q_off), cs, scale);  // frames >= F: zeros
     } else {
-      qf = row_frag(qkv + (row0 + (int64_t)(okq ? fq : 0) * HW) * QKV + h * DH + g * 8, rot, okq ? fq : 0, g, scale,
+      qf = row_frag(qkv + (qrow0 + (int64_t)(okq ? fq : 0) * qfs) * QKV + h * DH + g * 8, rot, okq ? fq : 0, g, scale,
                     true);
     }
     const float* bq = bl - 16 * qt;
@@ -635,7 +638,7 @@ template <int NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tflash_bwd_qw_kernel(
     const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
     const float* __restrict__ lse, const float* __restrict__ bias, const float* __restrict__ rot,
-    bf16* __restrict__ dqkv, float* __restrict__ dbuf, float* __restrict__ part, int F, int HW, float scale) {
+    bf16* __restrict__ dqkv, float* __restrict__ dbuf, float* __restrict__ part, int F, int HW, float scale, int pm) {
   constexpr int NP = (NT + 1) / 2, NR = 32 * NP, NC = 2 * NT - 1;
   constexpr int CH = (NR * TF_LD * 2) / (4 * 64 * 4);  // diagonals staged per chunk in the wave's row buffer
   static_assert(CH >= 1, "stage chunk");
@@ -660,7 +663,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
     for (int c = 0; c < NC; ++c) dba[r][c] = 0.f;
   // tile addressing as the forward's TF_BUF: wave-uniform tile base + one 32-bit lane offset for every tile, the
   // resource ends at the tile's last valid frame (loads past F return 0, stores are dropped)
-  const int fs_qkv = HW * QKV * 2, fs_io = HW * INNER * 2;  // < 2^31 / 16: checked on the host
+  // qkv / dqkv rows frame-major or pixel-major (pm, as the forward); dout / o frame-major
+  const int fs_qkv = (pm ? 1 : HW) * QKV * 2, fs_io = HW * INNER * 2;  // < 2^31 / 16: checked on the host
 
   for (int p = blockIdx.x * 4 + wid; p < HW; p += 4 * (int)gridDim.x) {
     int ln = lane;
@@ -668,12 +672,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
     const int lr = ln & 15, g = ln >> 4;
     const int lo_qkv = lr * fs_qkv + h * DH * 2 + g * 16, lo_io = lr * fs_io + h * DH * 2 + g * 16;
     const int64_t row0 = (int64_t)b * F * HW + p;
+    const int64_t qrow0 = pm ? ((int64_t)b * HW + p) * F : row0;
+    const int qfs = pm ? 1 : HW;
     const float* lsep = lse + (((int64_t)b * NH + h) * HW + p) * F;
     float* dbp = dbuf + (((int64_t)b * NH + h) * HW + p) * F;
     bf16x8 vf[NT], kf[TFQW_KREG ? NT : 1], ktf[TFQW_KTF ? NP : 1][2];
 #pragma unroll
     for (int kt = 0; kt < NT; ++kt) {
-      const auto rs = tile_rsrc(qkv + (row0 + (int64_t)kt * 16 * HW) * QKV, F - kt * 16, (int64_t)fs_qkv, QKV * 2);
+      const auto rs = tile_rsrc(qkv + (qrow0 + (int64_t)kt * 16 * qfs) * QKV, F - kt * 16, (int64_t)fs_qkv, QKV * 2);
       const bf16x8 kr = buf_ld16(rs, lo_qkv + INNER * 2);
       vf[kt] = buf_ld16(rs, lo_qkv + 2 * INNER * 2);
       const int f = kt * 16 + lr;
@@ -697,7 +703,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
       const int fq = qt * 16 + lr;
       const bool okq = fq < F;
       const int fqc = okq ? fq : 0;
-      const auto rq = tile_rsrc(qkv + (row0 + (int64_t)qt * 16 * HW) * QKV, F - qt * 16, (int64_t)fs_qkv, QKV * 2);
+      const auto rq = tile_rsrc(qkv + (qrow0 + (int64_t)qt * 16 * qfs) * QKV, F - qt * 16, (int64_t)fs_qkv, QKV * 2);
       const auto rd = tile_rsrc(dout + (row0 + (int64_t)qt * 16 * HW) * INNER, F - qt * 16, (int64_t)fs_io, INNER * 2);
       const auto ro = tile_rsrc(o + (row0 + (int64_t)qt * 16 * HW) * INNER, F - qt * 16, (int64_t)fs_io, INNER * 2);
       const bf16x8 qr = buf_ld16(rq, lo_qkv);
@@ -751,7 +757,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
       for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int c = 0; c < NC; ++c) asm volatile("" : "+v"(dba[r][c]));
-      const auto rw = tile_rsrc(dqkv + (row0 + (int64_t)qt * 16 * HW) * QKV, F - qt * 16, (int64_t)fs_qkv, QKV * 2);
+      const auto rw = tile_rsrc(dqkv + (qrow0 + (int64_t)qt * 16 * qfs) * QKV, F - qt * 16, (int64_t)fs_qkv, QKV * 2);
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const int d0 = t * 16 + 4 * g;
@@ -804,7 +810,7 @@ template <int NT>
 __global__ __launch_bounds__(256, 2) void tflash_bwd_kv_kernel(
     const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ dbuf, const float* __restrict__ bias, const float* __restrict__ rot,
-    bf16* __restrict__ dqkv, int F, int HW, float scale) {
+    bf16* __restrict__ dqkv, int F, int HW, float scale, int pm) {
   constexpr int NP = (NT + 1) / 2, NR = 32 * NP;
   __shared__ __attribute__((aligned(16))) float btab[4 * 32 * NT];
   __shared__ __attribute__((aligned(16))) bf16 stg[4][NR * TF_LD];
@@ -820,6 +826,8 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_kv_kernel(
   if (p >= HW) return;
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
   const int64_t row0 = (int64_t)b * F * HW + p;
+  const int64_t qrow0 = pm ? ((int64_t)b * HW + p) * F : row0;  // qkv / dqkv rows (pm: pixel-major)
+  const int qfs = pm ? 1 : HW;
   bf16* st = stg[wid];
   float* Ls = lds_l[wid];
   float* Ds = lds_d[wid];
@@ -840,7 +848,8 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_kv_kernel(
     const int f = qt * 16 + lr;
     const bool ok = f < F;
     const int64_t vq = row0 + (int64_t)(ok ? f : 0) * HW;
-    qa[qt] = row_frag(qkv + vq * QKV + h * DH + g * 8, rot, ok ? f : 0, g, scale, true);  // padded: P = dS = 0
+    qa[qt] = row_frag(qkv + (qrow0 + (int64_t)(ok ? f : 0) * qfs) * QKV + h * DH + g * 8, rot, ok ? f : 0, g, scale,
+                      true);  // padded: P = dS = 0
     da[qt] = row_frag(dout + vq * INNER + h * DH + g * 8, nullptr, 0, g, 1.f, true);
     *reinterpret_cast<bf16x8*>(st + f * TF_LD + g * 8) = qa[qt];
   }
@@ -864,7 +873,7 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_kv_kernel(
   float kcs[8];
   auto fetch = [&](int t) {
     const int fk = t * 16 + lr, fkc = fk < F ? fk : 0;
-    const int64_t rk = (row0 + (int64_t)fkc * HW) * QKV + h * DH + g * 8;
+    const int64_t rk = (qrow0 + (int64_t)fkc * qfs) * QKV + h * DH + g * 8;
     kraw = ld16(qkv + rk + INNER);
     vraw = ld16(qkv + rk + 2 * INNER);
     rot8_load(rot, fkc, g, kcs);
@@ -917,7 +926,7 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_kv_kernel(
         float k4[4] = {dk[t][0], dk[t][1], dk[t][2], dk[t][3]};
         float v4[4] = {dv[t][0], dv[t][1], dv[t][2], dv[t][3]};
         rope4_inv(k4, rot, fk, d0, 1.f);  // dk = R^T dK'
-        bf16* dst = dqkv + (row0 + (int64_t)fk * HW) * QKV + h * DH + d0;
+        bf16* dst = dqkv + (qrow0 + (int64_t)fk * qfs) * QKV + h * DH + d0;
         store4b(dst + INNER, k4);
         store4b(dst + 2 * INNER, v4);
       }
@@ -973,7 +982,9 @@ __global__ void tf_dtable_kernel(const float* __restrict__ off, float* __restric
 // collapses there), 96x144 3.61 -> 3.72, 48x72 1.00 -> 1.10, 24x36 0.37 -> 0.41 (profiles/r4c5_qw_check.txt).
 // CESM_TF_QW=1 forces it for every F > 16, CESM_TF_NO_QW=1 disables it.
 enum TfDq { TF_DQ_BLOCK, TF_DQ_DOV, TF_DQ_WAVE };
-static TfDq tf_dq_kind(int nt, int HW) {
+// Pixel-major qkv (pm) always takes the per-wave kernel: the block-per-pixel kernels read frame-major rows only.
+static TfDq tf_dq_kind(int nt, int HW, int pm = 0) {
+  if (nt >= 2 && pm) return TF_DQ_WAVE;
   if (nt >= 2 && (int64_t)16 * HW * QKV * 2 < (1ll << 31) && !getenv_flag("CESM_TF_NO_QW") &&
       (HW >= TF_QW_MINHW || getenv_flag("CESM_TF_QW")))
     return TF_DQ_WAVE;
@@ -982,7 +993,8 @@ static TfDq tf_dq_kind(int nt, int HW) {
 
 extern "C" {
 
-// name of the dq kernel cesm_tflash_bwd runs for (F, HW) (host-only query; "invalid" when F is unsupported)
+// name of the dq kernel cesm_tflash_bwd runs for (F, HW) with frame-major qkv (host-only query; "invalid" when F
+// is unsupported)
 const char* cesm_tflash_bwd_variant(int F, int HW) {
   static const char* names[3][9] = {
       {"", "tflash_bwd_q_kernel<1,false>", "tflash_bwd_q_kernel<2,false>", "tflash_bwd_q_kernel<3,false>",
@@ -1005,14 +1017,18 @@ int cesm_tflash_supported(int F) { return F >= 1 && F <= 16 * TF_MAXT; }
 int cesm_tflash_nblk(int HW) { return std::max(1, std::min(HW, 128)); }
 
 // forward: qkv [B*F*HW][768] bf16 -> out [B*F*HW][256] bf16, lse [B][8][HW][F] (log2 units, nullable);
-// bias [8][F][F] (expanded rel-pos bias), rot [F][16][2]
+// bias [8][F][F] (expanded rel-pos bias), rot [F][16][2].  qkv_pixel_major (F > 16 only): qkv rows ordered
+// [B][HW][F] (a pixel's frames adjacent) instead of [B][F][HW]; out stays [B][F][HW].
 int cesm_tflash_fwd(const void* qkv, const float* bias, const float* rot, void* out, float* lse, int B, int F, int HW,
-                    float scale, hipStream_t stream) {
+                    float scale, int qkv_pixel_major, hipStream_t stream) {
   if (!cesm_tflash_supported(F) || B < 1 || HW < 1) return CESM_EUNSUPPORTED;
-  if ((int64_t)16 * HW * QKV * 2 >= (1ll << 31)) return CESM_EUNSUPPORTED;  // TF_BUF 32-bit lane offsets
-  dim3 grid(tf_grid_x(HW), B);
   const int nt = (F + 15) / 16;
-#define TFF(N) tflash_fwd_kernel<N><<<grid, 256, 0, stream>>>((const bf16*)qkv, bias, rot, (bf16*)out, lse, F, HW, scale)
+  const int pm = qkv_pixel_major ? 1 : 0;
+  if (pm && nt < 2) return CESM_EUNSUPPORTED;
+  if ((int64_t)16 * HW * (pm ? INNER : QKV) * 2 >= (1ll << 31)) return CESM_EUNSUPPORTED;  // TF_BUF 32-bit lane offsets
+  dim3 grid(tf_grid_x(HW), B);
+#define TFF(N) \
+  tflash_fwd_kernel<N><<<grid, 256, 0, stream>>>((const bf16*)qkv, bias, rot, (bf16*)out, lse, F, HW, scale, pm)
   switch (nt) {
     case 1: TFF(1); break;
     case 2: TFF(2); break;
@@ -1028,23 +1044,27 @@ int cesm_tflash_fwd(const void* qkv, const float* bias, const float* rot, void* 
   return cesm_launch_status();
 }
 
-// backward: dqkv [B*F*HW][768] (every channel written), from qkv, the forward's o and lse, and dout [..][256];
+// backward: dqkv [B*F*HW][768] (every channel written; in qkv's row order), from qkv, the forward's o and lse, and
+// dout [..][256] (frame-major);
 // dtable (+)= the rel-pos table gradient (nullable).  Workspaces: dbuf B*8*HW*F floats, part
 // B*8*nblk*(2F-1) floats (nblk = cesm_tflash_nblk(HW)), off 8*(2F-1) floats.
 int cesm_tflash_bwd(const void* qkv, const void* o, const void* dout, const float* lse, const float* bias,
                     const float* rot, void* dqkv, float* dtable, float* dbuf, float* part, float* off, int B, int F,
-                    int HW, float scale, int num_buckets, int max_distance, int accumulate, hipStream_t stream) {
+                    int HW, float scale, int num_buckets, int max_distance, int accumulate, int qkv_pixel_major,
+                    hipStream_t stream) {
   if (!cesm_tflash_supported(F) || B < 1 || HW < 1) return CESM_EUNSUPPORTED;
   const int nt = (F + 15) / 16;
+  const int pm = qkv_pixel_major ? 1 : 0;
+  if (pm && (nt < 2 || (int64_t)16 * HW * INNER * 2 >= (1ll << 31))) return CESM_EUNSUPPORTED;
   const int nblk = cesm_tflash_nblk(HW);
   dim3 gq(nblk, B * NH), gk(tf_grid_x(HW), B);
-  const TfDq kind = tf_dq_kind(nt, HW);
+  const TfDq kind = tf_dq_kind(nt, HW, pm);
   const bool qw = kind == TF_DQ_WAVE, dov = kind == TF_DQ_DOV;
 #define TFB(N)                                                                                                         \
   if (qw && N >= 2)                                                                                                    \
     tflash_bwd_qw_kernel<(N >= 2 ? N : 2)><<<gq, 256, 0, stream>>>((const bf16*)qkv, (const bf16*)o,                   \
                                                                    (const bf16*)dout, lse, bias, rot, (bf16*)dqkv,    \
-                                                                   dbuf, part, F, HW, scale);                         \
+                                                                   dbuf, part, F, HW, scale, pm);                     \
   else if (dov && N >= 2)                                                                                              \
     tflash_bwd_q_kernel<N, (N >= 2)><<<gq, 64 * N, 0, stream>>>((const bf16*)qkv, (const bf16*)o, (const bf16*)dout,   \
                                                                 lse, bias, rot, (bf16*)dqkv, dbuf, part, F, HW, scale); \
@@ -1052,7 +1072,7 @@ int cesm_tflash_bwd(const void* qkv, const void* o, const void* dout, const floa
     tflash_bwd_q_kernel<N, false><<<gq, 64 * N, 0, stream>>>((const bf16*)qkv, (const bf16*)o, (const bf16*)dout, lse, \
                                                              bias, rot, (bf16*)dqkv, dbuf, part, F, HW, scale);       \
   tflash_bwd_kv_kernel<N><<<gk, 256, 0, stream>>>((const bf16*)qkv, (const bf16*)dout, lse, dbuf, bias, rot,           \
-                                                  (bf16*)dqkv, F, HW, scale)
+                                                  (bf16*)dqkv, F, HW, scale, pm)
   switch (nt) {
     case 1: TFB(1); break;
     case 2: TFB(2); break;

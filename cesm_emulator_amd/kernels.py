@@ -281,24 +281,29 @@ def gn_bwd(dout, y, stats, gamma, beta, ss, dgamma, dbeta, B, G, want_dss, dbias
     return dy, dss
 
 
-def ln_fwd(x, gamma, save=True, eps=1e-5):
+def ln_fwd(x, gamma, save=True, eps=1e-5, perm=None):
+    """perm = (F, HW): write the output rows of voxel (b, f, p) at (b, p, f) -- pixel-major, a pixel's frames
+    adjacent (mr stays in x's order)"""
     C = x.shape[-1]
     V = x.numel() // C
     out = empty(x.shape, x.dtype, x.device)
     mr = empty((V, 2), torch.float32, x.device) if save else None
-    call("cesm_ln_fwd", dtcode(x), P(x), P(gamma), P(out), P(mr), V, C, float(eps), S())
+    pf, phw = perm if perm else (0, 0)
+    call("cesm_ln_fwd", dtcode(x), P(x), P(gamma), P(out), P(mr), V, C, float(eps), pf, phw, S())
     return out, mr
 
 
-def ln_bwd(dy, x, mr, gamma, dgamma, dres=None):
+def ln_bwd(dy, x, mr, gamma, dgamma, dres=None, perm=None):
+    """perm = (F, HW): dy rows are pixel-major (as ln_fwd(perm=...) wrote the output); x, dres, dx in x's order"""
     C = x.shape[-1]
     V = x.numel() // C
     dx = empty(x.shape, x.dtype, x.device)
     nblk = 1024
     part = empty((nblk, C), torch.float32, x.device)
     _chk(dres, x.shape, x.dtype)
+    pf, phw = perm if perm else (0, 0)
     call("cesm_ln_bwd", dtcode(x), P(dy), P(x), P(mr), P(gamma), P(dres), P(dx), P(dgamma), P(part), nblk, V, C, 1,
-         S())
+         pf, phw, S())
     return dx
 
 
@@ -331,19 +336,24 @@ def _tflash(qkv, F):
     return TFLASH and qkv.dtype == torch.bfloat16 and lib().cesm_tflash_supported(F) == 1
 
 
-def tattn_fwd(qkv, bias, rot, B, F, HW, scale, save=True):
+def tattn_fwd(qkv, bias, rot, B, F, HW, scale, save=True, pixel_major=False):
+    """pixel_major (MFMA core, F > 16): qkv rows ordered [B][HW][F]; out stays [B][F][HW]"""
     V = qkv.shape[0]
     _chk(qkv, (B * F * HW, 768))
     out = empty((V, 256), qkv.dtype, qkv.device)
     lse = empty((B, 8, HW, F), torch.float32, qkv.device) if save else None
     if _tflash(qkv, F):
-        call("cesm_tflash_fwd", P(qkv), P(bias), P(rot), P(out), P(lse), B, F, HW, float(scale), S())
+        call("cesm_tflash_fwd", P(qkv), P(bias), P(rot), P(out), P(lse), B, F, HW, float(scale), int(pixel_major), S())
         return out, lse
+    if pixel_major:
+        raise ValueError("pixel-major qkv needs the MFMA temporal core (bf16, F <= 128)")
     call("cesm_tattn_fwd", dtcode(qkv), P(qkv), P(bias), P(rot), P(out), P(lse), B, F, HW, float(scale), S())
     return out, lse
 
 
-def tattn_bwd(qkv, o, dout, lse, bias, rot, dtable, B, F, HW, scale, num_buckets=32, max_distance=32):
+def tattn_bwd(qkv, o, dout, lse, bias, rot, dtable, B, F, HW, scale, num_buckets=32, max_distance=32,
+              pixel_major=False):
+    """pixel_major: qkv and the returned dqkv in [B][HW][F] row order (o, dout frame-major)"""
     dqkv = empty(qkv.shape, qkv.dtype, qkv.device)
     if _tflash(qkv, F):
         _chk(o, (qkv.shape[0], 256), qkv.dtype)
@@ -354,8 +364,10 @@ def tattn_bwd(qkv, o, dout, lse, bias, rot, dtable, B, F, HW, scale, num_buckets
         part = empty((B * 8 * nblk * (2 * F - 1),), torch.float32, dev)
         off = empty((8 * (2 * F - 1),), torch.float32, dev)
         call("cesm_tflash_bwd", P(qkv), P(o), P(dout), P(lse), P(bias), P(rot), P(dqkv), P(dtable), P(dbuf), P(part),
-             P(off), B, F, HW, float(scale), num_buckets, max_distance, 1, S())
+             P(off), B, F, HW, float(scale), num_buckets, max_distance, 1, int(pixel_major), S())
         return dqkv
+    if pixel_major:
+        raise ValueError("pixel-major qkv needs the MFMA temporal core (bf16, F <= 128)")
     nblk = lib().cesm_tattn_nblk(F, HW)
     part = empty((B * 8 * nblk, F, F), torch.float32, qkv.device)
     call("cesm_tattn_bwd", dtcode(qkv), P(qkv), P(o), P(dout), P(lse), P(bias), P(rot), P(dqkv), P(part), B, F, HW,

@@ -403,6 +403,14 @@ def _tblock_dw(rc, x):
     return TBLOCK_DW and _tblock_fused(rc, C) and K.tblock_bwd_dw_supported(rc.B, rc.F, H * W, C)
 
 
+# pixel-major qkv for the long-window attention core (CESM_TF_PM=0: frame-major)
+TF_PM = os.environ.get("CESM_TF_PM", "1") != "0"
+
+
+def _tf_pixel_major(rc, x):
+    return TF_PM and rc.F > 16 and x.dtype == torch.bfloat16 and K.lib().cesm_tflash_supported(rc.F) == 1 and K.TFLASH
+
+
 def tattn_fwd(rc, res_mod, x):
     """Residual(PreNorm(EinopsToAndFrom(Attention))) over frames (video_net.py:368-454).
     bf16: one fused kernel (csrc/tblock.hip); fp32 parity mode: LN -> to_qkv -> core -> to_out."""
@@ -436,12 +444,17 @@ def tattn_fwd(rc, res_mod, x):
                                      save=rc.save, eps=pre.norm.eps, save_o=save_o)
         st = SimpleNamespace(fused=True, fold=False, x=x, mr=mr, lse=lse, o=o) if rc.save else None
         return y, st
-    n, mr = K.ln_fwd(x, _flat(pre.norm.gamma), save=rc.save, eps=pre.norm.eps)
+    # long windows (MFMA core, F > 16): the LN output -- and with it the to_qkv GEMM's qkv rows and, in the backward,
+    # dqkv and dn -- in pixel-major order, so the attention kernels read a pixel's frames as adjacent rows
+    pm = _tf_pixel_major(rc, x)
+    perm = (rc.F, HW) if pm else None
+    n, mr = K.ln_fwd(x, _flat(pre.norm.gamma), save=rc.save, eps=pre.norm.eps, perm=perm)
     qspec, ospec = ConvSpec(attn.to_qkv), ConvSpec(attn.to_out)
     qkv, qst = conv_forward(rc, qspec, n)
-    o, lse = K.tattn_fwd(qkv.view(-1, 768), rc.bias, rc.rot, rc.B, rc.F, HW, attn.scale, save=rc.save)
+    o, lse = K.tattn_fwd(qkv.view(-1, 768), rc.bias, rc.rot, rc.B, rc.F, HW, attn.scale, save=rc.save,
+                         pixel_major=pm)
     y, ost = conv_forward(rc, ospec, o.view(Nb, H, W, 256), None, res=x)
-    st = SimpleNamespace(fused=False, x=x, mr=mr, qkv=qkv, o=o, lse=lse, qst=qst, ost=ost) if rc.save else None
+    st = SimpleNamespace(fused=False, x=x, mr=mr, qkv=qkv, o=o, lse=lse, qst=qst, ost=ost, perm=perm) if rc.save else None
     return y, st
 
 
@@ -477,9 +490,9 @@ def tattn_bwd(rc, res_mod, st, dy):
         return dx
     do = conv_backward(rc, ConvSpec(attn.to_out), st.ost, dy)
     dqkv = K.tattn_bwd(st.qkv.view(-1, 768), st.o, do.view(-1, 256), st.lse, rc.bias, rc.rot, rc.dtable, rc.B,
-                       rc.F, H * W, attn.scale)
+                       rc.F, H * W, attn.scale, pixel_major=st.perm is not None)
     dn = conv_backward(rc, ConvSpec(attn.to_qkv), st.qst, dqkv.view(Nb, H, W, 768))
-    return K.ln_bwd(dn, st.x, st.mr, _flat(pre.norm.gamma), gbuf(pre.norm.gamma), dres=dy)
+    return K.ln_bwd(dn, st.x, st.mr, _flat(pre.norm.gamma), gbuf(pre.norm.gamma), dres=dy, perm=st.perm)
 
 
 FUSED_SLA = os.environ.get("CESM_NO_FUSED_SLA", "0") != "1"

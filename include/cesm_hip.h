@@ -102,12 +102,15 @@ int cesm_gn_apply(int dtype, const void* y, const float* stats, const float* gam
 int cesm_gn_bwd(int dtype, const void* dout, const void* y, const float* stats, const float* gamma,
                 const float* beta, const float* ss, void* dy, float* dss, float* dgamma, float* dbeta, float* dbias,
                 float* ws, int B, int64_t rows_b, int C, int G, int accumulate, hipStream_t stream);
-/* channel LayerNorm (biased var, gamma only): video_net.py:78-87 */
+/* channel LayerNorm (biased var, gamma only): video_net.py:78-87.  perm_f > 0: x is [B][perm_f][perm_hw] voxels and
+ * out is written pixel-major ([B][perm_hw][perm_f], the long-window qkv order); 0: same order as x */
 int cesm_ln_fwd(int dtype, const void* x, const float* gamma, void* out, float* mr, int64_t V, int C, float eps,
-                hipStream_t stream);
-/* dx = LN backward + dres (the Residual wrapper's pass-through gradient, video_net.py:75) */
+                int perm_f, int perm_hw, hipStream_t stream);
+/* dx = LN backward + dres (the Residual wrapper's pass-through gradient, video_net.py:75); perm_f > 0: dy is
+ * pixel-major (as cesm_ln_fwd's permuted out) */
 int cesm_ln_bwd(int dtype, const void* dy, const void* x, const float* mr, const float* gamma, const void* dres,
-                void* dx, float* dgamma, float* part, int nblk, int64_t V, int C, int accumulate, hipStream_t stream);
+                void* dx, float* dgamma, float* part, int nblk, int64_t V, int C, int accumulate, int perm_f, int perm_hw,
+                hipStream_t stream);
 
 /* ---- attention (csrc/attn.hip) -----------------------------------------------------------
  * RoPE angle table (rotary_embedding.py:143-144, :275-278): rot[f][i] = (cos, sin)(f*freqs[i]). */
@@ -133,11 +136,14 @@ int cesm_tflash_supported(int F);
 int cesm_tflash_nblk(int HW);
 /* name of the dq kernel cesm_tflash_bwd runs for (F, HW) (host-only query) */
 const char* cesm_tflash_bwd_variant(int F, int HW);
+/* qkv_pixel_major (F > 16): qkv / dqkv rows ordered [B][HW][F] (a pixel's frames adjacent: the long-window path's
+ * LN writes its output in that order, so the to_qkv GEMM produces it); out / dout / lse keep their layouts */
 int cesm_tflash_fwd(const void* qkv, const float* bias, const float* rot, void* out, float* lse, int B, int F, int HW,
-                    float scale, hipStream_t stream);
+                    float scale, int qkv_pixel_major, hipStream_t stream);
 int cesm_tflash_bwd(const void* qkv, const void* o, const void* dout, const float* lse, const float* bias,
                     const float* rot, void* dqkv, float* dtable, float* dbuf, float* part, float* off, int B, int F,
-                    int HW, float scale, int num_buckets, int max_distance, int accumulate, hipStream_t stream);
+                    int HW, float scale, int num_buckets, int max_distance, int accumulate, int qkv_pixel_major,
+                    hipStream_t stream);
 /* Fused temporal-attention block forward, bf16 (csrc/tblock.hip): y = x + Residual(PreNorm(Attention))
  * (video_net.py:69-98, :350-454) with LN, QKV GEMM, RoPE, MFMA core, out-proj in one kernel; x,y
  * [B*F*HW][C], wqkv [768][C], wout [C][256] packed bf16; saves mr [B*F*HW][2] and lse [B][8][HW][F].

@@ -820,3 +820,28 @@ def test_sla_fold_forward_and_dw_backward(dev, H, W):
     print(f"sla fold/dw HxW={H}x{W}: " + " ".join(f"{k} {v:.2e}" for k, v in errs.items()))
     for k, v in errs.items():
         assert v < 3e-2, (k, v)
+
+
+@pytest.mark.parametrize("F,HW,B", [(120, 77, 2), (33, 300, 1), (17, 40, 3)])
+def test_tflash_pixel_major_matches_frame_major(dev, F, HW, B):
+    """the long-window attention core with pixel-major qkv rows ([B][HW][F], the layout the F > 16 path's LN / to_qkv
+    produce) gives the frame-major core's output bit for bit and the same gradients (dq / dk / dv in the same
+    pixel-major order; the dq kernels differ below 32768 pixels -- D from dO . O vs sum P dP -- hence a tolerance)"""
+    torch.manual_seed(F + HW)
+    scale = 32 ** -0.5
+    freqs = 1.0 / (10000 ** (torch.arange(0, 32, 2).float() / 32))
+    bias = K.relpos_fwd(torch.randn(32, 8).to(dev), F)
+    rot = K.rope_table(freqs.to(dev), F)
+    qkv = torch.randn(B * F * HW, 768, device=dev).to(torch.bfloat16)
+    to_pm = lambda t: t.view(B, F, HW, -1).transpose(1, 2).reshape(B * F * HW, -1).contiguous()  # noqa: E731
+    from_pm = lambda t: t.view(B, HW, F, -1).transpose(1, 2).reshape(B * F * HW, -1)  # noqa: E731
+    out, lse = K.tattn_fwd(qkv, bias, rot, B, F, HW, scale)
+    out_pm, lse_pm = K.tattn_fwd(to_pm(qkv), bias, rot, B, F, HW, scale, pixel_major=True)
+    assert torch.equal(out, out_pm) and torch.equal(lse, lse_pm)
+    g = torch.randn(B * F * HW, 256, device=dev).to(torch.bfloat16)
+    dt, dt_pm = torch.zeros(32, 8, device=dev), torch.zeros(32, 8, device=dev)
+    dqkv = K.tattn_bwd(qkv, out, g, lse, bias, rot, dt, B, F, HW, scale)
+    dqkv_pm = K.tattn_bwd(to_pm(qkv), out_pm, g, lse_pm, bias, rot, dt_pm, B, F, HW, scale, pixel_major=True)
+    torch.cuda.synchronize()
+    assert rel(from_pm(dqkv_pm).float(), dqkv.float()) < 1e-2
+    assert rel(dt_pm, dt) < 1e-3

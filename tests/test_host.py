@@ -198,3 +198,24 @@ def test_tflash_dq_dispatch():
     assert K.tflash_bwd_variant(12, 192 * 288) == "tflash_bwd_q_kernel<1,false>"
     assert K.tflash_bwd_variant(40, 200 * 200) == "tflash_bwd_qw_kernel<3>"
     assert K.tflash_bwd_variant(129, 64) == "invalid"
+
+
+def test_bench_probe_wrappers_accept_kernel_signatures():
+    """bench.py's live kernel probe replaces kernels.* functions with wrappers that compute a label and the work of
+    the call: every wrapper must accept every parameter of the function it wraps (a new keyword on a kernels.*
+    function would otherwise raise inside the timed bench step)"""
+    import ast
+    import inspect
+    import os
+    from cesm_emulator_amd import kernels as K
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")).read()
+    probe = [n for n in ast.parse(src).body if isinstance(n, ast.ClassDef) and n.name == "KernelProbe"][0]
+    init = [n for n in probe.body if isinstance(n, ast.FunctionDef) and n.name == "__init__"][0]
+    checked = 0
+    for n in init.body:
+        if isinstance(n, ast.FunctionDef) and hasattr(K, n.name):
+            have = [a.arg for a in n.args.args]
+            want = list(inspect.signature(getattr(K, n.name)).parameters)
+            assert [p for p in want if p not in have] == [], n.name
+            checked += 1
+    assert checked >= 15
