@@ -1685,11 +1685,6 @@ __device__ __forceinline__ s16x4 kslot4_ld(const bf16* tile, int ld, int lane) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tile + (4 * g + q) * ld + 4 * p));
 }
 
-#ifndef TWH_FULL
-// measured at B = 8 (tools/tblock_time.py): PG 2 / FULL 0 / EARLY_WT 0 4.47 ms (no spills); PG 2 with both on
-// 5.35 ms (40 VGPRs spilled); PG 1 4.86 ms
-#define TWH_FULL 0      // twh_bwd: the head's 12 q/k/v weight fragments at once (1) or in two-tile batches (0)
-#endif
 // twh_bwd: pixels whose attention-core backward is interleaved phase by phase.  Fixed at 1 (round 2: 3375 vs
 // 3460 us with 2, 2 spills vs 10); 2 no longer fits the LDS next to the round-3 tiles, so it is not a knob.
 constexpr int TWH_PG = 1;
@@ -1704,9 +1699,6 @@ constexpr int TWH_PG = 1;
 #endif
 #ifndef TWH_DO_PF
 #define TWH_DO_PF 1  // twh_bwd: the dO GEMM's weights issued during the last q/k/v batch (needs QKV_PIPE)
-#endif
-#ifndef TWH_EARLY_WT
-#define TWH_EARLY_WT 0  // twh_bwd: W'^T fragments of the dxn GEMM issued before the dW GEMM (1)
 #endif
 constexpr int TH_XLD = 72;   // xhat / dy tile row stride (bf16, 144-B rows)
 constexpr int TH_NVMAX = 3;  // voxel tiles per group (4*F <= 48): the 8 slices then fit in LDS
@@ -1748,10 +1740,6 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const int h = wid;
-#ifndef TWH_PRIO
-#define TWH_PRIO 0
-#endif
-  if (TWH_PRIO && wid >= 4) __builtin_amdgcn_s_setprio(1);  // second-dispatched half (MI355X_MICROARCH §Two waves per SIMD, item 4)
   bf16* sq = slices + wid * TWH_WSTRIDE(R);
   bf16* sk = sq + R * HLD;
   bf16* sv = sk + R * HLD;
@@ -2030,14 +2018,6 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
     }
     wave_lds_sync();
     TW_ST(3)
-    // this head's W'^T fragments for the dxn GEMM below, issued now so their latency hides behind the dW GEMM
-    bf16x8 wt[3][T::CT];
-    if constexpr (TWH_EARLY_WT != 0) {
-#pragma unroll
-      for (int kind = 0; kind < 3; ++kind)
-#pragma unroll
-        for (int ct = 0; ct < T::CT; ++ct) wt[kind][ct] = ld_img(wqt_g, ct, QKV / 32, kind * 8 + h, lane);
-    }
 #if TWH_WPIPE
     // the dxn GEMM's W'^T fragments (kind, ct) in a 3-deep ring: the first two in flight during the dW GEMM
     bf16x8 wring[TWH_RING];
@@ -2078,7 +2058,7 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
         if (idx + TWH_RING - 1 < 3 * T::CT) wring[(idx + TWH_RING - 1) % TWH_RING] = ldw(idx + TWH_RING - 1);
         const bf16x8 a = wring[idx % TWH_RING];
 #else
-        const bf16x8 a = TWH_EARLY_WT != 0 ? wt[kind][ct] : ld_img(wqt_g, ct, QKV / 32, kind * 8 + h, lane);
+        const bf16x8 a = ld_img(wqt_g, ct, QKV / 32, kind * 8 + h, lane);
 #endif
 #pragma unroll
         for (int vt = 0; vt < NV; ++vt)

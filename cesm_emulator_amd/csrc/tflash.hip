@@ -382,17 +382,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE)
 #ifndef TF_DO
 #define TF_DO 1
 #endif
-#ifndef TF_DO_PF
-#define TF_DO_PF 0  // A/B knob: register prefetch of the next pixel's rows in the single-pass (D from O) dq kernel, at
-                    // 159 VGPRs (one block per CU; at 128 it spills 31): F = 120 bwd 192x288 13.2 -> 15.1 ms, 96x144
-                    // 3.50 -> 3.96, 24x36 371 -> 467 us -- the second co-resident block hides the loads better
-                    // (profiles/r3_tf_dopf_ab.txt; single-pass without prefetch everywhere: 13.2 -> 13.8 ms)
-#endif
 #ifndef TF_DO_MAXHW
 #define TF_DO_MAXHW 8192
 #endif
 template <int NT, bool DOV>
-__global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(DOV && !TF_DO_PF ? 4 : 2))) void tflash_bwd_q_kernel(
+__global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(DOV ? 4 : 2))) void tflash_bwd_q_kernel(
     const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
     const float* __restrict__ lse, const float* __restrict__ bias, const float* __restrict__ rot,
     bf16* __restrict__ dqkv, float* __restrict__ dbuf, float* __restrict__ part, int F, int HW, float scale) {
@@ -440,8 +434,9 @@ __global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(DOV && 
   }
   bf16x8 kraw = zero8(), vraw = zero8(), qraw = zero8(), draw = zero8(), oraw = zero8();
   float lraw = 0.f;
-  // TF_DO_PF: the single-pass kernel prefetches the next pixel's rows too (K, V, q, dO, O, lse: 21 registers)
-  constexpr bool PF = !DO_ || TF_DO_PF;
+  // (a register prefetch of the next pixel's rows in the single-pass kernel measured slower, round 3:
+  // profiles/r3_tf_dopf_ab.txt -- the second co-resident block hides the loads better)
+  constexpr bool PF = !DO_;
   auto fetch = [&](int pp) {
     const int64_t r0 = (int64_t)b * F * HW + pp;
     const int64_t rs = (r0 + (int64_t)sfc * HW) * QKV + h * DH + sc * 8;
