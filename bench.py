@@ -193,8 +193,8 @@ class KernelProbe:
                       pixel_major=False):
             v = B * F * HW
             nt = (F + 15) // 16
-            # the dq kernel by dispatch (per-wave from 32768 pixels, block-per-pixel below: cesm_tflash_bwd_variant)
-            dq = f"tflash_bwd_qw_kernel<{nt}>" if pixel_major else K.tflash_bwd_variant(F, HW)
+            # the dq kernel by dispatch (cesm_tflash_bwd_variant)
+            dq = K.tflash_bwd_variant(F, HW)  # the same selection for pixel-major qkv
             lab = (f"{dq.replace(',false>', '>').replace(',true>', '>')} + "
                    f"tflash_bwd_kv_kernel<{nt}>" if K._tflash(qkv, F) else "tattn_bwd_kernel")
             # dP, dQ, dK, dV products (2x the forward); bytes: qkv, o, dout, lse read, dqkv written

@@ -389,7 +389,7 @@ template <int NT, bool DOV>
 __global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(DOV ? 4 : 2))) void tflash_bwd_q_kernel(
     const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
     const float* __restrict__ lse, const float* __restrict__ bias, const float* __restrict__ rot,
-    bf16* __restrict__ dqkv, float* __restrict__ dbuf, float* __restrict__ part, int F, int HW, float scale) {
+    bf16* __restrict__ dqkv, float* __restrict__ dbuf, float* __restrict__ part, int F, int HW, float scale, int pm) {
   constexpr int NP = (NT + 1) / 2, NR = 32 * NP, NTH = 64 * NT;
   constexpr bool DO_ = DOV;
   __shared__ __attribute__((aligned(16))) float btab[4 * 32 * NT];
@@ -437,14 +437,17 @@ __global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(DOV ? 4
   // (a register prefetch of the next pixel's rows in the single-pass kernel measured slower, round 3:
   // profiles/r3_tf_dopf_ab.txt -- the second co-resident block hides the loads better)
   constexpr bool PF = !DO_;
+  // qkv / dqkv rows frame-major or pixel-major (pm); dout / o frame-major
+  const int qfs = pm ? 1 : HW;
+  auto qrow = [&](int pp) { return pm ? ((int64_t)b * HW + pp) * F : (int64_t)b * F * HW + pp; };
   auto fetch = [&](int pp) {
-    const int64_t r0 = (int64_t)b * F * HW + pp;
-    const int64_t rs = (r0 + (int64_t)sfc * HW) * QKV + h * DH + sc * 8;
+    const int64_t r0 = (int64_t)b * F * HW + pp, q0 = qrow(pp);
+    const int64_t rs = (q0 + (int64_t)sfc * qfs) * QKV + h * DH + sc * 8;
     kraw = ld16(qkv + rs + INNER);
     vraw = ld16(qkv + rs + 2 * INNER);
     if (PF) {
       const int64_t vq = r0 + (int64_t)fqc * HW;
-      qraw = ld16(qkv + vq * QKV + h * DH + g * 8);
+      qraw = ld16(qkv + (q0 + (int64_t)fqc * qfs) * QKV + h * DH + g * 8);
       draw = ld16(dout + vq * INNER + h * DH + g * 8);
       if (DO_) oraw = ld16(o + vq * INNER + h * DH + g * 8);
       lraw = lse[(((int64_t)b * NH + h) * HW + pp) * F + fqc];
@@ -453,7 +456,7 @@ __global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(DOV ? 4
   if (PF && (int)blockIdx.x < HW) fetch(blockIdx.x);
 
   for (int p = blockIdx.x; p < HW; p += gridDim.x) {
-    const int64_t row0 = (int64_t)b * F * HW + p;
+    const int64_t row0 = (int64_t)b * F * HW + p, qrow0 = qrow(p);
     __syncthreads();  // previous pixel's rows consumed
     bf16x8 qf, dof;
     float Li, Do = 0.f;
@@ -464,7 +467,7 @@ __global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(DOV ? 4
       *reinterpret_cast<bf16x8*>(ks + sf * TF_LD + sc * 8) = sok ? rope8(kraw, cs, 1.f) : zero8();
       *reinterpret_cast<bf16x8*>(vs + sf * TF_LD + sc * 8) = sok ? vraw : zero8();
       const int64_t vq = row0 + (int64_t)fqc * HW;
-      const bf16x8 qr = PF ? qraw : ld16(qkv + vq * QKV + h * DH + g * 8);
+      const bf16x8 qr = PF ? qraw : ld16(qkv + (qrow0 + (int64_t)fqc * qfs) * QKV + h * DH + g * 8);
       dof = PF ? draw : ld16(dout + vq * INNER + h * DH + g * 8);
       const bf16x8 orw = PF ? oraw : ld16(o + vq * INNER + h * DH + g * 8);
       const float lr_ = PF ? lraw : lse[(((int64_t)b * NH + h) * HW + p) * F + fqc];
@@ -525,7 +528,7 @@ __global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(DOV ? 4
           const int d0 = t * 16 + 4 * g;
           float v4[4] = {dqt[t][0], dqt[t][1], dqt[t][2], dqt[t][3]};
           rope4_inv(v4, rot, fq, d0, scale);  // dq = scale R^T dQ'
-          store4b(dqkv + (row0 + (int64_t)fq * HW) * QKV + h * DH + d0, v4);
+          store4b(dqkv + (qrow0 + (int64_t)fq * qfs) * QKV + h * DH + d0, v4);
         }
       }
       continue;
@@ -576,7 +579,7 @@ __global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(DOV ? 4
         const int d0 = t * 16 + 4 * g;
         float v4[4] = {dqt[t][0], dqt[t][1], dqt[t][2], dqt[t][3]};
         rope4_inv(v4, rot, fq, d0, scale);  // dq = scale R^T dQ'
-        store4b(dqkv + (row0 + (int64_t)fq * HW) * QKV + h * DH + d0, v4);
+        store4b(dqkv + (qrow0 + (int64_t)fq * qfs) * QKV + h * DH + d0, v4);
       }
     }
   }
@@ -620,9 +623,6 @@ __global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(DOV ? 4
 // Every lane-derived quantity is recomputed per pixel from an opaque copy of the lane id: as loop invariants the
 // compiler hoisted them all (per-frame RoPE coefficients, bias-table reads, LDS and global addresses: > 200
 // VGPRs at NT = 8) out of the pixel loop and spilled.
-#ifndef TF_QW_MINHW
-#define TF_QW_MINHW 32768
-#endif
 #ifndef TFQW_KREG
 #define TFQW_KREG 1  // K' A fragments of the pixel held in registers (0: re-read from the staged rows per query tile)
 #endif
@@ -972,16 +972,14 @@ __global__ void tf_dtable_kernel(const float* __restrict__ off, float* __restric
 
 }  // namespace
 
-// which dq kernel cesm_tflash_bwd runs.  The per-wave kernel (32-bit tile offsets) from TF_QW_MINHW pixels: whole
-// F = 120 backward 192x288 94.6 -> 14.0 ms (the block-per-pixel kernel's 432-pixel barrier-lockstep walk per block
-// collapses there), 96x144 3.61 -> 3.72, 48x72 1.00 -> 1.10, 24x36 0.37 -> 0.41 (profiles/r4c5_qw_check.txt).
-// CESM_TF_QW=1 forces it for every F > 16, CESM_TF_NO_QW=1 disables it.
+// which dq kernel cesm_tflash_bwd runs.  The per-wave kernel is opt-in (CESM_TF_QW=1): in the F = 120 training step
+// the block-per-pixel kernels are faster at every level (whole step 229.9-230.0 vs 232.5-233.0 ms with it at level 0,
+// profiles/r4c13_env_ab.txt; its isolated 192x288 timing against them, profiles/r4c5_qw_check.txt, was not borne out
+// in the step).
 enum TfDq { TF_DQ_BLOCK, TF_DQ_DOV, TF_DQ_WAVE };
-// Pixel-major qkv (pm) always takes the per-wave kernel: the block-per-pixel kernels read frame-major rows only.
 static TfDq tf_dq_kind(int nt, int HW, int pm = 0) {
-  if (nt >= 2 && pm) return TF_DQ_WAVE;
-  if (nt >= 2 && (int64_t)16 * HW * QKV * 2 < (1ll << 31) && !getenv_flag("CESM_TF_NO_QW") &&
-      (HW >= TF_QW_MINHW || getenv_flag("CESM_TF_QW")))
+  if (nt >= 2 && getenv_flag("CESM_TF_QW") && !getenv_flag("CESM_TF_NO_QW") &&
+      (pm || (int64_t)16 * HW * QKV * 2 < (1ll << 31)))
     return TF_DQ_WAVE;
   return TF_DO && nt >= 2 && HW < TF_DO_MAXHW ? TF_DQ_DOV : TF_DQ_BLOCK;
 }
@@ -1062,10 +1060,11 @@ int cesm_tflash_bwd(const void* qkv, const void* o, const void* dout, const floa
                                                                    dbuf, part, F, HW, scale, pm);                     \
   else if (dov && N >= 2)                                                                                              \
     tflash_bwd_q_kernel<N, (N >= 2)><<<gq, 64 * N, 0, stream>>>((const bf16*)qkv, (const bf16*)o, (const bf16*)dout,   \
-                                                                lse, bias, rot, (bf16*)dqkv, dbuf, part, F, HW, scale); \
+                                                                lse, bias, rot, (bf16*)dqkv, dbuf, part, F, HW, scale, \
+                                                                pm);                                                  \
   else                                                                                                                 \
     tflash_bwd_q_kernel<N, false><<<gq, 64 * N, 0, stream>>>((const bf16*)qkv, (const bf16*)o, (const bf16*)dout, lse, \
-                                                             bias, rot, (bf16*)dqkv, dbuf, part, F, HW, scale);       \
+                                                             bias, rot, (bf16*)dqkv, dbuf, part, F, HW, scale, pm);   \
   tflash_bwd_kv_kernel<N><<<gk, 256, 0, stream>>>((const bf16*)qkv, (const bf16*)dout, lse, dbuf, bias, rot,           \
                                                   (bf16*)dqkv, F, HW, scale, pm)
   switch (nt) {

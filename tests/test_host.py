@@ -188,15 +188,14 @@ def test_bench_shape_dispatch_table():
 
 
 def test_tflash_dq_dispatch():
-    """the dq kernel of the long-window attention backward (cesm_tflash_bwd_variant, host only): the per-wave kernel
-    from 32768 pixels (config 4's level 0, 192x288), the block-per-pixel kernels below (D from O under 8192 pixels),
-    the exact two-pass form at F <= 16"""
+    """the dq kernel of the long-window attention backward (cesm_tflash_bwd_variant, host only): the block-per-pixel
+    kernels (D from O under 8192 pixels, the two-pass form above and at F <= 16); the per-wave kernel is opt-in"""
     from cesm_emulator_amd import kernels as K
-    assert K.tflash_bwd_variant(120, 192 * 288) == "tflash_bwd_qw_kernel<8>"
+    assert K.tflash_bwd_variant(120, 192 * 288) == "tflash_bwd_q_kernel<8,false>"
     assert K.tflash_bwd_variant(120, 96 * 144) == "tflash_bwd_q_kernel<8,false>"
     assert K.tflash_bwd_variant(120, 48 * 72) == "tflash_bwd_q_kernel<8,true>"
     assert K.tflash_bwd_variant(12, 192 * 288) == "tflash_bwd_q_kernel<1,false>"
-    assert K.tflash_bwd_variant(40, 200 * 200) == "tflash_bwd_qw_kernel<3>"
+    assert K.tflash_bwd_variant(40, 200 * 200) == "tflash_bwd_q_kernel<3,false>"
     assert K.tflash_bwd_variant(129, 64) == "invalid"
 
 
