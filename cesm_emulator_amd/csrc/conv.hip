@@ -1636,9 +1636,6 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
 #ifndef WS_TOUCH
 #define WS_TOUCH 1  // L2 touch of the next item's halo lines a step ahead of its stage DMA
 #endif
-#ifndef WS_COLMAJ
-#define WS_COLMAJ 0  // A/B knob: items in column runs per XCD (vertical halo sharing in L2)
-#endif
 #ifndef WS_RW
 #define WS_RW 1  // resident weights when Cin = 64 and one co block (the level-0 64 -> 64 conv)
 #endif
@@ -1655,25 +1652,13 @@ static_assert(2 * WS_WROWS * 64 + 2 * WS_HROWS * 64 == 2 * WS_STAGE, "resident-w
 constexpr int WS_HPMAX = (WS_HROWS / 16 + 3) / 4;          // halo pieces per loader wave (<= 7)
 constexpr int WS_WP = WS_WROWS / 16 / 4;                   // weight pieces per loader wave (9)
 
-__device__ __forceinline__ void ws_decode(int it, int ncob, int ntile, int tiles_x, int tiles_y, int& tile, int& cb) {
-  if (WS_COLMAJ && ncob == 1) {
-    // column runs (WS_COLMAJ): item it on XCD it % 8 takes the (it / 8)-th tile of that XCD's runs of tiles_y
-    // vertically adjacent tiles, so the tiles sharing halo rows are fetched by one L2 at about the same time
-    const int q = it >> 3, run = (q / tiles_y) * 8 + (it & 7);
-    const int tc = run * tiles_y + q % tiles_y;  // column-major tile index: ((n * tiles_x) + c) * tiles_y + r
-    const int col = tc / tiles_y, r = tc - col * tiles_y, n = col / tiles_x, c = col - n * tiles_x;
-    cb = 0;
-    tile = (n * tiles_y + r) * tiles_x + c;
-    if (n * tiles_x * tiles_y >= ntile) tile = ntile;  // past the last image: invalid (skipped)
-    return;
-  }
-  // co blocks of a tile 8 ids apart: the blocks b, b + 8, ... that take them share an XCD (round-robin placement)
+__device__ __forceinline__ void ws_decode(int it, int ncob, int& tile, int& cb) {
+  // co blocks of a tile 8 ids apart: the blocks b, b + 8, ... that take them share an XCD (round-robin placement).
+  // (Round 4: items in per-XCD runs of vertically adjacent tiles, so tiles sharing halo rows meet in one L2, measured
+  // 514-516 -> 548-552 us per launch in the step, profiles/r4c15_bench_ab.txt; removed.)
   const int g = it / (8 * ncob), r = it - g * 8 * ncob;
   cb = r >> 3;
   tile = g * 8 + (r & 7);
-  (void)ntile;
-  (void)tiles_x;
-  (void)tiles_y;
 }
 
 template <int TW, bool GN>
@@ -1696,13 +1681,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3ws_kernel(const bf16* __restric
   auto next_valid = [&](int it) {
     for (; it < nitems_pad; it += G) {
       int tile, cb;
-      ws_decode(it, ncob, ntile, tiles_x, tiles_per_img / tiles_x, tile, cb);
+      ws_decode(it, ncob, tile, cb);
       if (tile < ntile) return it;
     }
     return nitems_pad;
   };
   auto geo = [&](int it, int& n, int& y0, int& x0, int& cb, int& tile) {
-    ws_decode(it, ncob, ntile, tiles_x, tiles_per_img / tiles_x, tile, cb);
+    ws_decode(it, ncob, tile, cb);
     n = tile / tiles_per_img;
     const int r = tile - n * tiles_per_img, ty = r / tiles_x;
     y0 = ty * TH;
@@ -4345,7 +4330,7 @@ int conv_fwd_launch(int dtype, const void* x1, const void* x2, const void* wp, c
       const int tx = (int)cdiv(Wo, TW), ty = (int)cdiv(Ho, TH);
       const int ncob = Cout / 64;
       const int ntile = Nb * tx * ty;
-      const int nitems_pad = (WS_COLMAJ && ncob == 1) ? (int)cdiv(ntile, 8 * ty) * 8 * ty : (int)cdiv(ntile, 8) * 8 * ncob;
+      const int nitems_pad = (int)cdiv(ntile, 8) * 8 * ncob;
       const int nblk = std::min(nitems_pad, cesm_num_cus());
 #define WSL(TWv, GNv)                                                                                              \
   conv3x3ws_kernel<TWv, GNv><<<nblk, 512, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, TH, tx, tx * ty, ncob, \
