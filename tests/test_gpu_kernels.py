@@ -277,7 +277,7 @@ def _tattn_ref(qkv, bias, freqs, B, Fr, HW, scale):
 
 
 @pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("Fr", [1, 3, 12, 33, 64, 120])
+@pytest.mark.parametrize("Fr", [1, 3, 12, 33, 64, 80, 100, 120])
 def test_temporal_attention_core(dev, cdt, Fr):
     """unfused temporal attention; F > 32 exercises the F-sized LDS tables (decadal window F = 120)"""
     torch.manual_seed(4)
