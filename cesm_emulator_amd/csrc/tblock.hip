@@ -1688,6 +1688,9 @@ __device__ __forceinline__ s16x4 kslot4_ld(const bf16* tile, int ld, int lane) {
 // twh_bwd: pixels whose attention-core backward is interleaved phase by phase.  Fixed at 1 (round 2: 3375 vs
 // 3460 us with 2, 2 spills vs 10); 2 no longer fits the LDS next to the round-3 tiles, so it is not a knob.
 constexpr int TWH_PG = 1;
+#ifndef TWH_PK
+#define TWH_PK 1  // A/B knob: packed 2-wide fp32 VALU ops in twh_bwd's softmax-gradient elementwise step
+#endif
 #ifndef TWH_QKV_PIPE
 #define TWH_QKV_PIPE 1  // twh_bwd: double-buffered q/k/v weight batches, the first issued before barrier A
 #endif
@@ -1955,6 +1958,38 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
 #pragma unroll
         for (int q = 1; q < T::PW; ++q) Li = pp0 + u == q ? Lp[q] : Li;
         float pt[4], D = 0.f;
+#if TWH_PK
+        // two elements per VALU op (v_pk_fma / v_pk_add / v_pk_mul_f32) where the order allows, same results
+        float ds4[4];
+#pragma unroll
+        for (int r = 0; r < 4; r += 2) {
+          const f32x2 x2 = __builtin_elementwise_fma(f32x2{st[u][r], st[u][r + 1]}, f32x2{LOG2E, LOG2E},
+                                                     f32x2{bt[r], bt[r + 1]}) - f32x2{Li, Li};
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const bool ok = pix && lg * 4 + r + e < F && lr < F;
+            pt[r + e] = ok ? __builtin_amdgcn_exp2f(x2[e]) : 0.f;
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) D = fmaf(pt[r], dpt[u][r], D);
+        D = grp4_sum(D);
+#pragma unroll
+        for (int r = 0; r < 4; r += 2) {
+          const f32x2 d2 = f32x2{pt[r], pt[r + 1]} * (f32x2{dpt[u][r], dpt[u][r + 1]} - f32x2{D, D});
+          const f32x2 a2 = f32x2{dbacc[r], dbacc[r + 1]} + d2;
+          dbacc[r] = a2[0];
+          dbacc[r + 1] = a2[1];
+          ds4[r] = d2[0];
+          ds4[r + 1] = d2[1];
+        }
+        bf16x4 p4, d4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          d4[r] = (bf16)ds4[r];
+          p4[r] = (bf16)pt[r];
+        }
+#else
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const bool ok = pix && lg * 4 + r < F && lr < F;
@@ -1970,6 +2005,7 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
           d4[r] = (bf16)ds;
           p4[r] = (bf16)pt[r];
         }
+#endif
         dst_b[u] = __builtin_bit_cast(s16x4, d4);
         // tile[i = lr][j = 4g .. 4g+3]
         *reinterpret_cast<bf16x4*>(trt + (u * 2 + 0) * 256 + lr * 16 + lg * 4) = p4;

@@ -208,6 +208,9 @@ __device__ __forceinline__ const float* btab_lane(const float* tab, int lr, int 
 #ifndef TF_VH
 #define TF_VH 2  // forward V staging: key-tile pairs per part (4 = all at F = 128)
 #endif
+#ifndef TF_PK
+#define TF_PK 1  // A/B knob: packed 2-wide fp32 VALU ops in the dk / dv kernel's softmax-gradient elementwise step
+#endif
 #ifndef TF_BUF
 #define TF_BUF 1  // A/B knob: buffer-resource tile addressing in the per-query-tile loop (0 = 64-bit lane math)
 #endif
@@ -895,12 +898,27 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_kv_kernel(
           const f32x4 bo = *reinterpret_cast<const f32x4*>(bk + 16 * qt);
           const f32x4 lq = *reinterpret_cast<const f32x4*>(Ls + qt * 16 + 4 * g);
           const f32x4 dq = *reinterpret_cast<const f32x4*>(Ds + qt * 16 + 4 * g);
+#if TF_PK
+          // two elements per VALU op (v_pk_fma / v_pk_add / v_pk_mul_f32), same operations and order as below
+#pragma unroll
+          for (int r = 0; r < 4; r += 2) {
+            const f32x2 s2 = {sq[r], sq[r + 1]}, b2 = {bo[r], bo[r + 1]}, l2 = {lq[r], lq[r + 1]};
+            const f32x2 x2 = __builtin_elementwise_fma(s2, f32x2{LOG2E, LOG2E}, b2) - l2;
+            const f32x2 p2 = {__builtin_amdgcn_exp2f(x2[0]), __builtin_amdgcn_exp2f(x2[1])};
+            const f32x2 d2 = p2 * (f32x2{dp[r], dp[r + 1]} - f32x2{dq[r], dq[r + 1]});
+            pv[u][r] = p2[0];
+            pv[u][r + 1] = p2[1];
+            dsv[u][r] = d2[0];
+            dsv[u][r + 1] = d2[1];
+          }
+#else
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float pp = __builtin_amdgcn_exp2f(fmaf(sq[r], LOG2E, bo[r]) - lq[r]);
             pv[u][r] = pp;
             dsv[u][r] = pp * (dp[r] - dq[r]);
           }
+#endif
         } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r) pv[u][r] = dsv[u][r] = 0.f;
