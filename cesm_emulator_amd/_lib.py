@@ -17,6 +17,13 @@ import os
 # CESM_HIP_LIB selects a diagnostic build (tools/build_diag.sh); default: the in-tree product library
 LIBPATH = Path(os.environ["CESM_HIP_LIB"]) if os.environ.get("CESM_HIP_LIB") else PKG / "libcesm_hip.so"
 
+def header_abi_version(path: Path = HEADER) -> int:
+    m = re.search(r"#define\s+CESM_ABI_VERSION\s+(\d+)", path.read_text())
+    if not m:
+        raise RuntimeError(f"{path}: no CESM_ABI_VERSION")
+    return int(m.group(1))
+
+
 _CTYPE = {"int": ctypes.c_int, "int64_t": ctypes.c_int64, "float": ctypes.c_float, "double": ctypes.c_double}
 
 
@@ -31,7 +38,7 @@ def parse_header(path: Path = HEADER):
         types = []
         for a in args.split(","):
             a = " ".join(a.replace("const", " ").split())
-            if not a:
+            if not a or a == "void":
                 continue
             if "*" in a or a.startswith("hipStream_t"):
                 types.append(ctypes.c_void_p)
@@ -56,6 +63,10 @@ def lib():
             fn = getattr(handle, name)  # AttributeError -> missing export, fail loudly
             fn.restype = res
             fn.argtypes = args
+        have, want = handle.cesm_abi_version(), header_abi_version()
+        if have != want:
+            raise RuntimeError(f"{LIBPATH} has C ABI version {have}, include/cesm_hip.h declares {want}: rebuild "
+                               "the library (python -m cesm_emulator_amd.build)")
         _lib = handle
     return _lib
 

@@ -57,7 +57,8 @@ def build(force: bool = False) -> Path:
     if force or not LIB.exists() or any(o.stat().st_mtime > LIB.stat().st_mtime for o in objs):
         # link next to the library and rename over it: a reader (a running process, a tree snapshot) sees the old
         # or the new file, never a partly written one
-        tmp = LIB.with_name(LIB.name + ".tmp")
+        # (a per-process temp name: two concurrent builds must not link into the same file)
+        tmp = LIB.with_name(f"{LIB.name}.{os.getpid()}.tmp")
         cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-Wl,--no-undefined", *map(str, objs), "-o", str(tmp)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:

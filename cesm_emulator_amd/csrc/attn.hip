@@ -13,6 +13,7 @@
 //   qkv [V][768] = q | k | v, head-major inside each (channel = h*32 + d)
 //   out [V][256]
 #include "common.h"
+#include "cesm_hip.h"
 
 namespace {
 

@@ -17,6 +17,7 @@
 // Weight gradients use a second MFMA kernel (pixel axis = MFMA K) that writes fp32 split-K
 // slabs, reduced deterministically by conv_wgrad_reduce into the PyTorch weight layout.
 #include "common.h"
+#include "cesm_hip.h"
 
 namespace {
 
@@ -1667,9 +1668,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3ws_kernel(const bf16* __restric
                                                            const bf16* __restrict__ res, const bf16* __restrict__ res2,
                                                            bf16* __restrict__ y1, bf16* __restrict__ y2, ConvGeom g,
                                                            int TH, int tiles_x, int tiles_per_img, int ncob,
-                                                           int nitems_pad, float* __restrict__ gnp, int gn_fimg) {
-  __shared__ __attribute__((aligned(1024))) char lds[WS_LDS + 1024];  // + the touch loads' never-read rows
+                                                           int nitems_pad, float* __restrict__ gnp, int gn_fimg,
+                                                           int* __restrict__ queue) {
+  // + the touch loads' never-read rows (1 KiB) + 3 published item ids (dynamic claiming)
+  __shared__ __attribute__((aligned(1024))) char lds[WS_LDS + 1024 + 16];
   bf16* stg = reinterpret_cast<bf16*>(lds + 2 * WS_STAGE);
+  int* qslot = reinterpret_cast<int*>(lds + WS_LDS + 1024);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const bool loader = wid >= 4;  // wave-uniform role
   const int wl = wid & 3;
@@ -1685,6 +1689,39 @@ __global__ __launch_bounds__(512, 1) void conv3x3ws_kernel(const bf16* __restric
       if (tile < ntile) return it;
     }
     return nitems_pad;
+  };
+  // Item order.  Static (queue == null): item k of the block is the k-th valid id of blockIdx.x + j * G.  Dynamic
+  // (round 5; a caller-owned counter, see cesm_conv_fwd): every item is claimed from queue[0] by one returning atomic
+  // add -- a block slowed by co-running kernels (RCCL's, on the communication stream) or placed late takes fewer items
+  // (none, if it starts after the queue has run dry) instead of leaving a static split's tail.  Claims run two items
+  // ahead so every wave knows item k + 1 (the stage DMA, the L2 touch, the compute waves' bias and loop end) a full
+  // item before it starts: loader wave 0 claims item k + 2 at item k's first step and publishes it in
+  // qslot[(k + 2) % 3], which every wave reads at item k + 1's first step, a barrier later (the slot it overwrites
+  // held item k - 1, read a barrier before); items 0 and 1 are claimed before a block barrier ahead of the loops.
+  // The outputs do not depend on the order: an item is one block's whole 9 x Cin sum, and the GroupNorm partial slot
+  // belongs to the tile.  Needs nchunk >= 2 (else the static order).  The last block to finish resets the counter,
+  // so it is zero again for the next launch on the same stream.
+  const bool dyn = queue != nullptr && nchunk >= 2;
+  auto claim = [&]() {  // one lane; the next valid claimed id, or nitems_pad
+    while (true) {
+      const int it = atomicAdd(queue, 1);
+      if (it >= nitems_pad) return nitems_pad;
+      int tile, cb;
+      ws_decode(it, ncob, tile, cb);
+      if (tile < ntile) return it;
+    }
+  };
+  auto publish = [&](int k, int val) {  // loader wave 0: item k's id into its slot (readers: after a barrier)
+    if (lane == 0) qslot[k % 3] = val;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  auto finish_queue = [&]() {  // every block once, after its last claim: the last one resets the counter
+    if (dyn && tid == 0) {  // (device-scope atomics: no fence, nothing else is published through the counter)
+      if (atomicAdd(queue + 1, 1) == G - 1) {
+        atomicExch(queue, 0);
+        atomicExch(queue + 1, 0);
+      }
+    }
   };
   auto geo = [&](int it, int& n, int& y0, int& x0, int& cb, int& tile) {
     ws_decode(it, ncob, tile, cb);
@@ -1898,8 +1935,29 @@ __global__ __launch_bounds__(512, 1) void conv3x3ws_kernel(const bf16* __restric
 
   // ---------------- the step loops: one per role, the same sequence of steps and barriers (a loop per role keeps
   // the two roles' registers apart: one shared loop held the loader's residual rows live through the MFMAs)
-  int it0 = next_valid((int)blockIdx.x);
-  if (it0 >= nitems_pad) return;  // whole block, before any barrier
+  int it0;
+  if (dyn) {  // items 0 and 1, claimed by loader wave 0 and published before a block barrier
+    if (wid == 4) {
+      int s0 = nitems_pad, s1 = nitems_pad;
+      if (lane == 0) {
+        s0 = claim();
+        if (s0 < nitems_pad) s1 = claim();
+      }
+      publish(0, __builtin_amdgcn_readfirstlane(s0));
+      publish(1, __builtin_amdgcn_readfirstlane(s1));
+    }
+    __syncthreads();
+    it0 = qslot[0];
+    if (it0 >= nitems_pad) {  // the queue ran dry before this block started (whole block)
+      finish_queue();
+      return;
+    }
+  } else {
+    it0 = next_valid((int)blockIdx.x);
+    if (it0 >= nitems_pad) return;  // whole block, before any barrier
+  }
+  // the item after `it` (item k): static order, or the published claim (read at item k's first step)
+  auto successor = [&](int k, int it) { return dyn ? qslot[(k + 1) % 3] : next_valid(it + G); };
   if (loader) {
     if (rw) {
       issue_w(0, 0, wbase(0, 0));
@@ -1907,12 +1965,20 @@ __global__ __launch_bounds__(512, 1) void conv3x3ws_kernel(const bf16* __restric
     }
     issue_stage(it0, 0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int it = it0, ch = 0, s = 0, prev_it = -1;
+    int it = it0, ch = 0, s = 0, prev_it = -1, k = 0, succ = nitems_pad;
     const bool do_touch = WS_TOUCH && g.C1 * 2 <= 128 && nchunk >= 2;
     while (true) {
       __builtin_amdgcn_s_barrier();  // stage s landed; stage s - 1 consumed; staging of prev_it written (ch == 0)
+      if (ch == 0) {
+        succ = successor(k, it);
+        if (dyn && wid == 4) {  // claim item k + 2 (none once the queue has run dry)
+          int s2 = nitems_pad;
+          if (lane == 0 && succ < nitems_pad) s2 = claim();
+          publish(k + 2, __builtin_amdgcn_readfirstlane(s2));
+        }
+      }
       const int nxt_ch = ch + 1 < nchunk ? ch + 1 : 0;
-      const int nxt_it = ch + 1 < nchunk ? it : next_valid(it + G);
+      const int nxt_it = ch + 1 < nchunk ? it : succ;
       const bool more = nxt_it < nitems_pad;
       const bool epi = ch == 0 && prev_it >= 0;
       if (epi) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // residual rows of prev_it
@@ -1923,13 +1989,16 @@ __global__ __launch_bounds__(512, 1) void conv3x3ws_kernel(const bf16* __restric
       if (pre) load_res(nxt_it);
       // the item after next: its halo lines into L2 while this item's chunks run
       int tit = nitems_pad;
-      if (do_touch && ch == 0) tit = next_valid(it + G);
+      if (do_touch && ch == 0) tit = succ;
       const bool tch = tit < nitems_pad;
       if (tch) touch(tit);
       // wait for this step's DMA only: the epilogue's stores (8 rows [+ 1 GN partial]), the residual loads (8) and
       // the touches (2) issued after it may stay in flight
       vm_wait((epi ? (GN ? 9 : 8) : 0) + (pre ? 8 : 0) + (tch ? 2 : 0));
-      if (ch == nchunk - 1) prev_it = it;
+      if (ch == nchunk - 1) {
+        prev_it = it;
+        ++k;
+      }
       ch = nxt_ch;
       it = nxt_it;
       ++s;
@@ -1939,11 +2008,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3ws_kernel(const bf16* __restric
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     epilogue(prev_it);
   } else {
-    int it = it0, ch = 0, s = 0;
+    int it = it0, ch = 0, s = 0, k = 0, succ = nitems_pad;
     while (true) {
       __builtin_amdgcn_s_barrier();  // stage s landed; the staging tile free again (ch == 0)
+      if (ch == 0) succ = successor(k, it);
       const int nxt_ch = ch + 1 < nchunk ? ch + 1 : 0;
-      const int nxt_it = ch + 1 < nchunk ? it : next_valid(it + G);
+      const int nxt_it = ch + 1 < nchunk ? it : succ;
       if (ch == 0) {
         int n, y0, x0, cb, tile;
         geo(it, n, y0, x0, cb, tile);
@@ -1964,6 +2034,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3ws_kernel(const bf16* __restric
             acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
           }
         }
+        ++k;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging rows visible at the barrier
       ch = nxt_ch;
@@ -1973,6 +2044,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3ws_kernel(const bf16* __restric
     }
     __builtin_amdgcn_s_barrier();  // pairs with the loaders' last barrier
   }
+  finish_queue();
 }
 
 // ----------------------------------------------------------------------------------------
@@ -4269,7 +4341,7 @@ int64_t conv_gn_nslot(const ConvFwdPlan& pl, int Nb, int Ho, int Wo, int B) {
 
 int conv_fwd_launch(int dtype, const void* x1, const void* x2, const void* wp, const float* bias, const void* res,
                     const void* res2, void* y1, void* y2, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo,
-                    int Cout, int Co1, int KH, int KW, int S, int P, int U, float* gnp, int gn_fimg,
+                    int Cout, int Co1, int KH, int KW, int S, int P, int U, float* gnp, int gn_fimg, int* queue,
                     hipStream_t stream) {
   const ConvFwdPlan pl = conv_fwd_plan(dtype, Nb, Hi, Wi, C1, C2, Ho, Wo, Cout, Co1, KH, KW, S, P, U);
   if (pl.v == CFV_INVALID) return CESM_EINVAL;
@@ -4334,7 +4406,7 @@ int conv_fwd_launch(int dtype, const void* x1, const void* x2, const void* wp, c
       const int nblk = std::min(nitems_pad, cesm_num_cus());
 #define WSL(TWv, GNv)                                                                                              \
   conv3x3ws_kernel<TWv, GNv><<<nblk, 512, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, TH, tx, tx * ty, ncob, \
-                                                       nitems_pad, gnp, gn_fimg)
+                                                       nitems_pad, gnp, gn_fimg, queue)
       if (pl.v == CFV_WS36) { if (gnp) WSL(36, true); else WSL(36, false); }
       else { if (gnp) WSL(32, true); else WSL(32, false); }
 #undef WSL
@@ -4436,10 +4508,10 @@ extern "C" {
 // null if C2 == 0), wp [Cout][KH*KW][C1+C2] packed, y1 [Nb][Ho][Wo][Co1], y2 [..][Cout-Co1].
 int cesm_conv_fwd(int dtype, const void* x1, const void* x2, const void* wp, const float* bias, const void* res,
                   const void* res2, void* y1, void* y2, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout, int Co1,
-                  int KH, int KW, int S, int P, int U, hipStream_t stream) {
+                  int KH, int KW, int S, int P, int U, int* queue, hipStream_t stream) {
   if (Nb <= 0 || Ho <= 0 || Wo <= 0) return CESM_OK;
   return conv_fwd_launch(dtype, x1, x2, wp, bias, res, res2, y1, y2, Nb, Hi, Wi, C1, C2, Ho, Wo, Cout, Co1, KH, KW, S, P,
-                         U, nullptr, 1, stream);
+                         U, nullptr, 1, queue, stream);
 }
 
 int64_t cesm_conv_gn_nslot(int dtype, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout, int KH, int KW,
@@ -4450,13 +4522,13 @@ int64_t cesm_conv_gn_nslot(int dtype, int Nb, int Hi, int Wi, int C1, int C2, in
 
 int cesm_conv_fwd_gn(int dtype, const void* x1, const void* x2, const void* wp, const float* bias, void* y, float* gnpart,
                      int B, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout, int KH, int KW, int S,
-                     int P, int U, hipStream_t stream) {
+                     int P, int U, int* queue, hipStream_t stream) {
   if (Nb <= 0 || Ho <= 0 || Wo <= 0) return CESM_OK;
   const ConvFwdPlan pl = conv_fwd_plan(dtype, Nb, Hi, Wi, C1, C2, Ho, Wo, Cout, Cout, KH, KW, S, P, U);
   if (pl.v == CFV_INVALID) return CESM_EINVAL;
   if (!gnpart || conv_gn_nslot(pl, Nb, Ho, Wo, B) == 0) return CESM_EUNSUPPORTED;
   return conv_fwd_launch(dtype, x1, x2, wp, bias, nullptr, nullptr, y, nullptr, Nb, Hi, Wi, C1, C2, Ho, Wo, Cout, Cout,
-                         KH, KW, S, P, U, gnpart, Nb / B, stream);
+                         KH, KW, S, P, U, gnpart, Nb / B, queue, stream);
 }
 
 }  // extern "C"

@@ -12,6 +12,7 @@
 // so the streaming kernels keep a thread on one 8-channel group (coefficients in registers)
 // and touch HBM only for the activations.
 #include "common.h"
+#include "cesm_hip.h"
 
 namespace {
 

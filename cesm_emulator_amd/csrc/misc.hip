@@ -6,6 +6,7 @@
 //    (torch/optim/adam.py:417-547, decoupled weight decay) over one flat fp32 parameter buffer
 //  * dtype casts and the training-window gather (dataset_single_member.py:168-196)
 #include "common.h"
+#include "cesm_hip.h"
 
 namespace {
 
@@ -282,9 +283,36 @@ __global__ void window_gather_kernel(const float* __restrict__ cond, const float
   }
 }
 
+// One-GPU stand-in for the RCCL all-reduce kernels of an overlapped data-parallel backward (a measurement aid,
+// tools/overlap_sim.py): nblk blocks that each take a whole CU (the launch asks for the CU's full LDS) and idle on the
+// real-time clock (100 MHz) for `ticks`, as an RCCL channel block holds its CU for a bucket's transfer time.
+__global__ __launch_bounds__(64) void hold_cu_kernel(long long ticks) {
+  extern __shared__ char hold_lds[];
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  while ((long long)__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+  if (ticks < 0) hold_lds[threadIdx.x] = 0;  // never taken: keeps the allocation referenced
+}
+
 }  // namespace
 
 extern "C" {
+
+// The header's CESM_ABI_VERSION this library was compiled against (hosts compare it with their own header)
+int cesm_abi_version(void) { return CESM_ABI_VERSION; }
+
+int cesm_hold_cus(int nblk, float usec, hipStream_t stream) {
+  if (nblk < 1 || !(usec >= 0.f)) return CESM_EINVAL;
+  constexpr int kLds = 160 * 1024;
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)hold_cu_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kLds) !=
+        hipSuccess)
+      return CESM_ELAUNCH;
+    attr = true;
+  }
+  hold_cu_kernel<<<nblk, 64, kLds, stream>>>((long long)(usec * 100.f));
+  return cesm_launch_status();
+}
 
 int cesm_sinusoidal(const int64_t* t, float* emb, int B, int dim, hipStream_t stream) {
   sinusoidal_kernel<<<(unsigned)cdiv(B * (dim / 2), 256), 256, 0, stream>>>(t, emb, B, dim);

@@ -7,6 +7,7 @@
 //
 // LayerNorm: video_net.py:78-87 — per voxel over C, biased variance, eps 1e-5, gamma only.
 #include "common.h"
+#include "cesm_hip.h"
 
 namespace {
 

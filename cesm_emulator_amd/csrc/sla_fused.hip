@@ -13,6 +13,7 @@
 //                column i) is fed back as a B operand through the k-slot map
 //                slot (g, j<4) <-> k = 4g + j,  slot (g, 4+j) <-> k = 16 + 4g + j.
 #include "common.h"
+#include "cesm_hip.h"
 
 namespace {
 

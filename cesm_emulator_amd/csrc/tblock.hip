@@ -12,6 +12,7 @@
 // HBM traffic: x in, y out, LN stats and per-(voxel, head) log-sum-exp out — vs ~4 KB/voxel of
 // qkv/o round trips for the unfused path.
 #include "common.h"
+#include "cesm_hip.h"
 
 namespace {
 

@@ -16,6 +16,7 @@
 // selects the AGPR form of the MFMAs, and the score tiles -- consumed by VALU right away -- then cost 4
 // v_accvgpr_read each and share one accumulator quad, serialising the MFMAs behind s_nop waits.
 #include "common.h"
+#include "cesm_hip.h"
 
 namespace {
 

@@ -154,3 +154,50 @@ class GradAllReducer:
         self._armed = None
         if net is not None and getattr(net, "_grad_ready", None) is not None:
             net._grad_ready = None
+
+
+class XgmiModelReducer(GradAllReducer):
+    """One-GPU measurement of the overlapped data-parallel step (a measurement aid, not a training path): the same
+    bucketing, readiness hook and communication stream as GradAllReducer, but each bucket's RCCL all-reduce is
+    replaced by `cesm_hold_cus` -- `cus` blocks that each occupy a whole CU on the communication stream for the
+    bucket's modelled ring all-reduce time on `world` GPUs, 2 (world - 1) / world * bytes / busbw_gbs (xGMI: RCCL's
+    bus bandwidth for large all-reduces on one 8-GPU node).  The gradients are left as they are (scaled by 1.0, the
+    same pre-scale kernel), so the step trains exactly like the 1-GPU step and only the timing differs.
+    tools/overlap_sim.py compares it with the plain step."""
+
+    def __init__(self, world=8, cus=32, busbw_gbs=300.0, bucket_bytes=32 << 20):
+        super().__init__(bucket_bytes=bucket_bytes, use_side_stream=True)
+        self.model_world, self.cus, self.busbw = int(world), int(cus), float(busbw_gbs)
+        self.world = 1 if self.model_world <= 1 else self.model_world  # arms the hook (GradAllReducer.arm)
+        self.issued_us = []
+
+    def bucket_us(self, nbytes):
+        w = self.model_world
+        return 2.0 * (w - 1) / w * nbytes / (self.busbw * 1e3)
+
+    def _issue(self, a, b, streams):
+        from ._lib import call
+        st = self._armed
+        chunk = st["grad"][a:b]
+        comm = self._comm(chunk.device)
+        comm.wait_stream(torch.cuda.current_stream(chunk.device))
+        for s in streams:
+            if s is not None:
+                comm.wait_stream(s)
+        us = self.bucket_us(chunk.numel() * chunk.element_size())
+        self.issued_us.append(us)
+        with torch.cuda.stream(comm):
+            chunk.mul_(1.0)
+            call("cesm_hold_cus", self.cus, float(us), comm.cuda_stream)
+
+    def allreduce_grads(self, flat_grad):
+        """the non-overlapped form: every bucket held on the compute stream after the backward"""
+        from ._lib import call
+        for a, b in self.buckets(flat_grad.numel()):
+            us = self.bucket_us((b - a) * flat_grad.element_size())
+            self.issued_us.append(us)
+            flat_grad[a:b].mul_(1.0)
+            call("cesm_hold_cus", self.cus, float(us), torch.cuda.current_stream(flat_grad.device).cuda_stream)
+
+    def broadcast_params(self, flat_params, src=0):
+        return

@@ -69,6 +69,26 @@ def conv_pack_batch(jobs_dev, njobs, dtype, blocks_per_job=512):
     call("cesm_conv_pack_batch", _DT[dtype], P(jobs_dev), int(njobs), int(blocks_per_job), S())
 
 
+_QUEUES = {}
+
+
+def work_queue():
+    """the caller-owned int32[2] work counter of the persistent convs' dynamic item claiming (cesm_conv_fwd's queue):
+    one per (device, stream) -- launches on one stream run in order, so they share it; the kernels leave it zero.
+    CESM_CONV_STATIC=1 passes null (static item split)."""
+    if STATIC_CONV:
+        return 0
+    st = torch.cuda.current_stream()
+    key = (st.device.index, st.cuda_stream)
+    q = _QUEUES.get(key)
+    if q is None:
+        q = _QUEUES[key] = torch.zeros(4, dtype=torch.int32, device=st.device)
+    return q.data_ptr()
+
+
+STATIC_CONV = os.environ.get("CESM_CONV_STATIC", "0") == "1"
+
+
 def conv_fwd(x1, x2, wp, bias, geom, res=None, res2=None, out_split=None):
     """geom = (Ho, Wo, Cout, KH, KW, S, P, U).  Returns y (or (y1, y2) when out_split=Co1)."""
     Ho, Wo, Cout, KH, KW, St, Pd, U = geom
@@ -86,7 +106,7 @@ def conv_fwd(x1, x2, wp, bias, geom, res=None, res2=None, out_split=None):
     _chk(res, (Nb, Ho, Wo, Co1), x1.dtype)
     _chk(res2, (Nb, Ho, Wo, Cout - Co1), x1.dtype)
     call("cesm_conv_fwd", dtcode(x1), P(x1), P(x2), P(wp), P(bias), P(res), P(res2), P(y1), P(y2), Nb, Hi, Wi, C1,
-         C2, Ho, Wo, Cout, Co1, KH, KW, St, Pd, U, S())
+         C2, Ho, Wo, Cout, Co1, KH, KW, St, Pd, U, work_queue(), S())
     if CONV_TRACE is not None:
         CONV_TRACE.append(("fwd", Nb, Hi, Wi, C1 + C2, Ho, Wo, Cout, KH, KW, St, Pd, U))
     return y1 if y2 is None else (y1, y2)
@@ -115,7 +135,7 @@ def conv_fwd_gn(x1, x2, wp, bias, geom, B, nslot):
     y = empty((Nb, Ho, Wo, Cout), x1.dtype, x1.device)
     part = empty((B, nslot, Cout // 4, 2), torch.float32, x1.device)
     call("cesm_conv_fwd_gn", dtcode(x1), P(x1), P(x2), P(wp), P(bias), P(y), P(part), B, Nb, Hi, Wi, C1, C2, Ho, Wo,
-         Cout, KH, KW, St, Pd, U, S())
+         Cout, KH, KW, St, Pd, U, work_queue(), S())
     if CONV_TRACE is not None:
         CONV_TRACE.append(("fwd", Nb, Hi, Wi, C1 + C2, Ho, Wo, Cout, KH, KW, St, Pd, U))
     return y, part

@@ -26,6 +26,19 @@ extern "C" {
 #define CESM_DT_F32 0
 #define CESM_DT_BF16 1
 
+/* ABI version of this header.  Bumped whenever an entry point's argument list changes; a host binding compares it
+ * with cesm_abi_version() before the first call (cesm_emulator_amd/_lib.py does), so an old header cannot silently
+ * mis-call a newer library.  History:
+ *   4 (round 4): cesm_ln_fwd / cesm_ln_bwd gained (perm_f, perm_hw), cesm_tflash_fwd / cesm_tflash_bwd gained
+ *     qkv_pixel_major — each before the hipStream_t;
+ *   5 (round 5): cesm_abi_version() itself. */
+#define CESM_ABI_VERSION 5
+int cesm_abi_version(void);
+/* Measurement aid, not a training op: nblk blocks that each occupy one whole CU (full LDS) for `usec` microseconds on
+ * `stream` -- the one-GPU stand-in for the RCCL kernels of an overlapped gradient all-reduce (tools/overlap_sim.py,
+ * distributed.XgmiModelReducer). */
+int cesm_hold_cus(int nblk, float usec, hipStream_t stream);
+
 /* ---- convolutions (csrc/conv.hip) -------------------------------------------------------
  * Generic implicit-GEMM conv on MFMA. Replaces nn.Conv3d (1,k,k) at video_net.py:215 (Block.proj),
  * :246 (res_conv), :61-62 (Downsample), nn.ConvTranspose3d at :65-66 (Upsample), the attention
@@ -35,7 +48,7 @@ extern "C" {
  * output channels [0,Co1) go to y1 and [Co1,Cout) to y2. */
 int cesm_conv_fwd(int dtype, const void* x1, const void* x2, const void* wp, const float* bias, const void* res,
                   const void* res2, void* y1, void* y2, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout, int Co1,
-                  int KH, int KW, int S, int P, int U, hipStream_t stream);
+                  int KH, int KW, int S, int P, int U, int* queue, hipStream_t stream);
 /* cesm_conv_fwd (Co1 = Cout, no residual) that also writes the GroupNorm statistics partials of its output
  * y (the Block conv feeding GroupNorm, video_net.py:215-217): gnpart [B][nslot][Cout/4] float2 (sum, sum of
  * squares per channel quad over the pixels of one partial slot), every entry written once, no atomics;
@@ -45,7 +58,7 @@ int64_t cesm_conv_gn_nslot(int dtype, int Nb, int Hi, int Wi, int C1, int C2, in
                            int S, int P, int U, int B);
 int cesm_conv_fwd_gn(int dtype, const void* x1, const void* x2, const void* wp, const float* bias, void* y, float* gnpart,
                      int B, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout, int KH, int KW, int S,
-                     int P, int U, hipStream_t stream);
+                     int P, int U, int* queue, hipStream_t stream);
 /* name of the kernel cesm_conv_fwd launches for these arguments (host-only query, no GPU work; the
  * launcher itself selects through the same function).  "invalid" if cesm_conv_fwd would return EINVAL. */
 const char* cesm_conv_fwd_variant(int dtype, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout,

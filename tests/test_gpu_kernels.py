@@ -845,3 +845,128 @@ def test_tflash_pixel_major_matches_frame_major(dev, F, HW, B):
     torch.cuda.synchronize()
     assert rel(from_pm(dqkv_pm).float(), dqkv.float()) < 1e-2
     assert rel(dt_pm, dt) < 1e-3
+
+
+# ------------------------------------------------------------------ non-finite propagation (-fno-honor-nans)
+# The attention sources are built without NaN semantics (cesm_emulator_amd/build.py NO_NANS): the compiler may treat
+# fmaxf / comparisons as NaN-free.  The hardware arithmetic still propagates a NaN, and these tests pin that a NaN
+# entering the attention kernels leaves them non-finite -- crossing frames (temporal) and pixels (spatial) through the
+# attention mixing itself, not only along the residual -- so the reference's guard (train.py:860-861: a non-finite
+# loss skips the step) still sees it.
+def _nan_at(x, idx):
+    x = x.clone()
+    x[idx] = float("nan")
+    return x
+
+
+def test_nan_crosses_frames_in_fused_temporal_block(dev):
+    """cesm_tblock_fwd_fold / cesm_tblock_bwd_dw (C = 64, F = 12): a NaN in x at one voxel makes y non-finite at every
+    frame of that pixel (the softmax over frames mixes it in) and nowhere else; a NaN in dy at one voxel makes dx
+    non-finite at every frame of that pixel and the weight gradient non-finite"""
+    C, B, Fr, H, W = 64, 2, 12, 8, 12
+    torch.manual_seed(5)
+    rot_mod = VN.RotaryEmbedding(32)
+    res_mod = VN.Residual(VN.PreNorm(C, VN.EinopsToAndFrom(VN.Attention(C, 8, 32, rot_mod)))).to(dev)
+    attn = res_mod.fn.fn.fn
+    rc = make_rc(B, Fr, torch.bfloat16)
+    rc.bias = K.relpos_fwd(torch.randn(32, 8).to(dev), Fr)
+    rc.rot = K.rope_table(rot_mod.freqs.to(dev), Fr)
+    wqkv = attn.to_qkv.weight.detach().contiguous()
+    wout = attn.to_out.weight.detach()
+    wo = K.conv_pack(wout, torch.bfloat16, C, 256, 1, 1, 0, 0)
+    wo_t = K.conv_pack(wout, torch.bfloat16, 256, C, 1, 1, 1, 1)
+    gamma = res_mod.fn.norm.gamma.detach().reshape(-1).contiguous()
+    x = torch.randn(B, C, Fr, H, W)
+    g = torch.randn(B, C, Fr, H, W)
+    b0, f0, h0, w0 = 1, 4, 3, 7
+    xd = to_cl(_nan_at(x, (b0, slice(None), f0, h0, w0))).to(dev, torch.bfloat16)
+    y, mr, lse, _ = K.tblock_fwd_fold(xd, gamma, wqkv, wo, rc.bias, rc.rot, B, Fr, attn.scale)
+    torch.cuda.synchronize()
+    fin = torch.isfinite(from_cl(y, B).float().cpu()).all(dim=1)          # [B, F, H, W]
+    assert not fin[b0, :, h0, w0].any(), "a NaN at one frame must reach every frame of its pixel"
+    fin[b0, :, h0, w0] = True
+    assert fin.all(), "the NaN leaked to other pixels"
+    # backward: clean forward, NaN in dy at one voxel
+    xd = to_cl(x).to(dev, torch.bfloat16)
+    y, mr, lse, _ = K.tblock_fwd_fold(xd, gamma, wqkv, wo, rc.bias, rc.rot, B, Fr, attn.scale)
+    gd = to_cl(_nan_at(g, (b0, slice(None), f0, h0, w0))).to(dev, torch.bfloat16)
+    dgamma = torch.zeros(C, device=dev)
+    dtable = torch.zeros(32, 8, device=dev)
+    dwq = torch.zeros(768, C, device=dev)
+    dx = K.tblock_bwd_dw(xd, gd, mr, lse, wqkv, gamma, wo_t, rc.bias, rc.rot, dwq, dgamma, dtable, B, Fr, attn.scale)
+    torch.cuda.synchronize()
+    fin = torch.isfinite(from_cl(dx, B).float().cpu()).all(dim=1)
+    assert not fin[b0, :, h0, w0].any()
+    fin[b0, :, h0, w0] = True
+    assert fin.all()
+    assert not torch.isfinite(dwq).all() and not torch.isfinite(dgamma).all()
+
+
+def test_nan_crosses_pixels_in_fused_sla_block(dev):
+    """cesm_slaf_fwd / cesm_slaf_bwd_dw (C = 64): a NaN in x at one pixel of a frame makes y non-finite over that whole
+    frame (the context sums every pixel's k v^T) and in no other frame; a NaN in dy at one pixel does the same to dx"""
+    C, B, Fr, H, W = 64, 1, 3, 12, 20
+    torch.manual_seed(6)
+    res = _sla_block(C, dev)
+    sla = res.fn.fn
+    wqkv = sla.to_qkv.weight.detach().reshape(768, C).contiguous()
+    wout = sla.to_out.weight.detach().reshape(C, 256)
+    wo = K.conv_pack(wout, torch.bfloat16, C, 256, 1, 1, 0, 0)
+    wo_t = K.conv_pack(wout, torch.bfloat16, 256, C, 1, 1, 1, 1)
+    gamma = res.fn.norm.gamma.detach().reshape(-1).contiguous()
+    ones = torch.ones(C, device=dev)
+    wq_fold = K.pack_scaled(wqkv, gamma)
+    x = torch.randn(B, C, Fr, H, W)
+    g = torch.randn(B, C, Fr, H, W)
+    f0, h0, w0 = 1, 5, 11
+    xd = to_cl(_nan_at(x, (0, slice(None), f0, h0, w0))).to(dev, torch.bfloat16)
+    y, st = K.slaf_fwd(xd, ones, wq_fold, wo, sla.to_out.bias.detach(), sla.scale)
+    torch.cuda.synchronize()
+    fin = torch.isfinite(from_cl(y, B).float().cpu()).all(dim=1)[0]       # [F, H, W]
+    assert not fin[f0].any(), "a NaN at one pixel must reach every pixel of its frame"
+    assert fin[[f for f in range(Fr) if f != f0]].all()
+    xd = to_cl(x).to(dev, torch.bfloat16)
+    y, st = K.slaf_fwd(xd, ones, wq_fold, wo, sla.to_out.bias.detach(), sla.scale)
+    gd = to_cl(_nan_at(g, (0, slice(None), f0, h0, w0))).to(dev, torch.bfloat16)
+    dwq = torch.zeros(768, C, device=dev)
+    dgamma = torch.zeros(C, device=dev)
+    dx = K.slaf_bwd_dw(xd, gd, ones, wq_fold, wqkv, gamma, wo_t, st, dwq, dgamma, sla.scale)
+    torch.cuda.synchronize()
+    fin = torch.isfinite(from_cl(dx, B).float().cpu()).all(dim=1)[0]
+    assert not fin[f0].any()
+    assert fin[[f for f in range(Fr) if f != f0]].all()
+    assert not torch.isfinite(dwq).all()
+
+
+@pytest.mark.parametrize("F", [12, 120])
+def test_nan_crosses_frames_in_long_window_core(dev, F):
+    """the MFMA long-window core (tflash, F <= 128): a NaN in one (pixel, frame) qkv row makes that pixel's output
+    non-finite at every frame and leaves other pixels finite; a NaN in dout does the same to dqkv"""
+    B, HW = 1, 37
+    torch.manual_seed(F)
+    scale = 32 ** -0.5
+    freqs = 1.0 / (10000 ** (torch.arange(0, 32, 2).float() / 32))
+    bias = K.relpos_fwd(torch.randn(32, 8).to(dev), F)
+    rot = K.rope_table(freqs.to(dev), F)
+    qkv = torch.randn(B * F * HW, 768)
+    f0, p0 = F // 3, 17
+    row = f0 * HW + p0                                                    # frame-major rows [B][F][HW]
+    bad = qkv.clone()
+    bad[row] = float("nan")
+    out, lse = K.tattn_fwd(bad.to(dev, torch.bfloat16), bias, rot, B, F, HW, scale)
+    torch.cuda.synchronize()
+    fin = torch.isfinite(out.float().cpu()).all(dim=1).view(F, HW)
+    assert not fin[:, p0].any()
+    fin[:, p0] = True
+    assert fin.all()
+    qd = qkv.to(dev, torch.bfloat16)
+    out, lse = K.tattn_fwd(qd, bias, rot, B, F, HW, scale)
+    g = torch.randn(B * F * HW, 256)
+    g[row] = float("nan")
+    dqkv = K.tattn_bwd(qd, out, g.to(dev, torch.bfloat16), lse, bias, rot, torch.zeros(32, 8, device=dev),
+                       B, F, HW, scale)
+    torch.cuda.synchronize()
+    fin = torch.isfinite(dqkv.float().cpu()).all(dim=1).view(F, HW)
+    assert not fin[:, p0].any()
+    fin[:, p0] = True
+    assert fin.all()

@@ -161,6 +161,47 @@ def _concurrent_case(dev, Nb, H, W, var):
             assert torch.equal(outs[i], ref[i]), (rep, i)
 
 
+@pytest.mark.parametrize("gn,with_res", [(False, False), (False, True), (True, False)])
+def test_conv3x3ws_dynamic_claim_bit_exact(dev, monkeypatch, gn, with_res):
+    """the warp-specialized level-0 conv claiming its items from the caller-owned counter (cesm_conv_fwd's queue,
+    ABI 5) gives the static split's bits -- plain, with the fused residual, and the GroupNorm-partial variant --
+    also while 48 CUs are held by cesm_hold_cus on another stream (the stand-in for RCCL's kernels during an
+    overlapped backward), and leaves the counter zero after every launch"""
+    Nb, H, W, C = 24, 96, 288, 64
+    geom = (H, W, C, 3, 3, 1, 1, 1)
+    assert K.conv_fwd_variant(BF, Nb, H, W, C, 0, H, W, C, C, 3, 3, 1, 1, 1) == L0_WS
+    torch.manual_seed(33)
+    x = torch.randn(Nb, H, W, C, device=dev).to(BF)
+    w = K.conv_pack(torch.randn(C, C, 3, 3, device=dev) * 0.05, BF, C, C, 3, 3, False, False)
+    b = torch.randn(C, device=dev)
+    r = torch.randn(Nb, H, W, C, device=dev).to(BF) if with_res else None
+    B = 4
+    nslot = K.conv_gn_nslot(x, None, geom, B) if gn else 0
+
+    def launch():
+        if gn:
+            return K.conv_fwd_gn(x, None, w, b, geom, B, nslot)
+        return (K.conv_fwd(x, None, w, b, geom, res=r), None)
+
+    monkeypatch.setattr(K, "STATIC_CONV", True)
+    y_ref, p_ref = launch()
+    torch.cuda.synchronize()
+    monkeypatch.setattr(K, "STATIC_CONV", False)
+    side = torch.cuda.Stream(device=dev)
+    for rep in range(3):
+        if rep == 2:  # CUs held while the conv runs: its blocks start late or not at all on those CUs
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                K.call("cesm_hold_cus", 48, 3000.0, side.cuda_stream)
+        y, p = launch()
+        torch.cuda.synchronize()
+        assert torch.equal(y, y_ref), rep
+        if gn:
+            assert torch.equal(p, p_ref), rep
+        q = K._QUEUES[(dev.index if dev.index is not None else 0, torch.cuda.current_stream().cuda_stream)]
+        assert int(q[0]) == 0 and int(q[1]) == 0, q
+
+
 # ------------------------------------------------------------------ GroupNorm statistics from the conv epilogue
 @pytest.mark.parametrize("nslot, C", [(9000, 64), (28805, 128), (6048, 64)])
 def test_gn_stats_part_two_stage(dev, nslot, C):

@@ -118,6 +118,35 @@ def test_nonfinite_step_is_skipped_and_not_counted(dev):
     assert float(opt.state_dict()["state"][0]["step"]) == 1.0
 
 
+def test_nan_in_cond_skips_bf16_train_step(dev):
+    """the reference's guard (train.py:860-861) on the production path: a NaN at ONE pixel of one frame of `cond`
+    in a bf16 train_step (more_blocks mults, F = 12, 64 x 96: the fused level-0 attention kernels, built without
+    NaN semantics, build.py NO_NANS) must surface as a non-finite loss, skip the AdamW step on device and leave
+    every parameter and the optimizer state untouched; the next clean step then trains normally"""
+    torch.manual_seed(3)
+    net = UNet(ch_mults=(1, 2, 4, 8)).to(dev)
+    net.compute_dtype = torch.bfloat16
+    d = Diffusion(net).to(dev)
+    opt = FusedAdamW(d.parameters(), lr=1e-3, max_grad_norm=1.0)
+    g = torch.Generator().manual_seed(9)
+    x0 = torch.randn(1, 1, 64, 96, generator=g).to(dev)
+    cond = torch.randn(1, 1, 12, 64, 96, generator=g).to(dev)
+    t = torch.randint(0, 1000, (1,), generator=g).to(dev)
+    noise = torch.randn(1, 1, 64, 96, generator=g).to(dev)
+    bad = cond.clone()
+    bad[0, 0, 7, 40, 13] = float("nan")
+    before = opt.flat.data.clone()
+    loss = train_step(d, opt, x0, bad, 1.0, t=t, noise=noise)
+    torch.cuda.synchronize()
+    assert not torch.isfinite(loss).all(), float(loss)
+    assert opt.step_count == 0 and torch.equal(opt.flat.data, before)
+    assert opt.state_dict()["state"] == {}
+    loss = train_step(d, opt, x0, cond, 1.0, t=t, noise=noise)
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss).all() and opt.step_count == 1
+    assert torch.isfinite(opt.flat.data).all() and not torch.equal(opt.flat.data, before)
+
+
 def test_two_forwards_then_one_backward(dev):
     """each forward's autograd node owns its backward tape: (loss(a) + loss(b)).backward() == the sum of
     the separate gradients, and l1.backward() after a second forward replays l1's activations"""
