@@ -285,7 +285,9 @@ __global__ __launch_bounds__(256) void slaf_combine_kernel(const float* __restri
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const float zd = sZ[d0 + i];
-    const float c = zd > 0.f ? U[i] / zd : 0.f;
+    // Z >= 1 for every frame (the maximum's own term is exp(0)); no guard: a `Z > 0 ?` select turned a NaN Z into a
+    // zero context (a NaN at one pixel vanished from the frame instead of reaching every pixel, as in the reference)
+    const float c = U[i] / zd;
     sc[d0 + i][e] = c;
     ctx32[((int64_t)nh * 32 + d0 + i) * 32 + e] = c;
   }

@@ -14,6 +14,7 @@
 #   envab:<ENV=a|ENV=b|..>     whole-step A/B over environment settings ("-" = default), twice
 #   tb:<v1,v2,..>              fused attention block micro-timing (tools/tblock_time.py), default vs variants
 #   py:<script args..>         any tools/ python script (spaces as '+'), e.g. py:ws_check.py
+#   run:<name>:<cmd..>         any command (spaces as '+') with a 600 s limit -> gpurun_out/<tag>_<name>.txt
 # Extra bench arguments for ab/envab/prof/calls: BENCH_ARGS="--frames 120 --batch 1" tools/gpu_call.sh ...
 set -e
 tag=$1; shift
@@ -100,6 +101,10 @@ for step in "$@"; do
     py)
       timeout -k 10 400 python3 tools/${arg//+/ } > "gpurun_out/${tag}_$(echo "${arg%%+*}" | tr -c 'a-zA-Z0-9_\n' _).txt" 2>&1
       tail -5 "gpurun_out/${tag}_$(echo "${arg%%+*}" | tr -c 'a-zA-Z0-9_\n' _).txt";;
+    run)
+      name=${arg%%:*}; cmd=${arg#*:}
+      timeout -k 10 600 ${cmd//+/ } > "gpurun_out/${tag}_${name}.txt" 2>&1
+      tail -3 "gpurun_out/${tag}_${name}.txt";;
     *) echo "unknown step $step"; exit 2;;
   esac
 done
