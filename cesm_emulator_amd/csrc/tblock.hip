@@ -1704,6 +1704,16 @@ constexpr int TWH_PG = 1;
 #ifndef TWH_DO_PF
 #define TWH_DO_PF 1  // twh_bwd: the dO GEMM's weights issued during the last q/k/v batch (needs QKV_PIPE)
 #endif
+// the DWO instantiation (in-kernel dW_out, 32 more accumulators) trades prefetch registers for them:
+#ifndef TWH_QB_DWO
+#define TWH_QB_DWO 1     // q/k/v weight tiles per prefetch batch (2 in the plain kernel)
+#endif
+#ifndef TWH_DO_PF_DWO
+#define TWH_DO_PF_DWO 0  // dO weights prefetched during the last q/k/v batch
+#endif
+#ifndef TWH_WPIPE_DWO
+#define TWH_WPIPE_DWO 0  // the dxn GEMM's weight ring
+#endif
 constexpr int TH_XLD = 72;   // xhat / dy tile row stride (bf16, 144-B rows)
 constexpr int TH_NVMAX = 3;  // voxel tiles per group (4*F <= 48): the 8 slices then fit in LDS
 // twh_bwd keeps round 2's padded tiles (80-B slice rows, 144-B xhat / dy rows, 68-float partial rows): the region
@@ -1716,14 +1726,21 @@ constexpr int TWH_PLD = 68;  // fp32 row stride of a wave's partial dxn rows (wr
 // pixel read up to (PW-1)F + 16 - R <= 12 rows past dO (F = 4), which must be finite (the next wave's region may
 // still hold fp32 partial rows)
 #define TWH_WSTRIDE(R) (4 * (R) * HLD + 16 * HLD)
-static size_t twh_smem(int F, int NV) {
+static size_t twh_smem(int F, int NV, bool dwo) {
   (void)F;
   const int R = NV * 16;
-  return (size_t)16 * RS * 4 + (size_t)8 * TWH_PG * 2 * 256 * 2 + (size_t)2 * R * TH_XLD * 2 +
+  return (size_t)16 * RS * 4 + (size_t)8 * TWH_PG * 2 * 256 * 2 + (size_t)(2 * R + (dwo ? 16 : 0)) * TH_XLD * 2 +
          (size_t)8 * TWH_WSTRIDE(R) * 2;
 }
 
-template <int NV>
+// DWO (round 5): the to_out weight gradient in-kernel too.  Per pixel and head, O_h = P V_h (A = P straight from the
+// softmax registers, B = V through the k-slot read) comes out of the MFMA in exactly the B layout of
+// dW_out[:, h] += dy^T O_h (A = dy^T from the block's dy tile by the transposed read), so neither the forward's
+// 256-channel O (512 B per voxel written, then re-read by a wide weight-gradient GEMM with dy) nor an LDS round trip
+// is needed: 10 K = 16 MFMAs and 32 accumulator registers per wave.  Rows of O_h past the pixel's F frames are 0
+// (P is 0 there), so the dy rows the transposed read takes past them (the next pixel's, or the zeroed 16-row pad
+// after the tile) contribute nothing.
+template <int NV, bool DWO>
 __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ dy, const float* __restrict__ mr,
     const float* __restrict__ lse, const bf16* __restrict__ wqkv, const bf16* __restrict__ wqkv_t,
@@ -1739,8 +1756,8 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
   float* rot = smem;                                 // [16][RS]
   float* trbuf = rot + 16 * RS;                      // [8 waves][TWH_PG][2][16][16] bf16 P / dS tiles
   bf16* xt = reinterpret_cast<bf16*>(trbuf) + 8 * TWH_PG * 2 * 256;  // [R][TH_XLD] xhat (bf16)
-  bf16* dyt = xt + R * TH_XLD;                       // [R][TH_XLD] dy
-  bf16* slices = dyt + R * TH_XLD;                   // 8 x [q|k|v|dO][R][HLD]
+  bf16* dyt = xt + R * TH_XLD;                       // [R][TH_XLD] dy (+ a 16-row zero pad with DWO)
+  bf16* slices = dyt + (R + (DWO ? 16 : 0)) * TH_XLD;  // 8 x [q|k|v|dO][R][HLD]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const int h = wid;
@@ -1749,8 +1766,10 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
   bf16* sv = sk + R * HLD;
   bf16* sdo = sv + R * HLD;
   for (int e = tid; e < F * 32; e += 512) rot[(e >> 5) * RS + (e & 31)] = rotg[e];
-  // the wave's 16-row pad past dO (never written afterwards: the partial rows fit over the slices)
+  // the wave's 16-row pad past dO (never written afterwards: the partial rows fit over the slices), the dy tile's pad
   for (int e = lane; e < 8 * HLD; e += 64) reinterpret_cast<float*>(sq + 4 * R * HLD)[e] = 0.f;
+  if constexpr (DWO)
+    for (int e = tid; e < 8 * TH_XLD; e += 512) reinterpret_cast<float*>(dyt + R * TH_XLD)[e] = 0.f;
   // this wave's (head's) bias entries, log2 units: transposed (i = lr, j = 4g + r) and row-major (i = 4g + r, j = lr)
   float bt[4], brm[4];
 #pragma unroll
@@ -1802,6 +1821,10 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
 #pragma unroll
     for (int n = 0; n < 4; ++n) dwacc[m][n] = z4;
   float dbacc[4] = {0.f, 0.f, 0.f, 0.f};
+  // DWO: dW_out[c = ct * 16 + 4 lg + r][h * 32 + half * 16 + lr]
+  f32x4 dwo[DWO ? 4 : 1][2];
+#pragma unroll
+  for (int ct = 0; ct < (DWO ? 4 : 1); ++ct) dwo[ct][0] = dwo[ct][1] = z4;
 
   prefetch(blockIdx.x);
   TW_ST_DECL
@@ -1829,14 +1852,16 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
 #if TWH_QKV_PIPE
     // q/k/v weight fragments in two-tile batches, double-buffered: batch 0 issued before barrier A (its L2
     // latency overlaps the barrier wait), batch c+1 issued before batch c's MFMAs
-    bf16x8 wqa[2][2][T::KS];
+    // (TWH_QB tiles per batch: 2, or 1 -- half the registers, for the DWO instantiation's register budget)
+    constexpr int QB = DWO ? TWH_QB_DWO : 2;
+    bf16x8 wqa[2][QB][T::KS];
 #if TWH_DO_PF
-    bf16x8 wob[2][T::KS];
+    bf16x8 wob[DWO && !TWH_DO_PF_DWO ? 1 : 2][T::KS];
 #endif
-    auto ldq = [&](int c2, int buf) {
+    auto ldq = [&](int c0, int buf) {
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int ct = c2 + u, mt = (ct >> 1) * 16 + h * 2 + (ct & 1);
+      for (int u = 0; u < QB; ++u) {
+        const int ct = c0 + u, mt = (ct >> 1) * 16 + h * 2 + (ct & 1);
 #pragma unroll
         for (int ks = 0; ks < T::KS; ++ks) wqa[buf][u][ks] = ld_img(wq_g, mt, T::KS, ks, lane);
       }
@@ -1863,24 +1888,24 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
         for (int ks = 0; ks < T::KS; ++ks) xf[vt][ks] = ld16(xt + (vt * 16 + lr) * TH_XLD + ks * 32 + lg * 8);
 #if TWH_QKV_PIPE
 #pragma unroll
-      for (int c2 = 0; c2 < 6; c2 += 2) {
-        const int buf = (c2 >> 1) & 1;
-        if (c2 + 2 < 6) ldq(c2 + 2, buf ^ 1);
+      for (int c0 = 0; c0 < 6; c0 += QB) {
+        const int buf = (c0 / QB) & 1;
+        if (c0 + QB < 6) ldq(c0 + QB, buf ^ 1);
 #if TWH_DO_PF
-        else {  // the dO GEMM's W_out^T fragments, in flight during the last q/k/v batch
+        else if (!DWO || TWH_DO_PF_DWO) {  // the dO GEMM's W_out^T fragments, in flight during the last q/k/v batch
 #pragma unroll
           for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
-            for (int ks = 0; ks < T::KS; ++ks) wob[dt][ks] = ld_img(wot_g, h * 2 + dt, T::KS, ks, lane);
+            for (int ks = 0; ks < T::KS; ++ks) wob[DWO && !TWH_DO_PF_DWO ? 0 : dt][ks] = ld_img(wot_g, h * 2 + dt, T::KS, ks, lane);
         }
 #endif
-        const int kind = c2 >> 1;  // the pair (c2, c2 + 1) = both 16-dim halves of one kind
-        bf16* dst = kind == 0 ? sq : (kind == 1 ? sk : sv);
         // batched (round 4), one 16-dim half at a time: the half's RoPE coefficients read first, its NV tiles issued
         // back to back, then their epilogues (round 3: one MFMA -> s_nop -> LDS read -> wait -> VALU -> store chain
         // per tile; both halves at once spill at 256 VGPRs)
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int ub = 0; ub < QB; ++ub) {
+          const int ct = c0 + ub, kind = ct >> 1, u = ct & 1;
+          bf16* dst = kind == 0 ? sq : (kind == 1 ? sk : sv);
           f32x4 cs[NV];
           if (kind < 2) {
 #pragma unroll
@@ -1892,7 +1917,7 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
             qacc[vt] = z4;
 #pragma unroll
             for (int ks = 0; ks < T::KS; ++ks)
-              qacc[vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wqa[buf][u][ks], xf[vt][ks], qacc[vt], 0, 0, 0);
+              qacc[vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wqa[buf][ub][ks], xf[vt][ks], qacc[vt], 0, 0, 0);
           }
 #pragma unroll
           for (int vt = 0; vt < NV; ++vt) {
@@ -1901,7 +1926,6 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
             store4(dst + (vt * 16 + lr) * HLD + u * 16 + lg * 4, o4);
           }
         }
-
       }
 #else
 #error "TWH_QKV_PIPE=0: tw_qkv writes the region layout, twh_bwd reads 80-B rows"
@@ -1915,7 +1939,10 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
 #pragma unroll
       for (int ks = 0; ks < T::KS; ++ks) {
 #if TWH_DO_PF
-        a[ks] = wob[dt][ks];
+        if (!DWO || TWH_DO_PF_DWO)
+          a[ks] = wob[DWO && !TWH_DO_PF_DWO ? 0 : dt][ks];
+        else
+          a[ks] = ld_img(wot_g, h * 2 + dt, T::KS, ks, lane);
 #else
         a[ks] = ld_img(wot_g, h * 2 + dt, T::KS, ks, lane);
 #endif
@@ -1951,7 +1978,7 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
         st[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kr, qr, z4, 0, 0, 0);    // S^T[j][i]
         dpt[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vr, dor, z4, 0, 0, 0);  // dP^T[j][i]
       }
-      s16x4 dst_b[PG];
+      s16x4 dst_b[PG], pa_b[PG];
 #pragma unroll
       for (int u = 0; u < PG; ++u) {
         const bool pix = p0 + pp0 + u < HW;
@@ -2008,6 +2035,7 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
         }
 #endif
         dst_b[u] = __builtin_bit_cast(s16x4, d4);
+        pa_b[u] = __builtin_bit_cast(s16x4, p4);
         // tile[i = lr][j = 4g .. 4g+3]
         *reinterpret_cast<bf16x4*>(trt + (u * 2 + 0) * 256 + lr * 16 + lg * 4) = p4;
         *reinterpret_cast<bf16x4*>(trt + (u * 2 + 1) * 256 + lr * 16 + lg * 4) = d4;
@@ -2018,6 +2046,24 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
 #pragma unroll
         for (int half = 0; half < 2; ++half)
           dqt[u][half] = mfma_k16(kslot4_hld(sk, (pp0 + u) * F, half * 16, lane), dst_b[u], z4);  // dQ'^T[d][i]
+      if constexpr (DWO) {
+#pragma unroll
+        for (int u = 0; u < PG; ++u) {
+          const int rb = (pp0 + u) * F;
+          s16x4 ob[2];
+#pragma unroll
+          for (int half = 0; half < 2; ++half) {
+            const f32x4 oh = mfma_k16(pa_b[u], kslot4_hld(sv, rb, half * 16, lane), z4);  // O_h[i][d]
+            ob[half] = bf16x4_bits(oh[0], oh[1], oh[2], oh[3]);
+          }
+#pragma unroll
+          for (int ct = 0; ct < 4; ++ct) {
+            const s16x4 a = tr4(dyt, TH_XLD, rb, ct * 16, lane);  // dy^T[c][i]
+#pragma unroll
+            for (int half = 0; half < 2; ++half) dwo[ct][half] = mfma_k16(a, ob[half], dwo[ct][half]);
+          }
+        }
+      }
       wave_lds_sync();  // P / dS tiles visible
       f32x4 dkt[PG][2], dvt[PG][2];
 #pragma unroll
@@ -2055,13 +2101,14 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
     }
     wave_lds_sync();
     TW_ST(3)
-#if TWH_WPIPE
-    // the dxn GEMM's W'^T fragments (kind, ct) in a 3-deep ring: the first two in flight during the dW GEMM
-    bf16x8 wring[TWH_RING];
+    // the dxn GEMM's W'^T fragments (kind, ct) in a TWH_RING-deep ring: the first in flight during the dW GEMM
+    constexpr bool WP = DWO ? TWH_WPIPE_DWO : TWH_WPIPE;
+    bf16x8 wring[WP ? TWH_RING : 1];
     auto ldw = [&](int idx) { return ld_img(wqt_g, idx % T::CT, QKV / 32, (idx / T::CT) * 8 + h, lane); };
+    if constexpr (WP) {
 #pragma unroll
-    for (int r = 0; r < TWH_RING - 1; ++r) wring[r] = ldw(r);
-#endif
+      for (int r = 0; r < TWH_RING - 1; ++r) wring[r] = ldw(r);
+    }
     // dW'_h += dqkv_h^T . xhat over the group's voxels (K = voxels, 16 per step; padded rows are zero)
 #pragma unroll
     for (int kk = 0; kk < NV; ++kk) {
@@ -2090,13 +2137,14 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
       const bf16* src = kind == 0 ? sq : (kind == 1 ? sk : sv);
 #pragma unroll
       for (int ct = 0; ct < T::CT; ++ct) {
-#if TWH_WPIPE
-        const int idx = kind * T::CT + ct;
-        if (idx + TWH_RING - 1 < 3 * T::CT) wring[(idx + TWH_RING - 1) % TWH_RING] = ldw(idx + TWH_RING - 1);
-        const bf16x8 a = wring[idx % TWH_RING];
-#else
-        const bf16x8 a = ld_img(wqt_g, ct, QKV / 32, kind * 8 + h, lane);
-#endif
+        bf16x8 a;
+        if constexpr (WP) {
+          const int idx = kind * T::CT + ct;
+          if (idx + TWH_RING - 1 < 3 * T::CT) wring[(idx + TWH_RING - 1) % TWH_RING] = ldw(idx + TWH_RING - 1);
+          a = wring[idx % TWH_RING];
+        } else {
+          a = ld_img(wqt_g, ct, QKV / 32, kind * 8 + h, lane);
+        }
 #pragma unroll
         for (int vt = 0; vt < NV; ++vt)
           dxacc[ct][vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ld16(src + (vt * 16 + lr) * HLD + lg * 8),
@@ -2163,6 +2211,25 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
     const int j = lg * 4 + r;
     if (lr < F && j < F) dbias_part[((int64_t)h * gridDim.x + blockIdx.x) * FF + lr * F + j] = dbacc[r];
   }
+  if constexpr (DWO) {  // dW_out partial of this block: [C][256] after the gridDim.x dW' slabs
+    float* so = dw_slab + (int64_t)gridDim.x * QKV * C + (int64_t)blockIdx.x * C * INNER;
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+      for (int half = 0; half < 2; ++half)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) so[(int64_t)(ct * 16 + lg * 4 + r) * INNER + h * DH + half * 16 + lr] = dwo[ct][half][r];
+  }
+}
+
+// dst (+)= sum over the nblk slabs (fixed order) of [nblk][n] partials
+__global__ void slab_sum_kernel(const float* __restrict__ slab, int nblk, int64_t n, float* __restrict__ dst,
+                                int accumulate) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n) return;
+  float s = 0.f;
+  for (int k = 0; k < nblk; ++k) s += slab[(int64_t)k * n + e];
+  dst[e] = accumulate ? dst[e] + s : s;
 }
 
 
@@ -2300,8 +2367,8 @@ int cesm_tblock_fwd_fold(const void* x, const float* gamma, const float* wqkv_f3
 // B = 1).  Workspaces: slab nblk*768*C floats, tmp 768*C floats, wimg (2*768 + 256)*C bf16.
 int cesm_tblock_bwd_dw(const void* x, const void* dy, const float* mr, const float* lse, const float* wqkv_f32,
                        const float* gamma, const void* wout_t, const float* bias, const float* rot, void* dx,
-                       float* dwqkv, float* dgamma, float* dbias_part, float* slab, float* tmp, void* wimg, int nblk,
-                       int B, int F, int HW, int C, float scale, int accumulate, hipStream_t stream) {
+                       float* dwqkv, float* dgamma, float* dwout, float* dbias_part, float* slab, float* tmp, void* wimg,
+                       int nblk, int B, int F, int HW, int C, float scale, int accumulate, hipStream_t stream) {
   if (nblk < 1 || nblk != cesm_tblock_bwd_dw_nblk(B, F, HW, C)) return CESM_EUNSUPPORTED;
   bf16* iq = (bf16*)wimg;
   bf16* iqt = iq + 768 * C;
@@ -2312,18 +2379,24 @@ int cesm_tblock_bwd_dw(const void* x, const void* dy, const float* mr, const flo
   frag_image_f32_kernel<<<gi, 256, 0, stream>>>(wqkv_f32, gamma, iqt, C, 768, 1, INNER, scale);
   frag_image(wout_t, iot, INNER, C, stream);
   const int nv = (4 * F + 15) / 16;
-  const size_t sm = twh_smem(F, nv);
-#define TWH_LAUNCH(NVv)                                                                                      \
-  allow_smem(twh_bwd_kernel<NVv>, sm);                                                                       \
-  twh_bwd_kernel<NVv><<<nblk, 512, sm, stream>>>((const bf16*)x, (const bf16*)dy, mr, lse, iq, iqt, iot, bias, \
-                                                 rot, (bf16*)dx, slab, dbias_part, B, F, HW, scale)
+  const size_t sm = twh_smem(F, nv, dwout != nullptr);
+#define TWH_LAUNCH(NVv, DWOv)                                                                                     \
+  allow_smem(twh_bwd_kernel<NVv, DWOv>, sm);                                                                      \
+  twh_bwd_kernel<NVv, DWOv><<<nblk, 512, sm, stream>>>((const bf16*)x, (const bf16*)dy, mr, lse, iq, iqt, iot, bias, \
+                                                       rot, (bf16*)dx, slab, dbias_part, B, F, HW, scale)
+  const bool dwo = dwout != nullptr;
   switch (nv) {
-    case 1: TWH_LAUNCH(1); break;
-    case 2: TWH_LAUNCH(2); break;
-    case 3: TWH_LAUNCH(3); break;
+    case 1: if (dwo) { TWH_LAUNCH(1, true); } else { TWH_LAUNCH(1, false); } break;
+    case 2: if (dwo) { TWH_LAUNCH(2, true); } else { TWH_LAUNCH(2, false); } break;
+    case 3: if (dwo) { TWH_LAUNCH(3, true); } else { TWH_LAUNCH(3, false); } break;
     default: return CESM_EUNSUPPORTED;
   }
 #undef TWH_LAUNCH
+  if (dwo) {
+    const int64_t no = (int64_t)C * INNER;
+    slab_sum_kernel<<<(unsigned)cdiv(no, 256), 256, 0, stream>>>(slab + (int64_t)nblk * 768 * C, nblk, no, dwout,
+                                                                 accumulate);
+  }
   const int64_t nel = (int64_t)768 * C;
   twh_dw_reduce_kernel<<<(unsigned)cdiv(nel, 256), 256, 0, stream>>>(slab, nblk, wqkv_f32, gamma, dwqkv, tmp, 768, C,
                                                                     accumulate, INNER, scale);

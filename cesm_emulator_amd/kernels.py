@@ -476,10 +476,11 @@ def tblock_fwd_fold(x, gamma, wqkv_f32, wout, bias, rot, B, F, scale, save=True,
 
 
 def tblock_bwd_dw(x, dy, mr, lse, wqkv_f32, gamma, wout_t, bias, rot, dwqkv, dgamma, dtable, B, F, scale,
-                  num_buckets=32, max_distance=32):
+                  num_buckets=32, max_distance=32, dwout=None):
     """head-parallel fused temporal-block backward with in-kernel weight gradients (C = 64, 4F <= 48):
     returns dx; dwqkv (+)= the to_qkv weight gradient, dgamma (+)= the LN gamma gradient, dtable (+)= the
-    rel-pos table gradient (each nullable).  The forward must be tblock_fwd_fold's."""
+    rel-pos table gradient, dwout [C, 256] (+)= the to_out weight gradient (each nullable; with dwout the forward
+    need not save O).  The forward must be tblock_fwd_fold's."""
     Nb, H, W, C = x.shape
     HW = H * W
     _chk(x, dtype=torch.bfloat16)
@@ -497,11 +498,13 @@ def tblock_bwd_dw(x, dy, mr, lse, wqkv_f32, gamma, wout_t, bias, rot, dwqkv, dga
     dev = x.device
     dx = empty(x.shape, x.dtype, dev)
     dbp = empty((8, nblk, F, F), torch.float32, dev)
-    slab = empty((nblk, 768, C), torch.float32, dev)
+    if dwout is not None:
+        _chk(dwout, (C, 256), torch.float32)
+    slab = empty((nblk * (768 * C + (C * 256 if dwout is not None else 0)),), torch.float32, dev)
     tmp = empty((768, C), torch.float32, dev)
     wimg = empty(((2 * 768 + 256) * C,), torch.bfloat16, dev)
     call("cesm_tblock_bwd_dw", P(x), P(dy), P(mr), P(lse), P(wqkv_f32), P(gamma), P(wout_t), P(bias), P(rot), P(dx),
-         P(dwqkv), P(dgamma), P(dbp), P(slab), P(tmp), P(wimg), nblk, B, F, HW, C, float(scale), 1, S())
+         P(dwqkv), P(dgamma), P(dwout), P(dbp), P(slab), P(tmp), P(wimg), nblk, B, F, HW, C, float(scale), 1, S())
     if dtable is not None:
         ws = empty((8, F, F), torch.float32, dev)
         call("cesm_relpos_bwd", P(dbp), nblk, 1, P(dtable), P(ws), F, 8, num_buckets, max_distance, 1, S())

@@ -396,6 +396,11 @@ def _tblock_fused(rc, C):
 
 # head-parallel backward with in-kernel weight gradients (C = 64, F <= 12): no 768-channel dqkv round trip
 TBLOCK_DW = os.environ.get("CESM_NO_TBLOCK_DW", "0") != "1"
+# ... and, opt-in (CESM_TWH_DWOUT=1, round 5), the to_out weight gradient in that kernel too, so the forward writes no O.
+# Measured slower: the 32 extra accumulators push twh_bwd from 9 to 58-93 spilled registers and 3.3 to 5.3-5.5 ms per
+# level-0 call, more than the O write and the wide weight-gradient GEMM it removes.  Default: the forward
+# saves O for a wide weight-gradient GEMM with dy, as through round 4.
+TWH_DWOUT = os.environ.get("CESM_TWH_DWOUT", "0") == "1"
 
 
 def _tblock_dw(rc, x):
@@ -429,10 +434,11 @@ def tattn_fwd(rc, res_mod, x):
         return K.conv_fwd(v, None, wo, None, (H, W, C, 1, 1, 1, 0, 1), res=x), None
     if _tblock_dw(rc, x):
         # gamma folded into the QKV weights (images built from the fp32 master weight); the backward computes
-        # the to_qkv and gamma gradients in-kernel.  O is always saved for the to_out weight gradient.
+        # the to_qkv and gamma gradients in-kernel, and with TWH_DWOUT the to_out gradient too (no O saved).
         wo = rc.packed(attn.to_out.weight, C, 256, 1, 1, 0, 0)
         y, mr, lse, o = K.tblock_fwd_fold(x, _flat(pre.norm.gamma), attn.to_qkv.weight, wo, rc.bias, rc.rot, rc.B,
-                                          rc.F, attn.scale, save=rc.save, eps=pre.norm.eps, save_o=rc.save)
+                                          rc.F, attn.scale, save=rc.save, eps=pre.norm.eps,
+                                          save_o=rc.save and not TWH_DWOUT)
         st = SimpleNamespace(fused=True, fold=True, x=x, mr=mr, lse=lse, o=o) if rc.save else None
         return y, st
     if _tblock_fused(rc, C):
@@ -465,9 +471,11 @@ def tattn_bwd(rc, res_mod, st, dy):
     if st.fused and st.fold:
         wo_t = rc.packed(attn.to_out.weight, 256, C, 1, 1, 1, 1)
         dwo = gbuf(attn.to_out.weight)
+        in_kernel = st.o is None  # TWH_DWOUT: the forward wrote no O
         dx = K.tblock_bwd_dw(st.x, dy, st.mr, st.lse, attn.to_qkv.weight, _flat(pre.norm.gamma), wo_t, rc.bias, rc.rot,
-                             gbuf(attn.to_qkv.weight), _gflat(pre.norm.gamma), rc.dtable, rc.B, rc.F, attn.scale)
-        if dwo is not None:
+                             gbuf(attn.to_qkv.weight), _gflat(pre.norm.gamma), rc.dtable, rc.B, rc.F, attn.scale,
+                             dwout=dwo.view(C, 256) if in_kernel and dwo is not None else None)
+        if dwo is not None and not in_kernel:
             with rc.side(st.o, dy, attn=True):
                 K.conv_wgrad(st.o, None, dy, None, dwo, (H, W, C, 1, 1, 1, 0, 1), 0, 0)
         return dx

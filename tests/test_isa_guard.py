@@ -25,7 +25,8 @@ OBJDUMP = Path("/opt/rocm/llvm/bin/llvm-objdump")
 PK = re.compile(r"\bv_pk_(?:fma|mul|add)_f32\b")
 FUNC = re.compile(r"^[0-9a-f]+ <(.+)>:$")
 # kernel-name markers of the three NO_SLP sources -> max packed-fp32 instructions over that source's kernels
-LIMITS = {"tblock": (re.compile(r"tw_fwd_kernel|tw_bwd_kernel|twh_bwd_kernel|tblock_\w+_kernel"), 400),
+LIMITS = {"tblock": (re.compile(r"tw_fwd_kernel|tw_bwd_kernel|tblock_\w+_kernel"), 400),
+          "twh": (re.compile(r"twh_bwd_kernel"), 6 * 40),  # TWH_PK: 6 instantiations (NV 1-3 x DWO) x <= 40
           "tflash": (re.compile(r"tflash_(?!bwd_kv_)\w+_kernel"), 0),
           "tflash_kv": (re.compile(r"tflash_bwd_kv_kernel"), 640),  # TF_PK: 8 instantiations x <= 80
           "attn": (re.compile(r"tattn_\w+_kernel|rope_table_kernel"), 0)}

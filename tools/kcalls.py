@@ -16,7 +16,7 @@ def main():
         rows = list(c.execute("select name, start, end from kernels order by start"))
     except sqlite3.OperationalError:
         rows = list(c.execute("select kernel_name, start, end from kernels order by start"))
-    sel = [(re.sub(r"\(.*", "", n).replace("(anonymous namespace)::", "")[:70], (e - s) / 1e3)
+    sel = [(re.sub(r"\(.*", "", n.replace("(anonymous namespace)::", "")).replace("void ", "")[:90], (e - s) / 1e3)
            for n, s, e in rows if pat in n]
     for n, us in sel[-last:]:
         print(f"{us:10.1f} us  {n}")
