@@ -37,11 +37,9 @@ def bump_param_epoch():
 # parameter-gradient GEMM (conv / 1x1 / qkv wgrads, bias column sums, stem wgrad) is enqueued on a second
 # HIP stream ordered after the kernel that produced its inputs.  The wgrads are HBM-bound (the level-0 qkv
 # wgrad streams 4.4 GB) while the dX kernels are MFMA/latency-bound, so the two co-run on the CUs.
-# "0" (default): off, "attn": only the fused attention blocks' wgrads, "1": every wgrad.  "1" measured +1.3 %
-# samples/s on the bench config (130.1 vs 131.8-132.2 ms, profiles/r4_wgrad_stream_ab.txt, allocator counters flat,
-# profiles/r4_wgrad_stream_diag_*.txt) but the same library then ran config/baseline at 964 ms/step and the F = 120
-# leg at 1273 ms/step (7.5x / 5.4x slower, profiles/r4c4_bench.json): round 3's slowdown is config-dependent, so
-# the side stream stays opt-in.
+# "0" (default): off, "attn": only the fused attention blocks' wgrads, "1": every wgrad.  Rounds 3-4 saw 5-8x slower
+# steps with "1" whenever the host ran ahead of the GPU; the cause was the allocator's record_stream reuse rule (see
+# _Side), fixed in round 5.
 WGRAD_STREAM = os.environ.get("CESM_WGRAD_STREAM", "0")
 _WSTREAMS = {}
 
@@ -54,9 +52,15 @@ def _wgrad_stream(device):
 
 
 class _Side:
-    """Context: enqueue on the wgrad stream after everything already on the current stream; the
-    tensors read there are recorded on it so the caching allocator does not hand their memory to
-    the current stream before the wgrad kernels are done."""
+    """Context: enqueue on the wgrad stream after everything already on the current stream.  The tensors read there
+    are kept alive by the run context until rc.join() has made the current stream wait for the wgrad stream; freed
+    after that, their memory can only be reused by work ordered after the wgrad kernels.
+
+    (Round 5: these tensors used to be `record_stream`-ed on the wgrad stream instead.  The caching allocator then
+    reuses such a block only once the recorded event has completed, which it checks when it allocates; with the host
+    running steps ahead of the GPU (no per-step synchronize, as in bench.py) the events are still pending, so every
+    step took fresh segments from hipMalloc -- 171-223 hipMalloc calls over 3-4 steps, ~10 ms each with the device
+    busy: the 5-8x slower steps of rounds 3-4, profiles/r5_wgrad_stream_trace.txt.)"""
 
     def __init__(self, rc, tensors):
         self.rc, self.tensors = rc, tensors
@@ -74,9 +78,7 @@ class _Side:
         if ws is None:
             return False
         self._ctx.__exit__(*exc)
-        for t in self.tensors:
-            if t is not None:
-                t.record_stream(ws)
+        self.rc.keep.extend(t for t in self.tensors if t is not None)
         return False
 
 
@@ -91,6 +93,7 @@ class RunCtx:
         self.dt = None      # grad of the time embedding (allocated in backward)
         self.dtable = None  # grad of the rel-pos embedding table
         self.wstream = None  # weight-gradient stream (set by the backward when WGRAD_STREAM)
+        self.keep = []  # tensors the wgrad stream reads, alive until join()
 
     def packed(self, w, cout, cin, kh, kw, swap, flip):
         return self.net._packed(w, self.cdt, cout, cin, kh, kw, swap, flip)
@@ -99,9 +102,10 @@ class RunCtx:
         return _Side(self if (attn or WGRAD_STREAM == "1") else _NOSIDE, tensors)
 
     def join(self):
-        """current stream waits for every weight gradient enqueued so far"""
+        """current stream waits for every weight gradient enqueued so far; the tensors they read may go after that"""
         if self.wstream is not None:
             torch.cuda.current_stream().wait_stream(self.wstream)
+        self.keep.clear()
 
 
 def gbuf(p):
