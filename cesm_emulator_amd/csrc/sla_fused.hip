@@ -1095,6 +1095,17 @@ constexpr int SH_SLD = 128;  // slice row stride (bf16): raw q|k|v|do (128 cols)
 // rows were 2-way on the fragment and transposed reads (42 % of slah_dx's LDS cycles were conflicts).
 template <int R>
 __device__ __forceinline__ int sl_off(int r, int c) { return rg_off<2>(r, c, R * 16); }
+#ifndef SLAH_DXT
+#define SLAH_DXT 1  // slah_dx: dxn by whole output tiles after a block barrier (round 5); 0 = per-head partials
+#endif
+// SLAH_DXT g rows: the two `do` regions (columns 96..127 = regions 6, 7: 64 R contiguous bytes) of waves 0..3's
+// slices hold R / 4 rows of 256 B each
+template <int R>
+__device__ __forceinline__ int slah_gslot(int v) { return v % (R / 4); }
+template <int R>
+__device__ __forceinline__ float* slah_grow(bf16* slices, int v) {
+  return reinterpret_cast<float*>(slices + (v / (R / 4)) * R * SH_SLD + 6 * R * 16) + slah_gslot<R>(v) * 64;
+}
 
 static size_t slah_smem(int NV) {
   const int R = 16 * NV;
@@ -1343,6 +1354,67 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
           dwacc[m][nt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, bx[nt], dwacc[m][nt], 0, 0, 0);
       }
     }
+#if SLAH_DXT
+    // ---- dxn by whole output tiles (round 5, as twh_bwd's TWH_DXT): after a block barrier wave w computes
+    // g[v][c] = sum over all 768 qkv rows of W'^T[c][k] dqkv[v][k] for channel tile w & 3 and voxel tiles (w >> 2) + 2u,
+    // reading every head's slice; no per-head fp32 partials, 8 accumulator registers instead of 48.  g goes to 256-B
+    // rows in the `do` regions (columns 96..127, free after phase B) of waves 0-3: 16-B unit u of row slot s at u ^ (s & 7).
+    {
+      const int ct = wid & 3, vt0 = wid >> 2;
+      bf16x8 ring[3];
+      auto ldt = [&](int j) { return ld_img(wqt_g, ct, QKV / 32, j, lane); };  // j = kind * 8 + head
+      ring[0] = ldt(0);
+      ring[1] = ldt(1);
+      __syncthreads();  // (B') every head's dq | dk | dv in its slice
+      f32x4 dacc[2] = {z4, z4};
+#pragma unroll
+      for (int j = 0; j < 24; ++j) {
+        if (j + 2 < 24) ring[(j + 2) % 3] = ldt(j + 2);
+        const bf16x8 a = ring[j % 3];
+        const bf16* src = slices + (j & 7) * R * SH_SLD;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int vt = vt0 + 2 * u;
+          if (vt < NV)  // wave-uniform
+            dacc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ld16(src + sl_off<R>(vt * 16 + lr, (j >> 3) * 32 + lg * 8)),
+                                                              dacc[u], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int vt = vt0 + 2 * u;
+        if (vt < NV) {
+          const int v = vt * 16 + lr;
+          float* row = slah_grow<R>(slices, v);
+          *reinterpret_cast<f32x4*>(row + ((ct * 4 + lg) ^ (slah_gslot<R>(v) & 7)) * 4) = dacc[u];
+        }
+      }
+    }
+    __syncthreads();  // (B'') every g row written
+    // ---- LN backward of this thread's pixel chunk
+    {
+      const int v = vv < R ? vv : 0, s7 = slah_gslot<R>(v) & 7;
+      const float* row = slah_grow<R>(slices, v);
+      const f32x4 a0 = *reinterpret_cast<const f32x4*>(row + ((2 * cc) ^ s7) * 4);
+      const f32x4 a1 = *reinterpret_cast<const f32x4*>(row + ((2 * cc + 1) ^ s7) * 4);
+      const float g[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+      const bf16x8 xh = *reinterpret_cast<const bf16x8*>(xt + rg_off<1>(v, cc * 8, xt_rs(R)));
+      const bf16x8 dv = *reinterpret_cast<const bf16x8*>(dyt + rg_off<1>(v, cc * 8, xt_rs(R)));
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { s1 += g[e]; s2 = fmaf(g[e], (float)xh[e], s2); }
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
+      s1 *= 1.f / C;
+      s2 *= 1.f / C;
+      if (vv < R && ok_cur) {
+        bf16x8 o8;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o8[e] = (bf16)(rstd_cur * (g[e] - s1 - (float)xh[e] * s2) + (float)dv[e]);
+        __builtin_nontemporal_store(o8, reinterpret_cast<bf16x8*>(dx + ((int64_t)n * HW + p0 + vv) * C + cc * 8));
+      }
+    }
+#else
     // ---- dxn'_h (this head's share of g = gamma * dxn)
     f32x4 dxacc[CT][NV];
 #pragma unroll
@@ -1405,6 +1477,7 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
         __builtin_nontemporal_store(o8, reinterpret_cast<bf16x8*>(dx + ((int64_t)n * HW + p0 + vv) * C + cc * 8));
       }
     }
+#endif
   }
   float* slab = dw_slab + (int64_t)blockIdx.x * QKV * C;
 #pragma unroll

@@ -13,6 +13,7 @@
 // qkv/o round trips for the unfused path.
 #include "common.h"
 #include "cesm_hip.h"
+#include <type_traits>
 
 namespace {
 
@@ -1726,6 +1727,21 @@ constexpr int TWH_PLD = 68;  // fp32 row stride of a wave's partial dxn rows (wr
 // pixel read up to (PW-1)F + 16 - R <= 12 rows past dO (F = 4), which must be finite (the next wave's region may
 // still hold fp32 partial rows)
 #define TWH_WSTRIDE(R) (4 * (R) * HLD + 16 * HLD)
+#ifndef TWH_DXT
+#define TWH_DXT 1       // dxn by whole output tiles after a block barrier (round 5); 0 = per-head partials (round 2-4)
+#endif
+#ifndef TWH_DXT_RING
+#define TWH_DXT_RING 3  // W'^T fragments in flight in the tiled dxn GEMM
+#endif
+#ifndef TWH_DXT_ONELOOP
+#define TWH_DXT_ONELOOP 1  // the tiled dxn GEMM as one loop with per-MFMA wave-uniform skips (0: one copy per tile count)
+#endif
+// TWH_DXT: fp32 g rows (256 B) in the dO slices of waves 0..3, TWH_GRPR(R) rows per slice
+#define TWH_GRPR(R) ((R) * HLD * 2 / 256)
+__device__ __forceinline__ float* twh_grow(bf16* slices, int R, int v) {
+  const int rpr = TWH_GRPR(R);
+  return reinterpret_cast<float*>(slices + (v / rpr) * TWH_WSTRIDE(R) + 3 * R * HLD) + (v % rpr) * 64;
+}
 static size_t twh_smem(int F, int NV, bool dwo) {
   (void)F;
   const int R = NV * 16;
@@ -2101,96 +2117,212 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
     }
     wave_lds_sync();
     TW_ST(3)
-    // the dxn GEMM's W'^T fragments (kind, ct) in a TWH_RING-deep ring: the first in flight during the dW GEMM
-    constexpr bool WP = DWO ? TWH_WPIPE_DWO : TWH_WPIPE;
-    bf16x8 wring[WP ? TWH_RING : 1];
-    auto ldw = [&](int idx) { return ld_img(wqt_g, idx % T::CT, QKV / 32, (idx / T::CT) * 8 + h, lane); };
-    if constexpr (WP) {
+    if constexpr (TWH_DXT) {
+      // dW'_h += dqkv_h^T . xhat over the group's voxels (K = voxels, 16 per step; padded rows are zero)
 #pragma unroll
-      for (int r = 0; r < TWH_RING - 1; ++r) wring[r] = ldw(r);
-    }
-    // dW'_h += dqkv_h^T . xhat over the group's voxels (K = voxels, 16 per step; padded rows are zero)
+      for (int kk = 0; kk < NV; ++kk) {
+        s16x4 bx[4];
 #pragma unroll
-    for (int kk = 0; kk < NV; ++kk) {
-      s16x4 bx[4];
+        for (int nt = 0; nt < 4; ++nt) bx[nt] = tr4(xt, TH_XLD, kk * 16, nt * 16, lane);
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) bx[nt] = tr4(xt, TH_XLD, kk * 16, nt * 16, lane);
+        for (int m = 0; m < 6; ++m) {
+          const bf16* src = (m >> 1) == 0 ? sq : ((m >> 1) == 1 ? sk : sv);
+          const s16x4 a = tr4(src, HLD, kk * 16, (m & 1) * 16, lane);
 #pragma unroll
-      for (int m = 0; m < 6; ++m) {
-        const bf16* src = (m >> 1) == 0 ? sq : ((m >> 1) == 1 ? sk : sv);
-        const s16x4 a = tr4(src, HLD, kk * 16, (m & 1) * 16, lane);
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt)
-          dwacc[m][nt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, bx[nt], dwacc[m][nt], 0, 0, 0);
+          for (int nt = 0; nt < 4; ++nt)
+            dwacc[m][nt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, bx[nt], dwacc[m][nt], 0, 0, 0);
+        }
       }
-    }
-    TW_ST(4)
-    // dxn'_h^T = W'_qkv[h rows]^T . dqkv_h^T (this head's share; gamma folded: the sum over heads is
-    // g = gamma * dxn), kept in registers, then written as fp32 rows over the wave's own slices
-    f32x4 dxacc[T::CT][NV];
+      TW_ST(4)
+      // dxn by output tiles (round 5, TWH_DXT): after a block barrier every head's dq / dk / dv are in LDS, and wave w
+      // computes whole output tiles g[v][c] = sum over all 768 qkv rows of W'^T[c][k] dqkv[v][k] -- channel tile
+      // w & 3, voxel tiles (w >> 2) + 2u (a SIMD's two waves w, w + 4 share its 3 tiles at NV = 3) -- so no per-head
+      // fp32 partials are written and summed (98 KB of LDS stores per group before), the 48 accumulator registers of
+      // the per-head partial GEMM become 8, and LN backward reads one row instead of eight.  g goes to 256-B rows in
+      // the dO slices of waves 0-3 (not read in this phase), 16-B unit u of row slot s at u ^ (s & 7).
+      const int ct = wid & 3;
+      bf16x8 ring[TWH_DXT_RING];
+      auto ldt = [&](int j) { return ld_img(wqt_g, ct, QKV / 32, j, lane); };  // j = kind * 8 + head
 #pragma unroll
-    for (int ct = 0; ct < T::CT; ++ct)
+      for (int r = 0; r < TWH_DXT_RING - 1; ++r) ring[r] = ldt(r);
+      __syncthreads();  // (B') every head's dq / dk / dv in its slices
+      // the wave's voxel tiles vt0, vt0 + 2 (< NV): one straight-line GEMM per tile count (wave-uniform branch)
+      const int vt0 = wid >> 2;
+      auto tiles = [&](auto NTc) {
+        constexpr int NTL = decltype(NTc)::value;
+        f32x4 dacc[NTL];
 #pragma unroll
-      for (int vt = 0; vt < NV; ++vt) dxacc[ct][vt] = z4;
+        for (int u = 0; u < NTL; ++u) dacc[u] = z4;
 #pragma unroll
-    for (int kind = 0; kind < 3; ++kind) {
-      const bf16* src = kind == 0 ? sq : (kind == 1 ? sk : sv);
+        for (int j = 0; j < 24; ++j) {
+          if (j + TWH_DXT_RING - 1 < 24) ring[(j + TWH_DXT_RING - 1) % TWH_DXT_RING] = ldt(j + TWH_DXT_RING - 1);
+          const bf16x8 a = ring[j % TWH_DXT_RING];
+          const bf16* src = slices + (j & 7) * TWH_WSTRIDE(R) + (j >> 3) * R * HLD;
 #pragma unroll
-      for (int ct = 0; ct < T::CT; ++ct) {
-        bf16x8 a;
-        if constexpr (WP) {
-          const int idx = kind * T::CT + ct;
-          if (idx + TWH_RING - 1 < 3 * T::CT) wring[(idx + TWH_RING - 1) % TWH_RING] = ldw(idx + TWH_RING - 1);
-          a = wring[idx % TWH_RING];
-        } else {
-          a = ld_img(wqt_g, ct, QKV / 32, kind * 8 + h, lane);
+          for (int u = 0; u < NTL; ++u)
+            dacc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ld16(src + ((vt0 + 2 * u) * 16 + lr) * HLD + lg * 8),
+                                                              dacc[u], 0, 0, 0);
         }
 #pragma unroll
-        for (int vt = 0; vt < NV; ++vt)
-          dxacc[ct][vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ld16(src + (vt * 16 + lr) * HLD + lg * 8),
-                                                                  dxacc[ct][vt], 0, 0, 0);
+        for (int u = 0; u < NTL; ++u) {
+          const int v = (vt0 + 2 * u) * 16 + lr, sl = v % TWH_GRPR(R);
+          float* row = twh_grow(slices, R, v);
+          *reinterpret_cast<f32x4*>(row + ((ct * 4 + lg) ^ (sl & 7)) * 4) = dacc[u];
+        }
+      };
+#if TWH_DXT_ONELOOP
+      // one loop, a wave-uniform skip per second-tile MFMA (fewer registers than two inlined copies)
+      {
+        f32x4 dacc[2] = {z4, z4};
+#pragma unroll
+        for (int j = 0; j < 24; ++j) {
+          if (j + TWH_DXT_RING - 1 < 24) ring[(j + TWH_DXT_RING - 1) % TWH_DXT_RING] = ldt(j + TWH_DXT_RING - 1);
+          const bf16x8 a = ring[j % TWH_DXT_RING];
+          const bf16* src = slices + (j & 7) * TWH_WSTRIDE(R) + (j >> 3) * R * HLD;
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int vt = vt0 + 2 * u;
+            if (vt < NV)  // wave-uniform
+              dacc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ld16(src + (vt * 16 + lr) * HLD + lg * 8), dacc[u], 0,
+                                                                0, 0);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int vt = vt0 + 2 * u;
+          if (vt < NV) {
+            const int v = vt * 16 + lr, sl = v % TWH_GRPR(R);
+            float* row = twh_grow(slices, R, v);
+            *reinterpret_cast<f32x4*>(row + ((ct * 4 + lg) ^ (sl & 7)) * 4) = dacc[u];
+          }
+        }
       }
-    }
-    wave_lds_sync();  // every read of this wave's slices done: they now take its partial dxn rows
-    {
-      float* part = reinterpret_cast<float*>(sq);
-#pragma unroll
-      for (int ct = 0; ct < T::CT; ++ct)
-#pragma unroll
-        for (int vt = 0; vt < NV; ++vt)
-          *reinterpret_cast<f32x4*>(part + (vt * 16 + lr) * TWH_PLD + ct * 16 + lg * 4) = dxacc[ct][vt];
-    }
-    TW_ST(5)
-    __syncthreads();  // (B) every head's partial written
+#else
+      const int ntl = vt0 < NV ? (vt0 + 2 < NV ? 2 : 1) : 0;  // wave-uniform
+      if (ntl == 2) {
+        tiles(std::integral_constant<int, 2>{});
+      } else if (ntl == 1) {
+        tiles(std::integral_constant<int, 1>{});
+      }
+#endif
+      TW_ST(5)
+      __syncthreads();  // (B'') every g row written
 
-    // ---- LN backward of this thread's voxel chunk: dx = rstd (g - mean(g) - xhat mean(g xhat)) + dy
-    {
-      const int v = vv < R ? vv : 0;
-      float g[8];
+      // ---- LN backward of this thread's voxel chunk: dx = rstd (g - mean(g) - xhat mean(g xhat)) + dy
+      {
+        const int v = vv < R ? vv : 0, sl = v % TWH_GRPR(R);
+        const float* row = twh_grow(slices, R, v);
+        const f32x4 a0 = *reinterpret_cast<const f32x4*>(row + ((2 * cc) ^ (sl & 7)) * 4);
+        const f32x4 a1 = *reinterpret_cast<const f32x4*>(row + ((2 * cc + 1) ^ (sl & 7)) * 4);
+        const float g[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+        const bf16x8 xh = *reinterpret_cast<const bf16x8*>(xt + v * TH_XLD + cc * 8);
+        const bf16x8 dv = *reinterpret_cast<const bf16x8*>(dyt + v * TH_XLD + cc * 8);
+        float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) g[e] = 0.f;
+        for (int e = 0; e < 8; ++e) { s1 += g[e]; s2 = fmaf(g[e], (float)xh[e], s2); }
 #pragma unroll
-      for (int w = 0; w < 8; ++w) {
-        const float* pw = reinterpret_cast<const float*>(slices + w * TWH_WSTRIDE(R)) + v * TWH_PLD + cc * 8;
-        const f32x4 a0 = *reinterpret_cast<const f32x4*>(pw);
-        const f32x4 a1 = *reinterpret_cast<const f32x4*>(pw + 4);
+        for (int o = 1; o < 8; o <<= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
+        s1 *= 1.f / C;
+        s2 *= 1.f / C;
+        if (vv < R && ok_cur) {
+          bf16x8 o8;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) { g[e] += a0[e]; g[4 + e] += a1[e]; }
+          for (int e = 0; e < 8; ++e) o8[e] = (bf16)(rstd_cur * (g[e] - s1 - (float)xh[e] * s2) + (float)dv[e]);
+          stnt16(dx + vrow(gg, vv) * C + cc * 8, o8);
+        }
       }
-      const bf16x8 xh = *reinterpret_cast<const bf16x8*>(xt + v * TH_XLD + cc * 8);
-      const bf16x8 dv = *reinterpret_cast<const bf16x8*>(dyt + v * TH_XLD + cc * 8);
-      float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) { s1 += g[e]; s2 = fmaf(g[e], (float)xh[e], s2); }
-#pragma unroll
-      for (int o = 1; o < 8; o <<= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
-      s1 *= 1.f / C;
-      s2 *= 1.f / C;
-      if (vv < R && ok_cur) {
-        bf16x8 o8;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o8[e] = (bf16)(rstd_cur * (g[e] - s1 - (float)xh[e] * s2) + (float)dv[e]);
-        stnt16(dx + vrow(gg, vv) * C + cc * 8, o8);
+    } else {
+      // the dxn GEMM's W'^T fragments (kind, ct) in a TWH_RING-deep ring: the first in flight during the dW GEMM
+      constexpr bool WP = DWO ? TWH_WPIPE_DWO : TWH_WPIPE;
+      bf16x8 wring[WP ? TWH_RING : 1];
+      auto ldw = [&](int idx) { return ld_img(wqt_g, idx % T::CT, QKV / 32, (idx / T::CT) * 8 + h, lane); };
+      if constexpr (WP) {
+  #pragma unroll
+        for (int r = 0; r < TWH_RING - 1; ++r) wring[r] = ldw(r);
+      }
+      // dW'_h += dqkv_h^T . xhat over the group's voxels (K = voxels, 16 per step; padded rows are zero)
+  #pragma unroll
+      for (int kk = 0; kk < NV; ++kk) {
+        s16x4 bx[4];
+  #pragma unroll
+        for (int nt = 0; nt < 4; ++nt) bx[nt] = tr4(xt, TH_XLD, kk * 16, nt * 16, lane);
+  #pragma unroll
+        for (int m = 0; m < 6; ++m) {
+          const bf16* src = (m >> 1) == 0 ? sq : ((m >> 1) == 1 ? sk : sv);
+          const s16x4 a = tr4(src, HLD, kk * 16, (m & 1) * 16, lane);
+  #pragma unroll
+          for (int nt = 0; nt < 4; ++nt)
+            dwacc[m][nt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, bx[nt], dwacc[m][nt], 0, 0, 0);
+        }
+      }
+      TW_ST(4)
+      // dxn'_h^T = W'_qkv[h rows]^T . dqkv_h^T (this head's share; gamma folded: the sum over heads is
+      // g = gamma * dxn), kept in registers, then written as fp32 rows over the wave's own slices
+      f32x4 dxacc[T::CT][NV];
+  #pragma unroll
+      for (int ct = 0; ct < T::CT; ++ct)
+  #pragma unroll
+        for (int vt = 0; vt < NV; ++vt) dxacc[ct][vt] = z4;
+  #pragma unroll
+      for (int kind = 0; kind < 3; ++kind) {
+        const bf16* src = kind == 0 ? sq : (kind == 1 ? sk : sv);
+  #pragma unroll
+        for (int ct = 0; ct < T::CT; ++ct) {
+          bf16x8 a;
+          if constexpr (WP) {
+            const int idx = kind * T::CT + ct;
+            if (idx + TWH_RING - 1 < 3 * T::CT) wring[(idx + TWH_RING - 1) % TWH_RING] = ldw(idx + TWH_RING - 1);
+            a = wring[idx % TWH_RING];
+          } else {
+            a = ld_img(wqt_g, ct, QKV / 32, kind * 8 + h, lane);
+          }
+  #pragma unroll
+          for (int vt = 0; vt < NV; ++vt)
+            dxacc[ct][vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ld16(src + (vt * 16 + lr) * HLD + lg * 8),
+                                                                    dxacc[ct][vt], 0, 0, 0);
+        }
+      }
+      wave_lds_sync();  // every read of this wave's slices done: they now take its partial dxn rows
+      {
+        float* part = reinterpret_cast<float*>(sq);
+  #pragma unroll
+        for (int ct = 0; ct < T::CT; ++ct)
+  #pragma unroll
+          for (int vt = 0; vt < NV; ++vt)
+            *reinterpret_cast<f32x4*>(part + (vt * 16 + lr) * TWH_PLD + ct * 16 + lg * 4) = dxacc[ct][vt];
+      }
+      TW_ST(5)
+      __syncthreads();  // (B) every head's partial written
+
+      // ---- LN backward of this thread's voxel chunk: dx = rstd (g - mean(g) - xhat mean(g xhat)) + dy
+      {
+        const int v = vv < R ? vv : 0;
+        float g[8];
+  #pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = 0.f;
+  #pragma unroll
+        for (int w = 0; w < 8; ++w) {
+          const float* pw = reinterpret_cast<const float*>(slices + w * TWH_WSTRIDE(R)) + v * TWH_PLD + cc * 8;
+          const f32x4 a0 = *reinterpret_cast<const f32x4*>(pw);
+          const f32x4 a1 = *reinterpret_cast<const f32x4*>(pw + 4);
+  #pragma unroll
+          for (int e = 0; e < 4; ++e) { g[e] += a0[e]; g[4 + e] += a1[e]; }
+        }
+        const bf16x8 xh = *reinterpret_cast<const bf16x8*>(xt + v * TH_XLD + cc * 8);
+        const bf16x8 dv = *reinterpret_cast<const bf16x8*>(dyt + v * TH_XLD + cc * 8);
+        float s1 = 0.f, s2 = 0.f;
+  #pragma unroll
+        for (int e = 0; e < 8; ++e) { s1 += g[e]; s2 = fmaf(g[e], (float)xh[e], s2); }
+  #pragma unroll
+        for (int o = 1; o < 8; o <<= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
+        s1 *= 1.f / C;
+        s2 *= 1.f / C;
+        if (vv < R && ok_cur) {
+          bf16x8 o8;
+  #pragma unroll
+          for (int e = 0; e < 8; ++e) o8[e] = (bf16)(rstd_cur * (g[e] - s1 - (float)xh[e] * s2) + (float)dv[e]);
+          stnt16(dx + vrow(gg, vv) * C + cc * 8, o8);
+        }
       }
     }
     TW_ST(6)

@@ -73,6 +73,20 @@ def main():
             K.tblock_bwd_dw(x, dy, mrf, lsef, wqkv, gamma, wo_t, bias, rot, dwq, dgamma, dtable, B, F, 32 ** -0.5)
 
         tdw = timed(bwd_dw, reps)
+        # round 5: the in-kernel to_out weight gradient (no O from the forward) vs the O path's forward + wide wgrad
+        dwo = torch.zeros(C, 256, device=dev)
+
+        def bwd_dwo():
+            K.tblock_bwd_dw(x, dy, mrf, lsef, wqkv, gamma, wo_t, bias, rot, dwq, dgamma, dtable, B, F, 32 ** -0.5,
+                            dwout=dwo)
+
+        tdwo = timed(bwd_dwo, reps)
+        tfo = timed(lambda: K.tblock_fwd_fold(x, gamma, wqkv, wo_pack, bias, rot, B, F, 32 ** -0.5, save_o=True), reps)
+        tfn = timed(lambda: K.tblock_fwd_fold(x, gamma, wqkv, wo_pack, bias, rot, B, F, 32 ** -0.5, save_o=False), reps)
+        two = timed(lambda: K.conv_wgrad(of, None, dy, None, dwo, (H, W, C, 1, 1, 1, 0, 1), 0, 0), reps)
+        print(f"fold: fwd with O {tfo:.1f} us, without O {tfn:.1f} us; bwd_dw {tdw:.1f} us + O^T dy wgrad {two:.1f} us "
+              f"= O path {tfo + tdw + two:.1f} us; bwd_dw with in-kernel dW_out {tdwo:.1f} us = {tfn + tdwo:.1f} us",
+              flush=True)
     bout = torch.randn(C, device=dev) * 0.1
 
     def sfwd():
