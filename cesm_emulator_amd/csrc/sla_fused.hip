@@ -1096,7 +1096,8 @@ constexpr int SH_SLD = 128;  // slice row stride (bf16): raw q|k|v|do (128 cols)
 template <int R>
 __device__ __forceinline__ int sl_off(int r, int c) { return rg_off<2>(r, c, R * 16); }
 #ifndef SLAH_DXT
-#define SLAH_DXT 1  // slah_dx: dxn by whole output tiles after a block barrier (round 5); 0 = per-head partials
+#define SLAH_DXT 0  // 1: slah_dx dxn by whole output tiles after a block barrier (round 5: 4.69 -> 5.15 ms per
+                    // call, profiles/r5_dxt_tb.txt); 0 = per-head fp32 partials (round 2-4)
 #endif
 // SLAH_DXT g rows: the two `do` regions (columns 96..127 = regions 6, 7: 64 R contiguous bytes) of waves 0..3's
 // slices hold R / 4 rows of 256 B each

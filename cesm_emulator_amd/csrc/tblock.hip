@@ -1728,7 +1728,8 @@ constexpr int TWH_PLD = 68;  // fp32 row stride of a wave's partial dxn rows (wr
 // still hold fp32 partial rows)
 #define TWH_WSTRIDE(R) (4 * (R) * HLD + 16 * HLD)
 #ifndef TWH_DXT
-#define TWH_DXT 1       // dxn by whole output tiles after a block barrier (round 5); 0 = per-head partials (round 2-4)
+#define TWH_DXT 0       // 1: dxn by whole output tiles after a block barrier (round 5: 3.82 -> 4.35 ms per call,
+                        // profiles/r5_dxt_tb.txt); 0 = per-head fp32 partials (round 2-4)
 #endif
 #ifndef TWH_DXT_RING
 #define TWH_DXT_RING 3  // W'^T fragments in flight in the tiled dxn GEMM
