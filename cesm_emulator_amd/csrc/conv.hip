@@ -491,6 +491,9 @@ __device__ __forceinline__ int h3_off(int row, int ch) { return row * H3_LD + ((
 #ifndef H3_SQ
 #define H3_SQ 1  // A/B knob: 64 co x 64 px wave tiles (0 = 32 co x 128 px, round 2)
 #endif
+#ifndef H3_PRIO
+#define H3_PRIO 0  // A/B knob: s_setprio 1 around a chunk's MFMA phase
+#endif
 #ifndef H3_XCD
 #define H3_XCD 1  // A/B knob: XCD-grouped co blocks of a halo tile (0 = co-block-slowest order)
 #endif
@@ -674,6 +677,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
       for (int j = 0; j < NJ; ++j) fb[b][j] = *reinterpret_cast<const bf16x8*>(sh + boff[j][kx] + ky * H3_P * H3_LD);
     };
     rd(0, 0);
+    if (H3_PRIO) __builtin_amdgcn_s_setprio(1);  // A/B knob: the MFMA phase at priority 1 (the co-resident block stages)
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int b = tap & 1;
@@ -694,6 +698,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
       }
       __builtin_amdgcn_sched_barrier(0);
     }
+    if (H3_PRIO) __builtin_amdgcn_s_setprio(0);
 #else
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
@@ -1637,6 +1642,9 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
 #ifndef WS_TOUCH
 #define WS_TOUCH 1  // L2 touch of the next item's halo lines a step ahead of its stage DMA
 #endif
+#ifndef WS_PRIO
+#define WS_PRIO 0  // A/B knob (see the kernel)
+#endif
 #ifndef WS_RW
 #define WS_RW 1  // resident weights when Cin = 64 and one co block (the level-0 64 -> 64 conv)
 #endif
@@ -1676,6 +1684,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3ws_kernel(const bf16* __restric
   int* qslot = reinterpret_cast<int*>(lds + WS_LDS + 1024);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const bool loader = wid >= 4;  // wave-uniform role
+  // A/B knob WS_PRIO: static s_setprio 1 for the loader waves (1: the second-dispatched half, which loses the VALU
+  // arbitration by age) or for the compute waves (2)
+  if (WS_PRIO && (__builtin_amdgcn_readfirstlane(tid) >= 256) == (WS_PRIO == 1)) __builtin_amdgcn_s_setprio(1);
   const int wl = wid & 3;
   const int lr = lane & 15, lg = lane >> 4;
   const int Cin = g.C1 + g.C2, nchunk = Cin / 32;

@@ -1132,7 +1132,9 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
 #ifndef SLAH_PRIO
 #define SLAH_PRIO 0
 #endif
-  if (SLAH_PRIO && wid >= 4) __builtin_amdgcn_s_setprio(1);  // second-dispatched half (MI355X_MICROARCH §Two waves per SIMD, item 4)
+  // second-dispatched half (MI355X_MICROARCH §Two waves per SIMD, item 4); readfirstlane: a provably wave-uniform
+  // condition (with `wid >= 4` the scalar s_setprio ran unconditionally, in every wave -- the round-3 test was a no-op)
+  if (SLAH_PRIO && __builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
   bf16* sl = slices + wid * R * SH_SLD;
   const int npg = (HW + R - 1) / R;
   const int ngroups = Nf * npg;

@@ -1727,6 +1727,9 @@ constexpr int TWH_PLD = 68;  // fp32 row stride of a wave's partial dxn rows (wr
 // pixel read up to (PW-1)F + 16 - R <= 12 rows past dO (F = 4), which must be finite (the next wave's region may
 // still hold fp32 partial rows)
 #define TWH_WSTRIDE(R) (4 * (R) * HLD + 16 * HLD)
+#ifndef TWH_PRIO
+#define TWH_PRIO 0  // A/B knob: s_setprio 1 for waves 4-7 of twh_bwd
+#endif
 #ifndef TWH_DXT
 #define TWH_DXT 0       // 1: dxn by whole output tiles after a block barrier (round 5: 3.82 -> 4.35 ms per call,
                         // profiles/r5_dxt_tb.txt); 0 = per-head fp32 partials (round 2-4)
@@ -1782,6 +1785,9 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
   bf16* sk = sq + R * HLD;
   bf16* sv = sk + R * HLD;
   bf16* sdo = sv + R * HLD;
+  // static priority for the younger half (waves 4-7; TWH_PRIO A/B knob): the VALU-issue arbitration between the
+  // two waves of a SIMD is by priority, then age (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+  if (TWH_PRIO && __builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
   for (int e = tid; e < F * 32; e += 512) rot[(e >> 5) * RS + (e & 31)] = rotg[e];
   // the wave's 16-row pad past dO (never written afterwards: the partial rows fit over the slices), the dy tile's pad
   for (int e = lane; e < 8 * HLD; e += 64) reinterpret_cast<float*>(sq + 4 * R * HLD)[e] = 0.f;
