@@ -19,7 +19,7 @@ more_blocks net (D ~ 60 tensors on the level-0 path) lands near u*sqrt(D/3) ~ 9e
 and 1.0-1.1e-2 (more_blocks) at 64x96 and at the full 192x288 grid.
 Gradients pass through the forward's stored activations twice (recomputed products and dY chains), so
 per-parameter gradient errors are ~1-4x the forward error (measured median 0.9e-2 / 1.9e-2, worst 2.4e-2 /
-3.9e-2, cosine >= 0.9993 for baseline / more_blocks); the gates below are 2-4x the measured values, to fail
+3.9e-2, cosine >= 0.9993 for baseline / more_blocks); the gates below are 1.4-1.8x the measured values, to fail
 on a wrong gradient (O(1) error) and not on rounding.
 """
 import json
@@ -337,11 +337,15 @@ def _inputs(B, Fr, H, W, seed):
     return x0, cond, t, noise
 
 
-# (gates ~3x the measured worst case; see the module docstring)
-BF16_FWD_GATE = 3e-2
-BF16_GRAD_REL_GATE = 0.15
-BF16_GRAD_MEDIAN_GATE = 4e-2
-BF16_GRAD_COS_GATE = 0.99
+# Gates 1.4-1.8x the measured worst case over every test below (round 5, profiles/r5o_bf16_gates.txt; the inputs are
+# seeded and the kernels bit-repeatable, so the margin covers future changes of rounding order, not noise):
+# forward 1.14e-2 (more_blocks full grid), gradient median 2.12e-2 (more_blocks F = 120), worst gradient 3.61e-2
+# (more_blocks 64 x 96, a level-3 GroupNorm weight), worst cosine 0.99935.  (Rounds 2-4 gated at 3e-2 / 0.15 / 4e-2 /
+# 0.99.)
+BF16_FWD_GATE = 2e-2
+BF16_GRAD_REL_GATE = 6e-2
+BF16_GRAD_MEDIAN_GATE = 3e-2
+BF16_GRAD_COS_GATE = 0.999
 
 
 def _bf16_fwd_bwd(dev, mults, B, Fr, H, W, seed, tag):
