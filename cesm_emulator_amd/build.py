@@ -67,5 +67,22 @@ def build(force: bool = False) -> Path:
     return LIB
 
 
+def build_diag() -> list:
+    """Test-only diagnostic libraries (tools/diag/*.hip -> tools/diag/lib<name>.so): the register / LDS polluters
+    tests/test_gpu_determinism.py runs before the fused kernels.  Not part of libcesm_hip.so."""
+    out = []
+    for src in sorted((ROOT / "tools" / "diag").glob("*.hip")):
+        so = src.with_name(f"lib{src.stem}.so")
+        if not so.exists() or so.stat().st_mtime < src.stat().st_mtime:
+            tmp = so.with_name(f"{so.name}.{os.getpid()}.tmp")
+            cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-shared", "-fPIC", str(src), "-o", str(tmp)]
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr}")
+            os.replace(tmp, so)
+        out.append(so)
+    return out
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv))

@@ -1009,8 +1009,14 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
   for (int e = tid; e < F * 32; e += 256) rot[(e >> 5) * RS + (e & 31)] = rotg[e];
   // tail pad past the last wave's slices: its last pixel's unmasked V gathers read up to 16 - F4 <= 12 rows into it
   for (int e = tid; e < 256; e += 256) reinterpret_cast<float*>(reinterpret_cast<bf16*>(rot + 16 * RS) + 4 * 3 * R * HS)[e] = 0.f;
-  __syncthreads();
   const int p0 = (blockIdx.x * 4 + wid) * T::PW;
+  // a wave without pixels (the last block when cdiv(HW, PW) is not a multiple of 4) zeroes its q rows before it
+  // leaves: the previous wave's last pixel gathers up to 12 rows past its own slices, i.e. into this wave's q rows,
+  // which must be finite (P^T is 0 there, but 0 x a stale Inf / NaN pattern left by an earlier kernel is NaN; found by
+  // tools/vgpr_pollute_check.py at HW = 4: one pixel's y non-finite, depending on the LDS contents)
+  if (p0 >= HW)
+    for (int e = lane; e < R * HS / 8; e += 64) reinterpret_cast<bf16x8*>(sq)[e] = zero8();
+  __syncthreads();
   if (p0 >= HW) return;
   int fr[NV];
 #pragma unroll
@@ -1562,13 +1568,16 @@ static void allow_smem(K kernel, size_t bytes) {
   if (bytes > 65536) (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
+#ifndef TW_SMEM_PAD
+#define TW_SMEM_PAD 0  // diagnostic knob: extra dynamic LDS per tw_fwd block (forces fewer blocks per CU)
+#endif
 template <int C, int NV, bool FOLD = false>
 static void tw_fwd_launch_nv(const void* x, const float* gamma, const void* wqkv, const void* wout, const float* bias,
                              const float* rot, void* y, float* mr, float* lse, void* o, int B, int F, int HW,
                              float scale, float eps, hipStream_t stream) {
   const int npg = (int)cdiv(HW, TW<C>::PW);
   dim3 grid((unsigned)cdiv(npg, 4), B);
-  const size_t sm = tw_fwd_smem<C>(F);
+  const size_t sm = tw_fwd_smem<C>(F) + TW_SMEM_PAD;
   allow_smem(tw_fwd_kernel<C, NV, FOLD>, sm);
   tw_fwd_kernel<C, NV, FOLD><<<grid, 256, sm, stream>>>((const bf16*)x, gamma, (const bf16*)wqkv, (const bf16*)wout,
                                                         bias, rot, (bf16*)y, mr, lse, (bf16*)o, F, HW, scale, eps);
@@ -1727,6 +1736,9 @@ constexpr int TWH_PLD = 68;  // fp32 row stride of a wave's partial dxn rows (wr
 // pixel read up to (PW-1)F + 16 - R <= 12 rows past dO (F = 4), which must be finite (the next wave's region may
 // still hold fp32 partial rows)
 #define TWH_WSTRIDE(R) (4 * (R) * HLD + 16 * HLD)
+#ifndef TWH_POISON
+#define TWH_POISON 0  // diagnostic knob (see twh_bwd_kernel)
+#endif
 #ifndef TWH_PRIO
 #define TWH_PRIO 0  // A/B knob: s_setprio 1 for waves 4-7 of twh_bwd
 #endif
@@ -1772,6 +1784,15 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
   constexpr int R = NV * 16;
   static_assert(TWH_PLD * 4 <= 4 * HLD * 2, "partial dxn rows fit over the wave's slices");
   extern __shared__ __attribute__((aligned(16))) float smem[];
+#if TWH_POISON
+  {  // diagnostic (TWH_POISON = 1: every LDS word NaN, 2: zero) before first use: a read of LDS that this launch has
+     // not written then shows up as a NaN (or as a repeatable value)
+    constexpr int W = (16 * RS * 4 + 8 * TWH_PG * 2 * 256 * 2 + (2 * R + (DWO ? 16 : 0)) * TH_XLD * 2 +
+                       8 * TWH_WSTRIDE(R) * 2) / 4;
+    for (int e = threadIdx.x; e < W; e += 512) reinterpret_cast<unsigned*>(smem)[e] = TWH_POISON == 1 ? 0xffffffffu : 0u;
+    __syncthreads();
+  }
+#endif
   const int FF = F * F;
   float* rot = smem;                                 // [16][RS]
   float* trbuf = rot + 16 * RS;                      // [8 waves][TWH_PG][2][16][16] bf16 P / dS tiles

@@ -5,6 +5,9 @@ bit for bit.  This pins that property for the fused temporal-attention kernels a
 (where a miscompiled packed-fp32 RoPE epilogue once made ~1/3 of the dx rows differ between calls, see
 cesm_emulator_amd/build.py) and for a whole bf16 training step (loss and every parameter gradient).
 """
+import ctypes
+import os
+
 import pytest
 import torch
 
@@ -48,6 +51,51 @@ def test_temporal_block_repeatable(dev, B, H, W):
     for r in outs[1:]:
         for a, b, nm in zip(outs[0], r, ("dx", "dWqkv", "dgamma", "dtable")):
             assert torch.equal(a, b), f"backward {nm} differs between calls ({int((a != b).sum())} elements)"
+
+
+_DIAG = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "diag", "libvgpr_pollute.so")
+
+
+def _polluter():
+    assert os.path.exists(_DIAG), "tools/diag/libvgpr_pollute.so missing: run __graft_entry__.build()"
+    lib = ctypes.CDLL(_DIAG)
+    for fn in (lib.vgpr_pollute, lib.lds_pollute):
+        fn.argtypes = [ctypes.c_uint, ctypes.c_int, ctypes.c_void_p]
+    return lib
+
+
+@pytest.mark.parametrize("B,H,W", [(1, 1, 4), (1, 3, 4), (1, 5, 4), (1, 12, 16), (2, 48, 72)])
+def test_fused_temporal_block_independent_of_stale_state(dev, B, H, W):
+    """The fused temporal forward / backward must not read LDS or registers they have not written: before each call
+    every LDS word of the CUs and every VGPR / AGPR of the waves of a diagnostic kernel (tools/diag) are set to a
+    pattern (quiet NaN, 0, 1.0f, 3.4e38); outputs finite and bit-identical across patterns.  Found in round 5: with
+    cdiv(HW, 4) not a multiple of 4 the last forward block has pixel-less waves, whose unwritten q rows the previous
+    wave's last-pixel V gathers read (0 x a stale NaN); and an SLP-vectorized build of twh_bwd reads stale registers
+    (its outputs change with the register pattern) -- the same symptom as the RoPE-source repeatability failures of
+    rounds 2-3, for which these sources are built without SLP."""
+    F, C = 12, 64
+    pol = _polluter()
+    x, dy, gamma, wqkv, wout, bias, rot = _temporal_inputs(dev, B, F, H, W)
+    wo = K.conv_pack(wout, torch.bfloat16, C, 256, 1, 1, 0, 0)
+    wo_t = K.conv_pack(wout, torch.bfloat16, 256, C, 1, 1, 1, 1)
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    res = []
+    for bits in (0x7FC07FC0, 0, 0x3F800000, 0x7F7F7F7F):
+        torch.cuda.synchronize()
+        assert pol.lds_pollute(bits, 2048, st) == 0 and pol.vgpr_pollute(bits, 8192, st) == 0
+        y, mr, lse, o = K.tblock_fwd_fold(x, gamma, wqkv, wo, bias, rot, B, F, 32 ** -0.5, save_o=True)
+        dwq, dg, dt = torch.zeros(768, C, device=dev), torch.zeros(C, device=dev), torch.zeros(32, 8, device=dev)
+        torch.cuda.synchronize()
+        assert pol.lds_pollute(bits, 2048, st) == 0 and pol.vgpr_pollute(bits, 8192, st) == 0
+        dx = K.tblock_bwd_dw(x, dy, mr, lse, wqkv, gamma, wo_t, bias, rot, dwq, dg, dt, B, F, 32 ** -0.5)
+        torch.cuda.synchronize()
+        res.append((y, mr, lse, o, dx, dwq, dg, dt))
+    names = ("y", "mr", "lse", "o", "dx", "dWqkv", "dgamma", "dtable")
+    for k, r in enumerate(res):
+        for t, nm in zip(r, names):
+            assert torch.isfinite(t.float()).all(), f"pattern {k}: non-finite {nm}"
+        for a, b, nm in zip(res[0], r, names):
+            assert torch.equal(a, b), f"pattern {k}: {nm} depends on stale LDS / register contents"
 
 
 @pytest.mark.parametrize("B,H,W", [(2, 64, 96), (1, 192, 288)])
