@@ -17,11 +17,13 @@ OBJ = ROOT / "build" / "obj"
 LIB = PKG / "libcesm_hip.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-I", str(ROOT / "include")]
-# Sources whose kernels apply RoPE: the SLP vectorizer pairs the rotation's independent fp32 ops into packed
-# v_pk_{mul,fma}_f32 with op_sel / neg modifiers, and those epilogues gave run-to-run different q / k values on
-# gfx950 (identical inputs; ~1/3 of the level-0 dx rows differed between two calls).  Scalar fp32 there is
-# repeatable; the other sources keep the packed forms (their epilogues measured faster with them: conv -7 %,
-# fused SLA forward -18 %) and are covered by the same bit-exact repeat tests (tests/test_gpu_determinism.py).
+# Sources whose kernels apply RoPE: with the SLP vectorizer on, their results changed between identical calls (rounds
+# 2-3: ~1/3 of the level-0 dx rows).  Round 5 found why (tools/vgpr_pollute_check.py, profiles/r5_pollute_slp.txt):
+# the SLP-vectorized twh_bwd reads registers it has not written -- its outputs change with the contents a previous
+# kernel left in the register file -- while the scalar build's do not, for any register / LDS pattern
+# (tests/test_gpu_stale_state.py, tests/test_gpu_determinism.py).  So these sources stay scalar; the other sources keep
+# the packed forms (their epilogues measured faster with them: conv -7 %, fused SLA forward -18 %) and pass the same
+# stale-state tests.
 NO_SLP = {"tblock.hip", "tflash.hip", "attn.hip"}
 # Attention sources: no NaN semantics, so fmaxf after a lane permute (the softmax row maxima) needs no canonicalising
 # v_max per operand (round 4, same-call A/B: SLA backward 4.92 -> 4.68 ms, forward 2.59 -> 2.51 ms at level 0).  Not
