@@ -500,6 +500,80 @@ __device__ __forceinline__ int h3_off(int row, int ch) { return row * H3_LD + ((
 #ifndef H3_BIG
 #define H3_BIG 1  // A/B knob: 448-pixel tiles with 64 co x 112 px wave tiles (0 = 256-pixel tiles, 64 x 64)
 #endif
+// epilogue of the halo conv (conv3x3_bf16_kernel; a function since round 5's double-buffered variant): bias, residual, bf16 stores and the GroupNorm
+// statistics partials; lane holds co = n0 + wr*32 + i*16 + 4*lg + r of pixel pyx[j] (packed (py << 16) | px, -1 past TH)
+template <int NI, int NJ>
+__device__ __forceinline__ void h3_epilogue(const f32x4 (&acc)[NI][NJ], const int (&pyx)[NJ], const ConvGeom& g,
+                                            const float* __restrict__ bias, const bf16* __restrict__ res,
+                                            const bf16* __restrict__ res2, bf16* __restrict__ y1, bf16* __restrict__ y2,
+                                            float* __restrict__ gnp, int gn_fimg, int n, int tt, int ntile, int y0,
+                                            int x0, int n0, int wr, int wc, int lane) {
+  const int lr = lane & 15, lg = lane >> 4;
+  const int Co2 = g.Cout - g.Co1;
+  float bv[NI][4];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) epi_bias(bias, n0 + wr * 32 + i * 16 + lg * 4, bv[i]);
+  int64_t mj[NJ];
+  bool okj[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int oy = y0 + (pyx[j] >> 16), ox = x0 + (pyx[j] & 0xffff);
+    okj[j] = pyx[j] >= 0 && oy < g.Ho && ox < g.Wo;
+    mj[j] = okj[j] ? ((int64_t)n * g.Ho + oy) * g.Wo + ox : 0;
+  }
+  bf16x4 rv[NJ][NI];
+  if (res || res2) {  // uniform
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int i = 0; i < NI; ++i) rv[j][i] = epi_res(res, res2, mj[j], n0 + wr * 32 + i * 16 + lg * 4, g.Co1, Co2, okj[j]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int i = 0; i < NI; ++i) rv[j][i] = bf16x4{};
+  }
+  // GroupNorm statistics partials (gnp: the Block conv feeding a GroupNorm): per channel quad (i, lg) the sum
+  // and sum of squares of the stored bf16 output over this wave's valid pixels
+  float gsum[NI], gsq[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) gsum[i] = gsq[i] = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    if (!okj[j]) continue;
+    const int64_t m = mj[j];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int co = n0 + wr * 32 + i * 16 + lg * 4;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bv[i][r] + b2f(rv[j][i], r);
+      if (gnp) {  // uniform: the statistics of the stored (bf16-rounded) y, which GroupNorm then normalises
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (float)(bf16)v[r];
+      }
+      if (co < g.Co1) store4(y1 + m * g.Co1 + co, v);
+      else store4(y2 + m * Co2 + (co - g.Co1), v);
+      if (gnp) {  // uniform
+        gsum[i] += (v[0] + v[1]) + (v[2] + v[3]);
+        gsq[i] += fmaf(v[3], v[3], fmaf(v[2], v[2], fmaf(v[1], v[1], v[0] * v[0])));
+      }
+    }
+  }
+  if (gnp) {
+    const int b = n / gn_fimg, f = n - b * gn_fimg;
+    constexpr int SPT = 4 / (H3_SQ ? 1 : 2);  // GroupNorm slots per tile (= pixel ranges): h3_gn_slots
+    const int64_t nslot = (int64_t)gn_fimg * ntile * SPT;
+    const int64_t slot = ((int64_t)f * ntile + tt) * SPT + wc;
+    float2* dst = reinterpret_cast<float2*>(gnp) + ((int64_t)b * nslot + slot) * (g.Cout / 4) + (n0 + wr * 32) / 4 + lg;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const float a = row16_sum(gsum[i]), q = row16_sum(gsq[i]);
+      if (lr == 0) dst[i * 4] = make_float2(a, q);
+    }
+  }
+}
+
 // (Round 3: double-buffered chunks at one block per CU measured slower, conv total 64.0 -> 68.2 ms per step: the
 // second co-resident block hides the staging better than an in-block prefetch.  Removed.)
 template <int TW, int NJv = 4>
@@ -716,71 +790,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
     }
 #endif
   }
-  // epilogue: lane holds co = n0 + wr*32 + i*16 + 4*lg + r of pixel (py, px)
-  const int Co2 = g.Cout - g.Co1;
-  float bv[NI][4];
-#pragma unroll
-  for (int i = 0; i < NI; ++i) epi_bias(bias, n0 + wr * 32 + i * 16 + lg * 4, bv[i]);
-  int64_t mj[NJ];
-  bool okj[NJ];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int oy = y0 + (pyx[j] >> 16), ox = x0 + (pyx[j] & 0xffff);
-    okj[j] = pyx[j] >= 0 && oy < g.Ho && ox < g.Wo;
-    mj[j] = okj[j] ? ((int64_t)n * g.Ho + oy) * g.Wo + ox : 0;
-  }
-  bf16x4 rv[NJ][NI];
-  if (res || res2) {  // uniform
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int i = 0; i < NI; ++i) rv[j][i] = epi_res(res, res2, mj[j], n0 + wr * 32 + i * 16 + lg * 4, g.Co1, Co2, okj[j]);
-  } else {
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int i = 0; i < NI; ++i) rv[j][i] = bf16x4{};
-  }
-  // GroupNorm statistics partials (gnp: the Block conv feeding a GroupNorm): per channel quad (i, lg) the sum
-  // and sum of squares of the stored bf16 output over this wave's valid pixels
-  float gsum[NI], gsq[NI];
-#pragma unroll
-  for (int i = 0; i < NI; ++i) gsum[i] = gsq[i] = 0.f;
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    if (!okj[j]) continue;
-    const int64_t m = mj[j];
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const int co = n0 + wr * 32 + i * 16 + lg * 4;
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bv[i][r] + b2f(rv[j][i], r);
-      if (gnp) {  // uniform: the statistics of the stored (bf16-rounded) y, which GroupNorm then normalises
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = (float)(bf16)v[r];
-      }
-      if (co < g.Co1) store4(y1 + m * g.Co1 + co, v);
-      else store4(y2 + m * Co2 + (co - g.Co1), v);
-      if (gnp) {  // uniform
-        gsum[i] += (v[0] + v[1]) + (v[2] + v[3]);
-        gsq[i] += fmaf(v[3], v[3], fmaf(v[2], v[2], fmaf(v[1], v[1], v[0] * v[0])));
-      }
-    }
-  }
-  if (gnp) {
-    const int b = n / gn_fimg, f = n - b * gn_fimg;
-    constexpr int SPT = 4 / (H3_SQ ? 1 : 2);  // GroupNorm slots per tile (= pixel ranges): h3_gn_slots
-    const int64_t nslot = (int64_t)gn_fimg * ntile * SPT;
-    const int64_t slot = ((int64_t)f * ntile + tt) * SPT + wc;
-    float2* dst = reinterpret_cast<float2*>(gnp) + ((int64_t)b * nslot + slot) * (g.Cout / 4) + (n0 + wr * 32) / 4 + lg;
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const float a = row16_sum(gsum[i]), q = row16_sum(gsq[i]);
-      if (lr == 0) dst[i * 4] = make_float2(a, q);
-    }
-  }
+  h3_epilogue<NI, NJ>(acc, pyx, g, bias, res, res2, y1, y2, gnp, gn_fimg, n, tt, ntile, y0, x0, n0, wr, wc, lane);
 }
+
 
 
 // ----------------------------------------------------------------------------------------
