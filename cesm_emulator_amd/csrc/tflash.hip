@@ -948,6 +948,419 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_kv_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------------- backward, fused (round 5)
+// One pass over a (pixel, head) for F > 16 (video_net.py:426-452 differentiated): the two-kernel
+// backward above read q, k, v and dO twice, formed S, dP and exp twice and wrote D through HBM; here one wave reads
+// q, k, v, dO and O once and forms P and dS once per score tile.  Orientation S[q][key] (A = Q' rows, B = K' rows):
+// the MFMA D layout of P and dS (query = 4g + r, key = lane) is directly the B operand of dV^T = dO^T P and
+// dK'^T = Q'^T dS through the k-slot map over a query-tile pair (pack_kslot / tr_pair, as the dk / dv kernel), and
+// dS reaches the dQ product dQ'^T = K'^T dS^T through a 16 x 16 bf16 LDS tile read back transposed.  Key-tile pairs
+// outer (dK / dV of the pair in registers, stored after the pair), query tiles inner, dQ' of every query tile in
+// registers for the pixel (2 NT accumulators).  D_i = dO_i . O_i from the forward's output.
+// Per wave an LDS region (tfb_wave_bytes): Q' and dO rows of the pixel, the current K' pair (then two dS^T tiles), L, D;
+// 64-B rows with 16-B chunk c at c ^ ((row >> 1) & 3): the row-fragment reads, the transposed k-slot reads and the
+// staging stores are bank-conflict free (tools/lds_banks.py model).  Rows past the F staged ones are read only against
+// P = dS = 0 (padded queries: L = 1e30; padded keys: -inf mask); they fall into the next region's finite rows.
+// At F = 120 a block takes 75 KiB: two blocks per CU.
+// Rel-pos bias gradient by diagonal d = kt - qt (offset n = 16 d + lane - 4g - r): |d| <= ND in per-(r, d) registers;
+// beyond, when the host has checked that every offset there falls in the one saturated bucket per sign (num_buckets 32,
+// max_distance 32: |n| >= 27), one accumulator per sign, attributed to offset +-(F - 1) (same bucket, same dtable).
+// Grid (4 * TFB_NB, B): block L -> head pair L & 3 and pixel-pair stream L >> 2; its 4 waves are the 2 pixels x the 2
+// heads, so the two 64-B head halves of every 128-B qkv / dO / O line are read by one CU at about the same time (the
+// first form, one head per block with the 8 heads' blocks on one XCD, fetched 1.5x the algorithmic bytes).
+#ifndef TFB_PF
+#define TFB_PF 0  // A/B knob: the next key pair's K / V rows loaded while the current pair is computed (measured slower: 9.56 vs 8.55 ms at 192x288, F = 120)
+#endif
+#ifndef TFB_DIAG
+#define TFB_DIAG 0  // diagnostic builds only: 1 = every pixel reads pixel 0's rows (L2-resident), 2 = no dq / dk / dv stores
+#endif
+#ifndef TFB_SYNC
+#define TFB_SYNC 0  // A/B knob: wave-scope fences around the LDS round trips of the score loop (1 = round-5 first form)
+#endif
+// A wave's LDS operations execute in issue order (no s_waitcnt is needed between a ds_write and a later ds_read of the
+// same address), and the compiler keeps may-aliasing LDS accesses in program order; the score loop's round trips
+// (K' rows -> transposed reads, dS^T tiles -> transposed reads -> the next tile's stores) therefore need no fence,
+// and without one the compiler can issue the next tile's reads ahead of the current tile's MFMAs.
+__device__ __forceinline__ void tfb_sync() {
+  if (TFB_SYNC) wsync();
+}
+constexpr int TFB_NB = 128;
+template <typename K>
+static void allow_smem(K kernel, size_t bytes) {
+  if (bytes > 65536) (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}  // pixel-group streams (blocks) per (sample, head) = cesm_tflash_nblk
+__host__ __device__ constexpr int tfb_rq(int F) { return (F + 3) & ~3; }
+__host__ __device__ constexpr int tfb_wave_bytes(int F, int NT) {
+  return ((2 * tfb_rq(F) * 64 + 32 * 64 + 2 * 64 * NT) + 255) & ~255;
+}
+// block LDS: the two heads' bias tables (one copy each, 32 NT floats), the RoPE rows of frames 16 a (NT x 32 floats),
+// 4 wave regions
+static size_t tfb_smem(int F, int NT) { return (size_t)(3 * 32 * NT + 16 * 32) * 4 + 4 * (size_t)tfb_wave_bytes(F, NT); }
+__device__ __forceinline__ void rope4_cs(float* v, const float* cs, float scale) {  // R^T of two pairs, times scale
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const float c = cs[2 * u], s = cs[2 * u + 1];
+    const float a = v[2 * u], b = v[2 * u + 1];
+    v[2 * u] = (a * c + b * s) * scale;
+    v[2 * u + 1] = (b * c - a * s) * scale;
+  }
+}
+
+template <int NT, int ND>
+__global__ __launch_bounds__(256, 2) void tflash_bwd_fused_kernel(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
+    const float* __restrict__ lse, const float* __restrict__ bias, const float* __restrict__ rotg,
+    bf16* __restrict__ dqkv, float* __restrict__ part, int F, int HW, float scale, int pm) {
+  constexpr int NP = (NT + 1) / 2;
+  constexpr int NDG = 2 * ND + 1;    // exact diagonals d = kt - qt in [-ND, ND]
+  constexpr bool SAT = ND < NT - 1;  // diagonals beyond: one accumulator per sign
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* rtab = smem;  // [NT][16][2]: RoPE (cos, sin) of frame 16 a
+  float* rbase = smem + 3 * 32 * NT;  // [16][16][2]: RoPE (cos, sin) of frames 0 .. 15
+  // [2][32 NT]: the block's two heads' bias(n) (log2 units) at k = 16 NT - n (rows = queries: n = key - query)
+  float* btabs = smem + 32 * NT;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // block = (head pair, pixel-pair stream); wave = (pixel wid >> 1, head of the pair wid & 1): the two waves of a
+  // pixel read the two 64-B halves of the same 128-B qkv / dO / O lines at the same time (one HBM fetch per line)
+  const int L = blockIdx.x, hp = L & 3, kblk = L >> 2;
+  const int h = 2 * hp + (wid & 1);
+  const int b = blockIdx.y;
+  for (int e = tid; e < 32 * NT; e += 256) rtab[e] = rotg[(e >> 5) * 16 * 32 + (e & 31)];
+  for (int e = tid; e < 16 * 32; e += 256) rbase[e] = rotg[e];
+  for (int e = tid; e < 2 * 32 * NT; e += 256) {
+    const int hh = 2 * hp + e / (32 * NT), n = 16 * NT - e % (32 * NT);
+    float v = 0.f;
+    if (n > -F && n < F) {
+      const int i = n < 0 ? -n : 0, j = i + n;
+      v = bias[((int64_t)hh * F + i) * F + j] * LOG2E;
+    }
+    btabs[e] = v;
+  }
+  const float* btab = btabs + (wid & 1) * 32 * NT;
+  const int RQ = tfb_rq(F);
+  char* Qs = reinterpret_cast<char*>(smem + 3 * 32 * NT + 16 * 32) + wid * tfb_wave_bytes(F, NT);
+  char* Os = Qs + RQ * 64;
+  char* Ks = Os + RQ * 64;
+  // the two dS^T tiles live in the K' rows: those are read (into the dQ A fragments) before the pair's first store
+  char* Tt = Ks;
+  float* Ls = reinterpret_cast<float*>(Ks + 32 * 64);
+  float* Ds = Ls + 16 * NT;
+  for (int e = F + lane; e < 16 * NT; e += 64) {  // padded query rows: P = 0 (and so dS = 0)
+    Ls[e] = TF_LSE_PAD;
+    Ds[e] = 0.f;
+  }
+  __syncthreads();
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  const int lr = lane & 15, g = lane >> 4, q_ = (lane >> 2) & 3, p_ = lane & 3;
+  // row fragment (row lr of a 16-row tile, chunk g), transposed k-slot reads (rows 4g + q_ (+16), 8-B unit p_ of the
+  // 16 columns c0 = 16 t), the dS^T tile's store (row lr, 8-B unit g) and transposed read (row 4g + q_, unit p_)
+  const int frag = lr * 64 + ((g ^ ((lr >> 1) & 3)) << 4);
+  const int trrow = 4 * g + q_;
+  int tro[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) tro[t] = trrow * 64 + (((2 * t + (p_ >> 1)) ^ ((trrow >> 1) & 3)) << 4) + (p_ & 1) * 8;
+  const int tto = lr * 32 + ((g ^ ((lr >> 2) & 3)) << 3);
+  const int tti = trrow * 32 + ((p_ ^ g) << 3);
+  auto trp = [&](const char* base, int s, int t) -> bf16x8 {
+    const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(base + s * 2048 + tro[t]));
+    const s16x4 c = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(base + s * 2048 + 1024 + tro[t]));
+    bf16x8 r;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      r[j] = __builtin_bit_cast(bf16, (short)a[j]);
+      r[4 + j] = __builtin_bit_cast(bf16, (short)c[j]);
+    }
+    return r;
+  };
+  const float* bl0 = btab + 4 * g - lr + 16 * NT;  // + 16 (qt - kt) + r: bias of (query 16 qt + 4g + r, key 16 kt + lr)
+  // RoPE of frame 16 a + lr by angle addition: the (cos, sin) of frame lr (rbase) composed with the row of frame 16 a
+  // (rtab), both block tables in LDS.  (Read per use from the global table, each coefficient load waited behind the
+  // wave's earlier stores -- vmcnt counts loads and stores in order -- and the first version of this kernel stalled.)
+  auto compose = [](const float* base, f32x4 tile, float* cs, int npairs_off) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const float cb = base[npairs_off + 2 * u], sb = base[npairs_off + 2 * u + 1];
+      const float ct = tile[2 * u], st = tile[2 * u + 1];
+      cs[npairs_off + 2 * u] = cb * ct - sb * st;
+      cs[npairs_off + 2 * u + 1] = sb * ct + cb * st;
+    }
+  };
+  const float kmask = 16 * (NT - 1) + lr < F ? 0.f : -INFINITY;  // keys of the last key tile past F
+
+  float dba[4][NDG];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < NDG; ++c) dba[r][c] = 0.f;
+  float dsp = 0.f, dsn = 0.f;
+  const int ngroups = (HW + 1) / 2;
+  const int qfs = pm ? 1 : HW;
+  const int fs_qkv = qfs * QKV * 2, fs_io = HW * INNER * 2;  // 16 rows < 2^31 B: checked on the host
+  const int lo_qkv = lr * fs_qkv + h * DH * 2 + g * 16, lo_io = lr * fs_io + h * DH * 2 + g * 16;
+
+  for (int gp = kblk; gp < ngroups; gp += TFB_NB) {
+    const int p = gp * 2 + (wid >> 1);
+    if (p >= HW) break;  // wave-uniform
+    const int pl = TFB_DIAG == 1 ? (p & 1) : p;  // (diagnostic: the rows of pixels 0 / 1 for every pixel)
+    const int64_t row0 = (int64_t)b * F * HW + pl;
+    const int64_t qrow0 = pm ? ((int64_t)b * HW + pl) * F : row0;
+    // per-pixel opaque copies of the bias / RoPE-row bases: as loop invariants the compiler hoists every per-(tile,
+    // lane) bias vector and RoPE row out of the pixel loop (> 100 VGPRs at NT = 8) and spills
+    const float* bl = bl0 + opaque_zero();
+    const float* rt = rtab + opaque_zero();
+    const float* rb = rbase + lr * 32 + opaque_zero();
+    auto cs8 = [&](int a, float* cs) {  // pairs 4g .. 4g + 3 of frame 16 a + lr
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(rb + 8 * g), b1 = *reinterpret_cast<const f32x4*>(rb + 8 * g + 4);
+      const float cb[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+      compose(cb, *reinterpret_cast<const f32x4*>(rt + a * 32 + 8 * g), cs, 0);
+      compose(cb, *reinterpret_cast<const f32x4*>(rt + a * 32 + 8 * g + 4), cs, 4);
+    };
+    auto cs4 = [&](int a, int t, float* cs) {  // pairs 8t + 2g, +1 of frame 16 a + lr
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(rb + (8 * t + 2 * g) * 2);
+      const float cb[4] = {b0[0], b0[1], b0[2], b0[3]};
+      compose(cb, *reinterpret_cast<const f32x4*>(rt + a * 32 + (8 * t + 2 * g) * 2), cs, 0);
+    };
+    bf16x8 kraw[2], vraw[2];
+    auto ldkv = [&](int sk) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int kt = 2 * sk + u;
+        const auto rs = tile_rsrc(qkv + (qrow0 + (int64_t)kt * 16 * qfs) * QKV, F - kt * 16, (int64_t)fs_qkv, QKV * 2);
+        kraw[u] = buf_ld16(rs, lo_qkv + INNER * 2);  // frames >= F: zeros
+        vraw[u] = buf_ld16(rs, lo_qkv + 2 * INNER * 2);
+      }
+    };
+    ldkv(0);
+    wsync();  // the previous pixel's reads of the region done
+    // ---- stage Q' = scale R q and dO rows, L and D = dO . O of the pixel's queries: every load issued first (rows past
+    // F read as zeros), then branch-free stores -- Q' tiles before dO tiles, so the zero rows the last Q' tile writes
+    // past the RQ staged ones (into the dO rows) are overwritten; the dO tile's land in the K' rows, staged later
+    const float* lsep = lse + (((int64_t)b * NH + h) * HW + pl) * F;
+    bf16x8 qr[NT], dr[NT], orw[NT];
+    float lq[NT];
+#pragma unroll
+    for (int qt = 0; qt < NT; ++qt) {
+      const int nq = F - qt * 16;
+      const auto rq = tile_rsrc(qkv + (qrow0 + (int64_t)qt * 16 * qfs) * QKV, nq, (int64_t)fs_qkv, QKV * 2);
+      const auto rd = tile_rsrc(dout + (row0 + (int64_t)qt * 16 * HW) * INNER, nq, (int64_t)fs_io, INNER * 2);
+      const auto ro = tile_rsrc(o + (row0 + (int64_t)qt * 16 * HW) * INNER, nq, (int64_t)fs_io, INNER * 2);
+      qr[qt] = buf_ld16(rq, lo_qkv);
+      dr[qt] = buf_ld16(rd, lo_io);
+      orw[qt] = buf_ld16(ro, lo_io);
+      const int f = qt * 16 + lr;
+      lq[qt] = lsep[f < F ? f : 0];
+    }
+#pragma unroll
+    for (int qt = 0; qt < NT; ++qt) {
+      float cs[8];
+      cs8(qt, cs);
+      *reinterpret_cast<bf16x8*>(Qs + qt * 1024 + frag) = rope8(qr[qt], cs, scale);
+    }
+#pragma unroll
+    for (int qt = 0; qt < NT; ++qt) {
+      *reinterpret_cast<bf16x8*>(Os + qt * 1024 + frag) = dr[qt];
+      float Do = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) Do = fmaf((float)dr[qt][e], (float)orw[qt][e], Do);
+      const float D = grp4_sum(Do);
+      const int f = qt * 16 + lr;  // the 4 lanes of a row store the same values
+      Ls[f] = f < F ? lq[qt] : TF_LSE_PAD;
+      Ds[f] = f < F ? D : 0.f;
+    }
+    f32x4 dq[NT][2];
+#pragma unroll
+    for (int qt = 0; qt < NT; ++qt) dq[qt][0] = dq[qt][1] = z4;
+
+#pragma unroll
+    for (int sk = 0; sk < NP; ++sk) {
+      // K' rows of the key pair: B fragments of S, staged for the transposed reads of the dQ product
+      bf16x8 kb[2], vb[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        float cs[8];
+        cs8(2 * sk + u < NT ? 2 * sk + u : 0, cs);
+        kb[u] = rope8(kraw[u], cs, 1.f);  // keys >= F: zeros
+        vb[u] = vraw[u];
+        *reinterpret_cast<bf16x8*>(Ks + u * 1024 + frag) = kb[u];
+      }
+      if (TFB_PF && sk + 1 < NP) ldkv(sk + 1);
+      tfb_sync();
+      const bf16x8 ka[2] = {trp(Ks, 0, 0), trp(Ks, 0, 1)};  // K'^T[d][keys of the pair]
+      f32x4 dk[2][2], dv[2][2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) dk[u][0] = dk[u][1] = dv[u][0] = dv[u][1] = z4;
+#pragma unroll
+      for (int sq = 0; sq < NP; ++sq) {
+        // one 32 x 32 (query pair x key pair) block in three phases, so the MFMA and VALU work of a phase is
+        // independent (the co-resident wave fills the SIMD while this one waits on a phase's results):
+        // A: the 8 score / dP MFMAs; B: softmax gradient of the 4 tiles, dS^T tiles stored; C: dQ, dV, dK MFMAs
+        f32x4 sc[2][2], dp[2][2];
+        f32x4 Lq[2], Dq[2];
+#pragma unroll
+        for (int uq = 0; uq < 2; ++uq) {
+          const int qt = 2 * sq + uq;
+          if (qt >= NT) continue;
+          const bf16x8 qa = *reinterpret_cast<const bf16x8*>(Qs + qt * 1024 + frag);
+          const bf16x8 da = *reinterpret_cast<const bf16x8*>(Os + qt * 1024 + frag);
+          Lq[uq] = *reinterpret_cast<const f32x4*>(Ls + qt * 16 + 4 * g);
+          Dq[uq] = *reinterpret_cast<const f32x4*>(Ds + qt * 16 + 4 * g);
+#pragma unroll
+          for (int uk = 0; uk < 2; ++uk) {
+            if (2 * sk + uk >= NT) continue;
+            sc[uq][uk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kb[uk], z4, 0, 0, 0);   // S'[q][key]
+            dp[uq][uk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, vb[uk], z4, 0, 0, 0);  // dP[q][key]
+          }
+        }
+        // P and dS as bf16 k-slot B fragments per key tile (slots j < 4: query tile 2 sq, j >= 4: 2 sq + 1)
+        bf16x8 pb[2], sb[2];
+#pragma unroll
+        for (int uq = 0; uq < 2; ++uq) {
+          const int qt = 2 * sq + uq;
+#pragma unroll
+          for (int uk = 0; uk < 2; ++uk) {
+            const int kt = 2 * sk + uk;
+            float sv[4];
+            if (qt < NT && kt < NT) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                float x = fmaf(sc[uq][uk][r], LOG2E, bl[16 * (qt - kt) + r]) - Lq[uq][r];
+                if (kt == NT - 1) x += kmask;
+                const float pp = __builtin_amdgcn_exp2f(x);
+                const float ds = pp * (dp[uq][uk][r] - Dq[uq][r]);
+                pb[uk][4 * uq + r] = (bf16)pp;
+                sv[r] = ds;
+                const int dd = kt - qt;
+                if (dd >= -ND && dd <= ND) dba[r][dd + ND] += ds;
+                else if (dd > 0) dsp += ds;
+                else dsn += ds;
+              }
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                pb[uk][4 * uq + r] = (bf16)0.f;
+                sv[r] = 0.f;
+              }
+            }
+            const bf16x4 t4 = {(bf16)sv[0], (bf16)sv[1], (bf16)sv[2], (bf16)sv[3]};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sb[uk][4 * uq + r] = t4[r];
+            if (qt < NT)  // dS^T[key = lane][q = 4g .. 4g + 3] of tile (uq, uk)
+              *reinterpret_cast<bf16x4*>(Tt + (uq * 2 + uk) * 512 + tto) = t4;
+          }
+        }
+        tfb_sync();
+#pragma unroll
+        for (int uq = 0; uq < 2; ++uq) {
+          const int qt = 2 * sq + uq;
+          if (qt >= NT) continue;
+          // dQ'^T[d][q] += K'^T[d][keys] dS^T[keys][q] over the pair's 32 keys
+          const s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(Tt + (uq * 2) * 512 + tti));
+          const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(Tt + (uq * 2 + 1) * 512 + tti));
+          bf16x8 bsd;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            bsd[j] = __builtin_bit_cast(bf16, (short)t0[j]);
+            bsd[4 + j] = __builtin_bit_cast(bf16, (short)t1[j]);
+          }
+#pragma unroll
+          for (int t = 0; t < 2; ++t) dq[qt][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[t], bsd, dq[qt][t], 0, 0, 0);
+        }
+        // dV^T[d][key] += dO^T[d][q] P[q][key], dK'^T[d][key] += Q'^T[d][q] dS[q][key] over the query pair's 32 rows
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const bf16x8 dta = trp(Os, sq, t), qta = trp(Qs, sq, t);
+#pragma unroll
+          for (int uk = 0; uk < 2; ++uk) {
+            if (2 * sk + uk >= NT) continue;
+            dv[uk][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dta, pb[uk], dv[uk][t], 0, 0, 0);
+            dk[uk][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qta, sb[uk], dk[uk][t], 0, 0, 0);
+          }
+        }
+        tfb_sync();  // the tiles' reads done before the next block's stores
+      }
+      // dk = R^T dK', dv of the pair's keys (rows >= F dropped by the resource)
+#pragma unroll
+      for (int uk = 0; uk < 2; ++uk) {
+        const int kt = 2 * sk + uk;
+        if (kt >= NT) continue;
+        const auto rs = tile_rsrc(dqkv + (qrow0 + (int64_t)kt * 16 * qfs) * QKV, TFB_DIAG == 2 ? 0 : F - kt * 16,
+                                  (int64_t)fs_qkv, QKV * 2);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int d0 = t * 16 + 4 * g;
+          float k4[4] = {dk[uk][t][0], dk[uk][t][1], dk[uk][t][2], dk[uk][t][3]};
+          const float v4[4] = {dv[uk][t][0], dv[uk][t][1], dv[uk][t][2], dv[uk][t][3]};
+          float cs[4];
+          cs4(kt, t, cs);
+          rope4_cs(k4, cs, 1.f);
+          buf_st4b(rs, lr * fs_qkv + (INNER + h * DH + d0) * 2, k4);
+          buf_st4b(rs, lr * fs_qkv + (2 * INNER + h * DH + d0) * 2, v4);
+        }
+      }
+    }
+    // dq = scale R^T dQ'
+#pragma unroll
+    for (int qt = 0; qt < NT; ++qt) {
+      const auto rs = tile_rsrc(dqkv + (qrow0 + (int64_t)qt * 16 * qfs) * QKV, TFB_DIAG == 2 ? 0 : F - qt * 16,
+                                (int64_t)fs_qkv, QKV * 2);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int d0 = t * 16 + 4 * g;
+        float v4[4] = {dq[qt][t][0], dq[qt][t][1], dq[qt][t][2], dq[qt][t][3]};
+        float cs[4];
+        cs4(qt, t, cs);
+        rope4_cs(v4, cs, scale);
+        buf_st4b(rs, lr * fs_qkv + (h * DH + d0) * 2, v4);
+      }
+    }
+  }
+  // ---- rel-pos bias partials of the block: offset n = 16 d + l - 4 gg - r of lane (gg, l), register r, diagonal d;
+  // each lane sums the offsets n = lane + 64 j - (F - 1) over (d, gg, r) in a fixed order, the block its 4 waves in order
+  wsync();
+  float* stg = reinterpret_cast<float*>(Qs);  // NDG * 4 rows of 64 floats (<= the wave's Q', dO and K' rows)
+#pragma unroll
+  for (int c = 0; c < NDG; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) stg[(c * 4 + r) * 64 + lane] = dba[r][c];
+  const float tp = SAT ? wave_sum(dsp) : 0.f, tn = SAT ? wave_sum(dsn) : 0.f;
+  wsync();
+  float* wsum = reinterpret_cast<float*>(Ks);  // 256 floats (after the sums: the staged rows may reach into Ks)
+  float asum[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = lane + 64 * j - (F - 1);
+    float a = 0.f;
+    if (n < F) {
+#pragma nounroll
+      for (int c = 0; c < NDG; ++c)
+#pragma nounroll
+        for (int gg = 0; gg < 4; ++gg)
+#pragma nounroll
+          for (int r = 0; r < 4; ++r) {
+            const int l = n - 16 * (c - ND) + 4 * gg + r;
+            if (l >= 0 && l < 16) a += stg[(c * 4 + r) * 64 + gg * 16 + l];
+          }
+      if (SAT && n == F - 1) a += tp;
+      if (SAT && n == -(F - 1)) a += tn;
+    }
+    asum[j] = a;
+  }
+  wsync();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) wsum[lane + 64 * j] = asum[j];
+  __syncthreads();
+  if (part) {  // per head of the pair: its two waves (pixels) in order
+    const float* w0 = reinterpret_cast<const float*>(reinterpret_cast<char*>(smem + 3 * 32 * NT + 16 * 32) + 2 * (tfb_rq(F) * 64));
+    const int WB = tfb_wave_bytes(F, NT) / 4;
+#pragma clang loop vectorize(disable)  // (the tflash sources stay free of packed fp32: tests/test_isa_guard.py)
+    for (int e = tid; e < 2 * (2 * F - 1); e += 256) {
+      const int u = e / (2 * F - 1), n = e - u * (2 * F - 1);
+      part[((int64_t)(b * NH + 2 * hp + u) * TFB_NB + kblk) * (2 * F - 1) + n] = w0[u * WB + n] + w0[(2 + u) * WB + n];
+    }
+  }
+}
+
 // dtable[bucket][h] (+)= sum over partials and offsets n with bucket(n) of part[(b*8 + h)][blk][n + F - 1]
 __device__ int tf_bucket(int rel, int num_buckets, int max_distance) {  // relpos_bucket of attn.hip
   int n = -rel;
@@ -995,11 +1408,39 @@ __global__ void tf_dtable_kernel(const float* __restrict__ off, float* __restric
 // the block-per-pixel kernels are faster at every level (whole step 229.9-230.0 vs 232.5-233.0 ms with it at level 0,
 // profiles/r4c13_env_ab.txt; its isolated 192x288 timing against them, profiles/r4c5_qw_check.txt, was not borne out
 // in the step).
-enum TfDq { TF_DQ_BLOCK, TF_DQ_DOV, TF_DQ_WAVE };
+enum TfDq { TF_DQ_BLOCK, TF_DQ_DOV, TF_DQ_WAVE, TF_FUSED };
+// host copy of tf_bucket (relpos_bucket): the fused backward's saturated-diagonal check
+static int tf_bucket_host(int rel, int num_buckets, int max_distance) {
+  int n = -rel;
+  const int nb = num_buckets / 2;
+  int ret = n < 0 ? nb : 0;
+  n = n < 0 ? -n : n;
+  const int max_exact = nb / 2;
+  if (n < max_exact) return ret + n;
+  const float lg = logf((float)n / (float)max_exact) / logf((float)max_distance / (float)max_exact) *
+                   (float)(nb - max_exact);
+  int large = max_exact + (int)lg;
+  if (large > nb - 1) large = nb - 1;
+  return ret + large;
+}
+// exact bias-gradient diagonals per side the fused backward needs: the smallest nd whose beyond-diagonals' offsets
+// (|n| >= 16 nd + 1, with a margin of 2 for float rounding of the bucket logarithm) all share the bucket of +-(F - 1)
+static int tfb_nd(int F, int nt, int num_buckets, int max_distance) {
+  const int bp = tf_bucket_host(F - 1, num_buckets, max_distance), bn = tf_bucket_host(-(F - 1), num_buckets, max_distance);
+  for (int nd = 0; nd < nt - 1; ++nd) {
+    bool ok = true;
+    for (int n = std::max(1, 16 * nd - 1); n < F && ok; ++n)
+      ok = tf_bucket_host(n, num_buckets, max_distance) == bp && tf_bucket_host(-n, num_buckets, max_distance) == bn;
+    if (ok) return nd;
+  }
+  return nt - 1;
+}
 static TfDq tf_dq_kind(int nt, int HW, int pm = 0) {
   if (nt >= 2 && getenv_flag("CESM_TF_QW") && !getenv_flag("CESM_TF_NO_QW") &&
       (pm || (int64_t)16 * HW * QKV * 2 < (1ll << 31)))
     return TF_DQ_WAVE;
+  // the one-pass backward (round 5) for every long window; CESM_TF_FUSED=0: the two-kernel form
+  if (nt >= 2 && !(std::getenv("CESM_TF_FUSED") && std::strcmp(std::getenv("CESM_TF_FUSED"), "0") == 0)) return TF_FUSED;
   return TF_DO && nt >= 2 && HW < TF_DO_MAXHW ? TF_DQ_DOV : TF_DQ_BLOCK;
 }
 
@@ -1008,7 +1449,7 @@ extern "C" {
 // name of the dq kernel cesm_tflash_bwd runs for (F, HW) with frame-major qkv (host-only query; "invalid" when F
 // is unsupported)
 const char* cesm_tflash_bwd_variant(int F, int HW) {
-  static const char* names[3][9] = {
+  static const char* names[4][9] = {
       {"", "tflash_bwd_q_kernel<1,false>", "tflash_bwd_q_kernel<2,false>", "tflash_bwd_q_kernel<3,false>",
        "tflash_bwd_q_kernel<4,false>", "tflash_bwd_q_kernel<5,false>", "tflash_bwd_q_kernel<6,false>",
        "tflash_bwd_q_kernel<7,false>", "tflash_bwd_q_kernel<8,false>"},
@@ -1016,7 +1457,10 @@ const char* cesm_tflash_bwd_variant(int F, int HW) {
        "tflash_bwd_q_kernel<5,true>", "tflash_bwd_q_kernel<6,true>", "tflash_bwd_q_kernel<7,true>",
        "tflash_bwd_q_kernel<8,true>"},
       {"", "", "tflash_bwd_qw_kernel<2>", "tflash_bwd_qw_kernel<3>", "tflash_bwd_qw_kernel<4>",
-       "tflash_bwd_qw_kernel<5>", "tflash_bwd_qw_kernel<6>", "tflash_bwd_qw_kernel<7>", "tflash_bwd_qw_kernel<8>"}};
+       "tflash_bwd_qw_kernel<5>", "tflash_bwd_qw_kernel<6>", "tflash_bwd_qw_kernel<7>", "tflash_bwd_qw_kernel<8>"},
+      {"", "", "tflash_bwd_fused_kernel<2>", "tflash_bwd_fused_kernel<3>", "tflash_bwd_fused_kernel<4>",
+       "tflash_bwd_fused_kernel<5>", "tflash_bwd_fused_kernel<6>", "tflash_bwd_fused_kernel<7>",
+       "tflash_bwd_fused_kernel<8>"}};
   if (F < 1 || F > 16 * TF_MAXT || HW < 1) return "invalid";
   const int nt = (F + 15) / 16;
   return names[tf_dq_kind(nt, HW)][nt];
@@ -1026,7 +1470,7 @@ const char* cesm_tflash_bwd_variant(int F, int HW) {
 int cesm_tflash_supported(int F) { return F >= 1 && F <= 16 * TF_MAXT; }
 
 // blocks per (sample, head) of cesm_tflash_bwd's dq kernel (its dbias partial rows)
-int cesm_tflash_nblk(int HW) { return std::max(1, std::min(HW, 128)); }
+int cesm_tflash_nblk(int HW) { return (void)HW, TFB_NB; }
 
 // forward: qkv [B*F*HW][768] bf16 -> out [B*F*HW][256] bf16, lse [B][8][HW][F] (log2 units, nullable);
 // bias [8][F][F] (expanded rel-pos bias), rot [F][16][2].  qkv_pixel_major (F > 16 only): qkv rows ordered
@@ -1072,6 +1516,35 @@ int cesm_tflash_bwd(const void* qkv, const void* o, const void* dout, const floa
   dim3 gq(nblk, B * NH), gk(tf_grid_x(HW), B);
   const TfDq kind = tf_dq_kind(nt, HW, pm);
   const bool qw = kind == TF_DQ_WAVE, dov = kind == TF_DQ_DOV;
+  if (kind == TF_FUSED) {
+    if ((int64_t)16 * (pm ? 1 : HW) * QKV * 2 >= (1ll << 31))
+      return CESM_EUNSUPPORTED;  // 32-bit lane offsets of a 16-row tile
+    const int nd = tfb_nd(F, nt, num_buckets, max_distance);
+    const size_t sm = tfb_smem(F, nt);
+    dim3 gf(4 * TFB_NB, B);
+    float* pt = dtable ? part : nullptr;
+#define TFU(N, D)                                                                                                    \
+  {                                                                                                                  \
+    allow_smem(tflash_bwd_fused_kernel<N, D>, sm);                                                                   \
+    tflash_bwd_fused_kernel<N, D><<<gf, 256, sm, stream>>>((const bf16*)qkv, (const bf16*)o, (const bf16*)dout, lse, \
+                                                           bias, rot, (bf16*)dqkv, pt, F, HW, scale, pm);            \
+  }
+#define TFUN(N)                           \
+  if (N >= 4 && nd <= 2) TFU(N, (N >= 4 ? 2 : N - 1)) \
+  else TFU(N, N - 1)
+    switch (nt) {
+      case 2: TFU(2, 1); break;
+      case 3: TFU(3, 2); break;
+      case 4: TFUN(4); break;
+      case 5: TFUN(5); break;
+      case 6: TFUN(6); break;
+      case 7: TFUN(7); break;
+      case 8: TFUN(8); break;
+      default: return CESM_EUNSUPPORTED;
+    }
+#undef TFUN
+#undef TFU
+  } else {
 #define TFB(N)                                                                                                         \
   if (qw && N >= 2)                                                                                                    \
     tflash_bwd_qw_kernel<(N >= 2 ? N : 2)><<<gq, 256, 0, stream>>>((const bf16*)qkv, (const bf16*)o,                   \
@@ -1098,6 +1571,7 @@ int cesm_tflash_bwd(const void* qkv, const void* o, const void* dout, const floa
     default: return CESM_EUNSUPPORTED;
   }
 #undef TFB
+  }
   if (dtable) {
     tf_dbias_off_kernel<<<dim3(2 * F - 1, NH), 256, 0, stream>>>(part, off, nblk, B, F);
     tf_dtable_kernel<<<(unsigned)cdiv(num_buckets * NH, 64), 64, 0, stream>>>(off, dtable, F, num_buckets,

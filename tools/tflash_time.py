@@ -1,5 +1,5 @@
 """HIP-event timing of the temporal-attention core (unfused path): MFMA flash kernels (default) vs the VALU
-kernels (CESM_NO_TFLASH=1).  usage: python tools/tflash_time.py [F] [H] [W] [B] [reps]"""
+kernels (CESM_NO_TFLASH=1).  usage: python tools/tflash_time.py [F] [H] [W] [B] [reps] [pixel_major]"""
 import os
 import sys
 
@@ -27,6 +27,7 @@ def main():
     W = int(sys.argv[3]) if len(sys.argv) > 3 else 288
     B = int(sys.argv[4]) if len(sys.argv) > 4 else 1
     reps = int(sys.argv[5]) if len(sys.argv) > 5 else 3
+    pm = len(sys.argv) > 6 and sys.argv[6] == "1"
     HW = H * W
     dev = torch.device("cuda")
     torch.manual_seed(0)
@@ -36,7 +37,7 @@ def main():
     st = {}
 
     def fwd():
-        st["o"] = K.tattn_fwd(qkv, bias, rot, B, F, HW, 32 ** -0.5)
+        st["o"] = K.tattn_fwd(qkv, bias, rot, B, F, HW, 32 ** -0.5, pixel_major=pm)
 
     tf = timed(fwd, reps)
     out, lse = st["o"]
@@ -44,11 +45,13 @@ def main():
     dtable = torch.zeros(32, 8, device=dev)
 
     def bwd():
-        K.tattn_bwd(qkv, out, dout, lse, bias, rot, dtable, B, F, HW, 32 ** -0.5)
+        K.tattn_bwd(qkv, out, dout, lse, bias, rot, dtable, B, F, HW, 32 ** -0.5, pixel_major=pm)
 
     tb = timed(bwd, reps)
     flop = 2 * 2 * F * F * 32 * 8 * HW * B
     kind = "VALU" if os.environ.get("CESM_NO_TFLASH", "0") == "1" else "MFMA"
+    kind += " fused" if K.tflash_bwd_variant(F, HW).startswith("tflash_bwd_fused") else " 2-kernel"
+    kind += " pm" if pm else ""
     print(f"{kind} F={F} {H}x{W} B={B}: fwd {tf:.1f} us ({flop / tf / 1e6:.1f} TF/s)  bwd {tb:.1f} us "
           f"({2.5 * flop / tb / 1e6:.1f} TF/s)  out mean {float(out.float().abs().mean()):.6f}")
 
