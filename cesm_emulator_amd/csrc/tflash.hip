@@ -969,7 +969,11 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_kv_kernel(
 // heads, so the two 64-B head halves of every 128-B qkv / dO / O line are read by one CU at about the same time (the
 // first form, one head per block with the 8 heads' blocks on one XCD, fetched 1.5x the algorithmic bytes).
 #ifndef TFB_PF
-#define TFB_PF 0  // A/B knob: the next key pair's K / V rows loaded while the current pair is computed (measured slower: 9.56 vs 8.55 ms at 192x288, F = 120)
+#define TFB_PF 1  // A/B knob: the next key pair's K / V rows loaded while the current pair is computed (0: at its start)
+#endif
+#ifndef TFB_PHASE
+#define TFB_PHASE 0  // A/B knob: a 32 x 32 score block in three phases (all 8 score MFMAs, then the softmax VALU, then the
+                     // product MFMAs); 0 = tile by tile (192x288, F = 120: 8.9 vs 9.6 ms)
 #endif
 #ifndef TFB_DIAG
 #define TFB_DIAG 0  // diagnostic builds only: 1 = every pixel reads pixel 0's rows (L2-resident), 2 = no dq / dk / dv stores
@@ -1174,6 +1178,7 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_fused_kernel(
 
 #pragma unroll
     for (int sk = 0; sk < NP; ++sk) {
+      if (!TFB_PF && sk > 0) ldkv(sk);
       // K' rows of the key pair: B fragments of S, staged for the transposed reads of the dQ product
       bf16x8 kb[2], vb[2];
 #pragma unroll
@@ -1191,6 +1196,7 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_fused_kernel(
 #pragma unroll
       for (int u = 0; u < 2; ++u) dk[u][0] = dk[u][1] = dv[u][0] = dv[u][1] = z4;
 #pragma unroll
+#if TFB_PHASE
       for (int sq = 0; sq < NP; ++sq) {
         // one 32 x 32 (query pair x key pair) block in three phases, so the MFMA and VALU work of a phase is
         // independent (the co-resident wave fills the SIMD while this one waits on a phase's results):
@@ -1279,6 +1285,83 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_fused_kernel(
         }
         tfb_sync();  // the tiles' reads done before the next block's stores
       }
+#else
+      for (int sq = 0; sq < NP; ++sq) {
+        // P and dS of the pair block as bf16 k-slot B fragments per key tile (slots j < 4: query tile 2 sq, j >= 4: 2 sq + 1)
+        bf16x8 pb[2], sb[2];
+#pragma unroll
+        for (int uq = 0; uq < 2; ++uq) {
+          const int qt = 2 * sq + uq;
+          if (qt >= NT) {
+#pragma unroll
+            for (int uk = 0; uk < 2; ++uk)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) pb[uk][4 * uq + r] = sb[uk][4 * uq + r] = (bf16)0.f;
+            continue;
+          }
+          const bf16x8 qa = *reinterpret_cast<const bf16x8*>(Qs + qt * 1024 + frag);
+          const bf16x8 da = *reinterpret_cast<const bf16x8*>(Os + qt * 1024 + frag);
+          const f32x4 Lq = *reinterpret_cast<const f32x4*>(Ls + qt * 16 + 4 * g);
+          const f32x4 Dq = *reinterpret_cast<const f32x4*>(Ds + qt * 16 + 4 * g);
+#pragma unroll
+          for (int uk = 0; uk < 2; ++uk) {
+            const int kt = 2 * sk + uk;
+            float sv[4];
+            if (kt < NT) {
+              const f32x4 sc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kb[uk], z4, 0, 0, 0);  // S'[q][key]
+              const f32x4 dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, vb[uk], z4, 0, 0, 0);  // dP[q][key]
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                float x = fmaf(sc[r], LOG2E, bl[16 * (qt - kt) + r]) - Lq[r];
+                if (kt == NT - 1) x += kmask;
+                const float pp = __builtin_amdgcn_exp2f(x);
+                const float ds = pp * (dp[r] - Dq[r]);
+                pb[uk][4 * uq + r] = (bf16)pp;
+                sv[r] = ds;
+                const int dd = kt - qt;
+                if (dd >= -ND && dd <= ND) dba[r][dd + ND] += ds;
+                else if (dd > 0) dsp += ds;
+                else dsn += ds;
+              }
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                pb[uk][4 * uq + r] = (bf16)0.f;
+                sv[r] = 0.f;
+              }
+            }
+            const bf16x4 t4 = {(bf16)sv[0], (bf16)sv[1], (bf16)sv[2], (bf16)sv[3]};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sb[uk][4 * uq + r] = t4[r];
+            *reinterpret_cast<bf16x4*>(Tt + (uq * 2 + uk) * 512 + tto) = t4;  // dS^T[key = lane][q = 4g .. 4g + 3]
+          }
+          tfb_sync();
+          // dQ'^T[d][q] += K'^T[d][keys] dS^T[keys][q] over the pair's 32 keys
+          const s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(Tt + (uq * 2) * 512 + tti));
+          const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(Tt + (uq * 2 + 1) * 512 + tti));
+          bf16x8 bsd;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            bsd[j] = __builtin_bit_cast(bf16, (short)t0[j]);
+            bsd[4 + j] = __builtin_bit_cast(bf16, (short)t1[j]);
+          }
+#pragma unroll
+          for (int t = 0; t < 2; ++t) dq[qt][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[t], bsd, dq[qt][t], 0, 0, 0);
+        }
+        // dV^T[d][key] += dO^T[d][q] P[q][key], dK'^T[d][key] += Q'^T[d][q] dS[q][key] over the query pair's 32 rows
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const bf16x8 dta = trp(Os, sq, t), qta = trp(Qs, sq, t);
+#pragma unroll
+          for (int uk = 0; uk < 2; ++uk) {
+            if (2 * sk + uk >= NT) continue;
+            dv[uk][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dta, pb[uk], dv[uk][t], 0, 0, 0);
+            dk[uk][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qta, sb[uk], dk[uk][t], 0, 0, 0);
+          }
+        }
+        tfb_sync();  // the tiles' reads done before the next block's stores
+      }
+#endif
       // dk = R^T dK', dv of the pair's keys (rows >= F dropped by the resource)
 #pragma unroll
       for (int uk = 0; uk < 2; ++uk) {
