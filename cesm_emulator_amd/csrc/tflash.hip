@@ -215,6 +215,9 @@ __device__ __forceinline__ const float* btab_lane(const float* tab, int lr, int 
 #ifndef TF_BUF
 #define TF_BUF 1  // A/B knob: buffer-resource tile addressing in the per-query-tile loop (0 = 64-bit lane math)
 #endif
+#ifndef TF_FWD2
+#define TF_FWD2 1  // A/B knob: forward with every load up front and RoPE by angle addition (0 = round 2-4 form)
+#endif
 #ifndef TF_XCD_MAP
 #define TF_XCD_MAP 1  // A/B knob: 0 = head-major grid (round 2)
 #endif
@@ -367,6 +370,156 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE)
         store4b(out + (row0 + (int64_t)fq * HW) * INNER + h * DH + t * 16 + 4 * g, o4);
       }
       if (lse && g == 0) lse[(((int64_t)b * NH + h) * HW + p) * F + fq] = mm + log2f(l);
+    }
+  }
+}
+
+// Round 5 form of the forward (TF_FWD2, default): every global load of the wave is issued up front -- the raw K and Q
+// rows of all tiles through tile resources (frames >= F read as zeros) and the V rows of the first staging part --
+// and the RoPE coefficients come by angle addition (frame 16 a + lr = the block's row of frame 16 a composed with the
+// row of frame lr, two small LDS tables; the fused backward uses the same coefficients).  No load is issued after the
+// wave's first O store: vmcnt counts loads and stores in order, and in the first form (tflash_fwd_kernel) every query
+// tile's q and RoPE loads waited behind the previous tile's stores, and the K' prologue waited once per key tile.
+template <int NT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE))) void tflash_fwd2_kernel(
+    const bf16* __restrict__ qkv, const float* __restrict__ bias, const float* __restrict__ rot, bf16* __restrict__ out,
+    float* __restrict__ lse, int F, int HW, float scale, int pm) {
+  constexpr int NP = (NT + 1) / 2;
+  constexpr int VH = NP < TF_VH ? NP : TF_VH, NVR = 32 * VH;
+  __shared__ __attribute__((aligned(16))) float btab[4 * 32 * NT];
+  __shared__ __attribute__((aligned(16))) float rtab[32 * NT];    // RoPE (cos, sin) rows of frames 16 a
+  __shared__ __attribute__((aligned(16))) float rbase[16 * 32];   // ... of frames 0 .. 15 (0 past F)
+  __shared__ __attribute__((aligned(16))) bf16 vst[4][NVR * TF_LD];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, lr = lane & 15, g = lane >> 4;
+  int grp, h;
+  tf_block(grp, h);
+  const int b = blockIdx.y;
+  if (grp * 4 >= HW) return;  // whole block (padded groups)
+  load_btab<NT>(bias, btab, h, F, 1, tid, 256);
+  for (int e = tid; e < 32 * NT; e += 256) rtab[e] = rot[(e >> 5) * 16 * 32 + (e & 31)];
+  for (int e = tid; e < 16 * 32; e += 256) rbase[e] = e < F * 32 ? rot[e] : 0.f;
+  __syncthreads();
+  const int p = grp * 4 + __builtin_amdgcn_readfirstlane(wid);  // wave-uniform (buffer bases in SGPRs)
+  if (p >= HW) return;
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  const int64_t row0 = (int64_t)b * F * HW + p;
+  const int64_t qrow0 = pm ? ((int64_t)b * HW + p) * F : row0;
+  const int qfs = pm ? 1 : HW;
+  const int fs_qkv = qfs * QKV * 2;  // 16 rows < 2^31 B: checked on the host
+  const int lo = lr * fs_qkv + (h * DH + g * 8) * 2;
+  bf16x8 kr[NT], qr[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const __amdgpu_buffer_rsrc_t rs = tile_rsrc(qkv + (qrow0 + (int64_t)t * 16 * qfs) * QKV, F - t * 16, (int64_t)fs_qkv,
+                                               QKV * 2);
+    kr[t] = buf_ld16(rs, lo + INNER * 2);
+    qr[t] = buf_ld16(rs, lo);
+  }
+  bf16* vs = vst[wid];
+  auto vload = [&](int s0, bf16x8* vraw) {
+#pragma unroll
+    for (int i = 0; i < NVR * 4 / 64; ++i) {
+      const int e = lane + 64 * i, fl = e >> 2, c = e & 3, f = 32 * s0 + fl;
+      vraw[i] = ld16(qkv + (qrow0 + (int64_t)(f < F ? f : 0) * qfs) * QKV + 2 * INNER + h * DH + c * 8);
+      if (f >= F) vraw[i] = zero8();
+    }
+  };
+  bf16x8 vraw[NVR * 4 / 64];
+  vload(0, vraw);
+  const float* rb = rbase + lr * 32 + 8 * g;
+  auto cs8 = [&](int a, float* cs) {  // pairs 4g .. 4g + 3 of frame 16 a + lr
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float cb = rb[2 * u], sb = rb[2 * u + 1], ct = rtab[a * 32 + 8 * g + 2 * u], st = rtab[a * 32 + 8 * g + 2 * u + 1];
+      cs[2 * u] = cb * ct - sb * st;
+      cs[2 * u + 1] = sb * ct + cb * st;
+    }
+  };
+  bf16x8 kf[NT];
+#pragma unroll
+  for (int kt = 0; kt < NT; ++kt) {
+    float cs[8];
+    cs8(kt, cs);
+    kf[kt] = rope8(kr[kt], cs, 1.f);
+  }
+  bf16x8 vf[NP][2];
+#pragma unroll
+  for (int s0 = 0; s0 < NP; s0 += VH) {
+    if (s0) {
+      wsync();  // previous part's transposed reads done
+      vload(s0, vraw);
+    }
+#pragma unroll
+    for (int i = 0; i < NVR * 4 / 64; ++i) {
+      const int e = lane + 64 * i, fl = e >> 2, c = e & 3;
+      *reinterpret_cast<bf16x8*>(vs + fl * TF_LD + c * 8) = vraw[i];
+    }
+    wsync();
+#pragma unroll
+    for (int s = s0; s < s0 + VH && s < NP; ++s)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) vf[s][t] = tr_pair(vs, s - s0, t * 16, lane);
+  }
+  const float* bl = btab_lane<NT>(btab, lr, g);
+  float kmask[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) kmask[r] = 16 * (NT - 1) + 4 * g + r < F ? 0.f : -INFINITY;
+  const int o_off = (lr * HW * INNER + 4 * g) * 2;
+#pragma unroll
+  for (int qt = 0; qt < NT; ++qt) {
+    const int nq = F - qt * 16;
+    float cs[8];
+    cs8(qt, cs);
+    const bf16x8 qf = rope8(qr[qt], cs, scale);  // frames >= F: zeros
+    const float* bq = bl - 16 * qt;
+    float sc[2 * NP][4];
+    float m = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 2 * NP; ++kt) {
+      if (kt < NT) {
+        const f32x4 st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt < NT ? kt : 0], qf, z4, 0, 0, 0);
+        const f32x4 bo = *reinterpret_cast<const f32x4*>(bq + 16 * kt);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          sc[kt][r] = fmaf(st[r], LOG2E, bo[r]);
+          if (kt == NT - 1) sc[kt][r] += kmask[r];
+          m = fmaxf(m, sc[kt][r]);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sc[kt][r] = -INFINITY;
+      }
+    }
+    const float mm = grp4_max(m);  // finite: key 0 is valid for every query row
+    float l = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 2 * NP; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        sc[kt][r] = __builtin_amdgcn_exp2f(sc[kt][r] - mm);  // exp2(-inf) = 0
+        l += sc[kt][r];
+      }
+    l = grp4_sum(l);
+    f32x4 ot[2] = {z4, z4};
+#pragma unroll
+    for (int s = 0; s < NP; ++s) {
+      const bf16x8 pb = pack_kslot(sc[2 * s], sc[2 * s + 1]);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) ot[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[s][t], pb, ot[t], 0, 0, 0);
+    }
+    // stores of frames >= F fall outside the resources and are dropped
+    const float inv = __builtin_amdgcn_rcpf(l);
+    const __amdgpu_buffer_rsrc_t ors =
+        tile_rsrc(out + (row0 + (int64_t)qt * 16 * HW) * INNER + h * DH, nq, (int64_t)HW * INNER * 2, DH * 2);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      float o4[4] = {ot[t][0] * inv, ot[t][1] * inv, ot[t][2] * inv, ot[t][3] * inv};
+      buf_st4b(ors, o_off + t * 32, o4);
+    }
+    if (lse) {
+      const __amdgpu_buffer_rsrc_t lrs = tile_rsrc(lse + (((int64_t)b * NH + h) * HW + p) * F + qt * 16, nq, 4, 4);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, mm + log2f(l)), lrs,
+                                            g == 0 ? lr * 4 : 0x7ffffff0, 0, 0);
     }
   }
 }
@@ -1566,8 +1719,11 @@ int cesm_tflash_fwd(const void* qkv, const float* bias, const float* rot, void* 
   if (pm && nt < 2) return CESM_EUNSUPPORTED;
   if ((int64_t)16 * HW * (pm ? INNER : QKV) * 2 >= (1ll << 31)) return CESM_EUNSUPPORTED;  // TF_BUF 32-bit lane offsets
   dim3 grid(tf_grid_x(HW), B);
-#define TFF(N) \
-  tflash_fwd_kernel<N><<<grid, 256, 0, stream>>>((const bf16*)qkv, bias, rot, (bf16*)out, lse, F, HW, scale, pm)
+#define TFF(N)                                                                                                    \
+  if (TF_FWD2)                                                                                                    \
+    tflash_fwd2_kernel<N><<<grid, 256, 0, stream>>>((const bf16*)qkv, bias, rot, (bf16*)out, lse, F, HW, scale, pm); \
+  else                                                                                                            \
+    tflash_fwd_kernel<N><<<grid, 256, 0, stream>>>((const bf16*)qkv, bias, rot, (bf16*)out, lse, F, HW, scale, pm)
   switch (nt) {
     case 1: TFF(1); break;
     case 2: TFF(2); break;
