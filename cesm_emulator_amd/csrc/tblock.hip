@@ -1711,6 +1711,10 @@ constexpr int TWH_PG = 1;
 #ifndef TWH_RING
 #define TWH_RING 2
 #endif
+#ifndef TWH_DX_LATE
+#define TWH_DX_LATE 2  // twh_bwd: a group's dx stores issued after the next group's q/k/v/dO weight loads (1: after its first batch; vmcnt counts
+                       // loads and stores in order: issued before them, the loads' first wait also waited for the stores)
+#endif
 #ifndef TWH_DO_PF
 #define TWH_DO_PF 1  // twh_bwd: the dO GEMM's weights issued during the last q/k/v batch (needs QKV_PIPE)
 #endif
@@ -1871,6 +1875,9 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
   for (int ct = 0; ct < (DWO ? 4 : 1); ++ct) dwo[ct][0] = dwo[ct][1] = z4;
 
   prefetch(blockIdx.x);
+  // TWH_DX_LATE: the previous group's dx chunk of this thread and its row (-1: none)
+  bf16x8 dx_pend = zero8();
+  int64_t dx_row = -1;
   TW_ST_DECL
   for (int gg = blockIdx.x; gg < ngroups; gg += gridDim.x) {
     const int b = gg / npg, p0 = (gg - b * npg) * T::PW;
@@ -1912,6 +1919,10 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
     };
     ldq(0, 0);
 #endif
+    if (TWH_DX_LATE == 1 && dx_row >= 0) {  // the previous group's dx, behind this group's first weight loads
+      __builtin_amdgcn_sched_barrier(0);
+      stnt16(dx + dx_row * C + cc * 8, dx_pend);
+    }
     __syncthreads();  // (A) tiles of this group ready; previous group's partials consumed
     prefetch(gg + gridDim.x);  // next group's x / dy / stats: in flight during the head phase
     TW_ST(0)
@@ -2001,6 +2012,10 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
         float o4[4] = {acc[0], acc[1], acc[2], acc[3]};
         store4(sdo + (vt * 16 + lr) * HLD + dt * 16 + lg * 4, o4);
       }
+    }
+    if (TWH_DX_LATE == 2 && dx_row >= 0) {  // the previous group's dx, behind this group's q/k/v/dO weight loads
+      __builtin_amdgcn_sched_barrier(0);
+      stnt16(dx + dx_row * C + cc * 8, dx_pend);
     }
     wave_lds_sync();
     TW_ST(2)
@@ -2345,7 +2360,11 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
         for (int o = 1; o < 8; o <<= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
         s1 *= 1.f / C;
         s2 *= 1.f / C;
-        if (vv < R && ok_cur) {
+        if (TWH_DX_LATE) {
+  #pragma unroll
+          for (int e = 0; e < 8; ++e) dx_pend[e] = (bf16)(rstd_cur * (g[e] - s1 - (float)xh[e] * s2) + (float)dv[e]);
+          dx_row = vv < R && ok_cur ? vrow(gg, vv) : -1;
+        } else if (vv < R && ok_cur) {
           bf16x8 o8;
   #pragma unroll
           for (int e = 0; e < 8; ++e) o8[e] = (bf16)(rstd_cur * (g[e] - s1 - (float)xh[e] * s2) + (float)dv[e]);
@@ -2355,6 +2374,7 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
     }
     TW_ST(6)
   }
+  if (TWH_DX_LATE && dx_row >= 0) stnt16(dx + dx_row * C + cc * 8, dx_pend);
   TW_ST_FLUSH(blockIdx.x * 8 + wid)
   // ---- per-block outputs: dW'_h rows of the slab, dbias partials (cesm_relpos_bwd layout, B = 1)
   float* slab = dw_slab + (int64_t)blockIdx.x * QKV * C;

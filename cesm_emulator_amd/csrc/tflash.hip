@@ -1184,7 +1184,7 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_fused_kernel(
   const int h = 2 * hp + (wid & 1);
   const int b = blockIdx.y;
   for (int e = tid; e < 32 * NT; e += 256) rtab[e] = rotg[(e >> 5) * 16 * 32 + (e & 31)];
-  for (int e = tid; e < 16 * 32; e += 256) rbase[e] = rotg[e];
+  for (int e = tid; e < 16 * 32; e += 256) rbase[e] = e < F * 32 ? rotg[e] : 0.f;  // frames past F (F < 16): 0
   for (int e = tid; e < 2 * 32 * NT; e += 256) {
     const int hh = 2 * hp + e / (32 * NT), n = 16 * NT - e % (32 * NT);
     float v = 0.f;
@@ -1671,12 +1671,16 @@ static int tfb_nd(int F, int nt, int num_buckets, int max_distance) {
   }
   return nt - 1;
 }
-static TfDq tf_dq_kind(int nt, int HW, int pm = 0) {
+static bool tf_fused_ok(int nt, int F) { return nt >= 2 || F >= 8; }
+static TfDq tf_dq_kind(int nt, int HW, int pm = 0, int F = 17) {
   if (nt >= 2 && getenv_flag("CESM_TF_QW") && !getenv_flag("CESM_TF_NO_QW") &&
       (pm || (int64_t)16 * HW * QKV * 2 < (1ll << 31)))
     return TF_DQ_WAVE;
-  // the one-pass backward (round 5) for every long window; CESM_TF_FUSED=0: the two-kernel form
-  if (nt >= 2 && !(std::getenv("CESM_TF_FUSED") && std::strcmp(std::getenv("CESM_TF_FUSED"), "0") == 0)) return TF_FUSED;
+  // the one-pass backward (round 5) for every window of F >= 8 frames; CESM_TF_FUSED=0: the two-kernel form.  (Below
+  // 8 frames the two-kernel form stays: its D = sum P dP keeps the F = 1 rel-pos bias gradient exactly 0, where
+  // D = dO . O from the bf16 O would leave a rounding residue.)
+  if (tf_fused_ok(nt, F) && !(std::getenv("CESM_TF_FUSED") && std::strcmp(std::getenv("CESM_TF_FUSED"), "0") == 0))
+    return TF_FUSED;
   return TF_DO && nt >= 2 && HW < TF_DO_MAXHW ? TF_DQ_DOV : TF_DQ_BLOCK;
 }
 
@@ -1694,12 +1698,12 @@ const char* cesm_tflash_bwd_variant(int F, int HW) {
        "tflash_bwd_q_kernel<8,true>"},
       {"", "", "tflash_bwd_qw_kernel<2>", "tflash_bwd_qw_kernel<3>", "tflash_bwd_qw_kernel<4>",
        "tflash_bwd_qw_kernel<5>", "tflash_bwd_qw_kernel<6>", "tflash_bwd_qw_kernel<7>", "tflash_bwd_qw_kernel<8>"},
-      {"", "", "tflash_bwd_fused_kernel<2>", "tflash_bwd_fused_kernel<3>", "tflash_bwd_fused_kernel<4>",
+      {"", "tflash_bwd_fused_kernel<1>", "tflash_bwd_fused_kernel<2>", "tflash_bwd_fused_kernel<3>", "tflash_bwd_fused_kernel<4>",
        "tflash_bwd_fused_kernel<5>", "tflash_bwd_fused_kernel<6>", "tflash_bwd_fused_kernel<7>",
        "tflash_bwd_fused_kernel<8>"}};
   if (F < 1 || F > 16 * TF_MAXT || HW < 1) return "invalid";
   const int nt = (F + 15) / 16;
-  return names[tf_dq_kind(nt, HW)][nt];
+  return names[tf_dq_kind(nt, HW, 0, F)][nt];
 }
 
 // supported windows of the MFMA temporal-attention core (bf16)
@@ -1753,7 +1757,7 @@ int cesm_tflash_bwd(const void* qkv, const void* o, const void* dout, const floa
   if (pm && (nt < 2 || (int64_t)16 * HW * INNER * 2 >= (1ll << 31))) return CESM_EUNSUPPORTED;
   const int nblk = cesm_tflash_nblk(HW);
   dim3 gq(nblk, B * NH), gk(tf_grid_x(HW), B);
-  const TfDq kind = tf_dq_kind(nt, HW, pm);
+  const TfDq kind = tf_dq_kind(nt, HW, pm, F);
   const bool qw = kind == TF_DQ_WAVE, dov = kind == TF_DQ_DOV;
   if (kind == TF_FUSED) {
     if ((int64_t)16 * (pm ? 1 : HW) * QKV * 2 >= (1ll << 31))
@@ -1772,6 +1776,7 @@ int cesm_tflash_bwd(const void* qkv, const void* o, const void* dout, const floa
   if (N >= 4 && nd <= 2) TFU(N, (N >= 4 ? 2 : N - 1)) \
   else TFU(N, N - 1)
     switch (nt) {
+      case 1: TFU(1, 0); break;
       case 2: TFU(2, 1); break;
       case 3: TFU(3, 2); break;
       case 4: TFUN(4); break;

@@ -188,8 +188,8 @@ def test_bench_shape_dispatch_table():
 
 
 def test_tflash_dq_dispatch():
-    """the long-window attention backward (cesm_tflash_bwd_variant, host only): the one-pass fused kernel for every
-    F > 16 (round 5), the block-per-pixel dq kernel (+ the dk / dv kernel) at F <= 16; the two-kernel form for F > 16
+    """the temporal attention core backward (cesm_tflash_bwd_variant, host only): the one-pass fused kernel for every
+    F >= 8 (round 5), the block-per-pixel dq kernel (+ the dk / dv kernel) below; the two-kernel form for F >= 8
     (CESM_TF_FUSED=0) and the per-wave dq kernel (CESM_TF_QW=1) are opt-in, checked in a child process (the library
     reads its knobs once per process)"""
     import json
@@ -199,7 +199,8 @@ def test_tflash_dq_dispatch():
     assert K.tflash_bwd_variant(120, 192 * 288) == "tflash_bwd_fused_kernel<8>"
     assert K.tflash_bwd_variant(120, 48 * 72) == "tflash_bwd_fused_kernel<8>"
     assert K.tflash_bwd_variant(17, 40) == "tflash_bwd_fused_kernel<2>"
-    assert K.tflash_bwd_variant(12, 192 * 288) == "tflash_bwd_q_kernel<1,false>"
+    assert K.tflash_bwd_variant(12, 192 * 288) == "tflash_bwd_fused_kernel<1>"
+    assert K.tflash_bwd_variant(7, 192 * 288) == "tflash_bwd_q_kernel<1,false>"
     assert K.tflash_bwd_variant(40, 200 * 200) == "tflash_bwd_fused_kernel<3>"
     assert K.tflash_bwd_variant(129, 64) == "invalid"
     code = ("import json; from cesm_emulator_amd import kernels as K; print(json.dumps([K.tflash_bwd_variant(F, HW) "
