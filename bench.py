@@ -187,7 +187,7 @@ class KernelProbe:
 
         def tattn_fwd(qkv, bias, rot, B, F, HW, scale, save=True, pixel_major=False):
             v = B * F * HW
-            lab = (f"tflash_fwd_kernel<{(F + 15) // 16}>" if K._tflash(qkv, F) else "tattn_fwd_kernel")
+            lab = (f"tflash_fwd2_kernel<{(F + 15) // 16}>" if K._tflash(qkv, F) else "tattn_fwd_kernel")
             # q.k and attn.v over the F frames of each pixel and head; bytes: qkv read, out (+ lse) written
             return lab, 4.0 * F * 32 * 8 * v, float(v * (768 * 2 + 256 * 2 + (32 if save else 0)))
 
@@ -195,11 +195,16 @@ class KernelProbe:
                       pixel_major=False):
             v = B * F * HW
             nt = (F + 15) // 16
-            # the dq kernel by dispatch (cesm_tflash_bwd_variant)
+            # the kernel(s) by dispatch (cesm_tflash_bwd_variant): the one-pass fused backward (round 5), or the dq kernel
+            # + the dk / dv kernel
             dq = K.tflash_bwd_variant(F, HW)  # the same selection for pixel-major qkv
-            lab = (f"{dq.replace(',false>', '>').replace(',true>', '>')} + "
-                   f"tflash_bwd_kv_kernel<{nt}>" if K._tflash(qkv, F) else "tattn_bwd_kernel")
-            # dP, dQ, dK, dV products (2x the forward); bytes: qkv, o, dout, lse read, dqkv written
+            if not K._tflash(qkv, F):
+                lab = "tattn_bwd_kernel"
+            elif dq.startswith("tflash_bwd_fused"):
+                lab = dq
+            else:
+                lab = f"{dq.replace(',false>', '>').replace(',true>', '>')} + tflash_bwd_kv_kernel<{nt}>"
+            # dP, dQ, dK, dV products (2x the forward); bytes: qkv, o, dout, lse read once, dqkv written
             return lab, 8.0 * F * 32 * 8 * v, float(v * (768 * 2 * 2 + 256 * 2 * 2 + 32))
 
         def sla_flop(C):  # per voxel: to_qkv + to_out + context k v^T and context^T q (8 heads, 32 x 32)
