@@ -1679,8 +1679,8 @@ static TfDq tf_dq_kind(int nt, int HW, int pm = 0, int F = 17) {
   // the one-pass backward (round 5) for every window of F >= 8 frames; CESM_TF_FUSED=0: the two-kernel form.  (Below
   // 8 frames the two-kernel form stays: its D = sum P dP keeps the F = 1 rel-pos bias gradient exactly 0, where
   // D = dO . O from the bf16 O would leave a rounding residue.)
-  if (tf_fused_ok(nt, F) && !(std::getenv("CESM_TF_FUSED") && std::strcmp(std::getenv("CESM_TF_FUSED"), "0") == 0))
-    return TF_FUSED;
+  static const bool fused_off = std::getenv("CESM_TF_FUSED") && std::strcmp(std::getenv("CESM_TF_FUSED"), "0") == 0;
+  if (tf_fused_ok(nt, F) && !fused_off) return TF_FUSED;
   return TF_DO && nt >= 2 && HW < TF_DO_MAXHW ? TF_DQ_DOV : TF_DQ_BLOCK;
 }
 

@@ -145,10 +145,14 @@ int cesm_tattn_bwd(int dtype, const void* qkv, const void* o, const void* dout, 
  * cesm_tattn_bwd (video_net.py:403-454) for the unfused path (long windows, C >= 256 levels).  fwd: qkv
  * [B*F*HW][768] -> out [..][256], lse [B][8][HW][F] (log2 units, nullable); bias [8][F][F], rot [F][16][2].
  * bwd: dqkv [..][768] from qkv, o (the forward's out), lse, dout [..][256]; dtable (+)= the rel-pos table
- * gradient (nullable).  Workspaces: dbuf B*8*HW*F, part B*8*cesm_tflash_nblk(HW)*(2F-1), off 8*(2F-1) floats. */
+ * gradient (nullable).  Workspaces: dbuf B*8*HW*F, part B*8*cesm_tflash_nblk(HW)*(2F-1), off 8*(2F-1) floats.
+ * Round 5 (same argument lists, CESM_ABI_VERSION unchanged): F >= 8 runs the one-pass fused backward (dbuf then
+ * unused; CESM_TF_FUSED=0 in the environment restores the dq + dk / dv kernels), and cesm_tflash_nblk returns 128
+ * for every HW (the fused kernel's pixel streams per (sample, head)) -- size part from it, not from a formula. */
 int cesm_tflash_supported(int F);
 int cesm_tflash_nblk(int HW);
-/* name of the dq kernel cesm_tflash_bwd runs for (F, HW) (host-only query) */
+/* name of the backward kernel (the fused one, or the dq kernel of the two-kernel form) cesm_tflash_bwd runs for
+ * (F, HW) (host-only query) */
 const char* cesm_tflash_bwd_variant(int F, int HW);
 /* qkv_pixel_major (F > 16): qkv / dqkv rows ordered [B][HW][F] (a pixel's frames adjacent: the long-window path's
  * LN writes its output in that order, so the to_qkv GEMM produces it); out / dout / lse keep their layouts */

@@ -33,7 +33,7 @@ CONV_CASES = {
     "c256": (256, 0, 256, 24, 96, 1, 2),
 }
 # long-window core (F, HW, B): F = 120 (config 4), and frame counts with a partial 16-frame tile
-TF_CASES = {"f120": (120, 77, 2), "f33": (33, 300, 1), "f17": (17, 40, 3)}
+TF_CASES = {"f120": (120, 77, 2), "f33": (33, 300, 1), "f17": (17, 40, 3), "f12": (12, 300, 2)}
 
 
 def conv_case(name, dev):
@@ -76,6 +76,9 @@ def tf_case(name, dev):
     dt = torch.zeros(32, 8, device=dev)
     out["dqkv"] = K.tattn_bwd(qkv, o, dy, lse, bias, rot, dt, B, F, HW, scale)
     out["dtable"] = dt
+    if F <= 16:  # pixel-major qkv rows are a long-window layout (F > 16)
+        torch.cuda.synchronize()
+        return {k: (v.cpu() if torch.is_tensor(v) else v) for k, v in out.items()}
     # the output (and so dy) is frame-major for either qkv layout; dq / dk / dv come back in the qkv's order
     o_pm, lse_pm = K.tattn_fwd(to_pm(qkv), bias, rot, B, F, HW, scale, pixel_major=True)
     dt_pm = torch.zeros(32, 8, device=dev)
