@@ -90,17 +90,24 @@ __device__ __forceinline__ void store4(bf16* p, const float* v) {
 
 // streaming (non-temporal) accesses for per-voxel traffic that is touched once, so the weight
 // fragments the fused attention kernels re-read every head stay cache-resident
+#ifndef CESM_NT_STORES
+#define CESM_NT_STORES 1  // A/B knob: 0 = the stnt* helpers issue plain stores
+#endif
 __device__ __forceinline__ bf16x8 ldnt16(const bf16* p) {
   return __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(p));
 }
-__device__ __forceinline__ void stnt16(bf16* p, bf16x8 v) { __builtin_nontemporal_store(v, reinterpret_cast<bf16x8*>(p)); }
+__device__ __forceinline__ void stnt16(bf16* p, bf16x8 v) {
+  if (CESM_NT_STORES) __builtin_nontemporal_store(v, reinterpret_cast<bf16x8*>(p));
+  else *reinterpret_cast<bf16x8*>(p) = v;
+}
 __device__ __forceinline__ void ldnt4(const bf16* p, float* v) {
   const bf16x4 a = __builtin_nontemporal_load(reinterpret_cast<const bf16x4*>(p));
   v[0] = (float)a[0]; v[1] = (float)a[1]; v[2] = (float)a[2]; v[3] = (float)a[3];
 }
 __device__ __forceinline__ void stnt4(bf16* p, const float* v) {
   bf16x4 a = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-  __builtin_nontemporal_store(a, reinterpret_cast<bf16x4*>(p));
+  if (CESM_NT_STORES) __builtin_nontemporal_store(a, reinterpret_cast<bf16x4*>(p));
+  else *reinterpret_cast<bf16x4*>(p) = a;
 }
 
 __device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x)); }
