@@ -869,10 +869,17 @@ __device__ __forceinline__ void rope4c(float* o4, const f32x4 cs) {
 // issued back to back, the next kind's weight fragments are in flight meanwhile (double buffer), and the RoPE
 // coefficients are read from LDS before the MFMAs, so the epilogue waits on nothing.  (Round 3 ran each tile as
 // load-wait -> 2 MFMAs -> s_nop -> LDS read -> wait -> VALU -> store, one chain at a time.)
+// the first q/k/v weight tile of head h (tw_qkv_b's buffer 0)
+template <int C, int NV>
+__device__ __forceinline__ void tw_qkv_b_first(const bf16* __restrict__ wqkv, int h, bf16x8 (&a0)[TW<C, NV>::KS], int lr,
+                                               int lg) {
+#pragma unroll
+  for (int ks = 0; ks < TW<C, NV>::KS; ++ks) a0[ks] = ld_img(wqkv, h * 2, TW<C, NV>::KS, ks, lg * 16 + lr);
+}
 template <int C, int NV, bool QSCALE = true>
 __device__ __forceinline__ void tw_qkv_b(const bf16* __restrict__ wqkv, const bf16x8 (&xf)[NV][C / 32], int h,
                                          const int (&fr)[NV], float scale, const float* rot, bf16* sq, bf16* sk,
-                                         bf16* sv, int lr, int lg) {
+                                         bf16* sv, int lr, int lg, const bf16x8* a0 = nullptr) {
   using T = TW<C, NV>;
   constexpr int R = NV * 16;
   // 6 (kind, half) column tiles; the next tile's weight fragments in flight while this one computes
@@ -881,7 +888,12 @@ __device__ __forceinline__ void tw_qkv_b(const bf16* __restrict__ wqkv, const bf
 #pragma unroll
     for (int ks = 0; ks < T::KS; ++ks) a[buf][ks] = ld_img(wqkv, (ct >> 1) * 16 + h * 2 + (ct & 1), T::KS, ks, lg * 16 + lr);
   };
-  ld(0, 0);
+  if (a0) {  // issued by the caller (TW_QKV_EARLY: before the previous head's O stores)
+#pragma unroll
+    for (int ks = 0; ks < T::KS; ++ks) a[0][ks] = a0[ks];
+  } else {
+    ld(0, 0);
+  }
 #pragma unroll
   for (int ct = 0; ct < 6; ++ct) {
     const int buf = ct & 1, kind = ct >> 1, u = ct & 1;
@@ -980,6 +992,11 @@ __device__ __forceinline__ void tw_ln(const bf16* __restrict__ x, const float* _
 
 // waves per SIMD of tw_fwd: at C = 64 LDS-bound (per-wave q/k/v slices + tables: 3 blocks of 53 KB);
 // at C >= 128 register-bound (the out-projection accumulators spill below 256 VGPRs)
+#ifndef TW_QKV_EARLY
+#define TW_QKV_EARLY 2  // tw_fwd (C = 64), bit 0: the next head's first weight tile loaded before this head's O stores;
+                        // bit 1: the head's lse stored after the to_out weight loads (vmcnt counts loads and stores in
+                        // order: a load issued after a store also waits for it)
+#endif
 #ifndef TW_FWD_OCC64
 #define TW_FWD_OCC64 3
 #endif
@@ -1039,6 +1056,10 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
   constexpr bool PREF = C <= 64 && tw_fwd_occ<C>() <= 2;
   bf16x8 wq[6][PREF ? T::KS : 1];
   if constexpr (PREF) tw_load_wq<C, NV>(wq, wqkv, 0, lr, lg);
+  constexpr bool QE = (TW_QKV_EARLY & 1) && !PREF && C == 64;  // early first weight tile
+  constexpr bool LE = (TW_QKV_EARLY & 2) && !PREF && C == 64;  // deferred lse stores
+  bf16x8 a0n[T::KS];  // QE: the next head's first q/k/v weight tile
+  if constexpr (QE) tw_qkv_b_first<C, NV>(wqkv, 0, a0n, lr, lg);
   for (int h = 0; h < NH; ++h) {
     bf16x8 wo[T::CT];
     if constexpr (PREF) {
@@ -1049,7 +1070,7 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
       tw_qkv_pre<C, NV>(wq, xf, fr, FOLD ? 1.f : scale, rot, sq, sk, sv, lr, lg);  // FOLD: scale in the weights
       if (h + 1 < NH) tw_load_wq<C, NV>(wq, wqkv, h + 1, lr, lg);  // in flight during the core
     } else {
-      if constexpr (C == 64) tw_qkv_b<C, NV, !FOLD>(wqkv, xf, h, fr, scale, rot, sq, sk, sv, lr, lg);
+      if constexpr (C == 64) tw_qkv_b<C, NV, !FOLD>(wqkv, xf, h, fr, scale, rot, sq, sk, sv, lr, lg, QE ? a0n : nullptr);
       else tw_qkv<C, NV, false>(wqkv, xf, h, fr, FOLD ? 1.f : scale, rot, sq, sk, sv, lr, lg);  // two-tile batches
     }
     // bias (log2 units) of this lane's 4 entries (i = lr, j = 4g + r); -inf masks padding frames
@@ -1067,6 +1088,7 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
     // interleave instead of serialising on the MFMA result latency).  Pixels past HW hold zero rows
     // (their LN input is masked): computing them is harmless, only the lse store is guarded.
     constexpr int PG = TW_FWD_PG < T::PW ? TW_FWD_PG : T::PW;
+    float lsev[T::PW];  // QE: the pixels' lse (log2 units)
 #pragma unroll
     for (int pg = 0; pg < T::PW; pg += PG) {
       f32x4 st[PG];
@@ -1104,7 +1126,8 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
           l += pr[r];
         }
         l = grp4_sum(l);
-        if (lse && lg == 0 && lr < F && p < HW) lse[(((int64_t)b * NH + h) * HW + p) * F + lr] = m + log2f(l);  // log2 units
+        if (LE) lsev[pg + u] = m + log2f(l);  // stored after the to_out weight loads
+        else if (lse && lg == 0 && lr < F && p < HW) lse[(((int64_t)b * NH + h) * HW + p) * F + lr] = m + log2f(l);  // log2 units
         const float inv = __builtin_amdgcn_rcpf(l);
         pb[u] = bf16x4_bits(pr[0] * inv, pr[1] * inv, pr[2] * inv, pr[3] * inv);
       }
@@ -1125,11 +1148,23 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
 #pragma unroll
       for (int ct = 0; ct < T::CT; ++ct) wo[ct] = ld_img(wout, ct, INNER / 32, h, lane);
     }
+    if constexpr (LE) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (lse && lg == 0 && lr < F) {
+#pragma unroll
+        for (int u = 0; u < T::PW; ++u)
+          if (p0 + u < HW) lse[(((int64_t)b * NH + h) * HW + p0 + u) * F + lr] = lsev[u];
+      }
+    }
     wave_lds_sync();
     // y^T += W_out[:, h] . O_h^T
     bf16x8 ob[T::NVTM];
 #pragma unroll
     for (int vt = 0; vt < T::NVTM; ++vt) ob[vt] = vt < NVT ? ld16(sq + hs_off<R>(vt * 16 + lr, lg * 8)) : zero8();
+    if constexpr (QE) {  // the next head's first weight tile, ahead of this head's O stores
+      if (h + 1 < NH) tw_qkv_b_first<C, NV>(wqkv, h + 1, a0n, lr, lg);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     if (o_out) {  // O_h for the to_out weight gradient (the backward then skips its emission)
 #pragma unroll
       for (int vt = 0; vt < T::NVTM; ++vt) {
