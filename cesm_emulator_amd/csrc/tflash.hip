@@ -24,6 +24,10 @@ constexpr int NH = 8, DH = 32, INNER = 256, QKV = 768;
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr int TF_LD = 40;     // staged-row stride (bf16): 80-B rows
 constexpr int TF_MAXT = 8;    // 16-frame tiles: F <= 128
+// row stride (floats) of the LDS table of frames 0 .. 15's RoPE rows: lane (g, lr) reads row lr at float 8g (+4) or
+// (8t + 2g) * 2 -- with 32-float rows 16 lanes of a ds_read_b128 group hit 4 bank sets (16 cycles, 4x); with 40,
+// 8 and 4 cycles (tools/lds_banks.py)
+constexpr int TF_RBS = 40;
 
 __device__ __forceinline__ bf16x8 zero8() {
   bf16x8 z;
@@ -388,7 +392,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE)
   constexpr int VH = NP < TF_VH ? NP : TF_VH, NVR = 32 * VH;
   __shared__ __attribute__((aligned(16))) float btab[4 * 32 * NT];
   __shared__ __attribute__((aligned(16))) float rtab[32 * NT];    // RoPE (cos, sin) rows of frames 16 a
-  __shared__ __attribute__((aligned(16))) float rbase[16 * 32];   // ... of frames 0 .. 15 (0 past F)
+  __shared__ __attribute__((aligned(16))) float rbase[16 * TF_RBS];  // ... of frames 0 .. 15 (0 past F)
   __shared__ __attribute__((aligned(16))) bf16 vst[4][NVR * TF_LD];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, lr = lane & 15, g = lane >> 4;
   int grp, h;
@@ -397,7 +401,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE)
   if (grp * 4 >= HW) return;  // whole block (padded groups)
   load_btab<NT>(bias, btab, h, F, 1, tid, 256);
   for (int e = tid; e < 32 * NT; e += 256) rtab[e] = rot[(e >> 5) * 16 * 32 + (e & 31)];
-  for (int e = tid; e < 16 * 32; e += 256) rbase[e] = e < F * 32 ? rot[e] : 0.f;
+  for (int e = tid; e < 16 * 32; e += 256) rbase[(e >> 5) * TF_RBS + (e & 31)] = e < F * 32 ? rot[e] : 0.f;
   __syncthreads();
   const int p = grp * 4 + __builtin_amdgcn_readfirstlane(wid);  // wave-uniform (buffer bases in SGPRs)
   if (p >= HW) return;
@@ -426,7 +430,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE)
   };
   bf16x8 vraw[NVR * 4 / 64];
   vload(0, vraw);
-  const float* rb = rbase + lr * 32 + 8 * g;
+  const float* rb = rbase + lr * TF_RBS + 8 * g;
   auto cs8 = [&](int a, float* cs) {  // pairs 4g .. 4g + 3 of frame 16 a + lr
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -1152,7 +1156,7 @@ __host__ __device__ constexpr int tfb_wave_bytes(int F, int NT) {
 }
 // block LDS: the two heads' bias tables (one copy each, 32 NT floats), the RoPE rows of frames 16 a (NT x 32 floats),
 // 4 wave regions
-static size_t tfb_smem(int F, int NT) { return (size_t)(3 * 32 * NT + 16 * 32) * 4 + 4 * (size_t)tfb_wave_bytes(F, NT); }
+static size_t tfb_smem(int F, int NT) { return (size_t)(3 * 32 * NT + 16 * TF_RBS) * 4 + 4 * (size_t)tfb_wave_bytes(F, NT); }
 __device__ __forceinline__ void rope4_cs(float* v, const float* cs, float scale) {  // R^T of two pairs, times scale
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
@@ -1173,7 +1177,7 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_fused_kernel(
   constexpr bool SAT = ND < NT - 1;  // diagonals beyond: one accumulator per sign
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* rtab = smem;  // [NT][16][2]: RoPE (cos, sin) of frame 16 a
-  float* rbase = smem + 3 * 32 * NT;  // [16][16][2]: RoPE (cos, sin) of frames 0 .. 15
+  float* rbase = smem + 3 * 32 * NT;  // [16][TF_RBS]: RoPE (cos, sin) of frames 0 .. 15
   // [2][32 NT]: the block's two heads' bias(n) (log2 units) at k = 16 NT - n (rows = queries: n = key - query)
   float* btabs = smem + 32 * NT;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1184,7 +1188,8 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_fused_kernel(
   const int h = 2 * hp + (wid & 1);
   const int b = blockIdx.y;
   for (int e = tid; e < 32 * NT; e += 256) rtab[e] = rotg[(e >> 5) * 16 * 32 + (e & 31)];
-  for (int e = tid; e < 16 * 32; e += 256) rbase[e] = e < F * 32 ? rotg[e] : 0.f;  // frames past F (F < 16): 0
+  for (int e = tid; e < 16 * 32; e += 256)
+    rbase[(e >> 5) * TF_RBS + (e & 31)] = e < F * 32 ? rotg[e] : 0.f;  // frames past F (F < 16): 0
   for (int e = tid; e < 2 * 32 * NT; e += 256) {
     const int hh = 2 * hp + e / (32 * NT), n = 16 * NT - e % (32 * NT);
     float v = 0.f;
@@ -1196,7 +1201,7 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_fused_kernel(
   }
   const float* btab = btabs + (wid & 1) * 32 * NT;
   const int RQ = tfb_rq(F);
-  char* Qs = reinterpret_cast<char*>(smem + 3 * 32 * NT + 16 * 32) + wid * tfb_wave_bytes(F, NT);
+  char* Qs = reinterpret_cast<char*>(smem + 3 * 32 * NT + 16 * TF_RBS) + wid * tfb_wave_bytes(F, NT);
   char* Os = Qs + RQ * 64;
   char* Ks = Os + RQ * 64;
   // the two dS^T tiles live in the K' rows: those are read (into the dQ A fragments) before the pair's first store
@@ -1266,7 +1271,7 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_fused_kernel(
     // lane) bias vector and RoPE row out of the pixel loop (> 100 VGPRs at NT = 8) and spills
     const float* bl = bl0 + opaque_zero();
     const float* rt = rtab + opaque_zero();
-    const float* rb = rbase + lr * 32 + opaque_zero();
+    const float* rb = rbase + lr * TF_RBS + opaque_zero();
     auto cs8 = [&](int a, float* cs) {  // pairs 4g .. 4g + 3 of frame 16 a + lr
       const f32x4 b0 = *reinterpret_cast<const f32x4*>(rb + 8 * g), b1 = *reinterpret_cast<const f32x4*>(rb + 8 * g + 4);
       const float cb[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
@@ -1587,7 +1592,7 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_fused_kernel(
   for (int j = 0; j < 4; ++j) wsum[lane + 64 * j] = asum[j];
   __syncthreads();
   if (part) {  // per head of the pair: its two waves (pixels) in order
-    const float* w0 = reinterpret_cast<const float*>(reinterpret_cast<char*>(smem + 3 * 32 * NT + 16 * 32) + 2 * (tfb_rq(F) * 64));
+    const float* w0 = reinterpret_cast<const float*>(reinterpret_cast<char*>(smem + 3 * 32 * NT + 16 * TF_RBS) + 2 * (tfb_rq(F) * 64));
     const int WB = tfb_wave_bytes(F, NT) / 4;
 #pragma clang loop vectorize(disable)  // (the tflash sources stay free of packed fp32: tests/test_isa_guard.py)
     for (int e = tid; e < 2 * (2 * F - 1); e += 256) {
