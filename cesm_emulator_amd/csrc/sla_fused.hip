@@ -1083,6 +1083,15 @@ __device__ __forceinline__ void wave_lds_sync_s() {
 // the 8 shares summed through LDS -> LN backward -> dx.  No per-voxel intermediate reaches HBM (slab_dx
 // emitted the 768-channel dqkv and xn for a separate weight-gradient GEMM).
 // ===================================================================================================
+#ifndef SLAH_PF_LATE
+#define SLAH_PF_LATE 1  // slah_dx: next group's x / dy prefetch issued after phase B's operand loads (0: after barrier A)
+#endif
+#ifndef SLAH_PB_EARLY
+#define SLAH_PB_EARLY 0  // slah_dx: phase B's per-(frame, head) operands loaded during phase A (after its last weight batch)
+#endif
+#ifndef SLAH_DX_LATE
+#define SLAH_DX_LATE 0  // slah_dx: a group's dx stores issued in the next group after its weight / operand loads
+#endif
 #ifndef SLAH_WPIPE
 #define SLAH_WPIPE 1  // slah_dx: weight fragments issued one GEMM step ahead (first before barrier A / the dW GEMM)
 #endif
@@ -1163,6 +1172,9 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
     for (int nt = 0; nt < 4; ++nt) dwacc[m][nt] = z4;
 
   prefetch(blockIdx.x);
+  // SLAH_DX_LATE: the previous group's dx chunk of this thread and its row (-1: none)
+  bf16x8 dx_pend = zero8();
+  int64_t dx_row = -1;
   for (int gg = blockIdx.x; gg < ngroups; gg += gridDim.x) {
     const int n = gg / npg, p0 = (gg - n * npg) * R;
     // ---- LN of this thread's pixel chunk (statistics over its 8 lanes)
@@ -1211,13 +1223,35 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
     lda(0, 0);
 #endif
     __syncthreads();  // (A)
-    prefetch(gg + gridDim.x);
+    if (!SLAH_PF_LATE) prefetch(gg + gridDim.x);
+
+    // phase B's per-(frame, head) operands (L2-resident images): SLAH_PB_EARLY issues them in phase A, right after
+    // its last weight batch, so phase B does not wait for their latency
+    bf16x8 aT[2], ax[2], ad[2], adT[2];
+    f32x4 kg[4];
+    auto ldpb = [&]() {
+      const int64_t fo = ((int64_t)(n * NH + h) * 2) * 64 * 8;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        aT[t] = ld16(actT + fo + (t * 64 + lane) * 8);
+        ax[t] = ld16(actx + fo + (t * 64 + lane) * 8);
+        ad[t] = ld16(adc + fo + (t * 64 + lane) * 8);
+        adT[t] = ld16(adcT + fo + (t * 64 + lane) * 8);
+      }
+      const f32x4* ki = reinterpret_cast<const f32x4*>(kimg + ((int64_t)(n * NH + h) * 64 + lane) * 16);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) kg[q] = ki[q];
+      // SLAH_PF_LATE: the next group's x / dy behind phase A's weights and these operands (vmcnt retires in issue
+      // order: a load issued behind the HBM prefetch waits for it)
+      if (SLAH_PF_LATE) prefetch(gg + gridDim.x);
+    };
 
     // ---- phase A: raw q | k | v | do of head h, rows = pixels, cols kind*32 + d
 #pragma unroll
     for (int kind = 0; kind < 4; ++kind) {
 #if SLAH_WPIPE
       if (kind + 1 < 4) lda(kind + 1, (kind + 1) & 1);
+      if (SLAH_PB_EARLY && kind == 2) ldpb();
       const auto& a = wa[kind & 1];
 #else
       bf16x8 a[2][KS];
@@ -1246,21 +1280,14 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
     wave_lds_sync_s();
     // ---- phase B: per-pixel softmax backward (slab_dx's math); dq | dk | dv over cols 0..95
     {
-      const int64_t fo = ((int64_t)(n * NH + h) * 2) * 64 * 8;
-      bf16x8 aT[2], ax[2], ad[2], adT[2];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        aT[t] = ld16(actT + fo + (t * 64 + lane) * 8);
-        ax[t] = ld16(actx + fo + (t * 64 + lane) * 8);
-        ad[t] = ld16(adc + fo + (t * 64 + lane) * 8);
-        adT[t] = ld16(adcT + fo + (t * 64 + lane) * 8);
-      }
+      if (!(SLAH_PB_EARLY && SLAH_WPIPE)) ldpb();
       float Kofs[2][4], Gd[2][4];
-      {
-        const f32x4* ki = reinterpret_cast<const f32x4*>(kimg + ((int64_t)(n * NH + h) * 64 + lane) * 16);
-        const f32x4 k0 = ki[0], k1 = ki[1], g0 = ki[2], g1 = ki[3];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) { Kofs[0][r] = k0[r]; Kofs[1][r] = k1[r]; Gd[0][r] = g0[r]; Gd[1][r] = g1[r]; }
+      for (int r = 0; r < 4; ++r) { Kofs[0][r] = kg[0][r]; Kofs[1][r] = kg[1][r]; Gd[0][r] = kg[2][r]; Gd[1][r] = kg[3][r]; }
+      if (SLAH_DX_LATE && dx_row >= 0) {  // the previous group's dx, behind this group's weight and operand loads
+        __builtin_amdgcn_sched_barrier(0);
+        stnt16(dx + dx_row * C + cc * 8, dx_pend);
+        dx_row = -1;
       }
 #pragma unroll
       for (int vt = 0; vt < NV; ++vt) {
@@ -1477,11 +1504,17 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
         bf16x8 o8;
 #pragma unroll
         for (int e = 0; e < 8; ++e) o8[e] = (bf16)(rstd_cur * (g[e] - s1 - (float)xh[e] * s2) + (float)dv[e]);
-        __builtin_nontemporal_store(o8, reinterpret_cast<bf16x8*>(dx + ((int64_t)n * HW + p0 + vv) * C + cc * 8));
+        if (SLAH_DX_LATE) {
+          dx_pend = o8;
+          dx_row = (int64_t)n * HW + p0 + vv;
+        } else {
+          __builtin_nontemporal_store(o8, reinterpret_cast<bf16x8*>(dx + ((int64_t)n * HW + p0 + vv) * C + cc * 8));
+        }
       }
     }
 #endif
   }
+  if (SLAH_DX_LATE && dx_row >= 0) stnt16(dx + dx_row * C + cc * 8, dx_pend);
   float* slab = dw_slab + (int64_t)blockIdx.x * QKV * C;
 #pragma unroll
   for (int m = 0; m < 6; ++m) {

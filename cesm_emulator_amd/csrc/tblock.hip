@@ -1746,6 +1746,9 @@ constexpr int TWH_PG = 1;
 #ifndef TWH_RING
 #define TWH_RING 2
 #endif
+#ifndef TWH_PF_LATE
+#define TWH_PF_LATE 0  // twh_bwd: next group's x / dy prefetch issued after the head phase's weight loads (0: after barrier A)
+#endif
 #ifndef TWH_DX_LATE
 #define TWH_DX_LATE 2  // twh_bwd: a group's dx stores issued after the next group's q/k/v/dO weight loads (1: after its first batch; vmcnt counts
                        // loads and stores in order: issued before them, the loads' first wait also waited for the stores)
@@ -1959,7 +1962,7 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
       stnt16(dx + dx_row * C + cc * 8, dx_pend);
     }
     __syncthreads();  // (A) tiles of this group ready; previous group's partials consumed
-    prefetch(gg + gridDim.x);  // next group's x / dy / stats: in flight during the head phase
+    if (!TWH_PF_LATE) prefetch(gg + gridDim.x);  // next group's x / dy / stats: in flight during the head phase
     TW_ST(0)
 
     // ---- head phase: wave h
@@ -2021,6 +2024,9 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
 #error "TWH_QKV_PIPE=0: tw_qkv writes the region layout, twh_bwd reads 80-B rows"
 #endif
     }
+    // TWH_PF_LATE: the next group's x / dy after every q/k/v/dO weight load (vmcnt retires in issue order, so a
+    // weight batch issued behind the HBM prefetch waits for it)
+    if (TWH_PF_LATE) prefetch(gg + gridDim.x);
     TW_ST(1)
     // dO_h^T = W_out[:, h]^T . dy^T
 #pragma unroll
