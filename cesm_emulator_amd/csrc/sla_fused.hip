@@ -313,6 +313,10 @@ __global__ __launch_bounds__(256) void slaf_combine_kernel(const float* __restri
 // ---------------------------------------------------------------------------------------------------
 // slaf_out: wave = 16*NV pixels of one frame, all heads; grid (cdiv(HW, 64*NV), Nf), 256 threads.
 // ---------------------------------------------------------------------------------------------------
+typedef unsigned int sl_u32x2 __attribute__((ext_vector_type(2)));
+#ifndef SLAF_EPI_PRE
+#define SLAF_EPI_PRE 1  // slaf_out: all residual / bias loads of the y epilogue before its first store (0: per-tile load -> store)
+#endif
 template <int C, int NV>
 #ifndef SLAF_WPE
 #define SLAF_WPE 2  // slaf_out capped at 256 registers (VGPR-form MFMAs, no AGPR stash); 1 = round-2 allocation
@@ -444,6 +448,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLAF_WPE)))
     }
   }
   // y = x + W_o o + b_o
+#if SLAF_EPI_PRE
+  // every residual / bias load before the first y store, the stores branch-free through a buffer resource over frame
+  // n (pixels past HW go to an out-of-range offset, which the hardware drops): vmcnt retires in issue order, so a load
+  // behind a store waits for it (as tw_fwd's TW_EPI_PRE)
+  {
+    const __amdgpu_buffer_rsrc_t yrs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(y + (int64_t)n * HW * C), (short)0, HW * C * 2, 0x00020000);
+    f32x4 bo[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) bo[ct] = *reinterpret_cast<const f32x4*>(bout + ct * 16 + lg * 4);
+    bf16x4 xr[NV][CT];
+#pragma unroll
+    for (int vt = 0; vt < NV; ++vt) {
+      const int p = p0 + vt * 16 + lr;
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct)
+        xr[vt][ct] = *reinterpret_cast<const bf16x4*>(xb + (int64_t)(p < HW ? p : 0) * C + ct * 16 + lg * 4);
+    }
+#pragma unroll
+    for (int vt = 0; vt < NV; ++vt) {
+      const int p = p0 + vt * 16 + lr;
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (bf16)((float)xr[vt][ct][r] + yacc[ct][vt][r] + bo[ct][r]);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(sl_u32x2, o), yrs,
+                                              p < HW ? (p * C + ct * 16 + lg * 4) * 2 : 0x7ffffff0, 0, 0);
+      }
+    }
+  }
+#else
 #pragma unroll
   for (int vt = 0; vt < NV; ++vt) {
     const int p = p0 + vt * 16 + lr;
@@ -459,6 +495,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLAF_WPE)))
       store4(y + ((int64_t)n * HW + p) * C + co, o4);
     }
   }
+#endif
 }
 
 // ===================================================================================================

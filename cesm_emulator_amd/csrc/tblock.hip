@@ -992,6 +992,10 @@ __device__ __forceinline__ void tw_ln(const bf16* __restrict__ x, const float* _
 
 // waves per SIMD of tw_fwd: at C = 64 LDS-bound (per-wave q/k/v slices + tables: 3 blocks of 53 KB);
 // at C >= 128 register-bound (the out-projection accumulators spill below 256 VGPRs)
+typedef unsigned int tw_u32x2 __attribute__((ext_vector_type(2)));
+#ifndef TW_EPI_PRE
+#define TW_EPI_PRE 0  // tw_fwd: all residual loads of the y epilogue issued before its first store (0: per-tile load -> store)
+#endif
 #ifndef TW_QKV_EARLY
 #define TW_QKV_EARLY 2  // tw_fwd (C = 64), bit 0: the next head's first weight tile loaded before this head's O stores;
                         // bit 1: the head's lse stored after the to_out weight loads (vmcnt counts loads and stores in
@@ -1182,6 +1186,44 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
     wave_lds_sync();
   }
   // y = x + attn
+#if TW_EPI_PRE
+  // every residual load issued before the first y store, and the stores branch-free through a buffer resource over
+  // sample b (rows outside the tile go to an out-of-range offset, which the hardware drops): vmcnt retires in issue
+  // order, so a load behind a store waits for it, and the per-tile load -> store rounds serialised the store round
+  // trips (a branch per tile also let the compiler sink loads behind earlier stores)
+  const int64_t sbytes = (int64_t)F * HW * C * 2;
+  if (sbytes < 0x7fff0000) {  // uniform
+    const __amdgpu_buffer_rsrc_t yrs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(y + (int64_t)b * F * HW * C), (short)0, (int)sbytes, 0x00020000);
+    int voff[T::NVTM];
+    int64_t rows[T::NVTM];
+#pragma unroll
+    for (int vt = 0; vt < T::NVTM; ++vt) {
+      int64_t row = 0;
+      const bool ok = vt < NVT && tw_row(vt * 16 + lr, VW, F, F4, p0, HW, b, row);
+      rows[vt] = ok ? row : 0;
+      voff[vt] = ok ? (int)((row - (int64_t)b * F * HW) * C * 2) : 0x7ffffff0;
+    }
+    bf16x4 xr[T::NVTM][T::CT];
+#pragma unroll
+    for (int vt = 0; vt < T::NVTM; ++vt)
+#pragma unroll
+      for (int ct = 0; ct < T::CT; ++ct)
+        if (vt < NVT) xr[vt][ct] = *reinterpret_cast<const bf16x4*>(x + rows[vt] * C + ct * 16 + lg * 4);
+#pragma unroll
+    for (int vt = 0; vt < T::NVTM; ++vt) {
+      if (vt >= NVT) break;
+#pragma unroll
+      for (int ct = 0; ct < T::CT; ++ct) {
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (bf16)(yacc[ct][vt][r] + (float)xr[vt][ct][r]);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(tw_u32x2, o), yrs, voff[vt] + (ct * 16 + lg * 4) * 2, 0, 0);
+      }
+    }
+    return;
+  }
+#endif
 #pragma unroll
   for (int vt = 0; vt < T::NVTM; ++vt) {
     if (vt >= NVT) break;
