@@ -314,6 +314,9 @@ __global__ __launch_bounds__(256) void slaf_combine_kernel(const float* __restri
 // slaf_out: wave = 16*NV pixels of one frame, all heads; grid (cdiv(HW, 64*NV), Nf), 256 threads.
 // ---------------------------------------------------------------------------------------------------
 typedef unsigned int sl_u32x2 __attribute__((ext_vector_type(2)));
+#ifndef SLAB_EPI_PRE
+#define SLAB_EPI_PRE 1  // slab_dx: all x / dy loads of the LN-backward epilogue before its first dx store (1: C >= 128, 2: all, 0: per-tile rounds)
+#endif
 #ifndef SLAF_EPI_PRE
 #define SLAF_EPI_PRE 1  // slaf_out: all residual / bias loads of the y epilogue before its first store (0: per-tile load -> store)
 #endif
@@ -1038,6 +1041,68 @@ __global__ __launch_bounds__(256, 2) void slab_dx_kernel(
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     // LN backward + residual; dgamma partial
+    if constexpr (SLAB_EPI_PRE == 2 || (SLAB_EPI_PRE == 1 && C >= 128)) {  // (C = 64, NV = 2: 3 more spills)
+    // every x / dy load before the first dx store, the stores branch-free through a buffer resource over frame n
+    // (pixels past HW go to an out-of-range offset, which the hardware drops): vmcnt retires in issue order, so a
+    // load behind a store waits for it -- the per-channel-tile dy load -> dx store rounds serialised CT - 1 store
+    // round trips per tile
+    {
+      const __amdgpu_buffer_rsrc_t drs =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(dx + rb * C), (short)0, HW * C * 2, 0x00020000);
+      bf16x4 xr[NV][CT], dr[NV][CT];
+#pragma unroll
+      for (int vt = 0; vt < NV; ++vt) {
+        const int p = p0 + vt * 16 + lr;
+        const int64_t row = rb + (p < HW ? p : 0);
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          xr[vt][ct] = *reinterpret_cast<const bf16x4*>(x + row * C + ct * 16 + lg * 4);
+          dr[vt][ct] = *reinterpret_cast<const bf16x4*>(dy + row * C + ct * 16 + lg * 4);
+        }
+      }
+#pragma unroll
+      for (int vt = 0; vt < NV; ++vt) {
+        const int p = p0 + vt * 16 + lr;
+        const bool ok = p < HW;
+        float s1 = 0.f, s2 = 0.f;
+        float xh[CT][4];
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          const int co = ct * 16 + lg * 4;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            xh[ct][r] = ok ? ((float)xr[vt][ct][r] - mean[vt]) * rstd[vt] : 0.f;
+            const float g = dxacc[ct][vt][r] * sgm[co + r];
+            s1 += g;
+            s2 = fmaf(g, xh[ct][r], s2);
+          }
+        }
+        s1 = grp4_sum(s1) / C;
+        s2 = grp4_sum(s2) / C;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          const int co = ct * 16 + lg * 4;
+          float d4[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            d4[r] = dxacc[ct][vt][r] * xh[ct][r];
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) d4[r] += __shfl_xor(d4[r], o, 64);
+          }
+          if (lr == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sg[co + r] += d4[r];
+          }
+          bf16x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            o[r] = (bf16)(rstd[vt] * (dxacc[ct][vt][r] * sgm[co + r] - s1 - xh[ct][r] * s2) + (float)dr[vt][ct][r]);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(sl_u32x2, o), drs, ok ? (p * C + co) * 2 : 0x7ffffff0,
+                                                0, 0);
+        }
+      }
+    }
+    } else {
 #pragma unroll
     for (int vt = 0; vt < NV; ++vt) {
       const int p = p0 + vt * 16 + lr;
@@ -1082,6 +1147,7 @@ __global__ __launch_bounds__(256, 2) void slab_dx_kernel(
           store4(dx + (rb + p) * C + co, o4);
         }
       }
+    }
     }
   }
   __syncthreads();

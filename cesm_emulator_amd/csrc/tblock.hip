@@ -993,6 +993,9 @@ __device__ __forceinline__ void tw_ln(const bf16* __restrict__ x, const float* _
 // waves per SIMD of tw_fwd: at C = 64 LDS-bound (per-wave q/k/v slices + tables: 3 blocks of 53 KB);
 // at C >= 128 register-bound (the out-projection accumulators spill below 256 VGPRs)
 typedef unsigned int tw_u32x2 __attribute__((ext_vector_type(2)));
+#ifndef TWB_EPI_PRE
+#define TWB_EPI_PRE 1  // tw_bwd: all x / dy / stats loads of the LN-backward epilogue before its first dx store (0: per-tile rounds)
+#endif
 #ifndef TW_EPI_PRE
 #define TW_EPI_PRE 0  // tw_fwd: all residual loads of the y epilogue issued before its first store (0: per-tile load -> store)
 #endif
@@ -1542,6 +1545,78 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
     }
     if (false)
 #endif
+    if (TWB_EPI_PRE && (int64_t)F * HW * C * 2 < 0x7fff0000) {  // uniform
+      // every x / dy / stats load before the first dx store, the stores branch-free through a buffer resource over
+      // sample b (rows outside the group go to an out-of-range offset, which the hardware drops): vmcnt retires in
+      // issue order, so a load behind a store waits for it (the per-tile dy load -> dx store rounds)
+      const int64_t s0 = (int64_t)b * F * HW;
+      const __amdgpu_buffer_rsrc_t drs =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(dx + s0 * C), (short)0, (int)((int64_t)F * HW * C * 2), 0x00020000);
+      bf16x4 xr[T::NVTM][T::CT], dr[T::NVTM][T::CT];
+      float2 mrv[T::NVTM];
+      int voff[T::NVTM];
+      bool okv[T::NVTM];
+#pragma unroll
+      for (int vt = 0; vt < T::NVTM; ++vt) {
+        if (vt >= NVT) break;
+        int64_t row = 0;
+        okv[vt] = tw_row(vt * 16 + lr, VW, F, F4, p0, HW, b, row);
+        row = okv[vt] ? row : 0;
+        voff[vt] = okv[vt] ? (int)((row - s0) * C * 2) : 0x7ffffff0;
+        mrv[vt] = *reinterpret_cast<const float2*>(mr + row * 2);
+#pragma unroll
+        for (int ct = 0; ct < T::CT; ++ct) {
+          xr[vt][ct] = __builtin_nontemporal_load(reinterpret_cast<const bf16x4*>(x + row * C + ct * 16 + lg * 4));
+          dr[vt][ct] = __builtin_nontemporal_load(reinterpret_cast<const bf16x4*>(dy + row * C + ct * 16 + lg * 4));
+        }
+      }
+#pragma unroll
+      for (int vt = 0; vt < T::NVTM; ++vt) {
+        if (vt >= NVT) break;
+        const bool ok = okv[vt];
+        const float mean = ok ? mrv[vt].x : 0.f, rstd = ok ? mrv[vt].y : 0.f;
+        float s1 = 0.f, s2 = 0.f;
+        float xh[T::CT][4];
+#pragma unroll
+        for (int ct = 0; ct < T::CT; ++ct) {
+          const int co = ct * 16 + lg * 4;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            xh[ct][r] = ok ? ((float)xr[vt][ct][r] - mean) * rstd : 0.f;
+            const float g = dxacc[ct][vt][r] * sgm[co + r];
+            s1 += g;
+            s2 = fmaf(g, xh[ct][r], s2);
+            if constexpr (DG_REG) dgam[ct][r] = fmaf(dxacc[ct][vt][r], xh[ct][r], dgam[ct][r]);
+          }
+        }
+        s1 = grp4_sum(s1);
+        s2 = grp4_sum(s2);
+        s1 /= C;
+        s2 /= C;
+#pragma unroll
+        for (int ct = 0; ct < T::CT; ++ct) {
+          const int co = ct * 16 + lg * 4;
+          if constexpr (!DG_REG) {
+            float d4[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              d4[r] = dxacc[ct][vt][r] * xh[ct][r];
+#pragma unroll
+              for (int o = 1; o < 16; o <<= 1) d4[r] += __shfl_xor(d4[r], o, 64);
+            }
+            if (lr == 0) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) sg[co + r] += d4[r];
+            }
+          }
+          bf16x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            o[r] = (bf16)(rstd * (dxacc[ct][vt][r] * sgm[co + r] - s1 - xh[ct][r] * s2) + (float)dr[vt][ct][r]);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(tw_u32x2, o), drs, voff[vt] + co * 2, 0, 0);
+        }
+      }
+    } else
 #pragma unroll
     for (int vt = 0; vt < T::NVTM; ++vt) {
       if (vt >= NVT) break;
