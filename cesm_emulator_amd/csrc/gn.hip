@@ -256,6 +256,9 @@ __device__ __forceinline__ void gn_coef8(const GnAffine& q, int b, int c0, int C
 // (Round 3 measured two Infinity-Cache orders and removed them: the backward one sample at a time so gn_bwd_apply
 // re-reads (dout, y) on-die -- whole step 132.0 -> 138.0 ms; gn_apply in reversed sample order -- neutral.)
 
+#ifndef GN_BATCH
+#define GN_BATCH 0  // gn_apply / gn_bwd_apply: rows per step with all loads before the stores (0: per-row load -> store)
+#endif
 // grid (nchunk, B): thread = (8-channel group c8, row lane rr), rows strided by 256/(C/8)
 template <typename T>
 __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ y, const GnAffine coef,
@@ -270,8 +273,43 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ y, 
   const int64_t rpc = (rows_b + nchunk - 1) / nchunk;
   const int64_t r0 = chunk * rpc, r1 = min(rows_b, r0 + rpc);
   const int64_t off = (int64_t)b * rows_b * C + c8 * 8;
+  int64_t r = r0 + rr;
+#if GN_BATCH
+  // GN_BATCH rows per step with every load issued before the first store (vmcnt retires in issue order: the
+  // per-row load -> store loop made each row's loads wait for the previous row's store); the tail below
+  if (res) {  // uniform
+    for (; r + (GN_BATCH - 1) * rl < r1; r += GN_BATCH * rl) {
+      float v[GN_BATCH][8], rv[GN_BATCH][8];
+#pragma unroll
+      for (int u = 0; u < GN_BATCH; ++u) {
+        gl8(y + off + (r + u * rl) * C, v[u]);
+        gl8(res + off + (r + u * rl) * C, rv[u]);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // every load issued before the first store
+#pragma unroll
+      for (int u = 0; u < GN_BATCH; ++u) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[u][i] = silu_t<T>(fmaf(v[u][i], A1[i], A0[i])) + rv[u][i];
+        gs8(out + off + (r + u * rl) * C, v[u]);
+      }
+    }
+  } else {
+    for (; r + (GN_BATCH - 1) * rl < r1; r += GN_BATCH * rl) {
+      float v[GN_BATCH][8];
+#pragma unroll
+      for (int u = 0; u < GN_BATCH; ++u) gl8(y + off + (r + u * rl) * C, v[u]);
+      __builtin_amdgcn_sched_barrier(0);  // every load issued before the first store
+#pragma unroll
+      for (int u = 0; u < GN_BATCH; ++u) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[u][i] = silu_t<T>(fmaf(v[u][i], A1[i], A0[i]));
+        gs8(out + off + (r + u * rl) * C, v[u]);
+      }
+    }
+  }
+#endif
 #pragma unroll 4
-  for (int64_t r = r0 + rr; r < r1; r += rl) {
+  for (; r < r1; r += rl) {
     float v[8], rv[8];
     gl8(y + off + r * C, v);
     if (res) gl8(res + off + r * C, rv);
@@ -463,8 +501,30 @@ __global__ __launch_bounds__(256) void gn_bwd_apply_kernel(const T* __restrict__
   const int64_t rpc = (rows_b + nchunk - 1) / nchunk;
   const int64_t r0 = chunk * rpc, r1 = min(rows_b, r0 + rpc);
   const int64_t off = (int64_t)b * rows_b * C + c8 * 8;
+  int64_t r = r0 + rr;
+#if GN_BATCH
+  // as gn_apply_kernel: GN_BATCH rows per step, loads before stores
+  for (; r + (GN_BATCH - 1) * rl < r1; r += GN_BATCH * rl) {
+    float v[GN_BATCH][8], d[GN_BATCH][8];
+#pragma unroll
+    for (int u = 0; u < GN_BATCH; ++u) {
+      gl8(y + off + (r + u * rl) * C, v[u]);
+      gl8(dout + off + (r + u * rl) * C, d[u]);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // every load issued before the first store
+#pragma unroll
+    for (int u = 0; u < GN_BATCH; ++u) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float da = d[u][i] * dsilu_t<T>(fmaf(v[u][i], A1[i], A0[i]));
+        d[u][i] = fmaf(da, E1[i], fmaf(v[u][i], E2[i], E3[i]));
+      }
+      gs8(dy + off + (r + u * rl) * C, d[u]);
+    }
+  }
+#endif
 #pragma unroll 4
-  for (int64_t r = r0 + rr; r < r1; r += rl) {
+  for (; r < r1; r += rl) {
     float v[8], d[8];
     gl8(y + off + r * C, v);
     gl8(dout + off + r * C, d);
