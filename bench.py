@@ -174,16 +174,14 @@ class KernelProbe:
             return f"tw_fwd_kernel<{C},{nv},true>", v * tw_core_flop(C, F), float(b)
 
         def tblock_bwd_dw(x, dy, mr, lse, wqkv_f32, gamma, wout_t, bias, rot, dwqkv, dgamma, dtable, B, F, scale,
-                          num_buckets=32, max_distance=32, dwout=None):
+                          num_buckets=32, max_distance=32):
             Nb, H, W, C = x.shape
             v = Nb * H * W
             nv = (4 * F + 15) // 16
             # dgrad-equivalent work (the forward's FLOPs) + the in-kernel to_qkv weight gradient (2 * 768 * C per
-            # voxel) [+ the in-kernel to_out weight gradient, 2 * 256 * C per voxel]; bytes: x, dy, mr / lse read,
-            # dx written (no per-voxel intermediates)
+            # voxel); bytes: x, dy, mr / lse read, dx written (no per-voxel intermediates)
             return (f"twh_bwd_kernel<{nv}> (+ dW / dgamma / dbias reductions)",
-                    v * (tw_core_flop(C, F) + 2.0 * 768 * C + (2.0 * 256 * C if dwout is not None else 0.0)),
-                    float(v * (3 * C * 2 + 40)))
+                    v * (tw_core_flop(C, F) + 2.0 * 768 * C), float(v * (3 * C * 2 + 40)))
 
         def tattn_fwd(qkv, bias, rot, B, F, HW, scale, save=True, pixel_major=False):
             v = B * F * HW
@@ -615,6 +613,9 @@ def main():
     torch.cuda.synchronize()
     if probe is not None:
         probe.active = True
+    if dp is not None:
+        dp.pop_timing()
+        dp.timing = True  # HIP events around each bucket on the communication stream (no host sync in the loop)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         c, x = next_batch()
@@ -627,10 +628,24 @@ def main():
     if probe is not None:
         probe.active = False
     lval = float(loss.item())
+    dist_info = None
     if world > 1:
-        tt = torch.tensor([elapsed], device=dev)
+        ar_ms, ar_n, ar_bytes = dp.pop_timing()
+        dp.timing = False
+        # what the ranks saw: world size, backend, RCCL version, and the all-reduce time per step (max over ranks,
+        # from the events on the communication stream -- overlapped with the backward, so not additive to the step)
+        tt = torch.tensor([elapsed, ar_ms / a.steps], device=dev)
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        elapsed, ar_ms_step = float(tt[0].item()), float(tt[1].item())
+        try:
+            ver = torch.cuda.nccl.version()
+            ver = ".".join(map(str, ver)) if isinstance(ver, tuple) else str(ver)
+        except Exception as e:  # noqa: BLE001 - reported, not fatal
+            ver = f"unavailable ({type(e).__name__})"
+        dist_info = {"world_size": torch.distributed.get_world_size(), "backend": torch.distributed.get_backend(),
+                     "rccl_version": ver, "allreduce_ms_per_step": round(ar_ms_step, 3),
+                     "allreduce_buckets_per_step": ar_n // a.steps, "allreduce_mb_per_step": round(ar_bytes / a.steps / 2**20, 1),
+                     "bucket_mb": dp.bucket_elems * 4 / 2**20}
 
     if rank != 0:
         if world > 1:
@@ -661,6 +676,8 @@ def main():
         "roofline": roof,
         "top_kernels": top,
     }
+    if dist_info is not None:
+        out["distributed"] = dist_info
     log(f"timed {a.steps} steps: {elapsed:.2f}s -> {value:.2f} samples/s")
     if world == 1 and a.other_configs and a.dtype == "bf16":
         # BASELINE.json configs 2, 4 (per-GPU leg) and 5 (per-GPU batch), after the headline and outside its timed

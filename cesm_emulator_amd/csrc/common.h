@@ -89,16 +89,13 @@ __device__ __forceinline__ void store4(bf16* p, const float* v) {
 }
 
 // streaming (non-temporal) accesses for per-voxel traffic that is touched once, so the weight
-// fragments the fused attention kernels re-read every head stay cache-resident
-#ifndef CESM_NT_STORES
-#define CESM_NT_STORES 1  // A/B knob: 0 = the stnt* helpers issue plain stores
-#endif
+// fragments the fused attention kernels re-read every head stay cache-resident (round 5: plain stores instead,
+// whole step 130.3 / 130.4 -> 130.9 / 130.6 ms, profiles/r5f_nt_stores_ab.txt)
 __device__ __forceinline__ bf16x8 ldnt16(const bf16* p) {
   return __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(p));
 }
 __device__ __forceinline__ void stnt16(bf16* p, bf16x8 v) {
-  if (CESM_NT_STORES) __builtin_nontemporal_store(v, reinterpret_cast<bf16x8*>(p));
-  else *reinterpret_cast<bf16x8*>(p) = v;
+  __builtin_nontemporal_store(v, reinterpret_cast<bf16x8*>(p));
 }
 __device__ __forceinline__ void ldnt4(const bf16* p, float* v) {
   const bf16x4 a = __builtin_nontemporal_load(reinterpret_cast<const bf16x4*>(p));
@@ -106,8 +103,7 @@ __device__ __forceinline__ void ldnt4(const bf16* p, float* v) {
 }
 __device__ __forceinline__ void stnt4(bf16* p, const float* v) {
   bf16x4 a = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-  if (CESM_NT_STORES) __builtin_nontemporal_store(a, reinterpret_cast<bf16x4*>(p));
-  else *reinterpret_cast<bf16x4*>(p) = a;
+  __builtin_nontemporal_store(a, reinterpret_cast<bf16x4*>(p));
 }
 
 __device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x)); }

@@ -471,10 +471,6 @@ constexpr int H3_P = 40;                 // LDS halo row pitch (pixels): >= TW+2
 constexpr int H3_NROW = 10 * H3_P;       // LDS halo rows ((TH+2) <= 10 tile rows of H3_P pixels)
 constexpr int H3_LD = 32;                // bf16 per LDS row: 32 channels = 64 B, no padding
 constexpr int H3_BN = 64;
-constexpr int H3_HVEC = H3_NPIX * 4;     // 16-B vectors in the halo tile
-constexpr int H3_WVEC = 9 * H3_BN * 4;   // 16-B vectors in the weight tile
-constexpr int H3_HPT = (H3_HVEC + 255) / 256;
-constexpr int H3_WPT = H3_WVEC / 256;
 // element offset of 16-B chunk `ch` (8 channels) of LDS row `row`: 64-B rows, chunk index XORed with
 // bit 2 of the row.  ds_read_b128 of 16 rows r0..r0+15 (lane = row, lane group = chunk) is then
 // bank-conflict free for any r0 (the 80-B padded rows it replaces ran 2-3-way conflicted: PMC
@@ -482,24 +478,9 @@ constexpr int H3_WPT = H3_WVEC / 256;
 // tap offsets ky * H3_P and tap * 64 stay immediate.
 __device__ __forceinline__ int h3_off(int row, int ch) { return row * H3_LD + ((ch ^ ((row >> 1) & 2)) << 3); }
 
-#ifndef H3_DMA
-#define H3_DMA 1  // conv3x3_bf16_kernel: chunk staging by buffer-LDS-DMA (0: global -> registers -> LDS)
-#endif
-#ifndef H3_PIPE
-#define H3_PIPE 1  // conv3x3_bf16_kernel: software-pipelined tap fragments (0: the compiler's read -> MFMA order)
-#endif
-#ifndef H3_SQ
-#define H3_SQ 1  // A/B knob: 64 co x 64 px wave tiles (0 = 32 co x 128 px, round 2)
-#endif
-#ifndef H3_PRIO
-#define H3_PRIO 0  // A/B knob: s_setprio 1 around a chunk's MFMA phase
-#endif
-#ifndef H3_XCD
-#define H3_XCD 1  // A/B knob: XCD-grouped co blocks of a halo tile (0 = co-block-slowest order)
-#endif
-#ifndef H3_BIG
-#define H3_BIG 1  // A/B knob: 448-pixel tiles with 64 co x 112 px wave tiles (0 = 256-pixel tiles, 64 x 64)
-#endif
+// The halo conv's measured alternatives, removed in round 6 (profiles/r2_*, r3_*, r5_prio_ab.txt): staging
+// through registers instead of LDS-DMA, the compiler's read -> MFMA tap order, 32 co x 128 px wave tiles, co-block-
+// slowest (not XCD-grouped) block order, 256-pixel tiles only, and s_setprio around the MFMA phase.
 // epilogue of the halo conv (conv3x3_bf16_kernel; a function since round 5's double-buffered variant): bias, residual, bf16 stores and the GroupNorm
 // statistics partials; lane holds co = n0 + wr*32 + i*16 + 4*lg + r of pixel pyx[j] (packed (py << 16) | px, -1 past TH)
 template <int NI, int NJ>
@@ -562,7 +543,7 @@ __device__ __forceinline__ void h3_epilogue(const f32x4 (&acc)[NI][NJ], const in
   }
   if (gnp) {
     const int b = n / gn_fimg, f = n - b * gn_fimg;
-    constexpr int SPT = 4 / (H3_SQ ? 1 : 2);  // GroupNorm slots per tile (= pixel ranges): h3_gn_slots
+    constexpr int SPT = 4;  // GroupNorm slots per tile (= pixel ranges): h3_gn_slots
     const int64_t nslot = (int64_t)gn_fimg * ntile * SPT;
     const int64_t slot = ((int64_t)f * ntile + tt) * SPT + wc;
     float2* dst = reinterpret_cast<float2*>(gnp) + ((int64_t)b * nslot + slot) * (g.Cout / 4) + (n0 + wr * 32) / 4 + lg;
@@ -583,26 +564,26 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
                                                               bf16* __restrict__ y1, bf16* __restrict__ y2, ConvGeom g,
                                                               int tiles_x, int TH, float* __restrict__ gnp = nullptr,
                                                               int gn_fimg = 1) {
-  // NJv = 7 (H3_BIG): tiles of up to 448 pixels ((TH+2) <= 16 halo rows of H3_P), 64 co x 112 px per wave: 11
+  // NJv = 7: tiles of up to 448 pixels ((TH+2) <= 16 halo rows of H3_P), 64 co x 112 px per wave: 11
   // fragment reads per 28 MFMAs per tap (0.39 per MFMA instead of 0.5) and the 36-KiB weight chunk staged once
   // per 448 instead of 256 pixels; 77 KiB of LDS, still 2 blocks per CU
-  static_assert(NJv == 4 || (NJv == 7 && H3_SQ && H3_DMA), "big tiles need square wave tiles and DMA staging");
+  static_assert(NJv == 4 || NJv == 7, "256- or 448-pixel tiles");
   constexpr int NROWS = (NJv == 7 ? 16 : 10) * H3_P;
   __shared__ __attribute__((aligned(16))) bf16 sh[NROWS * H3_LD];
   __shared__ __attribute__((aligned(16))) bf16 sw[9 * H3_BN * H3_LD];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  // wave tile: H3_SQ (round 3) 64 co x 16 NJv px = 4 x NJv MFMA tiles per wave (8 fragment reads per 16 MFMAs per
+  // wave tile (round 3): 64 co x 16 NJv px = 4 x NJv MFMA tiles per wave (8 fragment reads per 16 MFMAs per
   // tap at NJv = 4); else 32 co x 128 px = 2 x 8 (10 reads per 16 MFMAs: the 4 waves' reads exceeded the LDS
   // array's 256 B/clk)
-  constexpr int NI = H3_SQ ? 4 : 2, NJ = H3_SQ ? NJv : 8;
-  const int wr = H3_SQ ? 0 : wid >> 1, wc = H3_SQ ? wid : wid & 1;
+  constexpr int NI = 4, NJ = NJv;
+  const int wr = 0, wc = wid;
   constexpr int PXW = 16 * NJ;  // pixels per wave
   // 1-D grid (h3_grid): the ncob co blocks of a (image, tile) run back to back on ONE XCD (linear id mod 8), so
   // its input halo is fetched into that XCD's L2 once (co-block-slowest order re-read every halo ncob times)
   const int ntile = tiles_x * ((g.Ho + TH - 1) / TH), ncob = g.Cout / H3_BN;
   const int L = blockIdx.x, jx = L >> 3;
-  const int cb = H3_XCD ? jx % ncob : L / (gridDim.x / ncob);
-  const int tflat = H3_XCD ? (jx / ncob) * 8 + (L & 7) : L % (gridDim.x / ncob);
+  const int cb = jx % ncob;
+  const int tflat = (jx / ncob) * 8 + (L & 7);
   if (tflat >= g.Nb * ntile) return;  // padded items (whole block)
   const int n = tflat / ntile, tt = tflat - n * ntile;
   const int ty = tt / tiles_x, tx = tt - ty * tiles_x;
@@ -613,7 +594,6 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
   const int Cin = g.C1 + g.C2;
   const int nchunk = Cin / 32;
 
-#if H3_DMA
   // stage one 32-channel chunk by buffer-LDS-DMA (no registers, no address VALU per element beyond one per
   // 16-B piece): 1-KiB pieces of 16 LDS rows, each lane fetching the global chunk that the row swizzle puts in
   // its slot (chunk = slot ^ ((row >> 1) & 2)); halo rows outside the tile / image read as zeros (out-of-range
@@ -657,50 +637,6 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
-#else
-  // stage one 32-channel chunk: global -> registers -> LDS (transient registers; the second
-  // co-resident block computes while this one loads)
-  auto stage = [&](int ch) {
-    const int c0 = ch * 32;
-    const bf16* src;
-    int cs, cc;
-    if (c0 < g.C1) { src = x1; cs = g.C1; cc = c0; } else { src = x2; cs = g.C2; cc = c0 - g.C1; }
-    bf16x8 hreg[H3_HPT], wreg[H3_WPT];
-#pragma unroll
-    for (int k = 0; k < H3_HPT; ++k) {
-      const int e = tid + k * 256;
-      bf16x8 v = {};
-      if (e < HP * 4) {
-        const int hp = e >> 2, part = e & 3;
-        const int r = hp / HWd, c = hp - r * HWd;
-        const int iy = y0 - 1 + r, ix = x0 - 1 + c;
-        if ((unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi)
-          v = *reinterpret_cast<const bf16x8*>(src + (((int64_t)n * g.Hi + iy) * g.Wi + ix) * cs + cc + part * 8);
-      }
-      hreg[k] = v;
-    }
-#pragma unroll
-    for (int k = 0; k < H3_WPT; ++k) {
-      const int e = tid + k * 256;
-      const int row = e >> 2, part = e & 3;      // row = tap*BN + co
-      const int tap = row / H3_BN, co = row - tap * H3_BN;
-      wreg[k] = *reinterpret_cast<const bf16x8*>(w + ((int64_t)(n0 + co) * 9 + tap) * Cin + c0 + part * 8);
-    }
-#pragma unroll
-    for (int k = 0; k < H3_HPT; ++k) {
-      const int e = tid + k * 256;
-      if (e < HP * 4) {
-        const int hp = e >> 2, r = hp / HWd, c = hp - r * HWd;
-        *reinterpret_cast<bf16x8*>(sh + h3_off(r * H3_P + c, e & 3)) = hreg[k];
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < H3_WPT; ++k) {
-      const int e = tid + k * 256;
-      *reinterpret_cast<bf16x8*>(sw + h3_off(e >> 2, e & 3)) = wreg[k];
-    }
-  };
-#endif
 
   f32x4 acc[NI][NJ];
 #pragma unroll
@@ -739,7 +675,6 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
     if (ch) __syncthreads();  // previous chunk fully consumed
     stage(ch);
     __syncthreads();
-#if H3_PIPE
     // the 10 fragment reads of tap t+1 are issued between the 16 MFMAs of tap t (two register sets), so no
     // MFMA waits on a read issued just before it (the compiler's order was read -> wait -> 2 MFMAs)
     bf16x8 fa[2][NI], fb[2][NJ];
@@ -751,7 +686,6 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
       for (int j = 0; j < NJ; ++j) fb[b][j] = *reinterpret_cast<const bf16x8*>(sh + boff[j][kx] + ky * H3_P * H3_LD);
     };
     rd(0, 0);
-    if (H3_PRIO) __builtin_amdgcn_s_setprio(1);  // A/B knob: the MFMA phase at priority 1 (the co-resident block stages)
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int b = tap & 1;
@@ -772,23 +706,6 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (H3_PRIO) __builtin_amdgcn_s_setprio(0);
-#else
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int ky = tap / 3, kx = tap - ky * 3;
-      bf16x8 af[NI];
-#pragma unroll
-      for (int i = 0; i < NI; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(sw + aoff[i] + tap * H3_BN * H3_LD);
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(sh + boff[j][kx] + ky * H3_P * H3_LD);
-#pragma unroll
-        for (int i = 0; i < NI; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][j], 0, 0, 0);
-      }
-    }
-#endif
   }
   h3_epilogue<NI, NJ>(acc, pyx, g, bias, res, res2, y1, y2, gnp, gn_fimg, n, tt, ntile, y0, x0, n0, wr, wc, lane);
 }
@@ -885,7 +802,6 @@ __global__ __launch_bounds__(256, 2) void convs2_bf16_kernel(const bf16* __restr
   const int nchunk = Cin / 32;
   constexpr int WPT = 4 * H3_BN * 4 / 256;  // weight vectors per thread (4 taps x 64 co x 4 vectors)
 
-#if H3_DMA
   // stage s by buffer-LDS-DMA (as conv3x3_bf16_kernel): halo of the (parity sub-)image and the 4 live taps'
   // weights for one 32-channel chunk
   (void)WPT;
@@ -923,48 +839,6 @@ __global__ __launch_bounds__(256, 2) void convs2_bf16_kernel(const bf16* __restr
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
-#else
-  // stage s: halo of the (parity sub-)image and the 4 live taps' weights for one 32-channel chunk
-  auto stage = [&](int ch, int a, int b, int by, int bx) {
-    const int c0 = ch * 32;
-    bf16x8 hreg[H3_HPT], wreg[WPT];
-#pragma unroll
-    for (int k = 0; k < H3_HPT; ++k) {
-      const int e = tid + k * 256;
-      bf16x8 v = {};
-      if (e < HP * 4) {
-        const int hp = e >> 2, part = e & 3;
-        const int r = hp / HWd, c = hp - r * HWd;
-        const int Y = y0 - 1 + r, X = x0 - 1 + c;
-        const int iy = UP ? Y : 2 * Y + a, ix = UP ? X : 2 * X + b;
-        if ((unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi)
-          v = *reinterpret_cast<const bf16x8*>(x + (((int64_t)n * g.Hi + iy) * g.Wi + ix) * Cin + c0 + part * 8);
-      }
-      hreg[k] = v;
-    }
-#pragma unroll
-    for (int k = 0; k < WPT; ++k) {
-      const int e = tid + k * 256;
-      const int row = e >> 2, part = e & 3;  // row = t * 64 + co
-      const int t = row / H3_BN, co = row - t * H3_BN;
-      const int tap = (by + 2 * (t >> 1)) * 4 + bx + 2 * (t & 1);
-      wreg[k] = *reinterpret_cast<const bf16x8*>(w + ((int64_t)(n0 + co) * 16 + tap) * Cin + c0 + part * 8);
-    }
-#pragma unroll
-    for (int k = 0; k < H3_HPT; ++k) {
-      const int e = tid + k * 256;
-      if (e < HP * 4) {
-        const int hp = e >> 2, r = hp / HWd, c = hp - r * HWd;
-        *reinterpret_cast<bf16x8*>(sh + h3_off(r * H3_P + c, e & 3)) = hreg[k];
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < WPT; ++k) {
-      const int e = tid + k * 256;
-      *reinterpret_cast<bf16x8*>(sw + h3_off(e >> 2, e & 3)) = wreg[k];
-    }
-  };
-#endif
 
   f32x4 acc[2][8];
 #pragma unroll
@@ -1125,129 +999,6 @@ __device__ __forceinline__ void cw_taps(const char* sh, const char* sw, const in
     __builtin_amdgcn_sched_barrier(0);
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
-
-template <int TW>
-__global__ __launch_bounds__(256, 2) void conv3x3w_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
-                                                          const bf16* __restrict__ w, const float* __restrict__ bias,
-                                                          const bf16* __restrict__ res, const bf16* __restrict__ res2,
-                                                          bf16* __restrict__ y1, bf16* __restrict__ y2, ConvGeom g,
-                                                          int tiles_x, int TH) {
-  __shared__ __attribute__((aligned(1024))) char lds[(CW_HROWS + CW_WROWS) * 64];
-  char* sh = lds;
-  char* sw = lds + CW_HROWS * 64;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int lr = lane & 15, lg = lane >> 4;
-  const int n = blockIdx.y;
-  const int ty = blockIdx.x / tiles_x, tx = blockIdx.x - ty * tiles_x;
-  const int y0 = ty * TH, x0 = tx * TW;
-  constexpr int HWd = TW + 2;
-  const int HP = (TH + 2) * HWd;
-  const int n0 = blockIdx.z * 64;
-  const int Cin = g.C1 + g.C2;
-  const int nchunk = Cin / 32;
-
-  // LDS-DMA through buffer descriptors (32-bit per-lane offsets, out-of-range -> zeros): halo piece
-  // k of wave w = rows 16*(w + 4k) + lane/4, 16-B slot lane&3 of each row
-  const int prow = lane >> 2, pslot = lane & 3;
-  const int hpieces = (HP + 15) >> 4;
-  int hpix[CW_HPW];  // source pixel (iy*Wi + ix) of this lane's row in halo piece k, -1 = zero row
-#pragma unroll
-  for (int k = 0; k < CW_HPW; ++k) {
-    const int row = 16 * (wid + 4 * k) + prow;
-    const int hy = row / HWd, hx = row - (row / HWd) * HWd;
-    const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
-    hpix[k] = (row < HP && (unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi) ? iy * g.Wi + ix : -1;
-  }
-  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(w + (int64_t)n0 * 9 * Cin), (short)0, 64 * 9 * Cin * 2, 0x00020000);
-
-  auto stage = [&](int ch) {
-    const int c0 = ch * 32;
-    const bf16* src;
-    int cs, cc;
-    if (c0 < g.C1) { src = x1; cs = g.C1; cc = c0; } else { src = x2; cs = g.C2; cc = c0 - g.C1; }
-    const int64_t img_elems = (int64_t)g.Hi * g.Wi * cs;
-    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(src + (int64_t)n * img_elems + cc), (short)0, (int)(img_elems * 2 - cc * 2), 0x00020000);
-#pragma unroll
-    for (int k = 0; k < CW_HPW; ++k) {
-      const int q = wid + 4 * k;
-      if (q < hpieces) {  // wave-uniform
-        const int chunk = pslot ^ cw_swz(16 * q + prow);
-        const int vo = hpix[k] >= 0 ? (hpix[k] * cs + chunk * 8) * 2 : 0x7ffffff0;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)(sh + q * 1024), 16, vo,
-                                                 0, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < CW_WPW; ++k) {
-      const int q = wid + 4 * k;
-      const int row = 16 * q + prow;  // tap*64 + co
-      const int chunk = pslot ^ cw_swz(row);
-      const int vo = (((row & 63) * 9 + (row >> 6)) * Cin + c0 + chunk * 8) * 2;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(sw + q * 1024), 16, vo, 0,
-                                               0, 0);
-    }
-  };
-
-  f32x4 acc[4][8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // halo row of tap (0,0) for fragment group j (pixels past TH*TW read row 0; results discarded)
-  int hoff[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int p = wid * 128 + j * 16 + lr;
-    const int py = p / TW, px = p - (p / TW) * TW;
-    hoff[j] = p < TH * TW ? py * HWd + px : 0;
-  }
-  for (int ch = 0; ch < nchunk; ++ch) {
-    if (ch) __syncthreads();  // all fragment reads of the previous chunk done before the DMA overwrites
-    stage(ch);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    cw_taps<TW>(sh, sw, hoff, lr, lg, acc);
-  }
-  // epilogue: lane holds co = n0 + i*16 + 4*lg + r of tile pixel wid*128 + j*16 + lr
-  const int Co2 = g.Cout - g.Co1;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int p = wid * 128 + j * 16 + lr;
-    if (p >= TH * TW) continue;
-    const int oy = y0 + p / TW, ox = x0 + (p - (p / TW) * TW);
-    if (oy >= g.Ho || ox >= g.Wo) continue;
-    const int64_t m = ((int64_t)n * g.Ho + oy) * g.Wo + ox;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int co = n0 + i * 16 + lg * 4;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (bias) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += bias[co + r];
-      }
-      if (co < g.Co1) {
-        if (res) {
-          float rv[4];
-          load4(res + m * g.Co1 + co, rv);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] += rv[r];
-        }
-        store4(y1 + m * g.Co1 + co, v);
-      } else {
-        if (res2) {
-          float rv[4];
-          load4(res2 + m * Co2 + (co - g.Co1), rv);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] += rv[r];
-        }
-        store4(y2 + m * Co2 + (co - g.Co1), v);
-      }
-    }
-  }
 }
 
 // ----------------------------------------------------------------------------------------
@@ -1651,15 +1402,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
 // epilogue (~40 % of conv3x3p's time at one wave per SIMD, where it could not overlap the MFMAs) runs beside the next
 // item's MFMAs.  Both roles pass exactly the same barriers.  LDS: 2 stages x 61 KiB + a 34 KiB staging tile.
 // ----------------------------------------------------------------------------------------
-#ifndef WS_TOUCH
-#define WS_TOUCH 1  // L2 touch of the next item's halo lines a step ahead of its stage DMA
-#endif
-#ifndef WS_PRIO
-#define WS_PRIO 0  // A/B knob (see the kernel)
-#endif
-#ifndef WS_RW
-#define WS_RW 1  // resident weights when Cin = 64 and one co block (the level-0 64 -> 64 conv)
-#endif
+// (Round 5, removed: s_setprio for the loader or the compute waves, within the spread -- profiles/r5_prio_ab.txt.)
 constexpr int WS_PITCH = 40;                               // halo row pitch (pixels): ky steps keep the swizzle
 constexpr int WS_MAXTH = 8;                                // tile rows: (8 + 2) * 40 = 400 halo rows
 constexpr int WS_HROWS = (WS_MAXTH + 2) * WS_PITCH;        // 400
@@ -1696,9 +1439,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3ws_kernel(const bf16* __restric
   int* qslot = reinterpret_cast<int*>(lds + WS_LDS + 1024);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const bool loader = wid >= 4;  // wave-uniform role
-  // A/B knob WS_PRIO: static s_setprio 1 for the loader waves (1: the second-dispatched half, which loses the VALU
-  // arbitration by age) or for the compute waves (2)
-  if (WS_PRIO && (__builtin_amdgcn_readfirstlane(tid) >= 256) == (WS_PRIO == 1)) __builtin_amdgcn_s_setprio(1);
   const int wl = wid & 3;
   const int lr = lane & 15, lg = lane >> 4;
   const int Cin = g.C1 + g.C2, nchunk = Cin / 32;
@@ -1764,11 +1504,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3ws_kernel(const bf16* __restric
     const int hy = row / WS_PITCH, hx = row - hy * WS_PITCH;
     hrel[k] = (hy < TH + 2 && hx < TW + 2) ? (hy << 16) | hx : -1;
   }
-  // RW (resident weights, WS_RW): with 64 input channels and one co block the two weight chunks never change, so
+  // RW (resident weights): with 64 input channels and one co block the two weight chunks never change, so
   // they are staged once and the per-step DMA carries only the halo chunk (25 KB instead of 61 KB: the LDS-DMA
   // fill rate per CU, not HBM, bounded the step).  The layout is the same 156 KB rearranged: weight chunks 0 / 1 at
   // [0, 73728), halo stages at 73728 + st * 25600 (else stage st = halo + weights at st * WS_STAGE).
-  const bool rw = WS_RW && Cin == 64 && ncob == 1;
+  const bool rw = Cin == 64 && ncob == 1;
   auto hbase = [&](int st) { return lds + (rw ? 2 * WS_WROWS * 64 + st * WS_HROWS * 64 : st * WS_STAGE); };
   auto wbase = [&](int st, int ch) { return rw ? lds + ch * WS_WROWS * 64 : lds + st * WS_STAGE + WS_HROWS * 64; };
   auto issue_w = [&](int cb, int ch, char* dst) {  // the weight chunk ch of co block cb
@@ -1844,7 +1584,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3ws_kernel(const bf16* __restric
     }
   };
   const bool has_res = (res != nullptr) || (res2 != nullptr);
-  // L2 touch of the next item's input halo (WS_TOUCH): one 4-B load per halo pixel line of x1, issued at an item's
+  // L2 touch of the next item's input halo: one 4-B load per halo pixel line of x1, issued at an item's
   // first step, so the stage DMA of that item -- a step later -- finds its lines in L2 instead of waiting out HBM
   // latency with one stage in flight.  Covers every channel of a pixel when C1 * 2 <= 128 B (level 0).  The loads
   // go LDS-direct into a never-read 256-B row per loader wave: no VGPRs held while they fly.
@@ -1989,7 +1729,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3ws_kernel(const bf16* __restric
     issue_stage(it0, 0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int it = it0, ch = 0, s = 0, prev_it = -1, k = 0, succ = nitems_pad;
-    const bool do_touch = WS_TOUCH && g.C1 * 2 <= 128 && nchunk >= 2;
+    const bool do_touch = g.C1 * 2 <= 128 && nchunk >= 2;
     while (true) {
       __builtin_amdgcn_s_barrier();  // stage s landed; stage s - 1 consumed; staging of prev_it written (ch == 0)
       if (ch == 0) {
@@ -2084,18 +1824,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3ws_kernel(const bf16* __restric
 // resource covers the block's own 128 rows only, so M * K is not limited to 2^31 bytes.
 // ----------------------------------------------------------------------------------------
 constexpr int G1_BM = 128;
-#ifndef G1_NS1
-#define G1_NS1 1   // A/B knob: single-stage K = 64 variant (0 = always two stages)
-#endif
-#ifndef G1_NT
-#define G1_NT 0    // A/B knob: non-temporal output stores
-#endif
-#ifndef G1_XCD
-#define G1_XCD 1   // A/B knob: XCD-grouped co blocks (0 = co-block-fastest linear order)
-#endif
-#ifndef G1_BIGM
-#define G1_BIGM 1  // A/B knob: gemm1x1 for M * K >= 2^31 bytes too (0 = generic conv there, round 2)
-#endif
+// (Measured and removed: non-temporal output stores -- GEMMs 5 % faster alone, whole step unchanged (round 3) and
+// within the spread on the F = 120 leg (round 5, profiles/r5f_g1nt_f120_ab.txt); co-block-fastest block order.)
 __device__ __forceinline__ int g1_off(int row, int chunk) { return (row << 7) + ((chunk ^ (row & 7)) << 4); }
 
 template <int BN, int NS>
@@ -2116,8 +1846,8 @@ __global__ __launch_bounds__(256, NS == 1 ? 4 : 2) void gemm1x1_kernel(const bf1
   // 1-D grid: the ncb co blocks of a pixel tile are dealt to ONE XCD back to back (linear id mod 8 = XCD), so
   // the tile's X rows are fetched into that XCD's L2 once instead of into up to ncb different L2s
   const int ncb = Cout / BN, L = blockIdx.x, jx = L >> 3;
-  const int cb = G1_XCD ? jx % ncb : L % ncb;
-  const int tile = G1_XCD ? (jx / ncb) * 8 + (L & 7) : L / ncb;
+  const int cb = jx % ncb;
+  const int tile = (jx / ncb) * 8 + (L & 7);
   if (tile * G1_BM >= M) return;  // padded tiles (whole block)
   const int m0 = tile * G1_BM, n0 = cb * BN;
   const int prow = lane >> 3, pslot = lane & 7;
@@ -2229,27 +1959,10 @@ __global__ __launch_bounds__(256, NS == 1 ? 4 : 2) void gemm1x1_kernel(const bf1
 #pragma unroll
       for (int q = 0; q < 8; ++q) v[q] = (bf16)((float)v[q] + (float)rv[it][q]);
     }
-    if (G1_NT) stnt16(dst, v);
-    else *reinterpret_cast<bf16x8*>(dst) = v;
+    *reinterpret_cast<bf16x8*>(dst) = v;
   }
 }
 
-// tile of the wide-wave conv: TW in {32, 36}, TH*TW <= 512, (TH+2)(TW+2) <= 640; maximise useful /
-// computed pixels (computed = 512 per tile), fewest tiles on ties
-static void cw_tile(int Ho, int Wo, int& TH, int& TW) {
-  double best = -1.0;
-  int bt = 1 << 30;
-  const int cands[2] = {32, 36};
-  for (int c = 0; c < 2; ++c) {
-    const int tw = cands[c];
-    for (int th = 1; th * tw <= 512; ++th) {
-      if ((th + 2) * (tw + 2) > CW_HROWS) break;
-      const int ntile = (int)(cdiv(Ho, th) * cdiv(Wo, tw));
-      const double util = (double)Ho * Wo / ((double)ntile * 512);
-      if (util > best + 1e-9 || (util > best - 1e-9 && ntile < bt)) { best = util; bt = ntile; TH = th; TW = tw; }
-    }
-  }
-}
 
 // ----------------------------------------------------------------------------------------
 // 3x3 / stride 1 / pad 1 conv (bf16), v2: persistent, software-pipelined halo conv.
@@ -2272,159 +1985,6 @@ static_assert(C2_NI % 4 == 0, "glds instructions must split evenly over the 4 wa
 __device__ __attribute__((aligned(16))) bf16 c2_zero_page[8] = {};
 
 __device__ __forceinline__ int c2_swz(int row) { return (row >> 2) & 3; }
-
-__global__ __launch_bounds__(256, 1) void conv3x3v2_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
-                                                           const bf16* __restrict__ w, const float* __restrict__ bias,
-                                                           const bf16* __restrict__ res, const bf16* __restrict__ res2,
-                                                           bf16* __restrict__ y1, bf16* __restrict__ y2, ConvGeom g,
-                                                           int TH, int TW, int tiles_x, int tiles_y, int ncob,
-                                                           int nitems) {
-  __shared__ __attribute__((aligned(1024))) char lds[2 * C2_STAGE_B];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 1, wc = wid & 1;
-  const int lr = lane & 15, lg = lane >> 4;
-  const int Cin = g.C1 + g.C2;
-  const int nchunk = Cin / 32;
-  const int HWd = TW + 2, HP = (TH + 2) * HWd;
-  const int per_img = tiles_x * tiles_y;
-  // this block's items: contiguous range (neighbouring tiles share halo rows and weights in L2)
-  const int ipb = (nitems + gridDim.x - 1) / gridDim.x;
-  const int it0 = blockIdx.x * ipb, it1 = min(nitems, it0 + ipb);
-  const int nsteps = (it1 > it0 ? it1 - it0 : 0) * nchunk;
-
-  // per-lane pixel offsets of the 8 B-fragment groups (independent of the item)
-  int hoff[8];
-  int pyx[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int p = wc * 128 + j * 16 + lr;
-    const int py = p / TW, px = p - (p / TW) * TW;
-    const bool in = p < TH * TW;
-    hoff[j] = in ? py * HWd + px : 0;
-    pyx[j] = in ? (py << 16) | px : -1;
-  }
-
-  auto item_geo = [&](int it, int& n, int& y0, int& x0, int& n0) {
-    const int cob = it % ncob, t = it / ncob;
-    n = t / per_img;
-    const int r = t - n * per_img;
-    y0 = (r / tiles_x) * TH;
-    x0 = (r % tiles_x) * TW;
-    n0 = cob * 64;
-  };
-  auto issue = [&](int s) {  // glds for step s into stage s & 1
-    const int it = it0 + s / nchunk, ch = s % nchunk;
-    int n, y0, x0, n0;
-    item_geo(it, n, y0, x0, n0);
-    const int c0 = ch * 32;
-    const bf16* src;
-    int cs, cc;
-    if (c0 < g.C1) { src = x1; cs = g.C1; cc = c0; } else { src = x2; cs = g.C2; cc = c0 - g.C1; }
-    char* base = lds + (s & 1) * C2_STAGE_B;
-#pragma unroll
-    for (int k = 0; k < C2_NPW; ++k) {
-      const int i = k * 4 + wid;
-      const int rsub = lane >> 2, slot = lane & 3;
-      const bf16* gp;
-      if (i < C2_HROWS / 16) {
-        const int row = i * 16 + rsub;
-        const int chunk = slot ^ c2_swz(row);
-        gp = c2_zero_page;
-        if (row < HP) {
-          const int hy = row / HWd, hx = row - (row / HWd) * HWd;
-          const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
-          if ((unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi)
-            gp = src + (((int64_t)n * g.Hi + iy) * g.Wi + ix) * cs + cc + chunk * 8;
-        }
-      } else {
-        const int row = (i - C2_HROWS / 16) * 16 + rsub;  // tap*64 + co
-        const int chunk = slot ^ c2_swz(row);
-        const int tap = row >> 6, co = row & 63;
-        gp = w + ((int64_t)(n0 + co) * 9 + tap) * Cin + c0 + chunk * 8;
-      }
-      __builtin_amdgcn_global_load_lds((const void*)gp, (__attribute__((address_space(3))) void*)(base + i * 1024), 16,
-                                       0, 0);
-    }
-  };
-
-  f32x4 acc[2][8];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  if (nsteps > 0) issue(0);
-  if (nsteps > 1) issue(1);
-  for (int s = 0; s < nsteps; ++s) {
-    if (s + 1 < nsteps) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");  // step s landed, s+1 in flight
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    const char* hb = lds + (s & 1) * C2_STAGE_B;
-    const char* wb = hb + C2_HALO_B;
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int ky = tap / 3, kx = tap - ky * 3;
-      bf16x8 af[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int row = tap * 64 + wr * 32 + i * 16 + lr;
-        af[i] = *reinterpret_cast<const bf16x8*>(wb + row * 64 + ((lg ^ c2_swz(row)) << 4));
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int row = hoff[j] + ky * HWd + kx;
-        const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(hb + row * 64 + ((lg ^ c2_swz(row)) << 4));
-        acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bfr, acc[0][j], 0, 0, 0);
-        acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bfr, acc[1][j], 0, 0, 0);
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // stage (s & 1) released
-    if (s + 2 < nsteps) issue(s + 2);
-    if ((s % nchunk) == nchunk - 1) {
-      // epilogue of the item: lane holds co = n0 + wr*32 + i*16 + 4*lg + r of pixel group j
-      int n, y0, x0, n0;
-      item_geo(it0 + s / nchunk, n, y0, x0, n0);
-      const int Co2 = g.Cout - g.Co1;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (pyx[j] < 0) continue;
-        const int oy = y0 + (pyx[j] >> 16), ox = x0 + (pyx[j] & 0xffff);
-        if (oy < g.Ho && ox < g.Wo) {
-          const int64_t m = ((int64_t)n * g.Ho + oy) * g.Wo + ox;
-#pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            const int co = n0 + wr * 32 + i * 16 + lg * 4;
-            float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-            if (bias) {
-#pragma unroll
-              for (int r = 0; r < 4; ++r) v[r] += bias[co + r];
-            }
-            if (co < g.Co1) {
-              if (res) {
-                float rv[4];
-                load4(res + m * g.Co1 + co, rv);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] += rv[r];
-              }
-              store4(y1 + m * g.Co1 + co, v);
-            } else {
-              if (res2) {
-                float rv[4];
-                load4(res2 + m * Co2 + (co - g.Co1), rv);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] += rv[r];
-              }
-              store4(y2 + m * Co2 + (co - g.Co1), v);
-            }
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
-  }
-}
 
 // tile shape for an Ho x Wo image: TW in {32, 36, 48}, TH*TW <= 256, (TH+2)(TW+2) <= 384; maximise
 // useful / computed pixels (fewest tiles on ties)
@@ -2668,11 +2228,8 @@ __device__ __forceinline__ int wgb_swz(int r) {  // XOR on 4-element chunk index
 // budget the compiler kept the accumulators in VGPRs and copied each one into a[0:3] before its MFMA and back after
 // (AGPR-form MFMAs: 64 v_accvgpr_write + 64 v_accvgpr_read + s_nop per 16 MFMAs in the BM = 256 loop, 244 + 40
 // registers); capped: VGPR-form MFMAs, no copies, 178 / 122 / 68 registers at BM = 256 / 128 / 64.
-#ifndef WW_WPE
-#define WW_WPE 2
-#endif
 template <int BM, bool BIAS = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WW_WPE))) void wgrad_wide_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void wgrad_wide_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
                                                          const bf16* __restrict__ dy1, const bf16* __restrict__ dy2,
                                                          float* __restrict__ slab, float* __restrict__ bslab, ConvGeom g,
                                                          int M, int px_per_split) {
@@ -2861,139 +2418,6 @@ constexpr int W3_P = 48;
 __device__ __forceinline__ int w3_swz_dy(int r) { return (((r >> 1) & 1) << 2) | (((r >> 3) & 1) << 3); }
 __device__ __forceinline__ int w3_swz_x(int r) { return ((r >> 3) & 1) << 2; }
 
-__global__ __launch_bounds__(256, 2) void wgrad3x3_bf16_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
-                                                               const bf16* __restrict__ dy1, const bf16* __restrict__ dy2,
-                                                               float* __restrict__ slab, ConvGeom g, int tiles_x,
-                                                               int ntiles) {
-  __shared__ __attribute__((aligned(16))) bf16 sdy[W3_TH * W3_TW * 64];   // 32 KB, 128-B rows
-  __shared__ __attribute__((aligned(16))) bf16 shx[(W3_TH + 2) * W3_P * 32];  // 30 KB, 64-B rows
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int cot0 = (wid >> 1) * 2, cit = wid & 1;
-  const int co0 = blockIdx.x * 64, ci0 = blockIdx.y * 32;
-  const int Cin = g.C1 + g.C2;
-  const bf16* xs; int xcs, xcc;
-  if (ci0 < g.C1) { xs = x1; xcs = g.C1; xcc = ci0; } else { xs = x2; xcs = g.C2; xcc = ci0 - g.C1; }
-  const bf16* ys; int ycs, ycc;
-  const int Co2 = g.Cout - g.Co1;
-  if (co0 < g.Co1) { ys = dy1; ycs = g.Co1; ycc = co0; } else { ys = dy2; ycs = Co2; ycc = co0 - g.Co1; }
-  const int tiles_per_img = tiles_x * ((g.Ho + W3_TH - 1) / W3_TH);
-
-  f32x4 acc[2][9];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int lr = lane & 15, lg = lane >> 4, q = lr >> 2, pp = lr & 3;
-  // per-lane fragment offsets (elements); row steps of 32 dY pixels / W3_P halo pixels keep the swizzles
-  int aoff[2][2], boff[2][3];
-#pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    const int r = lg * 8 + half * 4 + q;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) aoff[i][half] = r * 64 + ((((cot0 + i) * 4 + pp) ^ w3_swz_dy(r)) * 4);
-#pragma unroll
-    for (int kx = 0; kx < 3; ++kx) boff[half][kx] = (r + kx) * 32 + (((cit * 4 + pp) ^ w3_swz_x(r + kx)) * 4);
-  }
-  // the next tile's dY / halo vectors are loaded into registers (unpredicated: clamped address + select)
-  // while the current tile is consumed, and written to LDS after the barrier that ends its reads
-  bf16x8 yv[8], hv[6];
-  auto gload = [&](int tile) {
-    const int n = tile / tiles_per_img;
-    const int rem = tile - n * tiles_per_img;
-    const int ty = rem / tiles_x, tx = rem - ty * tiles_x;
-    const int y0 = ty * W3_TH, x0 = tx * W3_TW;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {       // dY: 256 px x 8 vectors
-      const int e = tid + k * 256;
-      const int p = e >> 3, part = e & 7;
-      const int oy = y0 + (p >> 5), ox = x0 + (p & 31);
-      const bool ok = oy < g.Ho && ox < g.Wo;
-      const bf16x8 v = *reinterpret_cast<const bf16x8*>(
-          ys + (ok ? (((int64_t)n * g.Ho + oy) * g.Wo + ox) * ycs : 0) + ycc + part * 8);
-      yv[k] = ok ? v : bf16x8{};
-    }
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {       // halo: 340 px x 4 vectors
-      const int e = tid + k * 256;
-      const int hp = e >> 2, part = e & 3;
-      const int r = hp / W3_HW, c = hp - r * W3_HW;
-      const int iy = y0 - 1 + r, ix = x0 - 1 + c;
-      const bool ok = e < W3_NPIX * 4 && (unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi;
-      const bf16x8 v = *reinterpret_cast<const bf16x8*>(
-          xs + (ok ? (((int64_t)n * g.Hi + iy) * g.Wi + ix) * xcs : 0) + xcc + part * 8);
-      hv[k] = ok ? v : bf16x8{};
-    }
-  };
-  if ((int)blockIdx.z < ntiles) gload(blockIdx.z);
-  for (int tile = blockIdx.z; tile < ntiles; tile += gridDim.z) {
-    __syncthreads();
-    {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int e = tid + k * 256;
-        const int p = e >> 3, part = e & 7;  // chunk pair (2part, 2part+1) of 8-B chunks
-        const int ch = (part * 2) ^ w3_swz_dy(p);
-        *reinterpret_cast<bf16x8*>(sdy + p * 64 + ch * 4) = yv[k];
-      }
-#pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        const int e = tid + k * 256;
-        if (e < W3_NPIX * 4) {
-          const int hp = e >> 2, part = e & 3;
-          const int r = hp / W3_HW, row = r * W3_P + (hp - r * W3_HW);
-          const int ch = (part * 2) ^ w3_swz_x(row);
-          *reinterpret_cast<bf16x8*>(shx + row * 32 + ch * 4) = hv[k];
-        }
-      }
-    }
-    __syncthreads();
-    if (tile + (int)gridDim.z < ntiles) gload(tile + gridDim.z);
-#pragma unroll 1
-    for (int py = 0; py < W3_TH; ++py) {
-      // A = dY^T (rows co, K = 32 pixels of row py): tr reads, rows = pixel py*32 + k
-      bf16x8 af[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-#pragma unroll
-        for (int half = 0; half < 2; ++half) {
-          const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(sdy + aoff[i][half] + py * 32 * 64));
-#pragma unroll
-          for (int e = 0; e < 4; ++e) af[i][half * 4 + e] = __builtin_bit_cast(bf16, (short)v[e]);
-        }
-      }
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const int ky = tap / 3, kx = tap - ky * 3;
-        bf16x8 bfr;
-#pragma unroll
-        for (int half = 0; half < 2; ++half) {
-          const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (LDS_PTR(s16x4))(shx + boff[half][kx] + (py + ky) * W3_P * 32));
-#pragma unroll
-          for (int e = 0; e < 4; ++e) bfr[half * 4 + e] = __builtin_bit_cast(bf16, (short)v[e]);
-        }
-        acc[0][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bfr, acc[0][tap], 0, 0, 0);
-        acc[1][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bfr, acc[1][tap], 0, 0, 0);
-      }
-    }
-  }
-  // D[co][ci] per tap: lane col lr -> ci, rows 4lg+r -> co
-  const int K = 9 * Cin;
-  float* out = slab + (int64_t)blockIdx.z * g.Cout * K;
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int ci = ci0 + cit * 16 + lr;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = co0 + (cot0 + i) * 16 + lg * 4 + r;
-        out[(int64_t)co * K + tap * Cin + ci] = acc[i][tap][r];
-      }
-    }
-}
-
 // Same weight gradient with blocks of 64 co x 64 ci and 8 waves (one block per CU, two waves per SIMD; wave w:
 // co tiles {2*(w>>2), 2*(w>>2)+1} x ci tile w&3).  The wgrad is bound by the per-CU load rate (~7.6 B/cycle
 // with plain 16-B loads: 54 KB per 8 x 32 tile of a 64 x 32 block, the dY tile re-read by every ci block):
@@ -3003,10 +2427,8 @@ constexpr int W3_PLANE = (W3_TH + 2) * W3_P * 32;  // halo plane (bf16 elements)
 
 // (Round 3 measured a 4-wave form -- one wave per SIMD, 144 accumulators, all four co tiles per wave -- as neutral,
 // 63.69 vs 63.58 ms conv total per step: fewer LDS reads per MFMA, less latency hiding.  Removed.)
-#ifndef WG_TOUCH
-#define WG_TOUCH 1  // 3x3 wgrad kernels: L2 touch of the tile after next (wgrad3x3c64 415 -> 389 us per launch in the step,
-                    // profiles/r4c7b_bench_ab.txt)
-#endif
+// 3x3 wgrad kernels: L2 touch of the tile after next (wgrad3x3c64 415 -> 389 us per launch in the step,
+// profiles/r4c7b_bench_ab.txt)
 constexpr int WG_NT = 512;  // threads per block
 constexpr int WG_NI = 2;    // co tiles per wave
 __global__ __launch_bounds__(WG_NT, 1) void wgrad3x3c64_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
@@ -3074,9 +2496,9 @@ __global__ __launch_bounds__(WG_NT, 1) void wgrad3x3c64_kernel(const bf16* __res
       hv[k] = ok ? v : bf16x8{};
     }
   };
-  // WG_TOUCH (A/B knob): the dY and input-halo lines of the tile after next, LDS-direct into a never-read row per wave
+  // L2 touch: the dY and input-halo lines of the tile after next, LDS-direct into a never-read row per wave
   // (4 B per 128-B pixel line), so the register prefetch of that tile a step later finds them in L2
-  __shared__ __attribute__((aligned(16))) int tdump[WG_TOUCH ? WG_NT : 1];
+  __shared__ __attribute__((aligned(16))) int tdump[WG_NT];
   auto touch = [&](int tile) {
     const int n = tile / tiles_per_img;
     const int rem = tile - n * tiles_per_img;
@@ -3087,7 +2509,7 @@ __global__ __launch_bounds__(WG_NT, 1) void wgrad3x3c64_kernel(const bf16* __res
         __builtin_amdgcn_make_buffer_rsrc((void*)(ys + n * yimg + ycc), (short)0, (int)(yimg * 2 - ycc * 2), 0x00020000);
     const __amdgpu_buffer_rsrc_t xrs =
         __builtin_amdgcn_make_buffer_rsrc((void*)(xs + n * ximg + xcc), (short)0, (int)(ximg * 2 - xcc * 2), 0x00020000);
-    auto* dst = (__attribute__((address_space(3))) void*)(tdump + (WG_TOUCH ? wid * 64 : 0));
+    auto* dst = (__attribute__((address_space(3))) void*)(tdump + wid * 64);
     {  // dY: 256 pixels
       const int p = tid & 255;
       const int oy = y0 + (p >> 5), ox = x0 + (p & 31);
@@ -3124,7 +2546,7 @@ __global__ __launch_bounds__(WG_NT, 1) void wgrad3x3c64_kernel(const bf16* __res
     }
     __syncthreads();
     if (tile + (int)gridDim.z < ntiles) gload(tile + gridDim.z);
-    if (WG_TOUCH && tile + 2 * (int)gridDim.z < ntiles) touch(tile + 2 * gridDim.z);
+    if (tile + 2 * (int)gridDim.z < ntiles) touch(tile + 2 * gridDim.z);
     // the fragment reads of pixel row py+1 (2 NI + 18) are issued between the 9 NI MFMAs of row py (two register
     // sets; 1 read : 1 MFMA via sched_group_barrier), so no row waits for its LDS reads
     bf16x8 fa[2][WG_NI], fb[2][9];
@@ -3193,7 +2615,7 @@ __global__ __launch_bounds__(WG_NT, 1) void wgrad3x3c64_kernel(const bf16* __res
 }
 
 // Weight gradient of the 4x4 / stride-2 / pad-1 conv (Downsample; the Upsample's weight gradient is the same
-// operation with dOut as the input and x as dY), halo-tiled like wgrad3x3_bf16_kernel on the low-resolution
+// operation with dOut as the input and x as dY), halo-tiled like wgrad3x3c64_kernel on the low-resolution
 // dY grid.  Block = (64 co) x (32 ci chunk) x one input parity (a, b) = its 4 live taps ky = (1-a) + 2t,
 // kx = (1-b) + 2u, whose inputs are the (TH+2) x (TW+2) halo of x_ab[Y][X] = x[2Y+a][2X+b] at offsets
 // (1-a+t, 1-b+u) - the forward's parity split (convs2_bf16_kernel).  Replaces the wide-tile wgrad, which
@@ -3340,147 +2762,6 @@ __global__ __launch_bounds__(256, 2) void wgrads2_bf16_kernel(const bf16* __rest
 // addresses).
 constexpr int W36_TH = 8, W36_TW = 36, W36_HW = W36_TW + 2, W36_NPIX = (W36_TH + 2) * W36_HW;  // 380 halo px
 constexpr int W36_NP = W36_TH * W36_TW;                                                          // 288 px
-
-__global__ __launch_bounds__(256, 2) void wgrad3x3w36_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
-                                                             const bf16* __restrict__ dy1, const bf16* __restrict__ dy2,
-                                                             float* __restrict__ slab, ConvGeom g, int tiles_x,
-                                                             int ntiles) {
-  __shared__ __attribute__((aligned(16))) bf16 sdy[W36_NP * 64];     // 36 KB, 128-B rows
-  __shared__ __attribute__((aligned(16))) bf16 shx[(W36_TH + 2) * W3_P * 32];  // 30 KB, 64-B rows
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int cot0 = (wid >> 1) * 2, cit = wid & 1;
-  const int co0 = blockIdx.x * 64, ci0 = blockIdx.y * 32;
-  const int Cin = g.C1 + g.C2;
-  const bf16* xs; int xcs, xcc;
-  if (ci0 < g.C1) { xs = x1; xcs = g.C1; xcc = ci0; } else { xs = x2; xcs = g.C2; xcc = ci0 - g.C1; }
-  const bf16* ys; int ycs, ycc;
-  const int Co2 = g.Cout - g.Co1;
-  if (co0 < g.Co1) { ys = dy1; ycs = g.Co1; ycc = co0; } else { ys = dy2; ycs = Co2; ycc = co0 - g.Co1; }
-  const int tiles_per_img = tiles_x * ((g.Ho + W36_TH - 1) / W36_TH);
-
-  f32x4 acc[2][9];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int lr = lane & 15, lg = lane >> 4, q = lr >> 2, pp = lr & 3;
-  int aoff[2][2];  // dY fragment offsets for K-chunk 0 (chunk kc adds kc*32 rows: swizzle-invariant)
-#pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    const int r = lg * 8 + half * 4 + q;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) aoff[i][half] = r * 64 + ((((cot0 + i) * 4 + pp) ^ w3_swz_dy(r)) * 4);
-  }
-  bf16x8 yv[9], hv[6];  // next tile's vectors in registers (see wgrad3x3_bf16_kernel)
-  auto gload = [&](int tile) {
-    const int n = tile / tiles_per_img;
-    const int rem = tile - n * tiles_per_img;
-    const int ty = rem / tiles_x, tx = rem - ty * tiles_x;
-    const int y0 = ty * W36_TH, x0 = tx * W36_TW;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {       // dY: 288 px x 8 vectors
-      const int e = tid + k * 256;
-      const int p = e >> 3, part = e & 7;
-      const int oy = y0 + p / W36_TW, ox = x0 + (p - (p / W36_TW) * W36_TW);
-      const bool ok = oy < g.Ho && ox < g.Wo;
-      const bf16x8 v = *reinterpret_cast<const bf16x8*>(
-          ys + (ok ? (((int64_t)n * g.Ho + oy) * g.Wo + ox) * ycs : 0) + ycc + part * 8);
-      yv[k] = ok ? v : bf16x8{};
-    }
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {       // halo: 380 px x 4 vectors
-      const int e = tid + k * 256;
-      const int hp = e >> 2, part = e & 3;
-      const int r = hp / W36_HW, c = hp - r * W36_HW;
-      const int iy = y0 - 1 + r, ix = x0 - 1 + c;
-      const bool ok = e < W36_NPIX * 4 && (unsigned)iy < (unsigned)g.Hi && (unsigned)ix < (unsigned)g.Wi;
-      const bf16x8 v = *reinterpret_cast<const bf16x8*>(
-          xs + (ok ? (((int64_t)n * g.Hi + iy) * g.Wi + ix) * xcs : 0) + xcc + part * 8);
-      hv[k] = ok ? v : bf16x8{};
-    }
-  };
-  if ((int)blockIdx.z < ntiles) gload(blockIdx.z);
-  for (int tile = blockIdx.z; tile < ntiles; tile += gridDim.z) {
-    __syncthreads();
-    {
-#pragma unroll
-      for (int k = 0; k < 9; ++k) {
-        const int e = tid + k * 256;
-        const int p = e >> 3, part = e & 7;
-        const int ch = (part * 2) ^ w3_swz_dy(p);
-        *reinterpret_cast<bf16x8*>(sdy + p * 64 + ch * 4) = yv[k];
-      }
-#pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        const int e = tid + k * 256;
-        if (e < W36_NPIX * 4) {
-          const int hp = e >> 2, part = e & 3;
-          const int r = hp / W36_HW, row = r * W3_P + (hp - r * W36_HW);
-          const int ch = (part * 2) ^ w3_swz_x(row);
-          *reinterpret_cast<bf16x8*>(shx + row * 32 + ch * 4) = hv[k];
-        }
-      }
-    }
-    __syncthreads();
-    if (tile + (int)gridDim.z < ntiles) gload(tile + gridDim.z);
-    // flat pixel of this lane's two 4-pixel groups in K-chunk kc: P = kc*32 + r0[half]; (row, col) of
-    // it in the 36-wide tile advance incrementally (32 < 36: at most one wrap per chunk)
-    int prow[2], pcol[2];
-#pragma unroll
-    for (int half = 0; half < 2; ++half) { prow[half] = 0; pcol[half] = lg * 8 + half * 4 + q; }
-#pragma unroll 1
-    for (int kc = 0; kc < W36_NP / 32; ++kc) {
-      // A = dY^T (rows co, K = flat pixels kc*32 .. +31): tr reads (swizzle invariant under kc*32)
-      bf16x8 af[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-#pragma unroll
-        for (int half = 0; half < 2; ++half) {
-          const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(sdy + aoff[i][half] + kc * 32 * 64));
-#pragma unroll
-          for (int e = 0; e < 4; ++e) af[i][half * 4 + e] = __builtin_bit_cast(bf16, (short)v[e]);
-        }
-      }
-      // halo row of tap (0,0) for each 4-pixel group -> offsets of kx = 0..2 (ky adds whole W3_P rows)
-      int bo[2][3];
-#pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        const int hb = prow[half] * W3_P + pcol[half];
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) bo[half][kx] = (hb + kx) * 32 + (((cit * 4 + pp) ^ w3_swz_x(hb + kx)) * 4);
-        pcol[half] += 32;
-        if (pcol[half] >= W36_TW) { pcol[half] -= W36_TW; ++prow[half]; }
-      }
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const int ky = tap / 3, kx = tap - ky * 3;
-        bf16x8 bfr;
-#pragma unroll
-        for (int half = 0; half < 2; ++half) {
-          const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(shx + bo[half][kx] + ky * W3_P * 32));
-#pragma unroll
-          for (int e = 0; e < 4; ++e) bfr[half * 4 + e] = __builtin_bit_cast(bf16, (short)v[e]);
-        }
-        acc[0][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bfr, acc[0][tap], 0, 0, 0);
-        acc[1][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bfr, acc[1][tap], 0, 0, 0);
-      }
-    }
-  }
-  const int K = 9 * Cin;
-  float* out = slab + (int64_t)blockIdx.z * g.Cout * K;
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int ci = ci0 + cit * 16 + lr;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = co0 + (cot0 + i) * 16 + lg * 4 + r;
-        out[(int64_t)co * K + tap * Cin + ci] = acc[i][tap][r];
-      }
-    }
-}
 
 // sum slabs over splits (fixed order) and scatter into the PyTorch weight layout
 // dst[((d0*D1 + d1)*KH + kyt)*KW + kxt], with (d0,d1) = swap ? (ci,co) : (co,ci) and
@@ -4233,14 +3514,11 @@ __global__ void head_reduce_kernel(const float* __restrict__ part, float* __rest
 // cesm_conv_fwd_variant query go through this one function, so tests can assert which kernel a shape reaches.
 enum ConvFwdVariant {
   CFV_INVALID = -1,
-  CFV_GEMM1X1_128 = 0, CFV_GEMM1X1_64, CFV_P36_RW, CFV_P36, CFV_P32_3STAGE, CFV_P32_RW, CFV_P32, CFV_W36, CFV_W32,
-  CFV_V2, CFV_HALO36, CFV_HALO32, CFV_TCONV_PAR_128, CFV_TCONV_PAR_64, CFV_GEN_BF16_128, CFV_GEN_BF16_64,
+  CFV_GEMM1X1_128 = 0, CFV_GEMM1X1_64, CFV_P32_RW, CFV_HALO36, CFV_HALO32, CFV_TCONV_PAR_128, CFV_TCONV_PAR_64, CFV_GEN_BF16_128, CFV_GEN_BF16_64,
   CFV_GEN_F32_128, CFV_GEN_F32_64, CFV_S2DOWN36, CFV_S2DOWN32, CFV_S2UP36, CFV_S2UP32, CFV_WS32, CFV_WS36, CFV_COUNT
 };
 static const char* const kConvFwdVariantName[CFV_COUNT] = {
-    "gemm1x1_kernel<128>", "gemm1x1_kernel<64>", "conv3x3p_kernel<36,8,true>", "conv3x3p_kernel<36,8,false>",
-    "conv3x3p_kernel<32,4,true,3,7>", "conv3x3p_kernel<32,7,true>", "conv3x3p_kernel<32,7,false>",
-    "conv3x3w_kernel<36>", "conv3x3w_kernel<32>", "conv3x3v2_kernel", "conv3x3_bf16_kernel<36>",
+    "gemm1x1_kernel<128>", "gemm1x1_kernel<64>", "conv3x3p_kernel<32,7,true>", "conv3x3_bf16_kernel<36>",
     "conv3x3_bf16_kernel<32>", "conv_fwd_bf16_kernel<128,true>", "conv_fwd_bf16_kernel<64,true>",
     "conv_fwd_bf16_kernel<128>", "conv_fwd_bf16_kernel<64>", "conv_fwd_kernel<float,128>",
     "conv_fwd_kernel<float,64>", "convs2_bf16_kernel<36,down>", "convs2_bf16_kernel<32,down>",
@@ -4248,7 +3526,7 @@ static const char* const kConvFwdVariantName[CFV_COUNT] = {
 
 struct ConvFwdPlan {
   ConvFwdVariant v = CFV_INVALID;
-  int TH = 0, TW = 0;  // halo tile (conv3x3p / conv3x3w / v2 / halo kernels)
+  int TH = 0, TW = 0;  // halo tile (conv3x3p / conv3x3ws / halo kernels)
 };
 
 static ConvFwdPlan conv_fwd_plan(int dtype, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout, int Co1,
@@ -4259,16 +3537,14 @@ static ConvFwdPlan conv_fwd_plan(int dtype, int Nb, int Hi, int Wi, int C1, int 
   const int64_t M = (int64_t)Nb * Ho * Wo;
   const int BN = (Cout % 128 == 0) ? 128 : 64;
   const bool halo3 = dtype == CESM_DT_BF16 && KH == 3 && KW == 3 && S == 1 && P == 1 && U == 1 && Ho == Hi &&
-                     Wo == Wi && (Co1 % H3_BN) == 0 && !getenv_flag("CESM_NO_HALO");
+                     Wo == Wi && (Co1 % H3_BN) == 0;
   const bool g1x1 = dtype == CESM_DT_BF16 && KH == 1 && KW == 1 && S == 1 && P == 0 && U == 1 && Ho == Hi &&
-                    Wo == Wi && (C1 % 64) == 0 && (C2 % 64) == 0 && (Co1 % 8) == 0 && M < (1ll << 31) &&
-                    (G1_BIGM || M * (C1 > C2 ? C1 : C2) * 2 < (1ll << 31)) && !getenv_flag("CESM_NO_GEMM1X1");
+                    Wo == Wi && (C1 % 64) == 0 && (C2 % 64) == 0 && (Co1 % 8) == 0 && M < (1ll << 31);
   int wth = 0, wtw = 0;
   // warp-specialized conv: by default for the level-0 64 -> 64 shape only (the conv3x3p case: 579 -> 518 us at
   // 96 x 192 x 288, profiles/r4c4_ws_check.txt); at 128 / 256 channels and for concat inputs it measured 0.85 - 1.01x
-  // of the halo conv, so there it is opt-in (CESM_CONV_WS=1); CESM_NO_CONV_WS=1 disables it
-  const bool ws = halo3 && (C1 + C2) >= 64 && !getenv_flag("CESM_NO_CONV_WS") &&
-                  (getenv_flag("CESM_CONV_WS") || (C1 == 64 && C2 == 0 && Cout == 64));
+  // of the halo conv, so there it is opt-in (CESM_CONV_WS=1)
+  const bool ws = halo3 && (C1 + C2) >= 64 && (getenv_flag("CESM_CONV_WS") || (C1 == 64 && C2 == 0 && Cout == 64));
   const double wutil = ws ? ws_tile(Ho, Wo, wth, wtw) : 0.0;
   if (g1x1) {
     pl.v = (Cout % 128 == 0) ? CFV_GEMM1X1_128 : CFV_GEMM1X1_64;
@@ -4277,42 +3553,19 @@ static ConvFwdPlan conv_fwd_plan(int dtype, int Nb, int Hi, int Wi, int C1, int 
     pl.v = wtw == 36 ? CFV_WS36 : CFV_WS32;
     pl.TH = wth;
     pl.TW = wtw;
-  } else if (halo3 && Cout <= 1024 && !getenv_flag("CESM_CONV3X3_V1") &&
-             (getenv_flag("CESM_CONV3X3_V4") || ((C1 + C2) == 64 && Cout == 64 && (Wo % 32) == 0))) {
-    // v4 (persistent, resident weights) for the level-0 64 -> 64 convs by default;
-    // CESM_CONV3X3_V4=1 forces it for every 3x3 conv, CESM_CONV3X3_V1=1 disables it
-    // TW = 32 -> TH = 14 (448 px = 4 waves x 7 groups); TW = 36 -> TH <= 14 (<= 504 px, 8 groups)
-    const bool w36 = (Wo % 32) != 0 && (Wo % 36) == 0;
-    pl.TW = w36 ? 36 : 32;
+  } else if (halo3 && (C1 + C2) == 64 && Cout == 64 && (Wo % 32) == 0) {
+    // v4 (persistent, resident weights) for the level-0 64 -> 64 convs the warp-specialized tiles do not cover
+    // (the reference's 64 / 128-wide crops): TW = 32 -> TH = 14 (448 px = 4 waves x 7 groups).  (Round 6 removed the
+    // env-selected alternatives: the halo conv here, this kernel everywhere, its 3-stage and streamed-weight forms,
+    // and the round-1 v2 / v3 kernels -- all measured slower, profiles/r2_*, r3_conv_v4_everywhere_ab.txt.)
+    pl.TW = 32;
     pl.TH = CP_TH;
-    if (w36) {  // fewest tiles, then least padding
-      int best = 1 << 30;
-      for (int th = CP_TH; th >= 8; --th) {
-        const int nt = (int)cdiv(Ho, th);
-        if (nt * th < best) { best = nt * th; pl.TH = th; }
-      }
-    }
-    const bool rw = (C1 + C2) == 64 && Cout == 64 && !getenv_flag("CESM_NO_RESIDENT_W");
-    if (w36) pl.v = rw ? CFV_P36_RW : CFV_P36;
-    else if (rw && getenv_flag("CESM_CONV3X3_3STAGE")) { pl.v = CFV_P32_3STAGE; pl.TH = 8; }
-    else pl.v = rw ? CFV_P32_RW : CFV_P32;
-  } else if (halo3 && getenv_flag("CESM_CONV3X3_V3")) {
-    pl.TH = 16; pl.TW = 32;
-    cw_tile(Ho, Wo, pl.TH, pl.TW);
-    pl.v = pl.TW == 36 ? CFV_W36 : CFV_W32;
-  } else if (halo3 && getenv_flag("CESM_CONV3X3_V2")) {
-    pl.TH = 8; pl.TW = 32;
-    c2_tile(Ho, Wo, pl.TH, pl.TW);
-    pl.v = CFV_V2;
+    pl.v = CFV_P32_RW;
   } else if (halo3) {
     pl.TH = H3_TH; pl.TW = H3_TW;
-    if (!getenv_flag("CESM_CONV3X3_FIXED_TILE")) {
-      if (H3_BIG && H3_SQ && H3_DMA) h3_big_tile(Ho, Wo, pl.TH, pl.TW);
-      else c2_tile(Ho, Wo, pl.TH, pl.TW, true);
-    }
+    h3_big_tile(Ho, Wo, pl.TH, pl.TW);
     pl.v = pl.TW == 36 ? CFV_HALO36 : CFV_HALO32;
   } else if (dtype == CESM_DT_BF16 && KH == 4 && KW == 4 && C2 == 0 && Co1 == Cout && (Cout % H3_BN) == 0 &&
-             !getenv_flag("CESM_NO_S2HALO") &&
              ((S == 2 && P == 1 && U == 1 && Hi == 2 * Ho && Wi == 2 * Wo) ||
               (S == 1 && P == 2 && U == 2 && Ho == 2 * Hi && Wo == 2 * Wi))) {
     // stride-2 4x4 conv / its transpose: halo kernel on the low-resolution grid
@@ -4322,7 +3575,7 @@ static ConvFwdPlan conv_fwd_plan(int dtype, int Nb, int Hi, int Wi, int C1, int 
     c2_tile(Hl, Wl, pl.TH, pl.TW, true);
     pl.v = up ? (pl.TW == 36 ? CFV_S2UP36 : CFV_S2UP32) : (pl.TW == 36 ? CFV_S2DOWN36 : CFV_S2DOWN32);
   } else if (dtype == CESM_DT_BF16 && U == 2 && S == 1 && KH % 2 == 0 && KW % 2 == 0 && Ho % 2 == 0 &&
-             Wo % 2 == 0 && !getenv_flag("CESM_NO_PARITY_TCONV")) {
+             Wo % 2 == 0) {
     pl.v = BN == 128 ? CFV_TCONV_PAR_128 : CFV_TCONV_PAR_64;
   } else if (dtype == CESM_DT_BF16) {
     pl.v = BN == 128 ? CFV_GEN_BF16_128 : CFV_GEN_BF16_64;
@@ -4355,8 +3608,8 @@ int64_t conv_gn_nslot(const ConvFwdPlan& pl, int Nb, int Ho, int Wo, int B) {
   const int64_t fimg = Nb / B;
   const int64_t tiles = (pl.TW > 0 && pl.TH > 0) ? cdiv(Wo, pl.TW) * cdiv(Ho, pl.TH) : 0;
   switch (pl.v) {
-    case CFV_P36_RW: case CFV_P36: case CFV_P32_RW: case CFV_P32: return fimg * tiles * 4;
-    case CFV_HALO36: case CFV_HALO32: return fimg * tiles * (H3_SQ ? 4 : 2);
+    case CFV_P32_RW: return fimg * tiles * 4;
+    case CFV_HALO36: case CFV_HALO32: return fimg * tiles * 4;
     case CFV_WS32: case CFV_WS36: return fimg * tiles * 4;
     default: return 0;
   }
@@ -4379,7 +3632,7 @@ int conv_fwd_launch(int dtype, const void* x1, const void* x2, const void* wp, c
   switch (pl.v) {
     case CFV_GEMM1X1_128:
     case CFV_GEMM1X1_64: {
-      const bool one = C1 + C2 == 64 && G1_NS1;
+      const bool one = C1 + C2 == 64;  // single-stage K = 64 variant
 #define G1L(BNv, NSv)                                                                                               \
   gemm1x1_kernel<BNv, NSv><<<dim3((unsigned)(Cout / BNv * 8 * cdiv(cdiv(M, G1_BM), 8))), 256, 0, stream>>>(      \
       bx1, bx2, bwp, bias, br, br2, by1, by2, (int)M, C1, C2, Cout, Co1)
@@ -4391,33 +3644,13 @@ int conv_fwd_launch(int dtype, const void* x1, const void* x2, const void* wp, c
 #undef G1L
       break;
     }
-    case CFV_P36_RW:
-    case CFV_P36:
-    case CFV_P32_3STAGE:
-    case CFV_P32_RW:
-    case CFV_P32: {
+    case CFV_P32_RW: {
       const int tx = (int)cdiv(Wo, TW), ty = (int)cdiv(Ho, TH);
       const int ncob = Cout / 64;
       const int nitems = Nb * tx * ty * ncob;
       const int nblk = std::min(nitems, cesm_num_cus());
-      if (pl.v == CFV_P36_RW)
-        conv3x3p_kernel<36, 8, true><<<nblk, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, tx * ty,
-                                                               TH, ncob, nitems, gnp, gn_fimg);
-      else if (pl.v == CFV_P36)
-        conv3x3p_kernel<36, 8, false><<<nblk, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx,
-                                                                tx * ty, TH, ncob, nitems, gnp, gn_fimg);
-      else if (pl.v == CFV_P32_3STAGE)
-        // experimental: 8 x 32 tiles, 3 LDS stages (two steps of DMA in flight) - measured slower than
-        // 2 stages of 14 x 32 tiles (345 vs 315 us): the level-0 conv is HBM-bound (block-0 stamps: 2.2 GHz,
-        // DMA-only 175 us vs MFMA-only 166 us per launch), deeper prefetch does not add overlap
-        conv3x3p_kernel<32, 4, true, 3, 7><<<std::min(nitems, cesm_num_cus()), 256, 0, stream>>>(
-            bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, tx * ty, TH, 1, Nb * tx * ty, nullptr, 1);
-      else if (pl.v == CFV_P32_RW)
-        conv3x3p_kernel<32, 7, true><<<nblk, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, tx * ty,
-                                                               TH, ncob, nitems, gnp, gn_fimg);
-      else
-        conv3x3p_kernel<32, 7, false><<<nblk, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx,
-                                                                tx * ty, TH, ncob, nitems, gnp, gn_fimg);
+      conv3x3p_kernel<32, 7, true><<<nblk, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, tx * ty, TH,
+                                                             ncob, nitems, gnp, gn_fimg);
       break;
     }
     case CFV_WS32:
@@ -4427,6 +3660,9 @@ int conv_fwd_launch(int dtype, const void* x1, const void* x2, const void* wp, c
       const int ntile = Nb * tx * ty;
       const int nitems_pad = (int)cdiv(ntile, 8) * 8 * ncob;
       const int nblk = std::min(nitems_pad, cesm_num_cus());
+      // a stale count (a launch cut short, an aborted capture) would make every block of this launch find the queue
+      // dry: zero it in stream order first (the kernel's last block also resets it)
+      if (queue) (void)hipMemsetAsync(queue, 0, 2 * sizeof(int), stream);
 #define WSL(TWv, GNv)                                                                                              \
   conv3x3ws_kernel<TWv, GNv><<<nblk, 512, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, TH, tx, tx * ty, ncob, \
                                                        nitems_pad, gnp, gn_fimg, queue)
@@ -4435,41 +3671,15 @@ int conv_fwd_launch(int dtype, const void* x1, const void* x2, const void* wp, c
 #undef WSL
       break;
     }
-    case CFV_W36:
-    case CFV_W32: {
-      const int tx = (int)cdiv(Wo, TW), ty = (int)cdiv(Ho, TH);
-      dim3 g3(tx * ty, Nb, Cout / 64);
-      if (pl.v == CFV_W36)
-        conv3x3w_kernel<36><<<g3, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, TH);
-      else
-        conv3x3w_kernel<32><<<g3, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, TH);
-      break;
-    }
-    case CFV_V2: {
-      const int tx = (int)cdiv(Wo, TW), ty = (int)cdiv(Ho, TH);
-      const int ncob = Cout / 64;
-      const int nitems = Nb * tx * ty * ncob;
-      const int nblk = std::min(nitems, cesm_num_cus());
-      conv3x3v2_kernel<<<nblk, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, TH, TW, tx, ty, ncob,
-                                                 nitems);
-      break;
-    }
     case CFV_HALO36:
     case CFV_HALO32: {
       const int tx = (int)cdiv(Wo, TW), ty = (int)cdiv(Ho, TH);
       const unsigned g3 = (unsigned)(Cout / H3_BN) * 8u * (unsigned)cdiv((int64_t)tx * ty * Nb, 8);
-      const bool big = TH * TW > 256;  // h3_tile chose a 448-pixel tile (H3_BIG)
+      const bool big = TH * TW > 256;  // h3_big_tile chose a 448-pixel tile
 #define H3L(TWv, NJv)                                                                                                \
   conv3x3_bf16_kernel<TWv, NJv><<<g3, 256, 0, stream>>>(bx1, bx2, bwp, bias, br, br2, by1, by2, g, tx, TH, gnp, gn_fimg)
-      // the 448-pixel instantiations exist only in builds with square wave tiles and DMA staging (the A/B knobs
-      // H3_SQ = 0 / H3_DMA = 0 keep compiling; conv_fwd_plan then never picks a big tile)
-#if H3_BIG && H3_SQ && H3_DMA
       if (pl.v == CFV_HALO36) { if (big) H3L(36, 7); else H3L(36, 4); }
       else { if (big) H3L(32, 7); else H3L(32, 4); }
-#else
-      (void)big;
-      if (pl.v == CFV_HALO36) H3L(36, 4); else H3L(32, 4);
-#endif
 #undef H3L
       break;
     }
@@ -4558,20 +3768,19 @@ int cesm_conv_fwd_gn(int dtype, const void* x1, const void* x2, const void* wp, 
 
 namespace {
 // Kernel selection of cesm_conv_wgrad (host only)
-enum WgradVariant { WGV_W36 = 0, WGV_W32, WGV_WIDE, WGV_GEN, WGV_S2, WGV_W32C64, WGV_W36C64 };
+enum WgradVariant { WGV_WIDE = 0, WGV_GEN, WGV_S2, WGV_W32C64, WGV_W36C64 };
 static int wgrad_plan(int dtype, int64_t M, int Hi, int Wi, int Ho, int Wo, int KH, int KW, int S, int P, int U) {
   const bool halo3 = dtype == CESM_DT_BF16 && KH == 3 && KW == 3 && S == 1 && P == 1 && U == 1 && Ho == Hi &&
-                     Wo == Wi && !getenv_flag("CESM_NO_HALO");
+                     Wo == Wi;
   // 8 x 36 tiles only where 32-wide tiles waste >= 20 % of the columns (W = 36, 72); at W = 144 / 288
   // the 8 x 32 kernel's row-aligned K chunks are faster despite the partial last tile
-  if (halo3 && (Wo % W36_TW) == 0 && 5 * Wo <= 4 * (int)cdiv(Wo, W3_TW) * W3_TW && !getenv_flag("CESM_NO_WGRAD36"))
-    return getenv_flag("CESM_WGRAD3X3_C32") ? WGV_W36 : WGV_W36C64;
-  if (halo3) return getenv_flag("CESM_WGRAD3X3_C32") ? WGV_W32 : WGV_W32C64;  // (C1 % 64 == 0: cesm_conv_wgrad)
+  if (halo3 && (Wo % W36_TW) == 0 && 5 * Wo <= 4 * (int)cdiv(Wo, W3_TW) * W3_TW) return WGV_W36C64;
+  if (halo3) return WGV_W32C64;  // (C1 % 64 == 0: cesm_conv_wgrad)
   // (32-wide pixel tiles: at Wo = 36 the second tile of a row is 8/9 empty and the wide kernel is faster)
   if (dtype == CESM_DT_BF16 && KH == 4 && KW == 4 && S == 2 && P == 1 && U == 1 && Hi == 2 * Ho && Wi == 2 * Wo &&
-      Wo >= 64 && !getenv_flag("CESM_NO_S2HALO"))
+      Wo >= 64)
     return WGV_S2;
-  if (dtype == CESM_DT_BF16 && M < (1ll << 31) && !getenv_flag("CESM_NO_WIDE_WGRAD")) return WGV_WIDE;
+  if (dtype == CESM_DT_BF16 && M < (1ll << 31)) return WGV_WIDE;
   return WGV_GEN;
 }
 }  // namespace
@@ -4584,8 +3793,6 @@ const char* cesm_conv_wgrad_variant(int dtype, int Nb, int Hi, int Wi, int C1, i
   int wv = wgrad_plan(dtype, M, Hi, Wi, Ho, Wo, KH, KW, S, P, U);
   if (wv == WGV_S2 && (with_bias || C2 || Co1 != Cout)) wv = WGV_WIDE;  // (cesm_conv_wgrad's fallback)
   switch (wv) {
-    case WGV_W36: return "wgrad3x3w36_kernel";
-    case WGV_W32: return "wgrad3x3_bf16_kernel";
     case WGV_W32C64: return "wgrad3x3c64_kernel";
     case WGV_W36C64: return "wgrad3x3w36c64_kernel";
     case WGV_S2: return "wgrads2_bf16_kernel";
@@ -4624,26 +3831,12 @@ int cesm_conv_wgrad(int dtype, const void* x1, const void* x2, const void* dy1, 
     wgrad3x3w36c64_kernel<<<g3, WG_NT, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
                                                   (const bf16*)dy2, slab, g, tx, ntiles);
     nsplit = (int)g3.z;
-  } else if (wv == WGV_W36) {
-    const int tx = Wo / W36_TW;
-    const int ntiles = Nb * tx * (int)cdiv(Ho, W36_TH);
-    dim3 g3(Cout / 64, Cin / 32, std::min(nsplit, ntiles));
-    wgrad3x3w36_kernel<<<g3, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
-                                               (const bf16*)dy2, slab, g, tx, ntiles);
-    nsplit = (int)g3.z;
   } else if (wv == WGV_W32C64) {
     const int tx = (int)cdiv(Wo, W3_TW);
     const int ntiles = Nb * tx * (int)cdiv(Ho, W3_TH);
     dim3 g3(Cout / 64, Cin / 64, std::min(nsplit, ntiles));
     wgrad3x3c64_kernel<<<g3, WG_NT, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
                                                (const bf16*)dy2, slab, g, tx, ntiles);
-    nsplit = (int)g3.z;
-  } else if (wv == WGV_W32) {
-    const int tx = (int)cdiv(Wo, W3_TW);
-    const int ntiles = Nb * tx * (int)cdiv(Ho, W3_TH);
-    dim3 g3(Cout / 64, Cin / 32, std::min(nsplit, ntiles));
-    wgrad3x3_bf16_kernel<<<g3, 256, 0, stream>>>((const bf16*)x1, (const bf16*)x2, (const bf16*)dy1,
-                                                 (const bf16*)dy2, slab, g, tx, ntiles);
     nsplit = (int)g3.z;
   } else if (wv == WGV_S2 && C2 == 0 && Co1 == Cout && !db) {
     const int tx = (int)cdiv(Wo, W3_TW);
@@ -4728,7 +3921,7 @@ int cesm_stem_fwd(int dtype, const float* xt, const float* cond, const float* w,
                   int F, int Fx, int Fc, int H, int W, int Co, int KS, hipStream_t stream) {
   if (KS > 7 || Co % 64) return CESM_EINVAL;
   dim3 grid((unsigned)(cdiv(H, 16) * cdiv(W, 16)), Co / 64, B * F);
-  if (dtype == CESM_DT_BF16 && 2 * KS * KS <= 128 && !getenv_flag("CESM_STEM_VALU")) {
+  if (dtype == CESM_DT_BF16 && 2 * KS * KS <= 128) {
     const int ntiles = (int)(cdiv(H, 16) * cdiv(W, 16)) * B * F;
     dim3 gp((unsigned)std::min(ntiles, 4 * cesm_num_cus()), Co / 64);
     stem_fwd_mfma_kernel<<<gp, 256, 0, stream>>>(xt, cond, w, bias, (bf16*)y, B, F, Fx, Fc, H, W, Co, KS, ntiles);

@@ -17,8 +17,7 @@
 namespace {
 
 // streaming activation accesses are non-temporal (bf16): measured at the level-0 bench shape stats 122 -> 107 us,
-// apply (+ residual) 389 -> 370 us, backward 679 -> 631 us (tools/gn_time.py); -DGN_NO_NT restores plain accesses
-#ifndef GN_NO_NT
+// apply (+ residual) 389 -> 370 us, backward 679 -> 631 us (tools/gn_time.py)
 __device__ __forceinline__ void gl8(const bf16* p, float* v) { ldnt4(p, v); ldnt4(p + 4, v + 4); }
 __device__ __forceinline__ void gl8(const float* p, float* v) { load8(p, v); }
 __device__ __forceinline__ void gs8(bf16* p, const float* v) {
@@ -28,22 +27,14 @@ __device__ __forceinline__ void gs8(bf16* p, const float* v) {
   stnt16(p, a);
 }
 __device__ __forceinline__ void gs8(float* p, const float* v) { store8(p, v); }
-#else
-template <typename T> __device__ __forceinline__ void gl8(const T* p, float* v) { load8(p, v); }
-template <typename T> __device__ __forceinline__ void gs8(T* p, const float* v) { store8(p, v); }
-#endif
 
 // row chunks per sample for the reduction kernels: >= ~8 row-iterations per thread, at most
 // max(256, 1024 / B) chunks, so a B = 1 long window (F = 120: ~1M rows per sample) still launches 1024
 // blocks = 4 per CU instead of 256 (measured: the 1-block-per-CU grid ran the bwd reduction at ~40 % of
 // the apply kernel's bandwidth).  Workspaces hold max(B * 256, 1024) chunk partials (gn_ws_chunks).
-#ifndef GN_SMALLB_CHUNKS
-#define GN_SMALLB_CHUNKS 1024  // A/B knob (256 = the round-2 fixed cap)
-#endif
-#ifndef GN_BIGB_CAP
-#define GN_BIGB_CAP 256  // A/B knob: chunks per sample at B >= 4 (<= 1024: the workspace holds B * 1024 partials);
-                         // whole step 256 -> 512 / 1024: +0.2 / +0.5 ms (profiles/r3_gn_cap_ab.txt)
-#endif
+constexpr int GN_SMALLB_CHUNKS = 1024;  // (256 = the round-2 fixed cap)
+constexpr int GN_BIGB_CAP = 256;  // chunks per sample at B >= 4 (<= 1024: the workspace holds B * 1024 partials);
+                                  // whole step 256 -> 512 / 1024: +0.2 / +0.5 ms (profiles/r3_gn_cap_ab.txt)
 static int gn_nchunk(int64_t rows_b, int C, int B) {
   const int rl = 256 / (C / 8);
   const int cap = B >= GN_SMALLB_CHUNKS / 256 ? GN_BIGB_CAP : GN_SMALLB_CHUNKS / B;
@@ -256,9 +247,8 @@ __device__ __forceinline__ void gn_coef8(const GnAffine& q, int b, int c0, int C
 // (Round 3 measured two Infinity-Cache orders and removed them: the backward one sample at a time so gn_bwd_apply
 // re-reads (dout, y) on-die -- whole step 132.0 -> 138.0 ms; gn_apply in reversed sample order -- neutral.)
 
-#ifndef GN_BATCH
-#define GN_BATCH 0  // gn_apply / gn_bwd_apply: rows per step with all loads before the stores (0: per-row load -> store)
-#endif
+// (Round 5: four rows per step with every load before the first store, GN_BATCH: whole step 61.58 / 61.83 ->
+// 61.75 / 61.89 samples/s, inside the spread; removed -- profiles/r5j_gn_batch_ab.txt.)
 // grid (nchunk, B): thread = (8-channel group c8, row lane rr), rows strided by 256/(C/8)
 template <typename T>
 __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ y, const GnAffine coef,
@@ -274,40 +264,6 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ y, 
   const int64_t r0 = chunk * rpc, r1 = min(rows_b, r0 + rpc);
   const int64_t off = (int64_t)b * rows_b * C + c8 * 8;
   int64_t r = r0 + rr;
-#if GN_BATCH
-  // GN_BATCH rows per step with every load issued before the first store (vmcnt retires in issue order: the
-  // per-row load -> store loop made each row's loads wait for the previous row's store); the tail below
-  if (res) {  // uniform
-    for (; r + (GN_BATCH - 1) * rl < r1; r += GN_BATCH * rl) {
-      float v[GN_BATCH][8], rv[GN_BATCH][8];
-#pragma unroll
-      for (int u = 0; u < GN_BATCH; ++u) {
-        gl8(y + off + (r + u * rl) * C, v[u]);
-        gl8(res + off + (r + u * rl) * C, rv[u]);
-      }
-      __builtin_amdgcn_sched_barrier(0);  // every load issued before the first store
-#pragma unroll
-      for (int u = 0; u < GN_BATCH; ++u) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) v[u][i] = silu_t<T>(fmaf(v[u][i], A1[i], A0[i])) + rv[u][i];
-        gs8(out + off + (r + u * rl) * C, v[u]);
-      }
-    }
-  } else {
-    for (; r + (GN_BATCH - 1) * rl < r1; r += GN_BATCH * rl) {
-      float v[GN_BATCH][8];
-#pragma unroll
-      for (int u = 0; u < GN_BATCH; ++u) gl8(y + off + (r + u * rl) * C, v[u]);
-      __builtin_amdgcn_sched_barrier(0);  // every load issued before the first store
-#pragma unroll
-      for (int u = 0; u < GN_BATCH; ++u) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) v[u][i] = silu_t<T>(fmaf(v[u][i], A1[i], A0[i]));
-        gs8(out + off + (r + u * rl) * C, v[u]);
-      }
-    }
-  }
-#endif
 #pragma unroll 4
   for (; r < r1; r += rl) {
     float v[8], rv[8];
@@ -502,27 +458,6 @@ __global__ __launch_bounds__(256) void gn_bwd_apply_kernel(const T* __restrict__
   const int64_t r0 = chunk * rpc, r1 = min(rows_b, r0 + rpc);
   const int64_t off = (int64_t)b * rows_b * C + c8 * 8;
   int64_t r = r0 + rr;
-#if GN_BATCH
-  // as gn_apply_kernel: GN_BATCH rows per step, loads before stores
-  for (; r + (GN_BATCH - 1) * rl < r1; r += GN_BATCH * rl) {
-    float v[GN_BATCH][8], d[GN_BATCH][8];
-#pragma unroll
-    for (int u = 0; u < GN_BATCH; ++u) {
-      gl8(y + off + (r + u * rl) * C, v[u]);
-      gl8(dout + off + (r + u * rl) * C, d[u]);
-    }
-    __builtin_amdgcn_sched_barrier(0);  // every load issued before the first store
-#pragma unroll
-    for (int u = 0; u < GN_BATCH; ++u) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float da = d[u][i] * dsilu_t<T>(fmaf(v[u][i], A1[i], A0[i]));
-        d[u][i] = fmaf(da, E1[i], fmaf(v[u][i], E2[i], E3[i]));
-      }
-      gs8(dy + off + (r + u * rl) * C, d[u]);
-    }
-  }
-#endif
 #pragma unroll 4
   for (; r < r1; r += rl) {
     float v[8], d[8];
@@ -544,10 +479,8 @@ static int dispatch_dt(int dtype, F&& f) {
   return CESM_EINVAL;
 }
 
-#ifndef GN_APPLY_ITERS
-#define GN_APPLY_ITERS 8  // row-iterations per thread of the streaming apply kernels: whole step 16 -> 8: -0.5 ms
-                          // (two calls, profiles/r3_gn_iters_ab.txt); 4 the same as 8, 32 +0.5 ms
-#endif
+constexpr int GN_APPLY_ITERS = 8;  // row-iterations per thread of the streaming apply kernels: whole step 16 -> 8:
+                                   // -0.5 ms (two calls, profiles/r3_gn_iters_ab.txt); 4 the same as 8, 32 +0.5 ms
 static int gn_apply_chunks(int64_t rows_b, int C) {
   const int rl = 256 / (C / 8);
   int64_t n = rows_b / (rl * GN_APPLY_ITERS);

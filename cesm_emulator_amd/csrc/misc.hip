@@ -303,13 +303,10 @@ int cesm_abi_version(void) { return CESM_ABI_VERSION; }
 int cesm_hold_cus(int nblk, float usec, hipStream_t stream) {
   if (nblk < 1 || !(usec >= 0.f)) return CESM_EINVAL;
   constexpr int kLds = 160 * 1024;
-  static bool attr = false;
-  if (!attr) {
-    if (hipFuncSetAttribute((const void*)hold_cu_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kLds) !=
-        hipSuccess)
-      return CESM_ELAUNCH;
-    attr = true;
-  }
+  // the attribute is per device: set it on every call (cheap) rather than caching one process-wide flag, which left a
+  // second device of the process without it
+  if (hipFuncSetAttribute((const void*)hold_cu_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kLds) != hipSuccess)
+    return CESM_ELAUNCH;
   hold_cu_kernel<<<nblk, 64, kLds, stream>>>((long long)(usec * 100.f));
   return cesm_launch_status();
 }

@@ -314,17 +314,9 @@ __global__ __launch_bounds__(256) void slaf_combine_kernel(const float* __restri
 // slaf_out: wave = 16*NV pixels of one frame, all heads; grid (cdiv(HW, 64*NV), Nf), 256 threads.
 // ---------------------------------------------------------------------------------------------------
 typedef unsigned int sl_u32x2 __attribute__((ext_vector_type(2)));
-#ifndef SLAB_EPI_PRE
-#define SLAB_EPI_PRE 1  // slab_dx: all x / dy loads of the LN-backward epilogue before its first dx store (1: C >= 128, 2: all, 0: per-tile rounds)
-#endif
-#ifndef SLAF_EPI_PRE
-#define SLAF_EPI_PRE 1  // slaf_out: all residual / bias loads of the y epilogue before its first store (0: per-tile load -> store)
-#endif
 template <int C, int NV>
-#ifndef SLAF_WPE
-#define SLAF_WPE 2  // slaf_out capped at 256 registers (VGPR-form MFMAs, no AGPR stash); 1 = round-2 allocation
-#endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLAF_WPE))) void slaf_out_kernel(const bf16* __restrict__ x, const float* __restrict__ gamma,
+// slaf_out capped at 256 registers (waves_per_eu 2: VGPR-form MFMAs, no AGPR stash)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void slaf_out_kernel(const bf16* __restrict__ x, const float* __restrict__ gamma,
                                                        const bf16* __restrict__ wqkv, const bf16* __restrict__ wout,
                                                        const float* __restrict__ bout, const bf16* __restrict__ actT,
                                                        bf16* __restrict__ y, bf16* __restrict__ o_out, int HW, float scale, float eps) {
@@ -451,10 +443,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLAF_WPE)))
     }
   }
   // y = x + W_o o + b_o
-#if SLAF_EPI_PRE
   // every residual / bias load before the first y store, the stores branch-free through a buffer resource over frame
   // n (pixels past HW go to an out-of-range offset, which the hardware drops): vmcnt retires in issue order, so a load
-  // behind a store waits for it (as tw_fwd's TW_EPI_PRE)
+  // behind a store waits for it (round 5: SLA forward 2.50 -> 2.48 ms, profiles/r5f_epilogue_loads_first_tb.txt)
   {
     const __amdgpu_buffer_rsrc_t yrs =
         __builtin_amdgcn_make_buffer_rsrc((void*)(y + (int64_t)n * HW * C), (short)0, HW * C * 2, 0x00020000);
@@ -482,23 +473,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLAF_WPE)))
       }
     }
   }
-#else
-#pragma unroll
-  for (int vt = 0; vt < NV; ++vt) {
-    const int p = p0 + vt * 16 + lr;
-    if (p >= HW) continue;
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) {
-      const int co = ct * 16 + lg * 4;
-      float xv[4];
-      load4(xb + (int64_t)p * C + co, xv);
-      float o4[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o4[r] = xv[r] + yacc[ct][vt][r] + bout[co + r];
-      store4(y + ((int64_t)n * HW + p) * C + co, o4);
-    }
-  }
-#endif
 }
 
 // ===================================================================================================
@@ -1041,7 +1015,7 @@ __global__ __launch_bounds__(256, 2) void slab_dx_kernel(
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     // LN backward + residual; dgamma partial
-    if constexpr (SLAB_EPI_PRE == 2 || (SLAB_EPI_PRE == 1 && C >= 128)) {  // (C = 64, NV = 2: 3 more spills)
+    if constexpr (C >= 128) {  // (C = 64, NV = 2: 3 more spills)
     // every x / dy load before the first dx store, the stores branch-free through a buffer resource over frame n
     // (pixels past HW go to an out-of-range offset, which the hardware drops): vmcnt retires in issue order, so a
     // load behind a store waits for it -- the per-channel-tile dy load -> dx store rounds serialised CT - 1 store
@@ -1186,18 +1160,10 @@ __device__ __forceinline__ void wave_lds_sync_s() {
 // the 8 shares summed through LDS -> LN backward -> dx.  No per-voxel intermediate reaches HBM (slab_dx
 // emitted the 768-channel dqkv and xn for a separate weight-gradient GEMM).
 // ===================================================================================================
-#ifndef SLAH_PF_LATE
-#define SLAH_PF_LATE 1  // slah_dx: next group's x / dy prefetch issued after phase B's operand loads (0: after barrier A)
-#endif
-#ifndef SLAH_PB_EARLY
-#define SLAH_PB_EARLY 0  // slah_dx: phase B's per-(frame, head) operands loaded during phase A (after its last weight batch)
-#endif
-#ifndef SLAH_DX_LATE
-#define SLAH_DX_LATE 0  // slah_dx: a group's dx stores issued in the next group after its weight / operand loads
-#endif
-#ifndef SLAH_WPIPE
-#define SLAH_WPIPE 1  // slah_dx: weight fragments issued one GEMM step ahead (first before barrier A / the dW GEMM)
-#endif
+// Measured and removed (round 5, profiles/r5f_prefetch_pos_tb.txt, r5f_slah_pb_early_tb.txt, r5_dxt_tb.txt, r5_prio_ab.txt):
+// phase B's operands loaded during phase A (+1 %), the dx stores deferred into the next group (10 spills, +5 %), dxn by
+// whole output tiles after a block barrier (4.69 -> 5.15 ms per call), s_setprio for waves 4-7 (within the spread);
+// round 2: weight fragments without the one-step-ahead pipeline +4 %.
 // xhat / dy tiles: region tiles (common.h xt_rs); fp32 partial dxn rows: pl_off layout over the wave's slice
 constexpr int SH_SLD = 128;  // slice row stride (bf16): raw q|k|v|do (128 cols), then dq|dk|dv; fp32 partials over it
 // Slice layout (round 3): a region tile (common.h rg_off<2>) of eight [R][16] regions -- q, k, v, do, two head-dim
@@ -1207,18 +1173,6 @@ constexpr int SH_SLD = 128;  // slice row stride (bf16): raw q|k|v|do (128 cols)
 // rows were 2-way on the fragment and transposed reads (42 % of slah_dx's LDS cycles were conflicts).
 template <int R>
 __device__ __forceinline__ int sl_off(int r, int c) { return rg_off<2>(r, c, R * 16); }
-#ifndef SLAH_DXT
-#define SLAH_DXT 0  // 1: slah_dx dxn by whole output tiles after a block barrier (round 5: 4.69 -> 5.15 ms per
-                    // call, profiles/r5_dxt_tb.txt); 0 = per-head fp32 partials (round 2-4)
-#endif
-// SLAH_DXT g rows: the two `do` regions (columns 96..127 = regions 6, 7: 64 R contiguous bytes) of waves 0..3's
-// slices hold R / 4 rows of 256 B each
-template <int R>
-__device__ __forceinline__ int slah_gslot(int v) { return v % (R / 4); }
-template <int R>
-__device__ __forceinline__ float* slah_grow(bf16* slices, int v) {
-  return reinterpret_cast<float*>(slices + (v / (R / 4)) * R * SH_SLD + 6 * R * 16) + slah_gslot<R>(v) * 64;
-}
 
 static size_t slah_smem(int NV) {
   const int R = 16 * NV;
@@ -1241,12 +1195,6 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const int h = wid;
-#ifndef SLAH_PRIO
-#define SLAH_PRIO 0
-#endif
-  // second-dispatched half (MI355X_MICROARCH §Two waves per SIMD, item 4); readfirstlane: a provably wave-uniform
-  // condition (with `wid >= 4` the scalar s_setprio ran unconditionally, in every wave -- the round-3 test was a no-op)
-  if (SLAH_PRIO && __builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
   bf16* sl = slices + wid * R * SH_SLD;
   const int npg = (HW + R - 1) / R;
   const int ngroups = Nf * npg;
@@ -1275,9 +1223,6 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
     for (int nt = 0; nt < 4; ++nt) dwacc[m][nt] = z4;
 
   prefetch(blockIdx.x);
-  // SLAH_DX_LATE: the previous group's dx chunk of this thread and its row (-1: none)
-  bf16x8 dx_pend = zero8();
-  int64_t dx_row = -1;
   for (int gg = blockIdx.x; gg < ngroups; gg += gridDim.x) {
     const int n = gg / npg, p0 = (gg - n * npg) * R;
     // ---- LN of this thread's pixel chunk (statistics over its 8 lanes)
@@ -1312,7 +1257,6 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
     const bf16* wq_g = wqkv + oz;
     const bf16* wqt_g = wqkv_t + oz;
     const bf16* wot_g = wout_t + oz;
-#if SLAH_WPIPE
     // phase A's weight fragments double-buffered per kind: kind 0 issued before barrier A (its L2 latency
     // overlaps the barrier wait), kind k+1 before kind k's MFMAs
     bf16x8 wa[2][2][KS];
@@ -1324,12 +1268,9 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
           wa[buf][t][ks] = kind < 3 ? ld_img(wq_g, kind * 16 + h * 2 + t, KS, ks, lane) : ld_img(wot_g, h * 2 + t, KS, ks, lane);
     };
     lda(0, 0);
-#endif
     __syncthreads();  // (A)
-    if (!SLAH_PF_LATE) prefetch(gg + gridDim.x);
 
-    // phase B's per-(frame, head) operands (L2-resident images): SLAH_PB_EARLY issues them in phase A, right after
-    // its last weight batch, so phase B does not wait for their latency
+    // phase B's per-(frame, head) operands (L2-resident images)
     bf16x8 aT[2], ax[2], ad[2], adT[2];
     f32x4 kg[4];
     auto ldpb = [&]() {
@@ -1344,26 +1285,16 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
       const f32x4* ki = reinterpret_cast<const f32x4*>(kimg + ((int64_t)(n * NH + h) * 64 + lane) * 16);
 #pragma unroll
       for (int q = 0; q < 4; ++q) kg[q] = ki[q];
-      // SLAH_PF_LATE: the next group's x / dy behind phase A's weights and these operands (vmcnt retires in issue
-      // order: a load issued behind the HBM prefetch waits for it)
-      if (SLAH_PF_LATE) prefetch(gg + gridDim.x);
+      // the next group's x / dy behind phase A's weights and these operands (vmcnt retires in issue order: a load
+      // issued behind the HBM prefetch waits for it; round 5, issued after barrier A: +3.5 %)
+      prefetch(gg + gridDim.x);
     };
 
     // ---- phase A: raw q | k | v | do of head h, rows = pixels, cols kind*32 + d
 #pragma unroll
     for (int kind = 0; kind < 4; ++kind) {
-#if SLAH_WPIPE
       if (kind + 1 < 4) lda(kind + 1, (kind + 1) & 1);
-      if (SLAH_PB_EARLY && kind == 2) ldpb();
       const auto& a = wa[kind & 1];
-#else
-      bf16x8 a[2][KS];
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks)
-          a[t][ks] = kind < 3 ? ld_img(wq_g, kind * 16 + h * 2 + t, KS, ks, lane) : ld_img(wot_g, h * 2 + t, KS, ks, lane);
-#endif
       const bf16* src = kind < 3 ? xt : dyt;
 #pragma unroll
       for (int vt = 0; vt < NV; ++vt) {
@@ -1383,15 +1314,10 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
     wave_lds_sync_s();
     // ---- phase B: per-pixel softmax backward (slab_dx's math); dq | dk | dv over cols 0..95
     {
-      if (!(SLAH_PB_EARLY && SLAH_WPIPE)) ldpb();
+      ldpb();
       float Kofs[2][4], Gd[2][4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) { Kofs[0][r] = kg[0][r]; Kofs[1][r] = kg[1][r]; Gd[0][r] = kg[2][r]; Gd[1][r] = kg[3][r]; }
-      if (SLAH_DX_LATE && dx_row >= 0) {  // the previous group's dx, behind this group's weight and operand loads
-        __builtin_amdgcn_sched_barrier(0);
-        stnt16(dx + dx_row * C + cc * 8, dx_pend);
-        dx_row = -1;
-      }
 #pragma unroll
       for (int vt = 0; vt < NV; ++vt) {
         const bool ok = p0 + vt * 16 + lr < HW;
@@ -1467,12 +1393,10 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
       }
     }
     wave_lds_sync_s();
-#if SLAH_WPIPE
     // the dxn GEMM's W'^T fragments one ahead: the first in flight during the dW GEMM
     bf16x8 wring[2];
     auto ldw = [&](int idx) { return ld_img(wqt_g, idx % CT, QKV / 32, (idx / CT) * 8 + h, lane); };
     wring[0] = ldw(0);
-#endif
     // ---- dW'_h += dqkv_h^T . xhat (K = pixels, 16 per step)
 #pragma unroll
     for (int kk = 0; kk < NV; ++kk) {
@@ -1487,67 +1411,6 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
           dwacc[m][nt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, bx[nt], dwacc[m][nt], 0, 0, 0);
       }
     }
-#if SLAH_DXT
-    // ---- dxn by whole output tiles (round 5, as twh_bwd's TWH_DXT): after a block barrier wave w computes
-    // g[v][c] = sum over all 768 qkv rows of W'^T[c][k] dqkv[v][k] for channel tile w & 3 and voxel tiles (w >> 2) + 2u,
-    // reading every head's slice; no per-head fp32 partials, 8 accumulator registers instead of 48.  g goes to 256-B
-    // rows in the `do` regions (columns 96..127, free after phase B) of waves 0-3: 16-B unit u of row slot s at u ^ (s & 7).
-    {
-      const int ct = wid & 3, vt0 = wid >> 2;
-      bf16x8 ring[3];
-      auto ldt = [&](int j) { return ld_img(wqt_g, ct, QKV / 32, j, lane); };  // j = kind * 8 + head
-      ring[0] = ldt(0);
-      ring[1] = ldt(1);
-      __syncthreads();  // (B') every head's dq | dk | dv in its slice
-      f32x4 dacc[2] = {z4, z4};
-#pragma unroll
-      for (int j = 0; j < 24; ++j) {
-        if (j + 2 < 24) ring[(j + 2) % 3] = ldt(j + 2);
-        const bf16x8 a = ring[j % 3];
-        const bf16* src = slices + (j & 7) * R * SH_SLD;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int vt = vt0 + 2 * u;
-          if (vt < NV)  // wave-uniform
-            dacc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ld16(src + sl_off<R>(vt * 16 + lr, (j >> 3) * 32 + lg * 8)),
-                                                              dacc[u], 0, 0, 0);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int vt = vt0 + 2 * u;
-        if (vt < NV) {
-          const int v = vt * 16 + lr;
-          float* row = slah_grow<R>(slices, v);
-          *reinterpret_cast<f32x4*>(row + ((ct * 4 + lg) ^ (slah_gslot<R>(v) & 7)) * 4) = dacc[u];
-        }
-      }
-    }
-    __syncthreads();  // (B'') every g row written
-    // ---- LN backward of this thread's pixel chunk
-    {
-      const int v = vv < R ? vv : 0, s7 = slah_gslot<R>(v) & 7;
-      const float* row = slah_grow<R>(slices, v);
-      const f32x4 a0 = *reinterpret_cast<const f32x4*>(row + ((2 * cc) ^ s7) * 4);
-      const f32x4 a1 = *reinterpret_cast<const f32x4*>(row + ((2 * cc + 1) ^ s7) * 4);
-      const float g[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-      const bf16x8 xh = *reinterpret_cast<const bf16x8*>(xt + rg_off<1>(v, cc * 8, xt_rs(R)));
-      const bf16x8 dv = *reinterpret_cast<const bf16x8*>(dyt + rg_off<1>(v, cc * 8, xt_rs(R)));
-      float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) { s1 += g[e]; s2 = fmaf(g[e], (float)xh[e], s2); }
-#pragma unroll
-      for (int o = 1; o < 8; o <<= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
-      s1 *= 1.f / C;
-      s2 *= 1.f / C;
-      if (vv < R && ok_cur) {
-        bf16x8 o8;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o8[e] = (bf16)(rstd_cur * (g[e] - s1 - (float)xh[e] * s2) + (float)dv[e]);
-        __builtin_nontemporal_store(o8, reinterpret_cast<bf16x8*>(dx + ((int64_t)n * HW + p0 + vv) * C + cc * 8));
-      }
-    }
-#else
     // ---- dxn'_h (this head's share of g = gamma * dxn)
     f32x4 dxacc[CT][NV];
 #pragma unroll
@@ -1558,13 +1421,9 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
     for (int kind = 0; kind < 3; ++kind)
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
-#if SLAH_WPIPE
         const int idx = kind * CT + ct;
         if (idx + 1 < 3 * CT) wring[(idx + 1) & 1] = ldw(idx + 1);
         const bf16x8 a = wring[idx & 1];
-#else
-        const bf16x8 a = ld_img(wqt_g, ct, QKV / 32, kind * 8 + h, lane);
-#endif
 #pragma unroll
         for (int vt = 0; vt < NV; ++vt)
           dxacc[ct][vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ld16(sl + sl_off<R>(vt * 16 + lr, kind * 32 + lg * 8)),
@@ -1607,17 +1466,10 @@ __global__ __launch_bounds__(512, 1) void slah_dx_kernel(
         bf16x8 o8;
 #pragma unroll
         for (int e = 0; e < 8; ++e) o8[e] = (bf16)(rstd_cur * (g[e] - s1 - (float)xh[e] * s2) + (float)dv[e]);
-        if (SLAH_DX_LATE) {
-          dx_pend = o8;
-          dx_row = (int64_t)n * HW + p0 + vv;
-        } else {
-          __builtin_nontemporal_store(o8, reinterpret_cast<bf16x8*>(dx + ((int64_t)n * HW + p0 + vv) * C + cc * 8));
-        }
+        __builtin_nontemporal_store(o8, reinterpret_cast<bf16x8*>(dx + ((int64_t)n * HW + p0 + vv) * C + cc * 8));
       }
     }
-#endif
   }
-  if (SLAH_DX_LATE && dx_row >= 0) stnt16(dx + dx_row * C + cc * 8, dx_pend);
   float* slab = dw_slab + (int64_t)blockIdx.x * QKV * C;
 #pragma unroll
   for (int m = 0; m < 6; ++m) {

@@ -662,32 +662,6 @@ __device__ __forceinline__ float grp4_max(float v) {
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
-// Diagnostic phase stamps (build with -DCESM_TW_STAMPS only): per-wave cycle sums of the tw_bwd
-// phases, written to g_tw_stamps[wave][8] at kernel end.
-#ifdef CESM_TW_STAMPS
-__device__ unsigned long long g_tw_stamps[4096 * 8];
-__device__ __forceinline__ unsigned long long tw_stamp() {
-  unsigned long long t;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-}
-#define TW_ST_DECL unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long st_t = tw_stamp();
-#define TW_ST(i) { const unsigned long long st_n = tw_stamp(); st_acc[i] += st_n - st_t; st_t = st_n; }
-#define TW_ST_FLUSH(w) { if ((threadIdx.x & 63) == 0) for (int i = 0; i < 8; ++i) g_tw_stamps[(w) * 8 + i] = st_acc[i]; }
-#else
-#define TW_ST_DECL
-#define TW_ST(i)
-#define TW_ST_FLUSH(w)
-#endif
-
-#ifndef TW_EMIT_LATE
-#define TW_EMIT_LATE 1  // tw_bwd: dqkv emission after the head's dxn GEMMs (see there)
-#endif
-#ifndef TW_FWD_PG
-#define TW_FWD_PG 1  // pixels per interleaved attention-core group in tw_fwd (2 / 4 measured neutral)
-#endif
 constexpr int RS = 36;  // RoPE table row stride (floats): 16-B aligned, spreads frames over banks
 constexpr float LOG2E = 1.4426950408889634f;
 
@@ -869,17 +843,10 @@ __device__ __forceinline__ void rope4c(float* o4, const f32x4 cs) {
 // issued back to back, the next kind's weight fragments are in flight meanwhile (double buffer), and the RoPE
 // coefficients are read from LDS before the MFMAs, so the epilogue waits on nothing.  (Round 3 ran each tile as
 // load-wait -> 2 MFMAs -> s_nop -> LDS read -> wait -> VALU -> store, one chain at a time.)
-// the first q/k/v weight tile of head h (tw_qkv_b's buffer 0)
-template <int C, int NV>
-__device__ __forceinline__ void tw_qkv_b_first(const bf16* __restrict__ wqkv, int h, bf16x8 (&a0)[TW<C, NV>::KS], int lr,
-                                               int lg) {
-#pragma unroll
-  for (int ks = 0; ks < TW<C, NV>::KS; ++ks) a0[ks] = ld_img(wqkv, h * 2, TW<C, NV>::KS, ks, lg * 16 + lr);
-}
 template <int C, int NV, bool QSCALE = true>
 __device__ __forceinline__ void tw_qkv_b(const bf16* __restrict__ wqkv, const bf16x8 (&xf)[NV][C / 32], int h,
                                          const int (&fr)[NV], float scale, const float* rot, bf16* sq, bf16* sk,
-                                         bf16* sv, int lr, int lg, const bf16x8* a0 = nullptr) {
+                                         bf16* sv, int lr, int lg) {
   using T = TW<C, NV>;
   constexpr int R = NV * 16;
   // 6 (kind, half) column tiles; the next tile's weight fragments in flight while this one computes
@@ -888,12 +855,7 @@ __device__ __forceinline__ void tw_qkv_b(const bf16* __restrict__ wqkv, const bf
 #pragma unroll
     for (int ks = 0; ks < T::KS; ++ks) a[buf][ks] = ld_img(wqkv, (ct >> 1) * 16 + h * 2 + (ct & 1), T::KS, ks, lg * 16 + lr);
   };
-  if (a0) {  // issued by the caller (TW_QKV_EARLY: before the previous head's O stores)
-#pragma unroll
-    for (int ks = 0; ks < T::KS; ++ks) a[0][ks] = a0[ks];
-  } else {
-    ld(0, 0);
-  }
+  ld(0, 0);
 #pragma unroll
   for (int ct = 0; ct < 6; ++ct) {
     const int buf = ct & 1, kind = ct >> 1, u = ct & 1;
@@ -993,22 +955,12 @@ __device__ __forceinline__ void tw_ln(const bf16* __restrict__ x, const float* _
 // waves per SIMD of tw_fwd: at C = 64 LDS-bound (per-wave q/k/v slices + tables: 3 blocks of 53 KB);
 // at C >= 128 register-bound (the out-projection accumulators spill below 256 VGPRs)
 typedef unsigned int tw_u32x2 __attribute__((ext_vector_type(2)));
-#ifndef TWB_EPI_PRE
-#define TWB_EPI_PRE 1  // tw_bwd: all x / dy / stats loads of the LN-backward epilogue before its first dx store (0: per-tile rounds)
-#endif
-#ifndef TW_EPI_PRE
-#define TW_EPI_PRE 0  // tw_fwd: all residual loads of the y epilogue issued before its first store (0: per-tile load -> store)
-#endif
-#ifndef TW_QKV_EARLY
-#define TW_QKV_EARLY 2  // tw_fwd (C = 64), bit 0: the next head's first weight tile loaded before this head's O stores;
-                        // bit 1: the head's lse stored after the to_out weight loads (vmcnt counts loads and stores in
-                        // order: a load issued after a store also waits for it)
-#endif
-#ifndef TW_FWD_OCC64
-#define TW_FWD_OCC64 3
-#endif
+// Measured and removed (profiles/r5f_tw_fwd_lse_late_tb.txt, r5f_epilogue_loads_first_tb.txt, r2_v13_*): the next
+// head's first weight tile loaded before the O stores (21 spilled registers, +5 %), every residual load before the y
+// stores (4 spills, +1-3 %), 2 waves per SIMD with the next head's weights prefetched in registers (+2 %), pixels
+// interleaved phase by phase in the attention core (neutral).
 template <int C>
-constexpr int tw_fwd_occ() { return C <= 64 ? TW_FWD_OCC64 : 2; }
+constexpr int tw_fwd_occ() { return C <= 64 ? 3 : 2; }
 template <int C, int NV, bool FOLD = false>
 __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ gamma,
                                                      const bf16* __restrict__ wqkv, const bf16* __restrict__ wout,
@@ -1058,28 +1010,13 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
     for (int vt = 0; vt < T::NVTM; ++vt) yacc[ct][vt] = f32x4{0.f, 0.f, 0.f, 0.f};
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
 
-  // next head's QKV weights prefetched into registers (48 VGPRs at C=64): only at 2 waves / SIMD, where
-  // the register budget has room and there is no third wave to hide the weight loads
-  constexpr bool PREF = C <= 64 && tw_fwd_occ<C>() <= 2;
-  bf16x8 wq[6][PREF ? T::KS : 1];
-  if constexpr (PREF) tw_load_wq<C, NV>(wq, wqkv, 0, lr, lg);
-  constexpr bool QE = (TW_QKV_EARLY & 1) && !PREF && C == 64;  // early first weight tile
-  constexpr bool LE = (TW_QKV_EARLY & 2) && !PREF && C == 64;  // deferred lse stores
-  bf16x8 a0n[T::KS];  // QE: the next head's first q/k/v weight tile
-  if constexpr (QE) tw_qkv_b_first<C, NV>(wqkv, 0, a0n, lr, lg);
+  // C = 64: the head's lse stored after the to_out weight loads (vmcnt counts loads and stores in order: a load
+  // issued after a store also waits for it; round 5 -0.8 %)
+  constexpr bool LE = C == 64;
   for (int h = 0; h < NH; ++h) {
     bf16x8 wo[T::CT];
-    if constexpr (PREF) {
-#pragma unroll
-      for (int ct = 0; ct < T::CT; ++ct) wo[ct] = ld_img(wout, ct, INNER / 32, h, lane);  // image of W_out [C][256]
-    }
-    if constexpr (PREF) {
-      tw_qkv_pre<C, NV>(wq, xf, fr, FOLD ? 1.f : scale, rot, sq, sk, sv, lr, lg);  // FOLD: scale in the weights
-      if (h + 1 < NH) tw_load_wq<C, NV>(wq, wqkv, h + 1, lr, lg);  // in flight during the core
-    } else {
-      if constexpr (C == 64) tw_qkv_b<C, NV, !FOLD>(wqkv, xf, h, fr, scale, rot, sq, sk, sv, lr, lg, QE ? a0n : nullptr);
-      else tw_qkv<C, NV, false>(wqkv, xf, h, fr, FOLD ? 1.f : scale, rot, sq, sk, sv, lr, lg);  // two-tile batches
-    }
+    if constexpr (C == 64) tw_qkv_b<C, NV, !FOLD>(wqkv, xf, h, fr, scale, rot, sq, sk, sv, lr, lg);
+    else tw_qkv<C, NV, false>(wqkv, xf, h, fr, FOLD ? 1.f : scale, rot, sq, sk, sv, lr, lg);  // two-tile batches
     // bias (log2 units) of this lane's 4 entries (i = lr, j = 4g + r); -inf masks padding frames
     float bt[4];
 #pragma unroll
@@ -1094,8 +1031,8 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
     // with each phase issued for the whole group (independent MFMA -> softmax -> MFMA chains
     // interleave instead of serialising on the MFMA result latency).  Pixels past HW hold zero rows
     // (their LN input is masked): computing them is harmless, only the lse store is guarded.
-    constexpr int PG = TW_FWD_PG < T::PW ? TW_FWD_PG : T::PW;
-    float lsev[T::PW];  // QE: the pixels' lse (log2 units)
+    constexpr int PG = 1;  // (2 / 4 measured neutral)
+    float lsev[T::PW];  // LE: the pixels' lse (log2 units)
 #pragma unroll
     for (int pg = 0; pg < T::PW; pg += PG) {
       f32x4 st[PG];
@@ -1151,7 +1088,7 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
         }
       }
     }
-    if constexpr (!PREF) {  // issued after the core: keeps the 16 registers out of the qkv phase
+    {  // issued after the core: keeps the 16 registers out of the qkv phase
 #pragma unroll
       for (int ct = 0; ct < T::CT; ++ct) wo[ct] = ld_img(wout, ct, INNER / 32, h, lane);
     }
@@ -1168,10 +1105,6 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
     bf16x8 ob[T::NVTM];
 #pragma unroll
     for (int vt = 0; vt < T::NVTM; ++vt) ob[vt] = vt < NVT ? ld16(sq + hs_off<R>(vt * 16 + lr, lg * 8)) : zero8();
-    if constexpr (QE) {  // the next head's first weight tile, ahead of this head's O stores
-      if (h + 1 < NH) tw_qkv_b_first<C, NV>(wqkv, h + 1, a0n, lr, lg);
-      __builtin_amdgcn_sched_barrier(0);
-    }
     if (o_out) {  // O_h for the to_out weight gradient (the backward then skips its emission)
 #pragma unroll
       for (int vt = 0; vt < T::NVTM; ++vt) {
@@ -1189,44 +1122,6 @@ __global__ __launch_bounds__(256, tw_fwd_occ<C>()) void tw_fwd_kernel(const bf16
     wave_lds_sync();
   }
   // y = x + attn
-#if TW_EPI_PRE
-  // every residual load issued before the first y store, and the stores branch-free through a buffer resource over
-  // sample b (rows outside the tile go to an out-of-range offset, which the hardware drops): vmcnt retires in issue
-  // order, so a load behind a store waits for it, and the per-tile load -> store rounds serialised the store round
-  // trips (a branch per tile also let the compiler sink loads behind earlier stores)
-  const int64_t sbytes = (int64_t)F * HW * C * 2;
-  if (sbytes < 0x7fff0000) {  // uniform
-    const __amdgpu_buffer_rsrc_t yrs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(y + (int64_t)b * F * HW * C), (short)0, (int)sbytes, 0x00020000);
-    int voff[T::NVTM];
-    int64_t rows[T::NVTM];
-#pragma unroll
-    for (int vt = 0; vt < T::NVTM; ++vt) {
-      int64_t row = 0;
-      const bool ok = vt < NVT && tw_row(vt * 16 + lr, VW, F, F4, p0, HW, b, row);
-      rows[vt] = ok ? row : 0;
-      voff[vt] = ok ? (int)((row - (int64_t)b * F * HW) * C * 2) : 0x7ffffff0;
-    }
-    bf16x4 xr[T::NVTM][T::CT];
-#pragma unroll
-    for (int vt = 0; vt < T::NVTM; ++vt)
-#pragma unroll
-      for (int ct = 0; ct < T::CT; ++ct)
-        if (vt < NVT) xr[vt][ct] = *reinterpret_cast<const bf16x4*>(x + rows[vt] * C + ct * 16 + lg * 4);
-#pragma unroll
-    for (int vt = 0; vt < T::NVTM; ++vt) {
-      if (vt >= NVT) break;
-#pragma unroll
-      for (int ct = 0; ct < T::CT; ++ct) {
-        bf16x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = (bf16)(yacc[ct][vt][r] + (float)xr[vt][ct][r]);
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(tw_u32x2, o), yrs, voff[vt] + (ct * 16 + lg * 4) * 2, 0, 0);
-      }
-    }
-    return;
-  }
-#endif
 #pragma unroll
   for (int vt = 0; vt < T::NVTM; ++vt) {
     if (vt >= NVT) break;
@@ -1298,7 +1193,6 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
 #pragma unroll
   for (int vt = 0; vt < NV; ++vt) fr[vt] = (vt * 16 + lr) % F4 < F ? (vt * 16 + lr) % F4 : 0;
 
-  TW_ST_DECL
   for (int pg = blockIdx.x * 4 + wid; pg < npg; pg += nw) {
     const int p0 = pg * T::PW;
     bf16x8 xf[T::NVTM][T::KS];
@@ -1329,7 +1223,6 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
           dyr[vt][ks] = sel8(vrow[vt] >= 0, ldnt16(dy + (vrow[vt] >= 0 ? vrow[vt] : 0) * C + ks * 32 + lg * 8));
     }
 
-    TW_ST(0)
     for (int h = 0; h < NH; ++h) {
       // issued ahead of the q/k/v GEMMs so its latency hides behind them: this head's log-sum-exp
       // of the wave's pixels (one per frame row lr)
@@ -1346,7 +1239,6 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
         }
       }
       tw_qkv<C, NV>(wqkv, xf, h, fr, scale, rot, sq, sk, sv, lr, lg);
-      TW_ST(1)
       // dO_h^T = W_out[:, h]^T . dy^T
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
@@ -1379,7 +1271,6 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
         brm[r] = ok ? sb[(h * F + c) * F + lr] : 0.f;
       }
       wave_lds_sync();
-      TW_ST(2)
       // core backward per pixel; dq/dk/dv overwrite the pixel's own q/k/v rows at the end
       float dbr[4] = {0.f, 0.f, 0.f, 0.f};
       for (int pp = 0; pp < T::PW; ++pp) {
@@ -1487,7 +1378,6 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
       for (int r = 0; r < 4; ++r)
         if (lr < F && lg * 4 + r < F) sdb[(h * F + lr) * F + lg * 4 + r] += dbr[r];
       wave_lds_sync();
-      TW_ST(3)
       // dxn^T += W_qkv[h rows]^T . [dq|dk|dv]_h^T ; emit dqkv_h
 #pragma unroll
       for (int kind = 0; kind < 3; ++kind) {
@@ -1502,19 +1392,10 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
           for (int vt = 0; vt < T::NVTM; ++vt)
             if (vt < NVT) dxacc[ct][vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bf[vt], dxacc[ct][vt], 0, 0, 0);
         }
-        if (dqkv_out && !TW_EMIT_LATE) {
-#pragma unroll
-          for (int vt = 0; vt < T::NVTM; ++vt) {
-            if (vt >= NVT) break;
-            int64_t row = 0;
-            if (tw_row(vt * 16 + lr, VW, F, F4, p0, HW, b, row))
-              stnt16(dqkv_out + row * QKV + kind * INNER + h * DH + lg * 8, bf[vt]);
-          }
-        }
       }
       // emission after all of the head's weight loads: a load issued behind a store waits for it
       // (vmcnt counts both in issue order), so storing between the kinds stalled the next kind's W^T loads
-      if (dqkv_out && TW_EMIT_LATE) {
+      if (dqkv_out) {
 #pragma unroll
         for (int kind = 0; kind < 3; ++kind) {
           const bf16* src = kind == 0 ? sq : (kind == 1 ? sk : sv);
@@ -1528,24 +1409,9 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
         }
       }
       wave_lds_sync();
-      TW_ST(4)
     }
     // LN backward: dx = rstd*(g - mean(g) - xhat*mean(g*xhat)) + dy, g = dxn*gamma
-#if defined(TWB_ABL_LNB) && TWB_ABL_LNB == 0
-    // ablation (diagnostic builds only): dx = dxn, no LN-backward loads / reductions
-#pragma unroll
-    for (int vt = 0; vt < T::NVTM; ++vt) {
-      int64_t row = 0;
-      if (vt < NVT && tw_row(vt * 16 + lr, VW, F, F4, p0, HW, b, row))
-#pragma unroll
-        for (int ct = 0; ct < T::CT; ++ct) {
-          float o4[4] = {dxacc[ct][vt][0], dxacc[ct][vt][1], dxacc[ct][vt][2], dxacc[ct][vt][3]};
-          stnt4(dx + row * C + ct * 16 + lg * 4, o4);
-        }
-    }
-    if (false)
-#endif
-    if (TWB_EPI_PRE && (int64_t)F * HW * C * 2 < 0x7fff0000) {  // uniform
+    if ((int64_t)F * HW * C * 2 < 0x7fff0000) {  // uniform
       // every x / dy / stats load before the first dx store, the stores branch-free through a buffer resource over
       // sample b (rows outside the group go to an out-of-range offset, which the hardware drops): vmcnt retires in
       // issue order, so a load behind a store waits for it (the per-tile dy load -> dx store rounds)
@@ -1562,7 +1428,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
         int64_t row = 0;
         okv[vt] = tw_row(vt * 16 + lr, VW, F, F4, p0, HW, b, row);
         row = okv[vt] ? row : 0;
-        voff[vt] = okv[vt] ? (int)((row - s0) * C * 2) : 0x7ffffff0;
+        voff[vt] = okv[vt] ? (int)((row - s0) * C * 2) : 0x7fff8000;  // + co * 2 stays < INT_MAX, > num_records
         mrv[vt] = *reinterpret_cast<const float2*>(mr + row * 2);
 #pragma unroll
         for (int ct = 0; ct < T::CT; ++ct) {
@@ -1671,9 +1537,7 @@ __global__ __launch_bounds__(256, 2) void tw_bwd_kernel(
         }
       }
     }
-    TW_ST(5)
   }
-  TW_ST_FLUSH(blockIdx.x * 4 + wid)
   if constexpr (DG_REG) {
 #pragma unroll
     for (int ct = 0; ct < T::CT; ++ct)
@@ -1720,16 +1584,13 @@ static void allow_smem(K kernel, size_t bytes) {
   if (bytes > 65536) (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
-#ifndef TW_SMEM_PAD
-#define TW_SMEM_PAD 0  // diagnostic knob: extra dynamic LDS per tw_fwd block (forces fewer blocks per CU)
-#endif
 template <int C, int NV, bool FOLD = false>
 static void tw_fwd_launch_nv(const void* x, const float* gamma, const void* wqkv, const void* wout, const float* bias,
                              const float* rot, void* y, float* mr, float* lse, void* o, int B, int F, int HW,
                              float scale, float eps, hipStream_t stream) {
   const int npg = (int)cdiv(HW, TW<C>::PW);
   dim3 grid((unsigned)cdiv(npg, 4), B);
-  const size_t sm = tw_fwd_smem<C>(F) + TW_SMEM_PAD;
+  const size_t sm = tw_fwd_smem<C>(F);
   allow_smem(tw_fwd_kernel<C, NV, FOLD>, sm);
   tw_fwd_kernel<C, NV, FOLD><<<grid, 256, sm, stream>>>((const bf16*)x, gamma, (const bf16*)wqkv, (const bf16*)wout,
                                                         bias, rot, (bf16*)y, mr, lse, (bf16*)o, F, HW, scale, eps);
@@ -1796,11 +1657,6 @@ static int tw_bwd_launch(const void* x, const void* dy, const float* gamma, cons
 }
 
 }  // namespace
-#ifdef CESM_TW_STAMPS
-extern "C" int cesm_diag_tw_stamps(unsigned long long* out, int n) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tw_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -3;
-}
-#endif
 
 // ============================================================================================
 // Head-parallel fused backward with in-kernel weight gradients (C = 64, 4*F <= 48).
@@ -1851,38 +1707,16 @@ __device__ __forceinline__ s16x4 kslot4_ld(const bf16* tile, int ld, int lane) {
 // twh_bwd: pixels whose attention-core backward is interleaved phase by phase.  Fixed at 1 (round 2: 3375 vs
 // 3460 us with 2, 2 spills vs 10); 2 no longer fits the LDS next to the round-3 tiles, so it is not a knob.
 constexpr int TWH_PG = 1;
-#ifndef TWH_PK
-#define TWH_PK 1  // A/B knob: packed 2-wide fp32 VALU ops in twh_bwd's softmax-gradient elementwise step
-#endif
-#ifndef TWH_QKV_PIPE
-#define TWH_QKV_PIPE 1  // twh_bwd: double-buffered q/k/v weight batches, the first issued before barrier A
-#endif
-#ifndef TWH_WPIPE
-#define TWH_WPIPE 1  // twh_bwd: the dxn GEMM's weight fragments in a TWH_RING-deep ring
-#endif
-#ifndef TWH_RING
-#define TWH_RING 2
-#endif
-#ifndef TWH_PF_LATE
-#define TWH_PF_LATE 0  // twh_bwd: next group's x / dy prefetch issued after the head phase's weight loads (0: after barrier A)
-#endif
-#ifndef TWH_DX_LATE
-#define TWH_DX_LATE 2  // twh_bwd: a group's dx stores issued after the next group's q/k/v/dO weight loads (1: after its first batch; vmcnt counts
-                       // loads and stores in order: issued before them, the loads' first wait also waited for the stores)
-#endif
-#ifndef TWH_DO_PF
-#define TWH_DO_PF 1  // twh_bwd: the dO GEMM's weights issued during the last q/k/v batch (needs QKV_PIPE)
-#endif
-// the DWO instantiation (in-kernel dW_out, 32 more accumulators) trades prefetch registers for them:
-#ifndef TWH_QB_DWO
-#define TWH_QB_DWO 1     // q/k/v weight tiles per prefetch batch (2 in the plain kernel)
-#endif
-#ifndef TWH_DO_PF_DWO
-#define TWH_DO_PF_DWO 0  // dO weights prefetched during the last q/k/v batch
-#endif
-#ifndef TWH_WPIPE_DWO
-#define TWH_WPIPE_DWO 0  // the dxn GEMM's weight ring
-#endif
+// The dxn GEMM's W'^T fragments in a ring of this depth (round 2: 3 +3-4 %, no ring +4.5 %).
+constexpr int TWH_RING = 2;
+// Measured and removed (A/B records: profiles/r2_v13_*, r3_attn_knobs_ab.txt, r4_attn_variants_ab.txt, r5_prio_ab.txt,
+// r5_dxt_tb.txt, r5f_prefetch_pos_tb.txt, r5f_twh_dx_late_tb.txt, r5f_twh_ldq_early_tb.txt, r5_twh_dwout_env_ab.txt):
+// q/k/v weights without the double-buffered batches (+1.5-2 %), the dO weights loaded after the q/k/v batches
+// (+1-2.5 %), scalar instead of packed fp32 in the softmax-gradient step (+0.5 %), the next group's x / dy prefetch
+// after the head phase (neutral), the dx stores right after LN backward or after the first weight batch (+0.8 %),
+// s_setprio for waves 4-7 (neutral), dxn by whole output tiles after a block barrier (3.82 -> 4.35 ms per call), and the
+// to_out weight gradient in-kernel (DWO: 32 persistent accumulators, 58-93 spilled registers, 3.3 -> 5.3 ms per call
+// -- more than the forward's O write and the O^T dy GEMM it removes).
 constexpr int TH_XLD = 72;   // xhat / dy tile row stride (bf16, 144-B rows)
 constexpr int TH_NVMAX = 3;  // voxel tiles per group (4*F <= 48): the 8 slices then fit in LDS
 // twh_bwd keeps round 2's padded tiles (80-B slice rows, 144-B xhat / dy rows, 68-float partial rows): the region
@@ -1895,43 +1729,14 @@ constexpr int TWH_PLD = 68;  // fp32 row stride of a wave's partial dxn rows (wr
 // pixel read up to (PW-1)F + 16 - R <= 12 rows past dO (F = 4), which must be finite (the next wave's region may
 // still hold fp32 partial rows)
 #define TWH_WSTRIDE(R) (4 * (R) * HLD + 16 * HLD)
-#ifndef TWH_POISON
-#define TWH_POISON 0  // diagnostic knob (see twh_bwd_kernel)
-#endif
-#ifndef TWH_PRIO
-#define TWH_PRIO 0  // A/B knob: s_setprio 1 for waves 4-7 of twh_bwd
-#endif
-#ifndef TWH_DXT
-#define TWH_DXT 0       // 1: dxn by whole output tiles after a block barrier (round 5: 3.82 -> 4.35 ms per call,
-                        // profiles/r5_dxt_tb.txt); 0 = per-head fp32 partials (round 2-4)
-#endif
-#ifndef TWH_DXT_RING
-#define TWH_DXT_RING 3  // W'^T fragments in flight in the tiled dxn GEMM
-#endif
-#ifndef TWH_DXT_ONELOOP
-#define TWH_DXT_ONELOOP 1  // the tiled dxn GEMM as one loop with per-MFMA wave-uniform skips (0: one copy per tile count)
-#endif
-// TWH_DXT: fp32 g rows (256 B) in the dO slices of waves 0..3, TWH_GRPR(R) rows per slice
-#define TWH_GRPR(R) ((R) * HLD * 2 / 256)
-__device__ __forceinline__ float* twh_grow(bf16* slices, int R, int v) {
-  const int rpr = TWH_GRPR(R);
-  return reinterpret_cast<float*>(slices + (v / rpr) * TWH_WSTRIDE(R) + 3 * R * HLD) + (v % rpr) * 64;
-}
-static size_t twh_smem(int F, int NV, bool dwo) {
+static size_t twh_smem(int F, int NV) {
   (void)F;
   const int R = NV * 16;
-  return (size_t)16 * RS * 4 + (size_t)8 * TWH_PG * 2 * 256 * 2 + (size_t)(2 * R + (dwo ? 16 : 0)) * TH_XLD * 2 +
+  return (size_t)16 * RS * 4 + (size_t)8 * TWH_PG * 2 * 256 * 2 + (size_t)(2 * R) * TH_XLD * 2 +
          (size_t)8 * TWH_WSTRIDE(R) * 2;
 }
 
-// DWO (round 5): the to_out weight gradient in-kernel too.  Per pixel and head, O_h = P V_h (A = P straight from the
-// softmax registers, B = V through the k-slot read) comes out of the MFMA in exactly the B layout of
-// dW_out[:, h] += dy^T O_h (A = dy^T from the block's dy tile by the transposed read), so neither the forward's
-// 256-channel O (512 B per voxel written, then re-read by a wide weight-gradient GEMM with dy) nor an LDS round trip
-// is needed: 10 K = 16 MFMAs and 32 accumulator registers per wave.  Rows of O_h past the pixel's F frames are 0
-// (P is 0 there), so the dy rows the transposed read takes past them (the next pixel's, or the zeroed 16-row pad
-// after the tile) contribute nothing.
-template <int NV, bool DWO>
+template <int NV>
 __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ dy, const float* __restrict__ mr,
     const float* __restrict__ lse, const bf16* __restrict__ wqkv, const bf16* __restrict__ wqkv_t,
@@ -1943,21 +1748,12 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
   constexpr int R = NV * 16;
   static_assert(TWH_PLD * 4 <= 4 * HLD * 2, "partial dxn rows fit over the wave's slices");
   extern __shared__ __attribute__((aligned(16))) float smem[];
-#if TWH_POISON
-  {  // diagnostic (TWH_POISON = 1: every LDS word NaN, 2: zero) before first use: a read of LDS that this launch has
-     // not written then shows up as a NaN (or as a repeatable value)
-    constexpr int W = (16 * RS * 4 + 8 * TWH_PG * 2 * 256 * 2 + (2 * R + (DWO ? 16 : 0)) * TH_XLD * 2 +
-                       8 * TWH_WSTRIDE(R) * 2) / 4;
-    for (int e = threadIdx.x; e < W; e += 512) reinterpret_cast<unsigned*>(smem)[e] = TWH_POISON == 1 ? 0xffffffffu : 0u;
-    __syncthreads();
-  }
-#endif
   const int FF = F * F;
   float* rot = smem;                                 // [16][RS]
   float* trbuf = rot + 16 * RS;                      // [8 waves][TWH_PG][2][16][16] bf16 P / dS tiles
   bf16* xt = reinterpret_cast<bf16*>(trbuf) + 8 * TWH_PG * 2 * 256;  // [R][TH_XLD] xhat (bf16)
-  bf16* dyt = xt + R * TH_XLD;                       // [R][TH_XLD] dy (+ a 16-row zero pad with DWO)
-  bf16* slices = dyt + (R + (DWO ? 16 : 0)) * TH_XLD;  // 8 x [q|k|v|dO][R][HLD]
+  bf16* dyt = xt + R * TH_XLD;                       // [R][TH_XLD] dy
+  bf16* slices = dyt + R * TH_XLD;                   // 8 x [q|k|v|dO][R][HLD]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const int h = wid;
@@ -1965,14 +1761,9 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
   bf16* sk = sq + R * HLD;
   bf16* sv = sk + R * HLD;
   bf16* sdo = sv + R * HLD;
-  // static priority for the younger half (waves 4-7; TWH_PRIO A/B knob): the VALU-issue arbitration between the
-  // two waves of a SIMD is by priority, then age (MI355X_MICROARCH.md, two waves per SIMD, item 4)
-  if (TWH_PRIO && __builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
   for (int e = tid; e < F * 32; e += 512) rot[(e >> 5) * RS + (e & 31)] = rotg[e];
-  // the wave's 16-row pad past dO (never written afterwards: the partial rows fit over the slices), the dy tile's pad
+  // the wave's 16-row pad past dO (never written afterwards: the partial rows fit over the slices)
   for (int e = lane; e < 8 * HLD; e += 64) reinterpret_cast<float*>(sq + 4 * R * HLD)[e] = 0.f;
-  if constexpr (DWO)
-    for (int e = tid; e < 8 * TH_XLD; e += 512) reinterpret_cast<float*>(dyt + R * TH_XLD)[e] = 0.f;
   // this wave's (head's) bias entries, log2 units: transposed (i = lr, j = 4g + r) and row-major (i = 4g + r, j = lr)
   float bt[4], brm[4];
 #pragma unroll
@@ -2024,16 +1815,13 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
 #pragma unroll
     for (int n = 0; n < 4; ++n) dwacc[m][n] = z4;
   float dbacc[4] = {0.f, 0.f, 0.f, 0.f};
-  // DWO: dW_out[c = ct * 16 + 4 lg + r][h * 32 + half * 16 + lr]
-  f32x4 dwo[DWO ? 4 : 1][2];
-#pragma unroll
-  for (int ct = 0; ct < (DWO ? 4 : 1); ++ct) dwo[ct][0] = dwo[ct][1] = z4;
 
   prefetch(blockIdx.x);
-  // TWH_DX_LATE: the previous group's dx chunk of this thread and its row (-1: none)
+  // the previous group's dx chunk of this thread and its row (-1: none): stored after this group's q/k/v/dO weight
+  // loads (vmcnt counts loads and stores in issue order: stored before them, the loads' first wait also waited for
+  // the stores; round 5 -0.8 %)
   bf16x8 dx_pend = zero8();
   int64_t dx_row = -1;
-  TW_ST_DECL
   for (int gg = blockIdx.x; gg < ngroups; gg += gridDim.x) {
     const int b = gg / npg, p0 = (gg - b * npg) * T::PW;
     // ---- LN of the group (this thread's voxel chunk) from the prefetch registers
@@ -2055,15 +1843,12 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
     const bf16* wq_g = wqkv + oz;
     const bf16* wqt_g = wqkv_t + oz;
     const bf16* wot_g = wout_t + oz;
-#if TWH_QKV_PIPE
     // q/k/v weight fragments in two-tile batches, double-buffered: batch 0 issued before barrier A (its L2
-    // latency overlaps the barrier wait), batch c+1 issued before batch c's MFMAs
-    // (TWH_QB tiles per batch: 2, or 1 -- half the registers, for the DWO instantiation's register budget)
-    constexpr int QB = DWO ? TWH_QB_DWO : 2;
+    // latency overlaps the barrier wait), batch c+1 issued before batch c's MFMAs; the dO GEMM's weights during the
+    // last batch
+    constexpr int QB = 2;
     bf16x8 wqa[2][QB][T::KS];
-#if TWH_DO_PF
-    bf16x8 wob[DWO && !TWH_DO_PF_DWO ? 1 : 2][T::KS];
-#endif
+    bf16x8 wob[2][T::KS];
     auto ldq = [&](int c0, int buf) {
 #pragma unroll
       for (int u = 0; u < QB; ++u) {
@@ -2073,14 +1858,8 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
       }
     };
     ldq(0, 0);
-#endif
-    if (TWH_DX_LATE == 1 && dx_row >= 0) {  // the previous group's dx, behind this group's first weight loads
-      __builtin_amdgcn_sched_barrier(0);
-      stnt16(dx + dx_row * C + cc * 8, dx_pend);
-    }
     __syncthreads();  // (A) tiles of this group ready; previous group's partials consumed
-    if (!TWH_PF_LATE) prefetch(gg + gridDim.x);  // next group's x / dy / stats: in flight during the head phase
-    TW_ST(0)
+    prefetch(gg + gridDim.x);  // next group's x / dy / stats: in flight during the head phase
 
     // ---- head phase: wave h
     float Lp[T::PW];
@@ -2096,19 +1875,16 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
       for (int vt = 0; vt < NV; ++vt)
 #pragma unroll
         for (int ks = 0; ks < T::KS; ++ks) xf[vt][ks] = ld16(xt + (vt * 16 + lr) * TH_XLD + ks * 32 + lg * 8);
-#if TWH_QKV_PIPE
 #pragma unroll
       for (int c0 = 0; c0 < 6; c0 += QB) {
         const int buf = (c0 / QB) & 1;
         if (c0 + QB < 6) ldq(c0 + QB, buf ^ 1);
-#if TWH_DO_PF
-        else if (!DWO || TWH_DO_PF_DWO) {  // the dO GEMM's W_out^T fragments, in flight during the last q/k/v batch
+        else {  // the dO GEMM's W_out^T fragments, in flight during the last q/k/v batch
 #pragma unroll
           for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
-            for (int ks = 0; ks < T::KS; ++ks) wob[DWO && !TWH_DO_PF_DWO ? 0 : dt][ks] = ld_img(wot_g, h * 2 + dt, T::KS, ks, lane);
+            for (int ks = 0; ks < T::KS; ++ks) wob[dt][ks] = ld_img(wot_g, h * 2 + dt, T::KS, ks, lane);
         }
-#endif
         // batched (round 4), one 16-dim half at a time: the half's RoPE coefficients read first, its NV tiles issued
         // back to back, then their epilogues (round 3: one MFMA -> s_nop -> LDS read -> wait -> VALU -> store chain
         // per tile; both halves at once spill at 256 VGPRs)
@@ -2137,29 +1913,11 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
           }
         }
       }
-#else
-#error "TWH_QKV_PIPE=0: tw_qkv writes the region layout, twh_bwd reads 80-B rows"
-#endif
     }
-    // TWH_PF_LATE: the next group's x / dy after every q/k/v/dO weight load (vmcnt retires in issue order, so a
-    // weight batch issued behind the HBM prefetch waits for it)
-    if (TWH_PF_LATE) prefetch(gg + gridDim.x);
-    TW_ST(1)
     // dO_h^T = W_out[:, h]^T . dy^T
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt) {
-      bf16x8 a[T::KS];
-#pragma unroll
-      for (int ks = 0; ks < T::KS; ++ks) {
-#if TWH_DO_PF
-        if (!DWO || TWH_DO_PF_DWO)
-          a[ks] = wob[DWO && !TWH_DO_PF_DWO ? 0 : dt][ks];
-        else
-          a[ks] = ld_img(wot_g, h * 2 + dt, T::KS, ks, lane);
-#else
-        a[ks] = ld_img(wot_g, h * 2 + dt, T::KS, ks, lane);
-#endif
-      }
+      const auto& a = wob[dt];
 #pragma unroll
       for (int vt = 0; vt < NV; ++vt) {
         f32x4 acc = z4;
@@ -2171,12 +1929,11 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
         store4(sdo + (vt * 16 + lr) * HLD + dt * 16 + lg * 4, o4);
       }
     }
-    if (TWH_DX_LATE == 2 && dx_row >= 0) {  // the previous group's dx, behind this group's q/k/v/dO weight loads
+    if (dx_row >= 0) {  // the previous group's dx, behind this group's q/k/v/dO weight loads
       __builtin_amdgcn_sched_barrier(0);
       stnt16(dx + dx_row * C + cc * 8, dx_pend);
     }
     wave_lds_sync();
-    TW_ST(2)
     // attention-core backward, TWH_PG pixels interleaved phase by phase; only the transposed orientation is
     // computed (S^T, dP^T on MFMA, softmax rows per lane), P and dS reach the row-major orientation of the
     // dK / dV products through a 16 x 16 bf16 LDS tile and the hardware transpose read
@@ -2203,7 +1960,6 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
 #pragma unroll
         for (int q = 1; q < T::PW; ++q) Li = pp0 + u == q ? Lp[q] : Li;
         float pt[4], D = 0.f;
-#if TWH_PK
         // two elements per VALU op (v_pk_fma / v_pk_add / v_pk_mul_f32) where the order allows, same results
         float ds4[4];
 #pragma unroll
@@ -2234,23 +1990,6 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
           d4[r] = (bf16)ds4[r];
           p4[r] = (bf16)pt[r];
         }
-#else
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bool ok = pix && lg * 4 + r < F && lr < F;
-          pt[r] = ok ? __builtin_amdgcn_exp2f(fmaf(st[u][r], LOG2E, bt[r]) - Li) : 0.f;
-          D = fmaf(pt[r], dpt[u][r], D);
-        }
-        D = grp4_sum(D);
-        bf16x4 p4, d4;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float ds = pt[r] * (dpt[u][r] - D);
-          dbacc[r] += ds;
-          d4[r] = (bf16)ds;
-          p4[r] = (bf16)pt[r];
-        }
-#endif
         dst_b[u] = __builtin_bit_cast(s16x4, d4);
         pa_b[u] = __builtin_bit_cast(s16x4, p4);
         // tile[i = lr][j = 4g .. 4g+3]
@@ -2263,24 +2002,6 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
 #pragma unroll
         for (int half = 0; half < 2; ++half)
           dqt[u][half] = mfma_k16(kslot4_hld(sk, (pp0 + u) * F, half * 16, lane), dst_b[u], z4);  // dQ'^T[d][i]
-      if constexpr (DWO) {
-#pragma unroll
-        for (int u = 0; u < PG; ++u) {
-          const int rb = (pp0 + u) * F;
-          s16x4 ob[2];
-#pragma unroll
-          for (int half = 0; half < 2; ++half) {
-            const f32x4 oh = mfma_k16(pa_b[u], kslot4_hld(sv, rb, half * 16, lane), z4);  // O_h[i][d]
-            ob[half] = bf16x4_bits(oh[0], oh[1], oh[2], oh[3]);
-          }
-#pragma unroll
-          for (int ct = 0; ct < 4; ++ct) {
-            const s16x4 a = tr4(dyt, TH_XLD, rb, ct * 16, lane);  // dy^T[c][i]
-#pragma unroll
-            for (int half = 0; half < 2; ++half) dwo[ct][half] = mfma_k16(a, ob[half], dwo[ct][half]);
-          }
-        }
-      }
       wave_lds_sync();  // P / dS tiles visible
       f32x4 dkt[PG][2], dvt[PG][2];
 #pragma unroll
@@ -2317,130 +2038,12 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
       }
     }
     wave_lds_sync();
-    TW_ST(3)
-    if constexpr (TWH_DXT) {
-      // dW'_h += dqkv_h^T . xhat over the group's voxels (K = voxels, 16 per step; padded rows are zero)
-#pragma unroll
-      for (int kk = 0; kk < NV; ++kk) {
-        s16x4 bx[4];
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) bx[nt] = tr4(xt, TH_XLD, kk * 16, nt * 16, lane);
-#pragma unroll
-        for (int m = 0; m < 6; ++m) {
-          const bf16* src = (m >> 1) == 0 ? sq : ((m >> 1) == 1 ? sk : sv);
-          const s16x4 a = tr4(src, HLD, kk * 16, (m & 1) * 16, lane);
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt)
-            dwacc[m][nt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, bx[nt], dwacc[m][nt], 0, 0, 0);
-        }
-      }
-      TW_ST(4)
-      // dxn by output tiles (round 5, TWH_DXT): after a block barrier every head's dq / dk / dv are in LDS, and wave w
-      // computes whole output tiles g[v][c] = sum over all 768 qkv rows of W'^T[c][k] dqkv[v][k] -- channel tile
-      // w & 3, voxel tiles (w >> 2) + 2u (a SIMD's two waves w, w + 4 share its 3 tiles at NV = 3) -- so no per-head
-      // fp32 partials are written and summed (98 KB of LDS stores per group before), the 48 accumulator registers of
-      // the per-head partial GEMM become 8, and LN backward reads one row instead of eight.  g goes to 256-B rows in
-      // the dO slices of waves 0-3 (not read in this phase), 16-B unit u of row slot s at u ^ (s & 7).
-      const int ct = wid & 3;
-      bf16x8 ring[TWH_DXT_RING];
-      auto ldt = [&](int j) { return ld_img(wqt_g, ct, QKV / 32, j, lane); };  // j = kind * 8 + head
-#pragma unroll
-      for (int r = 0; r < TWH_DXT_RING - 1; ++r) ring[r] = ldt(r);
-      __syncthreads();  // (B') every head's dq / dk / dv in its slices
-      // the wave's voxel tiles vt0, vt0 + 2 (< NV): one straight-line GEMM per tile count (wave-uniform branch)
-      const int vt0 = wid >> 2;
-      auto tiles = [&](auto NTc) {
-        constexpr int NTL = decltype(NTc)::value;
-        f32x4 dacc[NTL];
-#pragma unroll
-        for (int u = 0; u < NTL; ++u) dacc[u] = z4;
-#pragma unroll
-        for (int j = 0; j < 24; ++j) {
-          if (j + TWH_DXT_RING - 1 < 24) ring[(j + TWH_DXT_RING - 1) % TWH_DXT_RING] = ldt(j + TWH_DXT_RING - 1);
-          const bf16x8 a = ring[j % TWH_DXT_RING];
-          const bf16* src = slices + (j & 7) * TWH_WSTRIDE(R) + (j >> 3) * R * HLD;
-#pragma unroll
-          for (int u = 0; u < NTL; ++u)
-            dacc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ld16(src + ((vt0 + 2 * u) * 16 + lr) * HLD + lg * 8),
-                                                              dacc[u], 0, 0, 0);
-        }
-#pragma unroll
-        for (int u = 0; u < NTL; ++u) {
-          const int v = (vt0 + 2 * u) * 16 + lr, sl = v % TWH_GRPR(R);
-          float* row = twh_grow(slices, R, v);
-          *reinterpret_cast<f32x4*>(row + ((ct * 4 + lg) ^ (sl & 7)) * 4) = dacc[u];
-        }
-      };
-#if TWH_DXT_ONELOOP
-      // one loop, a wave-uniform skip per second-tile MFMA (fewer registers than two inlined copies)
-      {
-        f32x4 dacc[2] = {z4, z4};
-#pragma unroll
-        for (int j = 0; j < 24; ++j) {
-          if (j + TWH_DXT_RING - 1 < 24) ring[(j + TWH_DXT_RING - 1) % TWH_DXT_RING] = ldt(j + TWH_DXT_RING - 1);
-          const bf16x8 a = ring[j % TWH_DXT_RING];
-          const bf16* src = slices + (j & 7) * TWH_WSTRIDE(R) + (j >> 3) * R * HLD;
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            const int vt = vt0 + 2 * u;
-            if (vt < NV)  // wave-uniform
-              dacc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ld16(src + (vt * 16 + lr) * HLD + lg * 8), dacc[u], 0,
-                                                                0, 0);
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int vt = vt0 + 2 * u;
-          if (vt < NV) {
-            const int v = vt * 16 + lr, sl = v % TWH_GRPR(R);
-            float* row = twh_grow(slices, R, v);
-            *reinterpret_cast<f32x4*>(row + ((ct * 4 + lg) ^ (sl & 7)) * 4) = dacc[u];
-          }
-        }
-      }
-#else
-      const int ntl = vt0 < NV ? (vt0 + 2 < NV ? 2 : 1) : 0;  // wave-uniform
-      if (ntl == 2) {
-        tiles(std::integral_constant<int, 2>{});
-      } else if (ntl == 1) {
-        tiles(std::integral_constant<int, 1>{});
-      }
-#endif
-      TW_ST(5)
-      __syncthreads();  // (B'') every g row written
-
-      // ---- LN backward of this thread's voxel chunk: dx = rstd (g - mean(g) - xhat mean(g xhat)) + dy
-      {
-        const int v = vv < R ? vv : 0, sl = v % TWH_GRPR(R);
-        const float* row = twh_grow(slices, R, v);
-        const f32x4 a0 = *reinterpret_cast<const f32x4*>(row + ((2 * cc) ^ (sl & 7)) * 4);
-        const f32x4 a1 = *reinterpret_cast<const f32x4*>(row + ((2 * cc + 1) ^ (sl & 7)) * 4);
-        const float g[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-        const bf16x8 xh = *reinterpret_cast<const bf16x8*>(xt + v * TH_XLD + cc * 8);
-        const bf16x8 dv = *reinterpret_cast<const bf16x8*>(dyt + v * TH_XLD + cc * 8);
-        float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) { s1 += g[e]; s2 = fmaf(g[e], (float)xh[e], s2); }
-#pragma unroll
-        for (int o = 1; o < 8; o <<= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
-        s1 *= 1.f / C;
-        s2 *= 1.f / C;
-        if (vv < R && ok_cur) {
-          bf16x8 o8;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) o8[e] = (bf16)(rstd_cur * (g[e] - s1 - (float)xh[e] * s2) + (float)dv[e]);
-          stnt16(dx + vrow(gg, vv) * C + cc * 8, o8);
-        }
-      }
-    } else {
+    {
       // the dxn GEMM's W'^T fragments (kind, ct) in a TWH_RING-deep ring: the first in flight during the dW GEMM
-      constexpr bool WP = DWO ? TWH_WPIPE_DWO : TWH_WPIPE;
-      bf16x8 wring[WP ? TWH_RING : 1];
+      bf16x8 wring[TWH_RING];
       auto ldw = [&](int idx) { return ld_img(wqt_g, idx % T::CT, QKV / 32, (idx / T::CT) * 8 + h, lane); };
-      if constexpr (WP) {
   #pragma unroll
-        for (int r = 0; r < TWH_RING - 1; ++r) wring[r] = ldw(r);
-      }
+      for (int r = 0; r < TWH_RING - 1; ++r) wring[r] = ldw(r);
       // dW'_h += dqkv_h^T . xhat over the group's voxels (K = voxels, 16 per step; padded rows are zero)
   #pragma unroll
       for (int kk = 0; kk < NV; ++kk) {
@@ -2456,7 +2059,6 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
             dwacc[m][nt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, bx[nt], dwacc[m][nt], 0, 0, 0);
         }
       }
-      TW_ST(4)
       // dxn'_h^T = W'_qkv[h rows]^T . dqkv_h^T (this head's share; gamma folded: the sum over heads is
       // g = gamma * dxn), kept in registers, then written as fp32 rows over the wave's own slices
       f32x4 dxacc[T::CT][NV];
@@ -2469,14 +2071,9 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
         const bf16* src = kind == 0 ? sq : (kind == 1 ? sk : sv);
   #pragma unroll
         for (int ct = 0; ct < T::CT; ++ct) {
-          bf16x8 a;
-          if constexpr (WP) {
-            const int idx = kind * T::CT + ct;
-            if (idx + TWH_RING - 1 < 3 * T::CT) wring[(idx + TWH_RING - 1) % TWH_RING] = ldw(idx + TWH_RING - 1);
-            a = wring[idx % TWH_RING];
-          } else {
-            a = ld_img(wqt_g, ct, QKV / 32, kind * 8 + h, lane);
-          }
+          const int idx = kind * T::CT + ct;
+          if (idx + TWH_RING - 1 < 3 * T::CT) wring[(idx + TWH_RING - 1) % TWH_RING] = ldw(idx + TWH_RING - 1);
+          const bf16x8 a = wring[idx % TWH_RING];
   #pragma unroll
           for (int vt = 0; vt < NV; ++vt)
             dxacc[ct][vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ld16(src + (vt * 16 + lr) * HLD + lg * 8),
@@ -2492,7 +2089,6 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
           for (int vt = 0; vt < NV; ++vt)
             *reinterpret_cast<f32x4*>(part + (vt * 16 + lr) * TWH_PLD + ct * 16 + lg * 4) = dxacc[ct][vt];
       }
-      TW_ST(5)
       __syncthreads();  // (B) every head's partial written
 
       // ---- LN backward of this thread's voxel chunk: dx = rstd (g - mean(g) - xhat mean(g xhat)) + dy
@@ -2518,22 +2114,13 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
         for (int o = 1; o < 8; o <<= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
         s1 *= 1.f / C;
         s2 *= 1.f / C;
-        if (TWH_DX_LATE) {
   #pragma unroll
-          for (int e = 0; e < 8; ++e) dx_pend[e] = (bf16)(rstd_cur * (g[e] - s1 - (float)xh[e] * s2) + (float)dv[e]);
-          dx_row = vv < R && ok_cur ? vrow(gg, vv) : -1;
-        } else if (vv < R && ok_cur) {
-          bf16x8 o8;
-  #pragma unroll
-          for (int e = 0; e < 8; ++e) o8[e] = (bf16)(rstd_cur * (g[e] - s1 - (float)xh[e] * s2) + (float)dv[e]);
-          stnt16(dx + vrow(gg, vv) * C + cc * 8, o8);
-        }
+        for (int e = 0; e < 8; ++e) dx_pend[e] = (bf16)(rstd_cur * (g[e] - s1 - (float)xh[e] * s2) + (float)dv[e]);
+        dx_row = vv < R && ok_cur ? vrow(gg, vv) : -1;
       }
     }
-    TW_ST(6)
   }
-  if (TWH_DX_LATE && dx_row >= 0) stnt16(dx + dx_row * C + cc * 8, dx_pend);
-  TW_ST_FLUSH(blockIdx.x * 8 + wid)
+  if (dx_row >= 0) stnt16(dx + dx_row * C + cc * 8, dx_pend);
   // ---- per-block outputs: dW'_h rows of the slab, dbias partials (cesm_relpos_bwd layout, B = 1)
   float* slab = dw_slab + (int64_t)blockIdx.x * QKV * C;
 #pragma unroll
@@ -2549,26 +2136,8 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
     const int j = lg * 4 + r;
     if (lr < F && j < F) dbias_part[((int64_t)h * gridDim.x + blockIdx.x) * FF + lr * F + j] = dbacc[r];
   }
-  if constexpr (DWO) {  // dW_out partial of this block: [C][256] after the gridDim.x dW' slabs
-    float* so = dw_slab + (int64_t)gridDim.x * QKV * C + (int64_t)blockIdx.x * C * INNER;
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct)
-#pragma unroll
-      for (int half = 0; half < 2; ++half)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) so[(int64_t)(ct * 16 + lg * 4 + r) * INNER + h * DH + half * 16 + lr] = dwo[ct][half][r];
-  }
 }
 
-// dst (+)= sum over the nblk slabs (fixed order) of [nblk][n] partials
-__global__ void slab_sum_kernel(const float* __restrict__ slab, int nblk, int64_t n, float* __restrict__ dst,
-                                int accumulate) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (e >= n) return;
-  float s = 0.f;
-  for (int k = 0; k < nblk; ++k) s += slab[(int64_t)k * n + e];
-  dst[e] = accumulate ? dst[e] + s : s;
-}
 
 
 extern "C" {
@@ -2705,7 +2274,7 @@ int cesm_tblock_fwd_fold(const void* x, const float* gamma, const float* wqkv_f3
 // B = 1).  Workspaces: slab nblk*768*C floats, tmp 768*C floats, wimg (2*768 + 256)*C bf16.
 int cesm_tblock_bwd_dw(const void* x, const void* dy, const float* mr, const float* lse, const float* wqkv_f32,
                        const float* gamma, const void* wout_t, const float* bias, const float* rot, void* dx,
-                       float* dwqkv, float* dgamma, float* dwout, float* dbias_part, float* slab, float* tmp, void* wimg,
+                       float* dwqkv, float* dgamma, float* dbias_part, float* slab, float* tmp, void* wimg,
                        int nblk, int B, int F, int HW, int C, float scale, int accumulate, hipStream_t stream) {
   if (nblk < 1 || nblk != cesm_tblock_bwd_dw_nblk(B, F, HW, C)) return CESM_EUNSUPPORTED;
   bf16* iq = (bf16*)wimg;
@@ -2717,24 +2286,18 @@ int cesm_tblock_bwd_dw(const void* x, const void* dy, const float* mr, const flo
   frag_image_f32_kernel<<<gi, 256, 0, stream>>>(wqkv_f32, gamma, iqt, C, 768, 1, INNER, scale);
   frag_image(wout_t, iot, INNER, C, stream);
   const int nv = (4 * F + 15) / 16;
-  const size_t sm = twh_smem(F, nv, dwout != nullptr);
-#define TWH_LAUNCH(NVv, DWOv)                                                                                     \
-  allow_smem(twh_bwd_kernel<NVv, DWOv>, sm);                                                                      \
-  twh_bwd_kernel<NVv, DWOv><<<nblk, 512, sm, stream>>>((const bf16*)x, (const bf16*)dy, mr, lse, iq, iqt, iot, bias, \
-                                                       rot, (bf16*)dx, slab, dbias_part, B, F, HW, scale)
-  const bool dwo = dwout != nullptr;
+  const size_t sm = twh_smem(F, nv);
+#define TWH_LAUNCH(NVv)                                                                                           \
+  allow_smem(twh_bwd_kernel<NVv>, sm);                                                                            \
+  twh_bwd_kernel<NVv><<<nblk, 512, sm, stream>>>((const bf16*)x, (const bf16*)dy, mr, lse, iq, iqt, iot, bias, rot, \
+                                                 (bf16*)dx, slab, dbias_part, B, F, HW, scale)
   switch (nv) {
-    case 1: if (dwo) { TWH_LAUNCH(1, true); } else { TWH_LAUNCH(1, false); } break;
-    case 2: if (dwo) { TWH_LAUNCH(2, true); } else { TWH_LAUNCH(2, false); } break;
-    case 3: if (dwo) { TWH_LAUNCH(3, true); } else { TWH_LAUNCH(3, false); } break;
+    case 1: TWH_LAUNCH(1); break;
+    case 2: TWH_LAUNCH(2); break;
+    case 3: TWH_LAUNCH(3); break;
     default: return CESM_EUNSUPPORTED;
   }
 #undef TWH_LAUNCH
-  if (dwo) {
-    const int64_t no = (int64_t)C * INNER;
-    slab_sum_kernel<<<(unsigned)cdiv(no, 256), 256, 0, stream>>>(slab + (int64_t)nblk * 768 * C, nblk, no, dwout,
-                                                                 accumulate);
-  }
   const int64_t nel = (int64_t)768 * C;
   twh_dw_reduce_kernel<<<(unsigned)cdiv(nel, 256), 256, 0, stream>>>(slab, nblk, wqkv_f32, gamma, dwqkv, tmp, 768, C,
                                                                     accumulate, INNER, scale);

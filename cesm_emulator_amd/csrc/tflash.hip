@@ -86,7 +86,7 @@ __device__ __forceinline__ bf16x8 rope8(const bf16x8 v, const float* cs, float s
   return o;
 }
 
-// Buffer-resource addressing of a 16-frame tile (TF_BUF): the tile's base is wave-uniform (SGPRs), a lane's
+// Buffer-resource addressing of a 16-frame tile: the tile's base is wave-uniform (SGPRs), a lane's
 // frame row is a 32-bit byte offset lr * HW * rowbytes (< 2^31: checked on the host), and the resource ends
 // after the tile's last valid frame, so loads of frames >= F return zeros and stores to them are dropped --
 // no 64-bit lane address math and no predicate branch per tile (the 64-bit math was ~60 of the forward's
@@ -204,188 +204,31 @@ __device__ __forceinline__ const float* btab_lane(const float* tab, int lr, int 
 // 8 XCDs round-robin (linear id mod 8), so the 8 blocks an XCD receives back to back (ids L, L + 8, ...) are
 // the 8 heads of one pixel group: every line is fetched once into that XCD's L2 and used whole.  (One head per
 // grid row instead fetched each line twice from HBM: the head-pair partner ran 1/8 of the grid later.)
-#ifndef TF_FWD_WPE
-#define TF_FWD_WPE 2  // forward waves per SIMD the register allocation targets (>= 2: VGPR-form MFMAs)
-#endif
-#ifndef TF_KV_PF
-#define TF_KV_PF 1  // A/B knob: dk / dv key-tile rows prefetched a tile ahead
-#endif
-#ifndef TF_VH
-#define TF_VH 2  // forward V staging: key-tile pairs per part (4 = all at F = 128)
-#endif
-#ifndef TF_PK
-#define TF_PK 1  // A/B knob: packed 2-wide fp32 VALU ops in the dk / dv kernel's softmax-gradient elementwise step
-#endif
-#ifndef TF_BUF
-#define TF_BUF 1  // A/B knob: buffer-resource tile addressing in the per-query-tile loop (0 = 64-bit lane math)
-#endif
-#ifndef TF_FWD2
-#define TF_FWD2 1  // A/B knob: forward with every load up front and RoPE by angle addition (0 = round 2-4 form)
-#endif
-#ifndef TF_XCD_MAP
-#define TF_XCD_MAP 1  // A/B knob: 0 = head-major grid (round 2)
-#endif
+// (Round 3, head-major grid instead: forward +18 %.)
 __device__ __forceinline__ void tf_block(int& grp, int& h) {
   const int L = blockIdx.x, j = L >> 3;
-  h = TF_XCD_MAP ? j & 7 : L / (gridDim.x / 8);
-  grp = TF_XCD_MAP ? (j >> 3) * 8 + (L & 7) : L % (gridDim.x / 8);
+  h = j & 7;
+  grp = (j >> 3) * 8 + (L & 7);
 }
+constexpr int TF_VH = 2;  // forward V staging: key-tile pairs per part (4 = all at F = 128)
 static unsigned tf_grid_x(int HW) { return (unsigned)(64 * cdiv(cdiv(HW, 4), 8)); }
 
 // padded query rows: their lse makes every P entry exactly 0 (exp2(x - 1e30) = 0 for any finite x)
 constexpr float TF_LSE_PAD = 1e30f;
 
 // ------------------------------------------------------------------------------------------------ forward
-// grid (tf_grid_x(HW), B), 256 threads: wave = one pixel of one (sample, head) (tf_block)
-template <int NT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE))) void tflash_fwd_kernel(const bf16* __restrict__ qkv, const float* __restrict__ bias,
-                                                         const float* __restrict__ rot, bf16* __restrict__ out,
-                                                         float* __restrict__ lse, int F, int HW, float scale, int pm) {
-  constexpr int NP = (NT + 1) / 2, NR = 32 * NP;  // key-tile pairs, staged rows
-  // V rows are staged TF_VH key-tile pairs at a time: the V^T fragments live in registers afterwards, so the
-  // wave's staging slice only has to hold part of them -- less LDS per block, one more block per CU
-  constexpr int VH = NP < TF_VH ? NP : TF_VH, NVR = 32 * VH;
-  __shared__ __attribute__((aligned(16))) float btab[4 * 32 * NT];
-  __shared__ __attribute__((aligned(16))) bf16 vst[4][NVR * TF_LD];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, lr = lane & 15, g = lane >> 4;
-  int grp, h;
-  tf_block(grp, h);
-  const int b = blockIdx.y;
-  if (grp * 4 >= HW) return;  // whole block (padded groups)
-  load_btab<NT>(bias, btab, h, F, 1, tid, 256);
-  __syncthreads();
-  const int p = grp * 4 + __builtin_amdgcn_readfirstlane(wid);  // wave-uniform (buffer bases in SGPRs)
-  if (p >= HW) return;
-  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
-  const int64_t row0 = (int64_t)b * F * HW + p;  // voxel of frame f: row0 + f * HW
-  // qkv rows: frame-major [B][F][HW] (pm = 0) or pixel-major [B][HW][F] (pm = 1: a pixel's frames contiguous)
-  const int64_t qrow0 = pm ? ((int64_t)b * HW + p) * F : row0;
-  const int qfs = pm ? 1 : HW;
-  bf16* vs = vst[wid];
-  // TF_BUF lane offsets: frame lr of a 16-frame tile
-  const int q_off = (lr * qfs * QKV + g * 8) * 2, o_off = (lr * HW * INNER + 4 * g) * 2;
-  const __amdgpu_buffer_rsrc_t rot_rs = tile_rsrc(rot, F, 16 * 2 * 4, 16 * 2 * 4, TF_MAXT * 16);
-  const int rot_off = (lr * 16 + 4 * g) * 2 * 4;
-  // every K' fragment up front (all Q' fragments up front as well measured 1.7x slower at F = 120; the next query
-  // tile's rows prefetched a tile ahead, neutral: 192x288 4616 -> 4547 us, 48x72 -2 %, 24x36 +0..8 %)
-  bf16x8 kf[NT];
-#pragma unroll
-  for (int kt = 0; kt < NT; ++kt) {
-    const int f = kt * 16 + lr;
-    const bool ok = f < F;
-    const int64_t rr = (qrow0 + (int64_t)(ok ? f : 0) * qfs) * QKV + h * DH + g * 8;
-    kf[kt] = row_frag(qkv + rr + INNER, rot, ok ? f : 0, g, 1.f, true);
-  }
-  bf16x8 vf[NP][2];
-#pragma unroll
-  for (int s0 = 0; s0 < NP; s0 += VH) {
-    if (s0) wsync();  // previous part's transposed reads done
-    for (int e = lane; e < NVR * 4; e += 64) {  // V rows 32 s0 .. (zero past F)
-      const int fl = e >> 2, c = e & 3, f = 32 * s0 + fl;
-      const bf16x8 v = ld16(qkv + (qrow0 + (int64_t)(f < F ? f : 0) * qfs) * QKV + 2 * INNER + h * DH + c * 8);
-      *reinterpret_cast<bf16x8*>(vs + fl * TF_LD + c * 8) = f < F ? v : zero8();
-    }
-    wsync();
-#pragma unroll
-    for (int s = s0; s < s0 + VH && s < NP; ++s)
-#pragma unroll
-      for (int t = 0; t < 2; ++t) vf[s][t] = tr_pair(vs, s - s0, t * 16, lane);
-  }
+// grid (tf_grid_x(HW), B), 256 threads: wave = one pixel of one (sample, head) (tf_block); waves_per_eu(2): a
+// 256-register budget, VGPR-form MFMAs.
 
-  // Padded rows are never zeroed in registers: their loads are clamped to frame 0 (finite data).  Keys past F
-  // exist only in the last key tile and get an additive -inf there; padded query columns compute a finite
-  // softmax that is not stored.
-  const float* bl = btab_lane<NT>(btab, lr, g);
-  float kmask[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) kmask[r] = 16 * (NT - 1) + 4 * g + r < F ? 0.f : -INFINITY;
-
-  for (int qt = 0; qt < NT; ++qt) {
-    const int fq = qt * 16 + lr;
-    const bool okq = fq < F;
-    const int nq = F - qt * 16;  // valid frames of this query tile (wave-uniform)
-    bf16x8 qf;
-    if (TF_BUF) {
-      const __amdgpu_buffer_rsrc_t qrs =
-          tile_rsrc(qkv + (qrow0 + (int64_t)qt * 16 * qfs) * QKV + h * DH, nq, (int64_t)qfs * QKV * 2, DH * 2);
-      float cs[8];
-      buf_rot8(rot_rs, rot_off + qt * 16 * 16 * 2 * 4, cs);
-      qf = rope8(buf_ld16(qrs, q_off), cs, scale);  // frames >= F: zeros
-    } else {
-      qf = row_frag(qkv + (qrow0 + (int64_t)(okq ? fq : 0) * qfs) * QKV + h * DH + g * 8, rot, okq ? fq : 0, g, scale,
-                    true);
-    }
-    const float* bq = bl - 16 * qt;
-    float sc[2 * NP][4];
-    float m = -INFINITY;
-#pragma unroll
-    for (int kt = 0; kt < 2 * NP; ++kt) {
-      if (kt < NT) {
-        const f32x4 st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt < NT ? kt : 0], qf, z4, 0, 0, 0);
-        const f32x4 bo = *reinterpret_cast<const f32x4*>(bq + 16 * kt);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          sc[kt][r] = fmaf(st[r], LOG2E, bo[r]);
-          if (kt == NT - 1) sc[kt][r] += kmask[r];
-          m = fmaxf(m, sc[kt][r]);
-        }
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) sc[kt][r] = -INFINITY;
-      }
-    }
-    const float mm = grp4_max(m);  // finite: key 0 is valid for every query row
-    float l = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < 2 * NP; ++kt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        sc[kt][r] = __builtin_amdgcn_exp2f(sc[kt][r] - mm);  // exp2(-inf) = 0
-        l += sc[kt][r];
-      }
-    l = grp4_sum(l);
-    f32x4 ot[2] = {z4, z4};
-#pragma unroll
-    for (int s = 0; s < NP; ++s) {
-      const bf16x8 pb = pack_kslot(sc[2 * s], sc[2 * s + 1]);
-#pragma unroll
-      for (int t = 0; t < 2; ++t) ot[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[s][t], pb, ot[t], 0, 0, 0);
-    }
-    if (TF_BUF) {  // stores of frames >= F fall outside the resources and are dropped
-      const float inv = __builtin_amdgcn_rcpf(l);
-      const __amdgpu_buffer_rsrc_t ors =
-          tile_rsrc(out + (row0 + (int64_t)qt * 16 * HW) * INNER + h * DH, nq, (int64_t)HW * INNER * 2, DH * 2);
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        float o4[4] = {ot[t][0] * inv, ot[t][1] * inv, ot[t][2] * inv, ot[t][3] * inv};
-        buf_st4b(ors, o_off + t * 32, o4);
-      }
-      if (lse) {
-        const __amdgpu_buffer_rsrc_t lrs =
-            tile_rsrc(lse + (((int64_t)b * NH + h) * HW + p) * F + qt * 16, nq, 4, 4);
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, mm + log2f(l)), lrs,
-                                              g == 0 ? lr * 4 : 0x7ffffff0, 0, 0);
-      }
-    } else if (okq) {
-      const float inv = __builtin_amdgcn_rcpf(l);
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        float o4[4] = {ot[t][0] * inv, ot[t][1] * inv, ot[t][2] * inv, ot[t][3] * inv};
-        store4b(out + (row0 + (int64_t)fq * HW) * INNER + h * DH + t * 16 + 4 * g, o4);
-      }
-      if (lse && g == 0) lse[(((int64_t)b * NH + h) * HW + p) * F + fq] = mm + log2f(l);
-    }
-  }
-}
-
-// Round 5 form of the forward (TF_FWD2, default): every global load of the wave is issued up front -- the raw K and Q
+// Round 5 form of the forward: every global load of the wave is issued up front -- the raw K and Q
 // rows of all tiles through tile resources (frames >= F read as zeros) and the V rows of the first staging part --
 // and the RoPE coefficients come by angle addition (frame 16 a + lr = the block's row of frame 16 a composed with the
 // row of frame lr, two small LDS tables; the fused backward uses the same coefficients).  No load is issued after the
-// wave's first O store: vmcnt counts loads and stores in order, and in the first form (tflash_fwd_kernel) every query
-// tile's q and RoPE loads waited behind the previous tile's stores, and the K' prologue waited once per key tile.
+// wave's first O store: vmcnt counts loads and stores in order, and in the round 2-4 form (removed in round 6) every
+// query tile's q and RoPE loads waited behind the previous tile's stores, and the K' prologue waited once per key tile
+// (192 x 288, F = 120: 4.63 -> 4.12 ms).
 template <int NT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE))) void tflash_fwd2_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tflash_fwd2_kernel(
     const bf16* __restrict__ qkv, const float* __restrict__ bias, const float* __restrict__ rot, bf16* __restrict__ out,
     float* __restrict__ lse, int F, int HW, float scale, int pm) {
   constexpr int NP = (NT + 1) / 2;
@@ -533,26 +376,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_FWD_WPE)
 // the pixel's K' and V rows staged once in LDS for all waves.  Writes dq into dqkv, D_i = dO_i . O_i into dbuf
 // [B][8][HW][F], and per-block dbias-by-offset partials part[(b*8 + h)][blk][2F - 1].  With the query tile
 // fixed per wave, the dbias accumulator of (r, kt) holds one diagonal kt - qt for every pixel: static registers.
-// TF_DO (round 3): D_i = dO_i . O_i from the forward's (bf16) output instead of sum_j P_ij dP_ij, so one pass over
-// the key tiles does S, dP -> P, dS -> dbias, dQ with no P / dP arrays in registers (64 VGPRs at NT = 8): the
-// kernel fits 128 VGPRs, i.e. 2 blocks of 8 waves per CU instead of 1 (the pass-1 / pass-2 form was latency
-// bound at 2 waves per SIMD in barrier lockstep).  Only for F > 16 (NT >= 2): with D from O the F = 1 rel-pos
-// bias gradient would be the rounding difference of two 32-term dot products instead of exactly 0.  Measured at
-// F = 120 (tools/tf_ab.sh): 192x288 13.5 -> 14.3 ms (slower: the lost register prefetch), 96x144 +1 %, 48x72 -5 %,
-// 24x36 -17 % -> used below TF_DO_MAXHW pixels.
-#ifndef TF_DO
-#define TF_DO 1
-#endif
-#ifndef TF_DO_MAXHW
-#define TF_DO_MAXHW 8192
-#endif
-template <int NT, bool DOV>
-__global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(DOV ? 4 : 2))) void tflash_bwd_q_kernel(
+// Round 6: only the F < 8 windows take this two-kernel backward (the one-pass fused kernel takes every longer one);
+// D_i = sum_j P_ij dP_ij keeps the F = 1 rel-pos bias gradient exactly 0.  (The single-pass variant with D = dO . O
+// from the forward's output, round 3's TF_DO for small F > 16 levels, went with the fused kernel.)
+template <int NT>
+__global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(2))) void tflash_bwd_q_kernel(
     const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
     const float* __restrict__ lse, const float* __restrict__ bias, const float* __restrict__ rot,
     bf16* __restrict__ dqkv, float* __restrict__ dbuf, float* __restrict__ part, int F, int HW, float scale, int pm) {
   constexpr int NP = (NT + 1) / 2, NR = 32 * NP, NTH = 64 * NT;
-  constexpr bool DO_ = DOV;
   __shared__ __attribute__((aligned(16))) float btab[4 * 32 * NT];
   __shared__ float dacc[2 * 16 * TF_MAXT];
   __shared__ __attribute__((aligned(16))) bf16 ks[NR * TF_LD];
@@ -585,19 +417,11 @@ __global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(DOV ? 4
   const int sf = tid >> 2, sc = tid & 3;
   const bool sok = sf < F;
   const int sfc = sok ? sf : 0, fqc = okq ? fq : 0;
-  // TF_DO (two blocks per CU, <= 128 VGPRs): no register prefetch (the co-resident block hides this one's loads,
-  // all issued before the staging barrier), and the RoPE coefficients are re-read per pixel (L1 / L2-resident
-  // table) instead of living in 16 registers
-  float kcs[DO_ ? 1 : 8], qcs[DO_ ? 1 : 8];
-  if (!DO_) {
-    rot8_load(rot, sfc, sc, kcs);
-    rot8_load(rot, fqc, g, qcs);
-  }
-  bf16x8 kraw = zero8(), vraw = zero8(), qraw = zero8(), draw = zero8(), oraw = zero8();
+  float kcs[8], qcs[8];
+  rot8_load(rot, sfc, sc, kcs);
+  rot8_load(rot, fqc, g, qcs);
+  bf16x8 kraw = zero8(), vraw = zero8(), qraw = zero8(), draw = zero8();
   float lraw = 0.f;
-  // (a register prefetch of the next pixel's rows in the single-pass kernel measured slower, round 3:
-  // profiles/r3_tf_dopf_ab.txt -- the second co-resident block hides the loads better)
-  constexpr bool PF = !DO_;
   // qkv / dqkv rows frame-major or pixel-major (pm); dout / o frame-major
   const int qfs = pm ? 1 : HW;
   auto qrow = [&](int pp) { return pm ? ((int64_t)b * HW + pp) * F : (int64_t)b * F * HW + pp; };
@@ -606,39 +430,19 @@ __global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(DOV ? 4
     const int64_t rs = (q0 + (int64_t)sfc * qfs) * QKV + h * DH + sc * 8;
     kraw = ld16(qkv + rs + INNER);
     vraw = ld16(qkv + rs + 2 * INNER);
-    if (PF) {
-      const int64_t vq = r0 + (int64_t)fqc * HW;
-      qraw = ld16(qkv + (q0 + (int64_t)fqc * qfs) * QKV + h * DH + g * 8);
-      draw = ld16(dout + vq * INNER + h * DH + g * 8);
-      if (DO_) oraw = ld16(o + vq * INNER + h * DH + g * 8);
-      lraw = lse[(((int64_t)b * NH + h) * HW + pp) * F + fqc];
-    }
+    const int64_t vq = r0 + (int64_t)fqc * HW;
+    qraw = ld16(qkv + (q0 + (int64_t)fqc * qfs) * QKV + h * DH + g * 8);
+    draw = ld16(dout + vq * INNER + h * DH + g * 8);
+    lraw = lse[(((int64_t)b * NH + h) * HW + pp) * F + fqc];
   };
-  if (PF && (int)blockIdx.x < HW) fetch(blockIdx.x);
+  if ((int)blockIdx.x < HW) fetch(blockIdx.x);
 
   for (int p = blockIdx.x; p < HW; p += gridDim.x) {
     const int64_t row0 = (int64_t)b * F * HW + p, qrow0 = qrow(p);
     __syncthreads();  // previous pixel's rows consumed
     bf16x8 qf, dof;
-    float Li, Do = 0.f;
-    if (DO_) {
-      if (!PF) fetch(p);  // K / V rows of this pixel (the co-resident block hides the latency)
-      float cs[8];
-      rot8_load(rot, sfc, sc, cs);
-      *reinterpret_cast<bf16x8*>(ks + sf * TF_LD + sc * 8) = sok ? rope8(kraw, cs, 1.f) : zero8();
-      *reinterpret_cast<bf16x8*>(vs + sf * TF_LD + sc * 8) = sok ? vraw : zero8();
-      const int64_t vq = row0 + (int64_t)fqc * HW;
-      const bf16x8 qr = PF ? qraw : ld16(qkv + (qrow0 + (int64_t)fqc * qfs) * QKV + h * DH + g * 8);
-      dof = PF ? draw : ld16(dout + vq * INNER + h * DH + g * 8);
-      const bf16x8 orw = PF ? oraw : ld16(o + vq * INNER + h * DH + g * 8);
-      const float lr_ = PF ? lraw : lse[(((int64_t)b * NH + h) * HW + p) * F + fqc];
-      if (PF && p + (int)gridDim.x < HW) fetch(p + gridDim.x);
-      rot8_load(rot, fqc, g, cs);
-      qf = rope8(qr, cs, scale);
-      Li = okq ? lr_ : TF_LSE_PAD;  // padded query rows: P = 0 (so dS = 0 there)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) Do = fmaf((float)dof[e], (float)orw[e], Do);
-    } else {
+    float Li;
+    {
       *reinterpret_cast<bf16x8*>(ks + sf * TF_LD + sc * 8) = sok ? rope8(kraw, kcs, 1.f) : zero8();
       *reinterpret_cast<bf16x8*>(vs + sf * TF_LD + sc * 8) = sok ? vraw : zero8();
       // padded query rows: finite clamped data, P = 0 through Li (so D = dS = 0 there)
@@ -646,54 +450,8 @@ __global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(DOV ? 4
       dof = draw;
       Li = okq ? lraw : TF_LSE_PAD;
     }
-    if (!DO_ && p + (int)gridDim.x < HW) fetch(p + gridDim.x);
+    if (p + (int)gridDim.x < HW) fetch(p + gridDim.x);
     __syncthreads();  // rows staged
-    if (DO_) {
-      const float D = grp4_sum(Do);
-      if (okq && g == 0) dbuf[(((int64_t)b * NH + h) * HW + p) * F + fq] = D;
-      // one pass: S'^T, dP^T -> P^T, dS^T = P^T (dP^T - D) -> dbias, dQ'^T = K'^T dS^T
-      f32x4 dqt[2] = {z4, z4};
-#pragma unroll
-      for (int s = 0; s < NP; ++s) {
-        float dsv[2][4];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int kt = 2 * s + u;
-          if (kt < NT) {
-            const bf16x8 kf = ld16(ks + (kt * 16 + lr) * TF_LD + g * 8);
-            const bf16x8 vf = ld16(vs + (kt * 16 + lr) * TF_LD + g * 8);
-            const f32x4 st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf, z4, 0, 0, 0);   // S'^T
-            const f32x4 dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, dof, z4, 0, 0, 0);  // dP^T
-            const f32x4 bo = *reinterpret_cast<const f32x4*>(bq + 16 * kt);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              float pp = __builtin_amdgcn_exp2f(fmaf(st[r], LOG2E, bo[r]) - Li);
-              if (kt == NT - 1) pp = kok[r] ? pp : 0.f;
-              const float ds = pp * (dp[r] - D);
-              dsv[u][r] = ds;
-              dba[r][kt < NT ? kt : 0] += ds;
-            }
-          } else {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) dsv[u][r] = 0.f;
-          }
-        }
-        const bf16x8 db = pack_kslot(dsv[0], dsv[1]);
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-          dqt[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_pair(ks, s, t * 16, lane), db, dqt[t], 0, 0, 0);
-      }
-      if (okq) {
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const int d0 = t * 16 + 4 * g;
-          float v4[4] = {dqt[t][0], dqt[t][1], dqt[t][2], dqt[t][3]};
-          rope4_inv(v4, rot, fq, d0, scale);  // dq = scale R^T dQ'
-          store4b(dqkv + (qrow0 + (int64_t)fq * qfs) * QKV + h * DH + d0, v4);
-        }
-      }
-      continue;
-    }
     // pass 1: P^T and dP^T of every key tile, D_i = sum_j P_ij dP_ij (exact: at F = 1 the bias gradient is 0)
     float pt[NT][4], dpt[NT][4];
     float D = 0.f;
@@ -772,194 +530,6 @@ __global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(DOV ? 4
     part[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * (2 * F - 1) + e] = dacc[e];
 }
 
-// ------------------------------------------------------------------------------------------- backward, dq (per wave)
-// Round 4 form of the dq pass for F > 16 (NT >= 2): one wave owns a (pixel, head) at a time -- all NT query
-// tiles -- and walks its pixels with no block barrier.  V fragments of every key tile live in registers for the
-// pixel, K' rows are staged in the wave's LDS rows (A fragments and k-slot transposes are read from there); both
-// the query-tile and the key-tile loops are unrolled, so the dbias accumulator of every (r, kt - qt) diagonal is
-// a static register (dba[4][2 NT - 1], 60 at NT = 8), summed over the wave's pixels.  D_i = dO_i . O_i (the
-// forward's bf16 output).  The block-per-pixel form (tflash_bwd_q_kernel: query tile = wave, two barriers per
-// pixel) ran in barrier lockstep on the staged rows.  Grid (nblk, B * 8) x 256 threads; the 4 waves' dbias rows
-// are reduced in a fixed order into the block's partial row, the same part[(b*8 + h)][blk][2F - 1] contract.
-// Every lane-derived quantity is recomputed per pixel from an opaque copy of the lane id: as loop invariants the
-// compiler hoisted them all (per-frame RoPE coefficients, bias-table reads, LDS and global addresses: > 200
-// VGPRs at NT = 8) out of the pixel loop and spilled.
-#ifndef TFQW_KREG
-#define TFQW_KREG 1  // K' A fragments of the pixel held in registers (0: re-read from the staged rows per query tile)
-#endif
-#ifndef TFQW_KTF
-#define TFQW_KTF 1  // K'^T k-slot fragments held in registers (0: transpose-read from LDS per query tile)
-#endif
-template <int NT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tflash_bwd_qw_kernel(
-    const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
-    const float* __restrict__ lse, const float* __restrict__ bias, const float* __restrict__ rot,
-    bf16* __restrict__ dqkv, float* __restrict__ dbuf, float* __restrict__ part, int F, int HW, float scale, int pm) {
-  constexpr int NP = (NT + 1) / 2, NR = 32 * NP, NC = 2 * NT - 1;
-  constexpr int CH = (NR * TF_LD * 2) / (4 * 64 * 4);  // diagonals staged per chunk in the wave's row buffer
-  static_assert(CH >= 1, "stage chunk");
-  __shared__ __attribute__((aligned(16))) float btab[4 * 32 * NT];
-  __shared__ __attribute__((aligned(16))) bf16 ksw[4][NR * TF_LD];
-  __shared__ float wsum[4][256];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: tile bases in SGPRs
-  const int b = blockIdx.y >> 3, h = blockIdx.y & 7;
-  load_btab<NT>(bias, btab, h, F, 1, tid, 256);
-  bf16* ks = ksw[wid];
-  for (int e = lane; e < (NR - 16 * NT) * 4; e += 64) {  // rows past the last key tile stay zero
-    const int f = 16 * NT + (e >> 2), c = e & 3;
-    *reinterpret_cast<bf16x8*>(ks + f * TF_LD + c * 8) = zero8();
-  }
-  __syncthreads();
-  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
-  float dba[4][NC];
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int c = 0; c < NC; ++c) dba[r][c] = 0.f;
-  // tile addressing as the forward's TF_BUF: wave-uniform tile base + one 32-bit lane offset for every tile, the
-  // resource ends at the tile's last valid frame (loads past F return 0, stores are dropped)
-  // qkv / dqkv rows frame-major or pixel-major (pm, as the forward); dout / o frame-major
-  const int fs_qkv = (pm ? 1 : HW) * QKV * 2, fs_io = HW * INNER * 2;  // < 2^31 / 16: checked on the host
-
-  for (int p = blockIdx.x * 4 + wid; p < HW; p += 4 * (int)gridDim.x) {
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    const int lr = ln & 15, g = ln >> 4;
-    const int lo_qkv = lr * fs_qkv + h * DH * 2 + g * 16, lo_io = lr * fs_io + h * DH * 2 + g * 16;
-    const int64_t row0 = (int64_t)b * F * HW + p;
-    const int64_t qrow0 = pm ? ((int64_t)b * HW + p) * F : row0;
-    const int qfs = pm ? 1 : HW;
-    const float* lsep = lse + (((int64_t)b * NH + h) * HW + p) * F;
-    float* dbp = dbuf + (((int64_t)b * NH + h) * HW + p) * F;
-    bf16x8 vf[NT], kf[TFQW_KREG ? NT : 1], ktf[TFQW_KTF ? NP : 1][2];
-#pragma unroll
-    for (int kt = 0; kt < NT; ++kt) {
-      const auto rs = tile_rsrc(qkv + (qrow0 + (int64_t)kt * 16 * qfs) * QKV, F - kt * 16, (int64_t)fs_qkv, QKV * 2);
-      const bf16x8 kr = buf_ld16(rs, lo_qkv + INNER * 2);
-      vf[kt] = buf_ld16(rs, lo_qkv + 2 * INNER * 2);
-      const int f = kt * 16 + lr;
-      float cs[8];
-      rot8_load(rot, f < F ? f : 0, g, cs);
-      if (kt == 0) wsync();  // previous pixel's reads of the rows done
-      const bf16x8 kv = rope8(kr, cs, 1.f);  // frames >= F: zeros
-      if (TFQW_KREG) kf[TFQW_KREG ? kt : 0] = kv;
-      *reinterpret_cast<bf16x8*>(ks + f * TF_LD + g * 8) = kv;
-    }
-    wsync();
-    if (TFQW_KTF)
-#pragma unroll
-      for (int s = 0; s < NP; ++s)
-#pragma unroll
-        for (int t = 0; t < 2; ++t) ktf[TFQW_KTF ? s : 0][t] = tr_pair(ks, s, t * 16, ln);
-    const float* bl = btab_lane<NT>(btab, lr, g);
-
-#pragma unroll
-    for (int qt = 0; qt < NT; ++qt) {
-      const int fq = qt * 16 + lr;
-      const bool okq = fq < F;
-      const int fqc = okq ? fq : 0;
-      const auto rq = tile_rsrc(qkv + (qrow0 + (int64_t)qt * 16 * qfs) * QKV, F - qt * 16, (int64_t)fs_qkv, QKV * 2);
-      const auto rd = tile_rsrc(dout + (row0 + (int64_t)qt * 16 * HW) * INNER, F - qt * 16, (int64_t)fs_io, INNER * 2);
-      const auto ro = tile_rsrc(o + (row0 + (int64_t)qt * 16 * HW) * INNER, F - qt * 16, (int64_t)fs_io, INNER * 2);
-      const bf16x8 qr = buf_ld16(rq, lo_qkv);
-      const bf16x8 dof = buf_ld16(rd, lo_io);
-      const bf16x8 orw = buf_ld16(ro, lo_io);
-      const float lq = lsep[fqc];
-      float cs[8];
-      rot8_load(rot, fqc, g, cs);
-      const bf16x8 qf = rope8(qr, cs, scale);
-      const float Li = okq ? lq : TF_LSE_PAD;  // padded query rows: P = 0 (so dS = 0 there)
-      float Do = 0.f;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) Do = fmaf((float)dof[e], (float)orw[e], Do);
-      const float D = grp4_sum(Do);
-      if (okq && g == 0) dbp[fq] = D;
-      const float* bq = bl - 16 * qt;
-      f32x4 dqt[2] = {z4, z4};
-#pragma unroll
-      for (int s = 0; s < NP; ++s) {
-        float dsv[2][4];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int kt = 2 * s + u;
-          if (kt < NT) {
-            const bf16x8 ka = TFQW_KREG ? kf[TFQW_KREG ? kt : 0] : ld16(ks + (kt * 16 + lr) * TF_LD + g * 8);
-            const f32x4 st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf, z4, 0, 0, 0);        // S'^T
-            const f32x4 dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[kt], dof, z4, 0, 0, 0);  // dP^T
-            const f32x4 bo = *reinterpret_cast<const f32x4*>(bq + 16 * kt);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              float pp = __builtin_amdgcn_exp2f(fmaf(st[r], LOG2E, bo[r]) - Li);
-              if (kt == NT - 1) pp = 16 * (NT - 1) + 4 * g + r < F ? pp : 0.f;  // keys of the last tile below F
-              const float ds = pp * (dp[r] - D);
-              dsv[u][r] = ds;
-              dba[r][kt - qt + NT - 1] += ds;
-            }
-          } else {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) dsv[u][r] = 0.f;
-          }
-        }
-        const bf16x8 db = pack_kslot(dsv[0], dsv[1]);
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-          dqt[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(TFQW_KTF ? ktf[TFQW_KTF ? s : 0][t] : tr_pair(ks, s, t * 16, ln),
-                                                           db, dqt[t], 0, 0, 0);
-      }
-      // the query tile's dbias contributions are summed now: held back, the compiler kept ~5 VGPRs per (qt, kt)
-      // tile pair live to the end of the pixel and spilled
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c < NC; ++c) asm volatile("" : "+v"(dba[r][c]));
-      const auto rw = tile_rsrc(dqkv + (qrow0 + (int64_t)qt * 16 * qfs) * QKV, F - qt * 16, (int64_t)fs_qkv, QKV * 2);
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int d0 = t * 16 + 4 * g;
-        float v4[4] = {dqt[t][0], dqt[t][1], dqt[t][2], dqt[t][3]};
-        rope4_inv(v4, rot, fqc, d0, scale);  // dq = scale R^T dQ' (rows >= F dropped by the resource)
-        buf_st4b(rw, lr * fs_qkv + (h * DH + d0) * 2, v4);
-      }
-    }
-  }
-  // dbias by offset n = 16 (kt - qt) + 4g + r - lr, diagonal c = kt - qt + NT - 1: the wave's accumulators are
-  // staged CH diagonals at a time in its row buffer, each lane sums the offsets e = lane + 64 j in a fixed
-  // (c, g, r) order, then the block sums its 4 waves in order
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  float* stg = reinterpret_cast<float*>(ks);
-#pragma unroll
-  for (int c0 = 0; c0 < NC; c0 += CH) {
-    wsync();
-#pragma unroll
-    for (int c = c0; c < c0 + CH && c < NC; ++c)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) stg[((c - c0) * 4 + r) * 64 + lane] = dba[r][c];
-    wsync();
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = lane + 64 * j - (F - 1);
-      float a = acc[j];
-#pragma nounroll
-      for (int c = c0; c < c0 + CH && c < NC; ++c)
-#pragma nounroll
-        for (int gg = 0; gg < 4; ++gg)
-#pragma nounroll
-          for (int r = 0; r < 4; ++r) {
-            const int l = 16 * (c - (NT - 1)) + 4 * gg + r - n;
-            if (n < F && l >= 0 && l < 16) a += stg[((c - c0) * 4 + r) * 64 + gg * 16 + l];
-          }
-      acc[j] = a;
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) wsum[wid][lane + 64 * j] = acc[j];
-  __syncthreads();
-  if (tid < 2 * F - 1)
-    part[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * (2 * F - 1) + tid] =
-        ((wsum[0][tid] + wsum[1][tid]) + wsum[2][tid]) + wsum[3][tid];
-}
-
 // ------------------------------------------------------------------------------------------------ backward, dk dv
 // grid (tf_grid_x(HW), B), 256 threads: wave = one pixel (tf_block); key tiles outer, query-tile pairs inner
 template <int NT>
@@ -1024,7 +594,7 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_kv_kernel(
     for (int t = 0; t < 2; ++t) dtf[s][t] = tr_pair(st, s, t * 16, lane);
 
   const float* bl = btab_lane<NT>(btab, lr, g);
-  // key tile kt + 1's raw K / V rows and RoPE coefficients are loaded while tile kt is computed (TF_KV_PF)
+  // key tile kt + 1's raw K / V rows and RoPE coefficients are loaded while tile kt is computed
   bf16x8 kraw, vraw;
   float kcs[8];
   auto fetch = [&](int t) {
@@ -1034,15 +604,14 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_kv_kernel(
     vraw = ld16(qkv + rk + 2 * INNER);
     rot8_load(rot, fkc, g, kcs);
   };
-  if (TF_KV_PF) fetch(0);
+  fetch(0);
   for (int kt = 0; kt < NT; ++kt) {
     const int fk = kt * 16 + lr;
     const bool okk = fk < F;  // padded key columns: finite garbage, not stored
     const float* bk = bl - 16 * kt;
-    if (!TF_KV_PF) fetch(kt);
     const bf16x8 kb = rope8(kraw, kcs, 1.f);  // K'^T col
     const bf16x8 vb = vraw;                   // V^T col
-    if (TF_KV_PF && kt + 1 < NT) fetch(kt + 1);
+    if (kt + 1 < NT) fetch(kt + 1);
     f32x4 dk[2] = {z4, z4}, dv[2] = {z4, z4};
 #pragma unroll
     for (int s = 0; s < NP; ++s) {
@@ -1056,7 +625,6 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_kv_kernel(
           const f32x4 bo = *reinterpret_cast<const f32x4*>(bk + 16 * qt);
           const f32x4 lq = *reinterpret_cast<const f32x4*>(Ls + qt * 16 + 4 * g);
           const f32x4 dq = *reinterpret_cast<const f32x4*>(Ds + qt * 16 + 4 * g);
-#if TF_PK
           // two elements per VALU op (v_pk_fma / v_pk_add / v_pk_mul_f32), same operations and order as below
 #pragma unroll
           for (int r = 0; r < 4; r += 2) {
@@ -1069,14 +637,6 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_kv_kernel(
             dsv[u][r] = d2[0];
             dsv[u][r + 1] = d2[1];
           }
-#else
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float pp = __builtin_amdgcn_exp2f(fmaf(sq[r], LOG2E, bo[r]) - lq[r]);
-            pv[u][r] = pp;
-            dsv[u][r] = pp * (dp[r] - dq[r]);
-          }
-#endif
         } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r) pv[u][r] = dsv[u][r] = 0.f;
@@ -1125,26 +685,13 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_kv_kernel(
 // Grid (4 * TFB_NB, B): block L -> head pair L & 3 and pixel-pair stream L >> 2; its 4 waves are the 2 pixels x the 2
 // heads, so the two 64-B head halves of every 128-B qkv / dO / O line are read by one CU at about the same time (the
 // first form, one head per block with the 8 heads' blocks on one XCD, fetched 1.5x the algorithmic bytes).
-#ifndef TFB_PF
-#define TFB_PF 1  // A/B knob: the next key pair's K / V rows loaded while the current pair is computed (0: at its start)
-#endif
-#ifndef TFB_PHASE
-#define TFB_PHASE 0  // A/B knob: a 32 x 32 score block in three phases (all 8 score MFMAs, then the softmax VALU, then the
-                     // product MFMAs); 0 = tile by tile (192x288, F = 120: 8.9 vs 9.6 ms)
-#endif
-#ifndef TFB_DIAG
-#define TFB_DIAG 0  // diagnostic builds only: 1 = every pixel reads pixel 0's rows (L2-resident), 2 = no dq / dk / dv stores
-#endif
-#ifndef TFB_SYNC
-#define TFB_SYNC 0  // A/B knob: wave-scope fences around the LDS round trips of the score loop (1 = round-5 first form)
-#endif
+// Measured and removed (round 5, profiles/r5f_*): the next key pair's K / V rows loaded at its start instead of during
+// the current pair, a 32 x 32 score block in three phases (192x288, F = 120: 9.6 vs 8.9 ms tile by tile), and
+// wave-scope fences around the score loop's LDS round trips -- all within the spread or slower.
 // A wave's LDS operations execute in issue order (no s_waitcnt is needed between a ds_write and a later ds_read of the
 // same address), and the compiler keeps may-aliasing LDS accesses in program order; the score loop's round trips
 // (K' rows -> transposed reads, dS^T tiles -> transposed reads -> the next tile's stores) therefore need no fence,
 // and without one the compiler can issue the next tile's reads ahead of the current tile's MFMAs.
-__device__ __forceinline__ void tfb_sync() {
-  if (TFB_SYNC) wsync();
-}
 constexpr int TFB_NB = 128;
 template <typename K>
 static void allow_smem(K kernel, size_t bytes) {
@@ -1264,9 +811,8 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_fused_kernel(
   for (int gp = kblk; gp < ngroups; gp += TFB_NB) {
     const int p = gp * 2 + (wid >> 1);
     if (p >= HW) break;  // wave-uniform
-    const int pl = TFB_DIAG == 1 ? (p & 1) : p;  // (diagnostic: the rows of pixels 0 / 1 for every pixel)
-    const int64_t row0 = (int64_t)b * F * HW + pl;
-    const int64_t qrow0 = pm ? ((int64_t)b * HW + pl) * F : row0;
+    const int64_t row0 = (int64_t)b * F * HW + p;
+    const int64_t qrow0 = pm ? ((int64_t)b * HW + p) * F : row0;
     // per-pixel opaque copies of the bias / RoPE-row bases: as loop invariants the compiler hoists every per-(tile,
     // lane) bias vector and RoPE row out of the pixel loop (> 100 VGPRs at NT = 8) and spills
     const float* bl = bl0 + opaque_zero();
@@ -1298,7 +844,7 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_fused_kernel(
     // ---- stage Q' = scale R q and dO rows, L and D = dO . O of the pixel's queries: every load issued first (rows past
     // F read as zeros), then branch-free stores -- Q' tiles before dO tiles, so the zero rows the last Q' tile writes
     // past the RQ staged ones (into the dO rows) are overwritten; the dO tile's land in the K' rows, staged later
-    const float* lsep = lse + (((int64_t)b * NH + h) * HW + pl) * F;
+    const float* lsep = lse + (((int64_t)b * NH + h) * HW + p) * F;
     bf16x8 qr[NT], dr[NT], orw[NT];
     float lq[NT];
 #pragma unroll
@@ -1336,7 +882,6 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_fused_kernel(
 
 #pragma unroll
     for (int sk = 0; sk < NP; ++sk) {
-      if (!TFB_PF && sk > 0) ldkv(sk);
       // K' rows of the key pair: B fragments of S, staged for the transposed reads of the dQ product
       bf16x8 kb[2], vb[2];
 #pragma unroll
@@ -1347,103 +892,12 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_fused_kernel(
         vb[u] = vraw[u];
         *reinterpret_cast<bf16x8*>(Ks + u * 1024 + frag) = kb[u];
       }
-      if (TFB_PF && sk + 1 < NP) ldkv(sk + 1);
-      tfb_sync();
+      if (sk + 1 < NP) ldkv(sk + 1);
       const bf16x8 ka[2] = {trp(Ks, 0, 0), trp(Ks, 0, 1)};  // K'^T[d][keys of the pair]
       f32x4 dk[2][2], dv[2][2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) dk[u][0] = dk[u][1] = dv[u][0] = dv[u][1] = z4;
 #pragma unroll
-#if TFB_PHASE
-      for (int sq = 0; sq < NP; ++sq) {
-        // one 32 x 32 (query pair x key pair) block in three phases, so the MFMA and VALU work of a phase is
-        // independent (the co-resident wave fills the SIMD while this one waits on a phase's results):
-        // A: the 8 score / dP MFMAs; B: softmax gradient of the 4 tiles, dS^T tiles stored; C: dQ, dV, dK MFMAs
-        f32x4 sc[2][2], dp[2][2];
-        f32x4 Lq[2], Dq[2];
-#pragma unroll
-        for (int uq = 0; uq < 2; ++uq) {
-          const int qt = 2 * sq + uq;
-          if (qt >= NT) continue;
-          const bf16x8 qa = *reinterpret_cast<const bf16x8*>(Qs + qt * 1024 + frag);
-          const bf16x8 da = *reinterpret_cast<const bf16x8*>(Os + qt * 1024 + frag);
-          Lq[uq] = *reinterpret_cast<const f32x4*>(Ls + qt * 16 + 4 * g);
-          Dq[uq] = *reinterpret_cast<const f32x4*>(Ds + qt * 16 + 4 * g);
-#pragma unroll
-          for (int uk = 0; uk < 2; ++uk) {
-            if (2 * sk + uk >= NT) continue;
-            sc[uq][uk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kb[uk], z4, 0, 0, 0);   // S'[q][key]
-            dp[uq][uk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, vb[uk], z4, 0, 0, 0);  // dP[q][key]
-          }
-        }
-        // P and dS as bf16 k-slot B fragments per key tile (slots j < 4: query tile 2 sq, j >= 4: 2 sq + 1)
-        bf16x8 pb[2], sb[2];
-#pragma unroll
-        for (int uq = 0; uq < 2; ++uq) {
-          const int qt = 2 * sq + uq;
-#pragma unroll
-          for (int uk = 0; uk < 2; ++uk) {
-            const int kt = 2 * sk + uk;
-            float sv[4];
-            if (qt < NT && kt < NT) {
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                float x = fmaf(sc[uq][uk][r], LOG2E, bl[16 * (qt - kt) + r]) - Lq[uq][r];
-                if (kt == NT - 1) x += kmask;
-                const float pp = __builtin_amdgcn_exp2f(x);
-                const float ds = pp * (dp[uq][uk][r] - Dq[uq][r]);
-                pb[uk][4 * uq + r] = (bf16)pp;
-                sv[r] = ds;
-                const int dd = kt - qt;
-                if (dd >= -ND && dd <= ND) dba[r][dd + ND] += ds;
-                else if (dd > 0) dsp += ds;
-                else dsn += ds;
-              }
-            } else {
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                pb[uk][4 * uq + r] = (bf16)0.f;
-                sv[r] = 0.f;
-              }
-            }
-            const bf16x4 t4 = {(bf16)sv[0], (bf16)sv[1], (bf16)sv[2], (bf16)sv[3]};
-#pragma unroll
-            for (int r = 0; r < 4; ++r) sb[uk][4 * uq + r] = t4[r];
-            if (qt < NT)  // dS^T[key = lane][q = 4g .. 4g + 3] of tile (uq, uk)
-              *reinterpret_cast<bf16x4*>(Tt + (uq * 2 + uk) * 512 + tto) = t4;
-          }
-        }
-        tfb_sync();
-#pragma unroll
-        for (int uq = 0; uq < 2; ++uq) {
-          const int qt = 2 * sq + uq;
-          if (qt >= NT) continue;
-          // dQ'^T[d][q] += K'^T[d][keys] dS^T[keys][q] over the pair's 32 keys
-          const s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(Tt + (uq * 2) * 512 + tti));
-          const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(Tt + (uq * 2 + 1) * 512 + tti));
-          bf16x8 bsd;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            bsd[j] = __builtin_bit_cast(bf16, (short)t0[j]);
-            bsd[4 + j] = __builtin_bit_cast(bf16, (short)t1[j]);
-          }
-#pragma unroll
-          for (int t = 0; t < 2; ++t) dq[qt][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[t], bsd, dq[qt][t], 0, 0, 0);
-        }
-        // dV^T[d][key] += dO^T[d][q] P[q][key], dK'^T[d][key] += Q'^T[d][q] dS[q][key] over the query pair's 32 rows
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const bf16x8 dta = trp(Os, sq, t), qta = trp(Qs, sq, t);
-#pragma unroll
-          for (int uk = 0; uk < 2; ++uk) {
-            if (2 * sk + uk >= NT) continue;
-            dv[uk][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dta, pb[uk], dv[uk][t], 0, 0, 0);
-            dk[uk][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qta, sb[uk], dk[uk][t], 0, 0, 0);
-          }
-        }
-        tfb_sync();  // the tiles' reads done before the next block's stores
-      }
-#else
       for (int sq = 0; sq < NP; ++sq) {
         // P and dS of the pair block as bf16 k-slot B fragments per key tile (slots j < 4: query tile 2 sq, j >= 4: 2 sq + 1)
         bf16x8 pb[2], sb[2];
@@ -1493,7 +947,6 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_fused_kernel(
             for (int r = 0; r < 4; ++r) sb[uk][4 * uq + r] = t4[r];
             *reinterpret_cast<bf16x4*>(Tt + (uq * 2 + uk) * 512 + tto) = t4;  // dS^T[key = lane][q = 4g .. 4g + 3]
           }
-          tfb_sync();
           // dQ'^T[d][q] += K'^T[d][keys] dS^T[keys][q] over the pair's 32 keys
           const s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(Tt + (uq * 2) * 512 + tti));
           const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(Tt + (uq * 2 + 1) * 512 + tti));
@@ -1517,15 +970,13 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_fused_kernel(
             dk[uk][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qta, sb[uk], dk[uk][t], 0, 0, 0);
           }
         }
-        tfb_sync();  // the tiles' reads done before the next block's stores
       }
-#endif
       // dk = R^T dK', dv of the pair's keys (rows >= F dropped by the resource)
 #pragma unroll
       for (int uk = 0; uk < 2; ++uk) {
         const int kt = 2 * sk + uk;
         if (kt >= NT) continue;
-        const auto rs = tile_rsrc(dqkv + (qrow0 + (int64_t)kt * 16 * qfs) * QKV, TFB_DIAG == 2 ? 0 : F - kt * 16,
+        const auto rs = tile_rsrc(dqkv + (qrow0 + (int64_t)kt * 16 * qfs) * QKV, F - kt * 16,
                                   (int64_t)fs_qkv, QKV * 2);
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
@@ -1543,7 +994,7 @@ __global__ __launch_bounds__(256, 2) void tflash_bwd_fused_kernel(
     // dq = scale R^T dQ'
 #pragma unroll
     for (int qt = 0; qt < NT; ++qt) {
-      const auto rs = tile_rsrc(dqkv + (qrow0 + (int64_t)qt * 16 * qfs) * QKV, TFB_DIAG == 2 ? 0 : F - qt * 16,
+      const auto rs = tile_rsrc(dqkv + (qrow0 + (int64_t)qt * 16 * qfs) * QKV, F - qt * 16,
                                 (int64_t)fs_qkv, QKV * 2);
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -1645,11 +1096,12 @@ __global__ void tf_dtable_kernel(const float* __restrict__ off, float* __restric
 
 }  // namespace
 
-// which dq kernel cesm_tflash_bwd runs.  The per-wave kernel is opt-in (CESM_TF_QW=1): in the F = 120 training step
-// the block-per-pixel kernels are faster at every level (whole step 229.9-230.0 vs 232.5-233.0 ms with it at level 0,
-// profiles/r4c13_env_ab.txt; its isolated 192x288 timing against them, profiles/r4c5_qw_check.txt, was not borne out
-// in the step).
-enum TfDq { TF_DQ_BLOCK, TF_DQ_DOV, TF_DQ_WAVE, TF_FUSED };
+// which backward cesm_tflash_bwd runs: the one-pass fused kernel (round 5) for every window of F >= 8 frames, the
+// two-kernel form below that (its D = sum P dP keeps the F = 1 rel-pos bias gradient exactly 0, where D = dO . O from
+// the bf16 O would leave a rounding residue).  Round 6 removed the other dq kernels: the per-wave dq kernel (slower
+// in the F = 120 step: 232.5-233.0 vs 229.9-230.0 ms, profiles/r4c13_env_ab.txt), the single-pass D = dO . O kernel
+// for small levels, and the CESM_TF_FUSED=0 switch back to the two-kernel form at F >= 8.
+enum TfDq { TF_DQ_BLOCK, TF_FUSED };
 // host copy of tf_bucket (relpos_bucket): the fused backward's saturated-diagonal check
 static int tf_bucket_host(int rel, int num_buckets, int max_distance) {
   int n = -rel;
@@ -1676,39 +1128,19 @@ static int tfb_nd(int F, int nt, int num_buckets, int max_distance) {
   }
   return nt - 1;
 }
-static bool tf_fused_ok(int nt, int F) { return nt >= 2 || F >= 8; }
-static TfDq tf_dq_kind(int nt, int HW, int pm = 0, int F = 17) {
-  if (nt >= 2 && getenv_flag("CESM_TF_QW") && !getenv_flag("CESM_TF_NO_QW") &&
-      (pm || (int64_t)16 * HW * QKV * 2 < (1ll << 31)))
-    return TF_DQ_WAVE;
-  // the one-pass backward (round 5) for every window of F >= 8 frames; CESM_TF_FUSED=0: the two-kernel form.  (Below
-  // 8 frames the two-kernel form stays: its D = sum P dP keeps the F = 1 rel-pos bias gradient exactly 0, where
-  // D = dO . O from the bf16 O would leave a rounding residue.)
-  static const bool fused_off = std::getenv("CESM_TF_FUSED") && std::strcmp(std::getenv("CESM_TF_FUSED"), "0") == 0;
-  if (tf_fused_ok(nt, F) && !fused_off) return TF_FUSED;
-  return TF_DO && nt >= 2 && HW < TF_DO_MAXHW ? TF_DQ_DOV : TF_DQ_BLOCK;
-}
+static TfDq tf_dq_kind(int nt, int F) { return nt >= 2 || F >= 8 ? TF_FUSED : TF_DQ_BLOCK; }
 
 extern "C" {
 
 // name of the dq kernel cesm_tflash_bwd runs for (F, HW) with frame-major qkv (host-only query; "invalid" when F
 // is unsupported)
 const char* cesm_tflash_bwd_variant(int F, int HW) {
-  static const char* names[4][9] = {
-      {"", "tflash_bwd_q_kernel<1,false>", "tflash_bwd_q_kernel<2,false>", "tflash_bwd_q_kernel<3,false>",
-       "tflash_bwd_q_kernel<4,false>", "tflash_bwd_q_kernel<5,false>", "tflash_bwd_q_kernel<6,false>",
-       "tflash_bwd_q_kernel<7,false>", "tflash_bwd_q_kernel<8,false>"},
-      {"", "", "tflash_bwd_q_kernel<2,true>", "tflash_bwd_q_kernel<3,true>", "tflash_bwd_q_kernel<4,true>",
-       "tflash_bwd_q_kernel<5,true>", "tflash_bwd_q_kernel<6,true>", "tflash_bwd_q_kernel<7,true>",
-       "tflash_bwd_q_kernel<8,true>"},
-      {"", "", "tflash_bwd_qw_kernel<2>", "tflash_bwd_qw_kernel<3>", "tflash_bwd_qw_kernel<4>",
-       "tflash_bwd_qw_kernel<5>", "tflash_bwd_qw_kernel<6>", "tflash_bwd_qw_kernel<7>", "tflash_bwd_qw_kernel<8>"},
-      {"", "tflash_bwd_fused_kernel<1>", "tflash_bwd_fused_kernel<2>", "tflash_bwd_fused_kernel<3>", "tflash_bwd_fused_kernel<4>",
-       "tflash_bwd_fused_kernel<5>", "tflash_bwd_fused_kernel<6>", "tflash_bwd_fused_kernel<7>",
-       "tflash_bwd_fused_kernel<8>"}};
+  static const char* fused[9] = {"", "tflash_bwd_fused_kernel<1>", "tflash_bwd_fused_kernel<2>", "tflash_bwd_fused_kernel<3>",
+                                 "tflash_bwd_fused_kernel<4>", "tflash_bwd_fused_kernel<5>", "tflash_bwd_fused_kernel<6>",
+                                 "tflash_bwd_fused_kernel<7>", "tflash_bwd_fused_kernel<8>"};
   if (F < 1 || F > 16 * TF_MAXT || HW < 1) return "invalid";
   const int nt = (F + 15) / 16;
-  return names[tf_dq_kind(nt, HW, 0, F)][nt];
+  return tf_dq_kind(nt, F) == TF_FUSED ? fused[nt] : "tflash_bwd_q_kernel<1>";
 }
 
 // supported windows of the MFMA temporal-attention core (bf16)
@@ -1726,13 +1158,10 @@ int cesm_tflash_fwd(const void* qkv, const float* bias, const float* rot, void* 
   const int nt = (F + 15) / 16;
   const int pm = qkv_pixel_major ? 1 : 0;
   if (pm && nt < 2) return CESM_EUNSUPPORTED;
-  if ((int64_t)16 * HW * (pm ? INNER : QKV) * 2 >= (1ll << 31)) return CESM_EUNSUPPORTED;  // TF_BUF 32-bit lane offsets
+  if ((int64_t)16 * HW * (pm ? INNER : QKV) * 2 >= (1ll << 31)) return CESM_EUNSUPPORTED;  // 32-bit lane offsets
   dim3 grid(tf_grid_x(HW), B);
-#define TFF(N)                                                                                                    \
-  if (TF_FWD2)                                                                                                    \
-    tflash_fwd2_kernel<N><<<grid, 256, 0, stream>>>((const bf16*)qkv, bias, rot, (bf16*)out, lse, F, HW, scale, pm); \
-  else                                                                                                            \
-    tflash_fwd_kernel<N><<<grid, 256, 0, stream>>>((const bf16*)qkv, bias, rot, (bf16*)out, lse, F, HW, scale, pm)
+#define TFF(N) \
+  tflash_fwd2_kernel<N><<<grid, 256, 0, stream>>>((const bf16*)qkv, bias, rot, (bf16*)out, lse, F, HW, scale, pm)
   switch (nt) {
     case 1: TFF(1); break;
     case 2: TFF(2); break;
@@ -1762,8 +1191,7 @@ int cesm_tflash_bwd(const void* qkv, const void* o, const void* dout, const floa
   if (pm && (nt < 2 || (int64_t)16 * HW * INNER * 2 >= (1ll << 31))) return CESM_EUNSUPPORTED;
   const int nblk = cesm_tflash_nblk(HW);
   dim3 gq(nblk, B * NH), gk(tf_grid_x(HW), B);
-  const TfDq kind = tf_dq_kind(nt, HW, pm, F);
-  const bool qw = kind == TF_DQ_WAVE, dov = kind == TF_DQ_DOV;
+  const TfDq kind = tf_dq_kind(nt, F);
   if (kind == TF_FUSED) {
     if ((int64_t)16 * (pm ? 1 : HW) * QKV * 2 >= (1ll << 31))
       return CESM_EUNSUPPORTED;  // 32-bit lane offsets of a 16-row tile
@@ -1793,33 +1221,11 @@ int cesm_tflash_bwd(const void* qkv, const void* o, const void* dout, const floa
     }
 #undef TFUN
 #undef TFU
-  } else {
-#define TFB(N)                                                                                                         \
-  if (qw && N >= 2)                                                                                                    \
-    tflash_bwd_qw_kernel<(N >= 2 ? N : 2)><<<gq, 256, 0, stream>>>((const bf16*)qkv, (const bf16*)o,                   \
-                                                                   (const bf16*)dout, lse, bias, rot, (bf16*)dqkv,    \
-                                                                   dbuf, part, F, HW, scale, pm);                     \
-  else if (dov && N >= 2)                                                                                              \
-    tflash_bwd_q_kernel<N, (N >= 2)><<<gq, 64 * N, 0, stream>>>((const bf16*)qkv, (const bf16*)o, (const bf16*)dout,   \
-                                                                lse, bias, rot, (bf16*)dqkv, dbuf, part, F, HW, scale, \
-                                                                pm);                                                  \
-  else                                                                                                                 \
-    tflash_bwd_q_kernel<N, false><<<gq, 64 * N, 0, stream>>>((const bf16*)qkv, (const bf16*)o, (const bf16*)dout, lse, \
-                                                             bias, rot, (bf16*)dqkv, dbuf, part, F, HW, scale, pm);   \
-  tflash_bwd_kv_kernel<N><<<gk, 256, 0, stream>>>((const bf16*)qkv, (const bf16*)dout, lse, dbuf, bias, rot,           \
-                                                  (bf16*)dqkv, F, HW, scale, pm)
-  switch (nt) {
-    case 1: TFB(1); break;
-    case 2: TFB(2); break;
-    case 3: TFB(3); break;
-    case 4: TFB(4); break;
-    case 5: TFB(5); break;
-    case 6: TFB(6); break;
-    case 7: TFB(7); break;
-    case 8: TFB(8); break;
-    default: return CESM_EUNSUPPORTED;
-  }
-#undef TFB
+  } else {  // F < 8: one 16-frame tile
+    tflash_bwd_q_kernel<1><<<gq, 64, 0, stream>>>((const bf16*)qkv, (const bf16*)o, (const bf16*)dout, lse, bias, rot,
+                                                 (bf16*)dqkv, dbuf, part, F, HW, scale, pm);
+    tflash_bwd_kv_kernel<1><<<gk, 256, 0, stream>>>((const bf16*)qkv, (const bf16*)dout, lse, dbuf, bias, rot,
+                                                   (bf16*)dqkv, F, HW, scale, pm);
   }
   if (dtable) {
     tf_dbias_off_kernel<<<dim3(2 * F - 1, NH), 256, 0, stream>>>(part, off, nblk, B, F);

@@ -59,6 +59,10 @@ class GradAllReducer:
         self.side = use_side_stream
         self._stream = None
         self._armed = None
+        # timing = True: every overlapped bucket is bracketed by HIP events on the communication stream (the pre-scale
+        # and the all-reduce, which the stream waits for), so bench.py can report the measured all-reduce time per step
+        self.timing = False
+        self._events = []  # (start, end, bytes)
 
     def buckets(self, n):
         return [(s, min(n, s + self.bucket_elems)) for s in range(0, n, self.bucket_elems)]
@@ -81,6 +85,16 @@ class GradAllReducer:
         else:
             for a, b in self.buckets(flat_grad.numel()):
                 dist.all_reduce(flat_grad[a:b], op=dist.ReduceOp.SUM)
+
+    def pop_timing(self):
+        """(total all-reduce ms, bucket count, bytes) of the buckets timed since the last call (synchronizes)"""
+        if not self._events:
+            return 0.0, 0, 0
+        self._events[-1][1].synchronize()
+        ms = sum(a.elapsed_time(b) for a, b, _ in self._events)
+        n, nbytes = len(self._events), sum(x for _, _, x in self._events)
+        self._events = []
+        return ms, n, nbytes
 
     def broadcast_params(self, flat_params, src=0):
         """Initial replica sync (what DDP's constructor does at train.py:1076)."""
@@ -116,8 +130,17 @@ class GradAllReducer:
                 if s is not None:
                     comm.wait_stream(s)
             with torch.cuda.stream(comm):
+                ev = None
+                if self.timing:
+                    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    ev[0].record(comm)
                 chunk.mul_(1.0 / self.world)
-                st["works"].append(dist.all_reduce(chunk, op=dist.ReduceOp.SUM, async_op=True))
+                w = dist.all_reduce(chunk, op=dist.ReduceOp.SUM, async_op=True)
+                if ev is not None:
+                    w.wait()  # the communication stream waits for the collective: the end event follows it
+                    ev[1].record(comm)
+                    self._events.append((ev[0], ev[1], chunk.numel() * chunk.element_size()))
+                st["works"].append(w)
         else:
             chunk.mul_(1.0 / self.world)
             dist.all_reduce(chunk, op=dist.ReduceOp.SUM)

@@ -74,14 +74,19 @@ _QUEUES = {}
 
 def work_queue():
     """the caller-owned int32[2] work counter of the persistent convs' dynamic item claiming (cesm_conv_fwd's queue):
-    one per (device, stream) -- launches on one stream run in order, so they share it; the kernels leave it zero.
-    CESM_CONV_STATIC=1 passes null (static item split)."""
+    one per (device, stream) -- launches on one stream run in order, so they share it.  cesm_conv_fwd zeroes it with a
+    stream-ordered memset before every launch that uses it (round 6, ADVICE r5: a launch cut short can no longer leave
+    a stale count that makes the next one skip its items).  Not allocated during graph capture (the allocation would
+    belong to the graph's private pool): a capture that finds no counter for its stream gets the static item split, as
+    does CESM_CONV_STATIC=1."""
     if STATIC_CONV:
         return 0
     st = torch.cuda.current_stream()
     key = (st.device.index, st.cuda_stream)
     q = _QUEUES.get(key)
     if q is None:
+        if torch.cuda.is_current_stream_capturing():
+            return 0
         q = _QUEUES[key] = torch.zeros(4, dtype=torch.int32, device=st.device)
     return q.data_ptr()
 
@@ -147,8 +152,8 @@ CONV_TRACE = [] if os.environ.get("CESM_TRACE_CONV") else None
 
 # target block count of the split-K weight-gradient launches: every split writes a full fp32
 # [Cout][K] slab that conv_wgrad_reduce reads back, so more blocks than ~2-4 per CU only adds slab
-# traffic (override: CESM_WGRAD_BLOCKS)
-WGRAD_BLOCKS = int(os.environ.get("CESM_WGRAD_BLOCKS", "1024"))
+# traffic (round 3: 512 / 2048 blocks 144.7 / 131.2 ms per step against 129.7 at 1024)
+WGRAD_BLOCKS = 1024
 
 
 def _wgrad_nsplit(M, cout, K, bm=64, blocks=None):
@@ -186,7 +191,7 @@ def conv_wgrad(x1, x2, dy1, dy2, dw, geom, swap, flip, accumulate=True, db=None)
     # input parity (4 taps); its bias gradient is the caller's column sum (same condition as cesm_conv_wgrad)
     s2 = (KH == 4 and KW == 4 and St == 2 and Pd == 1 and U == 1 and Hi == 2 * Ho and Wi == 2 * Wo and Wo >= 64
           and x2 is None
-          and dy2 is None and x1.dtype == torch.bfloat16 and os.environ.get("CESM_NO_S2HALO", "0") in ("", "0"))
+          and dy2 is None and x1.dtype == torch.bfloat16)
     if (halo3 or s2) and x1.dtype == torch.bfloat16:
         # halo wgrad kernels: blocks of 64 co x 32 ci (all 9 taps / one parity's 4), split over pixel tiles
         nb = WGRAD_BLOCKS // 2
@@ -198,8 +203,7 @@ def conv_wgrad(x1, x2, dy1, dy2, dw, geom, swap, flip, accumulate=True, db=None)
     if CONV_TRACE is not None:
         CONV_TRACE.append(("wgrad", Nb, Hi, Wi, C1 + C2, Ho, Wo, Cout, KH, KW, St, Pd, U))
     # the bias rides on the wide-tile kernel only (same dispatch condition as cesm_conv_wgrad)
-    wide = (x1.dtype == torch.bfloat16 and not halo3 and not s2 and M < (1 << 31) and dy2 is None
-            and os.environ.get("CESM_NO_WIDE_WGRAD", "0") in ("", "0") and FUSED_BIAS_GRAD)
+    wide = x1.dtype == torch.bfloat16 and not halo3 and not s2 and M < (1 << 31) and dy2 is None
     if db is not None and wide:
         _chk(db, (Cout,), torch.float32)
         bslab = empty((nsplit, Cout), torch.float32, x1.device)
@@ -209,8 +213,6 @@ def conv_wgrad(x1, x2, dy1, dy2, dw, geom, swap, flip, accumulate=True, db=None)
          Hi, Wi, C1, C2, Ho, Wo, Cout, Co1, KH, KW, St, Pd, U, int(swap), int(flip), int(accumulate), S())
     return db is not None
 
-
-FUSED_BIAS_GRAD = os.environ.get("CESM_NO_FUSED_BIAS_GRAD", "0") != "1"
 
 
 def colsum(x, dst, accumulate=True):
@@ -348,12 +350,9 @@ def relpos_fwd(table, F, num_buckets=32, max_distance=32):
     return bias
 
 
-# bf16 temporal-attention core on MFMA (csrc/tflash.hip) for F <= 128; CESM_NO_TFLASH=1: the VALU kernels
-TFLASH = os.environ.get("CESM_NO_TFLASH", "0") != "1"
-
-
+# bf16 temporal-attention core on MFMA (csrc/tflash.hip) for F <= 128; fp32 (parity mode): the VALU kernels
 def _tflash(qkv, F):
-    return TFLASH and qkv.dtype == torch.bfloat16 and lib().cesm_tflash_supported(F) == 1
+    return qkv.dtype == torch.bfloat16 and lib().cesm_tflash_supported(F) == 1
 
 
 def tattn_fwd(qkv, bias, rot, B, F, HW, scale, save=True, pixel_major=False):
@@ -476,11 +475,10 @@ def tblock_fwd_fold(x, gamma, wqkv_f32, wout, bias, rot, B, F, scale, save=True,
 
 
 def tblock_bwd_dw(x, dy, mr, lse, wqkv_f32, gamma, wout_t, bias, rot, dwqkv, dgamma, dtable, B, F, scale,
-                  num_buckets=32, max_distance=32, dwout=None):
+                  num_buckets=32, max_distance=32):
     """head-parallel fused temporal-block backward with in-kernel weight gradients (C = 64, 4F <= 48):
     returns dx; dwqkv (+)= the to_qkv weight gradient, dgamma (+)= the LN gamma gradient, dtable (+)= the
-    rel-pos table gradient, dwout [C, 256] (+)= the to_out weight gradient (each nullable; with dwout the forward
-    need not save O).  The forward must be tblock_fwd_fold's."""
+    rel-pos table gradient (each nullable).  The forward must be tblock_fwd_fold's."""
     Nb, H, W, C = x.shape
     HW = H * W
     _chk(x, dtype=torch.bfloat16)
@@ -498,13 +496,11 @@ def tblock_bwd_dw(x, dy, mr, lse, wqkv_f32, gamma, wout_t, bias, rot, dwqkv, dga
     dev = x.device
     dx = empty(x.shape, x.dtype, dev)
     dbp = empty((8, nblk, F, F), torch.float32, dev)
-    if dwout is not None:
-        _chk(dwout, (C, 256), torch.float32)
-    slab = empty((nblk * (768 * C + (C * 256 if dwout is not None else 0)),), torch.float32, dev)
+    slab = empty((nblk * 768 * C,), torch.float32, dev)
     tmp = empty((768, C), torch.float32, dev)
     wimg = empty(((2 * 768 + 256) * C,), torch.bfloat16, dev)
     call("cesm_tblock_bwd_dw", P(x), P(dy), P(mr), P(lse), P(wqkv_f32), P(gamma), P(wout_t), P(bias), P(rot), P(dx),
-         P(dwqkv), P(dgamma), P(dwout), P(dbp), P(slab), P(tmp), P(wimg), nblk, B, F, HW, C, float(scale), 1, S())
+         P(dwqkv), P(dgamma), P(dbp), P(slab), P(tmp), P(wimg), nblk, B, F, HW, C, float(scale), 1, S())
     if dtable is not None:
         ws = empty((8, F, F), torch.float32, dev)
         call("cesm_relpos_bwd", P(dbp), nblk, 1, P(dtable), P(ws), F, 8, num_buckets, max_distance, 1, S())
@@ -512,8 +508,8 @@ def tblock_bwd_dw(x, dy, mr, lse, wqkv_f32, gamma, wout_t, bias, rot, dwqkv, dga
 
 
 # fused SLA at C = 64 and 128 (measured +0.8 % step throughput for C = 128 with the parallel context
-# combine); CESM_SLAF_C64_ONLY=1 restores the unfused path at C = 128
-SLAF_C = (64,) if os.environ.get("CESM_SLAF_C64_ONLY") else (64, 128)
+# combine)
+SLAF_C = (64, 128)
 
 
 def slaf_fwd(x, gamma, wqkv, wout, bout, scale, eps=1e-5, save_o=False):

@@ -93,7 +93,8 @@ class RunCtx:
         self.dt = None      # grad of the time embedding (allocated in backward)
         self.dtable = None  # grad of the rel-pos embedding table
         self.wstream = None  # weight-gradient stream (set by the backward when WGRAD_STREAM)
-        self.keep = []  # tensors the wgrad stream reads, alive until join()
+        self.keep = []  # tensors the wgrad stream reads, alive until released by checkpoint() / join()
+        self._mark = None  # (event on the wgrad stream, len(keep)) at the last checkpoint
 
     def packed(self, w, cout, cin, kh, kw, swap, flip):
         return self.net._packed(w, self.cdt, cout, cin, kh, kw, swap, flip)
@@ -101,11 +102,27 @@ class RunCtx:
     def side(self, *tensors, attn=False):
         return _Side(self if (attn or WGRAD_STREAM == "1") else _NOSIDE, tensors)
 
+    def checkpoint(self):
+        """a module boundary of the backward: release the tensors of the wgrad work enqueued before the PREVIOUS boundary,
+        once the current stream has been ordered after that work (round 6, ADVICE r5: join() alone kept every per-layer
+        dy / x the wgrad stream read until the end of the backward).  One level of overlap stays; the kept set is
+        bounded by about two levels' tensors."""
+        if self.wstream is None:
+            return
+        ev = torch.cuda.Event()
+        ev.record(self.wstream)
+        if self._mark is not None:
+            prev, n = self._mark
+            torch.cuda.current_stream().wait_event(prev)
+            del self.keep[:n]
+        self._mark = (ev, len(self.keep))
+
     def join(self):
         """current stream waits for every weight gradient enqueued so far; the tensors they read may go after that"""
         if self.wstream is not None:
             torch.cuda.current_stream().wait_stream(self.wstream)
         self.keep.clear()
+        self._mark = None
 
 
 def gbuf(p):
@@ -317,8 +334,8 @@ def _flat(p):
 
 
 # GroupNorm statistics from partials written by the Block conv's epilogue (halo conv kernels) instead of a
-# separate pass over y; CESM_NO_GN_EPI=1 restores the pass
-GN_EPI_STATS = os.environ.get("CESM_NO_GN_EPI", "0") != "1"
+# separate pass over y (round 2: the pass took 2.06 ms per step, the epilogue partials ~+3 % of the convs)
+GN_EPI_STATS = True
 
 
 def block_fwd(rc, blk, x1, x2, ss, res):
@@ -385,39 +402,28 @@ def resnet_bwd(rc, rb, st, dout):
     return dx  # tensor, or (dx1, dx2) for concat inputs
 
 
-FUSED_TBLOCK = os.environ.get("CESM_NO_FUSED_TBLOCK", "0") != "1"
-TW_FWD_O = os.environ.get("CESM_TW_FWD_O", "1") != "0"  # forward writes O for dW_out (else the backward emits it)
 # widest channel count routed to the fused kernels: below it the 768-channel qkv intermediate is what
 # costs (HBM); above it the level is small and the unfused GEMMs are cheaper than per-pixel-group
-# weight re-reads
-FUSED_TBLOCK_MAXC = int(os.environ.get("CESM_TBLOCK_MAXC", "128"))  # C = 256/512: unfused measured faster
+# weight re-reads (C = 256 / 512: unfused measured faster, rounds 1-2)
+FUSED_TBLOCK_MAXC = 128
 
 
 def _tblock_fused(rc, C):
-    return (FUSED_TBLOCK and rc.cdt == torch.bfloat16 and rc.F <= 16 and C in K.TBLOCK_C
-            and C <= FUSED_TBLOCK_MAXC)
+    return rc.cdt == torch.bfloat16 and rc.F <= 16 and C in K.TBLOCK_C and C <= FUSED_TBLOCK_MAXC
 
 
-# head-parallel backward with in-kernel weight gradients (C = 64, F <= 12): no 768-channel dqkv round trip
-TBLOCK_DW = os.environ.get("CESM_NO_TBLOCK_DW", "0") != "1"
-# ... and, opt-in (CESM_TWH_DWOUT=1, round 5), the to_out weight gradient in that kernel too, so the forward writes no O.
-# Measured slower: the 32 extra accumulators push twh_bwd from 9 to 58-93 spilled registers and 3.3 to 5.3-5.5 ms per
-# level-0 call, more than the O write and the wide weight-gradient GEMM it removes.  Default: the forward
-# saves O for a wide weight-gradient GEMM with dy, as through round 4.
-TWH_DWOUT = os.environ.get("CESM_TWH_DWOUT", "0") == "1"
-
-
+# head-parallel backward with in-kernel weight gradients (C = 64, F <= 12): no 768-channel dqkv round trip.  The forward
+# saves O for a wide to_out weight-gradient GEMM with dy (the in-kernel to_out gradient measured slower, round 5: 32 more
+# accumulators took twh_bwd from 9 to 58-93 spilled registers and 3.3 to 5.3 ms per level-0 call; removed in round 6).
 def _tblock_dw(rc, x):
     Nb, H, W, C = x.shape
-    return TBLOCK_DW and _tblock_fused(rc, C) and K.tblock_bwd_dw_supported(rc.B, rc.F, H * W, C)
+    return _tblock_fused(rc, C) and K.tblock_bwd_dw_supported(rc.B, rc.F, H * W, C)
 
 
-# pixel-major qkv for the long-window attention core (CESM_TF_PM=0: frame-major)
-TF_PM = os.environ.get("CESM_TF_PM", "1") != "0"
-
-
+# pixel-major qkv for the long-window attention core (round 4: a pixel's frames as adjacent rows, F = 120 step
+# 234.4-235.1 -> 232.0-232.3 ms)
 def _tf_pixel_major(rc, x):
-    return TF_PM and rc.F > 16 and x.dtype == torch.bfloat16 and K.lib().cesm_tflash_supported(rc.F) == 1 and K.TFLASH
+    return rc.F > 16 and x.dtype == torch.bfloat16 and K.lib().cesm_tflash_supported(rc.F) == 1
 
 
 def tattn_fwd(rc, res_mod, x):
@@ -438,18 +444,17 @@ def tattn_fwd(rc, res_mod, x):
         return K.conv_fwd(v, None, wo, None, (H, W, C, 1, 1, 1, 0, 1), res=x), None
     if _tblock_dw(rc, x):
         # gamma folded into the QKV weights (images built from the fp32 master weight); the backward computes
-        # the to_qkv and gamma gradients in-kernel, and with TWH_DWOUT the to_out gradient too (no O saved).
+        # the to_qkv and gamma gradients in-kernel, the to_out gradient from the saved O.
         wo = rc.packed(attn.to_out.weight, C, 256, 1, 1, 0, 0)
         y, mr, lse, o = K.tblock_fwd_fold(x, _flat(pre.norm.gamma), attn.to_qkv.weight, wo, rc.bias, rc.rot, rc.B,
-                                          rc.F, attn.scale, save=rc.save, eps=pre.norm.eps,
-                                          save_o=rc.save and not TWH_DWOUT)
+                                          rc.F, attn.scale, save=rc.save, eps=pre.norm.eps, save_o=rc.save)
         st = SimpleNamespace(fused=True, fold=True, x=x, mr=mr, lse=lse, o=o) if rc.save else None
         return y, st
     if _tblock_fused(rc, C):
         wq = rc.packed(attn.to_qkv.weight, 768, C, 1, 1, 0, 0)
         wo = rc.packed(attn.to_out.weight, C, 256, 1, 1, 0, 0)
         # training: the forward also writes O (to_out's input) so the backward does not emit it
-        save_o = rc.save and C <= 256 and TW_FWD_O
+        save_o = rc.save and C <= 256
         y, mr, lse, o = K.tblock_fwd(x, _flat(pre.norm.gamma), wq, wo, rc.bias, rc.rot, rc.B, rc.F, attn.scale,
                                      save=rc.save, eps=pre.norm.eps, save_o=save_o)
         st = SimpleNamespace(fused=True, fold=False, x=x, mr=mr, lse=lse, o=o) if rc.save else None
@@ -475,11 +480,9 @@ def tattn_bwd(rc, res_mod, st, dy):
     if st.fused and st.fold:
         wo_t = rc.packed(attn.to_out.weight, 256, C, 1, 1, 1, 1)
         dwo = gbuf(attn.to_out.weight)
-        in_kernel = st.o is None  # TWH_DWOUT: the forward wrote no O
         dx = K.tblock_bwd_dw(st.x, dy, st.mr, st.lse, attn.to_qkv.weight, _flat(pre.norm.gamma), wo_t, rc.bias, rc.rot,
-                             gbuf(attn.to_qkv.weight), _gflat(pre.norm.gamma), rc.dtable, rc.B, rc.F, attn.scale,
-                             dwout=dwo.view(C, 256) if in_kernel and dwo is not None else None)
-        if dwo is not None and not in_kernel:
+                             gbuf(attn.to_qkv.weight), _gflat(pre.norm.gamma), rc.dtable, rc.B, rc.F, attn.scale)
+        if dwo is not None:
             with rc.side(st.o, dy, attn=True):
                 K.conv_wgrad(st.o, None, dy, None, dwo, (H, W, C, 1, 1, 1, 0, 1), 0, 0)
         return dx
@@ -507,16 +510,10 @@ def tattn_bwd(rc, res_mod, st, dy):
     return K.ln_bwd(dn, st.x, st.mr, _flat(pre.norm.gamma), gbuf(pre.norm.gamma), dres=dy, perm=st.perm)
 
 
-FUSED_SLA = os.environ.get("CESM_NO_FUSED_SLA", "0") != "1"
-SLA_FWD_O = os.environ.get("CESM_SLA_FWD_O", "1") != "0"  # forward writes O for dW_out (else the backward emits it)
-
-
 def _sla_fused(rc, C):
-    return FUSED_SLA and rc.cdt == torch.bfloat16 and C in K.SLAF_C
+    return rc.cdt == torch.bfloat16 and C in K.SLAF_C
 
 
-# head-parallel SLA backward with in-kernel weight gradients (C = 64)
-SLA_DW = os.environ.get("CESM_NO_SLA_DW", "0") != "1"
 _ONES = {}
 
 
@@ -527,14 +524,11 @@ def _ones(C, device):
     return t
 
 
-# to_out weight / bias gradients of the in-kernel-dW SLA backward from the recomputed q~ and the forward's
-# context (no 256-channel O written by the forward); CESM_SLA_DWOUT=0 restores O + the wide weight-gradient GEMM
-SLA_DWOUT = os.environ.get("CESM_SLA_DWOUT", "1") != "0"
-
-
+# head-parallel SLA backward with in-kernel weight gradients (C = 64), the to_out weight / bias gradients from the
+# recomputed q~ and the forward's context (no 256-channel O written by the forward; round 2: 58.44 -> 59.30 samples/s)
 def _sla_dw(rc, x):
     Nb, H, W, C = x.shape
-    return SLA_DW and _sla_fused(rc, C) and K.slaf_bwd_dw_supported(Nb, H * W, C)
+    return _sla_fused(rc, C) and K.slaf_bwd_dw_supported(Nb, H * W, C)
 
 
 def sla_fwd(rc, res_mod, x):
@@ -545,14 +539,13 @@ def sla_fwd(rc, res_mod, x):
     Nb, H, W, C = x.shape
     if _sla_dw(rc, x):
         # LN gamma folded into the QKV weights (unit gamma in the kernels): the backward then produces the
-        # to_qkv and gamma gradients in-kernel, and (SLA_DWOUT) the to_out gradients from the recomputed q~ and
-        # the saved context, so O is not written; otherwise O is saved for a to_out weight-gradient GEMM.
+        # to_qkv and gamma gradients in-kernel, and the to_out gradients from the recomputed q~ and the saved
+        # context, so O is not written.
         gamma = _flat(pre.norm.gamma)
         wq_fold = K.pack_scaled(sla.to_qkv.weight.reshape(768, C), gamma)
         wo = rc.packed(sla.to_out.weight, C, 256, 1, 1, 0, 0)
         ones = _ones(C, x.device)
-        y, state = K.slaf_fwd(x, ones, wq_fold, wo, sla.to_out.bias, sla.scale, eps=pre.norm.eps,
-                              save_o=rc.save and not SLA_DWOUT)
+        y, state = K.slaf_fwd(x, ones, wq_fold, wo, sla.to_out.bias, sla.scale, eps=pre.norm.eps, save_o=False)
         st = SimpleNamespace(fused=True, fold=True, x=x, state=state, wq_fold=wq_fold) if rc.save else None
         return y, st
     if _sla_fused(rc, C):
@@ -560,7 +553,7 @@ def sla_fwd(rc, res_mod, x):
         wo = rc.packed(sla.to_out.weight, C, 256, 1, 1, 0, 0)
         # training: the forward also writes O (to_out's input) so the backward does not emit it
         y, state = K.slaf_fwd(x, _flat(pre.norm.gamma), wq, wo, sla.to_out.bias, sla.scale, eps=pre.norm.eps,
-                              save_o=rc.save and SLA_FWD_O)
+                              save_o=rc.save)
         st = SimpleNamespace(fused=True, fold=False, x=x, state=state) if rc.save else None
         return y, st
     n, mr = K.ln_fwd(x, _flat(pre.norm.gamma), save=rc.save, eps=pre.norm.eps)
@@ -578,24 +571,14 @@ def sla_bwd(rc, res_mod, st, dy):
     if st.fused and st.fold:
         wo_t = rc.packed(sla.to_out.weight, 256, C, 1, 1, 1, 1)
         dwo, dbo = gbuf(sla.to_out.weight), gbuf(sla.to_out.bias)
-        o = st.state[4]
-        in_kernel = o is None  # the forward did not write O (SLA_DWOUT): to_out gradients from the dctx pass
-        if in_kernel and (dwo is None) != (dbo is None):  # one of the two frozen: a scratch destination
+        if (dwo is None) != (dbo is None):  # one of the two frozen: a scratch destination
             dwo = dwo if dwo is not None else torch.zeros_like(sla.to_out.weight)
             dbo = dbo if dbo is not None else torch.zeros_like(sla.to_out.bias)
-        dx = K.slaf_bwd_dw(st.x, dy, _ones(C, dy.device), st.wq_fold, sla.to_qkv.weight.reshape(768, C),
-                           _flat(pre.norm.gamma), wo_t, st.state, _wflat(sla.to_qkv.weight), _gflat(pre.norm.gamma),
-                           sla.scale, eps=pre.norm.eps,
-                           dwout=dwo.view(C, 256) if in_kernel and dwo is not None else None,
-                           dbout=dbo if in_kernel and dwo is not None else None)
-        if in_kernel:
-            return dx
-        with rc.side(o, dy, attn=True):
-            if dwo is not None and K.conv_wgrad(o, None, dy, None, dwo, (H, W, C, 1, 1, 1, 0, 1), 0, 0, db=dbo):
-                dbo = None
-            if dbo is not None:
-                K.colsum(dy, dbo)
-        return dx
+        # to_out gradients from the dctx pass (the forward wrote no O)
+        return K.slaf_bwd_dw(st.x, dy, _ones(C, dy.device), st.wq_fold, sla.to_qkv.weight.reshape(768, C),
+                             _flat(pre.norm.gamma), wo_t, st.state, _wflat(sla.to_qkv.weight), _gflat(pre.norm.gamma),
+                             sla.scale, eps=pre.norm.eps, dwout=dwo.view(C, 256) if dwo is not None else None,
+                             dbout=dbo if dwo is not None else None)
     if st.fused:
         wq = rc.packed(sla.to_qkv.weight, 768, C, 1, 1, 0, 0)
         wq_t = rc.packed(sla.to_qkv.weight, C, 768, 1, 1, 1, 1)
@@ -795,6 +778,7 @@ class UNetModel3D(nn.Module):
         def done(*mods):  # data-parallel overlap: these modules' gradients are final (distributed.arm)
             if hook is not None:
                 hook([p for m in mods for p in m.parameters()], rc.wstream)
+            rc.checkpoint()
         if WGRAD_STREAM != "0" and dout.is_cuda:
             rc.wstream = _wgrad_stream(dev)
         rc.dt = torch.zeros((rc.B, self.time_mlp[1].out_features), dtype=torch.float32, device=dev)

@@ -32,8 +32,10 @@ extern "C" {
  *   4 (round 4): cesm_ln_fwd / cesm_ln_bwd gained (perm_f, perm_hw), cesm_tflash_fwd / cesm_tflash_bwd gained
  *     qkv_pixel_major — each before the hipStream_t;
  *   5 (round 5): cesm_abi_version() itself; cesm_conv_fwd / cesm_conv_fwd_gn gained `queue` and cesm_tblock_bwd_dw
- *     gained `dwout`, each before the hipStream_t / after dgamma. */
-#define CESM_ABI_VERSION 5
+ *     gained `dwout`, each before the hipStream_t / after dgamma;
+ *   6 (round 6): cesm_tblock_bwd_dw lost `dwout` again (the in-kernel to_out weight gradient measured slower than the
+ *     forward's O write and was removed). */
+#define CESM_ABI_VERSION 6
 int cesm_abi_version(void);
 /* Measurement aid, not a training op: nblk blocks that each occupy one whole CU (full LDS) for `usec` microseconds on
  * `stream` -- the one-GPU stand-in for the RCCL kernels of an overlapped gradient all-reduce (tools/overlap_sim.py,
@@ -185,10 +187,9 @@ int cesm_tblock_bwd(const void* x, const void* dy, const float* gamma, const flo
  * cesm_tblock_fwd_fold is cesm_tblock_fwd with LN gamma folded into the QKV weights (wqkv_f32: the fp32
  * master weight [768][C]; wimg (768 + 256) * C bf16); cesm_tblock_bwd_dw is its backward: dx, and
  * dwqkv (+)= dW_qkv, dgamma (+)= the LN gamma gradient (nullable) without the 768-channel dqkv / xn
- * intermediates; dbias_part [8][nblk][F][F] (cesm_relpos_bwd, B = 1); slab nblk*768*C (+ nblk*C*256 with
- * dwout) and tmp 768*C floats, wimg (2*768 + 256) * C bf16; nblk from cesm_tblock_bwd_dw_nblk (0 = unsupported
- * shape).  dwout (nullable; ABI 5): dW_out [C][256] (+)= the to_out weight gradient, computed in-kernel from the
- * recomputed attention probabilities (O = P V per head) -- the forward then need not write O (o = NULL).
+ * intermediates; dbias_part [8][nblk][F][F] (cesm_relpos_bwd, B = 1); slab nblk*768*C and tmp 768*C floats,
+ * wimg (2*768 + 256) * C bf16; nblk from cesm_tblock_bwd_dw_nblk (0 = unsupported shape).  The to_out weight
+ * gradient comes from the O the forward wrote (o) and a wide weight-gradient GEMM.
  * Replaces video_net.py:368-454 (Attention) + :90-98 (PreNorm LN) + :69-75 (Residual) and the
  * to_qkv / to_out weight gradients of its backward. */
 int cesm_tblock_bwd_dw_nblk(int B, int F, int HW, int C);
@@ -197,7 +198,7 @@ int cesm_tblock_fwd_fold(const void* x, const float* gamma, const float* wqkv_f3
                          int B, int F, int HW, int C, float scale, float eps, hipStream_t stream);
 int cesm_tblock_bwd_dw(const void* x, const void* dy, const float* mr, const float* lse, const float* wqkv_f32,
                        const float* gamma, const void* wout_t, const float* bias, const float* rot, void* dx,
-                       float* dwqkv, float* dgamma, float* dwout, float* dbias_part, float* slab, float* tmp, void* wimg,
+                       float* dwqkv, float* dgamma, float* dbias_part, float* slab, float* tmp, void* wimg,
                        int nblk, int B, int F, int HW, int C, float scale, int accumulate, hipStream_t stream);
 /* spatial linear attention core (video_net.py:335-345 between to_qkv and to_out) */
 int cesm_sla_nchunk(int HW);

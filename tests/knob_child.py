@@ -1,6 +1,6 @@
-"""Cases for tests/test_gpu_knobs.py, computed in a process whose environment selects a kernel variant.
+"""Cases for tests/test_gpu_knobs.py (and the polluter runs of tests/test_gpu_stale_state.py), computed in a process whose environment selects a kernel variant.
 
-The library reads its dispatch knobs (CESM_CONV_WS, CESM_TF_QW, ...) once per process (common.h getenv_flag caches
+The library reads its dispatch knobs (CESM_CONV_WS) once per process (common.h getenv_flag caches
 the first lookup), so a knob-on result comes from a child process started with the knob set before any GPU call:
 
   CESM_CONV_WS=1 python tests/knob_child.py <case> <out.pt>
@@ -89,7 +89,34 @@ def tf_case(name, dev):
     return {k: (v.cpu() if torch.is_tensor(v) else v) for k, v in out.items()}
 
 
+def train_step_case(dev):
+    """one bf16 training step of more_blocks (64 x 96, F = 12, B = 2): loss, every parameter gradient and the peak
+    allocated memory of the step (for CESM_WGRAD_STREAM=1 against the default)"""
+    from cesm_emulator_amd.model import UNet, Diffusion
+    torch.manual_seed(3)
+    net = UNet(ch_mults=(1, 2, 4, 8)).to(dev)
+    net.compute_dtype = torch.bfloat16
+    d = Diffusion(net).to(dev)
+    g = torch.Generator().manual_seed(5)
+    x0 = torch.randn(2, 1, 64, 96, generator=g).to(dev)
+    cond = torch.randn(2, 1, 12, 64, 96, generator=g).to(dev)
+    t = torch.randint(0, 1000, (2,), generator=g).to(dev)
+    noise = torch.randn(2, 1, 64, 96, generator=g).to(dev)
+    torch.cuda.synchronize()
+    torch.cuda.reset_peak_memory_stats(dev)
+    base = torch.cuda.memory_allocated(dev)
+    loss = d.loss(x0, cond, t=t, noise=noise)
+    loss.backward()
+    torch.cuda.synchronize()
+    out = {"variant": "train_step", "loss": loss.detach().cpu(),
+           "peak_bytes": torch.tensor(torch.cuda.max_memory_allocated(dev) - base)}
+    out.update({"grad." + n: p.grad.detach().cpu() for n, p in net.named_parameters() if p.grad is not None})
+    return out
+
+
 def compute(case, dev):
+    if case == "train_step":
+        return train_step_case(dev)
     return conv_case(case, dev) if case in CONV_CASES else tf_case(case, dev)
 
 

@@ -736,14 +736,7 @@ def test_tblock_fold_forward_and_dw_backward(dev, Fr, B, H, W):
     dtable = torch.zeros(32, 8, device=dev)
     dwq = torch.full((768, C), 0.5, device=dev)   # accumulates (+=)
     dx = K.tblock_bwd_dw(xd, gd, mr, lse, wqkv, gamma, wo_t, rc.bias, rc.rot, dwq, dgamma, dtable, B, Fr, attn.scale)
-    # the in-kernel to_out gradient (round 5: O = P V recomputed per head, no O from the forward), onto 0.5; the
-    # other outputs must not change
-    dwo_k = torch.full((C, 256), 0.5, device=dev)
-    dwq2, dgamma2, dtable2 = torch.full((768, C), 0.5, device=dev), torch.full((C,), 0.25, device=dev), torch.zeros(32, 8, device=dev)
-    dx2 = K.tblock_bwd_dw(xd, gd, mr, lse, wqkv, gamma, wo_t, rc.bias, rc.rot, dwq2, dgamma2, dtable2, B, Fr, attn.scale,
-                          dwout=dwo_k)
     torch.cuda.synchronize()
-    assert torch.equal(dx2, dx) and torch.equal(dwq2, dwq) and torch.equal(dgamma2, dgamma) and torch.equal(dtable2, dtable)
     dwo = gd.reshape(-1, C).double().t() @ o.reshape(-1, 256).double()
     from oracle import ref_cpu as R
     ref = R.Residual(R.PreNorm(C, R.EinopsToAndFrom(R.Attention(C, 8, 32, R.RotaryEmbedding(32))))).double()
@@ -762,7 +755,6 @@ def test_tblock_fold_forward_and_dw_backward(dev, Fr, B, H, W):
         "dtable": rel(dtable.double(), rp.relative_attention_bias.weight.grad),
         "dWqkv": rel(dwq.double() - 0.5, ref.fn.fn.fn.to_qkv.weight.grad),
         "dWout": rel(dwo, ref.fn.fn.fn.to_out.weight.grad),
-        "dWout_inkernel": rel(dwo_k.double() - 0.5, ref.fn.fn.fn.to_out.weight.grad),
     }
     print(f"tblock fold/dw C=64 F={Fr} B={B} {H}x{W}: " + " ".join(f"{k} {v:.2e}" for k, v in errs.items()))
     for k, v in errs.items():

@@ -7,8 +7,10 @@ default kernels on the same seeded inputs (tests/knob_child.py computes both sid
   The opt-in shapes exercise its other paths: 128 / 256 channels (more than one 64-wide co block: weights streamed
   per step, the ws_decode co-block order, GroupNorm slots at cb * 16), concat inputs (x2 as the chunk source),
   Cout != Cin -- plain, with the fused residual, and with the GroupNorm-partial epilogue.
-* CESM_TF_QW=1 selects the per-wave dq kernel (tflash_bwd_qw_kernel) of the long-window attention backward, for
-  frame-major and pixel-major qkv rows (the latter is the F > 16 path's default layout).
+(Round 6 removed the other dispatch knobs and the code paths behind them: every alternative measured slower or
+neutral -- DESIGN.md §6e lists them with their A/B records.  The remaining opt-in switches are CESM_CONV_WS (here),
+CESM_CONV_STATIC (tests/test_gpu_prod_parity.py::test_conv3x3ws_dynamic_claim_bit_exact), CESM_WGRAD_STREAM (here)
+and CESM_SAMPLE_GRAPH (tests/test_gpu_sampler.py).)
 """
 import os
 import subprocess
@@ -73,40 +75,19 @@ def test_conv_ws_opt_in_shapes(dev, tmp_path, case):
         assert dm < 1e-5 and dr < 1e-5, (side["variant"], dm, dr)
 
 
-@pytest.mark.parametrize("case", sorted(c for c, (F, _, _) in KC.TF_CASES.items() if F > 16))
-def test_tflash_qw_opt_in(dev, tmp_path, case):
-    """CESM_TF_QW=1: the per-wave dq kernel against the default block kernels, frame-major and pixel-major qkv rows
-    (dq from sum P dP per wave vs D = dO . O: different summation, hence a tolerance; dk / dv and the bias-table
-    gradient come from the same kv kernel but its dS input differs by dq's rounding path)"""
-    qw = run_child(case, {"CESM_TF_QW": "1"}, tmp_path)
-    ref = KC.compute(case, dev)
-    F, HW, _ = KC.TF_CASES[case]
-    assert qw["variant"].startswith("tflash_bwd_qw_kernel"), qw["variant"]
-    assert not ref["variant"].startswith("tflash_bwd_qw_kernel"), ref["variant"]
-    for k, kt in (("dqkv", "dtable"), ("dqkv_pm", "dtable_pm")):
-        e, et = rel(qw[k].float(), ref[k].float()), rel(qw[kt], ref[kt])
-        eq = rel(qw[k][:, :256].float(), ref[k][:, :256].float())
-        print(f"{case} F={F} HW={HW} {k}: rel dqkv {e:.2e} (dq {eq:.2e}) dtable {et:.2e}")
-        assert e < 1e-2 and et < 1e-3, (k, e, et)
-        assert torch.isfinite(qw[k].float()).all()
-
-
-@pytest.mark.parametrize("case", sorted(KC.TF_CASES))
-def test_tflash_two_kernel_opt_in(dev, tmp_path, case):
-    """CESM_TF_FUSED=0: the round-2..4 two-kernel long-window backward (dq kernel + dk / dv kernel) against the default
-    one-pass fused kernel (round 5), frame-major and pixel-major qkv rows.  Both take D = dO . O at F > 16; the fused
-    kernel rounds P and dS to bf16 once per tile where the two kernels do it per kernel, hence a tolerance.  At F <= 16
-    the two-kernel form takes D = sum P dP (exact) against the fused kernel's D = dO . O from the bf16 O: the bias-table
-    gradient, a sum of dS, differs by up to ~2e-3 there (both are checked against float64 in test_gpu_kernels.py)."""
-    two = run_child(case, {"CESM_TF_FUSED": "0"}, tmp_path)
-    ref = KC.compute(case, dev)
-    F, HW, _ = KC.TF_CASES[case]
-    assert ref["variant"].startswith("tflash_bwd_fused_kernel"), ref["variant"]
-    assert not two["variant"].startswith("tflash_bwd_fused_kernel"), two["variant"]
-    for k, kt in (("dqkv", "dtable"), ("dqkv_pm", "dtable_pm")):
-        if k not in two:
-            continue
-        e, et = rel(two[k].float(), ref[k].float()), rel(two[kt], ref[kt])
-        print(f"{case} F={F} HW={HW} {k}: {two['variant']} vs {ref['variant']}: rel dqkv {e:.2e} dtable {et:.2e}")
-        assert e < 1e-2 and et < (1e-3 if F > 16 else 3e-3), (k, e, et)
-        assert torch.isfinite(ref[k].float()).all()
+@pytest.mark.parametrize("mode", ["1", "attn"])
+def test_wgrad_stream_opt_in_step(dev, tmp_path, mode):
+    """CESM_WGRAD_STREAM=1 / attn: the weight gradients on a second HIP stream give the default step's loss and every
+    gradient bit for bit (the same kernels on the same inputs, ordered after their producers), and the tensors the side
+    stream reads are released level by level (RunCtx.checkpoint) -- peak memory of the step within 10 % of the
+    default (the whole-backward keep list of round 5 would hold every level's dy / x until the end)"""
+    side = run_child("train_step", {"CESM_WGRAD_STREAM": mode}, tmp_path)
+    ref = run_child("train_step", {"CESM_WGRAD_STREAM": "0"}, tmp_path)
+    assert torch.equal(side["loss"], ref["loss"])
+    names = [k for k in ref if k.startswith("grad.")]
+    assert len(names) > 100 and sorted(names) == sorted(k for k in side if k.startswith("grad."))
+    for k in names:
+        assert torch.equal(side[k], ref[k]), k
+    ps, pr = side["peak_bytes"].item(), ref["peak_bytes"].item()
+    print(f"CESM_WGRAD_STREAM={mode}: peak {ps / 2**20:.0f} MiB vs default {pr / 2**20:.0f} MiB")
+    assert ps <= 1.10 * pr, (ps, pr)

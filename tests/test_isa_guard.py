@@ -7,8 +7,8 @@ offload bundles) and fails if packed-fp32 VALU shows up in their kernels again -
 new kernel in these files is written with explicit packed math.  Measured (hipcc -S of each source): tblock 4658 /
 tflash 2906 / attn 2485 packed-fp32 instructions with SLP, 183 / 0 / 0 without (tblock's 183 are explicit vector
 code in tw_fwd / tw_bwd, not the RoPE epilogues).  Round 4 adds explicit packed math to the softmax-gradient step of
-twh_bwd (TWH_PK) and tflash_bwd_kv (TF_PK), away from the RoPE code; those kernels get their own allowance and the
-repeatability tests (test_gpu_determinism, the full-grid F = 120 two-step test) cover them.  CPU only: no GPU
+twh_bwd and tflash_bwd_kv, away from the RoPE code; those kernels get their own allowance and the repeatability tests
+(test_gpu_determinism, the full-grid F = 120 two-step test) cover them.  CPU only: no GPU
 needed, skipped if the library is not built.
 """
 import os
@@ -26,9 +26,9 @@ PK = re.compile(r"\bv_pk_(?:fma|mul|add)_f32\b")
 FUNC = re.compile(r"^[0-9a-f]+ <(.+)>:$")
 # kernel-name markers of the three NO_SLP sources -> max packed-fp32 instructions over that source's kernels
 LIMITS = {"tblock": (re.compile(r"tw_fwd_kernel|tw_bwd_kernel|tblock_\w+_kernel"), 400),
-          "twh": (re.compile(r"twh_bwd_kernel"), 6 * 40),  # TWH_PK: 6 instantiations (NV 1-3 x DWO) x <= 40
+          "twh": (re.compile(r"twh_bwd_kernel"), 3 * 40),  # packed softmax gradient: 3 instantiations (NV 1-3) x <= 40
           "tflash": (re.compile(r"tflash_(?!bwd_kv_)\w+_kernel"), 0),
-          "tflash_kv": (re.compile(r"tflash_bwd_kv_kernel"), 640),  # TF_PK: 8 instantiations x <= 80
+          "tflash_kv": (re.compile(r"tflash_bwd_kv_kernel"), 80),  # packed softmax gradient: 1 instantiation x <= 80
           "attn": (re.compile(r"tattn_\w+_kernel|rope_table_kernel"), 0)}
 
 
