@@ -146,6 +146,36 @@ def conv_fwd_gn(x1, x2, wp, bias, geom, B, nslot):
     return y, part
 
 
+def qkv_bwd_supported(M, C):
+    return lib().cesm_qkv_bwd_streams(int(M), 768, int(C)) > 0
+
+
+def qkv_bwd(dy, x, wt, dw, accumulate=True):
+    """backward of the 768-channel qkv projection, dqkv read once (csrc/qkvbwd.hip): returns dx [..., C] (the LN
+    output's gradient); dw [768, C] fp32 (+)= dy^T x (nullable).  dy [..., 768], x [..., C] bf16 with the same rows;
+    wt [C, 768] bf16 = the weight transposed (conv_pack(w, bf16, C, 768, 1, 1, 1, 1))."""
+    C = x.shape[-1]
+    M = x.numel() // C
+    _chk(x, dtype=torch.bfloat16)
+    _chk(dy, dtype=torch.bfloat16)
+    _chk(wt, (C, 768), torch.bfloat16)
+    if dy.numel() != M * 768:
+        raise RuntimeError(f"qkv_bwd: dy has {dy.numel()} elements, expected {M} x 768")
+    ns = lib().cesm_qkv_bwd_streams(M, 768, C)
+    if ns <= 0:
+        raise ValueError(f"qkv_bwd: unsupported shape M={M} C={C}")
+    dev = x.device
+    dx = empty(x.shape, torch.bfloat16, dev)
+    slab = None
+    if dw is not None:
+        _chk(dw, dtype=torch.float32)
+        if dw.numel() != 768 * C:
+            raise RuntimeError("qkv_bwd: dw must hold 768 x C floats")
+        slab = empty(((C // 64) * ns * 768 * 64,), torch.float32, dev)
+    call("cesm_qkv_bwd", P(dy), P(x), P(wt), P(dx), P(dw), P(slab), M, 768, C, int(accumulate), S())
+    return dx
+
+
 # shape log of conv launches (set CESM_TRACE_CONV=1; tools/conv_shapes.py prints it)
 CONV_TRACE = [] if os.environ.get("CESM_TRACE_CONV") else None
 

@@ -232,6 +232,26 @@ def conv_backward(rc, spec, st, dy, need_dx=True, dres1=None, dres2=None, bias_d
     return K.conv_fwd(dy, None, wp, None, geom, res=dres1, res2=dres2, out_split=split)
 
 
+# the fused to_qkv backward only at C = 64 (the decadal window's level 0: 3.49 vs 3.75 ms per call); at C >= 128 every
+# 64-channel slice re-reads dqkv and the dgrad GEMM + wide weight-gradient pair is faster (0.84-0.95x,
+# profiles/r6c_qkv_time.txt)
+QKV_BWD_MAXC = 64
+
+
+def qkv_backward(rc, spec, st, dqkv):
+    """backward of a to_qkv projection (768 outputs, no bias) on the unfused attention paths: dn and (+=) its weight
+    gradient, with dqkv read once by the fused kernel (csrc/qkvbwd.hip, round 6) in bf16; otherwise the dgrad GEMM +
+    weight-gradient GEMM of conv_backward."""
+    n = st.x1
+    Nb, H, W, C = n.shape
+    if (n.dtype == torch.bfloat16 and C == QKV_BWD_MAXC and st.x2 is None and spec.k == 1 and spec.cout == 768
+            and spec.mod.bias is None and not spec.transposed and K.qkv_bwd_supported(Nb * H * W, C)):
+        wt = rc.packed(spec.mod.weight, C, 768, 1, 1, 1, 1)
+        dw = gbuf(spec.mod.weight)
+        return K.qkv_bwd(dqkv, n, wt, None if dw is None else dw.view(768, C))
+    return conv_backward(rc, spec, st, dqkv)
+
+
 # ============================================================================ modules
 class Residual(nn.Module):
     def __init__(self, fn):
@@ -506,7 +526,7 @@ def tattn_bwd(rc, res_mod, st, dy):
     do = conv_backward(rc, ConvSpec(attn.to_out), st.ost, dy)
     dqkv = K.tattn_bwd(st.qkv.view(-1, 768), st.o, do.view(-1, 256), st.lse, rc.bias, rc.rot, rc.dtable, rc.B,
                        rc.F, H * W, attn.scale, pixel_major=st.perm is not None)
-    dn = conv_backward(rc, ConvSpec(attn.to_qkv), st.qst, dqkv.view(Nb, H, W, 768))
+    dn = qkv_backward(rc, ConvSpec(attn.to_qkv), st.qst, dqkv.view(Nb, H, W, 768))
     return K.ln_bwd(dn, st.x, st.mr, _flat(pre.norm.gamma), gbuf(pre.norm.gamma), dres=dy, perm=st.perm)
 
 
@@ -597,7 +617,7 @@ def sla_bwd(rc, res_mod, st, dy):
         return dx
     do = conv_backward(rc, ConvSpec(sla.to_out), st.ost, dy)
     dqkv = K.sla_bwd(st.qkv.view(-1, 768), do.view(-1, 256), st.ctx, st.ml, Nb, H * W, sla.scale)
-    dn = conv_backward(rc, ConvSpec(sla.to_qkv), st.qst, dqkv.view(Nb, H, W, 768))
+    dn = qkv_backward(rc, ConvSpec(sla.to_qkv), st.qst, dqkv.view(Nb, H, W, 768))
     return K.ln_bwd(dn, st.x, st.mr, _flat(pre.norm.gamma), gbuf(pre.norm.gamma), dres=dy)
 
 

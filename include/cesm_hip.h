@@ -34,7 +34,7 @@ extern "C" {
  *   5 (round 5): cesm_abi_version() itself; cesm_conv_fwd / cesm_conv_fwd_gn gained `queue` and cesm_tblock_bwd_dw
  *     gained `dwout`, each before the hipStream_t / after dgamma;
  *   6 (round 6): cesm_tblock_bwd_dw lost `dwout` again (the in-kernel to_out weight gradient measured slower than the
- *     forward's O write and was removed). */
+ *     forward's O write and was removed); cesm_qkv_bwd / cesm_qkv_bwd_streams added. */
 #define CESM_ABI_VERSION 6
 int cesm_abi_version(void);
 /* Measurement aid, not a training op: nblk blocks that each occupy one whole CU (full LDS) for `usec` microseconds on
@@ -200,6 +200,15 @@ int cesm_tblock_bwd_dw(const void* x, const void* dy, const float* mr, const flo
                        const float* gamma, const void* wout_t, const float* bias, const float* rot, void* dx,
                        float* dwqkv, float* dgamma, float* dbias_part, float* slab, float* tmp, void* wimg,
                        int nblk, int B, int F, int HW, int C, float scale, int accumulate, hipStream_t stream);
+/* Backward of the 768-channel qkv projection with dqkv read once (csrc/qkvbwd.hip, round 6): dx = dy . W (the LN
+ * output's gradient, written) and dw (+)= dy^T . x in one pass -- replaces the dgrad GEMM + wide weight-gradient GEMM
+ * pair of video_net.py:380-381 / :322-323 (to_qkv) on the unfused attention paths (long windows F > 16, C >= 256).
+ * dy [M][768] bf16, x [M][C] bf16 (C = 64 .. 512, C % 64 == 0), wt [C][768] bf16 (wt[c][n] = W[n][c]), dx [M][C] bf16,
+ * dw [768][C] fp32 (nullable), slab (C / 64) * streams * 768 * 64 floats with streams = cesm_qkv_bwd_streams (0 =
+ * unsupported shape).  Rows may be in any order (pixel- or frame-major) as long as dy, x and dx agree. */
+int cesm_qkv_bwd_streams(int64_t M, int N, int C);
+int cesm_qkv_bwd(const void* dy, const void* x, const void* wt, void* dx, float* dw, float* slab, int64_t M, int N,
+                 int C, int accumulate, hipStream_t stream);
 /* spatial linear attention core (video_net.py:335-345 between to_qkv and to_out) */
 int cesm_sla_nchunk(int HW);
 int cesm_sla_fwd(int dtype, const void* qkv, void* out, float* ctx, float* ml, float* ws, int Nf, int HW, float scale,

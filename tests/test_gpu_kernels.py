@@ -125,6 +125,40 @@ def test_wgrad_fused_bias(dev, cin, cout, k, st):
     assert torch.equal(dw1, dw2)
 
 
+@pytest.mark.parametrize("M,C", [(64, 64), (1000, 64), (40 * 77, 64), (6912 * 2 + 17, 128), (3000, 256), (777, 512)])
+def test_qkv_bwd_fused(dev, M, C):
+    """cesm_qkv_bwd (csrc/qkvbwd.hip: dqkv read once for dx and dW of the 768-channel to_qkv projection) against a
+    float64 evaluation on the bf16-rounded operands and against the two-GEMM path it replaces (1x1 dgrad conv + wide
+    weight-gradient GEMM); partial 64-pixel tiles, fewer tiles than streams (padding streams, zero slabs), every
+    C slice count; dW accumulates (+=) and both outputs repeat bit for bit"""
+    torch.manual_seed(M + C)
+    dy = torch.randn(M, 768, device=dev).to(torch.bfloat16)
+    x = torch.randn(M, C, device=dev).to(torch.bfloat16)
+    w = torch.randn(768, C, 1, 1, 1, device=dev) * C ** -0.5
+    wt = K.conv_pack(w, torch.bfloat16, C, 768, 1, 1, 1, 1)
+    assert K.qkv_bwd_supported(M, C)
+    dw = torch.full((768, C), 0.5, device=dev)
+    dx = K.qkv_bwd(dy, x, wt, dw)
+    dw2 = torch.full((768, C), 0.5, device=dev)
+    dx2 = K.qkv_bwd(dy, x, wt, dw2)
+    torch.cuda.synchronize()
+    assert torch.equal(dx, dx2) and torch.equal(dw, dw2)
+    wq = w.reshape(768, C).to(torch.bfloat16).double()
+    ref_dx = dy.double() @ wq
+    ref_dw = dy.double().t() @ x.double()
+    e_dx, e_dw = rel(dx, ref_dx), rel(dw - 0.5, ref_dw)
+    # the path it replaces: dgrad 1x1 conv (gemm1x1) + conv_wgrad
+    dx_ref = K.conv_fwd(dy.view(1, 1, M, 768), None, wt, None, (1, M, C, 1, 1, 1, 0, 1)).view(M, C)
+    dw_ref = torch.zeros(768, C, 1, 1, 1, device=dev)
+    K.conv_wgrad(x.view(1, 1, M, C), None, dy.view(1, 1, M, 768), None, dw_ref, (1, M, 768, 1, 1, 1, 0, 1), 0, 0)
+    e_old_dx, e_old_dw = rel(dx, dx_ref), rel(dw - 0.5, dw_ref.view(768, C))
+    print(f"qkv_bwd M={M} C={C}: dx {e_dx:.2e} dW {e_dw:.2e} vs float64; vs the two-GEMM path dx {e_old_dx:.2e} "
+          f"dW {e_old_dw:.2e}")
+    assert e_dx < 4e-3 and e_dw < 1e-5, (e_dx, e_dw)
+    assert e_old_dx < 4e-3 and e_old_dw < 1e-5, (e_old_dx, e_old_dw)
+    assert K.qkv_bwd(dy, x, wt, None).equal(dx)  # no weight gradient: the same dx
+
+
 @pytest.mark.parametrize("H,W,cin,cout", [(12, 72, 64, 64), (8, 36, 128, 64), (6, 36, 64, 128), (10, 36, 256, 512), (20, 64, 128, 64)])
 def test_conv3x3_tile_shapes_bf16(dev, H, W, cin, cout):
     """widths that are multiples of 36 take the 36-wide halo tiles (fwd/dgrad) and the 8 x 36 weight-
