@@ -174,14 +174,15 @@ class KernelProbe:
             return f"tw_fwd_kernel<{C},{nv},true>", v * tw_core_flop(C, F), float(b)
 
         def tblock_bwd_dw(x, dy, mr, lse, wqkv_f32, gamma, wout_t, bias, rot, dwqkv, dgamma, dtable, B, F, scale,
-                          num_buckets=32, max_distance=32):
+                          num_buckets=32, max_distance=32, emit_o=False):
             Nb, H, W, C = x.shape
             v = Nb * H * W
             nv = (4 * F + 15) // 16
             # dgrad-equivalent work (the forward's FLOPs) + the in-kernel to_qkv weight gradient (2 * 768 * C per
-            # voxel); bytes: x, dy, mr / lse read, dx written (no per-voxel intermediates)
+            # voxel; the O = P V recompute of emit_o is not counted); bytes: x, dy, mr / lse read, dx (and O) written
             return (f"twh_bwd_kernel<{nv}> (+ dW / dgamma / dbias reductions)",
-                    v * (tw_core_flop(C, F) + 2.0 * 768 * C), float(v * (3 * C * 2 + 40)))
+                    v * (tw_core_flop(C, F) + 2.0 * 768 * C),
+                    float(v * (3 * C * 2 + 40 + (512 if emit_o else 0))))
 
         def tattn_fwd(qkv, bias, rot, B, F, HW, scale, save=True, pixel_major=False):
             v = B * F * HW

@@ -273,18 +273,39 @@ __global__ void frag_image_f32_kernel(const float* __restrict__ W, const float* 
 
 // slab [nblk][J][C] (dW' partials) -> dW (+)= (sum_blk slab) diag(gamma); tmp[j][c] = W[j][c] * sum_blk slab.
 // Rows j < nq were computed against weights carrying qscale (frag_image_f32_kernel): their sums are scaled back.
-__global__ void twh_dw_reduce_kernel(const float* __restrict__ slab, int nblk, const float* __restrict__ w,
-                                     const float* __restrict__ gamma, float* __restrict__ dw, float* __restrict__ tmp,
-                                     int J, int C, int accumulate, int nq = 0, float qscale = 1.f) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (e >= (int64_t)J * C) return;
+// Block = 64 elements x 4 slab groups (k = grp mod 4, 8 loads in flight per lane), combined in a fixed order (round 6:
+// one element per thread kept too few loads in flight, 64 us for the 50 MB of a level-0 call)
+constexpr int TWH_RED_G = 4;
+__global__ __launch_bounds__(256) void twh_dw_reduce_kernel(const float* __restrict__ slab, int nblk,
+                                                            const float* __restrict__ w, const float* __restrict__ gamma,
+                                                            float* __restrict__ dw, float* __restrict__ tmp, int J,
+                                                            int C, int accumulate, int nq = 0, float qscale = 1.f) {
+  const int64_t JC = (int64_t)J * C;
+  const int64_t e = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+  const int grp = threadIdx.x >> 6;
   float s = 0.f;
-  for (int k = 0; k < nblk; ++k) s += slab[(int64_t)k * J * C + e];
+  if (e < JC) {
+    int k = grp;
+    for (; k + 7 * TWH_RED_G < nblk; k += 8 * TWH_RED_G) {
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = slab[(int64_t)(k + i * TWH_RED_G) * JC + e];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += v[i];
+    }
+    for (; k < nblk; k += TWH_RED_G) s += slab[(int64_t)k * JC + e];
+  }
+  __shared__ float red[TWH_RED_G][64];
+  red[grp][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (grp != 0 || e >= JC) return;
+  s = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
   if (e / C < nq) s *= qscale;
   const int c = (int)(e % C);
   if (dw) dw[e] = (accumulate ? dw[e] : 0.f) + s * gamma[c];
   tmp[e] = s * w[e];
 }
+static inline unsigned twh_dw_reduce_grid(int64_t nel) { return (unsigned)((nel + 63) / 64); }
 // dgamma[c] (+)= sum_j tmp[j][c]
 __global__ void twh_dgamma_kernel(const float* __restrict__ tmp, float* __restrict__ dgamma, int J, int C,
                                   int accumulate) {

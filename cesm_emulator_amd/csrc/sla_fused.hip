@@ -1630,7 +1630,7 @@ int cesm_slaf_bwd_dw(const void* x, const void* dy, const float* gamma_one, cons
                                                   (const bf16*)actT, (const bf16*)actx, (const bf16*)adc,
                                                   (const bf16*)adcT, (bf16*)dx, slab, Nf, HW, scale, eps);
   const int64_t nel = (int64_t)768 * C;
-  twh_dw_reduce_kernel<<<(unsigned)cdiv(nel, 256), 256, 0, stream>>>(slab, nblk_dx, wqkv_f32, gamma, dwqkv, tmp, 768,
+  twh_dw_reduce_kernel<<<twh_dw_reduce_grid(nel), 256, 0, stream>>>(slab, nblk_dx, wqkv_f32, gamma, dwqkv, tmp, 768,
                                                                     C, accumulate);
   if (dgamma) twh_dgamma_kernel<<<C, 256, 0, stream>>>(tmp, dgamma, 768, C, accumulate);
   return cesm_launch_status();

@@ -1741,8 +1741,8 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ dy, const float* __restrict__ mr,
     const float* __restrict__ lse, const bf16* __restrict__ wqkv, const bf16* __restrict__ wqkv_t,
     const bf16* __restrict__ wout_t, const float* __restrict__ bias, const float* __restrict__ rotg,
-    bf16* __restrict__ dx, float* __restrict__ dw_slab, float* __restrict__ dbias_part, int B, int F, int HW,
-    float scale) {
+    bf16* __restrict__ dx, bf16* __restrict__ o_out, float* __restrict__ dw_slab, float* __restrict__ dbias_part,
+    int B, int F, int HW, float scale) {
   constexpr int C = 64;
   using T = TW<C, NV>;
   constexpr int R = NV * 16;
@@ -2015,6 +2015,28 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
           dvt[u][half] = mfma_k16(kslot4_hld(sdo, rb, half * 16, lane), p_b, z4);   // dV^T[d][j]
         }
       }
+      // O^T[d][i] = V^T . P^T of these pixels (o_out: the to_out weight gradient's input, round 6), stored straight
+      // away (8 B per lane and half).  Parking it in the pixels' dead dO rows and storing it after the dW or the dxn
+      // GEMM measured slower (3884-4325 vs 3696-3992 us per level-0 call: 23-45 more spilled registers,
+      // profiles/r6g_twh_o_ab.txt)
+      if (o_out) {  // uniform
+#pragma unroll
+        for (int u = 0; u < PG; ++u) {
+          f32x4 ot[2];
+#pragma unroll
+          for (int half = 0; half < 2; ++half) ot[half] = mfma_k16(kslot4_hld(sv, (pp0 + u) * F, half * 16, lane), pa_b[u], z4);
+          if (lr < F && p0 + pp0 + u < HW) {
+            bf16* orow = o_out + (((int64_t)b * F + lr) * HW + p0 + pp0 + u) * INNER + h * DH + lg * 4;
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+              bf16x4 o4;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) o4[r] = (bf16)ot[half][r];
+              __builtin_nontemporal_store(__builtin_bit_cast(uint64_t, o4), reinterpret_cast<uint64_t*>(orow + half * 16));
+            }
+          }
+        }
+      }
       wave_lds_sync();  // all reads of these pixels' rows (and the tiles) done before they are overwritten
 #pragma unroll
       for (int u = 0; u < PG; ++u) {
@@ -2269,14 +2291,16 @@ int cesm_tblock_fwd_fold(const void* x, const float* gamma, const float* wqkv_f3
 }
 
 // Head-parallel fused backward of the temporal-attention block with in-kernel weight gradients (C = 64,
-// 4F <= 48; the forward must be cesm_tblock_fwd_fold's).  dx [B*F*HW][C]; dwqkv (+)= dW_qkv [768][C] and
+// 4F <= 48; the forward must be cesm_tblock_fwd_fold's).  dx [B*F*HW][C]; o (nullable) [B*F*HW][256] the attention
+// output recomputed from the backward's P (the to_out weight gradient's input); dwqkv (+)= dW_qkv [768][C] and
 // dgamma (+)= the LN gamma gradient (each nullable); dbias_part [8][nblk][F][F] (cesm_relpos_bwd with
 // B = 1).  Workspaces: slab nblk*768*C floats, tmp 768*C floats, wimg (2*768 + 256)*C bf16.
 int cesm_tblock_bwd_dw(const void* x, const void* dy, const float* mr, const float* lse, const float* wqkv_f32,
-                       const float* gamma, const void* wout_t, const float* bias, const float* rot, void* dx,
+                       const float* gamma, const void* wout_t, const float* bias, const float* rot, void* dx, void* o,
                        float* dwqkv, float* dgamma, float* dbias_part, float* slab, float* tmp, void* wimg,
                        int nblk, int B, int F, int HW, int C, float scale, int accumulate, hipStream_t stream) {
   if (nblk < 1 || nblk != cesm_tblock_bwd_dw_nblk(B, F, HW, C)) return CESM_EUNSUPPORTED;
+  if (o && (int64_t)F * HW * INNER >= ((int64_t)1 << 31)) return CESM_EUNSUPPORTED;  // 32-bit O row offsets per sample
   bf16* iq = (bf16*)wimg;
   bf16* iqt = iq + 768 * C;
   bf16* iot = iqt + 768 * C;
@@ -2290,7 +2314,7 @@ int cesm_tblock_bwd_dw(const void* x, const void* dy, const float* mr, const flo
 #define TWH_LAUNCH(NVv)                                                                                           \
   allow_smem(twh_bwd_kernel<NVv>, sm);                                                                            \
   twh_bwd_kernel<NVv><<<nblk, 512, sm, stream>>>((const bf16*)x, (const bf16*)dy, mr, lse, iq, iqt, iot, bias, rot, \
-                                                 (bf16*)dx, slab, dbias_part, B, F, HW, scale)
+                                                 (bf16*)dx, (bf16*)o, slab, dbias_part, B, F, HW, scale)
   switch (nv) {
     case 1: TWH_LAUNCH(1); break;
     case 2: TWH_LAUNCH(2); break;
@@ -2299,7 +2323,7 @@ int cesm_tblock_bwd_dw(const void* x, const void* dy, const float* mr, const flo
   }
 #undef TWH_LAUNCH
   const int64_t nel = (int64_t)768 * C;
-  twh_dw_reduce_kernel<<<(unsigned)cdiv(nel, 256), 256, 0, stream>>>(slab, nblk, wqkv_f32, gamma, dwqkv, tmp, 768, C,
+  twh_dw_reduce_kernel<<<twh_dw_reduce_grid(nel), 256, 0, stream>>>(slab, nblk, wqkv_f32, gamma, dwqkv, tmp, 768, C,
                                                                     accumulate, INNER, scale);
   if (dgamma) twh_dgamma_kernel<<<C, 256, 0, stream>>>(tmp, dgamma, 768, C, accumulate);
   return cesm_launch_status();

@@ -505,10 +505,12 @@ def tblock_fwd_fold(x, gamma, wqkv_f32, wout, bias, rot, B, F, scale, save=True,
 
 
 def tblock_bwd_dw(x, dy, mr, lse, wqkv_f32, gamma, wout_t, bias, rot, dwqkv, dgamma, dtable, B, F, scale,
-                  num_buckets=32, max_distance=32):
+                  num_buckets=32, max_distance=32, emit_o=False):
     """head-parallel fused temporal-block backward with in-kernel weight gradients (C = 64, 4F <= 48):
-    returns dx; dwqkv (+)= the to_qkv weight gradient, dgamma (+)= the LN gamma gradient, dtable (+)= the
-    rel-pos table gradient (each nullable).  The forward must be tblock_fwd_fold's."""
+    returns dx, or (dx, o) with emit_o -- o [Nb, H, W, 256] the attention output recomputed from the backward's P,
+    the to_out weight gradient's input (the forward then writes none); dwqkv (+)= the to_qkv weight gradient,
+    dgamma (+)= the LN gamma gradient, dtable (+)= the rel-pos table gradient (each nullable).  The forward must
+    be tblock_fwd_fold's."""
     Nb, H, W, C = x.shape
     HW = H * W
     _chk(x, dtype=torch.bfloat16)
@@ -525,16 +527,17 @@ def tblock_bwd_dw(x, dy, mr, lse, wqkv_f32, gamma, wout_t, bias, rot, dwqkv, dga
         raise ValueError(f"tblock_bwd_dw: unsupported shape C={C} F={F}")
     dev = x.device
     dx = empty(x.shape, x.dtype, dev)
+    o = empty((Nb, H, W, 256), x.dtype, dev) if emit_o else None
     dbp = empty((8, nblk, F, F), torch.float32, dev)
     slab = empty((nblk * 768 * C,), torch.float32, dev)
     tmp = empty((768, C), torch.float32, dev)
     wimg = empty(((2 * 768 + 256) * C,), torch.bfloat16, dev)
     call("cesm_tblock_bwd_dw", P(x), P(dy), P(mr), P(lse), P(wqkv_f32), P(gamma), P(wout_t), P(bias), P(rot), P(dx),
-         P(dwqkv), P(dgamma), P(dbp), P(slab), P(tmp), P(wimg), nblk, B, F, HW, C, float(scale), 1, S())
+         P(o), P(dwqkv), P(dgamma), P(dbp), P(slab), P(tmp), P(wimg), nblk, B, F, HW, C, float(scale), 1, S())
     if dtable is not None:
         ws = empty((8, F, F), torch.float32, dev)
         call("cesm_relpos_bwd", P(dbp), nblk, 1, P(dtable), P(ws), F, 8, num_buckets, max_distance, 1, S())
-    return dx
+    return (dx, o) if emit_o else dx
 
 
 # fused SLA at C = 64 and 128 (measured +0.8 % step throughput for C = 128 with the parallel context

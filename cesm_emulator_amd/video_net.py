@@ -432,9 +432,10 @@ def _tblock_fused(rc, C):
     return rc.cdt == torch.bfloat16 and rc.F <= 16 and C in K.TBLOCK_C and C <= FUSED_TBLOCK_MAXC
 
 
-# head-parallel backward with in-kernel weight gradients (C = 64, F <= 12): no 768-channel dqkv round trip.  The forward
-# saves O for a wide to_out weight-gradient GEMM with dy (the in-kernel to_out gradient measured slower, round 5: 32 more
-# accumulators took twh_bwd from 9 to 58-93 spilled registers and 3.3 to 5.3 ms per level-0 call; removed in round 6).
+# head-parallel backward with in-kernel weight gradients (C = 64, F <= 12): no 768-channel dqkv round trip.  The
+# backward recomputes O = P V from its own P and writes it for a wide to_out weight-gradient GEMM with dy (round 6: the
+# forward's O write cost 477 us of a 1892 us level-0 call, tools/fwd_o_cost.py; the in-kernel to_out gradient measured
+# slower, round 5: 32 more accumulators took twh_bwd from 9 to 58-93 spilled registers and 3.3 to 5.3 ms per call).
 def _tblock_dw(rc, x):
     Nb, H, W, C = x.shape
     return _tblock_fused(rc, C) and K.tblock_bwd_dw_supported(rc.B, rc.F, H * W, C)
@@ -464,11 +465,11 @@ def tattn_fwd(rc, res_mod, x):
         return K.conv_fwd(v, None, wo, None, (H, W, C, 1, 1, 1, 0, 1), res=x), None
     if _tblock_dw(rc, x):
         # gamma folded into the QKV weights (images built from the fp32 master weight); the backward computes
-        # the to_qkv and gamma gradients in-kernel, the to_out gradient from the saved O.
+        # the to_qkv and gamma gradients in-kernel, and O for the to_out gradient.
         wo = rc.packed(attn.to_out.weight, C, 256, 1, 1, 0, 0)
-        y, mr, lse, o = K.tblock_fwd_fold(x, _flat(pre.norm.gamma), attn.to_qkv.weight, wo, rc.bias, rc.rot, rc.B,
-                                          rc.F, attn.scale, save=rc.save, eps=pre.norm.eps, save_o=rc.save)
-        st = SimpleNamespace(fused=True, fold=True, x=x, mr=mr, lse=lse, o=o) if rc.save else None
+        y, mr, lse, _ = K.tblock_fwd_fold(x, _flat(pre.norm.gamma), attn.to_qkv.weight, wo, rc.bias, rc.rot, rc.B,
+                                          rc.F, attn.scale, save=rc.save, eps=pre.norm.eps, save_o=False)
+        st = SimpleNamespace(fused=True, fold=True, x=x, mr=mr, lse=lse) if rc.save else None
         return y, st
     if _tblock_fused(rc, C):
         wq = rc.packed(attn.to_qkv.weight, 768, C, 1, 1, 0, 0)
@@ -500,11 +501,14 @@ def tattn_bwd(rc, res_mod, st, dy):
     if st.fused and st.fold:
         wo_t = rc.packed(attn.to_out.weight, 256, C, 1, 1, 1, 1)
         dwo = gbuf(attn.to_out.weight)
-        dx = K.tblock_bwd_dw(st.x, dy, st.mr, st.lse, attn.to_qkv.weight, _flat(pre.norm.gamma), wo_t, rc.bias, rc.rot,
-                             gbuf(attn.to_qkv.weight), _gflat(pre.norm.gamma), rc.dtable, rc.B, rc.F, attn.scale)
-        if dwo is not None:
-            with rc.side(st.o, dy, attn=True):
-                K.conv_wgrad(st.o, None, dy, None, dwo, (H, W, C, 1, 1, 1, 0, 1), 0, 0)
+        r = K.tblock_bwd_dw(st.x, dy, st.mr, st.lse, attn.to_qkv.weight, _flat(pre.norm.gamma), wo_t, rc.bias, rc.rot,
+                            gbuf(attn.to_qkv.weight), _gflat(pre.norm.gamma), rc.dtable, rc.B, rc.F, attn.scale,
+                            emit_o=dwo is not None)
+        if dwo is None:
+            return r
+        dx, o = r
+        with rc.side(o, dy, attn=True):
+            K.conv_wgrad(o, None, dy, None, dwo, (H, W, C, 1, 1, 1, 0, 1), 0, 0)
         return dx
     if st.fused:
         wq = rc.packed(attn.to_qkv.weight, 768, C, 1, 1, 0, 0)

@@ -34,7 +34,8 @@ extern "C" {
  *   5 (round 5): cesm_abi_version() itself; cesm_conv_fwd / cesm_conv_fwd_gn gained `queue` and cesm_tblock_bwd_dw
  *     gained `dwout`, each before the hipStream_t / after dgamma;
  *   6 (round 6): cesm_tblock_bwd_dw lost `dwout` again (the in-kernel to_out weight gradient measured slower than the
- *     forward's O write and was removed); cesm_qkv_bwd / cesm_qkv_bwd_streams added. */
+ *     forward's O write and was removed) and gained `o` after dx (O emitted by the backward);
+ *     cesm_qkv_bwd / cesm_qkv_bwd_streams added. */
 #define CESM_ABI_VERSION 6
 int cesm_abi_version(void);
 /* Measurement aid, not a training op: nblk blocks that each occupy one whole CU (full LDS) for `usec` microseconds on
@@ -188,8 +189,9 @@ int cesm_tblock_bwd(const void* x, const void* dy, const float* gamma, const flo
  * master weight [768][C]; wimg (768 + 256) * C bf16); cesm_tblock_bwd_dw is its backward: dx, and
  * dwqkv (+)= dW_qkv, dgamma (+)= the LN gamma gradient (nullable) without the 768-channel dqkv / xn
  * intermediates; dbias_part [8][nblk][F][F] (cesm_relpos_bwd, B = 1); slab nblk*768*C and tmp 768*C floats,
- * wimg (2*768 + 256) * C bf16; nblk from cesm_tblock_bwd_dw_nblk (0 = unsupported shape).  The to_out weight
- * gradient comes from the O the forward wrote (o) and a wide weight-gradient GEMM.
+ * wimg (2*768 + 256) * C bf16; nblk from cesm_tblock_bwd_dw_nblk (0 = unsupported shape).  o (nullable) receives the
+ * attention output O [..][256] bf16 recomputed from the backward's P (round 6: the forward then writes no O), the input
+ * of the to_out weight gradient's wide GEMM.
  * Replaces video_net.py:368-454 (Attention) + :90-98 (PreNorm LN) + :69-75 (Residual) and the
  * to_qkv / to_out weight gradients of its backward. */
 int cesm_tblock_bwd_dw_nblk(int B, int F, int HW, int C);
@@ -197,7 +199,7 @@ int cesm_tblock_fwd_fold(const void* x, const float* gamma, const float* wqkv_f3
                          const float* bias, const float* rot, void* y, float* mr, float* lse, void* o, void* wimg,
                          int B, int F, int HW, int C, float scale, float eps, hipStream_t stream);
 int cesm_tblock_bwd_dw(const void* x, const void* dy, const float* mr, const float* lse, const float* wqkv_f32,
-                       const float* gamma, const void* wout_t, const float* bias, const float* rot, void* dx,
+                       const float* gamma, const void* wout_t, const float* bias, const float* rot, void* dx, void* o,
                        float* dwqkv, float* dgamma, float* dbias_part, float* slab, float* tmp, void* wimg,
                        int nblk, int B, int F, int HW, int C, float scale, int accumulate, hipStream_t stream);
 /* Backward of the 768-channel qkv projection with dqkv read once (csrc/qkvbwd.hip, round 6): dx = dy . W (the LN

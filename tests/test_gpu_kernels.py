@@ -769,9 +769,14 @@ def test_tblock_fold_forward_and_dw_backward(dev, Fr, B, H, W):
     dgamma = torch.full((C,), 0.25, device=dev)   # accumulates (+=)
     dtable = torch.zeros(32, 8, device=dev)
     dwq = torch.full((768, C), 0.5, device=dev)   # accumulates (+=)
-    dx = K.tblock_bwd_dw(xd, gd, mr, lse, wqkv, gamma, wo_t, rc.bias, rc.rot, dwq, dgamma, dtable, B, Fr, attn.scale)
+    dx, ob = K.tblock_bwd_dw(xd, gd, mr, lse, wqkv, gamma, wo_t, rc.bias, rc.rot, dwq, dgamma, dtable, B, Fr,
+                             attn.scale, emit_o=True)
+    # the O emission (round 6: the backward recomputes O = P V for the to_out weight gradient) leaves dx unchanged
+    dx2 = K.tblock_bwd_dw(xd, gd, mr, lse, wqkv, gamma, wo_t, rc.bias, rc.rot, None, None, None, B, Fr, attn.scale)
     torch.cuda.synchronize()
-    dwo = gd.reshape(-1, C).double().t() @ o.reshape(-1, 256).double()
+    assert torch.equal(dx, dx2)
+    # the to_out weight gradient from the backward's O (what the training path uses)
+    dwo = gd.reshape(-1, C).double().t() @ ob.reshape(-1, 256).double()
     from oracle import ref_cpu as R
     ref = R.Residual(R.PreNorm(C, R.EinopsToAndFrom(R.Attention(C, 8, 32, R.RotaryEmbedding(32))))).double()
     ref.fn.norm.gamma.data.copy_(gamma.cpu().double().view_as(ref.fn.norm.gamma))
@@ -789,10 +794,13 @@ def test_tblock_fold_forward_and_dw_backward(dev, Fr, B, H, W):
         "dtable": rel(dtable.double(), rp.relative_attention_bias.weight.grad),
         "dWqkv": rel(dwq.double() - 0.5, ref.fn.fn.fn.to_qkv.weight.grad),
         "dWout": rel(dwo, ref.fn.fn.fn.to_out.weight.grad),
+        # O from the backward's P vs the forward's O (both bf16 P . V): rounding-level only
+        "O_bwd_vs_fwd": rel(ob.double(), o.double()),
     }
     print(f"tblock fold/dw C=64 F={Fr} B={B} {H}x{W}: " + " ".join(f"{k} {v:.2e}" for k, v in errs.items()))
     for k, v in errs.items():
         assert v < 3e-2, (k, v)
+    assert errs["O_bwd_vs_fwd"] < 1e-2
 
 
 @pytest.mark.parametrize("H,W", [(8, 8), (12, 20), (37, 29), (48, 96)])
