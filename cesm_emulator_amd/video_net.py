@@ -426,6 +426,9 @@ def resnet_bwd(rc, rb, st, dout):
 # costs (HBM); above it the level is small and the unfused GEMMs are cheaper than per-pixel-group
 # weight re-reads (C = 256 / 512: unfused measured faster, rounds 1-2)
 FUSED_TBLOCK_MAXC = 128
+# widest C whose fused temporal forward writes O for the to_out weight gradient; above it the fused backward emits O
+# (round 6 A/B at C = 128: profiles/r6i_*)
+TBLOCK_FWD_O_MAXC = 256
 
 
 def _tblock_fused(rc, C):
@@ -475,7 +478,7 @@ def tattn_fwd(rc, res_mod, x):
         wq = rc.packed(attn.to_qkv.weight, 768, C, 1, 1, 0, 0)
         wo = rc.packed(attn.to_out.weight, C, 256, 1, 1, 0, 0)
         # training: the forward also writes O (to_out's input) so the backward does not emit it
-        save_o = rc.save and C <= 256
+        save_o = rc.save and C <= TBLOCK_FWD_O_MAXC
         y, mr, lse, o = K.tblock_fwd(x, _flat(pre.norm.gamma), wq, wo, rc.bias, rc.rot, rc.B, rc.F, attn.scale,
                                      save=rc.save, eps=pre.norm.eps, save_o=save_o)
         st = SimpleNamespace(fused=True, fold=False, x=x, mr=mr, lse=lse, o=o) if rc.save else None
