@@ -2981,25 +2981,76 @@ __global__ void conv_pack_kernel(const float* __restrict__ src, T* __restrict__ 
 }
 
 // batched repack after an optimizer step: job j = int64[8] {src, dst, Cout, Cin, KH, KW, swap, flip};
-// blockIdx.y = job, grid-stride over its elements in x (one launch for every cached pack)
+// One launch for every cached pack.  jobs: njobs rows of 8 int64 (src, dst, Cout, Cin, KH, KW, swap, flip), then njobs + 1
+// block starts (the exclusive prefix of the per-job tile counts), then the job index of every block.  A block takes one
+// (co, ci) tile of a job -- pb_co_t(T) output rows x 64 input channels x all T taps: it reads the tile's source runs
+// contiguously (co-major rows of Cin*T floats, or ci-major rows of Cout*T when swap), transposes through LDS and writes
+// dst[co][tap][ci] in 64-channel runs.  (Round 6: blockIdx.y = job with a fixed 512 blocks each dispatched ~92 k mostly
+// empty blocks and gathered every element with a stride-T read -- 309 us per optimizer step.)
+constexpr int PB_CI = 64;
+constexpr int PB_TILE = 4096;  // floats of LDS per tile
+__host__ __device__ inline int pb_co_t(int T) { const int c = PB_TILE / (T * PB_CI); return c < 1 ? 1 : (c > 64 ? 64 : c); }
+// one (co, ci) tile; NTC = the tap count when known at compile time (1, 9, 16), else 0 (runtime NT)
+template <typename T, int NTC>
+__device__ __forceinline__ void pb_tile(float* tile, const float* __restrict__ src, T* __restrict__ dst, int Cout, int Cin,
+                                        int NTr, int swap, int flip, int co0, int ci0, int nco, int ncc) {
+  const int NT = NTC ? NTC : NTr;
+  const int run = swap ? nco * NT : ncc * NT;  // contiguous source floats per outer index
+  const int nld = (swap ? ncc : nco) * run;
+  float v[PB_TILE / 256];
+#pragma unroll
+  for (int u = 0; u < PB_TILE / 256; ++u) {  // every load of the tile issued before the LDS writes
+    const int q = u * 256 + (int)threadIdx.x;
+    const int qq = q < nld ? q : 0;
+    const int o = qq / run, r = qq - o * run;
+    const int inner = r / NT, t = r - inner * NT;
+    const int co_l = swap ? inner : o, ci_l = swap ? o : inner;
+    v[u] = src[swap ? ((ci0 + ci_l) * Cout + co0 + co_l) * NT + t : ((co0 + co_l) * Cin + ci0 + ci_l) * NT + t];
+  }
+#pragma unroll
+  for (int u = 0; u < PB_TILE / 256; ++u) {
+    const int q = u * 256 + (int)threadIdx.x;
+    if (q < nld) {
+      const int o = q / run, r = q - o * run;
+      const int inner = r / NT, t = r - inner * NT;
+      const int co_l = swap ? inner : o, ci_l = swap ? o : inner;
+      tile[(co_l * NT + t) * PB_CI + ci_l] = v[u];
+    }
+  }
+  __syncthreads();
+  // store: dst[co][td][ci], 64-channel runs; flip reads the source tap NT - 1 - td
+  const int nst = nco * NT * PB_CI;
+#pragma unroll
+  for (int u = 0; u < PB_TILE / 256; ++u) {
+    const int q = u * 256 + (int)threadIdx.x;
+    const int ci_l = q & (PB_CI - 1), ct = q / PB_CI, co_l = ct / NT, td = ct - co_l * NT;
+    if (q < nst && ci_l < ncc) {
+      const int ts = flip ? NT - 1 - td : td;
+      dst[((int64_t)(co0 + co_l) * NT + td) * Cin + ci0 + ci_l] = from_f<T>(tile[(co_l * NT + ts) * PB_CI + ci_l]);
+    }
+  }
+}
 template <typename T>
-__global__ void conv_pack_batch_kernel(const int64_t* __restrict__ jobs) {
-  const int64_t* jb = jobs + (int64_t)blockIdx.y * 8;
-  const float* src = reinterpret_cast<const float*>(jb[0]);
-  T* dst = reinterpret_cast<T*>(jb[1]);
-  const int Cout = (int)jb[2], Cin = (int)jb[3], KH = (int)jb[4], KW = (int)jb[5], swap = (int)jb[6], flip = (int)jb[7];
-  // 32-bit index math (a weight has < 2^31 elements, checked on the host): the 64-bit divisions per element
-  // made this a 0.37 ms launch per optimizer step
-  const int K = KH * KW * Cin;
-  const int total = Cout * K;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
-    const int co = e / K;
-    const int kc = e - co * K;
-    const int tap = kc / Cin, ci = kc - tap * Cin;
-    int ky = tap / KW, kx = tap - ky * KW;
-    if (flip) { ky = KH - 1 - ky; kx = KW - 1 - kx; }
-    const int d0 = swap ? ci : co, d1 = swap ? co : ci, D1 = swap ? Cout : Cin;
-    dst[e] = from_f<T>(src[((d0 * D1 + d1) * KH + ky) * KW + kx]);
+__global__ __launch_bounds__(256) void conv_pack_batch_kernel(const int64_t* __restrict__ jobs, int njobs) {
+  __shared__ float tile[PB_TILE];
+  const int64_t* start = jobs + (int64_t)njobs * 8;
+  const int64_t nblocks = start[njobs];
+  const int64_t* bjob = start + njobs + 1;  // job of every block (one load, not a search)
+  for (int64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+    const int lo = (int)bjob[b];
+    const int64_t* jb = jobs + (int64_t)lo * 8;
+    const float* src = reinterpret_cast<const float*>(jb[0]);
+    T* dst = reinterpret_cast<T*>(jb[1]);
+    const int Cout = (int)jb[2], Cin = (int)jb[3], NT = (int)(jb[4] * jb[5]), swap = (int)jb[6], flip = (int)jb[7];
+    const int cot = pb_co_t(NT), nci = (Cin + PB_CI - 1) / PB_CI;
+    const int lb = (int)(b - start[lo]);
+    const int co0 = (lb / nci) * cot, ci0 = (lb % nci) * PB_CI;
+    const int nco = min(cot, Cout - co0), ncc = min(PB_CI, Cin - ci0);
+    __syncthreads();  // the previous tile's LDS reads are done
+    if (NT == 9) pb_tile<T, 9>(tile, src, dst, Cout, Cin, NT, swap, flip, co0, ci0, nco, ncc);
+    else if (NT == 1) pb_tile<T, 1>(tile, src, dst, Cout, Cin, NT, swap, flip, co0, ci0, nco, ncc);
+    else if (NT == 16) pb_tile<T, 16>(tile, src, dst, Cout, Cin, NT, swap, flip, co0, ci0, nco, ncc);
+    else pb_tile<T, 0>(tile, src, dst, Cout, Cin, NT, swap, flip, co0, ci0, nco, ncc);
   }
 }
 
@@ -3890,13 +3941,13 @@ int cesm_conv_pack(int dtype, const float* w, void* wp, int Cout, int Cin, int K
   return cesm_launch_status();
 }
 
-int cesm_conv_pack_batch(int dtype, const int64_t* jobs, int njobs, int blocks_per_job, hipStream_t stream) {
+int cesm_conv_pack_batch(int dtype, const int64_t* jobs, int njobs, int nblocks, hipStream_t stream) {
   if (njobs <= 0) return CESM_OK;
-  dim3 grid((unsigned)std::max(1, blocks_per_job), (unsigned)njobs);
+  const unsigned grid = (unsigned)std::max(1, nblocks);  // any grid is correct (block-stride loop)
   if (dtype == CESM_DT_BF16)
-    conv_pack_batch_kernel<bf16><<<grid, 256, 0, stream>>>(jobs);
+    conv_pack_batch_kernel<bf16><<<grid, 256, 0, stream>>>(jobs, njobs);
   else if (dtype == CESM_DT_F32)
-    conv_pack_batch_kernel<float><<<grid, 256, 0, stream>>>(jobs);
+    conv_pack_batch_kernel<float><<<grid, 256, 0, stream>>>(jobs, njobs);
   else
     return CESM_EINVAL;
   return cesm_launch_status();

@@ -64,9 +64,29 @@ def conv_pack_into(w, out, cout, cin, kh, kw, swap, flip):
     return out
 
 
-def conv_pack_batch(jobs_dev, njobs, dtype, blocks_per_job=512):
-    """one launch re-packing every job of a device int64 [njobs, 8] table (see cesm_conv_pack_batch)"""
-    call("cesm_conv_pack_batch", _DT[dtype], P(jobs_dev), int(njobs), int(blocks_per_job), S())
+def pack_blocks(cout, cin, kh, kw):
+    """blocks cesm_conv_pack_batch gives one job: (co, ci) tiles of pb_co_t(T) rows x 64 channels (csrc/conv.hip)"""
+    T = kh * kw
+    cot = min(64, max(1, 4096 // (T * 64)))
+    return -(-cout // cot) * -(-cin // 64)
+
+
+def conv_pack_table(rows, device):
+    """device job table of cesm_conv_pack_batch: rows [src ptr, dst ptr, Cout, Cin, KH, KW, swap, flip], then the
+    per-job block starts (exclusive prefix of pack_blocks), then the job index of every block; returns (table, nblocks)"""
+    assert len(rows) > 0 and all(r[4] * r[5] <= 64 for r in rows)  # a tile's taps x 64 channels fit the LDS tile
+    starts, bjob = [0], []
+    for j, r in enumerate(rows):
+        n = pack_blocks(r[2], r[3], r[4], r[5])
+        starts.append(starts[-1] + n)
+        bjob += [j] * n
+    flat = [v for r in rows for v in r] + starts + bjob
+    return torch.tensor(flat, dtype=torch.int64).to(device), starts[-1]
+
+
+def conv_pack_batch(jobs_dev, njobs, dtype, nblocks):
+    """one launch re-packing every job of a conv_pack_table (see cesm_conv_pack_batch)"""
+    call("cesm_conv_pack_batch", _DT[dtype], P(jobs_dev), int(njobs), int(nblocks), S())
 
 
 _QUEUES = {}

@@ -733,9 +733,8 @@ class UNetModel3D(nn.Module):
             if tab is None:
                 assert all(e.out.numel() < 2 ** 31 for e in ents)  # the batch kernel indexes in 32 bits
                 rows = [[e.w.data_ptr(), e.out.data_ptr(), *e.geo] for e in ents]
-                tab = torch.tensor(rows, dtype=torch.int64).to(ents[0].out.device)
-                self._pack_tables[cdt] = tab
-            K.conv_pack_batch(tab, len(ents), cdt)
+                tab = self._pack_tables[cdt] = K.conv_pack_table(rows, ents[0].out.device)
+            K.conv_pack_batch(tab[0], len(ents), cdt, tab[1])
             for e in ents:
                 e.epoch, e.version = ep, e.w._version
 

@@ -34,7 +34,8 @@ extern "C" {
  *   5 (round 5): cesm_abi_version() itself; cesm_conv_fwd / cesm_conv_fwd_gn gained `queue` and cesm_tblock_bwd_dw
  *     gained `dwout`, each before the hipStream_t / after dgamma;
  *   6 (round 6): cesm_tblock_bwd_dw lost `dwout` again (the in-kernel to_out weight gradient measured slower than the
- *     forward's O write and was removed) and gained `o` after dx (O emitted by the backward);
+ *     forward's O write and was removed) and gained `o` after dx (O emitted by the backward); cesm_conv_pack_batch's
+ *     job table gained per-job block starts and its fourth argument is the grid size;
  *     cesm_qkv_bwd / cesm_qkv_bwd_streams added. */
 #define CESM_ABI_VERSION 6
 int cesm_abi_version(void);
@@ -83,8 +84,12 @@ int cesm_conv_wgrad(int dtype, const void* x1, const void* x2, const void* dy1, 
 int cesm_conv_pack(int dtype, const float* w, void* wp, int Cout, int Cin, int KH, int KW, int swap, int flip,
                    hipStream_t stream);
 /* every cached pack of one dtype redone in ONE launch after an optimizer step: jobs = device
- * int64[njobs][8] {src fp32 ptr, dst ptr, Cout, Cin, KH, KW, swap, flip} (cesm_conv_pack semantics). */
-int cesm_conv_pack_batch(int dtype, const int64_t* jobs, int njobs, int blocks_per_job, hipStream_t stream);
+ * int64[njobs][8] {src fp32 ptr, dst ptr, Cout, Cin, KH, KW, swap, flip} (cesm_conv_pack semantics) followed by
+ * int64[njobs + 1] block starts, the exclusive prefix sum of the per-job tile counts cdiv(Cout, cot) * cdiv(Cin, 64)
+ * with cot = clamp(4096 / (KH * KW * 64), 1, 64), then int64[starts[njobs]] the job index of every block; nblocks = the grid
+ * (the last start is the work; any nblocks >= 1 is correct).  ABI 6: the table gained the starts, the fourth
+ * argument was blocks_per_job. */
+int cesm_conv_pack_batch(int dtype, const int64_t* jobs, int njobs, int nblocks, hipStream_t stream);
 /* dst[c] (+)= sum over rows of x[r][c]  (conv bias gradients) ; part: nsplit*C floats */
 int cesm_colsum(int dtype, const void* x, float* dst, float* part, int nsplit, int64_t rows, int C, int accumulate,
                 hipStream_t stream);

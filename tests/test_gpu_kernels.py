@@ -125,6 +125,32 @@ def test_wgrad_fused_bias(dev, cin, cout, k, st):
     assert torch.equal(dw1, dw2)
 
 
+@pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
+def test_conv_pack_batch(dev, cdt):
+    """cesm_conv_pack_batch (one launch for every cached weight pack, per-job (co, ci) tiles transposed through LDS)
+    == cesm_conv_pack per job: 1x1 / 3x3 / 4x4 / 7x7 shapes, swap and flip, partial tiles in co and ci"""
+    torch.manual_seed(5)
+    geos = [(64, 64, 3, 3, 0, 0), (64, 64, 3, 3, 1, 1), (128, 64, 4, 4, 1, 1), (768, 64, 1, 1, 0, 0),
+            (5, 7, 3, 3, 0, 1), (3, 1, 1, 1, 0, 0), (256, 512, 3, 3, 1, 1), (96, 40, 4, 4, 0, 0),
+            (64, 2, 7, 7, 0, 0), (1, 64, 3, 3, 1, 1), (130, 100, 3, 3, 1, 0)]
+    ws, outs, rows = [], [], []
+    for (co, ci, kh, kw, swap, flip) in geos:
+        w = torch.randn((ci, co, kh, kw) if swap else (co, ci, kh, kw), device=dev)
+        out = torch.full((co * kh * kw * ci,), float("nan"), device=dev).to(cdt)
+        ws.append(w)
+        outs.append(out)
+        rows.append([w.data_ptr(), out.data_ptr(), co, ci, kh, kw, swap, flip])
+    tab, nblocks = K.conv_pack_table(rows, dev)
+    assert nblocks == sum(K.pack_blocks(co, ci, kh, kw) for (co, ci, kh, kw, _, _) in geos)
+    for grid in (nblocks, 3):  # any grid is correct (block-stride loop)
+        for o in outs:
+            o.fill_(float("nan"))
+        K.conv_pack_batch(tab, len(rows), cdt, grid)
+        for w, o, (co, ci, kh, kw, swap, flip) in zip(ws, outs, geos):
+            ref = K.conv_pack(w, cdt, co, ci, kh, kw, swap, flip)
+            assert torch.equal(o.view(-1), ref.view(-1)), (grid, co, ci, kh, kw, swap, flip)
+
+
 @pytest.mark.parametrize("M,C", [(64, 64), (1000, 64), (40 * 77, 64), (6912 * 2 + 17, 128), (3000, 256), (777, 512)])
 def test_qkv_bwd_fused(dev, M, C):
     """cesm_qkv_bwd (csrc/qkvbwd.hip: dqkv read once for dx and dW of the 768-channel to_qkv projection) against a
