@@ -556,7 +556,11 @@ __device__ __forceinline__ void h3_epilogue(const f32x4 (&acc)[NI][NJ], const in
 }
 
 // (Round 3: double-buffered chunks at one block per CU measured slower, conv total 64.0 -> 68.2 ms per step: the
-// second co-resident block hides the staging better than an in-block prefetch.  Removed.)
+// second co-resident block hides the staging better than an in-block prefetch.  Removed.  Round 6: 16-channel stages in
+// a double buffer at two blocks per CU, each K = 32 MFMA step taking two taps of a stage (so the K = 32 rate is kept,
+// unlike round 5's K = 16 form), 44-pixel halo pitch with a conflict-free 32-B-row swizzle: correct, 385 vs 336 us per
+// launch -- the extra zero-half step for the 9th tap, twice the barriers and the per-tap address VALU outweigh the
+// overlap (profiles/r6o_tap_pair_conv_ab.txt).  Removed.)
 template <int TW, int NJv = 4>
 __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
                                                               const bf16* __restrict__ w, const float* __restrict__ bias,
