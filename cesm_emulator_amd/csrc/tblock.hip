@@ -2018,27 +2018,23 @@ __global__ __launch_bounds__(512, 1) void twh_bwd_kernel(
       // O^T[d][i] = V^T . P^T of these pixels (o_out: the to_out weight gradient's input, round 6), stored straight
       // away (8 B per lane and half).  Parking it in the pixels' dead dO rows and storing it after the dW or the dxn
       // GEMM measured slower (3884-4325 vs 3696-3992 us per level-0 call: 23-45 more spilled registers,
-      // profiles/r6g_twh_o_ab.txt)
+      // profiles/r6g_twh_o_ab.txt); lane pairs exchanging halves by v_permlane16_swap for one 16-B store per lane
+      // measured the same (+301 / +315 us for the emission, profiles/r6p_twh_o_paired_stores.txt)
       if (o_out) {  // uniform
 #pragma unroll
         for (int u = 0; u < PG; ++u) {
           f32x4 ot[2];
 #pragma unroll
           for (int half = 0; half < 2; ++half) ot[half] = mfma_k16(kslot4_hld(sv, (pp0 + u) * F, half * 16, lane), pa_b[u], z4);
-          // lane (lr, lg) holds dims 4lg .. 4lg+3 of both 16-dim halves; one v_permlane16_swap per word pairs lanes
-          // lg and lg ^ 1 so that each lane holds 8 consecutive dims (lg even: half 0, lg odd: half 1) -> one 16-B
-          // store per lane instead of two 8-B ones (the lanes of a pair share lr, so both are valid or neither)
-          const bf16x4 h0 = {(bf16)ot[0][0], (bf16)ot[0][1], (bf16)ot[0][2], (bf16)ot[0][3]};
-          const bf16x4 h1 = {(bf16)ot[1][0], (bf16)ot[1][1], (bf16)ot[1][2], (bf16)ot[1][3]};
-          const tw_u32x2 a2 = __builtin_bit_cast(tw_u32x2, h0), b2 = __builtin_bit_cast(tw_u32x2, h1);
-          const auto s0 = __builtin_amdgcn_permlane16_swap(a2[0], b2[0], false, false);
-          const auto s1 = __builtin_amdgcn_permlane16_swap(a2[1], b2[1], false, false);
           if (lr < F && p0 + pp0 + u < HW) {
-            const int d0 = (lg & 1) ? 16 + 4 * (lg - 1) : 4 * lg;
-            bf16* orow = o_out + (((int64_t)b * F + lr) * HW + p0 + pp0 + u) * INNER + h * DH + d0;
-            typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-            const u32x4_t v = {s0[0], s1[0], s0[1], s1[1]};
-            __builtin_nontemporal_store(v, reinterpret_cast<u32x4_t*>(orow));
+            bf16* orow = o_out + (((int64_t)b * F + lr) * HW + p0 + pp0 + u) * INNER + h * DH + lg * 4;
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+              bf16x4 o4;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) o4[r] = (bf16)ot[half][r];
+              __builtin_nontemporal_store(__builtin_bit_cast(uint64_t, o4), reinterpret_cast<uint64_t*>(orow + half * 16));
+            }
           }
         }
       }
