@@ -33,6 +33,7 @@ __global__ void linear_small_fwd_kernel(const float* __restrict__ x, const float
   const float* wr = w + (int64_t)o * I;
   for (int r0 = 0; r0 < R; r0 += 8) {
     float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
     for (int i = lane; i < I; i += 64) {
       const float wv = wr[i];
 #pragma unroll
@@ -64,8 +65,10 @@ __global__ __launch_bounds__(256) void linear_small_dx_kernel(const float* __res
   const int il = threadIdx.x & 15, os = threadIdx.x >> 4;
   const int i = blockIdx.x * 16 + il;
   float s = 0.f;
-  if (i < I)
+  if (i < I) {
+#pragma unroll 8
     for (int o = os; o < O; o += 16) s = fmaf(dy[(int64_t)r * O + o], w[(int64_t)o * I + i], s);
+  }
   red[os][il] = s;
   __syncthreads();
   if (os == 0 && i < I) {
