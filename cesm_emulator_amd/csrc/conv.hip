@@ -2404,6 +2404,125 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
 }
 
 // ----------------------------------------------------------------------------------------
+// 1x1 weight gradient with square tiles (round 6): BM = 256 output rows x BN = 256 (or 128) input channels per block,
+// 8 waves (4 row quarters x 2 column halves, 64 x BN/2 per wave).  wgrad_wide<256> reads the same 256-row dY slice
+// once per 64 input channels: at the 768-channel qkv projections of the C = 256 / 512 levels that is 4-8 reads of the
+// largest tensor, and the kernel is bound by those bytes (≈ 2 TB/s of loads at 0.15 of the MFMA peak).  Here dY is read
+// once per (row tile, pixel split) and x once per row tile.  Loads through registers as wgrad_wide (two steps in
+// flight), fragments by ds_read_b64_tr_b16 from the same XOR-swizzled rows.
+// ----------------------------------------------------------------------------------------
+template <int BN>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void wgrad_sq_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ dy, float* __restrict__ slab, int M, int Cout, int Cin,
+    int px_per_split) {
+  constexpr int BM = 256, MT = 4, NT = BN / 32;
+  constexpr int NY = WG_BP * BM / 8 / 512, NX = WG_BP * BN / 8 / 512;  // 16-B vectors per thread and step
+  __shared__ __attribute__((aligned(16))) bf16 tY[2][WG_BP * BM];
+  __shared__ __attribute__((aligned(16))) bf16 tX[2][WG_BP * BN];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int wr = wid & 3, wc = wid >> 2;
+  const int co0 = blockIdx.x * BM, k0 = blockIdx.y * BN;
+  const int pbeg = blockIdx.z * px_per_split;
+  const int pend = min(M, pbeg + px_per_split);
+  bf16x8 yr2[2][NY], xr2[2][NX];
+  auto gload = [&](int p0, auto slotc) {
+    constexpr int slot = decltype(slotc)::value;
+#pragma unroll
+    for (int u = 0; u < NY; ++u) {
+      const int v = tid + 512 * u, r = v / (BM / 8), c = (v % (BM / 8)) * 8;
+      const int m = p0 + r;
+      yr2[slot][u] = m < pend ? *reinterpret_cast<const bf16x8*>(dy + (int64_t)m * Cout + co0 + c) : bf16x8{};
+    }
+#pragma unroll
+    for (int u = 0; u < NX; ++u) {
+      const int v = tid + 512 * u, r = v / (BN / 8), c = (v % (BN / 8)) * 8;
+      const int m = p0 + r;
+      xr2[slot][u] = m < pend ? *reinterpret_cast<const bf16x8*>(x + (int64_t)m * Cin + k0 + c) : bf16x8{};
+    }
+  };
+  auto sstore = [&](auto bufc) {
+    constexpr int buf = decltype(bufc)::value;
+#pragma unroll
+    for (int u = 0; u < NY; ++u) {
+      const int v = tid + 512 * u, r = v / (BM / 8), c = (v % (BM / 8)) * 8;
+      *reinterpret_cast<bf16x8*>(tY[buf] + r * BM + (((c >> 2) ^ wgb_swz<BM>(r)) * 4)) = yr2[buf][u];
+    }
+#pragma unroll
+    for (int u = 0; u < NX; ++u) {
+      const int v = tid + 512 * u, r = v / (BN / 8), c = (v % (BN / 8)) * 8;
+      *reinterpret_cast<bf16x8*>(tX[buf] + r * BN + (((c >> 2) ^ wgb_swz<BN>(r)) * 4)) = xr2[buf][u];
+    }
+  };
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nsteps = (pend - pbeg + WG_BP - 1) / WG_BP;
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  if (nsteps > 0) {
+    gload(pbeg, I0{});
+    if (nsteps > 1) gload(pbeg + WG_BP, I1{});
+    sstore(I0{});
+  }
+  __syncthreads();
+  const int q = lr >> 2, pp = lr & 3;
+  auto step = [&](int s, auto bufc) {
+    constexpr int buf = decltype(bufc)::value;
+    if (s + 2 < nsteps) gload(pbeg + (s + 2) * WG_BP, bufc);
+    bf16x8 af[MT], bfr[NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const int c0 = wr * 64 + i * 16;
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const int r = lg * 8 + half * 4 + q;
+        const int ch = ((c0 >> 2) + pp) ^ wgb_swz<BM>(r);
+        const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tY[buf] + r * BM + ch * 4));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) af[i][half * 4 + e] = __builtin_bit_cast(bf16, (short)v[e]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int c0 = wc * (BN / 2) + j * 16;
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const int r = lg * 8 + half * 4 + q;
+        const int ch = ((c0 >> 2) + pp) ^ wgb_swz<BN>(r);
+        const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(tX[buf] + r * BN + ch * 4));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bfr[j][half * 4 + e] = __builtin_bit_cast(bf16, (short)v[e]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    if (s + 1 < nsteps) sstore(std::integral_constant<int, buf ^ 1>{});
+    __syncthreads();
+  };
+  for (int s = 0; s < nsteps; s += 2) {
+    step(s, I0{});
+    if (s + 1 < nsteps) step(s + 1, I1{});
+  }
+  float* out = slab + (int64_t)blockIdx.z * Cout * Cin;
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int kc = k0 + wc * (BN / 2) + j * 16 + lr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wr * 64 + i * 16 + lg * 4 + r;
+        out[(int64_t)co * Cin + kc] = acc[i][j][r];
+      }
+    }
+}
+
+// ----------------------------------------------------------------------------------------
 // 3x3 / stride 1 / pad 1 weight gradient (bf16), halo-tiled.  Block = (64 co) x (32 ci chunk) x
 // all 9 taps, looping over 8x32-pixel tiles (its share of the split-K over pixels).  Per tile the
 // dY tile [256 px][64 co] and the input halo [10x34 px][32 ci] are staged in LDS; pixels are the
@@ -3824,6 +3943,17 @@ int cesm_conv_fwd_gn(int dtype, const void* x1, const void* x2, const void* wp, 
 namespace {
 // Kernel selection of cesm_conv_wgrad (host only)
 enum WgradVariant { WGV_WIDE = 0, WGV_GEN, WGV_S2, WGV_W32C64, WGV_W36C64 };
+// input-channel tile of wgrad_sq_kernel for a bf16 1x1 weight gradient it takes (0: the wide kernel's 64-column
+// tiles): one source, one destination, no bias, Cout % 256 == 0; BN = 256 when Cin % 256 == 0, else 128
+static int wgrad_sq_bn(int KH, int KW, int S, int P, int U, int Hi, int Wi, int Ho, int Wo, int C1, int C2, int Cout,
+                       int Co1, bool with_bias) {
+  if (KH != 1 || KW != 1 || S != 1 || P != 0 || U != 1 || Hi != Ho || Wi != Wo || C2 != 0 || Co1 != Cout ||
+      with_bias || Cout % 256 != 0)
+    return 0;
+  if (C1 % 256 == 0) return 256;
+  if (C1 % 128 == 0) return 128;
+  return 0;
+}
 static int wgrad_plan(int dtype, int64_t M, int Hi, int Wi, int Ho, int Wo, int KH, int KW, int S, int P, int U) {
   const bool halo3 = dtype == CESM_DT_BF16 && KH == 3 && KW == 3 && S == 1 && P == 1 && U == 1 && Ho == Hi &&
                      Wo == Wi;
@@ -3842,6 +3972,15 @@ static int wgrad_plan(int dtype, int64_t M, int Hi, int Wi, int Ho, int Wo, int 
 
 extern "C" {
 
+// input-channel tile of the square-tile 1x1 weight-gradient kernel for this shape (0: not taken); the caller sizes
+// nsplit (and the slab) for Cout/256 x Cin/BN tiles when it is non-zero
+int cesm_conv_wgrad_sq_bn(int dtype, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout, int Co1, int KH,
+                          int KW, int S, int P, int U, int with_bias) {
+  const int64_t M = (int64_t)Nb * Ho * Wo;
+  if (wgrad_plan(dtype, M, Hi, Wi, Ho, Wo, KH, KW, S, P, U) != WGV_WIDE) return 0;
+  return wgrad_sq_bn(KH, KW, S, P, U, Hi, Wi, Ho, Wo, C1, C2, Cout, Co1, with_bias != 0);
+}
+
 const char* cesm_conv_wgrad_variant(int dtype, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout,
                                     int Co1, int KH, int KW, int S, int P, int U, int with_bias) {
   const int64_t M = (int64_t)Nb * Ho * Wo;
@@ -3852,6 +3991,8 @@ const char* cesm_conv_wgrad_variant(int dtype, int Nb, int Hi, int Wi, int C1, i
     case WGV_W36C64: return "wgrad3x3w36c64_kernel";
     case WGV_S2: return "wgrads2_bf16_kernel";
     case WGV_WIDE: {
+      const int sq = wgrad_sq_bn(KH, KW, S, P, U, Hi, Wi, Ho, Wo, C1, C2, Cout, Co1, with_bias != 0);
+      if (sq) return sq == 256 ? "wgrad_sq_kernel<256>" : "wgrad_sq_kernel<128>";
       const int bm = (Cout % 256 == 0 && Co1 % 256 == 0) ? 256 : ((Cout % 128 == 0 && Co1 % 128 == 0) ? 128 : 64);
       static const char* const names[6] = {"wgrad_wide_kernel<64,false>", "wgrad_wide_kernel<64,true>",
                                            "wgrad_wide_kernel<128,false>", "wgrad_wide_kernel<128,true>",
@@ -3899,6 +4040,15 @@ int cesm_conv_wgrad(int dtype, const void* x1, const void* x2, const void* dy1, 
     dim3 g3(Cout / 64, (Cin / 32) * 4, std::min(nsplit, ntiles));
     wgrads2_bf16_kernel<<<g3, 256, 0, stream>>>((const bf16*)x1, (const bf16*)dy1, slab, g, tx, ntiles);
     nsplit = (int)g3.z;
+  } else if (wv == WGV_WIDE && wgrad_sq_bn(KH, KW, S, P, U, Hi, Wi, Ho, Wo, C1, C2, Cout, Co1, db != nullptr) > 0) {
+    // square 256 x BN tiles for the 1x1 convs whose dY would be re-read once per 64 input channels (the caller sized
+    // nsplit for these tiles: cesm_conv_wgrad_sq_bn)
+    const int bn = wgrad_sq_bn(KH, KW, S, P, U, Hi, Wi, Ho, Wo, C1, C2, Cout, Co1, false);
+    const dim3 gq(Cout / 256, Cin / bn, nsplit);
+    if (bn == 256)
+      wgrad_sq_kernel<256><<<gq, 512, 0, stream>>>((const bf16*)x1, (const bf16*)dy1, slab, (int)M, Cout, Cin, (int)pps);
+    else
+      wgrad_sq_kernel<128><<<gq, 512, 0, stream>>>((const bf16*)x1, (const bf16*)dy1, slab, (int)M, Cout, Cin, (int)pps);
   } else if (wv == WGV_WIDE || wv == WGV_S2) {
     // wide-tile kernel; nsplit from the caller sized the slab for 64-row tiles, keep it
     const int bm = (Cout % 256 == 0 && Co1 % 256 == 0) ? 256 : ((Cout % 128 == 0 && Co1 % 128 == 0) ? 128 : 64);

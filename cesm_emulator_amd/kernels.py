@@ -204,6 +204,8 @@ CONV_TRACE = [] if os.environ.get("CESM_TRACE_CONV") else None
 # [Cout][K] slab that conv_wgrad_reduce reads back, so more blocks than ~2-4 per CU only adds slab
 # traffic (round 3: 512 / 2048 blocks 144.7 / 131.2 ms per step against 129.7 at 1024)
 WGRAD_BLOCKS = 1024
+# blocks of the square-tile 1x1 weight-gradient kernel (512 threads, 64 KB of LDS: two per CU)
+WGRAD_SQ_BLOCKS = 256
 
 
 def _wgrad_nsplit(M, cout, K, bm=64, blocks=None):
@@ -247,8 +249,14 @@ def conv_wgrad(x1, x2, dy1, dy2, dw, geom, swap, flip, accumulate=True, db=None)
         nb = WGRAD_BLOCKS // 2
         nsplit = max(1, min(nb // max(1, (Cout // 64) * ((C1 + C2) // 32) * (4 if s2 else 1)), max(1, M // 256)))
     else:
-        bm = _wgrad_bm(x1, Cout, Co1)
-        nsplit = _wgrad_nsplit(M, Cout, K, bm, WGRAD_BLOCKS // 2 if bm == 256 else WGRAD_BLOCKS)
+        sq = lib().cesm_conv_wgrad_sq_bn(dtcode(x1), Nb, Hi, Wi, C1, C2, Ho, Wo, Cout, Co1, KH, KW, St, Pd, U,
+                                         int(db is not None and dy2 is None))
+        if sq:
+            # square-tile 1x1 kernel: 512-thread blocks of 256 x sq, ~WGRAD_SQ_BLOCKS of them
+            nsplit = max(1, min(WGRAD_SQ_BLOCKS // ((Cout // 256) * (K // sq)), max(1, M // 256)))
+        else:
+            bm = _wgrad_bm(x1, Cout, Co1)
+            nsplit = _wgrad_nsplit(M, Cout, K, bm, WGRAD_BLOCKS // 2 if bm == 256 else WGRAD_BLOCKS)
     slab = empty((nsplit, Cout, K), torch.float32, x1.device)
     if CONV_TRACE is not None:
         CONV_TRACE.append(("wgrad", Nb, Hi, Wi, C1 + C2, Ho, Wo, Cout, KH, KW, St, Pd, U))

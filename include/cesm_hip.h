@@ -68,6 +68,10 @@ int cesm_conv_fwd_gn(int dtype, const void* x1, const void* x2, const void* wp, 
  * launcher itself selects through the same function).  "invalid" if cesm_conv_fwd would return EINVAL. */
 const char* cesm_conv_fwd_variant(int dtype, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout,
                                   int Co1, int KH, int KW, int S, int P, int U);
+/* Input-channel tile (256 / 128) of the square-tile 1x1 weight-gradient kernel cesm_conv_wgrad runs for this shape, 0 if
+ * it runs another kernel (host-only query).  When non-zero the caller sizes nsplit for Cout/256 x Cin/BN tiles. */
+int cesm_conv_wgrad_sq_bn(int dtype, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout, int Co1, int KH,
+                          int KW, int S, int P, int U, int with_bias);
 /* name of the kernel cesm_conv_wgrad launches (host-only query; with_bias: db != NULL) */
 const char* cesm_conv_wgrad_variant(int dtype, int Nb, int Hi, int Wi, int C1, int C2, int Ho, int Wo, int Cout,
                                     int Co1, int KH, int KW, int S, int P, int U, int with_bias);

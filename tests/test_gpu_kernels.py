@@ -125,6 +125,21 @@ def test_wgrad_fused_bias(dev, cin, cout, k, st):
     assert torch.equal(dw1, dw2)
 
 
+@pytest.mark.parametrize("M,N,C", [(4000, 768, 256), (1237, 768, 512), (3001, 256, 128), (96 * 48 * 72, 768, 256)])
+def test_wgrad_square_tiles(dev, M, N, C):
+    """1x1 weight gradient through the square-tile kernel (wgrad_sq_kernel, round 6: 256 x BN tiles, dY read once per
+    row tile) vs float64, accumulating into a non-zero dW; pixel counts that leave partial steps and splits"""
+    torch.manual_seed(11)
+    x = torch.randn(1, 1, M, C, device=dev).to(torch.bfloat16)
+    dy = torch.randn(1, 1, M, N, device=dev).to(torch.bfloat16)
+    assert K.conv_wgrad_variant(torch.bfloat16, 1, 1, M, C, 0, 1, M, N, N, 1, 1, 1, 0, 1).startswith("wgrad_sq_kernel")
+    dw = torch.full((N, C, 1, 1), 0.25, device=dev)
+    K.conv_wgrad(x, None, dy, None, dw, (1, M, N, 1, 1, 1, 0, 1), 0, 0)
+    ref = dy.view(M, N).double().t() @ x.view(M, C).double() + 0.25
+    err = rel(dw.view(N, C), ref)
+    assert err < 1e-5, err
+
+
 @pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
 def test_conv_pack_batch(dev, cdt):
     """cesm_conv_pack_batch (one launch for every cached weight pack, per-job (co, ci) tiles transposed through LDS)
