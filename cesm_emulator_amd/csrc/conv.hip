@@ -2404,24 +2404,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
 }
 
 // ----------------------------------------------------------------------------------------
-// 1x1 weight gradient with square tiles (round 6): BM = 256 output rows x BN = 256 (or 128) input channels per block,
-// 8 waves (4 row quarters x 2 column halves, 64 x BN/2 per wave).  wgrad_wide<256> reads the same 256-row dY slice
+// 1x1 weight gradient with square tiles (round 6): BM = 256 (or 64) output rows x BN = 256 (or 128) input channels per
+// block, 8 waves (BM/64 row quarters x 8/(BM/64) column slices, 64 rows per wave).  wgrad_wide<256> reads the same 256-row dY slice
 // once per 64 input channels: at the 768-channel qkv projections of the C = 256 / 512 levels that is 4-8 reads of the
 // largest tensor, and the kernel is bound by those bytes (≈ 2 TB/s of loads at 0.15 of the MFMA peak).  Here dY is read
 // once per (row tile, pixel split) and x once per row tile.  Loads through registers as wgrad_wide (two steps in
 // flight), fragments by ds_read_b64_tr_b16 from the same XOR-swizzled rows.
 // ----------------------------------------------------------------------------------------
-template <int BN>
+template <int BM, int BN>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void wgrad_sq_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ dy, float* __restrict__ slab, int M, int Cout, int Cin,
     int px_per_split) {
-  constexpr int BM = 256, MT = 4, NT = BN / 32;
-  constexpr int NY = WG_BP * BM / 8 / 512, NX = WG_BP * BN / 8 / 512;  // 16-B vectors per thread and step
+  // waves: WR row quarters of 64 rows x WC column slices of BN / WC columns
+  constexpr int WR = BM / 64, WC = 8 / WR, MT = 4, NT = BN / (16 * WC);
+  static_assert((BM == 256 || BM == 64) && NT >= 1, "wgrad_sq tiles");
+  constexpr int TY = WG_BP * BM / 8, TX = WG_BP * BN / 8;  // 16-B vectors per step
+  constexpr int NY = (TY + 511) / 512, NX = (TX + 511) / 512;
   __shared__ __attribute__((aligned(16))) bf16 tY[2][WG_BP * BM];
   __shared__ __attribute__((aligned(16))) bf16 tX[2][WG_BP * BN];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
-  const int wr = wid & 3, wc = wid >> 2;
+  const int wr = wid % WR, wc = wid / WR;
   const int co0 = blockIdx.x * BM, k0 = blockIdx.y * BN;
   const int pbeg = blockIdx.z * px_per_split;
   const int pend = min(M, pbeg + px_per_split);
@@ -2432,13 +2435,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
     for (int u = 0; u < NY; ++u) {
       const int v = tid + 512 * u, r = v / (BM / 8), c = (v % (BM / 8)) * 8;
       const int m = p0 + r;
-      yr2[slot][u] = m < pend ? *reinterpret_cast<const bf16x8*>(dy + (int64_t)m * Cout + co0 + c) : bf16x8{};
+      yr2[slot][u] = m < pend && v < TY ? *reinterpret_cast<const bf16x8*>(dy + (int64_t)m * Cout + co0 + c) : bf16x8{};
     }
 #pragma unroll
     for (int u = 0; u < NX; ++u) {
       const int v = tid + 512 * u, r = v / (BN / 8), c = (v % (BN / 8)) * 8;
       const int m = p0 + r;
-      xr2[slot][u] = m < pend ? *reinterpret_cast<const bf16x8*>(x + (int64_t)m * Cin + k0 + c) : bf16x8{};
+      xr2[slot][u] = m < pend && v < TX ? *reinterpret_cast<const bf16x8*>(x + (int64_t)m * Cin + k0 + c) : bf16x8{};
     }
   };
   auto sstore = [&](auto bufc) {
@@ -2446,12 +2449,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
 #pragma unroll
     for (int u = 0; u < NY; ++u) {
       const int v = tid + 512 * u, r = v / (BM / 8), c = (v % (BM / 8)) * 8;
-      *reinterpret_cast<bf16x8*>(tY[buf] + r * BM + (((c >> 2) ^ wgb_swz<BM>(r)) * 4)) = yr2[buf][u];
+      if (v < TY) *reinterpret_cast<bf16x8*>(tY[buf] + r * BM + (((c >> 2) ^ wgb_swz<BM>(r)) * 4)) = yr2[buf][u];
     }
 #pragma unroll
     for (int u = 0; u < NX; ++u) {
       const int v = tid + 512 * u, r = v / (BN / 8), c = (v % (BN / 8)) * 8;
-      *reinterpret_cast<bf16x8*>(tX[buf] + r * BN + (((c >> 2) ^ wgb_swz<BN>(r)) * 4)) = xr2[buf][u];
+      if (v < TX) *reinterpret_cast<bf16x8*>(tX[buf] + r * BN + (((c >> 2) ^ wgb_swz<BN>(r)) * 4)) = xr2[buf][u];
     }
   };
   f32x4 acc[MT][NT];
@@ -2487,7 +2490,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
     }
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
-      const int c0 = wc * (BN / 2) + j * 16;
+      const int c0 = wc * (BN / WC) + j * 16;
 #pragma unroll
       for (int half = 0; half < 2; ++half) {
         const int r = lg * 8 + half * 4 + q;
@@ -2513,7 +2516,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
   for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
-      const int kc = k0 + wc * (BN / 2) + j * 16 + lr;
+      const int kc = k0 + wc * (BN / WC) + j * 16 + lr;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = co0 + wr * 64 + i * 16 + lg * 4 + r;
@@ -3944,12 +3947,14 @@ namespace {
 // Kernel selection of cesm_conv_wgrad (host only)
 enum WgradVariant { WGV_WIDE = 0, WGV_GEN, WGV_S2, WGV_W32C64, WGV_W36C64 };
 // input-channel tile of wgrad_sq_kernel for a bf16 1x1 weight gradient it takes (0: the wide kernel's 64-column
-// tiles): one source, one destination, no bias, Cout % 256 == 0; BN = 256 when Cin % 256 == 0, else 128
+// tiles): one source, one destination, no bias; Cout % 256 == 0 with BN = 256 when Cin % 256 == 0, else 128; or
+// Cout = 64 with Cin % 256 == 0 (64 x 256 tiles)
 static int wgrad_sq_bn(int KH, int KW, int S, int P, int U, int Hi, int Wi, int Ho, int Wo, int C1, int C2, int Cout,
                        int Co1, bool with_bias) {
-  if (KH != 1 || KW != 1 || S != 1 || P != 0 || U != 1 || Hi != Ho || Wi != Wo || C2 != 0 || Co1 != Cout ||
-      with_bias || Cout % 256 != 0)
+  if (KH != 1 || KW != 1 || S != 1 || P != 0 || U != 1 || Hi != Ho || Wi != Wo || C2 != 0 || Co1 != Cout || with_bias)
     return 0;
+  if (Cout == 64) return C1 % 256 == 0 ? 256 : 0;  // 64 x 256 tiles (the level-0 to_out: dY read once, not per 64 ci)
+  if (Cout % 256 != 0) return 0;
   if (C1 % 256 == 0) return 256;
   if (C1 % 128 == 0) return 128;
   return 0;
@@ -3992,7 +3997,7 @@ const char* cesm_conv_wgrad_variant(int dtype, int Nb, int Hi, int Wi, int C1, i
     case WGV_S2: return "wgrads2_bf16_kernel";
     case WGV_WIDE: {
       const int sq = wgrad_sq_bn(KH, KW, S, P, U, Hi, Wi, Ho, Wo, C1, C2, Cout, Co1, with_bias != 0);
-      if (sq) return sq == 256 ? "wgrad_sq_kernel<256>" : "wgrad_sq_kernel<128>";
+      if (sq) return Cout == 64 ? "wgrad_sq_kernel<64,256>" : (sq == 256 ? "wgrad_sq_kernel<256,256>" : "wgrad_sq_kernel<256,128>");
       const int bm = (Cout % 256 == 0 && Co1 % 256 == 0) ? 256 : ((Cout % 128 == 0 && Co1 % 128 == 0) ? 128 : 64);
       static const char* const names[6] = {"wgrad_wide_kernel<64,false>", "wgrad_wide_kernel<64,true>",
                                            "wgrad_wide_kernel<128,false>", "wgrad_wide_kernel<128,true>",
@@ -4044,11 +4049,12 @@ int cesm_conv_wgrad(int dtype, const void* x1, const void* x2, const void* dy1, 
     // square 256 x BN tiles for the 1x1 convs whose dY would be re-read once per 64 input channels (the caller sized
     // nsplit for these tiles: cesm_conv_wgrad_sq_bn)
     const int bn = wgrad_sq_bn(KH, KW, S, P, U, Hi, Wi, Ho, Wo, C1, C2, Cout, Co1, false);
-    const dim3 gq(Cout / 256, Cin / bn, nsplit);
-    if (bn == 256)
-      wgrad_sq_kernel<256><<<gq, 512, 0, stream>>>((const bf16*)x1, (const bf16*)dy1, slab, (int)M, Cout, Cin, (int)pps);
-    else
-      wgrad_sq_kernel<128><<<gq, 512, 0, stream>>>((const bf16*)x1, (const bf16*)dy1, slab, (int)M, Cout, Cin, (int)pps);
+    const int bm = Cout % 256 == 0 ? 256 : 64;
+    const dim3 gq(Cout / bm, Cin / bn, nsplit);
+    const bf16 *qx = (const bf16*)x1, *qy = (const bf16*)dy1;
+    if (bm == 64) wgrad_sq_kernel<64, 256><<<gq, 512, 0, stream>>>(qx, qy, slab, (int)M, Cout, Cin, (int)pps);
+    else if (bn == 256) wgrad_sq_kernel<256, 256><<<gq, 512, 0, stream>>>(qx, qy, slab, (int)M, Cout, Cin, (int)pps);
+    else wgrad_sq_kernel<256, 128><<<gq, 512, 0, stream>>>(qx, qy, slab, (int)M, Cout, Cin, (int)pps);
   } else if (wv == WGV_WIDE || wv == WGV_S2) {
     // wide-tile kernel; nsplit from the caller sized the slab for 64-row tiles, keep it
     const int bm = (Cout % 256 == 0 && Co1 % 256 == 0) ? 256 : ((Cout % 128 == 0 && Co1 % 128 == 0) ? 128 : 64);

@@ -252,8 +252,10 @@ def conv_wgrad(x1, x2, dy1, dy2, dw, geom, swap, flip, accumulate=True, db=None)
         sq = lib().cesm_conv_wgrad_sq_bn(dtcode(x1), Nb, Hi, Wi, C1, C2, Ho, Wo, Cout, Co1, KH, KW, St, Pd, U,
                                          int(db is not None and dy2 is None))
         if sq:
-            # square-tile 1x1 kernel: 512-thread blocks of 256 x sq, ~WGRAD_SQ_BLOCKS of them
-            nsplit = max(1, min(WGRAD_SQ_BLOCKS // ((Cout // 256) * (K // sq)), max(1, M // 256)))
+            # square-tile 1x1 kernel: 512-thread blocks of 256 (or 64) x sq, ~WGRAD_SQ_BLOCKS of them (twice as many
+            # 64-row blocks: 100 registers, two per CU)
+            nb = WGRAD_SQ_BLOCKS * (2 if Cout == 64 else 1)
+            nsplit = max(1, min(nb // (max(1, Cout // 256) * (K // sq)), max(1, M // 256)))
         else:
             bm = _wgrad_bm(x1, Cout, Co1)
             nsplit = _wgrad_nsplit(M, Cout, K, bm, WGRAD_BLOCKS // 2 if bm == 256 else WGRAD_BLOCKS)

@@ -125,7 +125,8 @@ def test_wgrad_fused_bias(dev, cin, cout, k, st):
     assert torch.equal(dw1, dw2)
 
 
-@pytest.mark.parametrize("M,N,C", [(4000, 768, 256), (1237, 768, 512), (3001, 256, 128), (96 * 48 * 72, 768, 256)])
+@pytest.mark.parametrize("M,N,C", [(4000, 768, 256), (1237, 768, 512), (3001, 256, 128), (96 * 48 * 72, 768, 256),
+                                   (5000, 64, 256), (96 * 48 * 72 + 5, 64, 256)])
 def test_wgrad_square_tiles(dev, M, N, C):
     """1x1 weight gradient through the square-tile kernel (wgrad_sq_kernel, round 6: 256 x BN tiles, dY read once per
     row tile) vs float64, accumulating into a non-zero dW; pixel counts that leave partial steps and splits"""
