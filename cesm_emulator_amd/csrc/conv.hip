@@ -2411,10 +2411,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
 // once per (row tile, pixel split) and x once per row tile.  Loads through registers as wgrad_wide (two steps in
 // flight), fragments by ds_read_b64_tr_b16 from the same XOR-swizzled rows.
 // ----------------------------------------------------------------------------------------
-template <int BM, int BN>
+template <int BM, int BN, bool BIAS = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void wgrad_sq_kernel(
-    const bf16* __restrict__ x, const bf16* __restrict__ dy, float* __restrict__ slab, int M, int Cout, int Cin,
-    int px_per_split) {
+    const bf16* __restrict__ x, const bf16* __restrict__ dy, float* __restrict__ slab, float* __restrict__ bslab, int M,
+    int Cout, int Cin, int px_per_split) {
   // waves: WR row quarters of 64 rows x WC column slices of BN / WC columns
   constexpr int WR = BM / 64, WC = 8 / WR, MT = 4, NT = BN / (16 * WC);
   static_assert((BM == 256 || BM == 64) && NT >= 1, "wgrad_sq tiles");
@@ -2462,6 +2462,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
   for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // BIAS: the conv bias gradient sum_px dY[px][co] from the same dY fragments times a ones operand, by the waves of the
+  // first column slice of the first column block (as wgrad_wide<BM, true>); per-split partials bslab[z][co]
+  const bool bias_w = BIAS && blockIdx.y == 0 && wc == 0;  // wave-uniform
+  f32x4 bacc[BIAS ? MT : 1];
+#pragma unroll
+  for (int i = 0; i < (BIAS ? MT : 1); ++i) bacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.f;
   const int nsteps = (pend - pbeg + WG_BP - 1) / WG_BP;
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
@@ -2504,12 +2513,24 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
     for (int i = 0; i < MT; ++i)
 #pragma unroll
       for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    if constexpr (BIAS) {
+      if (bias_w) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i) bacc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, bacc[i], 0, 0, 0);
+      }
+    }
     if (s + 1 < nsteps) sstore(std::integral_constant<int, buf ^ 1>{});
     __syncthreads();
   };
   for (int s = 0; s < nsteps; s += 2) {
     step(s, I0{});
     if (s + 1 < nsteps) step(s + 1, I1{});
+  }
+  if (BIAS && bias_w && lr == 0) {  // every output column holds the row sum: column 0 writes it
+#pragma unroll
+    for (int i = 0; i < (BIAS ? MT : 1); ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bslab[(int64_t)blockIdx.z * Cout + co0 + wr * 64 + i * 16 + lg * 4 + r] = bacc[i][r];
   }
   float* out = slab + (int64_t)blockIdx.z * Cout * Cin;
 #pragma unroll
@@ -3951,8 +3972,8 @@ enum WgradVariant { WGV_WIDE = 0, WGV_GEN, WGV_S2, WGV_W32C64, WGV_W36C64 };
 // Cout = 64 with Cin % 256 == 0 (64 x 256 tiles)
 static int wgrad_sq_bn(int KH, int KW, int S, int P, int U, int Hi, int Wi, int Ho, int Wo, int C1, int C2, int Cout,
                        int Co1, bool with_bias) {
-  if (KH != 1 || KW != 1 || S != 1 || P != 0 || U != 1 || Hi != Ho || Wi != Wo || C2 != 0 || Co1 != Cout || with_bias)
-    return 0;
+  (void)with_bias;  // the bias gradient rides along (BIAS instantiations)
+  if (KH != 1 || KW != 1 || S != 1 || P != 0 || U != 1 || Hi != Ho || Wi != Wo || C2 != 0 || Co1 != Cout) return 0;
   if (Cout == 64) return C1 % 256 == 0 ? 256 : 0;  // 64 x 256 tiles (the level-0 to_out: dY read once, not per 64 ci)
   if (Cout % 256 != 0) return 0;
   if (C1 % 256 == 0) return 256;
@@ -3997,7 +4018,12 @@ const char* cesm_conv_wgrad_variant(int dtype, int Nb, int Hi, int Wi, int C1, i
     case WGV_S2: return "wgrads2_bf16_kernel";
     case WGV_WIDE: {
       const int sq = wgrad_sq_bn(KH, KW, S, P, U, Hi, Wi, Ho, Wo, C1, C2, Cout, Co1, with_bias != 0);
-      if (sq) return Cout == 64 ? "wgrad_sq_kernel<64,256>" : (sq == 256 ? "wgrad_sq_kernel<256,256>" : "wgrad_sq_kernel<256,128>");
+      if (sq) {
+        static const char* const sqn[6] = {"wgrad_sq_kernel<64,256>", "wgrad_sq_kernel<64,256,true>",
+                                           "wgrad_sq_kernel<256,256>", "wgrad_sq_kernel<256,256,true>",
+                                           "wgrad_sq_kernel<256,128>", "wgrad_sq_kernel<256,128,true>"};
+        return sqn[(Cout == 64 ? 0 : sq == 256 ? 2 : 4) + (with_bias ? 1 : 0)];
+      }
       const int bm = (Cout % 256 == 0 && Co1 % 256 == 0) ? 256 : ((Cout % 128 == 0 && Co1 % 128 == 0) ? 128 : 64);
       static const char* const names[6] = {"wgrad_wide_kernel<64,false>", "wgrad_wide_kernel<64,true>",
                                            "wgrad_wide_kernel<128,false>", "wgrad_wide_kernel<128,true>",
@@ -4048,13 +4074,17 @@ int cesm_conv_wgrad(int dtype, const void* x1, const void* x2, const void* dy1, 
   } else if (wv == WGV_WIDE && wgrad_sq_bn(KH, KW, S, P, U, Hi, Wi, Ho, Wo, C1, C2, Cout, Co1, db != nullptr) > 0) {
     // square 256 x BN tiles for the 1x1 convs whose dY would be re-read once per 64 input channels (the caller sized
     // nsplit for these tiles: cesm_conv_wgrad_sq_bn)
-    const int bn = wgrad_sq_bn(KH, KW, S, P, U, Hi, Wi, Ho, Wo, C1, C2, Cout, Co1, false);
+    const int bn = wgrad_sq_bn(KH, KW, S, P, U, Hi, Wi, Ho, Wo, C1, C2, Cout, Co1, db != nullptr);
     const int bm = Cout % 256 == 0 ? 256 : 64;
     const dim3 gq(Cout / bm, Cin / bn, nsplit);
     const bf16 *qx = (const bf16*)x1, *qy = (const bf16*)dy1;
-    if (bm == 64) wgrad_sq_kernel<64, 256><<<gq, 512, 0, stream>>>(qx, qy, slab, (int)M, Cout, Cin, (int)pps);
-    else if (bn == 256) wgrad_sq_kernel<256, 256><<<gq, 512, 0, stream>>>(qx, qy, slab, (int)M, Cout, Cin, (int)pps);
-    else wgrad_sq_kernel<256, 128><<<gq, 512, 0, stream>>>(qx, qy, slab, (int)M, Cout, Cin, (int)pps);
+#define SQL(BMv, BNv, Bv) \
+  wgrad_sq_kernel<BMv, BNv, Bv><<<gq, 512, 0, stream>>>(qx, qy, slab, bslab, (int)M, Cout, Cin, (int)pps)
+    if (bm == 64) { if (db) SQL(64, 256, true); else SQL(64, 256, false); }
+    else if (bn == 256) { if (db) SQL(256, 256, true); else SQL(256, 256, false); }
+    else { if (db) SQL(256, 128, true); else SQL(256, 128, false); }
+#undef SQL
+    if (db) colsum_final_kernel<<<Cout, 64, 0, stream>>>(bslab, db, nsplit, Cout, 1);
   } else if (wv == WGV_WIDE || wv == WGV_S2) {
     // wide-tile kernel; nsplit from the caller sized the slab for 64-row tiles, keep it
     const int bm = (Cout % 256 == 0 && Co1 % 256 == 0) ? 256 : ((Cout % 128 == 0 && Co1 % 128 == 0) ? 128 : 64);

@@ -250,7 +250,7 @@ def conv_wgrad(x1, x2, dy1, dy2, dw, geom, swap, flip, accumulate=True, db=None)
         nsplit = max(1, min(nb // max(1, (Cout // 64) * ((C1 + C2) // 32) * (4 if s2 else 1)), max(1, M // 256)))
     else:
         sq = lib().cesm_conv_wgrad_sq_bn(dtcode(x1), Nb, Hi, Wi, C1, C2, Ho, Wo, Cout, Co1, KH, KW, St, Pd, U,
-                                         int(db is not None and dy2 is None))
+                                         int(db is not None))
         if sq:
             # square-tile 1x1 kernel: 512-thread blocks of 256 (or 64) x sq, ~WGRAD_SQ_BLOCKS of them (twice as many
             # 64-row blocks: 100 registers, two per CU)

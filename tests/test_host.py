@@ -173,10 +173,10 @@ def test_bench_shape_dispatch_table():
     assert wv(96, 144, 128, 0, 96, 144, 768, 768, 1, 1, 1, 0, 1) == "wgrad_sq_kernel<256,128>"
     assert wv(48, 72, 256, 0, 48, 72, 768, 768, 1, 1, 1, 0, 1) == "wgrad_sq_kernel<256,256>"
     assert wv(24, 36, 512, 0, 24, 36, 768, 768, 1, 1, 1, 0, 1) == "wgrad_sq_kernel<256,256>"
-    assert wv(24, 36, 512, 0, 24, 36, 768, 768, 1, 1, 1, 0, 1, with_bias=True) == "wgrad_wide_kernel<256,true>"
+    assert wv(24, 36, 512, 0, 24, 36, 768, 768, 1, 1, 1, 0, 1, with_bias=True) == "wgrad_sq_kernel<256,256,true>"
     # the level-0 temporal to_out (256 -> 64, no bias): 64 x 256 tiles
     assert wv(192, 288, 256, 0, 192, 288, 64, 64, 1, 1, 1, 0, 1) == "wgrad_sq_kernel<64,256>"
-    assert wv(192, 288, 256, 0, 192, 288, 64, 64, 1, 1, 1, 0, 1, with_bias=True) == "wgrad_wide_kernel<64,true>"
+    assert wv(192, 288, 256, 0, 192, 288, 64, 64, 1, 1, 1, 0, 1, with_bias=True) == "wgrad_sq_kernel<64,256,true>"
     # 1x1 res_conv / to_qkv GEMMs, down- and up-sampling
     assert fv(192, 288, 64, 0, 192, 288, 768, 768, 1, 1, 1, 0, 1) == "gemm1x1_kernel<128>"
     # down / up (4x4 stride 2 and its transpose; tile width chosen on the low-resolution grid)
