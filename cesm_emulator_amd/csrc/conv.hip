@@ -26,7 +26,21 @@ struct ConvGeom {
   int C1, C2;       // input channels from source 1 / source 2 (concat on channel axis)
   int Cout, Co1;    // output channels; [0,Co1) -> y1, [Co1,Cout) -> y2
   int KH, KW, S, P, U;
+  int wch = 0;      // packed weights in the chunked layout (wpk_chunked)
 };
+
+// Packed conv weights (cesm_conv_pack): row-major Wp[co][tap][ci], or -- bf16 3x3 / 4x4 weights with Cout % 64 == 0 and
+// Cin % 32 == 0, the operands of the halo convs -- "chunked": one contiguous block per (64-co block, 32-channel chunk)
+// holding [tap][co % 64][ci % 32]: the weight tile a halo conv stages per K step is one contiguous block (3x3) or
+// 4-KB runs per live tap (4x4 stride-2), where the row-major layout gave 64-B pieces at a stride of Cin * 2 bytes.
+// The halo conv micro ran 7-22 % faster at levels 1-3, the step's halo conv calls 2-8 % (profiles/r7_h3_*.txt).
+__host__ __device__ inline bool wpk_chunked(bool bf16_dtype, int Cout, int Cin, int KH, int KW) {
+  return bf16_dtype && ((KH == 3 && KW == 3) || (KH == 4 && KW == 4)) && Cout % 64 == 0 && Cin % 32 == 0;
+}
+__host__ __device__ inline int64_t wpk_index(bool chunked, int co, int tap, int ci, int Cin, int NT) {
+  if (!chunked) return ((int64_t)co * NT + tap) * Cin + ci;
+  return ((((int64_t)(co >> 6) * (Cin >> 5) + (ci >> 5)) * NT + tap) * 64 + (co & 63)) * 32 + (ci & 31);
+}
 
 __device__ __forceinline__ bool tap_src(const ConvGeom& g, int oy, int ox, int ky, int kx, int& iy, int& ix) {
   int ny = oy * g.S - g.P + ky;
@@ -142,7 +156,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const T* __restrict__ x1,
 #pragma unroll
     for (int p = 0; p < W_PASS; ++p) {
       const int co = n0 + vrow + p * RPP;
-      const T* ptr = w + ((int64_t)co * (g.KH * g.KW) + tap) * Cin + c0 + vk;
+      const T* ptr = w + wpk_index(g.wch, co, tap, c0 + vk, Cin, g.KH * g.KW);
       if constexpr (VEC == 8) load8(ptr, wreg[p]); else load4(ptr, wreg[p]);
     }
   };
@@ -367,7 +381,7 @@ __global__ __launch_bounds__(256) void conv_fwd_bf16_kernel(const bf16* __restri
 #pragma unroll
     for (int p = 0; p < W_PASS; ++p) {
       const int co = n0 + vrow + p * RPP;
-      wreg[slot][p] = *reinterpret_cast<const bf16x8*>(w + ((int64_t)co * (g.KH * g.KW) + tap) * Cin + c0 + vch * 8);
+      wreg[slot][p] = *reinterpret_cast<const bf16x8*>(w + wpk_index(g.wch, co, tap, c0 + vch * 8, Cin, g.KH * g.KW));
     }
   };
   auto sstore = [&](int buf, int slot) {
@@ -561,6 +575,10 @@ __device__ __forceinline__ void h3_epilogue(const f32x4 (&acc)[NI][NJ], const in
 // unlike round 5's K = 16 form), 44-pixel halo pitch with a conflict-free 32-B-row swizzle: correct, 385 vs 336 us per
 // launch -- the extra zero-half step for the 9th tap, twice the barriers and the per-tap address VALU outweigh the
 // overlap (profiles/r6o_tap_pair_conv_ab.txt).  Removed.)
+#ifdef CESM_H3_STAMPS
+__device__ uint64_t* g_h3_stamp_buf = nullptr;
+__device__ int g_h3_stamp_blocks = 0;
+#endif
 template <int TW, int NJv = 4>
 __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __restrict__ x1, const bf16* __restrict__ x2,
                                                               const bf16* __restrict__ w, const float* __restrict__ bias,
@@ -610,8 +628,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
     const int64_t img = (int64_t)g.Hi * g.Wi * cs;
     const __amdgpu_buffer_rsrc_t xrs =
         __builtin_amdgcn_make_buffer_rsrc((void*)(src + n * img + cc), (short)0, (int)(img * 2 - cc * 2), 0x00020000);
+    // this (co block, chunk)'s weight tile: one contiguous [tap][co][32] block of the chunked pack (wpk_index)
     const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(w + (int64_t)n0 * 9 * Cin + c0), (short)0, H3_BN * 9 * Cin * 2 - c0 * 2, 0x00020000);
+        (void*)(w + ((int64_t)cb * nchunk + ch) * (9 * H3_BN * 32)), (short)0, 9 * H3_BN * 32 * 2, 0x00020000);
     const int prow = lane >> 2, pslot = lane & 3;
     constexpr int HPC = NROWS / 16;  // halo pieces (25 / 40)
     // NJv = 7: only the pieces the tile's halo rows span (pixels past the tile read row 0);
@@ -632,15 +651,27 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
       }
     }
 #pragma unroll
-    for (int k = 0; k < 9; ++k) {  // weights: 9 taps x 64 co rows = 36 pieces
+    for (int k = 0; k < 9; ++k) {  // weights: 9 taps x 64 co rows = 36 pieces, each 1 KiB of the tile
       const int q = wid + 4 * k, row = 16 * q + prow;  // row = tap * 64 + co
-      const int tap = row >> 6, co = row & 63;
       const int chunk = pslot ^ ((row >> 1) & 2);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(sw + q * 512), 16,
-                                               ((co * 9 + tap) * Cin + chunk * 8) * 2, 0, 0, 0);
+                                               (row * 32 + chunk * 8) * 2, 0, 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
+#ifdef CESM_H3_STAMPS
+  // diagnostic build only (tools/h3_stamps.py): per wave, cycles spent in each phase of the chunk loop
+  uint64_t hs[8] = {}, hland[8] = {};
+  const uint64_t h_t0 = __builtin_amdgcn_s_memtime();
+  uint64_t h_t = h_t0;
+  auto hstamp = [&](int k) {
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    hs[k] += t - h_t;
+    h_t = t;
+  };
+#define H3STAMP(k) hstamp(k)
+#else
+#define H3STAMP(k)
+#endif
 
   f32x4 acc[NI][NJ];
 #pragma unroll
@@ -677,8 +708,16 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
   for (int i = 0; i < NI; ++i) aoff[i] = h3_off(wr * 32 + i * 16 + lr, lg);
   for (int ch = 0; ch < nchunk; ++ch) {
     if (ch) __syncthreads();  // previous chunk fully consumed
+    H3STAMP(0);
     stage(ch);
+    H3STAMP(1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    H3STAMP(2);
     __syncthreads();
+    H3STAMP(3);
+#ifdef CESM_H3_STAMPS
+    if (ch < 8) hland[ch] = h_t;
+#endif
     // the 10 fragment reads of tap t+1 are issued between the 16 MFMAs of tap t (two register sets), so no
     // MFMA waits on a read issued just before it (the compiler's order was read -> wait -> 2 MFMAs)
     bf16x8 fa[2][NI], fb[2][NJ];
@@ -710,9 +749,27 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
       }
       __builtin_amdgcn_sched_barrier(0);
     }
+    H3STAMP(4);
   }
   h3_epilogue<NI, NJ>(acc, pyx, g, bias, res, res2, y1, y2, gnp, gn_fimg, n, tt, ntile, y0, x0, n0, wr, wc, lane);
+#ifdef CESM_H3_STAMPS
+  H3STAMP(5);
+  // record: [hw_id | xcc_id << 32, t0, t_end, hs[0..5], land[0..6]] -- vector stores from lane 0 to the diagnostic
+  // buffer only
+  if (g_h3_stamp_buf && lane == 0 && L < g_h3_stamp_blocks) {
+    uint64_t* o = g_h3_stamp_buf + ((int64_t)L * 4 + wid) * 16;
+    const uint32_t hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4), xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);
+    o[0] = hwid | ((uint64_t)xcc << 32);
+    o[1] = h_t0;
+    o[2] = h_t;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) o[3 + k] = hs[k];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) o[9 + k] = hland[k];
+  }
+#endif
 }
+#undef H3STAMP
 
 
 
@@ -839,7 +896,7 @@ __global__ __launch_bounds__(256, 2) void convs2_bf16_kernel(const bf16* __restr
       const int tap = (by + 2 * (t >> 1)) * 4 + bx + 2 * (t & 1);
       const int chunk = pslot ^ ((row >> 1) & 2);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(sw + q * 512), 16,
-                                               ((co * 16 + tap) * Cin + c0 + chunk * 8) * 2, 0, 0, 0);
+                                               (((ch * 16 + tap) * 64 + co) * 32 + chunk * 8) * 2, 0, 0, 0);  // chunked
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
@@ -1152,8 +1209,8 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
     const int64_t img_elems = (int64_t)g.Hi * g.Wi * dcs;
     dxrs = __builtin_amdgcn_make_buffer_rsrc((void*)(src + (int64_t)n * img_elems + cc), (short)0,
                                              (int)(img_elems * 2 - cc * 2), 0x00020000);
-    dwrs = __builtin_amdgcn_make_buffer_rsrc((void*)(w + (int64_t)cob * 64 * 9 * Cin + c0), (short)0,
-                                             64 * 9 * Cin * 2 - c0 * 2, 0x00020000);
+    dwrs = __builtin_amdgcn_make_buffer_rsrc((void*)(w + ((int64_t)cob * (Cin / 32) + ch) * (9 * 64 * 32)), (short)0,
+                                             9 * 64 * 32 * 2, 0x00020000);  // chunked pack (wpk_index)
     dsh = lds + (s % NST) * STG;
   };
   auto issue_piece = [&](int k) {
@@ -1171,7 +1228,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
       const int q = wid + 4 * (k - HPW);
       const int row = 16 * q + prow;  // tap*64 + co
       const int chunk = pslot ^ cw_swz(row);
-      const int vo = (((row & 63) * 9 + (row >> 6)) * Cin + chunk * 8) * 2;
+      const int vo = (row * 32 + chunk * 8) * 2;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(dwrs,
                                                (__attribute__((address_space(3))) void*)(dsh + CW_HROWS * 64 + q * 1024),
                                                16, vo, 0, 0, 0);
@@ -1192,7 +1249,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3p_kernel(const bf16* __restrict
         const int q = wid + 4 * k;
         const int row = 16 * q + prow;
         const int chunk = pslot ^ cw_swz(row);
-        const int vo = (((row & 63) * 9 + (row >> 6)) * 64 + ch * 32 + chunk * 8) * 2;
+        const int vo = (ch * 9 * 64 * 32 + row * 32 + chunk * 8) * 2;  // chunked pack (wpk_index)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
             wrs0, (__attribute__((address_space(3))) void*)(wres + ch * CW_WROWS * 64 + q * 1024), 16, vo, 0, 0, 0);
       }
@@ -1516,14 +1573,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3ws_kernel(const bf16* __restric
   auto hbase = [&](int st) { return lds + (rw ? 2 * WS_WROWS * 64 + st * WS_HROWS * 64 : st * WS_STAGE); };
   auto wbase = [&](int st, int ch) { return rw ? lds + ch * WS_WROWS * 64 : lds + st * WS_STAGE + WS_HROWS * 64; };
   auto issue_w = [&](int cb, int ch, char* dst) {  // the weight chunk ch of co block cb
-    const int c0 = ch * 32;
     const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(w + (int64_t)cb * 64 * 9 * Cin + c0), (short)0, 64 * 9 * Cin * 2 - c0 * 2, 0x00020000);
+        (void*)(w + ((int64_t)cb * (Cin / 32) + ch) * (9 * 64 * 32)), (short)0, 9 * 64 * 32 * 2, 0x00020000);
 #pragma unroll
-    for (int k = 0; k < WS_WP; ++k) {
+    for (int k = 0; k < WS_WP; ++k) {  // one contiguous tile of the chunked pack (wpk_index)
       const int q = wl + 4 * k, row = 16 * q + prow;  // row = tap * 64 + co
       const int chunk = pslot ^ cw_swz(row);
-      const int vo = (((row & 63) * 9 + (row >> 6)) * Cin + chunk * 8) * 2;
+      const int vo = (row * 32 + chunk * 8) * 2;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(dst + q * 1024), 16, vo,
                                                0, 0, 0);
     }
@@ -3108,7 +3164,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __r
   dst[di] = accumulate ? dst[di] + s : s;
 }
 
-// pack a PyTorch conv weight into the GEMM layout Wp[co][tap][ci] (cast to T)
+// pack a PyTorch conv weight into the GEMM layout Wp[co][tap][ci] or its chunked form (wpk_index; cast to T)
 template <typename T>
 __global__ void conv_pack_kernel(const float* __restrict__ src, T* __restrict__ dst, int Cout, int Cin, int KH,
                                  int KW, int swap, int flip) {
@@ -3116,6 +3172,7 @@ __global__ void conv_pack_kernel(const float* __restrict__ src, T* __restrict__ 
   // made this a 0.37 ms launch per optimizer step
   const int K = KH * KW * Cin;
   const int total = Cout * K;
+  const bool chk = wpk_chunked(std::is_same<T, bf16>::value, Cout, Cin, KH, KW);
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
     const int co = e / K;
     const int kc = e - co * K;
@@ -3123,7 +3180,7 @@ __global__ void conv_pack_kernel(const float* __restrict__ src, T* __restrict__ 
     int ky = tap / KW, kx = tap - ky * KW;
     if (flip) { ky = KH - 1 - ky; kx = KW - 1 - kx; }
     const int d0 = swap ? ci : co, d1 = swap ? co : ci, D1 = swap ? Cout : Cin;
-    dst[e] = from_f<T>(src[((d0 * D1 + d1) * KH + ky) * KW + kx]);
+    dst[chk ? wpk_index(true, co, tap, ci, Cin, KH * KW) : e] = from_f<T>(src[((d0 * D1 + d1) * KH + ky) * KW + kx]);
   }
 }
 
@@ -3140,7 +3197,7 @@ __host__ __device__ inline int pb_co_t(int T) { const int c = PB_TILE / (T * PB_
 // one (co, ci) tile; NTC = the tap count when known at compile time (1, 9, 16), else 0 (runtime NT)
 template <typename T, int NTC>
 __device__ __forceinline__ void pb_tile(float* tile, const float* __restrict__ src, T* __restrict__ dst, int Cout, int Cin,
-                                        int NTr, int swap, int flip, int co0, int ci0, int nco, int ncc) {
+                                        int NTr, int swap, int flip, int co0, int ci0, int nco, int ncc, bool chk) {
   const int NT = NTC ? NTC : NTr;
   const int run = swap ? nco * NT : ncc * NT;  // contiguous source floats per outer index
   const int nld = (swap ? ncc : nco) * run;
@@ -3173,7 +3230,7 @@ __device__ __forceinline__ void pb_tile(float* tile, const float* __restrict__ s
     const int ci_l = q & (PB_CI - 1), ct = q / PB_CI, co_l = ct / NT, td = ct - co_l * NT;
     if (q < nst && ci_l < ncc) {
       const int ts = flip ? NT - 1 - td : td;
-      dst[((int64_t)(co0 + co_l) * NT + td) * Cin + ci0 + ci_l] = from_f<T>(tile[(co_l * NT + ts) * PB_CI + ci_l]);
+      dst[wpk_index(chk, co0 + co_l, td, ci0 + ci_l, Cin, NT)] = from_f<T>(tile[(co_l * NT + ts) * PB_CI + ci_l]);
     }
   }
 }
@@ -3193,11 +3250,12 @@ __global__ __launch_bounds__(256) void conv_pack_batch_kernel(const int64_t* __r
     const int lb = (int)(b - start[lo]);
     const int co0 = (lb / nci) * cot, ci0 = (lb % nci) * PB_CI;
     const int nco = min(cot, Cout - co0), ncc = min(PB_CI, Cin - ci0);
+    const bool chk = wpk_chunked(std::is_same<T, bf16>::value, Cout, Cin, (int)jb[4], (int)jb[5]);
     __syncthreads();  // the previous tile's LDS reads are done
-    if (NT == 9) pb_tile<T, 9>(tile, src, dst, Cout, Cin, NT, swap, flip, co0, ci0, nco, ncc);
-    else if (NT == 1) pb_tile<T, 1>(tile, src, dst, Cout, Cin, NT, swap, flip, co0, ci0, nco, ncc);
-    else if (NT == 16) pb_tile<T, 16>(tile, src, dst, Cout, Cin, NT, swap, flip, co0, ci0, nco, ncc);
-    else pb_tile<T, 0>(tile, src, dst, Cout, Cin, NT, swap, flip, co0, ci0, nco, ncc);
+    if (NT == 9) pb_tile<T, 9>(tile, src, dst, Cout, Cin, NT, swap, flip, co0, ci0, nco, ncc, chk);
+    else if (NT == 1) pb_tile<T, 1>(tile, src, dst, Cout, Cin, NT, swap, flip, co0, ci0, nco, ncc, false);
+    else if (NT == 16) pb_tile<T, 16>(tile, src, dst, Cout, Cin, NT, swap, flip, co0, ci0, nco, ncc, chk);
+    else pb_tile<T, 0>(tile, src, dst, Cout, Cin, NT, swap, flip, co0, ci0, nco, ncc, false);
   }
 }
 
@@ -3820,6 +3878,7 @@ int conv_fwd_launch(int dtype, const void* x1, const void* x2, const void* wp, c
   const ConvFwdPlan pl = conv_fwd_plan(dtype, Nb, Hi, Wi, C1, C2, Ho, Wo, Cout, Co1, KH, KW, S, P, U);
   if (pl.v == CFV_INVALID) return CESM_EINVAL;
   ConvGeom g{Nb, Hi, Wi, Ho, Wo, C1, C2, Cout, Co1, KH, KW, S, P, U};
+  g.wch = wpk_chunked(dtype == CESM_DT_BF16, Cout, C1 + C2, KH, KW);
   const int64_t M = (int64_t)Nb * Ho * Wo;
   const int BN = (Cout % 128 == 0) ? 128 : 64;
   dim3 grid(Cout / BN, (unsigned)cdiv(M, BMP));
@@ -4228,3 +4287,14 @@ int cesm_head_bwd(int dtype, const float* dout, const void* x, const float* w, v
 }
 
 }  // extern "C"
+
+#ifdef CESM_H3_STAMPS
+// diagnostic build only (tools/h3_stamps.py): point the halo conv's phase stamps at buf (16 u64 per wave, 4 waves per
+// block, blocks [0, nblocks)); buf = nullptr turns them off
+extern "C" int cesm_diag_h3_stamps_set(void* buf, int nblocks) {
+  uint64_t* p = static_cast<uint64_t*>(buf);
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_h3_stamp_buf), &p, sizeof(p)) != hipSuccess) return CESM_EINVAL;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_h3_stamp_blocks), &nblocks, sizeof(nblocks)) != hipSuccess) return CESM_EINVAL;
+  return 0;
+}
+#endif
