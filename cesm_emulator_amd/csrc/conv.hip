@@ -574,7 +574,9 @@ __device__ __forceinline__ void h3_epilogue(const f32x4 (&acc)[NI][NJ], const in
 // a double buffer at two blocks per CU, each K = 32 MFMA step taking two taps of a stage (so the K = 32 rate is kept,
 // unlike round 5's K = 16 form), 44-pixel halo pitch with a conflict-free 32-B-row swizzle: correct, 385 vs 336 us per
 // launch -- the extra zero-half step for the 9th tap, twice the barriers and the per-tap address VALU outweigh the
-// overlap (profiles/r6o_tap_pair_conv_ab.txt).  Removed.)
+// overlap (profiles/r6o_tap_pair_conv_ab.txt).  Removed.  Also round 6: an L2 touch of chunk ch + 1's weight and
+// halo lines (4 B per 128-B line, LDS-direct) issued while chunk ch computes -- the step's halo conv calls 1 % faster,
+// the step 0.3 ms slower (profiles/r7_h3_touch_ab.txt).  Removed.)
 #ifdef CESM_H3_STAMPS
 __device__ uint64_t* g_h3_stamp_buf = nullptr;
 __device__ int g_h3_stamp_blocks = 0;
