@@ -577,6 +577,9 @@ __device__ __forceinline__ void h3_epilogue(const f32x4 (&acc)[NI][NJ], const in
 // overlap (profiles/r6o_tap_pair_conv_ab.txt).  Removed.  Also round 6: an L2 touch of chunk ch + 1's weight and
 // halo lines (4 B per 128-B line, LDS-direct) issued while chunk ch computes -- the step's halo conv calls 1 % faster,
 // the step 0.3 ms slower (profiles/r7_h3_touch_ab.txt).  Removed.)
+#ifndef H3_PW
+#define H3_PW 1
+#endif
 #ifdef CESM_H3_STAMPS
 __device__ uint64_t* g_h3_stamp_buf = nullptr;
 __device__ int g_h3_stamp_blocks = 0;
@@ -594,7 +597,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
   static_assert(NJv == 4 || NJv == 7, "256- or 448-pixel tiles");
   constexpr int NROWS = (NJv == 7 ? 16 : 10) * H3_P;
   __shared__ __attribute__((aligned(16))) bf16 sh[NROWS * H3_LD];
-  __shared__ __attribute__((aligned(16))) bf16 sw[9 * H3_BN * H3_LD];
+  // the weight tile as three arrays of 3 taps each: distinct LDS objects, so the compiler's wait insertion can see that
+  // reads of taps 0-2 do not depend on the DMA still landing taps 3-8 (H3_PW)
+  __shared__ __attribute__((aligned(16))) bf16 sw0[3 * H3_BN * H3_LD];
+  __shared__ __attribute__((aligned(16))) bf16 sw1[3 * H3_BN * H3_LD];
+  __shared__ __attribute__((aligned(16))) bf16 sw2[3 * H3_BN * H3_LD];
+  auto swt = [&](int k) { return k == 0 ? sw0 : (k == 1 ? sw1 : sw2); };  // k compile-time after unrolling
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   // wave tile (round 3): 64 co x 16 NJv px = 4 x NJv MFMA tiles per wave (8 fragment reads per 16 MFMAs per
   // tap at NJv = 4); else 32 co x 128 px = 2 x 8 (10 reads per 16 MFMAs: the 4 waves' reads exceeded the LDS
@@ -656,8 +664,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
     for (int k = 0; k < 9; ++k) {  // weights: 9 taps x 64 co rows = 36 pieces, each 1 KiB of the tile
       const int q = wid + 4 * k, row = 16 * q + prow;  // row = tap * 64 + co
       const int chunk = pslot ^ ((row >> 1) & 2);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(sw + q * 512), 16,
-                                               (row * 32 + chunk * 8) * 2, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(swt(k / 3) + (q - 12 * (k / 3)) * 512),
+                                               16, (row * 32 + chunk * 8) * 2, 0, 0, 0);
     }
   };
 #ifdef CESM_H3_STAMPS
@@ -713,9 +721,17 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
     H3STAMP(0);
     stage(ch);
     H3STAMP(1);
+#if H3_PW
+    // progressive landing: each wave's 9 weight pieces are the youngest, piece k = tap k; wait for the halo and taps
+    // 0-2 only, and for taps 3-5 / 6-8 at the tap loop's two later barriers
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    H3STAMP(2);
+    __builtin_amdgcn_s_barrier();
+#else
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     H3STAMP(2);
     __syncthreads();
+#endif
     H3STAMP(3);
 #ifdef CESM_H3_STAMPS
     if (ch < 8) hland[ch] = h_t;
@@ -726,7 +742,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
     auto rd = [&](int tap, int b) {
       const int ky = tap / 3, kx = tap - ky * 3;
 #pragma unroll
-      for (int i = 0; i < NI; ++i) fa[b][i] = *reinterpret_cast<const bf16x8*>(sw + aoff[i] + tap * H3_BN * H3_LD);
+      for (int i = 0; i < NI; ++i)
+        fa[b][i] = *reinterpret_cast<const bf16x8*>(swt(tap / 3) + aoff[i] + (tap % 3) * H3_BN * H3_LD);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) fb[b][j] = *reinterpret_cast<const bf16x8*>(sh + boff[j][kx] + ky * H3_P * H3_LD);
     };
@@ -734,14 +751,21 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(const bf16* __rest
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int b = tap & 1;
+      const bool gate = H3_PW && (tap == 2 || tap == 5);  // the next tap's weights land behind a barrier
       __builtin_amdgcn_sched_barrier(0);
-      if (tap + 1 < 9) rd(tap + 1, b ^ 1);
+      if (tap + 1 < 9 && !gate) rd(tap + 1, b ^ 1);
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int i = 0; i < NI; ++i)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[b][i], fb[b][j], acc[i][j], 0, 0, 0);
-      if (tap + 1 < 9) {
+      if (gate) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (tap == 2) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        rd(tap + 1, b ^ 1);
+      } else if (tap + 1 < 9) {
 #pragma unroll
         for (int q2 = 0; q2 < NI + NJ; ++q2) {
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
