@@ -84,7 +84,11 @@ int cesm_conv_wgrad(int dtype, const void* x1, const void* x2, const void* dy1, 
                     int Wo, int Cout, int Co1, int KH, int KW, int S, int P, int U, int swap, int flip, int accumulate,
                     hipStream_t stream);
 /* PyTorch conv weight (fp32) -> GEMM layout Wp[co][tap][ci] in dtype.  swap: GEMM co is dim 1 of
- * the torch tensor (transposed conv forward / conv dgrad); flip: taps reversed. */
+ * the torch tensor (transposed conv forward / conv dgrad); flip: taps reversed.  bf16 3x3 and 4x4 weights with
+ * Cout % 64 == 0 and Cin % 32 == 0 are written "chunked" instead: element (co, tap, ci) at
+ * (((co/64 * Cin/32 + ci/32) * KH*KW + tap) * 64 + co%64) * 32 + ci%32 -- one contiguous block per (64-co block,
+ * 32-channel chunk), the tile the halo convs stage.  The pack is opaque to callers: cesm_conv_fwd reads either
+ * layout by the same rule (same argument lists; round 6). */
 int cesm_conv_pack(int dtype, const float* w, void* wp, int Cout, int Cin, int KH, int KW, int swap, int flip,
                    hipStream_t stream);
 /* every cached pack of one dtype redone in ONE launch after an optimizer step: jobs = device
