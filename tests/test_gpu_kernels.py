@@ -167,6 +167,33 @@ def test_conv_pack_batch(dev, cdt):
             assert torch.equal(o.view(-1), ref.view(-1)), (grid, co, ci, kh, kw, swap, flip)
 
 
+def _pack_ref(w, cdt, co, ci, kh, kw, swap, flip):
+    """torch restatement of the documented cesm_conv_pack layouts (include/cesm_hip.h): Wp[co][tap][ci], or the chunked
+    form (bf16 3x3 / 4x4, Cout % 64 == 0, Cin % 32 == 0): element (co, tap, ci) at
+    (((co/64 * Cin/32 + ci/32) * T + tap) * 64 + co%64) * 32 + ci%32"""
+    g = w.transpose(0, 1) if swap else w  # [co][ci][kh][kw]
+    if flip:
+        g = g.flip(2, 3)
+    g = g.reshape(co, ci, kh * kw).permute(0, 2, 1)  # [co][tap][ci]
+    T = kh * kw
+    if cdt == torch.bfloat16 and (kh, kw) in ((3, 3), (4, 4)) and co % 64 == 0 and ci % 32 == 0:
+        g = g.reshape(co // 64, 64, T, ci // 32, 32).permute(0, 3, 2, 1, 4)  # [co/64][ci/32][tap][co%64][ci%32]
+    return g.contiguous().reshape(-1).to(cdt)
+
+
+@pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
+def test_conv_pack_layouts(dev, cdt):
+    """cesm_conv_pack == the header's layout rule: row-major for fp32, 1x1, 7x7 and ragged channel counts; chunked
+    for the bf16 3x3 / 4x4 packs the halo convs read (swap and flip included)"""
+    torch.manual_seed(11)
+    for (co, ci, kh, kw, swap, flip) in [(64, 64, 3, 3, 0, 0), (128, 64, 3, 3, 1, 1), (64, 96, 3, 3, 0, 1),
+                                         (128, 128, 4, 4, 1, 1), (256, 64, 4, 4, 0, 0), (768, 64, 1, 1, 0, 0),
+                                         (32, 64, 3, 3, 0, 0), (64, 40, 3, 3, 1, 1), (64, 2, 7, 7, 0, 0)]:
+        w = torch.randn((ci, co, kh, kw) if swap else (co, ci, kh, kw), device=dev)
+        got = K.conv_pack(w, cdt, co, ci, kh, kw, swap, flip)
+        assert torch.equal(got.view(-1), _pack_ref(w, cdt, co, ci, kh, kw, swap, flip)), (co, ci, kh, kw, swap, flip)
+
+
 @pytest.mark.parametrize("M,C", [(64, 64), (1000, 64), (40 * 77, 64), (6912 * 2 + 17, 128), (3000, 256), (777, 512)])
 def test_qkv_bwd_fused(dev, M, C):
     """cesm_qkv_bwd (csrc/qkvbwd.hip: dqkv read once for dx and dW of the 768-channel to_qkv projection) against a
