@@ -33,7 +33,7 @@ struct ConvGeom {
 // Cin % 32 == 0, the operands of the halo convs -- "chunked": one contiguous block per (64-co block, 32-channel chunk)
 // holding [tap][co % 64][ci % 32]: the weight tile a halo conv stages per K step is one contiguous block (3x3) or
 // 4-KB runs per live tap (4x4 stride-2), where the row-major layout gave 64-B pieces at a stride of Cin * 2 bytes.
-// The halo conv micro ran 7-22 % faster at levels 1-3, the step's halo conv calls 2-8 % (profiles/r7_h3_*.txt).
+// The halo conv micro ran 7-22 % faster at levels 1-3, the step's halo conv calls 2-8 % (profiles/r6late_h3_*.txt).
 __host__ __device__ inline bool wpk_chunked(bool bf16_dtype, int Cout, int Cin, int KH, int KW) {
   return bf16_dtype && ((KH == 3 && KW == 3) || (KH == 4 && KW == 4)) && Cout % 64 == 0 && Cin % 32 == 0;
 }
@@ -576,7 +576,7 @@ __device__ __forceinline__ void h3_epilogue(const f32x4 (&acc)[NI][NJ], const in
 // launch -- the extra zero-half step for the 9th tap, twice the barriers and the per-tap address VALU outweigh the
 // overlap (profiles/r6o_tap_pair_conv_ab.txt).  Removed.  Also round 6: an L2 touch of chunk ch + 1's weight and
 // halo lines (4 B per 128-B line, LDS-direct) issued while chunk ch computes -- the step's halo conv calls 1 % faster,
-// the step 0.3 ms slower (profiles/r7_h3_touch_ab.txt).  Removed.)
+// the step 0.3 ms slower (profiles/r6late_h3_touch_ab.txt).  Removed.)
 #ifndef H3_PW
 #define H3_PW 1
 #endif
@@ -2046,7 +2046,7 @@ __global__ __launch_bounds__(256, NS == 1 ? 4 : 2) void gemm1x1_kernel(const bf1
       for (int q = 0; q < 8; ++q) v[q] = (bf16)((float)v[q] + (float)rv[it][q]);
     }
     *reinterpret_cast<bf16x8*>(dst) = v;  // (round 6: non-temporal here -- isolated 1x1 convs 9 % faster, the F = 12
-                                          // step and the F = 120 leg unchanged, profiles/r7_g1_nontemporal_ab.txt)
+                                          // step and the F = 120 leg unchanged, profiles/r6late_g1_nontemporal_ab.txt)
   }
 }
 
