@@ -16,6 +16,8 @@ sys.path.insert(0, ".")
 from cesm_emulator_amd import _lib  # noqa: E402
 from cesm_emulator_amd import kernels as K  # noqa: E402
 
+# (the s_memtime stamp after the stage's issue already waits for the DMA to land -- see DESIGN §6e -- so "stage" is
+# issue + landing and "landing wait" is what is left after it)
 NAMES = ["end barrier", "stage issue", "landing wait", "post-land barrier", "MFMA taps", "epilogue"]
 
 
