@@ -100,11 +100,7 @@ def run(lvl, C1=None, Cout=None, Nb=96):
         h, _ = np.histogram(offs, bins=5, range=(0, 0.5))
         print(f"  co-resident pairs {npair}; landing offset / chunk period (0 = in phase, 0.5 = alternating): "
               f"mean {np.mean(offs):.2f}, histogram {h.tolist()}")
-    # s_memtime counters are per XCD: the span of each XCD's stamps over the launch time gives its clock
-    xcc = (hw >> np.uint64(32)).astype(np.int64)
-    ghz = [(t1[xcc == x].max() - t0[xcc == x].min()) / us / 1e3 for x in np.unique(xcc)]
-    print(f"  stamp clock per XCD (span / launch time): median {np.median(ghz):.2f} GHz, "
-          f"range {min(ghz):.2f}-{max(ghz):.2f}")
+
 
 
 def main():
