@@ -102,7 +102,6 @@ def run(lvl, C1=None, Cout=None, Nb=96):
               f"mean {np.mean(offs):.2f}, histogram {h.tolist()}")
 
 
-
 def main():
     levels = [int(v) for v in sys.argv[1].split(",")] if len(sys.argv) > 1 else [1, 2, 3]
     assert "diag" in os.environ.get("CESM_HIP_LIB", ""), "run with CESM_HIP_LIB=cesm_emulator_amd/libcesm_hip_diag.so"
