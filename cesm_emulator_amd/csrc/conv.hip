@@ -3174,8 +3174,19 @@ __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __r
   const int64_t e = blockIdx.x * 64ll + (threadIdx.x & 63);
   const int grp = threadIdx.x >> 6;
   float s = 0.f;
-  if (e < total)
-    for (int k = grp; k < nsplit; k += 4) s += slab[(int64_t)k * total + e];
+  if (e < total) {
+    // 8 slab loads in flight, summed in the same order as one at a time (the loop waited out every load: 18.5 us per
+    // call, 78 calls per step)
+    int k = grp;
+    for (; k + 28 < nsplit; k += 32) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = slab[(int64_t)(k + 4 * u) * total + e];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; k < nsplit; k += 4) s += slab[(int64_t)k * total + e];
+  }
   __shared__ float red[4][64];
   red[grp][threadIdx.x & 63] = s;
   __syncthreads();
