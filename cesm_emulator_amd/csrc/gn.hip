@@ -367,13 +367,32 @@ __global__ __launch_bounds__(1024) void gn_bwd_finalize_kernel(const float* __re
   __shared__ float gA[64], gB[64];
   const int gsz = C / G;
   float s1 = 0.f, s3 = 0.f, sy = 0.f;
-  if (c < C)
-    for (int k = kg; k < nchunk; k += GNF_KG) {
+  if (c < C) {
+    // four partials' loads in flight, summed in the same order as one at a time
+    int k = kg;
+    for (; k + 3 * GNF_KG < nchunk; k += 4 * GNF_KG) {
+      float v[4][3];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float* p = part + (((int64_t)bl * nchunk + k + u * GNF_KG) * C + c) * 3;
+        v[u][0] = p[0];
+        v[u][1] = p[1];
+        v[u][2] = p[2];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        s1 += v[u][0];
+        s3 += v[u][1];
+        sy += v[u][2];
+      }
+    }
+    for (; k < nchunk; k += GNF_KG) {
       const float* p = part + (((int64_t)bl * nchunk + k) * C + c) * 3;
       s1 += p[0];
       s3 += p[1];
       sy += p[2];
     }
+  }
   red[kg][0][cl] = s1;
   red[kg][1][cl] = s3;
   red[kg][2][cl] = sy;
